@@ -1,0 +1,483 @@
+// oracle/crdtree_oracle.cpp
+//
+// TEST INFRASTRUCTURE ONLY — the CPU restatement of the Elm reference
+// (maca/crdt-replicated-tree 5.0.0) used as the parity checker. Only tests/,
+// __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this
+// library. The product path (crdt-graph_amd/) never links or calls it.
+//
+// The reference cannot be compiled here (Elm 0.19, no compiler, no package
+// cache), so this is a line-by-line restatement over mutable
+// maps. Every function cites the Elm source it follows. Elm values are
+// persistent; a mutable restatement is equivalent as long as (1) every error
+// is detected before the first mutation of an op (true for addAfterHelp,
+// deleteHelp and update), (2) a top-level `apply` that fails leaves the tree
+// untouched (we apply to a deep copy and swap on success), and (3) the one
+// place Elm shares a node value between two dict slots — the findInsertion
+// "copy quirk" — makes a deep copy.
+//
+// Pinned by: the 83 reference tests transcribed in tests/test_oracle_kat.py
+// and the hand-traced vectors of SURVEY.md Appendix C.
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <utility>
+#include <vector>
+
+namespace {
+
+enum Kind : int { ROOT = 0, NODE = 1, TOMB = 2 };
+// Internal.Node.Error (src/Internal/Node.elm:35-38) + Ok
+enum NErr : int { N_OK = 0, N_NOTFOUND = 1, N_ALREADY = 2, N_INVALID = 3 };
+// CRDTree.Error (src/CRDTree.elm:104-107) + Ok
+enum TErr : int { T_OK = 0, T_INVALID_PATH = 1, T_NOT_FOUND = 2, T_OPERATION_FAILED = 3 };
+
+struct Node;
+// Children a = Dict Int (Node a)   (src/Internal/Node.elm:25-26). std::map keeps
+// Elm Dict's ascending key order for the canonical dump.
+using Dict = std::map<int64_t, Node>;
+
+// type Node a = Root (Children a) | Node a (Children a) (Array Int) (Maybe Int)
+//             | Tombstone (Array Int) (Maybe Int)        (src/Internal/Node.elm:29-32)
+struct Node {
+  int kind = ROOT;
+  uint32_t val = 0;             // value handle (Node only)
+  std::vector<int64_t> path;    // Node/Tombstone
+  bool has_next = false;        // Maybe Int
+  int64_t next = 0;
+  Dict children;                // Root/Node (Tombstone: always empty)
+};
+
+// emptyChildren = Dict.singleton 0 (Tombstone Array.empty Nothing)  (src/Internal/Node.elm:46-48)
+Dict emptyChildren() {
+  Dict d;
+  Node s;
+  s.kind = TOMB;
+  d.emplace(0, std::move(s));
+  return d;
+}
+
+// children (src/Internal/Node.elm:231-241): Tombstone -> Dict.empty
+// child ts node = children node |> Dict.get ts   (src/Internal/Node.elm:284-286)
+Node* child(int64_t ts, Node& n) {
+  if (n.kind == TOMB) return nullptr;
+  auto it = n.children.find(ts);
+  return it == n.children.end() ? nullptr : &it->second;
+}
+
+// nextNode (src/Internal/Node.elm:257-268): follow `next` keys, skipping Tombstones.
+Node* nextNode(Node* node, Dict& c) {
+  for (;;) {
+    if (node->kind == ROOT || !node->has_next) return nullptr;  // next (Root _) = Nothing
+    auto it = c.find(node->next);
+    if (it == c.end()) return nullptr;
+    if (it->second.kind == TOMB) { node = &it->second; continue; }
+    return &it->second;
+  }
+}
+
+// findInsertion (src/Internal/Node.elm:93-104). Returns (leftKey, leftNode);
+// after a tombstone skip leftKey != key(leftNode) (Appendix A.5).
+std::pair<int64_t, Node*> findInsertion(int64_t ts, int64_t n, Node* node, Dict& c) {
+  for (;;) {
+    if (node->kind == ROOT || !node->has_next) return {n, node};
+    Node* live = nextNode(node, c);
+    if (!live) return {n, node};
+    const int64_t k = node->next;
+    if (ts > k) return {n, node};
+    n = k;
+    node = live;
+  }
+}
+
+// insert (src/Internal/Node.elm:125-135): no-op on a Tombstone parent.
+void insert(int64_t ts, Node&& node, Node& parent) {
+  if (parent.kind == TOMB) return;
+  parent.children[ts] = std::move(node);
+}
+
+// addAfterHelp (src/Internal/Node.elm:56-90)
+int addAfterHelp(const std::vector<int64_t>& p, int64_t ts, uint32_t val, int64_t prevTs, Node& parent) {
+  if (child(ts, parent)) return N_ALREADY;
+  Node* found = child(prevTs, parent);
+  if (!found) return N_NOTFOUND;
+  Dict& c = parent.children;  // parent is Root/Node here (update rejected Tombstones)
+  auto [leftTs, left] = findInsertion(ts, prevTs, found, c);
+  Node node;
+  node.kind = NODE;
+  node.val = val;
+  node.path.assign(p.begin(), p.end() - 1);  // Array.slice 0 -1
+  node.path.push_back(ts);                   // Array.push ts
+  node.has_next = left->has_next;            // next left
+  node.next = left->next;
+  node.children = emptyChildren();
+  // parent |> insert leftTs (updateNext ts left) |> insert ts node
+  auto slot = c.find(leftTs);
+  if (slot != c.end() && &slot->second == left) {
+    left->has_next = true;  // updateNext in place: same value, same slot
+    left->next = ts;
+  } else {
+    Node copy = *left;      // copy quirk: slot leftTs receives a copy of left (deep: Elm values are persistent)
+    copy.has_next = true;
+    copy.next = ts;
+    insert(leftTs, std::move(copy), parent);
+  }
+  insert(ts, std::move(node), parent);
+  return N_OK;
+}
+
+// deleteHelp (src/Internal/Node.elm:112-122)
+int deleteHelp(int64_t ts, Node& parent) {
+  Node* c = child(ts, parent);
+  if (!c) return N_NOTFOUND;
+  if (c->kind == NODE) {  // Tombstone p n: drop value and children
+    c->kind = TOMB;
+    c->val = 0;
+    c->children.clear();
+    return N_OK;
+  }
+  return N_ALREADY;
+}
+
+// update (src/Internal/Node.elm:138-163). Mutates in place; every error is
+// returned before the leaf function mutates anything.
+template <class F>
+int update(F&& func, const int64_t* p, size_t len, Node& parent) {
+  if (parent.kind == TOMB) return N_ALREADY;
+  if (len == 0) return N_INVALID;
+  if (len == 1) return func(p[0], parent);
+  Node* found = child(p[0], parent);
+  if (!found) return N_INVALID;
+  return update(func, p + 1, len - 1, *found);
+}
+
+// Operation a = Add Int (List Int) a | Delete (List Int) | Batch (List (Operation a))
+// (src/Internal/Operation.elm:17-20)
+enum OpKind : int { OP_ADD = 0, OP_DEL = 1, OP_BATCH = 2 };
+struct Op {
+  int kind = OP_BATCH;
+  int64_t ts = 0;
+  std::vector<int64_t> path;
+  uint32_t val = 0;
+  int64_t index = -1;       // position in the caller's flattened op array
+  std::vector<Op> ops;      // Batch
+};
+
+// Timestamp.replicaId ts = ts // 2^32 (src/CRDTree/Timestamp.elm:16-18); Elm `//`
+// on JS numbers is (a / b) | 0 — truncation toward zero, exact for |ts| < 2^53.
+int64_t replicaId(int64_t ts) { return ts / 4294967296LL; }
+
+// CRDTree record (src/CRDTree.elm:112-120)
+struct Tree {
+  Node root;
+  int64_t timestamp = 0;
+  std::vector<int64_t> cursor;
+  std::vector<Op> operations;   // oldest-first here; Elm keeps newest-first (cons)
+  std::map<int64_t, int64_t> replicas;
+  bool last_is_batch = true;    // lastOperation: Batch list, or a single Add/Delete
+  std::vector<Op> last;
+  int64_t err_index = -1;
+};
+
+// Operation.toList (src/Internal/Operation.elm:58-68): a single Add/Delete is
+// held as a one-element list with last_is_batch = false, so toList is the list.
+std::vector<Op> toList(const std::vector<Op>& l) { return l; }
+
+// init (src/CRDTree.elm:130-139); Node.root (src/Internal/Node.elm:41-43)
+void initTree(Tree& t, int64_t replica) {
+  t.root = Node();
+  t.root.kind = ROOT;
+  t.root.children = emptyChildren();
+  t.timestamp = replica * 4294967296LL;  // replicaId * 2 ^ 32
+  t.cursor = {0};
+  t.operations.clear();
+  t.replicas.clear();
+  t.last_is_batch = true;
+  t.last.clear();
+}
+
+int64_t treeId(const Tree& t) { return replicaId(t.timestamp); }  // id (src/CRDTree.elm:378-380)
+
+// buildPath (src/CRDTree.elm:628-632)
+std::vector<int64_t> buildPath(int64_t ts, const std::vector<int64_t>& path) {
+  std::vector<int64_t> r;
+  if (!path.empty()) r.assign(path.begin(), path.end() - 1);
+  r.push_back(ts);
+  return r;
+}
+
+// updateTree (src/CRDTree.elm:298-325)
+int updateTree(const Op& op, const std::vector<int64_t>& path, int64_t ts, Tree& t, int nres) {
+  switch (nres) {
+    case N_OK:
+      t.cursor = buildPath(ts, path);
+      t.operations.push_back(op);
+      t.last_is_batch = false;
+      t.last.assign(1, op);
+      t.replicas[replicaId(ts)] = ts;
+      return T_OK;
+    case N_ALREADY:
+      t.last_is_batch = true;
+      t.last.clear();
+      return T_OK;
+    case N_INVALID:
+      t.err_index = op.index;
+      return T_INVALID_PATH;
+    default:
+      t.err_index = op.index;
+      return T_OPERATION_FAILED;
+  }
+}
+
+int apply(const Op& op, Tree& t);
+
+// batch (src/CRDTree.elm:224-232) with mergeOperations (:328-334) and
+// Operation.merge = Batch (toList a ++ toList b) (src/Internal/Operation.elm:80-82)
+int batch(const std::vector<Op>& ops, Tree& t) {
+  t.last_is_batch = true;
+  t.last.clear();
+  for (const Op& o : ops) {
+    std::vector<Op> prev = std::move(t.last);
+    t.last.clear();
+    int r = apply(o, t);
+    if (r != T_OK) return r;
+    // merge one.lastOperation two.lastOperation
+    std::vector<Op> merged = toList(prev);
+    for (auto& x : t.last) merged.push_back(x);
+    t.last = std::move(merged);
+    t.last_is_batch = true;
+  }
+  return T_OK;
+}
+
+// incrementTimestamp (src/CRDTree.elm:337-343)
+void incrementTimestamp(int64_t ts, Tree& t) {
+  if (replicaId(ts) == treeId(t)) t.timestamp = t.timestamp + 1;
+}
+
+// applyLocal (src/CRDTree.elm:275-295)
+int applyLocal(const Op& op, Tree& t) {
+  switch (op.kind) {
+    case OP_ADD: {
+      const int64_t ts = op.ts;
+      const uint32_t val = op.val;
+      const std::vector<int64_t>& p = op.path;
+      int nres = update(
+          [&](int64_t prevTs, Node& parent) { return addAfterHelp(p, ts, val, prevTs, parent); },
+          p.data(), p.size(), t.root);
+      int r = updateTree(op, p, ts, t, nres);
+      if (r == T_OK) incrementTimestamp(ts, t);
+      return r;
+    }
+    case OP_DEL: {
+      // Operation.timestamp (Delete p) = List.reverse p |> List.head, default 0
+      const int64_t ots = op.path.empty() ? 0 : op.path.back();
+      int nres = update([&](int64_t k, Node& parent) { return deleteHelp(k, parent); }, op.path.data(),
+                        op.path.size(), t.root);
+      return updateTree(op, op.path, ots, t, nres);
+    }
+    default:
+      return batch(op.ops, t);
+  }
+}
+
+// apply (src/CRDTree.elm:265-269): applyLocal, then restore the caller's cursor
+int apply(const Op& op, Tree& t) {
+  std::vector<int64_t> saved = t.cursor;
+  int r = applyLocal(op, t);
+  if (r == T_OK) t.cursor = saved;
+  return r;
+}
+
+// ---- canonical dumps (shared format with the product's crdtm_tree_canonical) ----
+
+constexpr uint64_t FNV_OFF = 1469598103934665603ULL, FNV_PRIME = 1099511628211ULL;
+struct Sink {
+  std::vector<int64_t>* out;  // may be null: hash only
+  uint64_t h = FNV_OFF;
+  uint64_t n = 0;
+  void put(int64_t w) {
+    if (out) out->push_back(w);
+    uint64_t u = static_cast<uint64_t>(w);
+    for (int i = 0; i < 8; ++i) { h ^= (u >> (8 * i)) & 0xff; h *= FNV_PRIME; }
+    ++n;
+  }
+};
+
+// Structure: every dict entry (incl. tombstones, sentinels, orphans), ascending keys, DFS.
+void dumpDict(const Dict& d, int64_t depth, Sink& s) {
+  for (const auto& [key, n] : d) {
+    s.put(depth);
+    s.put(key);
+    s.put(n.kind);
+    s.put(n.has_next ? 1 : 0);
+    s.put(n.has_next ? n.next : 0);
+    s.put(n.kind == NODE ? static_cast<int64_t>(n.val) : 0);
+    s.put(static_cast<int64_t>(n.path.size()));
+    for (int64_t x : n.path) s.put(x);
+    if (n.kind == NODE) dumpDict(n.children, depth + 1, s);
+  }
+}
+
+// Visible document order: from sentinel 0 follow nextNode (src/Internal/Node.elm:206-228),
+// recursing into each live node's children (pre-order).
+void dumpVisible(const Dict& cd, int64_t depth, Sink& s) {
+  Dict& c = const_cast<Dict&>(cd);
+  auto it = c.find(0);
+  if (it == c.end()) return;
+  Node* cur = &it->second;
+  for (;;) {
+    Node* nx = nextNode(cur, c);
+    if (!nx) break;
+    s.put(depth);
+    s.put(static_cast<int64_t>(nx->val));
+    s.put(static_cast<int64_t>(nx->path.size()));
+    for (int64_t x : nx->path) s.put(x);
+    dumpVisible(nx->children, depth + 1, s);
+    cur = nx;
+  }
+}
+
+Op makeOp(uint8_t kind, int64_t ts, const int64_t* path, uint32_t plen, uint32_t val, int64_t index) {
+  Op o;
+  o.kind = kind == 0 ? OP_ADD : OP_DEL;
+  o.ts = kind == 0 ? ts : 0;
+  o.path.assign(path, path + plen);
+  o.val = kind == 0 ? val : 0;
+  o.index = index;
+  return o;
+}
+
+Node* descendant(const int64_t* p, size_t len, Node& n) {  // src/Internal/Node.elm:289-299
+  if (len == 0) return nullptr;
+  Node* c = child(p[0], n);
+  if (len == 1 || !c) return c;
+  return descendant(p + 1, len - 1, *c);
+}
+
+}  // namespace
+
+extern "C" {
+
+struct orc_tree { Tree t; };
+
+orc_tree* orc_init(int64_t replica) {
+  auto* o = new orc_tree;
+  initTree(o->t, replica);
+  return o;
+}
+orc_tree* orc_clone(const orc_tree* o) { return new orc_tree(*o); }
+void orc_free(orc_tree* o) { delete o; }
+
+// apply (op | Batch ops) to the tree. Ops arrive flattened (kind 0 = Add,
+// 1 = Delete); is_batch selects `apply (Batch ops)` vs `apply op` (n_ops == 1).
+// local != 0 uses applyLocal (cursor not restored; the local add/addAfter path).
+// Returns CRDTree.Error code (0 = Ok); *err_index = flattened index of the
+// failing op. On error the tree is unchanged (Elm persistence).
+int orc_apply(orc_tree* o, int is_batch, int local, uint64_t n_ops, const uint8_t* kind, const int64_t* ts,
+              const uint32_t* path_off, const int64_t* path, const uint32_t* val, int64_t* err_index) {
+  Op top;
+  if (is_batch) {
+    top.kind = OP_BATCH;
+    top.ops.reserve(n_ops);
+    for (uint64_t i = 0; i < n_ops; ++i)
+      top.ops.push_back(makeOp(kind[i], ts[i], path + path_off[i], path_off[i + 1] - path_off[i], val[i],
+                               static_cast<int64_t>(i)));
+  } else {
+    top = makeOp(kind[0], ts[0], path + path_off[0], path_off[1] - path_off[0], val[0], 0);
+  }
+  Tree work = o->t;  // Elm: the caller still holds the old tree on Err
+  work.err_index = -1;
+  int r = local ? applyLocal(top, work) : apply(top, work);
+  if (err_index) *err_index = work.err_index;
+  if (r == T_OK) o->t = std::move(work);
+  return r;
+}
+
+int64_t orc_timestamp(const orc_tree* o) { return o->t.timestamp; }
+void orc_set_timestamp(orc_tree* o, int64_t ts) { o->t.timestamp = ts; }
+
+uint64_t orc_cursor(const orc_tree* o, int64_t* out, uint64_t cap) {
+  for (uint64_t i = 0; i < o->t.cursor.size() && i < cap; ++i) out[i] = o->t.cursor[i];
+  return o->t.cursor.size();
+}
+void orc_set_cursor(orc_tree* o, const int64_t* p, uint64_t n) { o->t.cursor.assign(p, p + n); }
+
+uint64_t orc_replicas(const orc_tree* o, int64_t* ids, int64_t* tss, uint64_t cap) {
+  uint64_t i = 0;
+  for (const auto& [k, v] : o->t.replicas) {
+    if (i < cap) { ids[i] = k; tss[i] = v; }
+    ++i;
+  }
+  return i;
+}
+
+// Op list export (operations log oldest-first, or lastOperation's list).
+// which: 0 = operations log, 1 = lastOperation. Returns count; fills arrays
+// when non-null (path buffer sized by *path_total on a first call).
+uint64_t orc_ops(const orc_tree* o, int which, uint8_t* kind, int64_t* ts, uint32_t* path_off, int64_t* path,
+                 uint32_t* val, uint64_t* path_total, int* is_batch) {
+  const std::vector<Op>& l = which == 0 ? o->t.operations : o->t.last;
+  if (is_batch) *is_batch = which == 0 ? 1 : (o->t.last_is_batch ? 1 : 0);
+  uint64_t pt = 0;
+  for (uint64_t i = 0; i < l.size(); ++i) {
+    if (kind) kind[i] = static_cast<uint8_t>(l[i].kind);
+    if (ts) ts[i] = l[i].ts;
+    if (val) val[i] = l[i].val;
+    if (path_off) path_off[i] = static_cast<uint32_t>(pt);
+    if (path) {
+      for (int64_t x : l[i].path) path[pt++] = x;
+    } else {
+      pt += l[i].path.size();
+    }
+  }
+  if (path_off) path_off[l.size()] = static_cast<uint32_t>(pt);
+  if (path_total) *path_total = pt;
+  return l.size();
+}
+
+// Canonical dumps. which: 0 = structure, 1 = visible order. If out is null
+// only the hash/word count are produced. Returns the word count.
+uint64_t orc_canonical(const orc_tree* o, int which, int64_t* out, uint64_t cap, uint64_t* hash) {
+  std::vector<int64_t> buf;
+  Sink s{out ? &buf : nullptr};
+  if (which == 0) dumpDict(o->t.root.children, 0, s);
+  else dumpVisible(o->t.root.children, 0, s);
+  if (out) for (uint64_t i = 0; i < buf.size() && i < cap; ++i) out[i] = buf[i];
+  if (hash) *hash = s.h;
+  return s.n;
+}
+
+// get path tree |> value (CRDTree.getValue, src/CRDTree.elm:486-488).
+// Returns 1 = Just (value in *val), 0 = Nothing (missing or tombstone).
+// *exists = 1 if `get` found a node (Node or Tombstone).
+int orc_get_value(orc_tree* o, const int64_t* p, uint64_t n, uint32_t* val, int* exists) {
+  Node* d = descendant(p, n, o->t.root);
+  if (exists) *exists = d ? 1 : 0;
+  if (!d || d->kind != NODE) return 0;
+  if (val) *val = d->val;
+  return 1;
+}
+
+// Node.path of the node at `p` (for the `delete` local cursor logic and tests).
+uint64_t orc_get_path(orc_tree* o, const int64_t* p, uint64_t n, int64_t* out, uint64_t cap) {
+  Node* d = descendant(p, n, o->t.root);
+  if (!d) return UINT64_MAX;
+  for (uint64_t i = 0; i < d->path.size() && i < cap; ++i) out[i] = d->path[i];
+  return d->path.size();
+}
+
+// lastOperation := Batch [] (the reset `batch` performs, src/CRDTree.elm:231)
+void orc_reset_last(orc_tree* o) { o->t.last_is_batch = true; o->t.last.clear(); }
+
+// Append lastOperation of `other` to `o`'s lastOperation (mergeOperations for
+// a Python-side `batch` of local functions, src/CRDTree.elm:328-334).
+void orc_merge_last(orc_tree* o, const orc_tree* prev) {
+  std::vector<Op> merged = prev->t.last;
+  for (auto& x : o->t.last) merged.push_back(x);
+  o->t.last = std::move(merged);
+  o->t.last_is_batch = true;
+}
+
+}  // extern "C"
