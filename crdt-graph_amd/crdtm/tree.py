@@ -1,0 +1,324 @@
+"""CRDTree — host mirror of the reference's public module (src/CRDTree.elm:1-26),
+backed by the gfx950 merge engine through the C ABI.
+
+Names and meaning follow the Elm API: `init`, `apply`, `batch`, `add`,
+`add_after`, `add_branch`, `delete`, `last_operation`, `operations_since`,
+`timestamp`, `id`, `last_replica_timestamp`, `get_value`. `apply` keeps the
+Elm persistence contract (the input tree stays valid): it clones the device
+state first; `apply_in_place` is the linear-use variant for throughput.
+Results are `Ok(tree)` / `Err(error)` like Elm's `Result (Error a) (CRDTree a)`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Any
+
+import numpy as np
+
+from . import _native as N
+from .operation import Add, Batch, Delete, flatten
+from .timestamp import TWO32, replica_id
+
+
+# ---- Result / Error (src/CRDTree.elm:104-107) ----
+@dataclass(frozen=True)
+class Ok:
+    value: Any
+    ok = True
+
+
+@dataclass(frozen=True)
+class Err:
+    error: Any
+    ok = False
+
+
+@dataclass(frozen=True)
+class InvalidPath:
+    pass
+
+
+@dataclass(frozen=True)
+class NotFound:
+    pass
+
+
+@dataclass(frozen=True)
+class OperationFailed:
+    operation: Any
+
+
+class Values:
+    """Opaque Elm values <-> u32 handles (the engine orders by timestamp only)."""
+
+    def __init__(self):
+        self._h = {}
+        self._v = []
+
+    def handle(self, v):
+        k = (type(v).__name__, v)
+        h = self._h.get(k)
+        if h is None:
+            h = len(self._v)
+            self._v.append(v)
+            self._h[k] = h
+        return h
+
+    def value(self, h):
+        return self._v[h]
+
+
+VALUES = Values()
+
+
+def pack(leaves, values=VALUES):
+    """Flattened Add/Delete leaves -> SoA numpy arrays (crdtm_ops layout)."""
+    n = len(leaves)
+    kind = np.zeros(n + 1, np.uint8)
+    ts = np.zeros(n + 1, np.int64)
+    val = np.zeros(n + 1, np.uint32)
+    off = np.zeros(n + 1, np.uint32)
+    path = []
+    for i, o in enumerate(leaves):
+        if o.kind == "add":
+            ts[i] = o.ts
+            val[i] = values.handle(o.val)
+        else:
+            kind[i] = 1
+        path.extend(o.path)
+        off[i + 1] = len(path)
+    return dict(kind=kind, ts=ts, path_off=off, path=np.array(path + [0], np.int64), val=val)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def ops_struct(arrs, n):
+    return N.Ops(n, int(arrs["path_off"][n]), _ptr(arrs["kind"]), _ptr(arrs["ts"]), _ptr(arrs["path_off"]),
+                 _ptr(arrs["path"]), _ptr(arrs["val"]), None)
+
+
+class CRDTree:
+    """CRDTree a (src/CRDTree.elm:112-120), device resident."""
+
+    def __init__(self, handle, device=0, cursor=(0,)):
+        self._h = handle
+        self.device = device
+        self._cursor = list(cursor)
+        self.last_result = None
+
+    # ---- lifecycle ----
+    @staticmethod
+    def init(replica_id_: int, device: int = 0) -> "CRDTree":
+        """CRDTree.init (src/CRDTree.elm:130-139)."""
+        ctx = N.context(device)
+        h = C.c_void_p()
+        N.check(N.lib().crdtm_tree_create(ctx, int(replica_id_), C.byref(h)), "crdtm_tree_create")
+        return CRDTree(h, device)
+
+    def clone(self) -> "CRDTree":
+        h = C.c_void_p()
+        N.check(N.lib().crdtm_tree_clone(self._h, C.byref(h)), "crdtm_tree_clone")
+        return CRDTree(h, self.device, self._cursor)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and N._lib is not None:
+            N._lib.crdtm_tree_destroy(h)
+            self._h = None
+
+    # ---- merge path ----
+    def apply_arrays(self, arrs, n, is_batch=True, on_device=False, status=None):
+        """Apply packed ops in place (crdtm_apply); returns the crdtm_result."""
+        res = N.Result()
+        ops = arrs if isinstance(arrs, N.Ops) else ops_struct(arrs, n)
+        st = _ptr(status) if status is not None else None
+        N.check(N.lib().crdtm_apply(self._h, C.byref(ops), 1 if on_device else 0, 1 if is_batch else 0, st,
+                                    C.byref(res)), "crdtm_apply")
+        self.last_result = res
+        return res
+
+    def _apply(self, op, in_place):
+        leaves = flatten(op) if op.kind == "batch" else [op]
+        is_batch = op.kind == "batch"
+        target = self if in_place else self.clone()
+        res = target.apply_arrays(pack(leaves), len(leaves), is_batch=is_batch)
+        if res.code == 0:
+            return Ok(target)
+        if res.code == 1:
+            return Err(InvalidPath())
+        return Err(OperationFailed(leaves[res.err_index]))
+
+    def apply(self, op) -> Any:
+        """CRDTree.apply (src/CRDTree.elm:265-269): Ok(new tree) | Err(error)."""
+        return self._apply(op, in_place=False)
+
+    def apply_in_place(self, op):
+        return self._apply(op, in_place=True)
+
+    # ---- local editing (src/CRDTree.elm:142-216) ----
+    def _local(self, op):
+        r = self.apply(op)
+        if r.ok:
+            t = r.value
+            # applyLocal sets the cursor to buildPath ts path (src/CRDTree.elm:310, :628-632)
+            path = list(op.path)
+            t._cursor = path[:-1] + [op.ts if op.kind == "add" else (path[-1] if path else 0)]
+        return r
+
+    def add(self, value):
+        return self.add_after(self._cursor, value)
+
+    def add_after(self, path, value):
+        """CRDTree.addAfter: Add (nextTimestamp tree) path value."""
+        return self._local(Add(self.timestamp() + 1, path, value))
+
+    def add_branch(self, value):
+        r = self.add(value)
+        if r.ok:
+            r.value._cursor = r.value._cursor + [0]
+        return r
+
+    def delete(self, path):
+        return self._local(Delete(path))
+
+    def batch(self, funcs):
+        """CRDTree.batch (src/CRDTree.elm:224-232) over functions tree -> Result."""
+        cur = self
+        ops = []
+        for f in funcs:
+            r = f(cur)
+            if not r.ok:
+                return r
+            nxt = r.value
+            lo = nxt.last_operation()
+            ops.extend(lo.ops if lo.kind == "batch" else [lo])
+            cur = nxt
+        cur._last_override = Batch(ops)
+        return Ok(cur)
+
+    # ---- queries ----
+    def cursor(self):
+        return list(self._cursor)
+
+    def timestamp(self) -> int:
+        v = C.c_int64()
+        N.check(N.lib().crdtm_tree_timestamp(self._h, C.byref(v)))
+        return v.value
+
+    def id(self) -> int:
+        return replica_id(self.timestamp())
+
+    def next_timestamp(self) -> int:
+        return self.timestamp() + 1
+
+    def replicas(self) -> dict:
+        n = C.c_uint64()
+        N.check(N.lib().crdtm_tree_replicas(self._h, None, None, 0, C.byref(n)))
+        ids = np.zeros(max(n.value, 1), np.int64)
+        tss = np.zeros(max(n.value, 1), np.int64)
+        N.check(N.lib().crdtm_tree_replicas(self._h, _ptr(ids), _ptr(tss), n.value, C.byref(n)))
+        return {int(a): int(b) for a, b in zip(ids[:n.value], tss[:n.value])}
+
+    def last_replica_timestamp(self, rid: int) -> int:
+        """CRDTree.lastReplicaTimestamp (src/CRDTree.elm:637-639)."""
+        return self.replicas().get(rid, 0)
+
+    def _ops(self, which):
+        o = N.Ops()
+        isb = C.c_int()
+        N.check(N.lib().crdtm_tree_ops(self._h, which, C.byref(o), C.byref(isb)))
+        n, npth = o.n_ops, o.n_path
+        kind = np.zeros(n + 1, np.uint8)
+        ts = np.zeros(n + 1, np.int64)
+        off = np.zeros(n + 1, np.uint32)
+        path = np.zeros(npth + 1, np.int64)
+        val = np.zeros(n + 1, np.uint32)
+        o2 = N.Ops(n, npth, _ptr(kind), _ptr(ts), _ptr(off), _ptr(path), _ptr(val), None)
+        N.check(N.lib().crdtm_tree_ops(self._h, which, C.byref(o2), C.byref(isb)))
+        out = []
+        for i in range(n):
+            p = [int(x) for x in path[off[i]:off[i + 1]]]
+            out.append(Add(int(ts[i]), p, VALUES.value(int(val[i]))) if kind[i] == 0 else Delete(p))
+        return out, bool(isb.value)
+
+    def operations(self) -> list:
+        """The log oldest-first (operationsSince 0)."""
+        return self._ops(0)[0]
+
+    def last_operation(self):
+        """CRDTree.lastOperation (src/CRDTree.elm:371-373)."""
+        ov = getattr(self, "_last_override", None)
+        if ov is not None:
+            return ov
+        ops, isb = self._ops(1)
+        return Batch(ops) if isb else ops[0]
+
+    def operations_since(self, ts: int) -> Batch:
+        """CRDTree.operationsSince (src/CRDTree.elm:408-418)."""
+        log = self.operations()
+        if ts == 0:
+            return Batch(log)
+        acc = []
+        for o in reversed(log):
+            acc.insert(0, o)
+            if o.kind == "add" and o.ts == ts:
+                return Batch(acc)
+        return Batch([])
+
+    def canonical(self, which=0, full=True):
+        n = C.c_uint64()
+        h = C.c_uint64()
+        if not full:
+            N.check(N.lib().crdtm_tree_canonical(self._h, which, None, 0, C.byref(n), C.byref(h)))
+            return None, n.value, h.value
+        N.check(N.lib().crdtm_tree_canonical(self._h, which, None, 0, C.byref(n), C.byref(h)))
+        buf = np.zeros(max(n.value, 1), np.int64)
+        N.check(N.lib().crdtm_tree_canonical(self._h, which, _ptr(buf), n.value, C.byref(n), C.byref(h)))
+        return buf[:n.value], n.value, h.value
+
+    def document_handles(self) -> np.ndarray:
+        """Value handles of the visible nodes in document order (device linearisation)."""
+        n = C.c_uint64()
+        N.check(N.lib().crdtm_tree_document(self._h, None, 0, C.byref(n)))
+        out = np.zeros(max(n.value, 1), np.uint32)
+        N.check(N.lib().crdtm_tree_document(self._h, _ptr(out), n.value, C.byref(n)))
+        return out[:n.value]
+
+    def document(self) -> list:
+        return [VALUES.value(int(h)) for h in self.document_handles()]
+
+    def visible_values(self, depth0_only=True):
+        words, n, _ = self.canonical(1)
+        out = []
+        i = 0
+        while i < n:
+            d, v, pl = int(words[i]), int(words[i + 1]), int(words[i + 2])
+            if d == 0 or not depth0_only:
+                out.append(VALUES.value(v))
+            i += 3 + pl
+        return out
+
+    def get_value(self, path):
+        """CRDTree.getValue (src/CRDTree.elm:486-488) over the canonical structure."""
+        words, n, _ = self.canonical(0)
+        want = [int(x) for x in path]
+        i = 0
+        stack = []
+        while i < n:
+            d, k, kind, hn, nx, v, pl = (int(x) for x in words[i:i + 7])
+            del stack[d:]
+            stack.append(k)
+            if stack == want:
+                return VALUES.value(v) if kind == 1 else None
+            i += 7 + pl
+        return None
+
+
+def init(replica_id_: int, device: int = 0) -> CRDTree:
+    return CRDTree.init(replica_id_, device)
+
+
+__all__ = ["CRDTree", "init", "Ok", "Err", "InvalidPath", "NotFound", "OperationFailed", "TWO32"]

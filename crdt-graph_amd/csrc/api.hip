@@ -1,0 +1,473 @@
+// api.hip — the C ABI (include/crdtm.h) over the gfx950 merge engine.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "engine.h"
+
+using namespace crdtm;
+
+namespace {
+
+constexpr uint64_t FNV_OFF = 1469598103934665603ULL, FNV_PRIME = 1099511628211ULL;
+
+struct Sink {
+  int64_t* out;
+  uint64_t cap;
+  uint64_t n = 0;
+  uint64_t h = FNV_OFF;
+  void put(int64_t w) {
+    if (out && n < cap) out[n] = w;
+    uint64_t u = static_cast<uint64_t>(w);
+    for (int i = 0; i < 8; ++i) {
+      h ^= (u >> (8 * i)) & 0xff;
+      h *= FNV_PRIME;
+    }
+    ++n;
+  }
+};
+
+// Host copy of a tree state (read APIs only: canonical dumps and egress).
+struct HostTree {
+  std::vector<long long> key;
+  std::vector<uint32_t> next, src, child, dict;
+  std::vector<uint8_t> flags;
+  std::vector<uint32_t> d_sent;
+  std::vector<uint8_t> l_kind;
+  std::vector<long long> l_ts;
+  std::vector<uint32_t> l_val, l_off;
+  std::vector<long long> l_path;
+  std::vector<std::vector<uint32_t>> members;
+};
+
+template <class T>
+int d2h(std::vector<T>& v, const T* p, uint64_t n) {
+  v.resize(n);
+  if (n) HIP_CHECK(hipMemcpy(v.data(), p, n * sizeof(T), hipMemcpyDeviceToHost));
+  return CRDTM_OK;
+}
+
+int fetch(const crdtm_tree* t, HostTree& h, bool members) {
+  HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+  const uint64_t S = t->n_slots, D = t->n_dicts;
+  int r;
+  if ((r = d2h(h.key, t->d.s_key, S)) || (r = d2h(h.next, t->d.s_next, S)) || (r = d2h(h.src, t->d.s_src, S)) ||
+      (r = d2h(h.child, t->d.s_child, S)) || (r = d2h(h.dict, t->d.s_dict, S)) ||
+      (r = d2h(h.flags, t->d.s_flags, S)) || (r = d2h(h.d_sent, t->d.d_sent, D)) ||
+      (r = d2h(h.l_kind, t->d.l_kind, t->log_n)) || (r = d2h(h.l_ts, t->d.l_ts, t->log_n)) ||
+      (r = d2h(h.l_val, t->d.l_val, t->log_n)) || (r = d2h(h.l_off, t->d.l_off, t->log_n + 1)) ||
+      (r = d2h(h.l_path, t->d.l_path, t->log_npath)))
+    return r;
+  if (members) {
+    h.members.assign(D, {});
+    for (uint64_t s = 0; s < S; ++s) h.members[h.dict[s]].push_back(static_cast<uint32_t>(s));
+  }
+  return CRDTM_OK;
+}
+
+void put_path(const HostTree& h, uint32_t src, Sink& s) {
+  if (src == NONE) {
+    s.put(0);
+    return;
+  }
+  const uint32_t b = h.l_off[src], e = h.l_off[src + 1];
+  const uint32_t L = e - b;  // node path = op path without its last element, then ts
+  s.put(static_cast<int64_t>(L));
+  for (uint32_t j = b; j + 1 < e; ++j) s.put(h.l_path[j]);
+  s.put(h.l_ts[src]);
+}
+
+void dump_dict(const HostTree& h, uint32_t d, int64_t depth, Sink& s) {
+  std::vector<uint32_t> m = h.members[d];
+  std::sort(m.begin(), m.end(), [&](uint32_t a, uint32_t b) { return h.key[a] < h.key[b]; });
+  for (uint32_t x : m) {
+    const bool tomb = h.flags[x] & F_TOMB;
+    s.put(depth);
+    s.put(h.key[x]);
+    s.put(tomb ? 2 : 1);
+    const uint32_t nx = h.next[x];
+    s.put(nx != NONE ? 1 : 0);
+    s.put(nx != NONE ? h.key[nx] : 0);
+    s.put(tomb ? 0 : static_cast<int64_t>(h.l_val[h.src[x]]));
+    put_path(h, h.src[x], s);
+    if (!tomb && h.child[x] != NONE) dump_dict(h, h.child[x], depth + 1, s);
+  }
+}
+
+void dump_visible(const HostTree& h, uint32_t d, int64_t depth, Sink& s) {
+  uint32_t cur = h.d_sent[d];
+  for (;;) {
+    uint32_t nx = h.next[cur];
+    while (nx != NONE && (h.flags[nx] & F_TOMB)) nx = h.next[nx];
+    if (nx == NONE) break;
+    s.put(depth);
+    s.put(static_cast<int64_t>(h.l_val[h.src[nx]]));
+    put_path(h, h.src[nx], s);
+    if (h.child[nx] != NONE) dump_visible(h, h.child[nx], depth + 1, s);
+    cur = nx;
+  }
+}
+
+uint64_t arena_need(uint64_t n, uint64_t np, const crdtm_tree* t) {
+  const uint64_t slots = t->cap.slots + 2 * n + 1024;
+  return 640 * n + 16 * np + 48 * slots + 32 * t->cap.dicts + (64ULL << 20);
+}
+
+int ensure_arena(crdtm_ctx* c, uint64_t bytes) {
+  if (c->ws.cap >= bytes) return CRDTM_OK;
+  HIP_CHECK(hipStreamSynchronize(c->stream));
+  if (c->ws.base) HIP_CHECK(hipFree(c->ws.base));
+  c->ws.base = nullptr;
+  c->ws.cap = 0;
+  const uint64_t cap = bytes + bytes / 4;
+  HIP_CHECK(hipMalloc(&c->ws.base, cap));
+  c->ws.cap = cap;
+  return CRDTM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int crdtm_version(void) { return 1; }
+
+int crdtm_device_count(int* count) {
+  if (!count) return CRDTM_E_ARG;
+  if (hipGetDeviceCount(count) != hipSuccess) {
+    *count = 0;
+    return CRDTM_E_NODEVICE;
+  }
+  return CRDTM_OK;
+}
+
+int crdtm_ctx_create(int device, void* stream, crdtm_ctx** out) {
+  if (!out) return CRDTM_E_ARG;
+  int nd = 0;
+  if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) return CRDTM_E_NODEVICE;
+  if (device < 0 || device >= nd) return CRDTM_E_ARG;
+  HIP_CHECK(hipSetDevice(device));
+  auto* c = new crdtm_ctx;
+  c->device = device;
+  if (stream) {
+    c->stream = static_cast<hipStream_t>(stream);
+  } else {
+    HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->own_stream = true;
+  }
+  HIP_CHECK(hipMalloc(&c->dres, sizeof(DevResult)));
+  HIP_CHECK(hipHostMalloc(&c->hres, sizeof(DevResult), hipHostMallocDefault));
+  HIP_CHECK(hipMalloc(&c->rtab, REPLICA_SLOTS * sizeof(uint32_t)));
+  HIP_CHECK(hipMemsetAsync(c->rtab, 0, REPLICA_SLOTS * sizeof(uint32_t), c->stream));
+  int r = ensure_arena(c, 64ULL << 20);
+  if (r) return r;
+  HIP_CHECK(hipStreamSynchronize(c->stream));
+  *out = c;
+  return CRDTM_OK;
+}
+
+int crdtm_ctx_destroy(crdtm_ctx* c) {
+  if (!c) return CRDTM_OK;
+  hipStreamSynchronize(c->stream);
+  for (auto& m : c->marks) hipEventDestroy(m.second);
+  if (c->ws.base) hipFree(c->ws.base);
+  hipFree(c->dres);
+  hipHostFree(c->hres);
+  hipFree(c->rtab);
+  if (c->own_stream) hipStreamDestroy(c->stream);
+  delete c;
+  return CRDTM_OK;
+}
+
+void* crdtm_ctx_stream(crdtm_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
+
+int crdtm_ctx_sync(crdtm_ctx* c) {
+  if (!c) return CRDTM_E_ARG;
+  HIP_CHECK(hipStreamSynchronize(c->stream));
+  return CRDTM_OK;
+}
+
+int crdtm_tree_create(crdtm_ctx* c, int64_t replica_id, crdtm_tree** out) {
+  if (!c || !out) return CRDTM_E_ARG;
+  HIP_CHECK(hipSetDevice(c->device));
+  auto* t = new crdtm_tree;
+  t->ctx = c;
+  TreeCaps need;
+  need.slots = 1024;
+  need.dicts = 512;
+  need.log = 1024;
+  need.lpath = 4096;
+  need.doc = 1024;
+  int r = grow_tree(t, need);
+  if (r) return r;
+  // init: Root {0: Tombstone [] Nothing} (src/Internal/Node.elm:41-48)
+  const long long k0 = 0;
+  const uint32_t none = NONE, zero = 0;
+  const uint8_t fl = F_TOMB | F_SENT;
+  HIP_CHECK(hipMemcpy(t->d.s_key, &k0, sizeof(k0), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(t->d.s_next, &none, 4, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(t->d.s_src, &none, 4, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(t->d.s_child, &none, 4, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(t->d.s_dict, &zero, 4, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(t->d.s_flags, &fl, 1, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(t->d.d_sent, &zero, 4, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(t->d.d_owner, &none, 4, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(t->d.l_off, &zero, 4, hipMemcpyHostToDevice));
+  t->n_slots = 1;
+  t->n_dicts = 1;
+  t->timestamp = replica_id * TWO32;  // replicaId * 2 ^ 32 (src/CRDTree.elm:137)
+  t->doc_valid = true;
+  t->doc_n = 0;
+  *out = t;
+  return CRDTM_OK;
+}
+
+int crdtm_tree_destroy(crdtm_tree* t) {
+  if (!t) return CRDTM_OK;
+  hipStreamSynchronize(t->ctx->stream);
+  void* ps[] = {t->d.s_key, t->d.s_next, t->d.s_src, t->d.s_child, t->d.s_dict, t->d.s_flags, t->d.d_sent,
+                t->d.d_owner, t->d.l_kind, t->d.l_ts, t->d.l_val, t->d.l_off, t->d.l_path, t->d.doc};
+  for (void* p : ps)
+    if (p) hipFree(p);
+  delete t;
+  return CRDTM_OK;
+}
+
+int crdtm_tree_clone(const crdtm_tree* t, crdtm_tree** out) {
+  if (!t || !out) return CRDTM_E_ARG;
+  HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+  auto* u = new crdtm_tree;
+  u->ctx = t->ctx;
+  int r = grow_tree(u, t->cap);
+  if (r) return r;
+  auto cp = [&](void* dst, const void* src, uint64_t bytes) -> int {
+    if (bytes) HIP_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice));
+    return CRDTM_OK;
+  };
+  const uint64_t S = t->n_slots, D = t->n_dicts, Ln = t->log_n;
+  if ((r = cp(u->d.s_key, t->d.s_key, S * 8)) || (r = cp(u->d.s_next, t->d.s_next, S * 4)) ||
+      (r = cp(u->d.s_src, t->d.s_src, S * 4)) || (r = cp(u->d.s_child, t->d.s_child, S * 4)) ||
+      (r = cp(u->d.s_dict, t->d.s_dict, S * 4)) || (r = cp(u->d.s_flags, t->d.s_flags, S)) ||
+      (r = cp(u->d.d_sent, t->d.d_sent, D * 4)) || (r = cp(u->d.d_owner, t->d.d_owner, D * 4)) ||
+      (r = cp(u->d.l_kind, t->d.l_kind, Ln)) || (r = cp(u->d.l_ts, t->d.l_ts, Ln * 8)) ||
+      (r = cp(u->d.l_val, t->d.l_val, Ln * 4)) || (r = cp(u->d.l_off, t->d.l_off, (Ln + 1) * 4)) ||
+      (r = cp(u->d.l_path, t->d.l_path, t->log_npath * 8)) ||
+      (r = cp(u->d.doc, t->d.doc, (t->doc_valid ? t->doc_n : 0) * 4)))
+    return r;
+  u->n_slots = S;
+  u->n_dicts = D;
+  u->log_n = Ln;
+  u->log_npath = t->log_npath;
+  u->doc_n = t->doc_n;
+  u->doc_valid = t->doc_valid;
+  u->max_depth = t->max_depth;
+  u->timestamp = t->timestamp;
+  u->replicas = t->replicas;
+  u->last_begin = t->last_begin;
+  u->last_end = t->last_end;
+  u->last_is_batch = t->last_is_batch;
+  *out = u;
+  return CRDTM_OK;
+}
+
+int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_batch, uint8_t* status_out,
+                crdtm_result* res) {
+  if (!t || !ops || !res) return CRDTM_E_ARG;
+  std::memset(res, 0, sizeof(*res));
+  res->err_index = -1;
+  if (!is_batch && ops->n_ops != 1) return CRDTM_E_ARG;
+  if (ops->n_ops >= 0x7FFFFFF0ULL) return CRDTM_E_ARG;
+  crdtm_ctx* c = t->ctx;
+  HIP_CHECK(hipSetDevice(c->device));
+  for (auto& m : c->marks) hipEventDestroy(m.second);
+  c->marks.clear();
+  const uint64_t n = ops->n_ops;
+  uint64_t np = ops->n_path;
+  if (!ops_on_device && n) np = ops->path_off[n];
+  int r = CRDTM_OK;
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    r = ensure_arena(c, arena_need(n, np, t) << attempt);
+    if (r) return r;
+    c->ws.reset();
+    try {
+      OpsDev o;
+      o.n = static_cast<uint32_t>(n);
+      o.n_path = np;
+      uint8_t* st_dev = nullptr;
+      if (ops_on_device) {
+        o.kind = ops->kind;
+        o.ts = reinterpret_cast<const long long*>(ops->ts);
+        o.off = ops->path_off;
+        o.path = reinterpret_cast<const long long*>(ops->path);
+        o.val = ops->val;
+        st_dev = status_out;
+      } else {
+        hipStream_t s = c->stream;
+        auto* kind = c->ws.alloc<uint8_t>(n + 1);
+        auto* ts = c->ws.alloc<long long>(n + 1);
+        auto* off = c->ws.alloc<uint32_t>(n + 1);
+        auto* path = c->ws.alloc<long long>(np + 1);
+        auto* val = c->ws.alloc<uint32_t>(n + 1);
+        if (n) {
+          HIP_CHECK(hipMemcpyAsync(kind, ops->kind, n, hipMemcpyHostToDevice, s));
+          HIP_CHECK(hipMemcpyAsync(ts, ops->ts, n * 8, hipMemcpyHostToDevice, s));
+          HIP_CHECK(hipMemcpyAsync(off, ops->path_off, (n + 1) * 4, hipMemcpyHostToDevice, s));
+          if (np) HIP_CHECK(hipMemcpyAsync(path, ops->path, np * 8, hipMemcpyHostToDevice, s));
+          HIP_CHECK(hipMemcpyAsync(val, ops->val, n * 4, hipMemcpyHostToDevice, s));
+        }
+        o.kind = kind;
+        o.ts = ts;
+        o.off = off;
+        o.path = path;
+        o.val = val;
+        if (status_out) st_dev = c->ws.alloc<uint8_t>(n + 1);
+      }
+      r = apply_batch(t, o, st_dev, res);
+      if (r == CRDTM_OK && status_out && !ops_on_device && n) {
+        HIP_CHECK(hipMemcpyAsync(status_out, st_dev, n, hipMemcpyDeviceToHost, c->stream));
+        HIP_CHECK(hipStreamSynchronize(c->stream));
+      }
+      break;
+    } catch (const ArenaOverflow&) {
+      HIP_CHECK(hipStreamSynchronize(c->stream));
+      r = CRDTM_E_NOMEM;
+    }
+  }
+  if (r != CRDTM_OK) {
+    res->code = r;
+    return r;
+  }
+  if (res->code == CRDTM_OK) {
+    // lastOperation: the op itself, or Batch of the applied ops; an
+    // AlreadyApplied single op leaves Batch [] (src/CRDTree.elm:318-319)
+    t->last_is_batch = (is_batch || res->n_applied == 0) ? 1 : 0;
+  }
+  res->timestamp = t->timestamp;
+  res->n_slots = t->n_slots;
+  if (c->profile) {
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    c->phases.clear();
+    for (size_t k = 1; k < c->marks.size(); ++k) {
+      float ms = 0;
+      hipEventElapsedTime(&ms, c->marks[k - 1].second, c->marks[k].second);
+      c->phases.emplace_back(c->marks[k].first, ms);
+    }
+  }
+  return res->code < 0 ? res->code : CRDTM_OK;
+}
+
+int crdtm_tree_timestamp(const crdtm_tree* t, int64_t* out) {
+  if (!t || !out) return CRDTM_E_ARG;
+  *out = t->timestamp;
+  return CRDTM_OK;
+}
+
+int crdtm_tree_replicas(const crdtm_tree* t, int64_t* ids, int64_t* tss, uint64_t cap, uint64_t* n) {
+  if (!t || !n) return CRDTM_E_ARG;
+  uint64_t i = 0;
+  for (const auto& kv : t->replicas) {
+    if (ids && tss && i < cap) {
+      ids[i] = kv.first;
+      tss[i] = kv.second;
+    }
+    ++i;
+  }
+  *n = i;
+  return CRDTM_OK;
+}
+
+int crdtm_tree_ops(const crdtm_tree* t, int which, crdtm_ops* out, int* is_batch) {
+  if (!t || !out) return CRDTM_E_ARG;
+  const uint64_t b = which == 0 ? 0 : t->last_begin;
+  const uint64_t e = which == 0 ? t->log_n : t->last_end;
+  if (is_batch) *is_batch = which == 0 ? 1 : t->last_is_batch;
+  const uint64_t n = e - b;
+  std::vector<uint32_t> off(n + 1);
+  HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+  if (n + 1) HIP_CHECK(hipMemcpy(off.data(), t->d.l_off + b, (n + 1) * 4, hipMemcpyDeviceToHost));
+  const uint64_t pb = off[0], pe = off[n];
+  const bool fill = out->kind != nullptr;
+  out->n_ops = n;
+  out->n_path = pe - pb;
+  if (!fill) return CRDTM_OK;
+  if (n) {
+    HIP_CHECK(hipMemcpy(out->kind, t->d.l_kind + b, n, hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(out->ts, t->d.l_ts + b, n * 8, hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(out->val, t->d.l_val + b, n * 4, hipMemcpyDeviceToHost));
+  }
+  for (uint64_t i = 0; i <= n; ++i) out->path_off[i] = off[i] - static_cast<uint32_t>(pb);
+  if (pe > pb) HIP_CHECK(hipMemcpy(out->path, t->d.l_path + pb, (pe - pb) * 8, hipMemcpyDeviceToHost));
+  return CRDTM_OK;
+}
+
+int crdtm_tree_canonical(const crdtm_tree* t, int which, int64_t* out, uint64_t cap, uint64_t* n_words,
+                         uint64_t* hash) {
+  if (!t) return CRDTM_E_ARG;
+  HostTree h;
+  int r = fetch(t, h, which == 0);
+  if (r) return r;
+  Sink s{out, cap};
+  if (which == 0) dump_dict(h, 0, 0, s);
+  else dump_visible(h, 0, 0, s);
+  if (n_words) *n_words = s.n;
+  if (hash) *hash = s.h;
+  return CRDTM_OK;
+}
+
+__global__ void k_doc_vals(const uint32_t* doc, uint64_t n, const uint32_t* src, const uint32_t* lval,
+                           uint32_t* out) {
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    out[i] = lval[src[doc[i]]];
+}
+
+int crdtm_tree_document(const crdtm_tree* tc, uint32_t* vals, uint64_t cap, uint64_t* n_visible) {
+  if (!tc || !n_visible) return CRDTM_E_ARG;
+  auto* t = const_cast<crdtm_tree*>(tc);
+  crdtm_ctx* c = t->ctx;
+  HIP_CHECK(hipSetDevice(c->device));
+  int r = ensure_arena(c, arena_need(0, 0, t) + 64 * (t->n_slots + t->n_dicts));
+  if (r) return r;
+  try {
+    if ((r = linearize(t))) return r;
+    *n_visible = t->doc_n;
+    if (vals && t->doc_n) {
+      c->ws.reset();
+      uint32_t* tmp = c->ws.alloc<uint32_t>(t->doc_n);
+      hipLaunchKernelGGL(k_doc_vals, dim3(grid_for(t->doc_n)), dim3(BLOCK), 0, c->stream, t->d.doc, t->doc_n,
+                         t->d.s_src, t->d.l_val, tmp);
+      const uint64_t m = std::min<uint64_t>(cap, t->doc_n);
+      HIP_CHECK(hipMemcpyAsync(vals, tmp, m * 4, hipMemcpyDeviceToHost, c->stream));
+      HIP_CHECK(hipStreamSynchronize(c->stream));
+    }
+  } catch (const ArenaOverflow&) {
+    return CRDTM_E_NOMEM;
+  }
+  return CRDTM_OK;
+}
+
+int crdtm_ctx_profile(crdtm_ctx* c, int enable) {
+  if (!c) return CRDTM_E_ARG;
+  c->profile = enable != 0;
+  return CRDTM_OK;
+}
+
+int crdtm_ctx_phase_times(crdtm_ctx* c, char* names, size_t names_cap, double* ms, int cap) {
+  if (!c) return CRDTM_E_ARG;
+  size_t pos = 0;
+  int k = 0;
+  for (auto& p : c->phases) {
+    if (k < cap) {
+      if (ms) ms[k] = p.second;
+      if (names && pos + p.first.size() + 1 <= names_cap) {
+        std::memcpy(names + pos, p.first.c_str(), p.first.size() + 1);
+        pos += p.first.size() + 1;
+      }
+    }
+    ++k;
+  }
+  return k;
+}
+
+void crdtm_free(void* p) { std::free(p); }
+
+}  // extern "C"

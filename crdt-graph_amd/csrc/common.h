@@ -1,0 +1,83 @@
+// common.h — shared host/device definitions of the crdtm engine (gfx950).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/crdtm.h"
+
+namespace crdtm {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;     // absent index / list end
+constexpr uint32_t ABSENT = 0xFFFFFFFEu;   // entry not part of a list
+constexpr int64_t TWO53 = 9007199254740992LL;
+constexpr int64_t TWO32 = 4294967296LL;
+constexpr int REPLICA_BITS = 22;           // replica ids in (-2^21, 2^21) when |ts| < 2^53
+constexpr uint32_t REPLICA_SLOTS = 1u << REPLICA_BITS;
+constexpr int BLOCK = 256;
+
+// Per-op status codes (crdtm.h CRDTM_ST_*) plus internal states.
+enum : uint8_t {
+  ST_APPLIED = CRDTM_ST_APPLIED,
+  ST_ALREADY = CRDTM_ST_ALREADY,
+  ST_INVALID = 4,   // Err InvalidPath
+  ST_NOTFOUND = 5,  // Err NotFound -> OperationFailed op
+  ST_PENDING = 6,
+};
+
+// Guard bits (crdtm_result.guard)
+enum : uint32_t {
+  G_COLLISION = 1u,     // same ts added under two different parents
+  G_DEL_BEFORE_ADD = 2u,// a dict saw a Delete before a later Add (tombstones in the skip walk)
+  G_REPLICA_DRIFT = 4u, // own replica id changes during the batch (timestamp crosses 2^32)
+  G_NOT_FRESH = 8u,     // tree already holds state (incremental merge)
+};
+
+// Small device-side result block (one copy back per phase).
+struct DevResult {
+  uint32_t err_index;       // atomicMin over erroring ops
+  uint32_t guard;           // G_* bits
+  uint32_t max_len;         // longest path
+  uint32_t bad_range;       // |ts| >= 2^53 present
+  uint32_t n_applied;
+  uint32_t n_already;
+  uint32_t n_adds_applied;
+  uint32_t own_ok_adds;     // Ok adds with replicaId(ts) == tree id (timestamp bumps)
+  uint32_t n_replica_out;
+  uint32_t n_nodes_kept;    // closed form: nodes that survive (dict alive)
+  uint32_t n_live_kept;     // kept nodes that own a children dict
+  uint32_t n_sentinels;     // present sentinels (Euler)
+  uint32_t log_n;           // applied ops (log entries appended)
+  uint32_t log_npath;
+  uint32_t replay_slots;    // replay: slots used
+  uint32_t replay_dicts;
+  uint32_t replay_overflow;
+  uint32_t replay_err_code;
+  int64_t replay_timestamp;
+  uint32_t n_split[8];      // list ranking level sizes
+  uint32_t big_segments;
+  uint32_t pad[3];
+};
+
+#define HIP_CHECK(x)                                                                         \
+  do {                                                                                       \
+    hipError_t e_ = (x);                                                                     \
+    if (e_ != hipSuccess) {                                                                  \
+      std::fprintf(stderr, "crdtm HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, \
+                   __LINE__);                                                                \
+      return CRDTM_E_HIP;                                                                    \
+    }                                                                                        \
+  } while (0)
+
+inline uint32_t grid_for(uint64_t n, int block = BLOCK, uint32_t cap = 1u << 20) {
+  uint64_t g = (n + block - 1) / block;
+  if (g == 0) g = 1;
+  return static_cast<uint32_t>(g < cap ? g : cap);
+}
+
+}  // namespace crdtm

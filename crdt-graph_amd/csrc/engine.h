@@ -1,0 +1,121 @@
+// engine.h — crdtm engine internals: workspace arena, context, tree state,
+// and the host-side launch entry points of each kernel family.
+#pragma once
+
+#include <stdexcept>
+
+#include "kernels.h"
+
+namespace crdtm {
+
+struct ArenaOverflow : std::runtime_error {
+  size_t need;
+  explicit ArenaOverflow(size_t n) : std::runtime_error("arena overflow"), need(n) {}
+};
+
+// Bump allocator over one device allocation, reset per call. Overflow throws
+// (host side, before any tree mutation); the API layer grows and retries.
+struct Arena {
+  char* base = nullptr;
+  size_t cap = 0;
+  size_t used = 0;
+  size_t high = 0;
+  template <class T>
+  T* alloc(uint64_t n) {
+    size_t b = (static_cast<size_t>(n) * sizeof(T) + 255) & ~static_cast<size_t>(255);
+    if (b == 0) b = 256;
+    if (used + b > cap) throw ArenaOverflow(used + b);
+    T* p = reinterpret_cast<T*>(base + used);
+    used += b;
+    if (used > high) high = used;
+    return p;
+  }
+  void reset() { used = 0; }
+};
+
+enum : uint8_t { F_TOMB = 1, F_ORPHAN = 2, F_SENT = 4 };
+
+// Device-resident CRDTree state (the "replay representation"): one slot per
+// dict entry. Slot s lives in dict s_dict[s] under key s_key[s]; s_next is the
+// slot of the entry named by its `next` key (Elm keeps the key; within a dict
+// the two are interchangeable); s_src is the op-log index of the Add whose
+// path and value the entry carries (a findInsertion copy carries the copied
+// node's source); s_child is the children dict of a live Node.
+struct TreeDev {
+  long long* s_key = nullptr;
+  uint32_t* s_next = nullptr;
+  uint32_t* s_src = nullptr;
+  uint32_t* s_child = nullptr;
+  uint32_t* s_dict = nullptr;
+  uint8_t* s_flags = nullptr;
+  uint32_t* d_sent = nullptr;   // dict -> sentinel slot
+  uint32_t* d_owner = nullptr;  // dict -> owning slot (NONE for the root dict)
+  // operation log, oldest first
+  uint8_t* l_kind = nullptr;
+  long long* l_ts = nullptr;
+  uint32_t* l_val = nullptr;
+  uint32_t* l_off = nullptr;
+  long long* l_path = nullptr;
+  // document order from the last closed-form merge (vis rank -> slot)
+  uint32_t* doc = nullptr;
+};
+
+struct TreeCaps {
+  uint64_t slots = 0, dicts = 0, log = 0, lpath = 0, doc = 0;
+};
+
+}  // namespace crdtm
+
+struct crdtm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  crdtm::Arena ws;
+  crdtm::DevResult* dres = nullptr;  // device
+  crdtm::DevResult* hres = nullptr;  // pinned host
+  uint32_t* rtab = nullptr;          // replica table [REPLICA_SLOTS], 0 = empty (kept clean between calls)
+  bool profile = false;
+  std::vector<std::pair<std::string, hipEvent_t>> marks;
+  std::vector<std::pair<std::string, double>> phases;
+};
+
+struct crdtm_tree {
+  crdtm_ctx* ctx = nullptr;
+  crdtm::TreeDev d;
+  crdtm::TreeCaps cap;
+  uint64_t n_slots = 0, n_dicts = 0, log_n = 0, log_npath = 0, doc_n = 0;
+  bool doc_valid = false;
+  uint32_t max_depth = 0;
+  int64_t timestamp = 0;
+  std::map<int64_t, int64_t> replicas;
+  uint64_t last_begin = 0, last_end = 0;
+  int last_is_batch = 1;
+};
+
+namespace crdtm {
+
+// primitives.hip
+int scan_excl_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* total, Arena& ws, hipStream_t st);
+int segmented_sort(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items,
+                   const long long* sort_key, Arena& ws, hipStream_t st, DevResult* dres);
+int list_rank(const uint32_t* succ, const unsigned long long* w, uint64_t n, uint32_t head,
+              unsigned long long* excl, Arena& ws, hipStream_t st, DevResult* dres, int level);
+
+// Device view of one batch of ops.
+struct OpsDev {
+  uint32_t n = 0;
+  uint64_t n_path = 0;
+  const uint8_t* kind = nullptr;
+  const long long* ts = nullptr;
+  const uint32_t* off = nullptr;
+  const long long* path = nullptr;
+  const uint32_t* val = nullptr;
+};
+
+// merge.hip
+int grow_tree(crdtm_tree* t, const TreeCaps& need);
+int apply_batch(crdtm_tree* t, const OpsDev& ops, uint8_t* status_dev, crdtm_result* res);
+int linearize(crdtm_tree* t);  // fills t->d.doc / t->doc_n from the tree state
+void mark(crdtm_ctx* c, const char* name);
+
+}  // namespace crdtm

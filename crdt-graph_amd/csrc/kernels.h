@@ -1,0 +1,121 @@
+// kernels.h — device helpers shared by the crdtm kernels (gfx950, wave64).
+#pragma once
+
+#include "common.h"
+
+namespace crdtm {
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z ^= z >> 33;
+  z *= 0xff51afd7ed558ccdULL;
+  z ^= z >> 33;
+  z *= 0xc4ceb9fe1a85ec53ULL;
+  z ^= z >> 33;
+  return z;
+}
+
+// replicaId ts = ts // 2^32 with Elm/JS (a / b) | 0 truncation (src/CRDTree/Timestamp.elm:16-18)
+__host__ __device__ __forceinline__ int64_t replica_of(int64_t ts) { return ts / TWO32; }
+
+// ---- ts -> first Add index (open addressing, linear probing). Keys are stored
+// XOR INT64_MIN so that an all-zero memset means "empty".
+struct TsHash {
+  unsigned long long* keys;  // ts ^ INT64_MIN, 0 = empty
+  uint32_t* vals;            // min op index, 0xFFFFFFFF = none
+  uint32_t mask;
+};
+
+__device__ __forceinline__ void tshash_insert(TsHash h, int64_t ts, uint32_t idx) {
+  const unsigned long long k = static_cast<unsigned long long>(ts) ^ 0x8000000000000000ULL;
+  uint32_t p = static_cast<uint32_t>(mix64(k)) & h.mask;
+  for (;;) {
+    unsigned long long prev = atomicCAS(&h.keys[p], 0ULL, k);
+    if (prev == 0ULL || prev == k) {
+      atomicMin(&h.vals[p], idx);
+      return;
+    }
+    p = (p + 1) & h.mask;
+  }
+}
+
+__device__ __forceinline__ uint32_t tshash_find(TsHash h, int64_t ts) {
+  const unsigned long long k = static_cast<unsigned long long>(ts) ^ 0x8000000000000000ULL;
+  uint32_t p = static_cast<uint32_t>(mix64(k)) & h.mask;
+  for (;;) {
+    unsigned long long kk = h.keys[p];
+    if (kk == k) return h.vals[p];
+    if (kk == 0ULL) return NONE;
+    p = (p + 1) & h.mask;
+  }
+}
+
+// ---- (dict, key) -> slot hash used by the exact replay (single writer per entry).
+struct SlotHash {
+  uint32_t* dict;
+  long long* key;
+  uint32_t* slot;  // NONE = empty
+  uint32_t mask;
+};
+
+__device__ __forceinline__ uint32_t slothash_pos(uint32_t d, int64_t k, uint32_t mask) {
+  return static_cast<uint32_t>(mix64(static_cast<uint64_t>(k) ^ (static_cast<uint64_t>(d) * 0x9E3779B97F4A7C15ULL))) &
+         mask;
+}
+
+__device__ __forceinline__ uint32_t slothash_find(const SlotHash& h, uint32_t d, int64_t k) {
+  uint32_t p = slothash_pos(d, k, h.mask);
+  for (;;) {
+    uint32_t s = h.slot[p];
+    if (s == NONE) return NONE;
+    if (h.dict[p] == d && h.key[p] == k) return s;
+    p = (p + 1) & h.mask;
+  }
+}
+
+// Sequential insert (replay thread) — the key must be absent.
+__device__ __forceinline__ void slothash_put_seq(const SlotHash& h, uint32_t d, int64_t k, uint32_t s) {
+  uint32_t p = slothash_pos(d, k, h.mask);
+  while (h.slot[p] != NONE) {
+    if (h.dict[p] == d && h.key[p] == k) { h.slot[p] = s; return; }
+    p = (p + 1) & h.mask;
+  }
+  h.dict[p] = d;
+  h.key[p] = k;
+  h.slot[p] = s;
+}
+
+// Parallel insert (build kernel) — distinct (d, k) per caller.
+__device__ __forceinline__ void slothash_put_par(const SlotHash& h, uint32_t d, int64_t k, uint32_t s) {
+  uint32_t p = slothash_pos(d, k, h.mask);
+  for (;;) {
+    if (atomicCAS(&h.slot[p], NONE, s) == NONE) {
+      h.dict[p] = d;
+      h.key[p] = k;
+      return;
+    }
+    p = (p + 1) & h.mask;
+  }
+}
+
+// wave64 inclusive scan of u32 (CDNA: 64 lanes, __shfl_up over width 64)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long long v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    unsigned long long t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+}  // namespace crdtm

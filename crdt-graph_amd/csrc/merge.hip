@@ -1,0 +1,1255 @@
+// merge.hip — the CRDTree batch merge on gfx950.
+//
+// Replaces the reference's sequential `apply (Batch ops)` (src/CRDTree.elm:
+// 224-232, :265-350; src/Internal/Node.elm:51-163) for a whole batch.
+//
+// Two exact paths share one device tree state (engine.h TreeDev):
+//  * closed form (fresh tree, guard holds): per-op status by level-synchronous
+//    path resolution (K1), effective-parent pointer jumping + segmented sibling
+//    sort (K2), tombstone scatter (K3), Euler tour + list ranking for the raw
+//    `next` chains and the document order (K4), then a commit that writes the
+//    tree state and appends the op log;
+//  * exact replay (everything else): one lane replays the batch with the
+//    reference's literal addAfterHelp/findInsertion/deleteHelp semantics,
+//    including the findInsertion copy quirk, with an undo log for atomicity.
+// DESIGN.md derives the closed form and its guard.
+
+#include "engine.h"
+
+namespace crdtm {
+
+constexpr uint32_t SENT_T = 0xFFFFFFFDu;  // leaf target: the dict's sentinel (key 0)
+constexpr uint32_t MISS_T = 0xFFFFFFFCu;  // leaf target: key not in the dict
+
+struct Work {  // per-call device arrays of the closed form (sized by n ops)
+  uint8_t* st;
+  uint32_t* cur;
+  uint32_t* nxt;
+  uint32_t* leaf;
+  uint32_t* addpar;
+  uint32_t* dtime;
+  uint8_t* dead;
+  uint32_t* maxadd;
+};
+
+__device__ __forceinline__ uint32_t op_len(const OpsDev& o, uint32_t i) { return o.off[i + 1] - o.off[i]; }
+
+// block-level OR/MAX reduction helpers (one atomic per block)
+__device__ __forceinline__ uint32_t block_max(uint32_t v) {
+  __shared__ uint32_t s[BLOCK / 64];
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t r = 0;
+  for (int w = 0; w < BLOCK / 64; ++w) r = max(r, s[w]);
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ uint32_t block_sum(uint32_t v) {
+  __shared__ uint32_t s[BLOCK / 64];
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t r = 0;
+  for (int w = 0; w < BLOCK / 64; ++w) r += s[w];
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ uint32_t block_min(uint32_t v) {
+  __shared__ uint32_t s[BLOCK / 64];
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t r = NONE;
+  for (int w = 0; w < BLOCK / 64; ++w) r = min(r, s[w]);
+  __syncthreads();
+  return r;
+}
+
+#define GRID_STRIDE(i, n) \
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += gridDim.x * blockDim.x)
+
+// ---------------------------------------------------------------------------
+// K1 — per-op status under sequential semantics (src/Internal/Node.elm:138-163,
+// :56-90, :112-122; src/CRDTree.elm:298-325). Nodes are named by the index of
+// the first Add of their timestamp; the root dict owner is ROOTN = n.
+// ---------------------------------------------------------------------------
+
+__global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, Work w, TsHash h, DevResult* dres) {
+  uint32_t mx = 0, bad = 0;
+  const uint32_t n = o.n;
+  // grid-stride with a uniform trip count so every lane reaches the block reductions
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t trips = (n + stride - 1) / stride;
+  for (uint32_t t = 0; t < trips; ++t) {
+    const uint32_t i = t * stride + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) continue;
+    const uint32_t L = op_len(o, i);
+    mx = max(mx, L);
+    const bool add = o.kind[i] == CRDTM_ADD;
+    const long long ts = add ? o.ts[i] : 0;
+    if (ts >= TWO53 || ts <= -TWO53) bad = 1;
+    w.st[i] = L == 0 ? ST_INVALID : ST_PENDING;
+    w.cur[i] = n;
+    w.addpar[i] = NONE;
+    w.dtime[i] = NONE;
+    if (add && L >= 1 && ts != 0 && !bad) tshash_insert(h, ts, i);
+  }
+  mx = block_max(mx);
+  bad = block_max(bad);
+  if (threadIdx.x == 0) {
+    if (mx) atomicMax(&dres->max_len, mx);
+    if (bad) atomicOr(&dres->bad_range, 1u);
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_path_range(const long long* path, uint64_t np, DevResult* dres) {
+  uint32_t bad = 0;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  const uint64_t trips = (np + stride - 1) / stride;
+  for (uint64_t t = 0; t < trips; ++t) {
+    const uint64_t p = t * stride + blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+    if (p < np) {
+      const long long x = path[p];
+      if (x >= TWO53 || x <= -TWO53) bad = 1;
+    }
+  }
+  bad = block_max(bad);
+  if (threadIdx.x == 0 && bad) atomicOr(&dres->bad_range, 1u);
+}
+
+// Adds whose path has length lvl record their dict owner (resolved prefix).
+__global__ void __launch_bounds__(BLOCK) k_lvl_addpar(OpsDev o, Work w, uint32_t lvl) {
+  GRID_STRIDE(i, o.n) {
+    if (o.kind[i] == CRDTM_ADD && w.st[i] == ST_PENDING && op_len(o, i) == lvl) w.addpar[i] = w.cur[i];
+  }
+}
+
+// The closed form names a node by its timestamp alone; the same ts added under
+// two different parents breaks that and routes the batch to the replay.
+__global__ void __launch_bounds__(BLOCK) k_lvl_collide(OpsDev o, Work w, TsHash h, uint32_t lvl, DevResult* dres) {
+  GRID_STRIDE(i, o.n) {
+    if (o.kind[i] != CRDTM_ADD || op_len(o, i) != lvl || w.addpar[i] == NONE) continue;
+    const long long ts = o.ts[i];
+    if (ts == 0) continue;
+    const uint32_t f = tshash_find(h, ts);
+    if (f != i && (op_len(o, f) != lvl || w.addpar[f] != w.addpar[i])) atomicOr(&dres->guard, G_COLLISION);
+  }
+}
+
+__device__ __forceinline__ uint32_t lookup_child(const OpsDev& o, const Work& w, const TsHash& h, uint32_t parent,
+                                                 long long k, uint32_t lvl) {
+  if (k == 0) return SENT_T;
+  const uint32_t f = tshash_find(h, k);
+  if (f == NONE || op_len(o, f) != lvl || w.addpar[f] != parent) return MISS_T;
+  return f;
+}
+
+// Resolve path element lvl (1-based) of every pending op.
+__global__ void __launch_bounds__(BLOCK) k_lvl_resolve(OpsDev o, Work w, TsHash h, uint32_t lvl) {
+  GRID_STRIDE(i, o.n) {
+    if (w.st[i] != ST_PENDING) continue;
+    const uint32_t L = op_len(o, i);
+    if (L < lvl) continue;
+    const long long k = o.path[o.off[i] + lvl - 1];
+    const uint32_t tgt = lookup_child(o, w, h, w.cur[i], k, lvl);
+    if (L > lvl) {
+      // update: child k missing -> InvalidPath; found Tombstone (the sentinel) -> AlreadyApplied
+      if (tgt == MISS_T || (tgt != SENT_T && tgt >= i)) w.st[i] = ST_INVALID;
+      else if (tgt == SENT_T) w.st[i] = ST_ALREADY;
+      else w.nxt[i] = tgt;
+    } else {
+      w.leaf[i] = tgt;
+    }
+  }
+}
+
+// Deletes at this level: deleteHelp (src/Internal/Node.elm:112-122). The first
+// Delete of a node that reaches it while its dict is live tombstones it.
+__global__ void __launch_bounds__(BLOCK) k_lvl_del(OpsDev o, Work w, uint32_t lvl) {
+  GRID_STRIDE(i, o.n) {
+    if (o.kind[i] != CRDTM_DELETE || w.st[i] != ST_PENDING || op_len(o, i) != lvl) continue;
+    const uint32_t t = w.leaf[i];
+    if (t == SENT_T) w.st[i] = ST_ALREADY;
+    else if (t == MISS_T || t > i) w.st[i] = ST_NOTFOUND;
+    else atomicMin(&w.dtime[t], i);
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_lvl_fin(OpsDev o, Work w, TsHash h, uint32_t lvl) {
+  const uint32_t n = o.n;
+  GRID_STRIDE(i, n) {
+    if (w.st[i] != ST_PENDING) continue;
+    const uint32_t L = op_len(o, i);
+    if (L > lvl) {
+      const uint32_t x = w.nxt[i];
+      if (w.dtime[x] < i) w.st[i] = ST_ALREADY;  // descending into a Tombstone
+      else w.cur[i] = x;
+    } else if (L == lvl) {
+      if (o.kind[i] == CRDTM_DELETE) {
+        w.st[i] = (w.dtime[w.leaf[i]] == i) ? ST_APPLIED : ST_ALREADY;
+      } else {
+        const long long ts = o.ts[i];
+        uint8_t s;
+        if (ts == 0) s = ST_ALREADY;                         // key 0 = the sentinel
+        else if (tshash_find(h, ts) != i) s = ST_ALREADY;    // child ts parent exists
+        else {
+          const uint32_t a = w.leaf[i];
+          s = (a == SENT_T || (a != MISS_T && a < i)) ? ST_APPLIED : ST_NOTFOUND;
+        }
+        w.st[i] = s;
+        if (s == ST_APPLIED) {
+          const uint32_t p = w.addpar[i];
+          w.dead[i] = (w.dtime[i] != NONE || (p != n && w.dead[p])) ? 1 : 0;
+        }
+      }
+    }
+  }
+}
+
+// Batch accounting + the guard (DESIGN.md "Guard"): tombstones present in a
+// dict while later Adds land in it can change findInsertion's walk.
+__global__ void __launch_bounds__(BLOCK) k_stats(OpsDev o, Work w, long long ts0, DevResult* dres) {
+  uint32_t app = 0, alr = 0, err = NONE, own = 0, addapp = 0;
+  const long long id0 = replica_of(ts0);
+  const uint32_t n = o.n;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t trips = (n + stride - 1) / stride;
+  for (uint32_t t = 0; t < trips; ++t) {
+    const uint32_t i = t * stride + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) continue;
+    const uint8_t s = w.st[i];
+    if (s == ST_APPLIED) ++app;
+    else if (s == ST_ALREADY) ++alr;
+    else err = min(err, i);
+    if (o.kind[i] == CRDTM_ADD) {
+      if ((s == ST_APPLIED || s == ST_ALREADY) && replica_of(o.ts[i]) == id0) ++own;
+      if (s == ST_APPLIED) {
+        ++addapp;
+        atomicMax(&w.maxadd[w.addpar[i]], i + 1);
+      }
+    }
+  }
+  app = block_sum(app);
+  alr = block_sum(alr);
+  own = block_sum(own);
+  addapp = block_sum(addapp);
+  err = block_min(err);
+  if (threadIdx.x == 0) {
+    atomicAdd(&dres->n_applied, app);
+    atomicAdd(&dres->n_already, alr);
+    atomicAdd(&dres->own_ok_adds, own);
+    atomicAdd(&dres->n_adds_applied, addapp);
+    if (err != NONE) atomicMin(&dres->err_index, err);
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_guard_del(OpsDev o, Work w, DevResult* dres) {
+  GRID_STRIDE(i, o.n) {
+    if (o.kind[i] != CRDTM_DELETE || w.st[i] != ST_APPLIED) continue;
+    const uint32_t p = w.addpar[w.leaf[i]];
+    if (w.maxadd[p] > i + 1) atomicOr(&dres->guard, G_DEL_BEFORE_ADD);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K2 — placement. Closed form: with no tombstone in any skip walk,
+// findInsertion (src/Internal/Node.elm:93-104) puts x after the subtree of its
+// effective parent ep(x) = first node on x's anchor chain with a smaller ts
+// (the dict's sentinel acts as -inf), among ep's children in descending ts.
+// Unified tree: node x -> x; sentinel of dict P -> n + P (root dict: 2n);
+// super root 2n + 1. A sentinel is the first child of its owner, so a node's
+// sub-document precedes its following siblings.
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t sent_uid(uint32_t owner, uint32_t n) { return owner == n ? 2 * n : n + owner; }
+
+__global__ void __launch_bounds__(BLOCK) k_ep_init(OpsDev o, Work w, uint32_t* anc) {
+  GRID_STRIDE(x, o.n) {
+    if (o.kind[x] != CRDTM_ADD || w.st[x] != ST_APPLIED) continue;
+    const uint32_t a = w.leaf[x];
+    anc[x] = a == SENT_T ? sent_uid(w.addpar[x], o.n) : a;
+  }
+}
+
+// Pointer jumping: follow other nodes' current candidates (relaxed agent-scope
+// loads; a stale value is an older, still-valid candidate, so the walk is
+// correct under any visibility and converges by doubling).
+__global__ void __launch_bounds__(BLOCK) k_ep_jump(OpsDev o, Work w, uint32_t* anc, uint8_t* sent_present) {
+  const uint32_t n = o.n;
+  GRID_STRIDE(x, n) {
+    if (o.kind[x] != CRDTM_ADD || w.st[x] != ST_APPLIED) continue;
+    const long long tx = o.ts[x];
+    uint32_t c = anc[x];
+    while (c < n && o.ts[c] > tx) {
+      c = __hip_atomic_load(&anc[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&anc[x], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (c >= n) sent_present[c - n] = 1;
+  }
+}
+
+__device__ __forceinline__ bool uni_present(const OpsDev& o, const Work& w, const uint8_t* sp, uint32_t v) {
+  const uint32_t n = o.n;
+  if (v < n) return o.kind[v] == CRDTM_ADD && w.st[v] == ST_APPLIED;
+  if (v <= 2 * n) return sp[v - n] != 0;
+  return v == 2 * n + 1;
+}
+
+__device__ __forceinline__ uint32_t uni_up(const OpsDev& o, const uint32_t* anc, uint32_t v) {
+  const uint32_t n = o.n;
+  if (v < n) return anc[v];
+  if (v < 2 * n) return v - n;
+  return 2 * n + 1;  // root sentinel -> super root
+}
+
+__global__ void __launch_bounds__(BLOCK) k_up_count(OpsDev o, Work w, const uint32_t* anc, const uint8_t* sp,
+                                                    uint32_t* cnt, long long* skey) {
+  const uint32_t n = o.n, U = 2 * n + 1;  // super root excluded (no parent)
+  GRID_STRIDE(v, U) {
+    if (!uni_present(o, w, sp, v)) continue;
+    atomicAdd(&cnt[uni_up(o, anc, v)], 1u);
+    skey[v] = v < n ? -o.ts[v] : (long long)0x8000000000000000LL;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_scatter(OpsDev o, Work w, const uint32_t* anc, const uint8_t* sp,
+                                                   const uint32_t* start, uint32_t* fill, uint32_t* carr) {
+  const uint32_t n = o.n, U = 2 * n + 1;
+  GRID_STRIDE(v, U) {
+    if (!uni_present(o, w, sp, v)) continue;
+    const uint32_t u = uni_up(o, anc, v);
+    carr[start[u] + atomicAdd(&fill[u], 1u)] = v;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_links(OpsDev o, const uint32_t* anc, const uint32_t* start,
+                                                 const uint32_t* total, const uint32_t* carr, uint32_t* fc,
+                                                 uint32_t* ns) {
+  const uint32_t tot = *total;
+  GRID_STRIDE(p, tot) {
+    const uint32_t v = carr[p];
+    const uint32_t u = uni_up(o, anc, v);
+    if (p == start[u]) fc[u] = v;
+    ns[v] = (p + 1 < start[u + 1]) ? carr[p + 1] : NONE;
+  }
+}
+
+// Euler tour: entry 2v = enter v, 2v+1 = leave v. Weight of enter v =
+// (1 << 32) | visible(v): the high word counts tour nodes (pre-order rank),
+// the low word counts visible nodes (document rank).
+__global__ void __launch_bounds__(BLOCK) k_euler(OpsDev o, Work w, const uint32_t* anc, const uint8_t* sp,
+                                                 const uint32_t* fc, const uint32_t* ns, uint32_t* succ,
+                                                 unsigned long long* wt) {
+  const uint32_t n = o.n, U = 2 * n + 2;
+  GRID_STRIDE(v, U) {
+    if (!uni_present(o, w, sp, v)) {
+      succ[2 * v] = ABSENT;
+      succ[2 * v + 1] = ABSENT;
+      wt[2 * v] = 0;
+      wt[2 * v + 1] = 0;
+      continue;
+    }
+    succ[2 * v] = fc[v] != NONE ? 2 * fc[v] : 2 * v + 1;
+    uint32_t after;
+    if (ns[v] != NONE) after = 2 * ns[v];
+    else if (v == 2 * n + 1) after = NONE;
+    else after = 2 * uni_up(o, anc, v) + 1;
+    succ[2 * v + 1] = after;
+    uint32_t vis = 0;
+    if (v < n) {
+      const uint32_t p = w.addpar[v];
+      vis = (w.dtime[v] == NONE && (p == n || !w.dead[p])) ? 1u : 0u;
+    }
+    wt[2 * v] = (1ULL << 32) | vis;
+    wt[2 * v + 1] = 0;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_order(OpsDev o, Work w, const uint8_t* sp,
+                                                 const unsigned long long* excl, uint32_t* order) {
+  const uint32_t n = o.n, U = 2 * n + 2;
+  GRID_STRIDE(v, U) {
+    if (!uni_present(o, w, sp, v)) continue;
+    order[static_cast<uint32_t>(excl[2 * v] >> 32)] = v;
+  }
+}
+
+// next(x) within its dict = the pre-order successor after x's own sub-document
+// when that node lives in the same dict (DESIGN.md "Raw next chains").
+__global__ void __launch_bounds__(BLOCK) k_next(OpsDev o, Work w, const uint8_t* sp, const unsigned long long* excl,
+                                                const uint32_t* order, uint32_t* nextn) {
+  const uint32_t n = o.n;
+  // tour nodes = enter-weights before leave(super root)
+  const uint32_t total = static_cast<uint32_t>(excl[2 * (2 * n + 1) + 1] >> 32);
+  GRID_STRIDE(x, n) {
+    if (o.kind[x] != CRDTM_ADD || w.st[x] != ST_APPLIED) continue;
+    uint32_t j = static_cast<uint32_t>(excl[2 * x] >> 32) + 1;
+    if (sp[x]) {
+      const uint32_t s = n + x;
+      j += static_cast<uint32_t>(excl[2 * s + 1] >> 32) - static_cast<uint32_t>(excl[2 * s] >> 32);
+    }
+    uint32_t y = j < total ? order[j] : NONE;
+    nextn[x] = (y < n && w.addpar[y] == w.addpar[x]) ? y : NONE;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K3 + commit — tombstones, kept/live flags, op log, tree state.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(BLOCK) k_commit_flags(OpsDev o, Work w, uint32_t* appl, uint32_t* plen,
+                                                        uint32_t* kept, uint32_t* live) {
+  const uint32_t n = o.n;
+  GRID_STRIDE(i, n) {
+    const bool a = w.st[i] == ST_APPLIED;
+    appl[i] = a;
+    plen[i] = a ? op_len(o, i) : 0;
+    uint32_t k = 0, l = 0;
+    if (a && o.kind[i] == CRDTM_ADD) {
+      const uint32_t p = w.addpar[i];
+      k = (p == n || !w.dead[p]) ? 1 : 0;
+      l = (k && w.dtime[i] == NONE) ? 1 : 0;
+    }
+    if (kept) kept[i] = k;
+    if (live) live[i] = l;
+  }
+}
+
+struct CommitArgs {
+  uint32_t base_slot;     // first new slot
+  uint32_t n_kept;        // K
+  uint32_t base_dict;     // first new dict
+  uint32_t log_base;
+};
+
+__global__ void __launch_bounds__(BLOCK) k_commit_nodes(OpsDev o, Work w, TreeDev T, CommitArgs a,
+                                                        const uint32_t* kslot, const uint32_t* lslot,
+                                                        const uint32_t* logidx, const uint32_t* nextn,
+                                                        const uint32_t* fc, const unsigned long long* excl,
+                                                        uint32_t* doc) {
+  const uint32_t n = o.n;
+  GRID_STRIDE(x, n) {
+    if (o.kind[x] != CRDTM_ADD || w.st[x] != ST_APPLIED) continue;
+    const uint32_t p = w.addpar[x];
+    if (p != n && w.dead[p]) continue;  // dict discarded (owner or an ancestor tombstoned)
+    const uint32_t slot = a.base_slot + kslot[x];
+    const bool tomb = w.dtime[x] != NONE;
+    T.s_key[slot] = o.ts[x];
+    T.s_dict[slot] = p == n ? 0u : a.base_dict + lslot[p];
+    T.s_next[slot] = nextn[x] != NONE ? a.base_slot + kslot[nextn[x]] : NONE;
+    T.s_src[slot] = a.log_base + logidx[x];
+    T.s_flags[slot] = tomb ? F_TOMB : 0;
+    if (!tomb) {
+      const uint32_t dd = a.base_dict + lslot[x];
+      const uint32_t ss = a.base_slot + a.n_kept + lslot[x];
+      T.s_child[slot] = dd;
+      T.s_key[ss] = 0;
+      T.s_dict[ss] = dd;
+      const uint32_t f = fc[n + x];
+      T.s_next[ss] = f != NONE ? a.base_slot + kslot[f] : NONE;
+      T.s_src[ss] = NONE;
+      T.s_child[ss] = NONE;
+      T.s_flags[ss] = F_TOMB | F_SENT;
+      T.d_sent[dd] = ss;
+      T.d_owner[dd] = slot;
+      doc[static_cast<uint32_t>(excl[2 * x])] = slot;  // document rank (low word) -> slot
+    } else {
+      T.s_child[slot] = NONE;
+    }
+  }
+}
+
+__global__ void k_commit_root(OpsDev o, TreeDev T, const uint32_t* kslot, const uint32_t* fc, uint32_t base_slot) {
+  const uint32_t f = fc[2 * o.n];
+  T.s_next[0] = f != NONE ? base_slot + kslot[f] : NONE;
+}
+
+// Append applied ops to the log (operations, src/CRDTree.elm:311).
+__global__ void __launch_bounds__(BLOCK) k_log(OpsDev o, const uint8_t* st, TreeDev T, uint32_t log_base,
+                                               uint32_t lpath_base, const uint32_t* logidx, const uint32_t* lpoff) {
+  GRID_STRIDE(i, o.n) {
+    if (st[i] != ST_APPLIED) continue;
+    const uint32_t li = log_base + logidx[i];
+    const bool add = o.kind[i] == CRDTM_ADD;
+    T.l_kind[li] = o.kind[i];
+    T.l_ts[li] = add ? o.ts[i] : 0;
+    T.l_val[li] = add ? o.val[i] : 0;
+    const uint32_t b = lpath_base + lpoff[i];
+    T.l_off[li] = b;
+    const uint32_t s = o.off[i], L = o.off[i + 1] - s;
+    for (uint32_t j = 0; j < L; ++j) T.l_path[b + j] = o.path[s + j];
+  }
+}
+
+__global__ void k_log_tail(TreeDev T, uint32_t log_base, const uint32_t* n_app, uint32_t lpath_base,
+                           const uint32_t* n_path) {
+  T.l_off[log_base + *n_app] = lpath_base + *n_path;
+}
+
+// replicas[replicaId t] := t, last writer wins (src/CRDTree.elm:313). For a
+// Delete t is the deleted node's key (Operation.timestamp, src/Internal/Operation.elm:100-101).
+__device__ __forceinline__ long long op_t(const OpsDev& o, uint32_t i) {
+  return o.kind[i] == CRDTM_ADD ? o.ts[i] : o.path[o.off[i + 1] - 1];
+}
+
+__global__ void __launch_bounds__(BLOCK) k_rep_max(OpsDev o, const uint8_t* st, uint32_t* rtab) {
+  GRID_STRIDE(i, o.n) {
+    if (st[i] != ST_APPLIED) continue;
+    const uint32_t r = static_cast<uint32_t>(replica_of(op_t(o, i)) + (1LL << (REPLICA_BITS - 1)));
+    atomicMax(&rtab[r], i + 1);
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_rep_out(OpsDev o, const uint8_t* st, const uint32_t* rtab,
+                                                   long long* out, uint32_t* n_out) {
+  GRID_STRIDE(i, o.n) {
+    if (st[i] != ST_APPLIED) continue;
+    const long long t = op_t(o, i);
+    const uint32_t r = static_cast<uint32_t>(replica_of(t) + (1LL << (REPLICA_BITS - 1)));
+    if (rtab[r] == i + 1) {
+      const uint32_t k = atomicAdd(n_out, 1u);
+      out[2 * k] = replica_of(t);
+      out[2 * k + 1] = t;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_rep_reset(OpsDev o, const uint8_t* st, uint32_t* rtab) {
+  GRID_STRIDE(i, o.n) {
+    if (st[i] != ST_APPLIED) continue;
+    rtab[static_cast<uint32_t>(replica_of(op_t(o, i)) + (1LL << (REPLICA_BITS - 1)))] = 0;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_status_out(const uint8_t* st, uint32_t n, uint32_t err, uint8_t* out) {
+  GRID_STRIDE(i, n) {
+    uint8_t s = st[i];
+    if (i > err) s = CRDTM_ST_UNREACHED;
+    else if (s == ST_INVALID || s == ST_NOTFOUND) s = CRDTM_ST_ERROR;
+    out[i] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Exact replay (one lane per tree): the reference's literal sequential
+// semantics over the slot state, including the findInsertion copy quirk
+// (src/Internal/Node.elm:87-89 with leftTs != key(left)) as a persistent deep
+// copy of the copied node's children. In-place edits of committed slots are
+// undo-logged so that an error leaves the tree unchanged.
+// ---------------------------------------------------------------------------
+struct ReplayArgs {
+  TreeDev T;
+  SlotHash H;
+  uint32_t* dhead;   // per dict: first member slot
+  uint32_t* mnext;   // per slot: next member of the same dict
+  uint32_t* undo;    // triples (slot, field, old)
+  uint32_t undo_cap;
+  uint32_t* queue;   // deep-copy BFS queue of (src dict, dst dict)
+  uint32_t queue_cap;
+  uint32_t committed_slots;
+  uint32_t n_slots, n_dicts;
+  uint32_t cap_slots, cap_dicts;
+  uint32_t hash_limit;
+  uint32_t log_base;
+  long long ts0;
+};
+
+enum : uint32_t { UF_NEXT = 0, UF_SRC = 1, UF_CHILD = 2, UF_FLAGS = 3 };
+
+struct Replayer {
+  ReplayArgs a;
+  uint32_t slots, dicts, inserted, undo_n;
+  bool overflow;
+
+  __device__ void log_undo(uint32_t s, uint32_t field, uint32_t old) {
+    if (s >= a.committed_slots) return;
+    if (undo_n + 1 > a.undo_cap) { overflow = true; return; }
+    a.undo[3 * undo_n] = s;
+    a.undo[3 * undo_n + 1] = field;
+    a.undo[3 * undo_n + 2] = old;
+    ++undo_n;
+  }
+  __device__ void set_next(uint32_t s, uint32_t v) { log_undo(s, UF_NEXT, a.T.s_next[s]); a.T.s_next[s] = v; }
+  __device__ void set_src(uint32_t s, uint32_t v) { log_undo(s, UF_SRC, a.T.s_src[s]); a.T.s_src[s] = v; }
+  __device__ void set_child(uint32_t s, uint32_t v) { log_undo(s, UF_CHILD, a.T.s_child[s]); a.T.s_child[s] = v; }
+  __device__ void set_flags(uint32_t s, uint32_t v) { log_undo(s, UF_FLAGS, a.T.s_flags[s]); a.T.s_flags[s] = static_cast<uint8_t>(v); }
+
+  __device__ void rollback() {
+    while (undo_n > 0) {
+      --undo_n;
+      const uint32_t s = a.undo[3 * undo_n], f = a.undo[3 * undo_n + 1], v = a.undo[3 * undo_n + 2];
+      if (f == UF_NEXT) a.T.s_next[s] = v;
+      else if (f == UF_SRC) a.T.s_src[s] = v;
+      else if (f == UF_CHILD) a.T.s_child[s] = v;
+      else a.T.s_flags[s] = static_cast<uint8_t>(v);
+    }
+  }
+
+  __device__ uint32_t new_slot(uint32_t d, long long key, uint32_t next, uint32_t src, uint32_t child, uint8_t flags) {
+    if (slots >= a.cap_slots || inserted + 1 > a.hash_limit) { overflow = true; return NONE; }
+    const uint32_t s = slots++;
+    a.T.s_key[s] = key;
+    a.T.s_dict[s] = d;
+    a.T.s_next[s] = next;
+    a.T.s_src[s] = src;
+    a.T.s_child[s] = child;
+    a.T.s_flags[s] = flags;
+    slothash_put_seq(a.H, d, key, s);
+    ++inserted;
+    a.mnext[s] = a.dhead[d];
+    a.dhead[d] = s;
+    return s;
+  }
+
+  __device__ uint32_t new_dict(uint32_t owner) {
+    if (dicts >= a.cap_dicts) { overflow = true; return NONE; }
+    const uint32_t d = dicts++;
+    a.dhead[d] = NONE;
+    a.T.d_owner[d] = owner;
+    a.T.d_sent[d] = NONE;
+    return d;
+  }
+
+  // Persistent copy of dict `src` (and every dict below it) into `dst`.
+  __device__ void deep_copy(uint32_t src, uint32_t dst) {
+    uint32_t qh = 0, qt = 0;
+    a.queue[0] = src;
+    a.queue[1] = dst;
+    qt = 1;
+    while (qh < qt && !overflow) {
+      const uint32_t sd = a.queue[2 * qh], dd = a.queue[2 * qh + 1];
+      ++qh;
+      for (uint32_t m = a.dhead[sd]; m != NONE && !overflow; m = a.mnext[m]) {
+        const uint8_t fl = a.T.s_flags[m];
+        const uint32_t nm = new_slot(dd, a.T.s_key[m], NONE, a.T.s_src[m], NONE, fl);
+        if (nm == NONE) break;
+        if (fl & F_SENT) a.T.d_sent[dd] = nm;
+        const uint32_t c = a.T.s_child[m];
+        if (c != NONE) {
+          const uint32_t nc = new_dict(nm);
+          if (nc == NONE) break;
+          a.T.s_child[nm] = nc;
+          if (qt + 1 > a.queue_cap) { overflow = true; break; }
+          a.queue[2 * qt] = c;
+          a.queue[2 * qt + 1] = nc;
+          ++qt;
+        }
+      }
+      // re-link `next` keys inside the copy
+      for (uint32_t m = a.dhead[sd]; m != NONE && !overflow; m = a.mnext[m]) {
+        const uint32_t nx = a.T.s_next[m];
+        if (nx == NONE) continue;
+        const uint32_t nm = slothash_find(a.H, dd, a.T.s_key[m]);
+        a.T.s_next[nm] = slothash_find(a.H, dd, a.T.s_key[nx]);
+      }
+    }
+  }
+
+  // One op; returns ST_* (src/CRDTree.elm:275-295 with src/Internal/Node.elm).
+  __device__ uint8_t op(const OpsDev& o, uint32_t i, uint32_t applied) {
+    const uint32_t b = o.off[i], L = o.off[i + 1] - b;
+    if (L == 0) return ST_INVALID;
+    uint32_t d = 0;
+    for (uint32_t l = 0; l + 1 < L; ++l) {  // update: descend
+      const uint32_t s = slothash_find(a.H, d, o.path[b + l]);
+      if (s == NONE) return ST_INVALID;
+      if (a.T.s_flags[s] & F_TOMB) return ST_ALREADY;
+      d = a.T.s_child[s];
+    }
+    const long long k = o.path[b + L - 1];
+    if (o.kind[i] == CRDTM_DELETE) {  // deleteHelp
+      const uint32_t s = slothash_find(a.H, d, k);
+      if (s == NONE) return ST_NOTFOUND;
+      if (a.T.s_flags[s] & F_TOMB) return ST_ALREADY;
+      set_flags(s, a.T.s_flags[s] | F_TOMB);
+      set_child(s, NONE);  // Tombstone drops the children
+      return ST_APPLIED;
+    }
+    const long long ts = o.ts[i];  // addAfterHelp
+    if (slothash_find(a.H, d, ts) != NONE) return ST_ALREADY;
+    const uint32_t found = slothash_find(a.H, d, k);
+    if (found == NONE) return ST_NOTFOUND;
+    long long nkey = k;  // findInsertion
+    uint32_t node = found;
+    for (;;) {
+      const uint32_t rn = a.T.s_next[node];
+      if (rn == NONE) break;
+      uint32_t live = rn;
+      while (live != NONE && (a.T.s_flags[live] & F_TOMB)) live = a.T.s_next[live];
+      if (live == NONE) break;
+      const long long rk = a.T.s_key[rn];
+      if (ts > rk) break;
+      nkey = rk;
+      node = live;
+    }
+    const uint32_t x = new_slot(d, ts, a.T.s_next[node], a.log_base + applied, NONE, 0);
+    if (x == NONE) return ST_PENDING;
+    const uint32_t dd = new_dict(x);
+    if (dd == NONE) return ST_PENDING;
+    a.T.s_child[x] = dd;
+    const uint32_t ss = new_slot(dd, 0, NONE, NONE, NONE, F_TOMB | F_SENT);
+    if (ss == NONE) return ST_PENDING;
+    a.T.d_sent[dd] = ss;
+    const uint32_t ls = slothash_find(a.H, d, nkey);
+    // x is reachable from the dict's sentinel iff its predecessor is (an Add
+    // anchored at an orphan hangs off the chain)
+    if (a.T.s_flags[ls] & F_ORPHAN) a.T.s_flags[x] |= F_ORPHAN;
+    if (ls == node) {
+      set_next(node, x);
+    } else {
+      // copy quirk: slot nkey := copy of node with next = ts; the entries
+      // between it and node drop off the chain (orphans) when it was on it.
+      if (!(a.T.s_flags[ls] & F_ORPHAN)) {
+        for (uint32_t q = a.T.s_next[ls]; q != NONE; q = a.T.s_next[q]) {
+          set_flags(q, a.T.s_flags[q] | F_ORPHAN);
+          if (q == node) break;
+        }
+      }
+      set_src(ls, a.T.s_src[node]);
+      set_flags(ls, (a.T.s_flags[node] & ~F_ORPHAN) | (a.T.s_flags[ls] & F_ORPHAN));
+      set_next(ls, x);
+      const uint32_t c = a.T.s_child[node];
+      uint32_t nc = NONE;
+      if (c != NONE) {
+        nc = new_dict(ls);
+        if (nc == NONE) return ST_PENDING;
+        deep_copy(c, nc);
+        if (overflow) return ST_PENDING;
+      }
+      set_child(ls, nc);
+    }
+    return overflow ? ST_PENDING : ST_APPLIED;
+  }
+};
+
+__global__ void k_replay(OpsDev o, ReplayArgs args, uint8_t* st, DevResult* dres) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Replayer r;
+  r.a = args;
+  r.slots = args.n_slots;
+  r.dicts = args.n_dicts;
+  r.inserted = args.n_slots;
+  r.undo_n = 0;
+  r.overflow = false;
+  long long ts = args.ts0;
+  uint32_t applied = 0, already = 0, err = NONE, code = 0;
+  for (uint32_t i = 0; i < o.n; ++i) {
+    const uint8_t s = r.op(o, i, applied);
+    if (r.overflow) break;
+    st[i] = s;
+    if (s == ST_INVALID || s == ST_NOTFOUND) {
+      err = i;
+      code = s == ST_INVALID ? CRDTM_INVALID_PATH : CRDTM_OPERATION_FAILED;
+      break;
+    }
+    if (s == ST_APPLIED) ++applied;
+    else ++already;
+    // incrementTimestamp (src/CRDTree.elm:337-343): Ok Adds of the own replica
+    if (o.kind[i] == CRDTM_ADD && replica_of(o.ts[i]) == replica_of(ts)) ++ts;
+  }
+  if (r.overflow || err != NONE) r.rollback();
+  dres->replay_overflow = r.overflow ? 1u : 0u;
+  dres->err_index = err;
+  dres->replay_err_code = code;
+  dres->n_applied = applied;
+  dres->n_already = already;
+  dres->replay_slots = r.slots;
+  dres->replay_dicts = r.dicts;
+  dres->replay_timestamp = ts;
+}
+
+// Build the (dict, key) -> slot hash and the dict member lists of the state.
+__global__ void __launch_bounds__(BLOCK) k_replay_index(TreeDev T, uint32_t n_slots, SlotHash H, uint32_t* dhead,
+                                                        uint32_t* mnext) {
+  GRID_STRIDE(s, n_slots) {
+    const uint32_t d = T.s_dict[s];
+    slothash_put_par(H, d, T.s_key[s], s);
+    mnext[s] = atomicExch(&dhead[d], s);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Generic linearisation of a tree state (document order of any state, e.g.
+// after a replay): entries enter(s) = s, exit(d) = S + d. A dict is alive when
+// every owner up its chain is an on-chain live node.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(BLOCK) k_dict_alive_init(TreeDev T, uint32_t n_dicts, uint8_t* ok, uint32_t* up) {
+  GRID_STRIDE(d, n_dicts) {
+    if (d == 0) { ok[d] = 1; up[d] = 0; continue; }
+    const uint32_t o = T.d_owner[d];
+    const bool good = o != NONE && T.s_child[o] == d && !(T.s_flags[o] & (F_TOMB | F_ORPHAN));
+    ok[d] = good ? 1 : 0;
+    up[d] = good ? T.s_dict[o] : 0;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_dict_alive_jump(uint32_t n_dicts, uint8_t* ok, uint32_t* up,
+                                                           uint8_t* ok2, uint32_t* up2) {
+  GRID_STRIDE(d, n_dicts) {
+    const uint32_t u = up[d];
+    ok2[d] = ok[d] & ok[u];
+    up2[d] = up[u];
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_lin_entries(TreeDev T, uint32_t S, uint32_t D, const uint8_t* alive,
+                                                       uint32_t* succ, unsigned long long* wt) {
+  GRID_STRIDE(e, S + D) {
+    if (e < S) {
+      const uint32_t s = e;
+      const uint8_t f = T.s_flags[s];
+      if (!alive[T.s_dict[s]] || (f & F_ORPHAN)) { succ[e] = ABSENT; wt[e] = 0; continue; }
+      const uint32_t c = T.s_child[s];
+      if (!(f & F_TOMB) && c != NONE) succ[e] = T.d_sent[c];
+      else succ[e] = T.s_next[s] != NONE ? T.s_next[s] : S + T.s_dict[s];
+      wt[e] = (f & F_TOMB) ? 0ULL : 1ULL;
+    } else {
+      const uint32_t d = e - S;
+      if (!alive[d]) { succ[e] = ABSENT; wt[e] = 0; continue; }
+      wt[e] = 0;
+      if (d == 0) { succ[e] = NONE; continue; }
+      const uint32_t o = T.d_owner[d];
+      succ[e] = T.s_next[o] != NONE ? T.s_next[o] : S + T.s_dict[o];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_lin_doc(TreeDev T, uint32_t S, const unsigned long long* excl,
+                                                   uint32_t* doc, uint64_t cap) {
+  GRID_STRIDE(s, S) {
+    const unsigned long long e = excl[s];
+    if (e == ~0ULL) continue;
+    const uint8_t f = T.s_flags[s];
+    if (f & (F_TOMB | F_ORPHAN)) continue;
+    if (e < cap) doc[static_cast<uint32_t>(e)] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host orchestration
+// ---------------------------------------------------------------------------
+void mark(crdtm_ctx* c, const char* name) {
+  if (!c->profile) return;
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return;
+  hipEventRecord(e, c->stream);
+  c->marks.emplace_back(name, e);
+}
+
+template <class T>
+static int grow_array(T*& p, uint64_t old_n, uint64_t new_n) {
+  T* q = nullptr;
+  HIP_CHECK(hipMalloc(&q, new_n * sizeof(T) + 256));
+  if (p) {
+    if (old_n) HIP_CHECK(hipMemcpy(q, p, old_n * sizeof(T), hipMemcpyDeviceToDevice));
+    HIP_CHECK(hipFree(p));
+  }
+  p = q;
+  return CRDTM_OK;
+}
+
+int grow_tree(crdtm_tree* t, const TreeCaps& need) {
+  HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+  TreeCaps& c = t->cap;
+  auto bump = [](uint64_t have, uint64_t want) { return want <= have ? have : (want + want / 4 + 1024); };
+  if (need.slots > c.slots) {
+    uint64_t n = bump(c.slots, need.slots);
+    int r = 0;
+    if ((r = grow_array(t->d.s_key, t->n_slots, n)) || (r = grow_array(t->d.s_next, t->n_slots, n)) ||
+        (r = grow_array(t->d.s_src, t->n_slots, n)) || (r = grow_array(t->d.s_child, t->n_slots, n)) ||
+        (r = grow_array(t->d.s_dict, t->n_slots, n)) || (r = grow_array(t->d.s_flags, t->n_slots, n)))
+      return r;
+    c.slots = n;
+  }
+  if (need.dicts > c.dicts) {
+    uint64_t n = bump(c.dicts, need.dicts);
+    int r = 0;
+    if ((r = grow_array(t->d.d_sent, t->n_dicts, n)) || (r = grow_array(t->d.d_owner, t->n_dicts, n))) return r;
+    c.dicts = n;
+  }
+  if (need.log > c.log) {
+    uint64_t n = bump(c.log, need.log);
+    int r = 0;
+    if ((r = grow_array(t->d.l_kind, t->log_n, n)) || (r = grow_array(t->d.l_ts, t->log_n, n)) ||
+        (r = grow_array(t->d.l_val, t->log_n, n)) || (r = grow_array(t->d.l_off, t->log_n + 1, n + 1)))
+      return r;
+    c.log = n;
+  }
+  if (need.lpath > c.lpath) {
+    uint64_t n = bump(c.lpath, need.lpath);
+    int r = grow_array(t->d.l_path, t->log_npath, n);
+    if (r) return r;
+    c.lpath = n;
+  }
+  if (need.doc > c.doc) {
+    uint64_t n = bump(c.doc, need.doc);
+    int r = grow_array(t->d.doc, 0, n);
+    if (r) return r;
+    c.doc = n;
+  }
+  return CRDTM_OK;
+}
+
+static uint32_t pow2_at_least(uint64_t x) {
+  uint64_t p = 1024;
+  while (p < x) p <<= 1;
+  return static_cast<uint32_t>(p);
+}
+
+static int sync_read(crdtm_ctx* c) {
+  HIP_CHECK(hipMemcpyAsync(c->hres, c->dres, sizeof(DevResult), hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(hipStreamSynchronize(c->stream));
+  return CRDTM_OK;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_post_flags(OpsDev o, const uint8_t* st, uint32_t* appl, uint32_t* plen) {
+  GRID_STRIDE(i, o.n) {
+    const bool a = st[i] == ST_APPLIED;
+    appl[i] = a;
+    plen[i] = a ? o.off[i + 1] - o.off[i] : 0;
+  }
+}
+
+// Append the applied ops to the log and fold replicas; shared by both paths.
+static int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& ws) {
+  crdtm_ctx* c = t->ctx;
+  hipStream_t s = c->stream;
+  const uint32_t n = o.n;
+  uint32_t* appl = ws.alloc<uint32_t>(n + 1);
+  uint32_t* plen = ws.alloc<uint32_t>(n + 1);
+  long long* rep = ws.alloc<long long>(2 * static_cast<uint64_t>(n) + 2);
+  hipLaunchKernelGGL(k_post_flags, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, appl, plen);
+  DevResult* dr = c->dres;
+  int r;
+  if ((r = scan_excl_u32(appl, appl, n, &dr->log_n, ws, s))) return r;
+  if ((r = scan_excl_u32(plen, plen, n, &dr->log_npath, ws, s))) return r;
+  hipLaunchKernelGGL(k_log, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, t->d, static_cast<uint32_t>(t->log_n),
+                     static_cast<uint32_t>(t->log_npath), appl, plen);
+  hipLaunchKernelGGL(k_log_tail, dim3(1), dim3(1), 0, s, t->d, static_cast<uint32_t>(t->log_n), &dr->log_n,
+                     static_cast<uint32_t>(t->log_npath), &dr->log_npath);
+  HIP_CHECK(hipMemsetAsync(&dr->n_replica_out, 0, sizeof(uint32_t), s));
+  hipLaunchKernelGGL(k_rep_max, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab);
+  hipLaunchKernelGGL(k_rep_out, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab, rep, &dr->n_replica_out);
+  hipLaunchKernelGGL(k_rep_reset, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab);
+  mark(c, "log+replicas");
+  if ((r = sync_read(c))) return r;
+  const uint32_t nrep = c->hres->n_replica_out;
+  if (nrep) {
+    std::vector<long long> h(2 * static_cast<size_t>(nrep));
+    HIP_CHECK(hipMemcpy(h.data(), rep, h.size() * sizeof(long long), hipMemcpyDeviceToHost));
+    for (uint32_t k = 0; k < nrep; ++k) t->replicas[h[2 * k]] = h[2 * k + 1];
+  }
+  t->last_begin = t->log_n;
+  t->log_n += c->hres->log_n;
+  t->log_npath += c->hres->log_npath;
+  t->last_end = t->log_n;
+  return CRDTM_OK;
+}
+
+static int run_replay(crdtm_tree* t, const OpsDev& o, uint8_t* st, crdtm_result* res, uint32_t guard) {
+  crdtm_ctx* c = t->ctx;
+  hipStream_t s = c->stream;
+  uint64_t nadd = o.n;  // upper bound on new nodes
+  uint64_t extra = 64;
+  const size_t arena_mark = c->ws.used;
+  for (int attempt = 0; attempt < 8; ++attempt) {
+    TreeCaps need = t->cap;
+    need.slots = std::max<uint64_t>(need.slots, t->n_slots + 2 * nadd + extra);
+    need.dicts = std::max<uint64_t>(need.dicts, t->n_dicts + nadd + extra);
+    need.log = std::max<uint64_t>(need.log, t->log_n + o.n + 1);
+    need.lpath = std::max<uint64_t>(need.lpath, t->log_npath + o.n_path + 1);
+    int r = grow_tree(t, need);
+    if (r) return r;
+    Arena& ws = c->ws;
+    ws.used = arena_mark;
+    const uint64_t slot_cap = t->cap.slots;
+    const uint32_t H = pow2_at_least(2 * slot_cap);
+    SlotHash hh;
+    hh.dict = ws.alloc<uint32_t>(H);
+    hh.key = ws.alloc<long long>(H);
+    hh.slot = ws.alloc<uint32_t>(H);
+    hh.mask = H - 1;
+    uint32_t* dhead = ws.alloc<uint32_t>(t->cap.dicts);
+    uint32_t* mnext = ws.alloc<uint32_t>(slot_cap);
+    const uint32_t undo_cap = static_cast<uint32_t>(4 * static_cast<uint64_t>(o.n) + 4 * extra + 1024);
+    uint32_t* undo = ws.alloc<uint32_t>(3 * static_cast<uint64_t>(undo_cap));
+    const uint32_t qcap = static_cast<uint32_t>(t->cap.dicts);
+    uint32_t* queue = ws.alloc<uint32_t>(2 * static_cast<uint64_t>(qcap) + 2);
+    HIP_CHECK(hipMemsetAsync(hh.slot, 0xFF, H * sizeof(uint32_t), s));
+    HIP_CHECK(hipMemsetAsync(dhead, 0xFF, t->cap.dicts * sizeof(uint32_t), s));
+    hipLaunchKernelGGL(k_replay_index, dim3(grid_for(t->n_slots)), dim3(BLOCK), 0, s, t->d,
+                       static_cast<uint32_t>(t->n_slots), hh, dhead, mnext);
+    ReplayArgs a;
+    a.T = t->d;
+    a.H = hh;
+    a.dhead = dhead;
+    a.mnext = mnext;
+    a.undo = undo;
+    a.undo_cap = undo_cap;
+    a.queue = queue;
+    a.queue_cap = qcap;
+    a.committed_slots = static_cast<uint32_t>(t->n_slots);
+    a.n_slots = static_cast<uint32_t>(t->n_slots);
+    a.n_dicts = static_cast<uint32_t>(t->n_dicts);
+    a.cap_slots = static_cast<uint32_t>(slot_cap);
+    a.cap_dicts = static_cast<uint32_t>(t->cap.dicts);
+    a.hash_limit = H / 2;
+    a.log_base = static_cast<uint32_t>(t->log_n);
+    a.ts0 = t->timestamp;
+    HIP_CHECK(hipMemsetAsync(c->dres, 0, sizeof(DevResult), s));
+    hipLaunchKernelGGL(k_replay, dim3(1), dim3(64), 0, s, o, a, st, c->dres);
+    mark(c, "replay");
+    if ((r = sync_read(c))) return r;
+    const DevResult& h = *c->hres;
+    if (h.replay_overflow) {
+      extra = extra * 4 + t->n_slots;  // deep copies need more room
+      continue;
+    }
+    res->path_taken = CRDTM_PATH_REPLAY;
+    res->guard = guard;
+    if (h.err_index != NONE) {
+      res->code = static_cast<int32_t>(h.replay_err_code);
+      res->err_index = h.err_index;
+      return CRDTM_OK;
+    }
+    res->n_applied = h.n_applied;
+    res->n_already = h.n_already;
+    const long long new_ts = h.replay_timestamp;
+    const uint32_t new_slots = h.replay_slots, new_dicts = h.replay_dicts;
+    if ((r = post_pass(t, o, st, ws))) return r;
+    t->n_slots = new_slots;
+    t->n_dicts = new_dicts;
+    t->timestamp = new_ts;
+    t->doc_valid = false;
+    res->code = CRDTM_OK;
+    return CRDTM_OK;
+  }
+  return CRDTM_E_NOMEM;
+}
+
+int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res) {
+  crdtm_ctx* c = t->ctx;
+  hipStream_t s = c->stream;
+  Arena& ws = c->ws;  // reset by the caller (inputs may live in it)
+  const uint32_t n = o.n;
+  res->err_index = -1;
+  res->code = CRDTM_OK;
+  if (n == 0) {
+    res->path_taken = CRDTM_PATH_CLOSED_FORM;
+    t->last_begin = t->last_end = t->log_n;
+    return CRDTM_OK;
+  }
+  Work w;
+  w.st = ws.alloc<uint8_t>(n);
+  w.cur = ws.alloc<uint32_t>(n);
+  w.nxt = ws.alloc<uint32_t>(n);
+  w.leaf = ws.alloc<uint32_t>(n);
+  w.addpar = ws.alloc<uint32_t>(n);
+  w.dtime = ws.alloc<uint32_t>(n);
+  w.dead = ws.alloc<uint8_t>(n);
+  w.maxadd = ws.alloc<uint32_t>(n + 1);
+  const uint32_t H = pow2_at_least(2 * static_cast<uint64_t>(n));
+  TsHash h;
+  h.keys = ws.alloc<unsigned long long>(H);
+  h.vals = ws.alloc<uint32_t>(H);
+  h.mask = H - 1;
+  DevResult* dr = c->dres;
+  mark(c, "begin");
+  HIP_CHECK(hipMemsetAsync(dr, 0, sizeof(DevResult), s));
+  HIP_CHECK(hipMemsetAsync(&dr->err_index, 0xFF, sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(h.keys, 0, H * sizeof(unsigned long long), s));
+  HIP_CHECK(hipMemsetAsync(h.vals, 0xFF, H * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(w.maxadd, 0, (n + 1) * sizeof(uint32_t), s));
+  hipLaunchKernelGGL(k_pre, dim3(grid_for(n, BLOCK, 4096)), dim3(BLOCK), 0, s, o, w, h, dr);
+  hipLaunchKernelGGL(k_path_range, dim3(grid_for(o.n_path, BLOCK, 2048)), dim3(BLOCK), 0, s, o.path, o.n_path, dr);
+  mark(c, "K1.index");
+  int r;
+  if ((r = sync_read(c))) return r;
+  if (c->hres->bad_range) return CRDTM_E_RANGE;
+  const uint32_t maxlen = c->hres->max_len;
+  const uint32_t g = grid_for(n);
+  for (uint32_t lvl = 1; lvl <= maxlen; ++lvl) {
+    hipLaunchKernelGGL(k_lvl_addpar, dim3(g), dim3(BLOCK), 0, s, o, w, lvl);
+    hipLaunchKernelGGL(k_lvl_collide, dim3(g), dim3(BLOCK), 0, s, o, w, h, lvl, dr);
+    hipLaunchKernelGGL(k_lvl_resolve, dim3(g), dim3(BLOCK), 0, s, o, w, h, lvl);
+    hipLaunchKernelGGL(k_lvl_del, dim3(g), dim3(BLOCK), 0, s, o, w, lvl);
+    hipLaunchKernelGGL(k_lvl_fin, dim3(g), dim3(BLOCK), 0, s, o, w, h, lvl);
+  }
+  hipLaunchKernelGGL(k_stats, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, o, w, t->timestamp, dr);
+  hipLaunchKernelGGL(k_guard_del, dim3(g), dim3(BLOCK), 0, s, o, w, dr);
+  mark(c, "K1.status");
+  if ((r = sync_read(c))) return r;
+  DevResult h1 = *c->hres;
+  uint32_t guard = h1.guard;
+  if (t->n_slots != 1 || t->log_n != 0) guard |= G_NOT_FRESH;
+  const long long id0 = replica_of(t->timestamp);
+  const long long new_ts = t->timestamp + h1.own_ok_adds;
+  if (replica_of(new_ts) != id0) guard |= G_REPLICA_DRIFT;
+  res->guard = guard;
+  if (t->max_depth < maxlen) t->max_depth = maxlen;
+  if (guard) {
+    // exact sequential replay decides statuses (and errors) itself
+    r = run_replay(t, o, w.st, res, guard);
+    if (r == CRDTM_OK && st_out)
+      hipLaunchKernelGGL(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n,
+                         res->err_index >= 0 ? static_cast<uint32_t>(res->err_index) : NONE, st_out);
+    return r;
+  }
+  res->path_taken = CRDTM_PATH_CLOSED_FORM;
+  if (h1.err_index != NONE) {
+    // error class of the first failing op
+    uint8_t est = 0;
+    HIP_CHECK(hipMemcpy(&est, w.st + h1.err_index, 1, hipMemcpyDeviceToHost));
+    res->code = est == ST_INVALID ? CRDTM_INVALID_PATH : CRDTM_OPERATION_FAILED;
+    res->err_index = h1.err_index;
+    if (st_out) hipLaunchKernelGGL(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n, h1.err_index, st_out);
+    return CRDTM_OK;
+  }
+  res->n_applied = h1.n_applied;
+  res->n_already = h1.n_already;
+
+  // ---- K2: effective parents, unified tree, sibling sort ----
+  const uint32_t U = 2 * n + 2;
+  uint32_t* anc = ws.alloc<uint32_t>(n);
+  uint8_t* sp = ws.alloc<uint8_t>(n + 1);
+  uint32_t* cnt = ws.alloc<uint32_t>(U + 1);
+  uint32_t* fill = ws.alloc<uint32_t>(U + 1);
+  long long* skey = ws.alloc<long long>(U);
+  uint32_t* carr = ws.alloc<uint32_t>(U);
+  uint32_t* fc = ws.alloc<uint32_t>(U);
+  uint32_t* ns = ws.alloc<uint32_t>(U);
+  HIP_CHECK(hipMemsetAsync(sp, 0, n + 1, s));
+  HIP_CHECK(hipMemsetAsync(cnt, 0, (U + 1) * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(fill, 0, (U + 1) * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(fc, 0xFF, U * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(ns, 0xFF, U * sizeof(uint32_t), s));
+  hipLaunchKernelGGL(k_ep_init, dim3(g), dim3(BLOCK), 0, s, o, w, anc);
+  hipLaunchKernelGGL(k_ep_jump, dim3(g), dim3(BLOCK), 0, s, o, w, anc, sp);
+  mark(c, "K2.ep");
+  const uint32_t gU = grid_for(U);
+  hipLaunchKernelGGL(k_up_count, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, skey);
+  uint32_t* n_child_total = &dr->n_sentinels;  // scratch word for the scan total
+  if ((r = scan_excl_u32(cnt, cnt, U + 1, n_child_total, ws, s))) return r;
+  hipLaunchKernelGGL(k_scatter, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, fill, carr);
+  if ((r = segmented_sort(cnt, U, carr, U, skey, ws, s, dr))) return r;
+  hipLaunchKernelGGL(k_links, dim3(gU), dim3(BLOCK), 0, s, o, anc, cnt, n_child_total, carr, fc, ns);
+  mark(c, "K2.sort");
+
+  // ---- K4: Euler tour + list ranking ----
+  const uint64_t E = 2ULL * U;
+  uint32_t* succ = ws.alloc<uint32_t>(E);
+  unsigned long long* wt = ws.alloc<unsigned long long>(E);
+  unsigned long long* excl = ws.alloc<unsigned long long>(E);
+  hipLaunchKernelGGL(k_euler, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, fc, ns, succ, wt);
+  if ((r = list_rank(succ, wt, E, 2 * (2 * n + 1), excl, ws, s, dr, 0))) return r;
+  mark(c, "K4.rank");
+  uint32_t* order = ws.alloc<uint32_t>(U);
+  uint32_t* nextn = ws.alloc<uint32_t>(n);
+  hipLaunchKernelGGL(k_order, dim3(gU), dim3(BLOCK), 0, s, o, w, sp, excl, order);
+  hipLaunchKernelGGL(k_next, dim3(g), dim3(BLOCK), 0, s, o, w, sp, excl, order, nextn);
+  mark(c, "K4.next");
+
+  // ---- K3 + commit ----
+  uint32_t* appl = ws.alloc<uint32_t>(n + 1);
+  uint32_t* plen = ws.alloc<uint32_t>(n + 1);
+  uint32_t* kept = ws.alloc<uint32_t>(n + 1);
+  uint32_t* live = ws.alloc<uint32_t>(n + 1);
+  hipLaunchKernelGGL(k_commit_flags, dim3(g), dim3(BLOCK), 0, s, o, w, appl, plen, kept, live);
+  if ((r = scan_excl_u32(kept, kept, n, &dr->n_nodes_kept, ws, s))) return r;
+  if ((r = scan_excl_u32(live, live, n, &dr->n_live_kept, ws, s))) return r;
+  if ((r = scan_excl_u32(appl, appl, n, &dr->log_n, ws, s))) return r;
+  if ((r = scan_excl_u32(plen, plen, n, &dr->log_npath, ws, s))) return r;
+  TreeCaps need = t->cap;
+  need.slots = std::max<uint64_t>(need.slots, 1 + 2ULL * h1.n_adds_applied + 1);
+  need.dicts = std::max<uint64_t>(need.dicts, 1 + h1.n_adds_applied + 1);
+  need.log = std::max<uint64_t>(need.log, t->log_n + h1.n_applied + 1);
+  need.lpath = std::max<uint64_t>(need.lpath, t->log_npath + o.n_path + 1);
+  need.doc = std::max<uint64_t>(need.doc, h1.n_adds_applied + 1);
+  // capacity changes synchronise; they only happen on the first calls
+  if (need.slots > t->cap.slots || need.dicts > t->cap.dicts || need.log > t->cap.log ||
+      need.lpath > t->cap.lpath || need.doc > t->cap.doc) {
+    if ((r = grow_tree(t, need))) return r;
+  }
+  long long* rep = ws.alloc<long long>(2 * static_cast<uint64_t>(n) + 2);
+  if ((r = sync_read(c))) return r;
+  const uint32_t K = c->hres->n_nodes_kept;
+  CommitArgs ca;
+  ca.base_slot = 1;
+  ca.n_kept = K;
+  ca.base_dict = 1;
+  ca.log_base = static_cast<uint32_t>(t->log_n);
+  hipLaunchKernelGGL(k_commit_nodes, dim3(g), dim3(BLOCK), 0, s, o, w, t->d, ca, kept, live, appl, nextn, fc, excl,
+                     t->d.doc);
+  hipLaunchKernelGGL(k_commit_root, dim3(1), dim3(1), 0, s, o, t->d, kept, fc, 1u);
+  hipLaunchKernelGGL(k_log, dim3(g), dim3(BLOCK), 0, s, o, w.st, t->d, static_cast<uint32_t>(t->log_n),
+                     static_cast<uint32_t>(t->log_npath), appl, plen);
+  hipLaunchKernelGGL(k_log_tail, dim3(1), dim3(1), 0, s, t->d, static_cast<uint32_t>(t->log_n), &dr->log_n,
+                     static_cast<uint32_t>(t->log_npath), &dr->log_npath);
+  mark(c, "K3.commit");
+  hipLaunchKernelGGL(k_rep_max, dim3(g), dim3(BLOCK), 0, s, o, w.st, c->rtab);
+  hipLaunchKernelGGL(k_rep_out, dim3(g), dim3(BLOCK), 0, s, o, w.st, c->rtab, rep, &dr->n_replica_out);
+  hipLaunchKernelGGL(k_rep_reset, dim3(g), dim3(BLOCK), 0, s, o, w.st, c->rtab);
+  if (st_out) hipLaunchKernelGGL(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n, NONE, st_out);
+  mark(c, "replicas");
+  if ((r = sync_read(c))) return r;
+  const DevResult& h2 = *c->hres;
+  const uint32_t nrep = h2.n_replica_out;
+  if (nrep) {
+    std::vector<long long> hv(2 * static_cast<size_t>(nrep));
+    HIP_CHECK(hipMemcpy(hv.data(), rep, hv.size() * sizeof(long long), hipMemcpyDeviceToHost));
+    for (uint32_t k = 0; k < nrep; ++k) t->replicas[hv[2 * k]] = hv[2 * k + 1];
+  }
+  t->n_slots = 1 + static_cast<uint64_t>(h2.n_nodes_kept) + h2.n_live_kept;
+  t->n_dicts = 1 + static_cast<uint64_t>(h2.n_live_kept);
+  t->last_begin = t->log_n;
+  t->log_n += h2.log_n;
+  t->log_npath += h2.log_npath;
+  t->last_end = t->log_n;
+  t->timestamp = new_ts;
+  t->doc_n = h2.n_live_kept;  // visible nodes = kept live nodes
+  t->doc_valid = true;
+  return CRDTM_OK;
+}
+
+int linearize(crdtm_tree* t) {
+  if (t->doc_valid) return CRDTM_OK;
+  crdtm_ctx* c = t->ctx;
+  hipStream_t s = c->stream;
+  Arena& ws = c->ws;
+  ws.reset();
+  const uint32_t S = static_cast<uint32_t>(t->n_slots), D = static_cast<uint32_t>(t->n_dicts);
+  uint8_t* ok = ws.alloc<uint8_t>(D);
+  uint8_t* ok2 = ws.alloc<uint8_t>(D);
+  uint32_t* up = ws.alloc<uint32_t>(D);
+  uint32_t* up2 = ws.alloc<uint32_t>(D);
+  hipLaunchKernelGGL(k_dict_alive_init, dim3(grid_for(D)), dim3(BLOCK), 0, s, t->d, D, ok, up);
+  // pointer doubling up the owner chain (depth bounded by the longest path)
+  uint32_t rounds = 1;
+  while ((1u << rounds) < t->max_depth + 2) ++rounds;
+  rounds += 1;
+  for (uint32_t k = 0; k < rounds; ++k) {
+    hipLaunchKernelGGL(k_dict_alive_jump, dim3(grid_for(D)), dim3(BLOCK), 0, s, D, ok, up, ok2, up2);
+    std::swap(ok, ok2);
+    std::swap(up, up2);
+  }
+  const uint64_t E = static_cast<uint64_t>(S) + D;
+  uint32_t* succ = ws.alloc<uint32_t>(E);
+  unsigned long long* wt = ws.alloc<unsigned long long>(E);
+  unsigned long long* excl = ws.alloc<unsigned long long>(E);
+  hipLaunchKernelGGL(k_lin_entries, dim3(grid_for(E)), dim3(BLOCK), 0, s, t->d, S, D, ok, succ, wt);
+  int r = list_rank(succ, wt, E, 0u /* root sentinel slot */, excl, ws, s, c->dres, 0);
+  if (r) return r;
+  TreeCaps need = t->cap;
+  need.doc = std::max<uint64_t>(need.doc, S + 1);
+  if (need.doc > t->cap.doc && (r = grow_tree(t, need))) return r;
+  hipLaunchKernelGGL(k_lin_doc, dim3(grid_for(S)), dim3(BLOCK), 0, s, t->d, S, excl, t->d.doc, t->cap.doc);
+  // number of visible entries = weight sum up to the end: excl at exit(0)
+  unsigned long long tot = 0;
+  HIP_CHECK(hipMemcpyAsync(&tot, excl + S, sizeof(tot), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  t->doc_n = (tot == ~0ULL || tot > S) ? 0 : tot;
+  t->doc_valid = true;
+  return CRDTM_OK;
+}
+
+}  // namespace crdtm

@@ -242,9 +242,10 @@ int batch(const std::vector<Op>& ops, Tree& t) {
     t.last.clear();
     int r = apply(o, t);
     if (r != T_OK) return r;
-    // merge one.lastOperation two.lastOperation
-    std::vector<Op> merged = toList(prev);
-    for (auto& x : t.last) merged.push_back(x);
+    // merge one.lastOperation two.lastOperation = Batch (toList one ++ toList two);
+    // appended in place (the reference copies the accumulator: O(n^2), §6)
+    std::vector<Op> merged = std::move(prev);
+    for (auto& x : toList(t.last)) merged.push_back(std::move(x));
     t.last = std::move(merged);
     t.last_is_batch = true;
   }

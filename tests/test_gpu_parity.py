@@ -1,0 +1,116 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle.
+
+Bit-exact on every output the reference defines: dict structure (every entry,
+incl. tombstones, sentinels and copy-quirk orphans), visible document order,
+operation log, lastOperation, timestamp and replicas; plus the device
+document-order linearisation against the oracle's pre-order.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from crdtm import _native as N  # noqa: E402
+from crdtm.operation import flatten  # noqa: E402
+from crdtm.tree import CRDTree, pack  # noqa: E402
+from kat_cases import SCENARIOS  # noqa: E402
+from parity_util import (engine_log, engine_summary, oracle_apply_arrays, oracle_log, oracle_summary,  # noqa: E402
+                         oracle_visible_vals)
+
+
+def run_both(replica, calls):
+    """Apply each top-level op to a fresh oracle tree and a fresh engine tree."""
+    from oracle.oracle import lib as olib
+    ot = olib().orc_init(replica)
+    et = CRDTree.init(replica)
+    results = []
+    for op in calls:
+        leaves = flatten(op) if op.kind == "batch" else [op]
+        arrs = pack(leaves)
+        n = len(leaves)
+        _, rc, oerr = oracle_apply_arrays(arrs, n, is_batch=op.kind == "batch", tree=ot)
+        res = et.apply_arrays(arrs, n, is_batch=op.kind == "batch")
+        results.append((rc, oerr, res.code, res.err_index, res.path_taken))
+    return ot, et, results
+
+
+@pytest.mark.parametrize("name", sorted(SCENARIOS))
+def test_scenarios(name):
+    replica, calls = SCENARIOS[name]
+    ot, et, results = run_both(replica, calls)
+    for rc, oerr, code, eerr, _ in results:
+        assert code == rc, (name, results)
+        if rc != 0:
+            assert eerr == oerr
+    assert engine_summary(et) == oracle_summary(ot)
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    assert engine_log(et, 1) == oracle_log(ot, 1)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+
+
+def synth_case(**kw):
+    s = N.synth(**kw)
+    return s, len(s["kind"])
+
+
+CASES = {
+    # config 1 (2 replicas, 70/30 interleaved, depth <= 3): quirks fire -> exact replay
+    "cfg1": dict(n_ops=10000, replicas=2, window=8, p_delete=0.3, p_branch=0.05, max_depth=3, seed=0xC0FFEE01),
+    # config 2 shape at reduced size (16 replicas, 80/20, branches, depth <= 4)
+    "cfg2_small": dict(n_ops=20000, replicas=16, window=64, p_delete=0.2, p_branch=0.1, max_depth=4,
+                       seed=0xC0FFEE02),
+    # config 3 shape (flat, adds only, 64 replicas): closed form
+    "cfg3_small": dict(n_ops=50000, replicas=64, window=256, seed=0xC0FFEE03),
+    # config 4 shape (depth 12, <= 8 children, deletes after adds): closed form with tombstones
+    "cfg4_small": dict(n_ops=60000, replicas=16, p_delete=1 / 3, max_depth=12, max_children=8, deletes_last=1,
+                       seed=0xC0FFEE04),
+    # flat with deletes after adds
+    "flat_deletes_last": dict(n_ops=30000, replicas=8, window=32, p_delete=0.4, deletes_last=1, seed=7),
+    # nested, adds only
+    "nested_adds": dict(n_ops=30000, replicas=8, window=16, p_branch=0.2, max_depth=6, seed=11),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_synthetic_streams(name):
+    s, n = synth_case(**CASES[name])
+    ot, rc, oerr = oracle_apply_arrays(s, n)
+    et = CRDTree.init(0)
+    res = et.apply_arrays(s, n)
+    assert res.code == rc
+    if rc == 0:
+        assert engine_summary(et) == oracle_summary(ot)
+        assert engine_log(et, 0) == oracle_log(ot, 0)
+        assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+    if name in ("cfg3_small", "cfg4_small", "flat_deletes_last", "nested_adds"):
+        assert res.path_taken == N.PATH_CLOSED_FORM, f"expected the closed form, guard={res.guard}"
+
+
+def test_incremental_batches():
+    """Successive applies of chunks equal one apply of the whole stream's chunks on the oracle."""
+    s, n = synth_case(n_ops=20000, replicas=8, window=16, p_delete=0.2, p_branch=0.1, max_depth=3, seed=5)
+    from oracle.oracle import lib as olib
+    ot = olib().orc_init(0)
+    et = CRDTree.init(0)
+    off = s["path_off"]
+    for a in range(0, n, 5000):
+        b = min(n, a + 5000)
+        chunk = dict(kind=s["kind"][a:b].copy(), ts=s["ts"][a:b].copy(), val=s["val"][a:b].copy(),
+                     path_off=(off[a:b + 1] - off[a]).astype(np.uint32), path=s["path"][off[a]:off[b]].copy())
+        _, rc, _ = oracle_apply_arrays(chunk, b - a, tree=ot)
+        res = et.apply_arrays(chunk, b - a)
+        assert res.code == rc == 0
+        assert engine_summary(et) == oracle_summary(ot)
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    assert engine_log(et, 1) == oracle_log(ot, 1)
+
+
+def test_error_leaves_tree_unchanged():
+    et = CRDTree.init(0)
+    from crdtm.operation import Add, Batch
+    r = et.apply_in_place(Batch([Add(1, [0], "a"), Add(2, [1], "b")]))
+    assert r.ok
+    before = engine_summary(et)
+    r = et.apply_in_place(Batch([Add(3, [2], "c"), Add(4, [99], "d")]))
+    assert not r.ok and type(r.error).__name__ == "OperationFailed"
+    assert engine_summary(et) == before
