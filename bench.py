@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Benchmark: merged ops/sec of CRDTree batch merges on MI355X.
+
+Metric (BASELINE.json): merged ops/sec (whole node) on a 10M-op batch, % of
+HBM peak, 1/2/4/8 GPU. One step = one `apply (Batch ops)` of the whole
+synthetic batch onto a fresh tree (crdtm_tree_reset + crdtm_apply through the
+C ABI), inputs already resident in HBM.
+
+Default workload = SURVEY.md config 3: one flat RGA text document, 10M char
+inserts from 64 replicas (window 256, seed 0xC0FFEE03). With N ranks (one
+process per GPU, torchrun), every rank merges its own independent document
+(seed + rank): documents shard by id with no data-path collective, so the
+scaling is weak; the only collectives are the timing barrier and max.
+
+    python bench.py --gpus N --steps K --warmup W [--workload flat10m|deep10m]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "crdt-graph_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
+
+WORKLOADS = {
+    # SURVEY.md §8d config 3
+    "flat10m": dict(n_ops=10_000_000, replicas=64, window=256, seed=0xC0FFEE03),
+    # depth <= 12, <= 8 children, 6.67M adds then deletes of half the nodes
+    "deep10m": dict(n_ops=10_000_000, replicas=16, p_delete=1 / 3, max_depth=12, max_children=8, deletes_last=1,
+                    seed=0xC0FFEE04),
+}
+CPU_SAMPLE = {"flat10m": 150_000, "deep10m": 2_000_000}
+
+
+def alg_bytes(s):
+    """Add = 49 + 8L bytes, Delete = 9 + 8L bytes (read op once, write result once)."""
+    L = np.diff(s["path_off"].astype(np.int64))
+    add = s["kind"] == 0
+    return int(np.sum(np.where(add, 49 + 8 * L, 9 + 8 * L)))
+
+
+def head(s, m):
+    off = s["path_off"]
+    return dict(kind=s["kind"][:m].copy(), ts=s["ts"][:m].copy(), val=s["val"][:m].copy(),
+                path_off=off[:m + 1].copy(), path=s["path"][:off[m]].copy())
+
+
+def cpu_baseline(s, m):
+    """Oracle restatement (oracle/, test infrastructure) on the first m ops, one core."""
+    from oracle.oracle import lib as olib, _ptr
+    sub = head(s, m)
+    L = olib()
+    t = L.orc_init(0)
+    err = C.c_int64(-1)
+    t0 = time.perf_counter()
+    rc = L.orc_apply(t, 1, 0, m, _ptr(sub["kind"]), _ptr(sub["ts"]), _ptr(sub["path_off"]), _ptr(sub["path"]),
+                     _ptr(sub["val"]), C.byref(err))
+    dt = time.perf_counter() - t0
+    L.orc_free(t)
+    assert rc == 0
+    return m / dt, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="flat10m", choices=sorted(WORKLOADS))
+    ap.add_argument("--n-ops", type=int, default=0, help="override the batch size (parity/debug only)")
+    ap.add_argument("--cpu-sample", type=int, default=-1, help="oracle sample ops (0 = skip)")
+    ap.add_argument("--profile-steps", type=int, default=3)
+    ap.add_argument("--verbose", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from crdtm import _native as N
+    from crdtm.tree import _ptr
+    L = N.lib()
+
+    spec = dict(WORKLOADS[args.workload])
+    if args.n_ops:
+        spec["n_ops"] = args.n_ops
+    spec["seed"] = spec["seed"] + rank  # an independent document per rank
+    s = N.synth(**spec)
+    n = len(s["kind"])
+    B_alg = alg_bytes(s)
+
+    dev = torch.device("cuda", local_rank)
+    tens = {k: torch.from_numpy(s[k]).to(dev) for k in ("kind", "ts", "path_off", "path", "val")}
+    ops = N.Ops(n, int(s["path_off"][n]), tens["kind"].data_ptr(), tens["ts"].data_ptr(),
+                tens["path_off"].data_ptr(), tens["path"].data_ptr(), tens["val"].data_ptr(), None)
+    stream = torch.cuda.current_stream()
+    ctx = C.c_void_p()
+    N.check(L.crdtm_ctx_create(local_rank, C.c_void_p(stream.cuda_stream), C.byref(ctx)), "ctx")
+    tree = C.c_void_p()
+    N.check(L.crdtm_tree_create(ctx, 0, C.byref(tree)), "tree")
+    res = N.Result()
+
+    def step():
+        N.check(L.crdtm_tree_reset(tree, 0), "reset")
+        N.check(L.crdtm_apply(tree, C.byref(ops), 1, 1, None, C.byref(res)), "apply")
+        if res.code != 0:
+            raise RuntimeError(f"merge failed: code {res.code} at op {res.err_index}")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    path_taken = res.path_taken
+
+    # Per-kernel device time (HIP events recorded on the launch stream) over a
+    # few extra, untimed steps.
+    L.crdtm_ctx_profile(ctx, 1)
+    acc = {}
+    for _ in range(max(1, args.profile_steps)):
+        step()
+        names = C.create_string_buffer(1 << 16)
+        ms = (C.c_double * 512)()
+        k = L.crdtm_ctx_phase_times(ctx, names, len(names), ms, 512)
+        labels = names.raw.split(b"\0")
+        for j in range(min(k, 512)):
+            nm = labels[j].decode()
+            acc.setdefault(nm, []).append(ms[j])
+    L.crdtm_ctx_profile(ctx, 0)
+    # a kernel launched several times per step is summed within the step
+    per_step = {}
+    for nm, v in acc.items():
+        per_step[nm] = sum(v) / max(1, args.profile_steps)
+    dominant = max(per_step, key=per_step.get)
+    # average duration of one launch of the dominant kernel
+    launches = len(acc[dominant]) / max(1, args.profile_steps)
+    t_dom = per_step[dominant] / launches / 1e3
+
+    ms_step = elapsed / args.steps * 1e3
+    value = world * n * args.steps / elapsed
+    achieved = B_alg / t_dom / 1e9
+    line = {
+        "metric": "merged ops/sec (whole node) on 10M-op batch",
+        "value": value,
+        "unit": "ops/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (deterministic generator, SURVEY.md §8d)",
+        "config": {"workload": f"{args.workload}: {n} ops per GPU, one document per GPU",
+                   "replicas": spec.get("replicas"), "window": spec.get("window", 0),
+                   "path": {1: "closed-form", 2: "replay"}.get(path_taken, "?"),
+                   "parallelism": f"documents sharded by id over {world} GPU(s)"},
+        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "alg_bytes_per_launch": B_alg, "kernel_ms": t_dom * 1e3,
+                     "merge_frac": B_alg / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS},
+    }
+    if args.verbose and rank == 0:
+        for nm, v in sorted(per_step.items(), key=lambda kv: -kv[1]):
+            print(f"  {nm:28s} {v:9.3f} ms/step ({len(acc[nm]) // max(1, args.profile_steps)} launches)",
+                  file=sys.stderr)
+    if rank == 0 and world == 1:
+        m = args.cpu_sample if args.cpu_sample >= 0 else CPU_SAMPLE[args.workload]
+        if m > 0:
+            m = min(m, n)
+            ops_s, dt = cpu_baseline(s, m)
+            line["cpu_baseline"] = {"value": ops_s, "unit": "ops/s", "cores": 1, "kind": "port",
+                                    "sample": f"first {m} ops of the same batch, oracle/ C++ restatement, "
+                                              f"{dt:.1f} s (cost grows with the batch: skip walks)"}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    L.crdtm_tree_destroy(tree)
+    L.crdtm_ctx_destroy(ctx)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -48,6 +48,7 @@ SIGNATURES = [
     ("crdtm_ctx_sync", C.c_int, [P]),
     ("crdtm_tree_create", C.c_int, [P, C.c_int64, C.POINTER(P)]),
     ("crdtm_tree_destroy", C.c_int, [P]),
+    ("crdtm_tree_reset", C.c_int, [P, C.c_int64]),
     ("crdtm_tree_clone", C.c_int, [P, C.POINTER(P)]),
     ("crdtm_apply", C.c_int, [P, C.POINTER(Ops), C.c_int, C.c_int, P, C.POINTER(Result)]),
     ("crdtm_tree_timestamp", C.c_int, [P, C.POINTER(C.c_int64)]),

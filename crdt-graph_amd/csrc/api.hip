@@ -221,6 +221,27 @@ int crdtm_tree_create(crdtm_ctx* c, int64_t replica_id, crdtm_tree** out) {
   return CRDTM_OK;
 }
 
+int crdtm_tree_reset(crdtm_tree* t, int64_t replica_id) {
+  if (!t) return CRDTM_E_ARG;
+  // slot 0 / dict 0 / l_off[0] keep their init values: only the root
+  // sentinel's `next` can change, and only to a slot we now drop.
+  const uint32_t none = NONE;
+  HIP_CHECK(hipMemcpyAsync(t->d.s_next, &none, 4, hipMemcpyHostToDevice, t->ctx->stream));
+  HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+  t->n_slots = 1;
+  t->n_dicts = 1;
+  t->log_n = 0;
+  t->log_npath = 0;
+  t->doc_n = 0;
+  t->doc_valid = true;
+  t->max_depth = 0;
+  t->timestamp = replica_id * TWO32;
+  t->replicas.clear();
+  t->last_begin = t->last_end = 0;
+  t->last_is_batch = 1;
+  return CRDTM_OK;
+}
+
 int crdtm_tree_destroy(crdtm_tree* t) {
   if (!t) return CRDTM_OK;
   hipStreamSynchronize(t->ctx->stream);
@@ -321,7 +342,10 @@ int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_b
         o.val = val;
         if (status_out) st_dev = c->ws.alloc<uint8_t>(n + 1);
       }
+      g_prof = c->profile ? c : nullptr;
+      mark(c, "start");
       r = apply_batch(t, o, st_dev, res);
+      g_prof = nullptr;
       if (r == CRDTM_OK && status_out && !ops_on_device && n) {
         HIP_CHECK(hipMemcpyAsync(status_out, st_dev, n, hipMemcpyDeviceToHost, c->stream));
         HIP_CHECK(hipStreamSynchronize(c->stream));

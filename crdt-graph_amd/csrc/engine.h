@@ -117,5 +117,16 @@ int grow_tree(crdtm_tree* t, const TreeCaps& need);
 int apply_batch(crdtm_tree* t, const OpsDev& ops, uint8_t* status_dev, crdtm_result* res);
 int linearize(crdtm_tree* t);  // fills t->d.doc / t->doc_n from the tree state
 void mark(crdtm_ctx* c, const char* name);
+// Profiling hook: when the current context profiles, every launch records a
+// HIP event on the launch stream so each kernel's device time is measurable.
+extern thread_local crdtm_ctx* g_prof;
+inline void prof_mark(const char* name) {
+  if (g_prof) mark(g_prof, name);
+}
+#define LAUNCH(k, grid, block, shm, st, ...)                    \
+  do {                                                          \
+    hipLaunchKernelGGL(k, grid, block, shm, st, __VA_ARGS__);   \
+    ::crdtm::prof_mark(#k);                                     \
+  } while (0)
 
 }  // namespace crdtm

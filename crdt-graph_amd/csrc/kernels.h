@@ -97,6 +97,20 @@ __device__ __forceinline__ void slothash_put_par(const SlotHash& h, uint32_t d, 
   }
 }
 
+// Wave-aggregated counter increment: one atomic per wave; every lane of the
+// wave must call it (pred selects the lanes that take a ticket).
+__device__ __forceinline__ uint32_t wave_ticket(uint32_t* ctr, bool pred) {
+  const unsigned long long m = __ballot(pred);
+  const int lane = threadIdx.x & 63;
+  uint32_t base = 0;
+  if (m) {
+    const int leader = __ffsll(static_cast<long long>(m)) - 1;
+    if (lane == leader) base = atomicAdd(ctr, static_cast<uint32_t>(__popcll(m)));
+    base = __shfl(base, leader, 64);
+  }
+  return base + static_cast<uint32_t>(__popcll(m & ((1ULL << lane) - 1ULL)));
+}
+
 // wave64 inclusive scan of u32 (CDNA: 64 lanes, __shfl_up over width 64)
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const int lane = threadIdx.x & 63;

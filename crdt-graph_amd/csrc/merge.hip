@@ -208,9 +208,12 @@ __global__ void __launch_bounds__(BLOCK) k_lvl_fin(OpsDev o, Work w, TsHash h, u
 }
 
 // Batch accounting + the guard (DESIGN.md "Guard"): tombstones present in a
-// dict while later Adds land in it can change findInsertion's walk.
+// dict while later Adds land in it can change findInsertion's walk. The
+// common cases (no Deletes; Deletes after every Add) are decided from the
+// batch-wide last applied Add and first applied Delete; only a batch that
+// interleaves them pays the per-dict check (k_guard_dicts).
 __global__ void __launch_bounds__(BLOCK) k_stats(OpsDev o, Work w, long long ts0, DevResult* dres) {
-  uint32_t app = 0, alr = 0, err = NONE, own = 0, addapp = 0;
+  uint32_t app = 0, alr = 0, err = NONE, own = 0, addapp = 0, last_add = 0, first_del = NONE;
   const long long id0 = replica_of(ts0);
   const uint32_t n = o.n;
   const uint32_t stride = gridDim.x * blockDim.x;
@@ -226,8 +229,10 @@ __global__ void __launch_bounds__(BLOCK) k_stats(OpsDev o, Work w, long long ts0
       if ((s == ST_APPLIED || s == ST_ALREADY) && replica_of(o.ts[i]) == id0) ++own;
       if (s == ST_APPLIED) {
         ++addapp;
-        atomicMax(&w.maxadd[w.addpar[i]], i + 1);
+        last_add = max(last_add, i + 1);
       }
+    } else if (s == ST_APPLIED) {
+      first_del = min(first_del, i);
     }
   }
   app = block_sum(app);
@@ -235,12 +240,23 @@ __global__ void __launch_bounds__(BLOCK) k_stats(OpsDev o, Work w, long long ts0
   own = block_sum(own);
   addapp = block_sum(addapp);
   err = block_min(err);
+  last_add = block_max(last_add);
+  first_del = block_min(first_del);
   if (threadIdx.x == 0) {
     atomicAdd(&dres->n_applied, app);
     atomicAdd(&dres->n_already, alr);
     atomicAdd(&dres->own_ok_adds, own);
     atomicAdd(&dres->n_adds_applied, addapp);
     if (err != NONE) atomicMin(&dres->err_index, err);
+    if (last_add) atomicMax(&dres->last_add, last_add);
+    if (first_del != NONE) atomicMin(&dres->first_del, first_del);
+  }
+}
+
+// Per-dict guard, only when the batch interleaves Deletes before later Adds.
+__global__ void __launch_bounds__(BLOCK) k_guard_maxadd(OpsDev o, Work w) {
+  GRID_STRIDE(i, o.n) {
+    if (o.kind[i] == CRDTM_ADD && w.st[i] == ST_APPLIED) atomicMax(&w.maxadd[w.addpar[i]], i + 1);
   }
 }
 
@@ -492,12 +508,37 @@ __device__ __forceinline__ long long op_t(const OpsDev& o, uint32_t i) {
   return o.kind[i] == CRDTM_ADD ? o.ts[i] : o.path[o.off[i + 1] - 1];
 }
 
+// Each block folds a contiguous chunk of ops into an LDS table (replica ->
+// last applied op), then publishes one atomicMax per distinct replica.
+constexpr uint32_t REP_LDS = 512;
 __global__ void __launch_bounds__(BLOCK) k_rep_max(OpsDev o, const uint8_t* st, uint32_t* rtab) {
-  GRID_STRIDE(i, o.n) {
+  __shared__ uint32_t rk[REP_LDS];
+  __shared__ uint32_t rv[REP_LDS];
+  for (uint32_t j = threadIdx.x; j < REP_LDS; j += blockDim.x) {
+    rk[j] = NONE;
+    rv[j] = 0;
+  }
+  __syncthreads();
+  const uint32_t n = o.n;
+  const uint32_t chunk = (n + gridDim.x - 1) / gridDim.x;
+  const uint32_t b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
+  for (uint32_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
     if (st[i] != ST_APPLIED) continue;
     const uint32_t r = static_cast<uint32_t>(replica_of(op_t(o, i)) + (1LL << (REPLICA_BITS - 1)));
-    atomicMax(&rtab[r], i + 1);
+    uint32_t p = (r * 0x9E3779B1u) >> 23;  // 9 bits
+    bool done = false;
+    for (uint32_t probe = 0; probe < 16 && !done; ++probe, p = (p + 1) & (REP_LDS - 1)) {
+      const uint32_t prev = atomicCAS(&rk[p], NONE, r);
+      if (prev == NONE || prev == r) {
+        atomicMax(&rv[p], i + 1);
+        done = true;
+      }
+    }
+    if (!done) atomicMax(&rtab[r], i + 1);  // LDS table crowded: publish directly
   }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < REP_LDS; j += blockDim.x)
+    if (rk[j] != NONE) atomicMax(&rtab[rk[j]], rv[j]);
 }
 
 __global__ void __launch_bounds__(BLOCK) k_rep_out(OpsDev o, const uint8_t* st, const uint32_t* rtab,
@@ -828,6 +869,8 @@ __global__ void __launch_bounds__(BLOCK) k_lin_doc(TreeDev T, uint32_t S, const 
 // ---------------------------------------------------------------------------
 // Host orchestration
 // ---------------------------------------------------------------------------
+thread_local crdtm_ctx* g_prof = nullptr;
+
 void mark(crdtm_ctx* c, const char* name) {
   if (!c->profile) return;
   hipEvent_t e;
@@ -918,19 +961,19 @@ static int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& w
   uint32_t* appl = ws.alloc<uint32_t>(n + 1);
   uint32_t* plen = ws.alloc<uint32_t>(n + 1);
   long long* rep = ws.alloc<long long>(2 * static_cast<uint64_t>(n) + 2);
-  hipLaunchKernelGGL(k_post_flags, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, appl, plen);
+  LAUNCH(k_post_flags, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, appl, plen);
   DevResult* dr = c->dres;
   int r;
   if ((r = scan_excl_u32(appl, appl, n, &dr->log_n, ws, s))) return r;
   if ((r = scan_excl_u32(plen, plen, n, &dr->log_npath, ws, s))) return r;
-  hipLaunchKernelGGL(k_log, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, t->d, static_cast<uint32_t>(t->log_n),
+  LAUNCH(k_log, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, t->d, static_cast<uint32_t>(t->log_n),
                      static_cast<uint32_t>(t->log_npath), appl, plen);
-  hipLaunchKernelGGL(k_log_tail, dim3(1), dim3(1), 0, s, t->d, static_cast<uint32_t>(t->log_n), &dr->log_n,
+  LAUNCH(k_log_tail, dim3(1), dim3(1), 0, s, t->d, static_cast<uint32_t>(t->log_n), &dr->log_n,
                      static_cast<uint32_t>(t->log_npath), &dr->log_npath);
   HIP_CHECK(hipMemsetAsync(&dr->n_replica_out, 0, sizeof(uint32_t), s));
-  hipLaunchKernelGGL(k_rep_max, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab);
-  hipLaunchKernelGGL(k_rep_out, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab, rep, &dr->n_replica_out);
-  hipLaunchKernelGGL(k_rep_reset, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab);
+  LAUNCH(k_rep_max, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, s, o, st, c->rtab);
+  LAUNCH(k_rep_out, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab, rep, &dr->n_replica_out);
+  LAUNCH(k_rep_reset, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab);
   mark(c, "log+replicas");
   if ((r = sync_read(c))) return r;
   const uint32_t nrep = c->hres->n_replica_out;
@@ -977,7 +1020,7 @@ static int run_replay(crdtm_tree* t, const OpsDev& o, uint8_t* st, crdtm_result*
     uint32_t* queue = ws.alloc<uint32_t>(2 * static_cast<uint64_t>(qcap) + 2);
     HIP_CHECK(hipMemsetAsync(hh.slot, 0xFF, H * sizeof(uint32_t), s));
     HIP_CHECK(hipMemsetAsync(dhead, 0xFF, t->cap.dicts * sizeof(uint32_t), s));
-    hipLaunchKernelGGL(k_replay_index, dim3(grid_for(t->n_slots)), dim3(BLOCK), 0, s, t->d,
+    LAUNCH(k_replay_index, dim3(grid_for(t->n_slots)), dim3(BLOCK), 0, s, t->d,
                        static_cast<uint32_t>(t->n_slots), hh, dhead, mnext);
     ReplayArgs a;
     a.T = t->d;
@@ -997,7 +1040,7 @@ static int run_replay(crdtm_tree* t, const OpsDev& o, uint8_t* st, crdtm_result*
     a.log_base = static_cast<uint32_t>(t->log_n);
     a.ts0 = t->timestamp;
     HIP_CHECK(hipMemsetAsync(c->dres, 0, sizeof(DevResult), s));
-    hipLaunchKernelGGL(k_replay, dim3(1), dim3(64), 0, s, o, a, st, c->dres);
+    LAUNCH(k_replay, dim3(1), dim3(64), 0, s, o, a, st, c->dres);
     mark(c, "replay");
     if ((r = sync_read(c))) return r;
     const DevResult& h = *c->hres;
@@ -1054,31 +1097,33 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   h.vals = ws.alloc<uint32_t>(H);
   h.mask = H - 1;
   DevResult* dr = c->dres;
-  mark(c, "begin");
   HIP_CHECK(hipMemsetAsync(dr, 0, sizeof(DevResult), s));
   HIP_CHECK(hipMemsetAsync(&dr->err_index, 0xFF, sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(h.keys, 0, H * sizeof(unsigned long long), s));
   HIP_CHECK(hipMemsetAsync(h.vals, 0xFF, H * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(w.maxadd, 0, (n + 1) * sizeof(uint32_t), s));
-  hipLaunchKernelGGL(k_pre, dim3(grid_for(n, BLOCK, 4096)), dim3(BLOCK), 0, s, o, w, h, dr);
-  hipLaunchKernelGGL(k_path_range, dim3(grid_for(o.n_path, BLOCK, 2048)), dim3(BLOCK), 0, s, o.path, o.n_path, dr);
-  mark(c, "K1.index");
+  LAUNCH(k_pre, dim3(grid_for(n, BLOCK, 4096)), dim3(BLOCK), 0, s, o, w, h, dr);
+  LAUNCH(k_path_range, dim3(grid_for(o.n_path, BLOCK, 2048)), dim3(BLOCK), 0, s, o.path, o.n_path, dr);
   int r;
   if ((r = sync_read(c))) return r;
   if (c->hres->bad_range) return CRDTM_E_RANGE;
   const uint32_t maxlen = c->hres->max_len;
   const uint32_t g = grid_for(n);
   for (uint32_t lvl = 1; lvl <= maxlen; ++lvl) {
-    hipLaunchKernelGGL(k_lvl_addpar, dim3(g), dim3(BLOCK), 0, s, o, w, lvl);
-    hipLaunchKernelGGL(k_lvl_collide, dim3(g), dim3(BLOCK), 0, s, o, w, h, lvl, dr);
-    hipLaunchKernelGGL(k_lvl_resolve, dim3(g), dim3(BLOCK), 0, s, o, w, h, lvl);
-    hipLaunchKernelGGL(k_lvl_del, dim3(g), dim3(BLOCK), 0, s, o, w, lvl);
-    hipLaunchKernelGGL(k_lvl_fin, dim3(g), dim3(BLOCK), 0, s, o, w, h, lvl);
+    LAUNCH(k_lvl_addpar, dim3(g), dim3(BLOCK), 0, s, o, w, lvl);
+    LAUNCH(k_lvl_collide, dim3(g), dim3(BLOCK), 0, s, o, w, h, lvl, dr);
+    LAUNCH(k_lvl_resolve, dim3(g), dim3(BLOCK), 0, s, o, w, h, lvl);
+    LAUNCH(k_lvl_del, dim3(g), dim3(BLOCK), 0, s, o, w, lvl);
+    LAUNCH(k_lvl_fin, dim3(g), dim3(BLOCK), 0, s, o, w, h, lvl);
   }
-  hipLaunchKernelGGL(k_stats, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, o, w, t->timestamp, dr);
-  hipLaunchKernelGGL(k_guard_del, dim3(g), dim3(BLOCK), 0, s, o, w, dr);
-  mark(c, "K1.status");
+  HIP_CHECK(hipMemsetAsync(&dr->first_del, 0xFF, sizeof(uint32_t), s));
+  LAUNCH(k_stats, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, o, w, t->timestamp, dr);
   if ((r = sync_read(c))) return r;
+  if (c->hres->first_del != NONE && c->hres->last_add > c->hres->first_del + 1) {
+    LAUNCH(k_guard_maxadd, dim3(g), dim3(BLOCK), 0, s, o, w);
+    LAUNCH(k_guard_del, dim3(g), dim3(BLOCK), 0, s, o, w, dr);
+    if ((r = sync_read(c))) return r;
+  }
   DevResult h1 = *c->hres;
   uint32_t guard = h1.guard;
   if (t->n_slots != 1 || t->log_n != 0) guard |= G_NOT_FRESH;
@@ -1091,7 +1136,7 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
     // exact sequential replay decides statuses (and errors) itself
     r = run_replay(t, o, w.st, res, guard);
     if (r == CRDTM_OK && st_out)
-      hipLaunchKernelGGL(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n,
+      LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n,
                          res->err_index >= 0 ? static_cast<uint32_t>(res->err_index) : NONE, st_out);
     return r;
   }
@@ -1102,7 +1147,7 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
     HIP_CHECK(hipMemcpy(&est, w.st + h1.err_index, 1, hipMemcpyDeviceToHost));
     res->code = est == ST_INVALID ? CRDTM_INVALID_PATH : CRDTM_OPERATION_FAILED;
     res->err_index = h1.err_index;
-    if (st_out) hipLaunchKernelGGL(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n, h1.err_index, st_out);
+    if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n, h1.err_index, st_out);
     return CRDTM_OK;
   }
   res->n_applied = h1.n_applied;
@@ -1123,38 +1168,34 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   HIP_CHECK(hipMemsetAsync(fill, 0, (U + 1) * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(fc, 0xFF, U * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(ns, 0xFF, U * sizeof(uint32_t), s));
-  hipLaunchKernelGGL(k_ep_init, dim3(g), dim3(BLOCK), 0, s, o, w, anc);
-  hipLaunchKernelGGL(k_ep_jump, dim3(g), dim3(BLOCK), 0, s, o, w, anc, sp);
-  mark(c, "K2.ep");
+  LAUNCH(k_ep_init, dim3(g), dim3(BLOCK), 0, s, o, w, anc);
+  LAUNCH(k_ep_jump, dim3(g), dim3(BLOCK), 0, s, o, w, anc, sp);
   const uint32_t gU = grid_for(U);
-  hipLaunchKernelGGL(k_up_count, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, skey);
+  LAUNCH(k_up_count, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, skey);
   uint32_t* n_child_total = &dr->n_sentinels;  // scratch word for the scan total
   if ((r = scan_excl_u32(cnt, cnt, U + 1, n_child_total, ws, s))) return r;
-  hipLaunchKernelGGL(k_scatter, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, fill, carr);
+  LAUNCH(k_scatter, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, fill, carr);
   if ((r = segmented_sort(cnt, U, carr, U, skey, ws, s, dr))) return r;
-  hipLaunchKernelGGL(k_links, dim3(gU), dim3(BLOCK), 0, s, o, anc, cnt, n_child_total, carr, fc, ns);
-  mark(c, "K2.sort");
+  LAUNCH(k_links, dim3(gU), dim3(BLOCK), 0, s, o, anc, cnt, n_child_total, carr, fc, ns);
 
   // ---- K4: Euler tour + list ranking ----
   const uint64_t E = 2ULL * U;
   uint32_t* succ = ws.alloc<uint32_t>(E);
   unsigned long long* wt = ws.alloc<unsigned long long>(E);
   unsigned long long* excl = ws.alloc<unsigned long long>(E);
-  hipLaunchKernelGGL(k_euler, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, fc, ns, succ, wt);
+  LAUNCH(k_euler, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, fc, ns, succ, wt);
   if ((r = list_rank(succ, wt, E, 2 * (2 * n + 1), excl, ws, s, dr, 0))) return r;
-  mark(c, "K4.rank");
   uint32_t* order = ws.alloc<uint32_t>(U);
   uint32_t* nextn = ws.alloc<uint32_t>(n);
-  hipLaunchKernelGGL(k_order, dim3(gU), dim3(BLOCK), 0, s, o, w, sp, excl, order);
-  hipLaunchKernelGGL(k_next, dim3(g), dim3(BLOCK), 0, s, o, w, sp, excl, order, nextn);
-  mark(c, "K4.next");
+  LAUNCH(k_order, dim3(gU), dim3(BLOCK), 0, s, o, w, sp, excl, order);
+  LAUNCH(k_next, dim3(g), dim3(BLOCK), 0, s, o, w, sp, excl, order, nextn);
 
   // ---- K3 + commit ----
   uint32_t* appl = ws.alloc<uint32_t>(n + 1);
   uint32_t* plen = ws.alloc<uint32_t>(n + 1);
   uint32_t* kept = ws.alloc<uint32_t>(n + 1);
   uint32_t* live = ws.alloc<uint32_t>(n + 1);
-  hipLaunchKernelGGL(k_commit_flags, dim3(g), dim3(BLOCK), 0, s, o, w, appl, plen, kept, live);
+  LAUNCH(k_commit_flags, dim3(g), dim3(BLOCK), 0, s, o, w, appl, plen, kept, live);
   if ((r = scan_excl_u32(kept, kept, n, &dr->n_nodes_kept, ws, s))) return r;
   if ((r = scan_excl_u32(live, live, n, &dr->n_live_kept, ws, s))) return r;
   if ((r = scan_excl_u32(appl, appl, n, &dr->log_n, ws, s))) return r;
@@ -1178,19 +1219,17 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   ca.n_kept = K;
   ca.base_dict = 1;
   ca.log_base = static_cast<uint32_t>(t->log_n);
-  hipLaunchKernelGGL(k_commit_nodes, dim3(g), dim3(BLOCK), 0, s, o, w, t->d, ca, kept, live, appl, nextn, fc, excl,
+  LAUNCH(k_commit_nodes, dim3(g), dim3(BLOCK), 0, s, o, w, t->d, ca, kept, live, appl, nextn, fc, excl,
                      t->d.doc);
-  hipLaunchKernelGGL(k_commit_root, dim3(1), dim3(1), 0, s, o, t->d, kept, fc, 1u);
-  hipLaunchKernelGGL(k_log, dim3(g), dim3(BLOCK), 0, s, o, w.st, t->d, static_cast<uint32_t>(t->log_n),
+  LAUNCH(k_commit_root, dim3(1), dim3(1), 0, s, o, t->d, kept, fc, 1u);
+  LAUNCH(k_log, dim3(g), dim3(BLOCK), 0, s, o, w.st, t->d, static_cast<uint32_t>(t->log_n),
                      static_cast<uint32_t>(t->log_npath), appl, plen);
-  hipLaunchKernelGGL(k_log_tail, dim3(1), dim3(1), 0, s, t->d, static_cast<uint32_t>(t->log_n), &dr->log_n,
+  LAUNCH(k_log_tail, dim3(1), dim3(1), 0, s, t->d, static_cast<uint32_t>(t->log_n), &dr->log_n,
                      static_cast<uint32_t>(t->log_npath), &dr->log_npath);
-  mark(c, "K3.commit");
-  hipLaunchKernelGGL(k_rep_max, dim3(g), dim3(BLOCK), 0, s, o, w.st, c->rtab);
-  hipLaunchKernelGGL(k_rep_out, dim3(g), dim3(BLOCK), 0, s, o, w.st, c->rtab, rep, &dr->n_replica_out);
-  hipLaunchKernelGGL(k_rep_reset, dim3(g), dim3(BLOCK), 0, s, o, w.st, c->rtab);
-  if (st_out) hipLaunchKernelGGL(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n, NONE, st_out);
-  mark(c, "replicas");
+  LAUNCH(k_rep_max, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, s, o, w.st, c->rtab);
+  LAUNCH(k_rep_out, dim3(g), dim3(BLOCK), 0, s, o, w.st, c->rtab, rep, &dr->n_replica_out);
+  LAUNCH(k_rep_reset, dim3(g), dim3(BLOCK), 0, s, o, w.st, c->rtab);
+  if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n, NONE, st_out);
   if ((r = sync_read(c))) return r;
   const DevResult& h2 = *c->hres;
   const uint32_t nrep = h2.n_replica_out;
@@ -1222,13 +1261,13 @@ int linearize(crdtm_tree* t) {
   uint8_t* ok2 = ws.alloc<uint8_t>(D);
   uint32_t* up = ws.alloc<uint32_t>(D);
   uint32_t* up2 = ws.alloc<uint32_t>(D);
-  hipLaunchKernelGGL(k_dict_alive_init, dim3(grid_for(D)), dim3(BLOCK), 0, s, t->d, D, ok, up);
+  LAUNCH(k_dict_alive_init, dim3(grid_for(D)), dim3(BLOCK), 0, s, t->d, D, ok, up);
   // pointer doubling up the owner chain (depth bounded by the longest path)
   uint32_t rounds = 1;
   while ((1u << rounds) < t->max_depth + 2) ++rounds;
   rounds += 1;
   for (uint32_t k = 0; k < rounds; ++k) {
-    hipLaunchKernelGGL(k_dict_alive_jump, dim3(grid_for(D)), dim3(BLOCK), 0, s, D, ok, up, ok2, up2);
+    LAUNCH(k_dict_alive_jump, dim3(grid_for(D)), dim3(BLOCK), 0, s, D, ok, up, ok2, up2);
     std::swap(ok, ok2);
     std::swap(up, up2);
   }
@@ -1236,13 +1275,13 @@ int linearize(crdtm_tree* t) {
   uint32_t* succ = ws.alloc<uint32_t>(E);
   unsigned long long* wt = ws.alloc<unsigned long long>(E);
   unsigned long long* excl = ws.alloc<unsigned long long>(E);
-  hipLaunchKernelGGL(k_lin_entries, dim3(grid_for(E)), dim3(BLOCK), 0, s, t->d, S, D, ok, succ, wt);
+  LAUNCH(k_lin_entries, dim3(grid_for(E)), dim3(BLOCK), 0, s, t->d, S, D, ok, succ, wt);
   int r = list_rank(succ, wt, E, 0u /* root sentinel slot */, excl, ws, s, c->dres, 0);
   if (r) return r;
   TreeCaps need = t->cap;
   need.doc = std::max<uint64_t>(need.doc, S + 1);
   if (need.doc > t->cap.doc && (r = grow_tree(t, need))) return r;
-  hipLaunchKernelGGL(k_lin_doc, dim3(grid_for(S)), dim3(BLOCK), 0, s, t->d, S, excl, t->d.doc, t->cap.doc);
+  LAUNCH(k_lin_doc, dim3(grid_for(S)), dim3(BLOCK), 0, s, t->d, S, excl, t->d.doc, t->cap.doc);
   // number of visible entries = weight sum up to the end: excl at exit(0)
   unsigned long long tot = 0;
   HIP_CHECK(hipMemcpyAsync(&tot, excl + S, sizeof(tot), hipMemcpyDeviceToHost, s));

@@ -77,13 +77,13 @@ int scan_excl_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* total
   // keep the last input element: `in` may alias `out`
   uint32_t* last_in = ws.alloc<uint32_t>(1);
   HIP_CHECK(hipMemcpyAsync(last_in, in + n - 1, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-  hipLaunchKernelGGL(k_scan_tiles, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, in, out, sums, n);
+  LAUNCH(k_scan_tiles, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, in, out, sums, n);
   if (tiles > 1) {
     int r = scan_excl_u32(sums, sums, tiles, nullptr, ws, st);
     if (r) return r;
-    hipLaunchKernelGGL(k_scan_add, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, out, sums, n);
+    LAUNCH(k_scan_add, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, out, sums, n);
   }
-  if (total) hipLaunchKernelGGL(k_store_total, dim3(1), dim3(1), 0, st, last_in, out + n - 1, total);
+  if (total) LAUNCH(k_store_total, dim3(1), dim3(1), 0, st, last_in, out + n - 1, total);
   return CRDTM_OK;
 }
 
@@ -254,10 +254,10 @@ int segmented_sort(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, ui
   uint32_t* big = ws.alloc<uint32_t>(n_seg + 1);
   uint32_t* nbig = &dres->big_segments;
   HIP_CHECK(hipMemsetAsync(nbig, 0, sizeof(uint32_t), st));
-  hipLaunchKernelGGL(k_sort_small, dim3(grid_for(n_seg)), dim3(BLOCK), 0, st, seg_start, n_seg, carr, sort_key, big,
+  LAUNCH(k_sort_small, dim3(grid_for(n_seg)), dim3(BLOCK), 0, st, seg_start, n_seg, carr, sort_key, big,
                      nbig);
   uint32_t* scratch = ws.alloc<uint32_t>(n_items + 1);
-  hipLaunchKernelGGL(k_sort_big, dim3(512), dim3(1024), 0, st, seg_start, big, nbig, carr, scratch, sort_key);
+  LAUNCH(k_sort_big, dim3(512), dim3(1024), 0, st, seg_start, big, nbig, carr, scratch, sort_key);
   return CRDTM_OK;
 }
 
@@ -280,18 +280,21 @@ __global__ void k_lr_head(uint32_t head, uint32_t* split_entry, uint32_t* n_spli
 __global__ void __launch_bounds__(BLOCK) k_lr_pick(const uint32_t* __restrict__ succ, uint64_t n, uint32_t head,
                                                    uint32_t kmask, uint64_t cap, uint32_t* __restrict__ split_id,
                                                    uint32_t* __restrict__ split_entry, uint32_t* __restrict__ n_split) {
-  for (uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; e < n;
-       e += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  const uint64_t trips = (n + stride - 1) / stride;  // uniform trip count: wave_ticket needs every lane
+  for (uint64_t t = 0; t < trips; ++t) {
+    const uint64_t e = t * stride + blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+    const bool in = e < n;
+    const bool pick = in && e != head && succ[e] != ABSENT &&
+                      (static_cast<uint32_t>(mix64(e * 0x9E3779B97F4A7C15ULL + 0x632BE59BD9B4E019ULL)) & kmask) == 0;
+    const uint32_t tk = wave_ticket(n_split, pick);
+    if (!in) continue;
     uint32_t id = NONE;
     if (e == head) {
       id = 0;
-    } else if (succ[e] != ABSENT &&
-               (static_cast<uint32_t>(mix64(e * 0x9E3779B97F4A7C15ULL + 0x632BE59BD9B4E019ULL)) & kmask) == 0) {
-      uint32_t t = atomicAdd(n_split, 1u);
-      if (t < cap) {
-        id = t;
-        split_entry[t] = static_cast<uint32_t>(e);
-      }
+    } else if (pick && tk < cap) {
+      id = tk;
+      split_entry[tk] = static_cast<uint32_t>(e);
     }
     split_id[e] = id;
   }
@@ -368,18 +371,18 @@ int list_rank(const uint32_t* succ, const unsigned long long* w, uint64_t n, uin
   unsigned long long* red_excl = ws.alloc<unsigned long long>(cap);
   uint32_t* nsp = &dres->n_split[level < 8 ? level : 7];
   HIP_CHECK(hipMemsetAsync(owner, 0xFF, n * sizeof(uint32_t), st));
-  hipLaunchKernelGGL(k_lr_head, dim3(1), dim3(1), 0, st, head, split_entry, nsp);
-  hipLaunchKernelGGL(k_lr_pick, dim3(grid_for(n)), dim3(BLOCK), 0, st, succ, n, head, kmask, cap, split_id,
+  LAUNCH(k_lr_head, dim3(1), dim3(1), 0, st, head, split_entry, nsp);
+  LAUNCH(k_lr_pick, dim3(grid_for(n, BLOCK, 4096)), dim3(BLOCK), 0, st, succ, n, head, kmask, cap, split_id,
                      split_entry, nsp);
-  hipLaunchKernelGGL(k_lr_walk, dim3(grid_for(cap)), dim3(BLOCK), 0, st, succ, w, split_id, split_entry, nsp, cap,
+  LAUNCH(k_lr_walk, dim3(grid_for(cap)), dim3(BLOCK), 0, st, succ, w, split_id, split_entry, nsp, cap,
                      n, local, owner, red_succ, red_w);
   if (cap <= LR_SERIAL || level >= 7) {
-    hipLaunchKernelGGL(k_lr_serial, dim3(1), dim3(64), 0, st, red_succ, red_w, red_excl, cap);
+    LAUNCH(k_lr_serial, dim3(1), dim3(64), 0, st, red_succ, red_w, red_excl, cap);
   } else {
     int r = list_rank(red_succ, red_w, cap, 0u, red_excl, ws, st, dres, level + 1);
     if (r) return r;
   }
-  hipLaunchKernelGGL(k_lr_apply, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, owner, local, red_excl, excl);
+  LAUNCH(k_lr_apply, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, owner, local, red_excl, excl);
   return CRDTM_OK;
 }
 

@@ -92,6 +92,8 @@ int crdtm_ctx_sync(crdtm_ctx *ctx);
 /* CRDTree.init replicaId (src/CRDTree.elm:130-139) */
 int crdtm_tree_create(crdtm_ctx *ctx, int64_t replica_id, crdtm_tree **out);
 int crdtm_tree_destroy(crdtm_tree *t);
+/* Reset to `init replica_id` keeping the device allocations (benchmarks, pooling). */
+int crdtm_tree_reset(crdtm_tree *t, int64_t replica_id);
 /* Elm values are persistent: clone before apply to keep the old version. */
 int crdtm_tree_clone(const crdtm_tree *t, crdtm_tree **out);
 
