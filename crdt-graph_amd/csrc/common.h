@@ -61,9 +61,9 @@ struct DevResult {
   int64_t replay_timestamp;
   uint32_t n_split[8];      // list ranking level sizes
   uint32_t big_segments;
+  uint32_t huge_segments;
   uint32_t last_add;        // 1 + index of the last applied Add
   uint32_t first_del;       // index of the first applied Delete
-  uint32_t pad;
 };
 
 #define HIP_CHECK(x)                                                                         \

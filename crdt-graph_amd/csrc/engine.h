@@ -98,8 +98,8 @@ namespace crdtm {
 int scan_excl_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* total, Arena& ws, hipStream_t st);
 int segmented_sort(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items,
                    const long long* sort_key, Arena& ws, hipStream_t st, DevResult* dres);
-int list_rank(const uint32_t* succ, const unsigned long long* w, uint64_t n, uint32_t head,
-              unsigned long long* excl, Arena& ws, hipStream_t st, DevResult* dres, int level);
+// ent[e] = {succ, wbits}: see primitives.hip
+int list_rank(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws, hipStream_t st);
 
 // Device view of one batch of ops.
 struct OpsDev {

@@ -5,7 +5,7 @@
 
 namespace crdtm {
 
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z ^= z >> 33;
   z *= 0xff51afd7ed558ccdULL;
   z ^= z >> 33;

@@ -319,23 +319,59 @@ __device__ __forceinline__ uint32_t uni_up(const OpsDev& o, const uint32_t* anc,
   return 2 * n + 1;  // root sentinel -> super root
 }
 
+// Child counting and placement. The root dict's sentinel (uid 2n) can own a
+// large share of all nodes (every node whose anchor chain holds no smaller
+// timestamp), so its counter is aggregated per workgroup instead of taking
+// one same-address atomic per child.
+__device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* total) {
+  __shared__ uint32_t sw[BLOCK / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t inc = wave_incl_scan(v);
+  if (lane == 63) sw[wave] = inc;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+  for (int k = 0; k < BLOCK / 64; ++k) {
+    if (k < wave) base += sw[k];
+    tot += sw[k];
+  }
+  __syncthreads();
+  *total = tot;
+  return base + inc - v;
+}
+
 __global__ void __launch_bounds__(BLOCK) k_up_count(OpsDev o, Work w, const uint32_t* anc, const uint8_t* sp,
                                                     uint32_t* cnt, long long* skey) {
-  const uint32_t n = o.n, U = 2 * n + 1;  // super root excluded (no parent)
+  const uint32_t n = o.n, U = 2 * n + 1, H = 2 * n;  // super root excluded (no parent)
+  uint32_t hot = 0;
   GRID_STRIDE(v, U) {
     if (!uni_present(o, w, sp, v)) continue;
-    atomicAdd(&cnt[uni_up(o, anc, v)], 1u);
+    const uint32_t u = uni_up(o, anc, v);
+    if (u == H) ++hot;
+    else atomicAdd(&cnt[u], 1u);
     skey[v] = v < n ? -o.ts[v] : (long long)0x8000000000000000LL;
   }
+  hot = block_sum(hot);
+  if (threadIdx.x == 0 && hot) atomicAdd(&cnt[H], hot);
 }
 
 __global__ void __launch_bounds__(BLOCK) k_scatter(OpsDev o, Work w, const uint32_t* anc, const uint8_t* sp,
                                                    const uint32_t* start, uint32_t* fill, uint32_t* carr) {
-  const uint32_t n = o.n, U = 2 * n + 1;
+  __shared__ uint32_t blk_base;
+  const uint32_t n = o.n, U = 2 * n + 1, H = 2 * n;
+  uint32_t hot = 0;
+  GRID_STRIDE(v, U) {
+    if (uni_present(o, w, sp, v) && uni_up(o, anc, v) == H) ++hot;
+  }
+  uint32_t tot;
+  uint32_t mine = block_excl_sum(hot, &tot);
+  if (threadIdx.x == 0) blk_base = tot ? atomicAdd(&fill[H], tot) : 0u;
+  __syncthreads();
+  mine += blk_base + start[H];
   GRID_STRIDE(v, U) {
     if (!uni_present(o, w, sp, v)) continue;
     const uint32_t u = uni_up(o, anc, v);
-    carr[start[u] + atomicAdd(&fill[u], 1u)] = v;
+    if (u == H) carr[mine++] = v;
+    else carr[start[u] + atomicAdd(&fill[u], 1u)] = v;
   }
 }
 
@@ -351,34 +387,29 @@ __global__ void __launch_bounds__(BLOCK) k_links(OpsDev o, const uint32_t* anc, 
   }
 }
 
-// Euler tour: entry 2v = enter v, 2v+1 = leave v. Weight of enter v =
-// (1 << 32) | visible(v): the high word counts tour nodes (pre-order rank),
-// the low word counts visible nodes (document rank).
+// Euler tour: entry 2v = enter v, 2v+1 = leave v. The weight of enter v is
+// (1 << 32) | visible(v) (wbits 0b1x): the high word counts tour nodes
+// (pre-order rank), the low word counts visible nodes (document rank).
 __global__ void __launch_bounds__(BLOCK) k_euler(OpsDev o, Work w, const uint32_t* anc, const uint8_t* sp,
-                                                 const uint32_t* fc, const uint32_t* ns, uint32_t* succ,
-                                                 unsigned long long* wt) {
+                                                 const uint32_t* fc, const uint32_t* ns, uint2* ent) {
   const uint32_t n = o.n, U = 2 * n + 2;
   GRID_STRIDE(v, U) {
     if (!uni_present(o, w, sp, v)) {
-      succ[2 * v] = ABSENT;
-      succ[2 * v + 1] = ABSENT;
-      wt[2 * v] = 0;
-      wt[2 * v + 1] = 0;
+      ent[2 * v] = make_uint2(ABSENT, 0u);
+      ent[2 * v + 1] = make_uint2(ABSENT, 0u);
       continue;
     }
-    succ[2 * v] = fc[v] != NONE ? 2 * fc[v] : 2 * v + 1;
     uint32_t after;
     if (ns[v] != NONE) after = 2 * ns[v];
     else if (v == 2 * n + 1) after = NONE;
     else after = 2 * uni_up(o, anc, v) + 1;
-    succ[2 * v + 1] = after;
     uint32_t vis = 0;
     if (v < n) {
       const uint32_t p = w.addpar[v];
       vis = (w.dtime[v] == NONE && (p == n || !w.dead[p])) ? 1u : 0u;
     }
-    wt[2 * v] = (1ULL << 32) | vis;
-    wt[2 * v + 1] = 0;
+    ent[2 * v] = make_uint2(fc[v] != NONE ? 2 * fc[v] : 2 * v + 1, 2u | vis);
+    ent[2 * v + 1] = make_uint2(after, 0u);
   }
 }
 
@@ -834,23 +865,23 @@ __global__ void __launch_bounds__(BLOCK) k_dict_alive_jump(uint32_t n_dicts, uin
 }
 
 __global__ void __launch_bounds__(BLOCK) k_lin_entries(TreeDev T, uint32_t S, uint32_t D, const uint8_t* alive,
-                                                       uint32_t* succ, unsigned long long* wt) {
+                                                       uint2* ent) {
   GRID_STRIDE(e, S + D) {
     if (e < S) {
       const uint32_t s = e;
       const uint8_t f = T.s_flags[s];
-      if (!alive[T.s_dict[s]] || (f & F_ORPHAN)) { succ[e] = ABSENT; wt[e] = 0; continue; }
+      if (!alive[T.s_dict[s]] || (f & F_ORPHAN)) { ent[e] = make_uint2(ABSENT, 0u); continue; }
       const uint32_t c = T.s_child[s];
-      if (!(f & F_TOMB) && c != NONE) succ[e] = T.d_sent[c];
-      else succ[e] = T.s_next[s] != NONE ? T.s_next[s] : S + T.s_dict[s];
-      wt[e] = (f & F_TOMB) ? 0ULL : 1ULL;
+      uint32_t nx;
+      if (!(f & F_TOMB) && c != NONE) nx = T.d_sent[c];
+      else nx = T.s_next[s] != NONE ? T.s_next[s] : S + T.s_dict[s];
+      ent[e] = make_uint2(nx, (f & F_TOMB) ? 0u : 1u);
     } else {
       const uint32_t d = e - S;
-      if (!alive[d]) { succ[e] = ABSENT; wt[e] = 0; continue; }
-      wt[e] = 0;
-      if (d == 0) { succ[e] = NONE; continue; }
+      if (!alive[d]) { ent[e] = make_uint2(ABSENT, 0u); continue; }
+      if (d == 0) { ent[e] = make_uint2(NONE, 0u); continue; }
       const uint32_t o = T.d_owner[d];
-      succ[e] = T.s_next[o] != NONE ? T.s_next[o] : S + T.s_dict[o];
+      ent[e] = make_uint2(T.s_next[o] != NONE ? T.s_next[o] : S + T.s_dict[o], 0u);
     }
   }
 }
@@ -1171,20 +1202,19 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   LAUNCH(k_ep_init, dim3(g), dim3(BLOCK), 0, s, o, w, anc);
   LAUNCH(k_ep_jump, dim3(g), dim3(BLOCK), 0, s, o, w, anc, sp);
   const uint32_t gU = grid_for(U);
-  LAUNCH(k_up_count, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, skey);
+  LAUNCH(k_up_count, dim3(grid_for(U, BLOCK, 2048)), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, skey);
   uint32_t* n_child_total = &dr->n_sentinels;  // scratch word for the scan total
   if ((r = scan_excl_u32(cnt, cnt, U + 1, n_child_total, ws, s))) return r;
-  LAUNCH(k_scatter, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, fill, carr);
+  LAUNCH(k_scatter, dim3(grid_for(U, BLOCK, 2048)), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, fill, carr);
   if ((r = segmented_sort(cnt, U, carr, U, skey, ws, s, dr))) return r;
   LAUNCH(k_links, dim3(gU), dim3(BLOCK), 0, s, o, anc, cnt, n_child_total, carr, fc, ns);
 
   // ---- K4: Euler tour + list ranking ----
   const uint64_t E = 2ULL * U;
-  uint32_t* succ = ws.alloc<uint32_t>(E);
-  unsigned long long* wt = ws.alloc<unsigned long long>(E);
+  uint2* ent = ws.alloc<uint2>(E);
   unsigned long long* excl = ws.alloc<unsigned long long>(E);
-  LAUNCH(k_euler, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, fc, ns, succ, wt);
-  if ((r = list_rank(succ, wt, E, 2 * (2 * n + 1), excl, ws, s, dr, 0))) return r;
+  LAUNCH(k_euler, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, fc, ns, ent);
+  if ((r = list_rank(ent, E, 2 * (2 * n + 1), excl, ws, s))) return r;
   uint32_t* order = ws.alloc<uint32_t>(U);
   uint32_t* nextn = ws.alloc<uint32_t>(n);
   LAUNCH(k_order, dim3(gU), dim3(BLOCK), 0, s, o, w, sp, excl, order);
@@ -1272,11 +1302,10 @@ int linearize(crdtm_tree* t) {
     std::swap(up, up2);
   }
   const uint64_t E = static_cast<uint64_t>(S) + D;
-  uint32_t* succ = ws.alloc<uint32_t>(E);
-  unsigned long long* wt = ws.alloc<unsigned long long>(E);
+  uint2* ent = ws.alloc<uint2>(E);
   unsigned long long* excl = ws.alloc<unsigned long long>(E);
-  LAUNCH(k_lin_entries, dim3(grid_for(E)), dim3(BLOCK), 0, s, t->d, S, D, ok, succ, wt);
-  int r = list_rank(succ, wt, E, 0u /* root sentinel slot */, excl, ws, s, c->dres, 0);
+  LAUNCH(k_lin_entries, dim3(grid_for(E)), dim3(BLOCK), 0, s, t->d, S, D, ok, ent);
+  int r = list_rank(ent, E, 0u /* root sentinel slot */, excl, ws, s);
   if (r) return r;
   TreeCaps need = t->cap;
   need.doc = std::max<uint64_t>(need.doc, S + 1);

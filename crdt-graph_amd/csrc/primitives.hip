@@ -140,6 +140,7 @@ __global__ void __launch_bounds__(1024) k_sort_big(const uint32_t* __restrict__ 
   for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
     const uint32_t u = big_list[bi];
     const uint32_t b = seg_start[u], len = seg_start[u + 1] - b;
+    if (len > LDS_SORT_MAX) continue;  // huge: multi-workgroup path (segmented_sort)
     if (len <= LDS_SORT_MAX) {
       uint32_t p2 = 1;
       while (p2 < len) p2 <<= 1;
@@ -249,95 +250,192 @@ __global__ void __launch_bounds__(1024) k_sort_big(const uint32_t* __restrict__ 
   }
 }
 
+// Huge segments (> LDS_SORT_MAX): chunk-sort in LDS, then merge passes with
+// merge-path partitioning, every pass spread over many workgroups.
+__global__ void __launch_bounds__(1024) k_sort_chunks(uint32_t* __restrict__ carr, uint32_t b, uint32_t len,
+                                                       const long long* __restrict__ sort_key) {
+  __shared__ long long skey[LDS_SORT_MAX];
+  __shared__ uint32_t sid[LDS_SORT_MAX];
+  const uint32_t r0 = blockIdx.x * LDS_SORT_MAX;
+  const uint32_t rl = min(LDS_SORT_MAX, len - r0);
+  for (uint32_t j = threadIdx.x; j < LDS_SORT_MAX; j += blockDim.x) {
+    if (j < rl) {
+      uint32_t v = carr[b + r0 + j];
+      sid[j] = v;
+      skey[j] = sort_key[v];
+    } else {
+      sid[j] = NONE;
+      skey[j] = 0x7fffffffffffffffLL;
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = 2; k <= LDS_SORT_MAX; k <<= 1) {
+    for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+      for (uint32_t i = threadIdx.x; i < LDS_SORT_MAX; i += blockDim.x) {
+        uint32_t ixj = i ^ jj;
+        if (ixj > i) {
+          bool up = (i & k) == 0;
+          long long a = skey[i], c = skey[ixj];
+          if ((a > c) == up) {
+            skey[i] = c;
+            skey[ixj] = a;
+            uint32_t t = sid[i];
+            sid[i] = sid[ixj];
+            sid[ixj] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t j = threadIdx.x; j < rl; j += blockDim.x) carr[b + r0 + j] = sid[j];
+}
+
+constexpr uint32_t MERGE_PER_THREAD = 8;
+constexpr uint32_t MERGE_TILE = BLOCK * MERGE_PER_THREAD;  // 2048 outputs per workgroup
+
+__global__ void __launch_bounds__(BLOCK) k_merge_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                      uint32_t len, uint32_t width,
+                                                      const long long* __restrict__ sort_key) {
+  const uint32_t d0 = blockIdx.x * MERGE_TILE + threadIdx.x * MERGE_PER_THREAD;
+  if (d0 >= len) return;
+  const uint32_t pair = d0 / (2 * width);
+  const uint32_t a0 = pair * 2 * width, a1 = min(a0 + width, len), b1 = min(a0 + 2 * width, len);
+  const uint32_t na = a1 - a0, nb = b1 - a1;
+  const uint32_t d = d0 - a0;  // output rank within the pair
+  uint32_t lo = d > nb ? d - nb : 0, hi = min(d, na);
+  while (lo < hi) {  // merge path: #taken from A among the first d outputs
+    const uint32_t mid = (lo + hi) >> 1;
+    if (sort_key[src[a0 + mid]] < sort_key[src[a1 + d - mid - 1]]) lo = mid + 1;
+    else hi = mid;
+  }
+  uint32_t i = lo, j = d - lo;
+  const uint32_t dend = min(d + MERGE_PER_THREAD, na + nb);
+  for (uint32_t q = d; q < dend; ++q) {
+    bool takeA;
+    if (i >= na) takeA = false;
+    else if (j >= nb) takeA = true;
+    else takeA = sort_key[src[a0 + i]] < sort_key[src[a1 + j]];
+    dst[a0 + q] = takeA ? src[a0 + i++] : src[a1 + j++];
+  }
+}
+
+__global__ void k_sort_big_filter(const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ big_list,
+                                  const uint32_t* __restrict__ n_big, uint32_t* __restrict__ huge,
+                                  uint32_t* __restrict__ n_huge) {
+  const uint32_t nb = *n_big;
+  for (uint32_t bi = blockIdx.x * blockDim.x + threadIdx.x; bi < nb; bi += gridDim.x * blockDim.x) {
+    const uint32_t u = big_list[bi];
+    if (seg_start[u + 1] - seg_start[u] > LDS_SORT_MAX) huge[atomicAdd(n_huge, 1u)] = u;
+  }
+}
+
 int segmented_sort(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items,
                    const long long* sort_key, Arena& ws, hipStream_t st, DevResult* dres) {
   uint32_t* big = ws.alloc<uint32_t>(n_seg + 1);
-  uint32_t* nbig = &dres->big_segments;
-  HIP_CHECK(hipMemsetAsync(nbig, 0, sizeof(uint32_t), st));
-  LAUNCH(k_sort_small, dim3(grid_for(n_seg)), dim3(BLOCK), 0, st, seg_start, n_seg, carr, sort_key, big,
-                     nbig);
+  uint32_t* huge = ws.alloc<uint32_t>(n_seg + 1);
   uint32_t* scratch = ws.alloc<uint32_t>(n_items + 1);
+  uint32_t* nbig = &dres->big_segments;
+  uint32_t* nhuge = &dres->huge_segments;
+  HIP_CHECK(hipMemsetAsync(nbig, 0, 2 * sizeof(uint32_t), st));  // big_segments, huge_segments
+  LAUNCH(k_sort_small, dim3(grid_for(n_seg)), dim3(BLOCK), 0, st, seg_start, n_seg, carr, sort_key, big, nbig);
+  // segments of 17..LDS_SORT_MAX: one workgroup each (huge ones are skipped there)
   LAUNCH(k_sort_big, dim3(512), dim3(1024), 0, st, seg_start, big, nbig, carr, scratch, sort_key);
+  LAUNCH(k_sort_big_filter, dim3(16), dim3(BLOCK), 0, st, seg_start, big, nbig, huge, nhuge);
+  uint32_t nh = 0;
+  HIP_CHECK(hipMemcpyAsync(&nh, nhuge, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  if (nh == 0) return CRDTM_OK;
+  std::vector<uint32_t> hh(nh);
+  HIP_CHECK(hipMemcpy(hh.data(), huge, nh * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  for (uint32_t u : hh) {
+    uint32_t se[2];
+    HIP_CHECK(hipMemcpy(se, seg_start + u, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    const uint32_t b = se[0], len = se[1] - se[0];
+    LAUNCH(k_sort_chunks, dim3((len + LDS_SORT_MAX - 1) / LDS_SORT_MAX), dim3(1024), 0, st, carr, b, len, sort_key);
+    uint32_t* src = carr + b;
+    uint32_t* dst = scratch + b;
+    for (uint32_t w = LDS_SORT_MAX; w < len; w <<= 1) {
+      LAUNCH(k_merge_pass, dim3((len + MERGE_TILE - 1) / MERGE_TILE), dim3(BLOCK), 0, st, src, dst, len, w,
+             sort_key);
+      std::swap(src, dst);
+    }
+    if (src != carr + b)
+      HIP_CHECK(hipMemcpyAsync(carr + b, src, len * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+  }
   return CRDTM_OK;
 }
 
 // ---------------------------------------------------------------------------
-// List ranking (north-star kernel 4). Input: succ[e] (NONE = end of list,
-// ABSENT = not in any list), weight[e] (u64), head. Output: excl[e] = sum of
-// weights of the entries before e along the list from head.
-// Sublist method: the head (id 0) plus hashed splitters (~1/K of the entries)
-// each walk their sublist; the reduced list of splitters (head id 0) is ranked
-// recursively, serially once it is short; a last pass adds each splitter's
-// prefix to the entries of its sublist.
+// List ranking (north-star kernel 4). Level 0 input: ent[e] = {succ, wbits}
+// (succ: NONE = end of list, ABSENT = not in any list; wbits bit1 -> high
+// word +1, bit0 -> low word +1). Output: excl[e] = sum of the weights of the
+// entries before e along the list from `head` (~0 for entries not on it).
+//
+// Sublist method with deterministic splitters: index block b (2^kbits
+// entries) nominates one hashed candidate; present candidates (plus the head)
+// walk their sublist, each step one 8-byte load. The reduced list (one entry
+// per block, + the head) is ranked recursively, serially once it is short,
+// and a last pass adds each splitter's prefix to its sublist. No atomics.
 // ---------------------------------------------------------------------------
 constexpr uint64_t LR_SERIAL = 2048;
 
-__global__ void k_lr_head(uint32_t head, uint32_t* split_entry, uint32_t* n_split) {
-  split_entry[0] = head;
-  *n_split = 1;
+__host__ __device__ __forceinline__ uint64_t lr_cand(uint64_t b, uint32_t kbits) {
+  return (b << kbits) + (mix64(b * 0x9E3779B97F4A7C15ULL + 0x632BE59BD9B4E019ULL) & ((1ULL << kbits) - 1));
 }
 
-__global__ void __launch_bounds__(BLOCK) k_lr_pick(const uint32_t* __restrict__ succ, uint64_t n, uint32_t head,
-                                                   uint32_t kmask, uint64_t cap, uint32_t* __restrict__ split_id,
-                                                   uint32_t* __restrict__ split_entry, uint32_t* __restrict__ n_split) {
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  const uint64_t trips = (n + stride - 1) / stride;  // uniform trip count: wave_ticket needs every lane
-  for (uint64_t t = 0; t < trips; ++t) {
-    const uint64_t e = t * stride + blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-    const bool in = e < n;
-    const bool pick = in && e != head && succ[e] != ABSENT &&
-                      (static_cast<uint32_t>(mix64(e * 0x9E3779B97F4A7C15ULL + 0x632BE59BD9B4E019ULL)) & kmask) == 0;
-    const uint32_t tk = wave_ticket(n_split, pick);
-    if (!in) continue;
-    uint32_t id = NONE;
-    if (e == head) {
-      id = 0;
-    } else if (pick && tk < cap) {
-      id = tk;
-      split_entry[tk] = static_cast<uint32_t>(e);
-    }
-    split_id[e] = id;
-  }
+__device__ __forceinline__ unsigned long long lr_weight(uint32_t wbits) {
+  return (static_cast<unsigned long long>((wbits >> 1) & 1u) << 32) | (wbits & 1u);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_lr_walk(const uint32_t* __restrict__ succ,
-                                                   const unsigned long long* __restrict__ w,
-                                                   const uint32_t* __restrict__ split_id,
-                                                   const uint32_t* __restrict__ split_entry,
-                                                   const uint32_t* __restrict__ n_split, uint64_t cap,
-                                                   uint64_t n_entries, unsigned long long* __restrict__ local,
-                                                   uint32_t* __restrict__ owner, uint32_t* __restrict__ red_succ,
+template <bool PACKED>
+__global__ void __launch_bounds__(BLOCK) k_lr_walk(const uint2* __restrict__ ent, const uint32_t* __restrict__ succ,
+                                                   const unsigned long long* __restrict__ w, uint64_t n,
+                                                   uint32_t kbits, uint32_t head, uint64_t head_id, uint64_t nb,
+                                                   uint32_t* __restrict__ owner, unsigned long long* __restrict__ local,
+                                                   uint32_t* __restrict__ red_succ,
                                                    unsigned long long* __restrict__ red_w) {
-  const uint64_t ns = min(static_cast<uint64_t>(*n_split), cap);
-  for (uint64_t id = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; id < cap;
+  for (uint64_t id = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; id <= nb;
        id += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    if (id >= ns) {
-      red_succ[id] = ABSENT;
-      continue;
+    uint64_t e;
+    if (id == nb) {
+      if (head_id != nb) { red_succ[id] = ABSENT; continue; }
+      e = head;
+    } else {
+      e = lr_cand(id, kbits);
+      const uint32_t s0 = e < n ? (PACKED ? ent[e].x : succ[e]) : ABSENT;
+      if (s0 == ABSENT) { red_succ[id] = ABSENT; continue; }
     }
-    uint32_t cur = split_entry[id];
+    uint32_t cur = static_cast<uint32_t>(e);
     unsigned long long acc = 0;
     uint32_t nxt;
     for (uint64_t steps = 0;; ++steps) {
-      if (steps > n_entries) { nxt = NONE; break; }  // cycle guard (never taken on a valid list)
-      local[cur] = acc;
+      unsigned long long wc;
+      if (PACKED) {
+        const uint2 x = ent[cur];
+        nxt = x.x;
+        wc = lr_weight(x.y);
+      } else {
+        nxt = succ[cur];
+        wc = w[cur];
+      }
       owner[cur] = static_cast<uint32_t>(id);
-      acc += w[cur];
-      nxt = succ[cur];
-      if (nxt >= n_entries) { nxt = NONE; break; }  // end (or a malformed link)
-      if (split_id[nxt] != NONE) break;
+      local[cur] = acc;
+      acc += wc;
+      if (nxt >= n || steps > n) { nxt = NONE; break; }  // end (cycle guard never taken on a valid list)
+      if (nxt == lr_cand(nxt >> kbits, kbits)) break;      // next splitter
       cur = nxt;
     }
     red_w[id] = acc;
-    red_succ[id] = (nxt == NONE) ? NONE : split_id[nxt];
+    red_succ[id] = nxt == NONE ? NONE : (nxt >> kbits);
   }
 }
 
-// Serial ranking of a short list by one lane (head id 0).
+// Serial ranking of a short list by one lane.
 __global__ void k_lr_serial(const uint32_t* __restrict__ succ, const unsigned long long* __restrict__ w,
-                            unsigned long long* __restrict__ excl, uint64_t n_entries) {
+                            uint64_t head, unsigned long long* __restrict__ excl, uint64_t n_entries) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint32_t cur = 0;
+  uint64_t cur = head;
   unsigned long long acc = 0;
   for (uint64_t steps = 0; cur < n_entries && steps <= n_entries; ++steps) {
     excl[cur] = acc;
@@ -353,37 +451,41 @@ __global__ void __launch_bounds__(BLOCK) k_lr_apply(uint64_t n, const uint32_t* 
   for (uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; e < n;
        e += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
     const uint32_t o = owner[e];
-    excl[e] = (o == NONE) ? ~0ULL : red_excl[o] + local[e];  // ~0: not on the list
+    excl[e] = (o == NONE) ? ~0ULL : red_excl[o] + local[e];
   }
 }
 
-int list_rank(const uint32_t* succ, const unsigned long long* w, uint64_t n, uint32_t head,
-              unsigned long long* excl, Arena& ws, hipStream_t st, DevResult* dres, int level) {
-  const uint32_t kmask = level == 0 ? 31u : 15u;
-  uint64_t cap = n / (kmask + 1) * 2 + 1024;
-  if (cap > n) cap = n;
-  uint32_t* split_id = ws.alloc<uint32_t>(n);
-  uint32_t* split_entry = ws.alloc<uint32_t>(cap);
+static int list_rank_level(const uint2* ent, const uint32_t* succ, const unsigned long long* w, uint64_t n,
+                           uint32_t head, unsigned long long* excl, Arena& ws, hipStream_t st, int level) {
+  const uint32_t kbits = level == 0 ? 5u : 4u;
+  const uint64_t nb = (n + (1ULL << kbits) - 1) >> kbits;
+  const uint64_t head_id = (lr_cand(head >> kbits, kbits) == head) ? (head >> kbits) : nb;
   uint32_t* owner = ws.alloc<uint32_t>(n);
   unsigned long long* local = ws.alloc<unsigned long long>(n);
-  uint32_t* red_succ = ws.alloc<uint32_t>(cap);
-  unsigned long long* red_w = ws.alloc<unsigned long long>(cap);
-  unsigned long long* red_excl = ws.alloc<unsigned long long>(cap);
-  uint32_t* nsp = &dres->n_split[level < 8 ? level : 7];
+  uint32_t* red_succ = ws.alloc<uint32_t>(nb + 1);
+  unsigned long long* red_w = ws.alloc<unsigned long long>(nb + 1);
+  unsigned long long* red_excl = ws.alloc<unsigned long long>(nb + 1);
   HIP_CHECK(hipMemsetAsync(owner, 0xFF, n * sizeof(uint32_t), st));
-  LAUNCH(k_lr_head, dim3(1), dim3(1), 0, st, head, split_entry, nsp);
-  LAUNCH(k_lr_pick, dim3(grid_for(n, BLOCK, 4096)), dim3(BLOCK), 0, st, succ, n, head, kmask, cap, split_id,
-                     split_entry, nsp);
-  LAUNCH(k_lr_walk, dim3(grid_for(cap)), dim3(BLOCK), 0, st, succ, w, split_id, split_entry, nsp, cap,
-                     n, local, owner, red_succ, red_w);
-  if (cap <= LR_SERIAL || level >= 7) {
-    LAUNCH(k_lr_serial, dim3(1), dim3(64), 0, st, red_succ, red_w, red_excl, cap);
+  if (ent) {
+    LAUNCH(k_lr_walk<true>, dim3(grid_for(nb + 1)), dim3(BLOCK), 0, st, ent, nullptr, nullptr, n, kbits, head,
+           head_id, nb, owner, local, red_succ, red_w);
   } else {
-    int r = list_rank(red_succ, red_w, cap, 0u, red_excl, ws, st, dres, level + 1);
+    LAUNCH(k_lr_walk<false>, dim3(grid_for(nb + 1)), dim3(BLOCK), 0, st, nullptr, succ, w, n, kbits, head, head_id,
+           nb, owner, local, red_succ, red_w);
+  }
+  if (nb + 1 <= LR_SERIAL || level >= 7) {
+    LAUNCH(k_lr_serial, dim3(1), dim3(64), 0, st, red_succ, red_w, head_id, red_excl, nb + 1);
+  } else {
+    int r = list_rank_level(nullptr, red_succ, red_w, nb + 1, static_cast<uint32_t>(head_id), red_excl, ws, st,
+                            level + 1);
     if (r) return r;
   }
   LAUNCH(k_lr_apply, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, owner, local, red_excl, excl);
   return CRDTM_OK;
+}
+
+int list_rank(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws, hipStream_t st) {
+  return list_rank_level(ent, nullptr, nullptr, n, head, excl, ws, st, 0);
 }
 
 }  // namespace crdtm
