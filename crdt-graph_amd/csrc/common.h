@@ -64,6 +64,9 @@ struct DevResult {
   uint32_t huge_segments;
   uint32_t last_add;        // 1 + index of the last applied Add
   uint32_t first_del;       // index of the first applied Delete
+  uint32_t has_negative;    // some Add ts < 0 (dense index impossible)
+  uint32_t n_del;           // Delete ops in the batch
+  uint32_t range_total;     // dense index size
 };
 
 #define HIP_CHECK(x)                                                                         \

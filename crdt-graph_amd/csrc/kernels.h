@@ -49,6 +49,46 @@ __device__ __forceinline__ uint32_t tshash_find(TsHash h, int64_t ts) {
   }
 }
 
+// ---- ts -> first Add index, direct-addressed when counters are dense.
+// A timestamp is replicaId * 2^32 + counter (src/CRDTree.elm:137, :348-350),
+// and each replica's counters form a dense run, so when every Add ts is
+// non-negative and the per-replica counter ranges add up to O(n) the index is
+// a flat array: base[r] + (counter - cmin[r]). No hashing, no CAS, and ops of
+// one replica land in one contiguous run (cache-friendly). Otherwise the
+// open-addressing TsHash above serves.
+constexpr uint32_t RID_BITS = 21;  // ts < 2^53
+constexpr uint32_t RID_SLOTS = 1u << RID_BITS;
+
+struct TsIndex {
+  uint32_t dense;
+  TsHash h;
+  const uint32_t* cmin;  // [RID_SLOTS] per replica min counter (0xFFFFFFFF = no Add)
+  const uint32_t* cmax;  // [RID_SLOTS]
+  const uint32_t* base;  // [RID_SLOTS] exclusive scan of range sizes
+  uint32_t* first;       // [total range] min op index, 0xFFFFFFFF = none
+};
+
+__device__ __forceinline__ uint32_t tsindex_slot(const TsIndex& x, int64_t ts) {
+  if (ts <= 0) return NONE;
+  const uint64_t r = static_cast<uint64_t>(ts) >> 32;
+  if (r >= RID_SLOTS) return NONE;
+  const uint32_t c = static_cast<uint32_t>(ts);
+  const uint32_t lo = x.cmin[r];
+  if (lo == NONE || c < lo || c > x.cmax[r]) return NONE;
+  return x.base[r] + (c - lo);
+}
+
+__device__ __forceinline__ uint32_t tsindex_find(const TsIndex& x, int64_t ts) {
+  if (!x.dense) return tshash_find(x.h, ts);
+  const uint32_t p = tsindex_slot(x, ts);
+  return p == NONE ? NONE : x.first[p];
+}
+
+__device__ __forceinline__ void tsindex_insert(const TsIndex& x, int64_t ts, uint32_t idx) {
+  if (!x.dense) { tshash_insert(x.h, ts, idx); return; }
+  atomicMin(&x.first[tsindex_slot(x, ts)], idx);
+}
+
 // ---- (dict, key) -> slot hash used by the exact replay (single writer per entry).
 struct SlotHash {
   uint32_t* dict;

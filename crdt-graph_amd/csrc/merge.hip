@@ -18,6 +18,8 @@
 
 namespace crdtm {
 
+constexpr uint32_t REP_LDS_PRE_BITS = 9;
+constexpr uint32_t REP_LDS_PRE = 1u << REP_LDS_PRE_BITS;
 constexpr uint32_t SENT_T = 0xFFFFFFFDu;  // leaf target: the dict's sentinel (key 0)
 constexpr uint32_t MISS_T = 0xFFFFFFFCu;  // leaf target: key not in the dict
 
@@ -75,31 +77,117 @@ __device__ __forceinline__ uint32_t block_min(uint32_t v) {
 // the first Add of their timestamp; the root dict owner is ROOTN = n.
 // ---------------------------------------------------------------------------
 
-__global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, Work w, TsHash h, DevResult* dres) {
-  uint32_t mx = 0, bad = 0;
+__global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, Work w, uint32_t* cmin, uint32_t* cmax, DevResult* dres) {
+  // per-block (replica -> counter min/max) table; replicas are few, so one
+  // global atomic pair per (block, replica) instead of one per op
+  __shared__ uint32_t rk[REP_LDS_PRE];
+  __shared__ uint32_t rlo[REP_LDS_PRE];
+  __shared__ uint32_t rhi[REP_LDS_PRE];
+  for (uint32_t j = threadIdx.x; j < REP_LDS_PRE; j += blockDim.x) {
+    rk[j] = NONE;
+    rlo[j] = NONE;
+    rhi[j] = 0;
+  }
+  __syncthreads();
+  uint32_t mx = 0, bad = 0, neg = 0, ndel = 0;
   const uint32_t n = o.n;
-  // grid-stride with a uniform trip count so every lane reaches the block reductions
-  const uint32_t stride = gridDim.x * blockDim.x;
-  const uint32_t trips = (n + stride - 1) / stride;
-  for (uint32_t t = 0; t < trips; ++t) {
-    const uint32_t i = t * stride + blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) continue;
+  const uint32_t chunk = (n + gridDim.x - 1) / gridDim.x;
+  const uint32_t b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
+  for (uint32_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
     const uint32_t L = op_len(o, i);
     mx = max(mx, L);
     const bool add = o.kind[i] == CRDTM_ADD;
     const long long ts = add ? o.ts[i] : 0;
     if (ts >= TWO53 || ts <= -TWO53) bad = 1;
+    if (!add) ++ndel;
     w.st[i] = L == 0 ? ST_INVALID : ST_PENDING;
     w.cur[i] = n;
     w.addpar[i] = NONE;
     w.dtime[i] = NONE;
-    if (add && L >= 1 && ts != 0 && !bad) tshash_insert(h, ts, i);
+    if (add && L >= 1 && ts != 0) {
+      if (ts < 0) {
+        neg = 1;
+      } else if (ts < TWO53) {
+        const uint32_t r = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32), c = static_cast<uint32_t>(ts);
+        uint32_t p = (r * 0x9E3779B1u) >> (32 - REP_LDS_PRE_BITS);
+        bool done = false;
+        for (uint32_t probe = 0; probe < 16 && !done; ++probe, p = (p + 1) & (REP_LDS_PRE - 1)) {
+          const uint32_t prev = atomicCAS(&rk[p], NONE, r);
+          if (prev == NONE || prev == r) {
+            atomicMin(&rlo[p], c);
+            atomicMax(&rhi[p], c);
+            done = true;
+          }
+        }
+        if (!done) {
+          atomicMin(&cmin[r], c);
+          atomicMax(&cmax[r], c);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < REP_LDS_PRE; j += blockDim.x) {
+    if (rk[j] != NONE) {
+      atomicMin(&cmin[rk[j]], rlo[j]);
+      atomicMax(&cmax[rk[j]], rhi[j]);
+    }
   }
   mx = block_max(mx);
   bad = block_max(bad);
+  neg = block_max(neg);
+  ndel = block_sum(ndel);
   if (threadIdx.x == 0) {
     if (mx) atomicMax(&dres->max_len, mx);
     if (bad) atomicOr(&dres->bad_range, 1u);
+    if (neg) atomicOr(&dres->has_negative, 1u);
+    if (ndel) atomicAdd(&dres->n_del, ndel);
+  }
+}
+
+// range size per replica -> scan -> base (dense index layout)
+__global__ void __launch_bounds__(BLOCK) k_range_size(const uint32_t* cmin, const uint32_t* cmax, uint32_t* sz) {
+  GRID_STRIDE(r, RID_SLOTS) {
+    const uint32_t lo = cmin[r];
+    sz[r] = lo == NONE ? 0u : cmax[r] - lo + 1u;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_index_insert(OpsDev o, TsIndex x) {
+  GRID_STRIDE(i, o.n) {
+    if (o.kind[i] != CRDTM_ADD || op_len(o, i) == 0) continue;
+    const long long ts = o.ts[i];
+    if (ts != 0) tsindex_insert(x, ts, i);
+  }
+}
+
+// Fused K1 for the common single-level, Adds-only batch (a flat document):
+// status, dict owner and the effective-parent seed in one pass.
+__global__ void __launch_bounds__(BLOCK) k_flat_status(OpsDev o, Work w, TsIndex x, uint32_t* anc) {
+  const uint32_t n = o.n;
+  GRID_STRIDE(i, n) {
+    if (w.st[i] != ST_PENDING) continue;  // L == 0: InvalidPath
+    w.addpar[i] = n;                      // parent = the root
+    const long long ts = o.ts[i];
+    uint8_t s;
+    if (ts == 0 || tsindex_find(x, ts) != i) {
+      s = ST_ALREADY;  // key 0 is the sentinel / child ts parent exists
+    } else {
+      const long long k = o.path[o.off[i]];
+      uint32_t a;
+      if (k == 0) {
+        a = SENT_T;
+      } else {
+        const uint32_t f = tsindex_find(x, k);
+        a = (f != NONE && op_len(o, f) == 1) ? f : MISS_T;
+      }
+      s = (a == SENT_T || (a != MISS_T && a < i)) ? ST_APPLIED : ST_NOTFOUND;
+      if (s == ST_APPLIED) {
+        w.dead[i] = 0;
+        anc[i] = a == SENT_T ? 2 * n : a;
+      }
+    }
+    w.st[i] = s;
   }
 }
 
@@ -127,26 +215,26 @@ __global__ void __launch_bounds__(BLOCK) k_lvl_addpar(OpsDev o, Work w, uint32_t
 
 // The closed form names a node by its timestamp alone; the same ts added under
 // two different parents breaks that and routes the batch to the replay.
-__global__ void __launch_bounds__(BLOCK) k_lvl_collide(OpsDev o, Work w, TsHash h, uint32_t lvl, DevResult* dres) {
+__global__ void __launch_bounds__(BLOCK) k_lvl_collide(OpsDev o, Work w, TsIndex h, uint32_t lvl, DevResult* dres) {
   GRID_STRIDE(i, o.n) {
     if (o.kind[i] != CRDTM_ADD || op_len(o, i) != lvl || w.addpar[i] == NONE) continue;
     const long long ts = o.ts[i];
     if (ts == 0) continue;
-    const uint32_t f = tshash_find(h, ts);
+    const uint32_t f = tsindex_find(h, ts);
     if (f != i && (op_len(o, f) != lvl || w.addpar[f] != w.addpar[i])) atomicOr(&dres->guard, G_COLLISION);
   }
 }
 
-__device__ __forceinline__ uint32_t lookup_child(const OpsDev& o, const Work& w, const TsHash& h, uint32_t parent,
+__device__ __forceinline__ uint32_t lookup_child(const OpsDev& o, const Work& w, const TsIndex& h, uint32_t parent,
                                                  long long k, uint32_t lvl) {
   if (k == 0) return SENT_T;
-  const uint32_t f = tshash_find(h, k);
+  const uint32_t f = tsindex_find(h, k);
   if (f == NONE || op_len(o, f) != lvl || w.addpar[f] != parent) return MISS_T;
   return f;
 }
 
 // Resolve path element lvl (1-based) of every pending op.
-__global__ void __launch_bounds__(BLOCK) k_lvl_resolve(OpsDev o, Work w, TsHash h, uint32_t lvl) {
+__global__ void __launch_bounds__(BLOCK) k_lvl_resolve(OpsDev o, Work w, TsIndex h, uint32_t lvl) {
   GRID_STRIDE(i, o.n) {
     if (w.st[i] != ST_PENDING) continue;
     const uint32_t L = op_len(o, i);
@@ -176,7 +264,7 @@ __global__ void __launch_bounds__(BLOCK) k_lvl_del(OpsDev o, Work w, uint32_t lv
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_lvl_fin(OpsDev o, Work w, TsHash h, uint32_t lvl) {
+__global__ void __launch_bounds__(BLOCK) k_lvl_fin(OpsDev o, Work w, TsIndex h, uint32_t lvl) {
   const uint32_t n = o.n;
   GRID_STRIDE(i, n) {
     if (w.st[i] != ST_PENDING) continue;
@@ -192,7 +280,7 @@ __global__ void __launch_bounds__(BLOCK) k_lvl_fin(OpsDev o, Work w, TsHash h, u
         const long long ts = o.ts[i];
         uint8_t s;
         if (ts == 0) s = ST_ALREADY;                         // key 0 = the sentinel
-        else if (tshash_find(h, ts) != i) s = ST_ALREADY;    // child ts parent exists
+        else if (tsindex_find(h, ts) != i) s = ST_ALREADY;    // child ts parent exists
         else {
           const uint32_t a = w.leaf[i];
           s = (a == SENT_T || (a != MISS_T && a < i)) ? ST_APPLIED : ST_NOTFOUND;
@@ -1122,30 +1210,66 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   w.dtime = ws.alloc<uint32_t>(n);
   w.dead = ws.alloc<uint8_t>(n);
   w.maxadd = ws.alloc<uint32_t>(n + 1);
-  const uint32_t H = pow2_at_least(2 * static_cast<uint64_t>(n));
-  TsHash h;
-  h.keys = ws.alloc<unsigned long long>(H);
-  h.vals = ws.alloc<uint32_t>(H);
-  h.mask = H - 1;
+  uint32_t* anc = ws.alloc<uint32_t>(n);
+  uint32_t* cmin = ws.alloc<uint32_t>(RID_SLOTS);
+  uint32_t* cmax = ws.alloc<uint32_t>(RID_SLOTS);
+  uint32_t* rbase = ws.alloc<uint32_t>(RID_SLOTS + 1);
   DevResult* dr = c->dres;
   HIP_CHECK(hipMemsetAsync(dr, 0, sizeof(DevResult), s));
   HIP_CHECK(hipMemsetAsync(&dr->err_index, 0xFF, sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(h.keys, 0, H * sizeof(unsigned long long), s));
-  HIP_CHECK(hipMemsetAsync(h.vals, 0xFF, H * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(w.maxadd, 0, (n + 1) * sizeof(uint32_t), s));
-  LAUNCH(k_pre, dim3(grid_for(n, BLOCK, 4096)), dim3(BLOCK), 0, s, o, w, h, dr);
+  HIP_CHECK(hipMemsetAsync(cmin, 0xFF, RID_SLOTS * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(cmax, 0, RID_SLOTS * sizeof(uint32_t), s));
+  LAUNCH(k_pre, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, o, w, cmin, cmax, dr);
   LAUNCH(k_path_range, dim3(grid_for(o.n_path, BLOCK, 2048)), dim3(BLOCK), 0, s, o.path, o.n_path, dr);
+  LAUNCH(k_range_size, dim3(grid_for(RID_SLOTS)), dim3(BLOCK), 0, s, cmin, cmax, rbase);
   int r;
+  if ((r = scan_excl_u32(rbase, rbase, RID_SLOTS, &dr->range_total, ws, s))) return r;
   if ((r = sync_read(c))) return r;
   if (c->hres->bad_range) return CRDTM_E_RANGE;
   const uint32_t maxlen = c->hres->max_len;
+  if (t->max_depth < maxlen) t->max_depth = maxlen;
   const uint32_t g = grid_for(n);
-  for (uint32_t lvl = 1; lvl <= maxlen; ++lvl) {
-    LAUNCH(k_lvl_addpar, dim3(g), dim3(BLOCK), 0, s, o, w, lvl);
-    LAUNCH(k_lvl_collide, dim3(g), dim3(BLOCK), 0, s, o, w, h, lvl, dr);
-    LAUNCH(k_lvl_resolve, dim3(g), dim3(BLOCK), 0, s, o, w, h, lvl);
-    LAUNCH(k_lvl_del, dim3(g), dim3(BLOCK), 0, s, o, w, lvl);
-    LAUNCH(k_lvl_fin, dim3(g), dim3(BLOCK), 0, s, o, w, h, lvl);
+  if (t->n_slots != 1 || t->log_n != 0) {
+    // incremental merge into existing state: exact replay
+    r = run_replay(t, o, w.st, res, G_NOT_FRESH);
+    if (r == CRDTM_OK && st_out)
+      LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n,
+             res->err_index >= 0 ? static_cast<uint32_t>(res->err_index) : NONE, st_out);
+    return r;
+  }
+  // ts index: dense per-replica runs when possible, else an open-addressing hash
+  TsIndex ix;
+  ix.cmin = cmin;
+  ix.cmax = cmax;
+  ix.base = rbase;
+  const uint64_t range_total = c->hres->range_total;
+  ix.dense = (!c->hres->has_negative && range_total <= 4ULL * n + 65536) ? 1u : 0u;
+  if (ix.dense) {
+    ix.first = ws.alloc<uint32_t>(range_total + 1);
+    ix.h = TsHash{nullptr, nullptr, 0};
+    HIP_CHECK(hipMemsetAsync(ix.first, 0xFF, (range_total + 1) * sizeof(uint32_t), s));
+  } else {
+    const uint32_t H = pow2_at_least(2 * static_cast<uint64_t>(n));
+    ix.first = nullptr;
+    ix.h.keys = ws.alloc<unsigned long long>(H);
+    ix.h.vals = ws.alloc<uint32_t>(H);
+    ix.h.mask = H - 1;
+    HIP_CHECK(hipMemsetAsync(ix.h.keys, 0, H * sizeof(unsigned long long), s));
+    HIP_CHECK(hipMemsetAsync(ix.h.vals, 0xFF, H * sizeof(uint32_t), s));
+  }
+  LAUNCH(k_index_insert, dim3(g), dim3(BLOCK), 0, s, o, ix);
+  const bool flat = maxlen == 1 && c->hres->n_del == 0;
+  if (flat) {
+    LAUNCH(k_flat_status, dim3(g), dim3(BLOCK), 0, s, o, w, ix, anc);
+  } else {
+    HIP_CHECK(hipMemsetAsync(w.maxadd, 0, (n + 1) * sizeof(uint32_t), s));
+    for (uint32_t lvl = 1; lvl <= maxlen; ++lvl) {
+      LAUNCH(k_lvl_addpar, dim3(g), dim3(BLOCK), 0, s, o, w, lvl);
+      LAUNCH(k_lvl_collide, dim3(g), dim3(BLOCK), 0, s, o, w, ix, lvl, dr);
+      LAUNCH(k_lvl_resolve, dim3(g), dim3(BLOCK), 0, s, o, w, ix, lvl);
+      LAUNCH(k_lvl_del, dim3(g), dim3(BLOCK), 0, s, o, w, lvl);
+      LAUNCH(k_lvl_fin, dim3(g), dim3(BLOCK), 0, s, o, w, ix, lvl);
+    }
   }
   HIP_CHECK(hipMemsetAsync(&dr->first_del, 0xFF, sizeof(uint32_t), s));
   LAUNCH(k_stats, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, o, w, t->timestamp, dr);
@@ -1157,12 +1281,10 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   }
   DevResult h1 = *c->hres;
   uint32_t guard = h1.guard;
-  if (t->n_slots != 1 || t->log_n != 0) guard |= G_NOT_FRESH;
   const long long id0 = replica_of(t->timestamp);
   const long long new_ts = t->timestamp + h1.own_ok_adds;
   if (replica_of(new_ts) != id0) guard |= G_REPLICA_DRIFT;
   res->guard = guard;
-  if (t->max_depth < maxlen) t->max_depth = maxlen;
   if (guard) {
     // exact sequential replay decides statuses (and errors) itself
     r = run_replay(t, o, w.st, res, guard);
@@ -1186,7 +1308,6 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
 
   // ---- K2: effective parents, unified tree, sibling sort ----
   const uint32_t U = 2 * n + 2;
-  uint32_t* anc = ws.alloc<uint32_t>(n);
   uint8_t* sp = ws.alloc<uint8_t>(n + 1);
   uint32_t* cnt = ws.alloc<uint32_t>(U + 1);
   uint32_t* fill = ws.alloc<uint32_t>(U + 1);
@@ -1199,7 +1320,7 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   HIP_CHECK(hipMemsetAsync(fill, 0, (U + 1) * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(fc, 0xFF, U * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(ns, 0xFF, U * sizeof(uint32_t), s));
-  LAUNCH(k_ep_init, dim3(g), dim3(BLOCK), 0, s, o, w, anc);
+  if (!flat) LAUNCH(k_ep_init, dim3(g), dim3(BLOCK), 0, s, o, w, anc);
   LAUNCH(k_ep_jump, dim3(g), dim3(BLOCK), 0, s, o, w, anc, sp);
   const uint32_t gU = grid_for(U);
   LAUNCH(k_up_count, dim3(grid_for(U, BLOCK, 2048)), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, skey);
