@@ -3,6 +3,4 @@
 extern "C" {
 int crdtm_forest_apply(crdtm_ctx*, int64_t, const crdtm_ops*, const uint32_t*, uint64_t, int, int32_t*, int64_t*,
                        uint32_t*, uint64_t*) { return CRDTM_E_ARG; }
-int crdtm_json_decode(const char*, size_t, crdtm_ops**, char**, uint64_t**, uint64_t*, int*) { return CRDTM_E_ARG; }
-int crdtm_json_encode(const crdtm_ops*, int, const char*, const uint64_t*, char**, size_t*) { return CRDTM_E_ARG; }
 }

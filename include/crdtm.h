@@ -165,6 +165,9 @@ int crdtm_json_decode(const char *json, size_t len, crdtm_ops **ops, char **val_
  * to `Encode.encode 0 (encoder valueEncoder op)`; values from the value table. */
 int crdtm_json_encode(const crdtm_ops *ops, int is_batch, const char *val_bytes, const uint64_t *val_off,
                       char **out, size_t *out_len);
+/* JSON.stringify(JSON.parse(text)) for one value: the canonical text the
+ * decoder stores in the value table (Decode.value / Encode.value round trip). */
+int crdtm_json_canonical(const char *text, size_t len, char **out, size_t *out_len);
 void crdtm_free(void *p);
 
 /* ---- profiling: per-kernel device time of the last apply (HIP events) ---- */

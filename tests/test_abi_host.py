@@ -1,0 +1,85 @@
+"""CPU-only checks of the C ABI library and host logic (no compute calls)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from crdtm import _native as N
+from oracle.oracle import _ptr, lib as olib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "crdtm.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(crdtm_\w+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_function():
+    L = N.lib()
+    names = header_functions()
+    assert len(names) >= 20
+    bound = {s[0] for s in N.SIGNATURES}
+    for name in names:
+        assert hasattr(L, name), f"{name} not exported by libcrdtm.so"
+        assert name in bound, f"{name} has no ctypes signature in crdtm/_native.py"
+
+
+def test_library_is_a_gfx950_code_object():
+    so = open(N.LIB_PATH, "rb").read()
+    assert b"gfx950" in so, "libcrdtm.so must embed gfx950 device code"
+
+
+def test_version_and_no_cpu_fallback():
+    L = N.lib()
+    assert L.crdtm_version() == 1
+    n = C.c_int(-1)
+    rc = L.crdtm_device_count(C.byref(n))
+    if rc != 0 or n.value == 0:  # CPU container: context creation must refuse, not fall back
+        h = C.c_void_p()
+        assert L.crdtm_ctx_create(0, None, C.byref(h)) == -5  # CRDTM_E_NODEVICE
+
+
+def test_synth_is_deterministic():
+    a = N.synth(n_ops=5000, replicas=8, window=16, p_delete=0.2, p_branch=0.1, max_depth=3, seed=42)
+    b = N.synth(n_ops=5000, replicas=8, window=16, p_delete=0.2, p_branch=0.1, max_depth=3, seed=42)
+    c = N.synth(n_ops=5000, replicas=8, window=16, p_delete=0.2, p_branch=0.1, max_depth=3, seed=43)
+    for k in ("kind", "ts", "path_off", "path", "val"):
+        assert np.array_equal(a[k], b[k])
+    assert not np.array_equal(a["ts"], c["ts"])
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(n_ops=10000, replicas=2, window=8, p_delete=0.3, p_branch=0.05, max_depth=3, seed=0xC0FFEE01),
+    dict(n_ops=20000, replicas=16, window=64, p_delete=0.2, p_branch=0.1, max_depth=4, seed=0xC0FFEE02),
+    dict(n_ops=20000, replicas=64, window=256, seed=0xC0FFEE03),
+    dict(n_ops=30000, replicas=16, p_delete=1 / 3, max_depth=12, max_children=8, deletes_last=1, seed=0xC0FFEE04),
+])
+def test_synth_streams_apply_cleanly_on_the_oracle(cfg):
+    """The generator only references earlier nodes, so `apply (Batch ops)` succeeds."""
+    s = N.synth(**cfg)
+    n = len(s["kind"])
+    L = olib()
+    t = L.orc_init(0)
+    err = C.c_int64(-1)
+    rc = L.orc_apply(t, 1, 0, n, _ptr(s["kind"]), _ptr(s["ts"]), _ptr(s["path_off"]), _ptr(s["path"]),
+                     _ptr(s["val"]), C.byref(err))
+    L.orc_free(t)
+    assert rc == 0, (rc, err.value)
+    L_ = np.diff(s["path_off"].astype(np.int64))
+    assert L_.min() >= 1 and L_.max() <= cfg.get("max_depth", 1)
+    frac_del = np.mean(s["kind"] == 1)
+    assert abs(frac_del - cfg.get("p_delete", 0.0)) < 0.1
+    if cfg.get("deletes_last"):
+        first_del = np.argmax(s["kind"] == 1)
+        assert np.all(s["kind"][first_del:] == 1)
+
+
+def test_synth_forest_shape():
+    s = N.synth(n_ops=1000, n_docs=7, replicas=8, window=16, p_delete=0.2, seed=5)
+    assert len(s["kind"]) == 7000
+    assert np.array_equal(np.unique(s["tree"]), np.arange(7))
+    assert np.all(np.diff(s["tree"].astype(np.int64)) >= 0)
