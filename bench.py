@@ -36,7 +36,10 @@ WORKLOADS = {
     "deep10m": dict(n_ops=10_000_000, replicas=16, p_delete=1 / 3, max_depth=12, max_children=8, deletes_last=1,
                     seed=0xC0FFEE04),
 }
-CPU_SAMPLE = {"flat10m": 150_000, "deep10m": 2_000_000}
+CPU_SAMPLE = {"flat10m": 150_000, "deep10m": 2_000_000, "trees": 2_000_000}
+# 100k documents x 1k ops (80/20), 8 replicas, sharded by
+# document id; 12.5k documents per GPU (100k at 8 GPUs), weak scaling.
+TREES = dict(per_doc=1000, docs_per_gpu=12_500, replicas=8, window=16, p_delete=0.2, seed=0xC0FFEE05)
 
 
 def alg_bytes(s):
@@ -73,7 +76,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="flat10m", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="flat10m", choices=sorted(WORKLOADS) + ["trees"])
+    ap.add_argument("--docs-per-gpu", type=int, default=0, help="trees workload: override documents per GPU")
     ap.add_argument("--n-ops", type=int, default=0, help="override the batch size (parity/debug only)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="oracle sample ops (0 = skip)")
     ap.add_argument("--profile-steps", type=int, default=3)
@@ -90,8 +94,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     from crdtm import _native as N
-    from crdtm.tree import _ptr
     L = N.lib()
+    if args.workload == "trees":
+        return run_trees(args, rank, world, local_rank)
 
     spec = dict(WORKLOADS[args.workload])
     if args.n_ops:
@@ -201,6 +206,132 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     L.crdtm_tree_destroy(tree)
+    L.crdtm_ctx_destroy(ctx)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_trees(args, rank, world, local_rank):
+    """Config 5: all-gather of the simulated replicas' op logs (RCCL), then every
+    rank merges the documents it owns (document t -> rank t mod world)."""
+    import torch
+    import torch.distributed as dist
+    from crdtm import _native as N
+    from crdtm import shard
+    L = N.lib()
+    per = TREES["per_doc"]
+    dpg = args.docs_per_gpu or TREES["docs_per_gpu"]
+    n_docs = dpg * world
+    dev = torch.device("cuda", local_rank)
+    # this rank's replicas' op logs for every document (generated in chunks)
+    logs = []
+    chunk = 2000
+    for d0 in range(0, n_docs, chunk):
+        nd = min(chunk, n_docs - d0)
+        s = N.synth(n_ops=per, n_docs=nd, replicas=TREES["replicas"], window=TREES["window"],
+                    p_delete=TREES["p_delete"], seed=TREES["seed"], doc_base=d0)
+        doc_off = np.arange(nd + 1, dtype=np.uint32) * per
+        rec = shard.local_log(s, doc_off, rank, world, TREES["replicas"])
+        rec[:, 0] += (np.int64(d0) << 32)  # global document id
+        logs.append(rec)
+    local = torch.from_numpy(np.concatenate(logs)).to(dev)
+    del logs
+    ctx = C.c_void_p()
+    stream = torch.cuda.current_stream()
+    N.check(L.crdtm_ctx_create(local_rank, C.c_void_p(stream.cuda_stream), C.byref(ctx)), "ctx")
+    n_mine = (n_docs - rank + world - 1) // world
+    code = np.zeros(n_mine, np.int32)
+    applied = np.zeros(n_mine, np.uint32)
+    state = {}
+
+    def step():
+        allrec = shard.all_gather_records(local)
+        ops_t, doc_off, _ = shard.assemble(allrec, rank, world, n_docs, per)
+        n = int(doc_off[-1])
+        ops = N.Ops(n, n, ops_t["kind"].data_ptr(), ops_t["ts"].data_ptr(), ops_t["path_off"].data_ptr(),
+                    ops_t["path"].data_ptr(), ops_t["val"].data_ptr(), None)
+        rc = L.crdtm_forest_apply(ctx, 0, C.byref(ops), doc_off.ctypes.data_as(C.c_void_p), n_mine, 1,
+                                  code.ctypes.data_as(C.c_void_p), None, applied.ctypes.data_as(C.c_void_p),
+                                  None, None, None)
+        N.check(rc, "forest")
+        state["ops_t"] = ops_t
+        state["n"] = n
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    n = state["n"]
+    ok_docs = int(np.sum(code == 0))
+    # dominant kernel time (HIP events on the launch stream)
+    L.crdtm_ctx_profile(ctx, 1)
+    step()
+    names = C.create_string_buffer(1 << 14)
+    ms = (C.c_double * 64)()
+    k = L.crdtm_ctx_phase_times(ctx, names, len(names), ms, 64)
+    labels = names.raw.split(b"\0")
+    L.crdtm_ctx_profile(ctx, 0)
+    per_k = {labels[j].decode(): ms[j] for j in range(min(k, 64))}
+    dominant = max(per_k, key=per_k.get)
+    ot = state["ops_t"]
+    kinds = ot["kind"].cpu().numpy()
+    B_alg = int(np.sum(np.where(kinds == 0, 57, 17)))  # flat documents: L = 1
+    t_dom = per_k[dominant] / 1e3
+    ms_step = elapsed / args.steps * 1e3
+    line = {
+        "metric": "merged ops/sec (whole node) on 10M-op batch",
+        "value": world * n * args.steps / elapsed, "unit": "ops/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int64", "data": "synthetic (deterministic generator, SURVEY.md §8d)",
+        "config": {"workload": f"trees: {n_mine} documents x {per} ops per GPU ({n} ops), {n_docs} documents total",
+                   "replicas": TREES["replicas"], "documents_ok": ok_docs,
+                   "parallelism": f"documents sharded by id over {world} GPU(s); op logs all-gathered (RCCL)"},
+        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": B_alg / t_dom / 1e9, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": B_alg / t_dom / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "alg_bytes_per_launch": B_alg, "kernel_ms": t_dom * 1e3,
+                     "merge_frac": B_alg / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS},
+    }
+    if args.verbose and rank == 0:
+        for nm, v in sorted(per_k.items(), key=lambda kv: -kv[1])[:12]:
+            print(f"  {nm:28s} {v:9.3f} ms", file=sys.stderr)
+    if rank == 0 and world == 1:
+        m = args.cpu_sample if args.cpu_sample >= 0 else CPU_SAMPLE["trees"]
+        if m > 0:
+            from oracle.oracle import lib as olib, _ptr
+            Lo = olib()
+            host = {k: v.cpu().numpy() for k, v in ot.items()}
+            host["val"] = host["val"].astype(np.uint32)
+            host["path_off"] = host["path_off"].astype(np.uint32)
+            ndoc = max(1, min(n_mine, m // per))
+            t0 = time.perf_counter()
+            for d in range(ndoc):
+                a, b = d * per, (d + 1) * per
+                sub = dict(kind=host["kind"][a:b].copy(), ts=host["ts"][a:b].copy(), val=host["val"][a:b].copy(),
+                           path_off=np.arange(per + 1, dtype=np.uint32), path=host["path"][a:b].copy())
+                t = Lo.orc_init(0)
+                err = C.c_int64(-1)
+                Lo.orc_apply(t, 1, 0, per, _ptr(sub["kind"]), _ptr(sub["ts"]), _ptr(sub["path_off"]),
+                             _ptr(sub["path"]), _ptr(sub["val"]), C.byref(err))
+                Lo.orc_free(t)
+            dt = time.perf_counter() - t0
+            line["cpu_baseline"] = {"value": ndoc * per / dt, "unit": "ops/s", "cores": 1, "kind": "port",
+                                    "sample": f"{ndoc} documents x {per} ops, oracle/ C++ restatement, {dt:.1f} s"}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     L.crdtm_ctx_destroy(ctx)
     if world > 1:
         dist.destroy_process_group()

@@ -34,7 +34,7 @@ class SynthParams(C.Structure):
     _fields_ = [("n_ops", C.c_uint64), ("n_docs", C.c_uint64), ("replicas", C.c_uint32), ("window", C.c_uint32),
                 ("p_delete", C.c_double), ("p_branch", C.c_double), ("p_continue", C.c_double),
                 ("max_depth", C.c_uint32), ("max_children", C.c_uint32), ("deletes_last", C.c_uint32),
-                ("seed", C.c_uint64)]
+                ("seed", C.c_uint64), ("doc_base", C.c_uint64)]
 
 
 # every function the header declares: (name, restype, argtypes)
@@ -56,8 +56,7 @@ SIGNATURES = [
     ("crdtm_tree_ops", C.c_int, [P, C.c_int, C.POINTER(Ops), C.POINTER(C.c_int)]),
     ("crdtm_tree_canonical", C.c_int, [P, C.c_int, P, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("crdtm_tree_document", C.c_int, [P, P, C.c_uint64, C.POINTER(C.c_uint64)]),
-    ("crdtm_forest_apply", C.c_int, [P, C.c_int64, C.POINTER(Ops), P, C.c_uint64, C.c_int, P, P, P,
-                                     C.POINTER(C.c_uint64)]),
+    ("crdtm_forest_apply", C.c_int, [P, C.c_int64, C.POINTER(Ops), P, C.c_uint64, C.c_int, P, P, P, P, P, P]),
     ("crdtm_synth", C.c_int, [C.POINTER(SynthParams), C.POINTER(C.POINTER(Ops))]),
     ("crdtm_ops_free", C.c_int, [C.POINTER(Ops)]),
     ("crdtm_json_decode", C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.POINTER(Ops)), C.POINTER(C.c_void_p),
@@ -116,11 +115,11 @@ def context(device=0):
 
 
 def synth(n_ops, n_docs=1, replicas=2, window=8, p_delete=0.0, p_branch=0.0, p_continue=0.9, max_depth=1,
-          max_children=0, deletes_last=0, seed=1):
+          max_children=0, deletes_last=0, seed=1, doc_base=0):
     """Generate a synthetic op stream (host numpy arrays, copied out of the engine)."""
     import numpy as np
     p = SynthParams(n_ops, n_docs, replicas, window, p_delete, p_branch, p_continue, max_depth, max_children,
-                    deletes_last, seed)
+                    deletes_last, seed, doc_base)
     out = C.POINTER(Ops)()
     check(lib().crdtm_synth(C.byref(p), C.byref(out)), "crdtm_synth")
     o = out.contents

@@ -1,0 +1,105 @@
+"""Multi-GPU sharding of many independent documents.
+
+One process per GPU. Every rank hosts some of the R simulated replicas and
+holds, for every document, the ops those replicas authored (their op logs).
+A step is: all-gather the op logs (RCCL over xGMI with backend "nccl"; gloo
+in CPU tests), keep the documents this rank owns (document t -> rank
+t mod world), put each document's ops back in causal order, and merge every
+owned document with `crdtm_forest_apply`. There is no second exchange: the
+documents are independent CRDTrees.
+
+Op record (4 x int64, flat documents): [doc << 32 | seq, kind << 32 | val, ts, anchor]
+where seq is the op's position in its document's causal stream.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REC_W = 4
+
+
+def owner(doc, world):
+    return doc % world
+
+
+def hosted_replicas(rank, world, replicas):
+    """Replica ids 1..R hosted by `rank` (round-robin)."""
+    return [r for r in range(1, replicas + 1) if (r - 1) % world == rank]
+
+
+def pack_records(s, doc_off, mask):
+    """Host op arrays (flat documents) -> records of the ops selected by mask."""
+    n = len(s["kind"])
+    doc = np.repeat(np.arange(len(doc_off) - 1, dtype=np.int64), np.diff(doc_off.astype(np.int64)))
+    seq = np.arange(n, dtype=np.int64) - doc_off.astype(np.int64)[doc]
+    rec = np.empty((n, REC_W), np.int64)
+    rec[:, 0] = (doc << 32) | seq
+    rec[:, 1] = (s["kind"].astype(np.int64) << 32) | s["val"].astype(np.int64)
+    rec[:, 2] = s["ts"]
+    rec[:, 3] = s["path"][s["path_off"][:-1].astype(np.int64)]
+    return rec[mask]
+
+
+def local_log(s, doc_off, rank, world, replicas):
+    """This rank's share of every document's stream: the ops its replicas authored.
+    Deletes carry no timestamp; they are attributed to the replica of the node
+    they delete (its key's replica id), which spreads them over the ranks."""
+    key = np.where(s["kind"] == 0, s["ts"], s["path"][s["path_off"][:-1].astype(np.int64)])
+    rid = key >> 32
+    mine = np.isin(rid, hosted_replicas(rank, world, replicas))
+    if rank == 0:
+        mine |= (rid < 1) | (rid > replicas)  # anything unattributed stays with rank 0
+    return pack_records(s, doc_off, mine)
+
+
+def all_gather_records(local: torch.Tensor, group=None) -> torch.Tensor:
+    """All-gather variable-length record blocks: counts first, then padded blocks."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return local
+    world = dist.get_world_size(group)
+    if world == 1:
+        return local
+    cnt = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
+    cnts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt, group=group)
+    cnts = [int(c.item()) for c in cnts]
+    m = max(cnts)
+    pad = torch.zeros((m, REC_W), dtype=torch.int64, device=local.device)
+    pad[:local.shape[0]] = local
+    if local.device.type == "cuda":
+        out = torch.empty((world * m, REC_W), dtype=torch.int64, device=local.device)
+        dist.all_gather_into_tensor(out, pad, group=group)
+        parts = [out[k * m:k * m + cnts[k]] for k in range(world)]
+    else:
+        bufs = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(bufs, pad, group=group)
+        parts = [bufs[k][:cnts[k]] for k in range(world)]
+    return torch.cat(parts, 0)
+
+
+def assemble(records: torch.Tensor, rank, world, n_docs, per_doc):
+    """Records of every replica -> SoA ops of this rank's documents in causal order.
+    Documents owned: t = rank, rank + world, ... (local index t // world);
+    every document holds exactly per_doc ops."""
+    doc = records[:, 0] >> 32
+    keep = (doc % world) == rank
+    r = records[keep]
+    doc = r[:, 0] >> 32
+    seq = r[:, 0] & 0xFFFFFFFF
+    n_mine = (n_docs - rank + world - 1) // world
+    dst = (doc // world) * per_doc + seq
+    n = n_mine * per_doc
+    dev = records.device
+    kind = torch.zeros(n, dtype=torch.uint8, device=dev)
+    val = torch.zeros(n, dtype=torch.int32, device=dev)
+    ts = torch.zeros(n, dtype=torch.int64, device=dev)
+    path = torch.zeros(n, dtype=torch.int64, device=dev)
+    kind[dst] = (r[:, 1] >> 32).to(torch.uint8)
+    val[dst] = (r[:, 1] & 0xFFFFFFFF).to(torch.int32)
+    ts[dst] = r[:, 2]
+    path[dst] = r[:, 3]
+    path_off = torch.arange(n + 1, dtype=torch.int32, device=dev)
+    doc_off = np.arange(n_mine + 1, dtype=np.uint32) * per_doc
+    return dict(kind=kind, ts=ts, path_off=path_off, path=path, val=val), doc_off, int(keep.sum().item())

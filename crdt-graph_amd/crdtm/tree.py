@@ -322,3 +322,20 @@ def init(replica_id_: int, device: int = 0) -> CRDTree:
 
 
 __all__ = ["CRDTree", "init", "Ok", "Err", "InvalidPath", "NotFound", "OperationFailed", "TWO32"]
+
+
+def forest_apply(arrs, doc_off, replica_id=0, device=0, on_device=False):
+    """crdtm_forest_apply: every document fresh, `apply (Batch ops_d)` each.
+    Returns dict of per-document numpy arrays (code, err, applied, hash, words, timestamp)."""
+    n_docs = len(doc_off) - 1
+    ctx = N.context(device)
+    doc_off = np.ascontiguousarray(doc_off, dtype=np.uint32)
+    out = dict(code=np.zeros(n_docs, np.int32), err=np.zeros(n_docs, np.int64), applied=np.zeros(n_docs, np.uint32),
+               hash=np.zeros(n_docs, np.uint64), words=np.zeros(n_docs, np.uint64),
+               timestamp=np.zeros(n_docs, np.int64))
+    ops = arrs if isinstance(arrs, N.Ops) else ops_struct(arrs, int(doc_off[-1]))
+    rc = N.lib().crdtm_forest_apply(ctx, int(replica_id), C.byref(ops), _ptr(doc_off), n_docs, 1 if on_device else 0,
+                                    _ptr(out["code"]), _ptr(out["err"]), _ptr(out["applied"]), _ptr(out["hash"]),
+                                    _ptr(out["words"]), _ptr(out["timestamp"]))
+    out["rc"] = rc
+    return out

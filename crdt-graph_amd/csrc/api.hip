@@ -492,6 +492,70 @@ int crdtm_ctx_phase_times(crdtm_ctx* c, char* names, size_t names_cap, double* m
   return k;
 }
 
+int crdtm_forest_apply(crdtm_ctx* c, int64_t replica_id, const crdtm_ops* ops, const uint32_t* doc_off,
+                       uint64_t n_docs, int on_device, int32_t* doc_code, int64_t* doc_err, uint32_t* doc_applied,
+                       uint64_t* doc_hash, uint64_t* doc_words, int64_t* doc_timestamp) {
+  if (!c || !ops || !doc_off || !doc_code) return CRDTM_E_ARG;
+  HIP_CHECK(hipSetDevice(c->device));
+  const uint64_t n = ops->n_ops;
+  if (doc_off[n_docs] != n || n >= 0x7FFFFFF0ULL) return CRDTM_E_ARG;
+  uint64_t np = ops->n_path;
+  if (!on_device && n) np = ops->path_off[n];
+  int r = ensure_arena(c, forest_ws_bytes(doc_off, n_docs, n, np));
+  if (r) return r;
+  c->ws.reset();
+  for (auto& m : c->marks) hipEventDestroy(m.second);
+  c->marks.clear();
+  try {
+    OpsDev o;
+    o.n = static_cast<uint32_t>(n);
+    o.n_path = np;
+    if (on_device) {
+      o.kind = ops->kind;
+      o.ts = reinterpret_cast<const long long*>(ops->ts);
+      o.off = ops->path_off;
+      o.path = reinterpret_cast<const long long*>(ops->path);
+      o.val = ops->val;
+    } else {
+      hipStream_t s = c->stream;
+      auto* kind = c->ws.alloc<uint8_t>(n + 1);
+      auto* ts = c->ws.alloc<long long>(n + 1);
+      auto* off = c->ws.alloc<uint32_t>(n + 1);
+      auto* path = c->ws.alloc<long long>(np + 1);
+      auto* val = c->ws.alloc<uint32_t>(n + 1);
+      if (n) {
+        HIP_CHECK(hipMemcpyAsync(kind, ops->kind, n, hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipMemcpyAsync(ts, ops->ts, n * 8, hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipMemcpyAsync(off, ops->path_off, (n + 1) * 4, hipMemcpyHostToDevice, s));
+        if (np) HIP_CHECK(hipMemcpyAsync(path, ops->path, np * 8, hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipMemcpyAsync(val, ops->val, n * 4, hipMemcpyHostToDevice, s));
+      }
+      o.kind = kind;
+      o.ts = ts;
+      o.off = off;
+      o.path = path;
+      o.val = val;
+    }
+    g_prof = c->profile ? c : nullptr;
+    mark(c, "start");
+    r = forest_apply(c, replica_id, o, doc_off, n_docs, doc_code, doc_err, doc_applied, doc_hash, doc_words,
+                     doc_timestamp);
+    g_prof = nullptr;
+  } catch (const ArenaOverflow&) {
+    return CRDTM_E_NOMEM;
+  }
+  if (c->profile) {
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    c->phases.clear();
+    for (size_t k = 1; k < c->marks.size(); ++k) {
+      float ms = 0;
+      hipEventElapsedTime(&ms, c->marks[k - 1].second, c->marks[k].second);
+      c->phases.emplace_back(c->marks[k].first, ms);
+    }
+  }
+  return r;
+}
+
 void crdtm_free(void* p) { std::free(p); }
 
 }  // extern "C"

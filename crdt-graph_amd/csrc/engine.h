@@ -116,6 +116,9 @@ struct OpsDev {
 int grow_tree(crdtm_tree* t, const TreeCaps& need);
 int apply_batch(crdtm_tree* t, const OpsDev& ops, uint8_t* status_dev, crdtm_result* res);
 int linearize(crdtm_tree* t);  // fills t->d.doc / t->doc_n from the tree state
+int forest_apply(crdtm_ctx* c, int64_t replica_id, const OpsDev& o, const uint32_t* doc_off_host, uint64_t n_docs,
+                 int32_t* code, int64_t* err, uint32_t* applied, uint64_t* vhash, uint64_t* vwords, int64_t* tstamp);
+uint64_t forest_ws_bytes(const uint32_t* doc_off_host, uint64_t n_docs, uint64_t n_ops, uint64_t n_path);
 void mark(crdtm_ctx* c, const char* name);
 // Profiling hook: when the current context profiles, every launch records a
 // HIP event on the launch stream so each kernel's device time is measurable.

@@ -712,6 +712,8 @@ struct ReplayArgs {
   uint32_t hash_limit;
   uint32_t log_base;
   long long ts0;
+  uint32_t root_dict;   // 0 for a tree state; a document's own root dict in a forest
+  uint32_t src_is_op;   // forest: s_src = global op index (no log is kept)
 };
 
 enum : uint32_t { UF_NEXT = 0, UF_SRC = 1, UF_CHILD = 2, UF_FLAGS = 3 };
@@ -809,7 +811,7 @@ struct Replayer {
   __device__ uint8_t op(const OpsDev& o, uint32_t i, uint32_t applied) {
     const uint32_t b = o.off[i], L = o.off[i + 1] - b;
     if (L == 0) return ST_INVALID;
-    uint32_t d = 0;
+    uint32_t d = a.root_dict;
     for (uint32_t l = 0; l + 1 < L; ++l) {  // update: descend
       const uint32_t s = slothash_find(a.H, d, o.path[b + l]);
       if (s == NONE) return ST_INVALID;
@@ -842,7 +844,7 @@ struct Replayer {
       nkey = rk;
       node = live;
     }
-    const uint32_t x = new_slot(d, ts, a.T.s_next[node], a.log_base + applied, NONE, 0);
+    const uint32_t x = new_slot(d, ts, a.T.s_next[node], a.src_is_op ? i : a.log_base + applied, NONE, 0);
     if (x == NONE) return ST_PENDING;
     const uint32_t dd = new_dict(x);
     if (dd == NONE) return ST_PENDING;
@@ -983,6 +985,141 @@ __global__ void __launch_bounds__(BLOCK) k_lin_doc(TreeDev T, uint32_t S, const 
     if (f & (F_TOMB | F_ORPHAN)) continue;
     if (e < cap) doc[static_cast<uint32_t>(e)] = s;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Forest: many independent documents, each replayed
+// exactly by one lane (documents are the parallel axis; cfg-5 streams
+// interleave Deletes with concurrent inserts, where the closed form's guard
+// rarely holds). Each lane owns a region of the slot/dict/hash arenas sized
+// from its op count, and ends by hashing its visible document with the same
+// canonical words as the oracle (FNV-1a over depth, value, path).
+// ---------------------------------------------------------------------------
+struct ForestArgs {
+  TreeDev T;               // shared slot/dict arrays (per-document regions)
+  const uint32_t* doc_off; // [n_docs + 1] ops of document d = [doc_off[d], doc_off[d+1])
+  uint32_t n_docs;
+  long long ts0;
+  uint32_t* dhead;
+  uint32_t* mnext;
+  uint32_t* hdict;
+  long long* hkey;
+  uint32_t* hslot;
+  uint32_t* queue;
+  int32_t* code;
+  uint32_t* err;
+  uint32_t* applied;
+  unsigned long long* vhash;
+  unsigned long long* vwords;
+  long long* tstamp;
+  uint32_t* overflow;
+};
+
+__host__ __device__ __forceinline__ uint64_t forest_slot_cap(uint32_t nops) { return 2ULL * nops + 64; }
+__host__ __device__ __forceinline__ uint64_t forest_dict_cap(uint32_t nops) { return nops + 32; }
+__host__ __device__ __forceinline__ uint32_t forest_hash_cap(uint32_t nops) {
+  uint32_t h = 64;
+  while (h < 2 * forest_slot_cap(nops)) h <<= 1;
+  return h;
+}
+
+struct Fnv {
+  unsigned long long h = 1469598103934665603ULL, n = 0;
+  __device__ void put(long long w) {
+    const unsigned long long u = static_cast<unsigned long long>(w);
+    for (int k = 0; k < 8; ++k) {
+      h ^= (u >> (8 * k)) & 0xff;
+      h *= 1099511628211ULL;
+    }
+    ++n;
+  }
+};
+
+__global__ void __launch_bounds__(64) k_forest(OpsDev o, ForestArgs f, const uint64_t* sbase, const uint64_t* dbase,
+                                               const uint64_t* hbase) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= f.n_docs) return;
+  const uint32_t ob = f.doc_off[d], oe = f.doc_off[d + 1], nops = oe - ob;
+  const uint32_t s0 = static_cast<uint32_t>(sbase[d]), d0 = static_cast<uint32_t>(dbase[d]);
+  const uint32_t H = forest_hash_cap(nops);
+  // fresh document: root dict d0 with its sentinel slot s0
+  Replayer r;
+  r.a.T = f.T;
+  r.a.H.dict = f.hdict + hbase[d];
+  r.a.H.key = f.hkey + hbase[d];
+  r.a.H.slot = f.hslot + hbase[d];
+  r.a.H.mask = H - 1;
+  r.a.dhead = f.dhead;
+  r.a.mnext = f.mnext;
+  r.a.undo = nullptr;
+  r.a.undo_cap = 0;
+  r.a.queue = f.queue + 2 * dbase[d];
+  r.a.queue_cap = static_cast<uint32_t>(forest_dict_cap(nops));
+  r.a.committed_slots = s0;  // nothing to undo: every slot of the document is new
+  r.a.n_slots = s0;
+  r.a.n_dicts = d0;
+  r.a.cap_slots = s0 + static_cast<uint32_t>(forest_slot_cap(nops));
+  r.a.cap_dicts = d0 + static_cast<uint32_t>(forest_dict_cap(nops));
+  r.a.hash_limit = H / 2;
+  r.a.log_base = 0;
+  r.a.ts0 = f.ts0;
+  r.a.root_dict = d0;
+  r.a.src_is_op = 1;
+  r.slots = s0;
+  r.dicts = d0;
+  r.inserted = 0;
+  r.undo_n = 0;
+  r.overflow = false;
+  f.dhead[d0] = NONE;
+  f.T.d_owner[d0] = NONE;
+  r.dicts = d0 + 1;
+  const uint32_t root = r.new_slot(d0, 0, NONE, NONE, NONE, F_TOMB | F_SENT);
+  f.T.d_sent[d0] = root;
+  long long ts = f.ts0;
+  uint32_t applied = 0, err = NONE;
+  int32_t code = CRDTM_OK;
+  for (uint32_t i = ob; i < oe; ++i) {
+    const uint8_t s = r.op(o, i, applied);
+    if (r.overflow) break;
+    if (s == ST_INVALID || s == ST_NOTFOUND) {
+      err = i - ob;
+      code = s == ST_INVALID ? CRDTM_INVALID_PATH : CRDTM_OPERATION_FAILED;
+      break;
+    }
+    if (s == ST_APPLIED) ++applied;
+    if (o.kind[i] == CRDTM_ADD && replica_of(o.ts[i]) == replica_of(ts)) ++ts;
+  }
+  f.overflow[d] = r.overflow ? 1u : 0u;
+  f.code[d] = code;
+  f.err[d] = err;
+  f.applied[d] = applied;
+  f.tstamp[d] = ts;
+  // visible document, pre-order (the oracle's dumpVisible words)
+  Fnv h;
+  if (code == CRDTM_OK && !r.overflow) {
+    constexpr int MAXD = 64;
+    uint32_t stack[MAXD];
+    int depth = 0;
+    stack[0] = root;
+    while (depth >= 0) {
+      uint32_t nx = f.T.s_next[stack[depth]];
+      while (nx != NONE && (f.T.s_flags[nx] & F_TOMB)) nx = f.T.s_next[nx];
+      if (nx == NONE) { --depth; continue; }
+      stack[depth] = nx;
+      const uint32_t src = f.T.s_src[nx];
+      const uint32_t pb = o.off[src], pe = o.off[src + 1];
+      h.put(depth);
+      h.put(static_cast<long long>(o.val[src]));
+      h.put(static_cast<long long>(pe - pb));
+      for (uint32_t j = pb; j + 1 < pe; ++j) h.put(o.path[j]);
+      h.put(o.ts[src]);
+      const uint32_t c = f.T.s_child[nx];
+      if (c != NONE && depth + 1 < MAXD) stack[++depth] = f.T.d_sent[c];
+      else if (c != NONE) f.overflow[d] = 2u;
+    }
+  }
+  f.vhash[d] = h.h;
+  f.vwords[d] = h.n;
 }
 
 // ---------------------------------------------------------------------------
@@ -1158,6 +1295,8 @@ static int run_replay(crdtm_tree* t, const OpsDev& o, uint8_t* st, crdtm_result*
     a.hash_limit = H / 2;
     a.log_base = static_cast<uint32_t>(t->log_n);
     a.ts0 = t->timestamp;
+    a.root_dict = 0;
+    a.src_is_op = 0;
     HIP_CHECK(hipMemsetAsync(c->dres, 0, sizeof(DevResult), s));
     LAUNCH(k_replay, dim3(1), dim3(64), 0, s, o, a, st, c->dres);
     mark(c, "replay");
@@ -1439,6 +1578,90 @@ int linearize(crdtm_tree* t) {
   t->doc_n = (tot == ~0ULL || tot > S) ? 0 : tot;
   t->doc_valid = true;
   return CRDTM_OK;
+}
+
+}  // namespace crdtm
+
+namespace crdtm {
+
+int forest_apply(crdtm_ctx* c, int64_t replica_id, const OpsDev& o, const uint32_t* doc_off_host, uint64_t n_docs,
+                 int32_t* code, int64_t* err, uint32_t* applied, uint64_t* vhash, uint64_t* vwords,
+                 int64_t* tstamp) {
+  hipStream_t s = c->stream;
+  Arena& ws = c->ws;
+  std::vector<uint64_t> sb(n_docs + 1), db(n_docs + 1), hb(n_docs + 1);
+  for (uint64_t d = 0; d < n_docs; ++d) {
+    const uint32_t nops = doc_off_host[d + 1] - doc_off_host[d];
+    sb[d + 1] = sb[d] + forest_slot_cap(nops);
+    db[d + 1] = db[d] + forest_dict_cap(nops);
+    hb[d + 1] = hb[d] + forest_hash_cap(nops);
+  }
+  const uint64_t S = sb[n_docs], D = db[n_docs], Hn = hb[n_docs];
+  if (S >= 0xFFFFFFF0ULL || D >= 0xFFFFFFF0ULL) return CRDTM_E_ARG;
+  ForestArgs f;
+  f.T.s_key = ws.alloc<long long>(S);
+  f.T.s_next = ws.alloc<uint32_t>(S);
+  f.T.s_src = ws.alloc<uint32_t>(S);
+  f.T.s_child = ws.alloc<uint32_t>(S);
+  f.T.s_dict = ws.alloc<uint32_t>(S);
+  f.T.s_flags = ws.alloc<uint8_t>(S);
+  f.T.d_sent = ws.alloc<uint32_t>(D);
+  f.T.d_owner = ws.alloc<uint32_t>(D);
+  f.dhead = ws.alloc<uint32_t>(D);
+  f.mnext = ws.alloc<uint32_t>(S);
+  f.hdict = ws.alloc<uint32_t>(Hn);
+  f.hkey = ws.alloc<long long>(Hn);
+  f.hslot = ws.alloc<uint32_t>(Hn);
+  f.queue = ws.alloc<uint32_t>(2 * D);
+  uint32_t* doff = ws.alloc<uint32_t>(n_docs + 1);
+  uint64_t* dsb = ws.alloc<uint64_t>(n_docs + 1);
+  uint64_t* ddb = ws.alloc<uint64_t>(n_docs + 1);
+  uint64_t* dhb = ws.alloc<uint64_t>(n_docs + 1);
+  f.code = ws.alloc<int32_t>(n_docs);
+  f.err = ws.alloc<uint32_t>(n_docs);
+  f.applied = ws.alloc<uint32_t>(n_docs);
+  f.vhash = ws.alloc<unsigned long long>(n_docs);
+  f.vwords = ws.alloc<unsigned long long>(n_docs);
+  f.tstamp = ws.alloc<long long>(n_docs);
+  f.overflow = ws.alloc<uint32_t>(n_docs);
+  f.doc_off = doff;
+  f.n_docs = static_cast<uint32_t>(n_docs);
+  f.ts0 = replica_id * TWO32;
+  HIP_CHECK(hipMemcpyAsync(doff, doc_off_host, (n_docs + 1) * 4, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(dsb, sb.data(), (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(ddb, db.data(), (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(dhb, hb.data(), (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemsetAsync(f.hslot, 0xFF, Hn * sizeof(uint32_t), s));
+  LAUNCH(k_forest, dim3(static_cast<uint32_t>((n_docs + 63) / 64)), dim3(64), 0, s, o, f, dsb, ddb, dhb);
+  std::vector<uint32_t> e(n_docs), ov(n_docs);
+  HIP_CHECK(hipMemcpyAsync(code, f.code, n_docs * 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(e.data(), f.err, n_docs * 4, hipMemcpyDeviceToHost, s));
+  if (applied) HIP_CHECK(hipMemcpyAsync(applied, f.applied, n_docs * 4, hipMemcpyDeviceToHost, s));
+  if (vhash) HIP_CHECK(hipMemcpyAsync(vhash, f.vhash, n_docs * 8, hipMemcpyDeviceToHost, s));
+  if (vwords) HIP_CHECK(hipMemcpyAsync(vwords, f.vwords, n_docs * 8, hipMemcpyDeviceToHost, s));
+  if (tstamp) HIP_CHECK(hipMemcpyAsync(tstamp, f.tstamp, n_docs * 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(ov.data(), f.overflow, n_docs * 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  int rc = CRDTM_OK;
+  for (uint64_t d = 0; d < n_docs; ++d) {
+    if (err) err[d] = e[d] == NONE ? -1 : static_cast<int64_t>(e[d]);
+    if (ov[d]) {  // a document outgrew its arena (deep copies): reported, never silently wrong
+      code[d] = CRDTM_E_NOMEM;
+      rc = CRDTM_E_NOMEM;
+    }
+  }
+  return rc;
+}
+
+uint64_t forest_ws_bytes(const uint32_t* doc_off_host, uint64_t n_docs, uint64_t n_ops, uint64_t n_path) {
+  uint64_t S = 0, D = 0, H = 0;
+  for (uint64_t d = 0; d < n_docs; ++d) {
+    const uint32_t nops = doc_off_host[d + 1] - doc_off_host[d];
+    S += forest_slot_cap(nops);
+    D += forest_dict_cap(nops);
+    H += forest_hash_cap(nops);
+  }
+  return S * 29 + D * 20 + H * 16 + n_docs * 96 + n_ops * 32 + n_path * 8 + (64ULL << 20);
 }
 
 }  // namespace crdtm

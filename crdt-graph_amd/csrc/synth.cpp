@@ -243,9 +243,11 @@ extern "C" int crdtm_synth(const crdtm_synth_params* p, crdtm_ops** out) {
     o.off.reserve(p->n_ops * docs + 1);
     o.tree.reserve(p->n_ops * docs);
     for (uint64_t d = 0; d < docs; ++d) {
-      const uint64_t seed = p->seed ^ (0xD1B54A32D192ED03ULL * (d + 1));
-      if (p->max_children > 0) genDeep(*p, seed, static_cast<uint32_t>(d), o);
-      else genTyping(*p, docs == 1 ? p->seed : seed, static_cast<uint32_t>(d), o);
+      const uint64_t id = p->doc_base + d;
+      const uint64_t seed = p->seed ^ (0xD1B54A32D192ED03ULL * (id + 1));
+      const bool single = docs == 1 && p->doc_base == 0;
+      if (p->max_children > 0) genDeep(*p, single ? p->seed : seed, static_cast<uint32_t>(id), o);
+      else genTyping(*p, single ? p->seed : seed, static_cast<uint32_t>(id), o);
     }
     auto* r = static_cast<crdtm_ops*>(std::calloc(1, sizeof(crdtm_ops)));
     if (!r) return CRDTM_E_NOMEM;
@@ -256,7 +258,7 @@ extern "C" int crdtm_synth(const crdtm_synth_params* p, crdtm_ops** out) {
     r->path_off = dup(o.off);
     r->path = dup(o.path);
     r->val = dup(o.val);
-    r->tree = docs > 1 ? dup(o.tree) : nullptr;
+    r->tree = (docs > 1 || p->doc_base > 0) ? dup(o.tree) : nullptr;
     *out = r;
     return CRDTM_OK;
   } catch (const std::bad_alloc&) {

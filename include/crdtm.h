@@ -129,12 +129,17 @@ int crdtm_tree_canonical(const crdtm_tree *t, int which, int64_t *out, uint64_t 
 int crdtm_tree_document(const crdtm_tree *t, uint32_t *vals, uint64_t cap, uint64_t *n_visible);
 
 /* ---- forest: many independent documents in one call (config 5) ----
- * ops sorted by document (tree[] ascending, application order within a document);
- * doc_off[n_docs+1] CSR over ops. Every document starts fresh (init replica_id).
- * Per-document results: code (CRDTM_OK / error), err_index (local), applied count. */
+ * ops grouped by document, application order within a document; doc_off
+ * [n_docs+1] is a host CSR over ops (ops in device memory when on_device).
+ * Every document starts as `init replica_id` and takes `apply (Batch ops_d)`
+ * with the exact sequential semantics. Per-document host outputs (any may be
+ * NULL except doc_code): CRDTree.Error code, local err index (-1), applied
+ * count, FNV-1a hash + word count of the visible-document canonical dump
+ * (same words as crdtm_tree_canonical(which = 1)), final timestamp.
+ * Replaces: CRDTree.apply (src/CRDTree.elm:265-269) over many trees. */
 int crdtm_forest_apply(crdtm_ctx *ctx, int64_t replica_id, const crdtm_ops *ops, const uint32_t *doc_off,
                        uint64_t n_docs, int on_device, int32_t *doc_code, int64_t *doc_err, uint32_t *doc_applied,
-                       uint64_t *checksum);
+                       uint64_t *doc_hash, uint64_t *doc_words, int64_t *doc_timestamp);
 
 /* ---- synthetic op streams ---- */
 typedef struct crdtm_synth_params {
@@ -149,6 +154,7 @@ typedef struct crdtm_synth_params {
   uint32_t max_children;/* 0 = unbounded (deep-tree config uses 8) */
   uint32_t deletes_last;/* 1: all Deletes after all Adds (config 4) */
   uint64_t seed;
+  uint64_t doc_base;    /* forest: id of the first generated document (streams depend on seed and id) */
 } crdtm_synth_params;
 /* Generates host arrays owned by the engine; free with crdtm_ops_free. */
 int crdtm_synth(const crdtm_synth_params *p, crdtm_ops **out);

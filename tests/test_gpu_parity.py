@@ -114,3 +114,38 @@ def test_error_leaves_tree_unchanged():
     r = et.apply_in_place(Batch([Add(3, [2], "c"), Add(4, [99], "d")]))
     assert not r.ok and type(r.error).__name__ == "OperationFailed"
     assert engine_summary(et) == before
+
+
+def test_forest_matches_oracle_per_document():
+    """Config 5 shape: many independent documents, exact replay per document."""
+    import ctypes as C
+    from crdtm.tree import forest_apply
+    from oracle.oracle import lib as olib, _ptr as optr
+    n_docs, per = 300, 1000
+    s = N.synth(n_ops=per, n_docs=n_docs, replicas=8, window=16, p_delete=0.2, seed=0xC0FFEE05)
+    doc_off = np.searchsorted(s["tree"], np.arange(n_docs + 1)).astype(np.uint32)
+    out = forest_apply(s, doc_off)
+    assert out["rc"] == 0
+    L = olib()
+    for d in range(0, n_docs, 7):
+        a, b = int(doc_off[d]), int(doc_off[d + 1])
+        off = s["path_off"]
+        sub = dict(kind=s["kind"][a:b].copy(), ts=s["ts"][a:b].copy(), val=s["val"][a:b].copy(),
+                   path_off=(off[a:b + 1] - off[a]).astype(np.uint32), path=s["path"][off[a]:off[b]].copy())
+        t, rc, err = oracle_apply_arrays(sub, b - a)
+        assert out["code"][d] == rc
+        h = C.c_uint64()
+        nw = L.orc_canonical(t, 1, None, 0, C.byref(h))
+        assert (int(out["words"][d]), int(out["hash"][d])) == (nw, h.value), f"document {d}"
+        assert int(out["timestamp"][d]) == L.orc_timestamp(t)
+        L.orc_free(t)
+    # the same document through the single-tree API gives the same visible hash
+    d = 5
+    a, b = int(doc_off[d]), int(doc_off[d + 1])
+    off = s["path_off"]
+    sub = dict(kind=s["kind"][a:b].copy(), ts=s["ts"][a:b].copy(), val=s["val"][a:b].copy(),
+               path_off=(off[a:b + 1] - off[a]).astype(np.uint32), path=s["path"][off[a]:off[b]].copy())
+    et = CRDTree.init(0)
+    et.apply_arrays(sub, b - a)
+    _, nw, hh = et.canonical(1, full=False)
+    assert (nw, hh) == (int(out["words"][d]), int(out["hash"][d]))
