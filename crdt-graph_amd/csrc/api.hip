@@ -156,6 +156,7 @@ int crdtm_ctx_create(int device, void* stream, crdtm_ctx** out) {
   }
   HIP_CHECK(hipMalloc(&c->dres, sizeof(DevResult)));
   HIP_CHECK(hipHostMalloc(&c->hres, sizeof(DevResult), hipHostMallocDefault));
+  HIP_CHECK(hipHostMalloc(&c->hrange, 3 * HOST_RANGES * sizeof(uint32_t), hipHostMallocDefault));
   HIP_CHECK(hipMalloc(&c->rtab, REPLICA_SLOTS * sizeof(uint32_t)));
   HIP_CHECK(hipMemsetAsync(c->rtab, 0, REPLICA_SLOTS * sizeof(uint32_t), c->stream));
   int r = ensure_arena(c, 64ULL << 20);
@@ -172,6 +173,7 @@ int crdtm_ctx_destroy(crdtm_ctx* c) {
   if (c->ws.base) hipFree(c->ws.base);
   hipFree(c->dres);
   hipHostFree(c->hres);
+  hipHostFree(c->hrange);
   hipFree(c->rtab);
   if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;

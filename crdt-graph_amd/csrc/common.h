@@ -67,6 +67,7 @@ struct DevResult {
   uint32_t has_negative;    // some Add ts < 0 (dense index impossible)
   uint32_t n_del;           // Delete ops in the batch
   uint32_t range_total;     // dense index size
+  uint32_t max_replica;     // largest replica id of an Add timestamp
 };
 
 #define HIP_CHECK(x)                                                                         \

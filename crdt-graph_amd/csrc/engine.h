@@ -35,6 +35,8 @@ struct Arena {
 
 enum : uint8_t { F_TOMB = 1, F_ORPHAN = 2, F_SENT = 4 };
 
+constexpr uint32_t HOST_RANGES = 4096;  // replica ranges scanned on the host
+
 // Device-resident CRDTree state (the "replay representation"): one slot per
 // dict entry. Slot s lives in dict s_dict[s] under key s_key[s]; s_next is the
 // slot of the entry named by its `next` key (Elm keeps the key; within a dict
@@ -74,6 +76,7 @@ struct crdtm_ctx {
   crdtm::DevResult* dres = nullptr;  // device
   crdtm::DevResult* hres = nullptr;  // pinned host
   uint32_t* rtab = nullptr;          // replica table [REPLICA_SLOTS], 0 = empty (kept clean between calls)
+  uint32_t* hrange = nullptr;        // pinned host: cmin/cmax/base of the first HOST_RANGES replicas
   bool profile = false;
   std::vector<std::pair<std::string, hipEvent_t>> marks;
   std::vector<std::pair<std::string, double>> phases;
@@ -98,6 +101,9 @@ namespace crdtm {
 int scan_excl_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* total, Arena& ws, hipStream_t st);
 int segmented_sort(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items,
                    const long long* sort_key, Arena& ws, hipStream_t st, DevResult* dres);
+// same, ordering items by descending id (timestamp-slot numbering)
+int segmented_sort_desc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items, Arena& ws,
+                           hipStream_t st, DevResult* dres);
 // ent[e] = {succ, wbits}: see primitives.hip
 int list_rank(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws, hipStream_t st);
 

@@ -18,8 +18,6 @@
 
 namespace crdtm {
 
-constexpr uint32_t REP_LDS_PRE_BITS = 9;
-constexpr uint32_t REP_LDS_PRE = 1u << REP_LDS_PRE_BITS;
 constexpr uint32_t SENT_T = 0xFFFFFFFDu;  // leaf target: the dict's sentinel (key 0)
 constexpr uint32_t MISS_T = 0xFFFFFFFCu;  // leaf target: key not in the dict
 
@@ -77,19 +75,21 @@ __device__ __forceinline__ uint32_t block_min(uint32_t v) {
 // the first Add of their timestamp; the root dict owner is ROOTN = n.
 // ---------------------------------------------------------------------------
 
-__global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, Work w, uint32_t* cmin, uint32_t* cmax, DevResult* dres) {
-  // per-block (replica -> counter min/max) table; replicas are few, so one
-  // global atomic pair per (block, replica) instead of one per op
-  __shared__ uint32_t rk[REP_LDS_PRE];
-  __shared__ uint32_t rlo[REP_LDS_PRE];
-  __shared__ uint32_t rhi[REP_LDS_PRE];
-  for (uint32_t j = threadIdx.x; j < REP_LDS_PRE; j += blockDim.x) {
-    rk[j] = NONE;
+// Batch pre-pass: per-replica counter ranges of the Add timestamps (dense
+// index layout), longest path, |x| < 2^53 range checks over ts and path
+// elements, negative timestamps, Delete count and the largest replica id.
+// Replica ids below REP_DIRECT fold into a direct-mapped LDS table with
+// no-return LDS atomics; larger ids go straight to the global table.
+constexpr uint32_t REP_DIRECT = 4096;
+__global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint32_t* cmin, uint32_t* cmax, DevResult* dres) {
+  __shared__ uint32_t rlo[REP_DIRECT];
+  __shared__ uint32_t rhi[REP_DIRECT];
+  for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) {
     rlo[j] = NONE;
     rhi[j] = 0;
   }
   __syncthreads();
-  uint32_t mx = 0, bad = 0, neg = 0, ndel = 0;
+  uint32_t mx = 0, bad = 0, neg = 0, ndel = 0, maxr = 0;
   const uint32_t n = o.n;
   const uint32_t chunk = (n + gridDim.x - 1) / gridDim.x;
   const uint32_t b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
@@ -97,57 +97,70 @@ __global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, Work w, uint32_t* cmin,
     const uint32_t L = op_len(o, i);
     mx = max(mx, L);
     const bool add = o.kind[i] == CRDTM_ADD;
-    const long long ts = add ? o.ts[i] : 0;
-    if (ts >= TWO53 || ts <= -TWO53) bad = 1;
-    if (!add) ++ndel;
-    w.st[i] = L == 0 ? ST_INVALID : ST_PENDING;
-    w.cur[i] = n;
-    w.addpar[i] = NONE;
-    w.dtime[i] = NONE;
-    if (add && L >= 1 && ts != 0) {
-      if (ts < 0) {
-        neg = 1;
-      } else if (ts < TWO53) {
-        const uint32_t r = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32), c = static_cast<uint32_t>(ts);
-        uint32_t p = (r * 0x9E3779B1u) >> (32 - REP_LDS_PRE_BITS);
-        bool done = false;
-        for (uint32_t probe = 0; probe < 16 && !done; ++probe, p = (p + 1) & (REP_LDS_PRE - 1)) {
-          const uint32_t prev = atomicCAS(&rk[p], NONE, r);
-          if (prev == NONE || prev == r) {
-            atomicMin(&rlo[p], c);
-            atomicMax(&rhi[p], c);
-            done = true;
-          }
-        }
-        if (!done) {
-          atomicMin(&cmin[r], c);
-          atomicMax(&cmax[r], c);
-        }
+    if (!add) {
+      ++ndel;
+      continue;
+    }
+    const long long ts = o.ts[i];
+    if (ts >= TWO53 || ts <= -TWO53) {
+      bad = 1;
+    } else if (ts < 0) {
+      neg = 1;
+    } else if (L >= 1 && ts != 0) {
+      const uint32_t r = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32), c = static_cast<uint32_t>(ts);
+      maxr = max(maxr, r);
+      if (r < REP_DIRECT) {
+        atomicMin(&rlo[r], c);
+        atomicMax(&rhi[r], c);
+      } else {
+        atomicMin(&cmin[r], c);
+        atomicMax(&cmax[r], c);
       }
     }
   }
+  // path elements (the same chunking over the path array)
+  const uint64_t np = o.n_path;
+  const uint64_t pchunk = (np + gridDim.x - 1) / gridDim.x;
+  const uint64_t p0 = blockIdx.x * pchunk, p1 = min(np, p0 + pchunk);
+  for (uint64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+    const long long v = o.path[p];
+    if (v >= TWO53 || v <= -TWO53) bad = 1;
+  }
   __syncthreads();
-  for (uint32_t j = threadIdx.x; j < REP_LDS_PRE; j += blockDim.x) {
-    if (rk[j] != NONE) {
-      atomicMin(&cmin[rk[j]], rlo[j]);
-      atomicMax(&cmax[rk[j]], rhi[j]);
+  for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) {
+    if (rlo[j] != NONE) {
+      atomicMin(&cmin[j], rlo[j]);
+      atomicMax(&cmax[j], rhi[j]);
     }
   }
   mx = block_max(mx);
   bad = block_max(bad);
   neg = block_max(neg);
+  maxr = block_max(maxr);
   ndel = block_sum(ndel);
   if (threadIdx.x == 0) {
     if (mx) atomicMax(&dres->max_len, mx);
     if (bad) atomicOr(&dres->bad_range, 1u);
     if (neg) atomicOr(&dres->has_negative, 1u);
     if (ndel) atomicAdd(&dres->n_del, ndel);
+    if (maxr) atomicMax(&dres->max_replica, maxr);
+  }
+}
+
+// Per-op state of the level-synchronous (nested / hash-indexed) path.
+__global__ void __launch_bounds__(BLOCK) k_work_init(OpsDev o, Work w) {
+  GRID_STRIDE(i, o.n) {
+    w.st[i] = op_len(o, i) == 0 ? ST_INVALID : ST_PENDING;
+    w.cur[i] = o.n;
+    w.addpar[i] = NONE;
+    w.dtime[i] = NONE;
   }
 }
 
 // range size per replica -> scan -> base (dense index layout)
-__global__ void __launch_bounds__(BLOCK) k_range_size(const uint32_t* cmin, const uint32_t* cmax, uint32_t* sz) {
-  GRID_STRIDE(r, RID_SLOTS) {
+__global__ void __launch_bounds__(BLOCK) k_range_size(const uint32_t* cmin, const uint32_t* cmax, uint32_t* sz,
+                                                      uint32_t nr) {
+  GRID_STRIDE(r, nr) {
     const uint32_t lo = cmin[r];
     sz[r] = lo == NONE ? 0u : cmax[r] - lo + 1u;
   }
@@ -158,6 +171,28 @@ __global__ void __launch_bounds__(BLOCK) k_index_insert(OpsDev o, TsIndex x) {
     if (o.kind[i] != CRDTM_ADD || op_len(o, i) == 0) continue;
     const long long ts = o.ts[i];
     if (ts != 0) tsindex_insert(x, ts, i);
+  }
+}
+
+// Dense index without atomics: every Add stores its op index into its slot
+// (one arbitrary writer wins among duplicates), then every Add that did not
+// win takes an atomicMin, so the slot ends as the first Add of that
+// timestamp. Batches without duplicate timestamps pay no atomic at all.
+__global__ void __launch_bounds__(BLOCK) k_index_store(OpsDev o, TsIndex x) {
+  GRID_STRIDE(i, o.n) {
+    if (o.kind[i] != CRDTM_ADD || op_len(o, i) == 0) continue;
+    const long long ts = o.ts[i];
+    if (ts > 0) x.first[tsindex_slot(x, ts)] = i;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_index_fix(OpsDev o, TsIndex x) {
+  GRID_STRIDE(i, o.n) {
+    if (o.kind[i] != CRDTM_ADD || op_len(o, i) == 0) continue;
+    const long long ts = o.ts[i];
+    if (ts <= 0) continue;
+    uint32_t* f = &x.first[tsindex_slot(x, ts)];
+    if (*f != i) atomicMin(f, i);
   }
 }
 
@@ -189,21 +224,6 @@ __global__ void __launch_bounds__(BLOCK) k_flat_status(OpsDev o, Work w, TsIndex
     }
     w.st[i] = s;
   }
-}
-
-__global__ void __launch_bounds__(BLOCK) k_path_range(const long long* path, uint64_t np, DevResult* dres) {
-  uint32_t bad = 0;
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  const uint64_t trips = (np + stride - 1) / stride;
-  for (uint64_t t = 0; t < trips; ++t) {
-    const uint64_t p = t * stride + blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-    if (p < np) {
-      const long long x = path[p];
-      if (x >= TWO53 || x <= -TWO53) bad = 1;
-    }
-  }
-  bad = block_max(bad);
-  if (threadIdx.x == 0 && bad) atomicOr(&dres->bad_range, 1u);
 }
 
 // Adds whose path has length lvl record their dict owner (resolved prefix).
@@ -1123,6 +1143,258 @@ __global__ void __launch_bounds__(64) k_forest(OpsDev o, ForestArgs f, const uin
 }
 
 // ---------------------------------------------------------------------------
+// Flat closed form in timestamp-slot space: a fresh tree, a single-level
+// Adds-only batch, and a dense timestamp index. Node q = the dense slot of
+// its timestamp (base[replica] + counter - cmin[replica]), so slot order IS
+// timestamp order (src/Internal/Node.elm:100 compares the Int key), and a
+// replica's typing run x_c -> x_{c+1} -> ... occupies consecutive slots: the
+// effective-parent chains, the child counting, the Euler tour and the
+// list-ranking walks step through memory sequentially instead of hopping
+// ~R ops apart. The root dict's sentinel (key 0, -inf in the order) is node
+// Q. anc[q] = ABSENT marks a slot without an applied Add.
+// ---------------------------------------------------------------------------
+
+// K1 (flat): status of every op; applied Adds record their anchor slot.
+__global__ void __launch_bounds__(BLOCK) k_fl_status(OpsDev o, uint8_t* st, TsIndex x, uint32_t Q, uint32_t* anc) {
+  GRID_STRIDE(i, o.n) {
+    const uint32_t L = op_len(o, i);
+    uint8_t s;
+    if (L == 0) {
+      s = ST_INVALID;  // update [] = InvalidPath (src/Internal/Node.elm:147-148)
+    } else {
+      const uint32_t q = tsindex_slot(x, o.ts[i]);
+      if (q == NONE || x.first[q] != i) {
+        s = ST_ALREADY;  // ts 0 is the sentinel's key / `child ts parent` exists (:63-65)
+      } else {
+        const long long k = o.path[o.off[i]];
+        uint32_t a = Q;  // anchor 0 = the dict's sentinel
+        if (k != 0) {
+          const uint32_t qa = tsindex_slot(x, k);
+          const uint32_t fa = qa == NONE ? NONE : x.first[qa];
+          a = (fa != NONE && fa < i) ? qa : NONE;  // anchor must exist before op i (:68-70)
+        }
+        if (a == NONE) {
+          s = ST_NOTFOUND;
+        } else {
+          s = ST_APPLIED;
+          anc[q] = a;
+        }
+      }
+    }
+    st[i] = s;
+  }
+}
+
+// K2a: effective parent. A typing run is a maximal slot interval [h, c]
+// with anc[q] = q - 1 for q in (h, c]; rh[q] = h (inclusive max-scan, see
+// k_rh_*). Walking x's anchor chain from c down a run visits c, c-1, ..., h
+// in slot order, so the first node below x is x - 1 when h < x, and the
+// whole run is skipped otherwise: one step per run instead of per node
+// (flat10m: max walk 312 nodes -> 23 runs). anc[] is overwritten with ep as
+// walks finish; a concurrent reader then sees ep(h) instead of anchor(h),
+// which skips only nodes > h > x, so every walk stays exact.
+__global__ void __launch_bounds__(BLOCK) k_fl_ep(uint32_t Q, uint32_t* anc, const uint32_t* rh) {
+  GRID_STRIDE(x, Q) {
+    uint32_t d = anc[x];
+    if (d == ABSENT || d == Q || d < x) continue;
+    while (d != Q && d > x) {
+      const uint32_t h = rh[d];
+      if (h < x) {
+        d = x - 1;
+        break;
+      }
+      d = __hip_atomic_load(&anc[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __hip_atomic_store(&anc[x], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Run heads: rh[q] = max{q' <= q : anc[q'] != q' - 1}, a three-phase
+// inclusive max-scan (tiles of 2048 slots; tile maxima scanned recursively).
+constexpr int RH_ITEMS = 8;
+constexpr int RH_TILE = BLOCK * RH_ITEMS;
+
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v = max(v, t);
+  }
+  return v;
+}
+
+// in == nullptr: values from anc (head flags); else a plain max-scan of in.
+__global__ void __launch_bounds__(BLOCK) k_rh_tiles(const uint32_t* anc, const uint32_t* in, uint32_t* out,
+                                                    uint32_t* tile_max, uint32_t n) {
+  __shared__ uint32_t lw[BLOCK / 64];
+  const uint32_t b = blockIdx.x * RH_TILE + threadIdx.x * RH_ITEMS;
+  uint32_t v[RH_ITEMS];
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < RH_ITEMS; ++j) {
+    const uint32_t q = b + j;
+    uint32_t x = 0;
+    if (q < n) x = in ? in[q] : ((q == 0 || anc[q] != q - 1) ? q : 0u);
+    m = max(m, x);
+    v[j] = m;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t inc = wave_incl_max(m);
+  if (lane == 63) lw[wave] = inc;
+  __syncthreads();
+  uint32_t pre = __shfl_up(inc, 1, 64);
+  if (lane == 0) pre = 0;
+  for (int w = 0; w < wave; ++w) pre = max(pre, lw[w]);
+  uint32_t tot = 0;
+  for (int w = 0; w < BLOCK / 64; ++w) tot = max(tot, lw[w]);
+#pragma unroll
+  for (int j = 0; j < RH_ITEMS; ++j)
+    if (b + j < n) out[b + j] = max(v[j], pre);
+  if (threadIdx.x == 0) tile_max[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_rh_add(uint32_t* out, const uint32_t* tile_incl, uint32_t n) {
+  if (blockIdx.x == 0) return;
+  const uint32_t add = tile_incl[blockIdx.x - 1];
+  const uint32_t b = blockIdx.x * RH_TILE + threadIdx.x * RH_ITEMS;
+#pragma unroll
+  for (int j = 0; j < RH_ITEMS; ++j)
+    if (b + j < n) out[b + j] = max(out[b + j], add);
+}
+
+// inclusive max-scan; anc != nullptr derives the values from run-head flags
+static int max_scan_incl(const uint32_t* anc, const uint32_t* in, uint32_t* out, uint32_t n, Arena& ws,
+                         hipStream_t st) {
+  const uint32_t tiles = (n + RH_TILE - 1) / RH_TILE;
+  uint32_t* tm = ws.alloc<uint32_t>(tiles + 1);
+  LAUNCH(k_rh_tiles, dim3(tiles), dim3(BLOCK), 0, st, anc, in, out, tm, n);
+  if (tiles > 1) {
+    int r = max_scan_incl(nullptr, tm, tm, tiles, ws, st);
+    if (r) return r;
+    LAUNCH(k_rh_add, dim3(tiles), dim3(BLOCK), 0, st, out, tm, n);
+  }
+  return CRDTM_OK;
+}
+
+// K2b: children per parent (the sentinel's count aggregated per workgroup).
+__global__ void __launch_bounds__(BLOCK) k_fl_count(uint32_t Q, const uint32_t* anc, uint32_t* cnt) {
+  uint32_t hot = 0;
+  GRID_STRIDE(q, Q) {
+    const uint32_t p = anc[q];
+    if (p == ABSENT) continue;
+    if (p == Q) ++hot;
+    else atomicAdd(&cnt[p], 1u);
+  }
+  hot = block_sum(hot);
+  if (threadIdx.x == 0 && hot) atomicAdd(&cnt[Q], hot);
+}
+
+// Counting-sort scatter; single-child parents (the common case in a typing
+// stream) take a plain store.
+__global__ void __launch_bounds__(BLOCK) k_fl_scatter(uint32_t Q, const uint32_t* anc, const uint32_t* start,
+                                                      uint32_t* fill, uint32_t* carr) {
+  __shared__ uint32_t blk_base;
+  uint32_t hot = 0;
+  GRID_STRIDE(q, Q) {
+    if (anc[q] == Q) ++hot;
+  }
+  uint32_t tot;
+  uint32_t mine = block_excl_sum(hot, &tot);
+  if (threadIdx.x == 0) blk_base = tot ? atomicAdd(&fill[Q], tot) : 0u;
+  __syncthreads();
+  mine += blk_base + start[Q];
+  GRID_STRIDE(q, Q) {
+    const uint32_t p = anc[q];
+    if (p == ABSENT) continue;
+    if (p == Q) {
+      carr[mine++] = q;
+    } else {
+      const uint32_t b = start[p];
+      carr[start[p + 1] - b == 1 ? b : b + atomicAdd(&fill[p], 1u)] = q;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_fl_links(const uint32_t* anc, const uint32_t* start, const uint32_t* total,
+                                                    const uint32_t* carr, uint32_t* ns) {
+  const uint32_t tot = *total;
+  GRID_STRIDE(pos, tot) {
+    const uint32_t v = carr[pos];
+    ns[v] = (pos + 1 < start[anc[v] + 1]) ? carr[pos + 1] : NONE;
+  }
+}
+
+// K4a: Euler tour, enter(u) = 2u, leave(u) = 2u + 1; enter of a node weighs
+// 1 (document rank). Both entries of u go out as one 16-byte store.
+__global__ void __launch_bounds__(BLOCK) k_fl_euler(uint32_t Q, const uint32_t* anc, const uint32_t* start,
+                                                    const uint32_t* carr, const uint32_t* ns, uint4* ent) {
+  GRID_STRIDE(u, Q + 1) {
+    const uint32_t p = u < Q ? anc[u] : Q;
+    if (p == ABSENT) {
+      ent[u] = make_uint4(ABSENT, 0u, ABSENT, 0u);
+      continue;
+    }
+    const uint32_t b = start[u], e = start[u + 1];
+    const uint32_t enter = b < e ? 2 * carr[b] : 2 * u + 1;
+    uint32_t after = NONE;
+    if (u < Q) after = ns[u] != NONE ? 2 * ns[u] : 2 * p + 1;
+    ent[u] = make_uint4(enter, u < Q ? 1u : 0u, after, 0u);
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_fl_order(uint32_t Q, const uint32_t* anc, const unsigned long long* excl,
+                                                    uint32_t* order) {
+  GRID_STRIDE(q, Q) {
+    if (anc[q] != ABSENT) order[static_cast<uint32_t>(excl[2 * q])] = q;
+  }
+}
+
+// Commit in document order: node of rank r -> slot 1 + r, its children
+// dict 1 + r with sentinel slot 1 + K + r. Within the root dict the raw
+// `next` chain is the document order (no tombstones).
+__global__ void __launch_bounds__(BLOCK) k_fl_commit(OpsDev o, TsIndex x, uint32_t K, const uint32_t* order,
+                                                     const uint32_t* logidx, TreeDev T) {
+  GRID_STRIDE(r, K) {
+    const uint32_t q = order[r];
+    const uint32_t i = x.first[q];
+    const uint32_t slot = 1 + r, ss = 1 + K + r, dd = 1 + r;
+    T.s_key[slot] = o.ts[i];
+    T.s_dict[slot] = 0;
+    T.s_next[slot] = r + 1 < K ? slot + 1 : NONE;
+    T.s_src[slot] = logidx ? logidx[i] : i;
+    T.s_flags[slot] = 0;
+    T.s_child[slot] = dd;
+    T.s_key[ss] = 0;
+    T.s_dict[ss] = dd;
+    T.s_next[ss] = NONE;
+    T.s_src[ss] = NONE;
+    T.s_child[ss] = NONE;
+    T.s_flags[ss] = F_TOMB | F_SENT;
+    T.d_sent[dd] = ss;
+    T.d_owner[dd] = slot;
+    T.doc[r] = slot;
+    if (r == 0) T.s_next[0] = slot;  // the root sentinel leads to the first node
+  }
+}
+
+// Log append into a fresh tree when every op applied: the log is the batch
+// itself (same CSR layout, path elements [0, n_path)).
+__global__ void __launch_bounds__(BLOCK) k_fl_log_copy(OpsDev o, TreeDev T) {
+  GRID_STRIDE(i, o.n + 1) {
+    T.l_off[i] = o.off[i];
+    if (i == o.n) continue;
+    T.l_kind[i] = o.kind[i];
+    T.l_ts[i] = o.ts[i];
+    T.l_val[i] = o.val[i];
+  }
+  const uint64_t np = o.n_path;
+  for (uint64_t p = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; p < np;
+       p += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    T.l_path[p] = o.path[p];
+}
+
+// ---------------------------------------------------------------------------
 // Host orchestration
 // ---------------------------------------------------------------------------
 thread_local crdtm_ctx* g_prof = nullptr;
@@ -1328,6 +1600,126 @@ static int run_replay(crdtm_tree* t, const OpsDev& o, uint8_t* st, crdtm_result*
   return CRDTM_E_NOMEM;
 }
 
+// Flat closed form (see the k_fl_* kernels): the index `ix` is dense and
+// already built; Q = its slot range.
+static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_t Q, uint8_t* st,
+                      uint8_t* st_out, crdtm_result* res) {
+  crdtm_ctx* c = t->ctx;
+  hipStream_t s = c->stream;
+  Arena& ws = c->ws;
+  DevResult* dr = c->dres;
+  const uint32_t n = o.n;
+  const uint32_t g = grid_for(n);
+  uint32_t* anc = ws.alloc<uint32_t>(static_cast<uint64_t>(Q) + 1);
+  HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(anc), static_cast<int>(ABSENT), Q + 1, s));
+  LAUNCH(k_fl_status, dim3(g), dim3(BLOCK), 0, s, o, st, ix, Q, anc);
+  Work w{};
+  w.st = st;
+  HIP_CHECK(hipMemsetAsync(&dr->first_del, 0xFF, sizeof(uint32_t), s));
+  LAUNCH(k_stats, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, o, w, t->timestamp, dr);
+  int r;
+  if ((r = sync_read(c))) return r;
+  const DevResult h1 = *c->hres;
+  uint32_t guard = 0;
+  const long long new_ts = t->timestamp + h1.own_ok_adds;
+  if (replica_of(new_ts) != replica_of(t->timestamp)) guard |= G_REPLICA_DRIFT;
+  res->guard = guard;
+  if (guard) {
+    r = run_replay(t, o, st, res, guard);
+    if (r == CRDTM_OK && st_out)
+      LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, st, n,
+             res->err_index >= 0 ? static_cast<uint32_t>(res->err_index) : NONE, st_out);
+    return r;
+  }
+  res->path_taken = CRDTM_PATH_CLOSED_FORM;
+  if (h1.err_index != NONE) {
+    uint8_t est = 0;
+    HIP_CHECK(hipMemcpy(&est, st + h1.err_index, 1, hipMemcpyDeviceToHost));
+    res->code = est == ST_INVALID ? CRDTM_INVALID_PATH : CRDTM_OPERATION_FAILED;
+    res->err_index = h1.err_index;
+    if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, st, n, h1.err_index, st_out);
+    return CRDTM_OK;
+  }
+  res->n_applied = h1.n_applied;
+  res->n_already = h1.n_already;
+  const uint32_t K = h1.n_adds_applied;
+  const bool all_applied = h1.n_applied == n;
+  TreeCaps need = t->cap;
+  need.slots = std::max<uint64_t>(need.slots, 1 + 2ULL * K + 1);
+  need.dicts = std::max<uint64_t>(need.dicts, 1ULL + K + 1);
+  need.log = std::max<uint64_t>(need.log, t->log_n + h1.n_applied + 1);
+  need.lpath = std::max<uint64_t>(need.lpath, t->log_npath + o.n_path + 1);
+  need.doc = std::max<uint64_t>(need.doc, 1ULL + K);
+  if (need.slots > t->cap.slots || need.dicts > t->cap.dicts || need.log > t->cap.log ||
+      need.lpath > t->cap.lpath || need.doc > t->cap.doc) {
+    if ((r = grow_tree(t, need))) return r;
+  }
+  if (K > 0) {
+    // ---- K2: effective parents, children lists in descending slot order ----
+    const uint32_t U = Q + 1;  // nodes + the root sentinel
+    uint32_t* cnt = ws.alloc<uint32_t>(U + 1);
+    uint32_t* fill = ws.alloc<uint32_t>(U + 1);
+    uint32_t* carr = ws.alloc<uint32_t>(U);
+    uint32_t* ns = ws.alloc<uint32_t>(U);
+    HIP_CHECK(hipMemsetAsync(cnt, 0, (U + 1) * sizeof(uint32_t), s));
+    HIP_CHECK(hipMemsetAsync(fill, 0, (U + 1) * sizeof(uint32_t), s));
+    const uint32_t gq = grid_for(Q);
+    uint32_t* rh = ws.alloc<uint32_t>(Q);
+    if ((r = max_scan_incl(anc, nullptr, rh, Q, ws, s))) return r;
+    LAUNCH(k_fl_ep, dim3(gq), dim3(BLOCK), 0, s, Q, anc, rh);
+    LAUNCH(k_fl_count, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, cnt);
+    uint32_t* n_child = &dr->n_sentinels;  // scratch word for the scan total
+    if ((r = scan_excl_u32(cnt, cnt, U + 1, n_child, ws, s))) return r;
+    LAUNCH(k_fl_scatter, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, cnt, fill, carr);
+    if ((r = segmented_sort_desc_id(cnt, U, carr, U, ws, s, dr))) return r;
+    LAUNCH(k_fl_links, dim3(gq), dim3(BLOCK), 0, s, anc, cnt, n_child, carr, ns);
+    // ---- K4: Euler tour + list ranking -> document rank ----
+    const uint64_t E = 2ULL * U;
+    uint4* ent = ws.alloc<uint4>(U);
+    unsigned long long* excl = ws.alloc<unsigned long long>(E);
+    LAUNCH(k_fl_euler, dim3(grid_for(U)), dim3(BLOCK), 0, s, Q, anc, cnt, carr, ns, ent);
+    if ((r = list_rank(reinterpret_cast<const uint2*>(ent), E, 2 * Q, excl, ws, s))) return r;
+    uint32_t* order = ws.alloc<uint32_t>(K);
+    LAUNCH(k_fl_order, dim3(gq), dim3(BLOCK), 0, s, Q, anc, excl, order);
+    // ---- commit in document order ----
+    uint32_t* logidx = nullptr;
+    if (!all_applied) {
+      logidx = ws.alloc<uint32_t>(n + 1);
+      uint32_t* plen = ws.alloc<uint32_t>(n + 1);
+      LAUNCH(k_post_flags, dim3(g), dim3(BLOCK), 0, s, o, st, logidx, plen);
+      if ((r = scan_excl_u32(logidx, logidx, n, &dr->log_n, ws, s))) return r;
+      if ((r = scan_excl_u32(plen, plen, n, &dr->log_npath, ws, s))) return r;
+      LAUNCH(k_log, dim3(g), dim3(BLOCK), 0, s, o, st, t->d, 0u, 0u, logidx, plen);
+      LAUNCH(k_log_tail, dim3(1), dim3(1), 0, s, t->d, 0u, &dr->log_n, 0u, &dr->log_npath);
+    }
+    LAUNCH(k_fl_commit, dim3(grid_for(K)), dim3(BLOCK), 0, s, o, ix, K, order, logidx, t->d);
+  }
+  if (all_applied) LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
+  long long* rep = ws.alloc<long long>(2 * static_cast<uint64_t>(n) + 2);
+  LAUNCH(k_rep_max, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, s, o, st, c->rtab);
+  LAUNCH(k_rep_out, dim3(g), dim3(BLOCK), 0, s, o, st, c->rtab, rep, &dr->n_replica_out);
+  LAUNCH(k_rep_reset, dim3(g), dim3(BLOCK), 0, s, o, st, c->rtab);
+  if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, st, n, NONE, st_out);
+  if ((r = sync_read(c))) return r;
+  const DevResult& h2 = *c->hres;
+  const uint32_t nrep = h2.n_replica_out;
+  if (nrep) {
+    std::vector<long long> hv(2 * static_cast<size_t>(nrep));
+    HIP_CHECK(hipMemcpy(hv.data(), rep, hv.size() * sizeof(long long), hipMemcpyDeviceToHost));
+    for (uint32_t k = 0; k < nrep; ++k) t->replicas[hv[2 * k]] = hv[2 * k + 1];
+  }
+  t->n_slots = 1 + 2ULL * K;
+  t->n_dicts = 1ULL + K;
+  t->last_begin = t->log_n;
+  t->log_n += h1.n_applied;
+  t->log_npath += all_applied ? o.n_path : h2.log_npath;
+  t->last_end = t->log_n;
+  t->timestamp = new_ts;
+  t->doc_n = K;
+  t->doc_valid = true;
+  return CRDTM_OK;
+}
+
 int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res) {
   crdtm_ctx* c = t->ctx;
   hipStream_t s = c->stream;
@@ -1342,14 +1734,6 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   }
   Work w;
   w.st = ws.alloc<uint8_t>(n);
-  w.cur = ws.alloc<uint32_t>(n);
-  w.nxt = ws.alloc<uint32_t>(n);
-  w.leaf = ws.alloc<uint32_t>(n);
-  w.addpar = ws.alloc<uint32_t>(n);
-  w.dtime = ws.alloc<uint32_t>(n);
-  w.dead = ws.alloc<uint8_t>(n);
-  w.maxadd = ws.alloc<uint32_t>(n + 1);
-  uint32_t* anc = ws.alloc<uint32_t>(n);
   uint32_t* cmin = ws.alloc<uint32_t>(RID_SLOTS);
   uint32_t* cmax = ws.alloc<uint32_t>(RID_SLOTS);
   uint32_t* rbase = ws.alloc<uint32_t>(RID_SLOTS + 1);
@@ -1358,11 +1742,12 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   HIP_CHECK(hipMemsetAsync(&dr->err_index, 0xFF, sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(cmin, 0xFF, RID_SLOTS * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(cmax, 0, RID_SLOTS * sizeof(uint32_t), s));
-  LAUNCH(k_pre, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, o, w, cmin, cmax, dr);
-  LAUNCH(k_path_range, dim3(grid_for(o.n_path, BLOCK, 2048)), dim3(BLOCK), 0, s, o.path, o.n_path, dr);
-  LAUNCH(k_range_size, dim3(grid_for(RID_SLOTS)), dim3(BLOCK), 0, s, cmin, cmax, rbase);
+  LAUNCH(k_pre, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, o, cmin, cmax, dr);
+  // the first HOST_RANGES replica ranges come back with the result block:
+  // the dense index layout (exclusive scan of range sizes) is then a host loop
+  HIP_CHECK(hipMemcpyAsync(c->hrange, cmin, HOST_RANGES * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(c->hrange + HOST_RANGES, cmax, HOST_RANGES * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   int r;
-  if ((r = scan_excl_u32(rbase, rbase, RID_SLOTS, &dr->range_total, ws, s))) return r;
   if ((r = sync_read(c))) return r;
   if (c->hres->bad_range) return CRDTM_E_RANGE;
   const uint32_t maxlen = c->hres->max_len;
@@ -1376,17 +1761,36 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
              res->err_index >= 0 ? static_cast<uint32_t>(res->err_index) : NONE, st_out);
     return r;
   }
+  const uint32_t maxr = c->hres->max_replica;
+  uint64_t range_total = 0;
+  if (maxr < HOST_RANGES) {
+    uint32_t* hb = c->hrange + 2 * HOST_RANGES;
+    for (uint32_t q = 0; q <= maxr; ++q) {
+      hb[q] = static_cast<uint32_t>(std::min<uint64_t>(range_total, NONE));
+      const uint32_t lo = c->hrange[q];
+      if (lo != NONE) range_total += static_cast<uint64_t>(c->hrange[HOST_RANGES + q]) - lo + 1;
+    }
+    HIP_CHECK(hipMemcpyAsync(rbase, hb, (maxr + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  } else {
+    LAUNCH(k_range_size, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, cmin, cmax, rbase, maxr + 1);
+    if ((r = scan_excl_u32(rbase, rbase, maxr + 1, &dr->range_total, ws, s))) return r;
+    if ((r = sync_read(c))) return r;
+    range_total = c->hres->range_total;
+  }
   // ts index: dense per-replica runs when possible, else an open-addressing hash
   TsIndex ix;
   ix.cmin = cmin;
   ix.cmax = cmax;
   ix.base = rbase;
-  const uint64_t range_total = c->hres->range_total;
   ix.dense = (!c->hres->has_negative && range_total <= 4ULL * n + 65536) ? 1u : 0u;
+  const bool flat = maxlen == 1 && c->hres->n_del == 0;
   if (ix.dense) {
     ix.first = ws.alloc<uint32_t>(range_total + 1);
     ix.h = TsHash{nullptr, nullptr, 0};
     HIP_CHECK(hipMemsetAsync(ix.first, 0xFF, (range_total + 1) * sizeof(uint32_t), s));
+    LAUNCH(k_index_store, dim3(g), dim3(BLOCK), 0, s, o, ix);
+    LAUNCH(k_index_fix, dim3(g), dim3(BLOCK), 0, s, o, ix);
+    if (flat) return apply_flat(t, o, ix, static_cast<uint32_t>(range_total), w.st, st_out, res);
   } else {
     const uint32_t H = pow2_at_least(2 * static_cast<uint64_t>(n));
     ix.first = nullptr;
@@ -1395,9 +1799,17 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
     ix.h.mask = H - 1;
     HIP_CHECK(hipMemsetAsync(ix.h.keys, 0, H * sizeof(unsigned long long), s));
     HIP_CHECK(hipMemsetAsync(ix.h.vals, 0xFF, H * sizeof(uint32_t), s));
+    LAUNCH(k_index_insert, dim3(g), dim3(BLOCK), 0, s, o, ix);
   }
-  LAUNCH(k_index_insert, dim3(g), dim3(BLOCK), 0, s, o, ix);
-  const bool flat = maxlen == 1 && c->hres->n_del == 0;
+  w.cur = ws.alloc<uint32_t>(n);
+  w.nxt = ws.alloc<uint32_t>(n);
+  w.leaf = ws.alloc<uint32_t>(n);
+  w.addpar = ws.alloc<uint32_t>(n);
+  w.dtime = ws.alloc<uint32_t>(n);
+  w.dead = ws.alloc<uint8_t>(n);
+  w.maxadd = ws.alloc<uint32_t>(n + 1);
+  uint32_t* anc = ws.alloc<uint32_t>(n);
+  LAUNCH(k_work_init, dim3(g), dim3(BLOCK), 0, s, o, w);
   if (flat) {
     LAUNCH(k_flat_status, dim3(g), dim3(BLOCK), 0, s, o, w, ix, anc);
   } else {

@@ -89,16 +89,27 @@ int scan_excl_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* total
 
 // ---------------------------------------------------------------------------
 // Segmented sort of children by key (ascending, unique keys per segment).
-// seg_start[u]..seg_start[u+1) of carr; key(v) from sort_key[v].
+// seg_start[u]..seg_start[u+1) of carr; key(v) from sort_key(v).
 // Small segments: one lane each (insertion sort). Large: one workgroup each,
 // bitonic in LDS up to LDS_SORT_MAX, else a workgroup merge sort in HBM.
 // ---------------------------------------------------------------------------
 constexpr uint32_t SMALL_SEG = 16;
 constexpr uint32_t LDS_SORT_MAX = 4096;
 
+// Sort keys: an explicit per-item array, or the item id itself descending
+// (timestamp-slot numbering: slot order == timestamp order).
+struct ArrKey {
+  const long long* k;
+  __device__ __forceinline__ long long operator()(uint32_t v) const { return k[v]; }
+};
+struct NegIdKey {
+  __device__ __forceinline__ long long operator()(uint32_t v) const { return -static_cast<long long>(v); }
+};
+
+template <class KEY>
 __global__ void __launch_bounds__(BLOCK) k_sort_small(const uint32_t* __restrict__ seg_start, uint32_t n_seg,
                                                       uint32_t* __restrict__ carr,
-                                                      const long long* __restrict__ sort_key,
+                                                      KEY sort_key,
                                                       uint32_t* __restrict__ big_list, uint32_t* __restrict__ n_big) {
   for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < n_seg; u += gridDim.x * blockDim.x) {
     const uint32_t b = seg_start[u], e = seg_start[u + 1];
@@ -112,7 +123,7 @@ __global__ void __launch_bounds__(BLOCK) k_sort_small(const uint32_t* __restrict
     long long keys[SMALL_SEG];
     for (uint32_t j = 0; j < len; ++j) {
       uint32_t v = carr[b + j];
-      long long k = sort_key[v];
+      long long k = sort_key(v);
       uint32_t p = j;
       while (p > 0 && keys[p - 1] > k) {
         keys[p] = keys[p - 1];
@@ -129,11 +140,12 @@ __global__ void __launch_bounds__(BLOCK) k_sort_small(const uint32_t* __restrict
 // One workgroup per large segment. Bitonic sort over the next power of two
 // in LDS (keys padded with +inf) when it fits; otherwise an in-HBM merge sort
 // with ping-pong through `scratch` (same offsets as carr).
+template <class KEY>
 __global__ void __launch_bounds__(1024) k_sort_big(const uint32_t* __restrict__ seg_start,
                                                     const uint32_t* __restrict__ big_list,
                                                     const uint32_t* __restrict__ n_big, uint32_t* __restrict__ carr,
                                                     uint32_t* __restrict__ scratch,
-                                                    const long long* __restrict__ sort_key) {
+                                                    KEY sort_key) {
   __shared__ long long skey[LDS_SORT_MAX];
   __shared__ uint32_t sid[LDS_SORT_MAX];
   const uint32_t nb = *n_big;
@@ -148,7 +160,7 @@ __global__ void __launch_bounds__(1024) k_sort_big(const uint32_t* __restrict__ 
         if (j < len) {
           uint32_t v = carr[b + j];
           sid[j] = v;
-          skey[j] = sort_key[v];
+          skey[j] = sort_key(v);
         } else {
           sid[j] = NONE;
           skey[j] = 0x7fffffffffffffffLL;
@@ -184,7 +196,7 @@ __global__ void __launch_bounds__(1024) k_sort_big(const uint32_t* __restrict__ 
           if (j < rl) {
             uint32_t v = carr[b + r0 + j];
             sid[j] = v;
-            skey[j] = sort_key[v];
+            skey[j] = sort_key(v);
           } else {
             sid[j] = NONE;
             skey[j] = 0x7fffffffffffffffLL;
@@ -226,7 +238,7 @@ __global__ void __launch_bounds__(1024) k_sort_big(const uint32_t* __restrict__ 
           uint32_t lo = d0 > nbb ? d0 - nbb : 0, hi = min(d0, na);
           while (lo < hi) {
             uint32_t mid = (lo + hi) >> 1;
-            if (sort_key[src[a0 + mid]] < sort_key[src[a1 + d0 - mid - 1]]) lo = mid + 1;
+            if (sort_key(src[a0 + mid]) < sort_key(src[a1 + d0 - mid - 1])) lo = mid + 1;
             else hi = mid;
           }
           uint32_t i = lo, j = d0 - lo;
@@ -234,7 +246,7 @@ __global__ void __launch_bounds__(1024) k_sort_big(const uint32_t* __restrict__ 
             bool takeA;
             if (i >= na) takeA = false;
             else if (j >= nbb) takeA = true;
-            else takeA = sort_key[src[a0 + i]] < sort_key[src[a1 + j]];
+            else takeA = sort_key(src[a0 + i]) < sort_key(src[a1 + j]);
             dst[m0 + d] = takeA ? src[a0 + i++] : src[a1 + j++];
           }
         }
@@ -252,8 +264,9 @@ __global__ void __launch_bounds__(1024) k_sort_big(const uint32_t* __restrict__ 
 
 // Huge segments (> LDS_SORT_MAX): chunk-sort in LDS, then merge passes with
 // merge-path partitioning, every pass spread over many workgroups.
+template <class KEY>
 __global__ void __launch_bounds__(1024) k_sort_chunks(uint32_t* __restrict__ carr, uint32_t b, uint32_t len,
-                                                       const long long* __restrict__ sort_key) {
+                                                       KEY sort_key) {
   __shared__ long long skey[LDS_SORT_MAX];
   __shared__ uint32_t sid[LDS_SORT_MAX];
   const uint32_t r0 = blockIdx.x * LDS_SORT_MAX;
@@ -262,7 +275,7 @@ __global__ void __launch_bounds__(1024) k_sort_chunks(uint32_t* __restrict__ car
     if (j < rl) {
       uint32_t v = carr[b + r0 + j];
       sid[j] = v;
-      skey[j] = sort_key[v];
+      skey[j] = sort_key(v);
     } else {
       sid[j] = NONE;
       skey[j] = 0x7fffffffffffffffLL;
@@ -294,9 +307,10 @@ __global__ void __launch_bounds__(1024) k_sort_chunks(uint32_t* __restrict__ car
 constexpr uint32_t MERGE_PER_THREAD = 8;
 constexpr uint32_t MERGE_TILE = BLOCK * MERGE_PER_THREAD;  // 2048 outputs per workgroup
 
+template <class KEY>
 __global__ void __launch_bounds__(BLOCK) k_merge_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                                       uint32_t len, uint32_t width,
-                                                      const long long* __restrict__ sort_key) {
+                                                      KEY sort_key) {
   const uint32_t d0 = blockIdx.x * MERGE_TILE + threadIdx.x * MERGE_PER_THREAD;
   if (d0 >= len) return;
   const uint32_t pair = d0 / (2 * width);
@@ -306,7 +320,7 @@ __global__ void __launch_bounds__(BLOCK) k_merge_pass(const uint32_t* __restrict
   uint32_t lo = d > nb ? d - nb : 0, hi = min(d, na);
   while (lo < hi) {  // merge path: #taken from A among the first d outputs
     const uint32_t mid = (lo + hi) >> 1;
-    if (sort_key[src[a0 + mid]] < sort_key[src[a1 + d - mid - 1]]) lo = mid + 1;
+    if (sort_key(src[a0 + mid]) < sort_key(src[a1 + d - mid - 1])) lo = mid + 1;
     else hi = mid;
   }
   uint32_t i = lo, j = d - lo;
@@ -315,7 +329,7 @@ __global__ void __launch_bounds__(BLOCK) k_merge_pass(const uint32_t* __restrict
     bool takeA;
     if (i >= na) takeA = false;
     else if (j >= nb) takeA = true;
-    else takeA = sort_key[src[a0 + i]] < sort_key[src[a1 + j]];
+    else takeA = sort_key(src[a0 + i]) < sort_key(src[a1 + j]);
     dst[a0 + q] = takeA ? src[a0 + i++] : src[a1 + j++];
   }
 }
@@ -330,17 +344,18 @@ __global__ void k_sort_big_filter(const uint32_t* __restrict__ seg_start, const 
   }
 }
 
-int segmented_sort(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items,
-                   const long long* sort_key, Arena& ws, hipStream_t st, DevResult* dres) {
+template <class KEY>
+static int segmented_sort_t(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items, KEY sort_key,
+                            Arena& ws, hipStream_t st, DevResult* dres) {
   uint32_t* big = ws.alloc<uint32_t>(n_seg + 1);
   uint32_t* huge = ws.alloc<uint32_t>(n_seg + 1);
   uint32_t* scratch = ws.alloc<uint32_t>(n_items + 1);
   uint32_t* nbig = &dres->big_segments;
   uint32_t* nhuge = &dres->huge_segments;
   HIP_CHECK(hipMemsetAsync(nbig, 0, 2 * sizeof(uint32_t), st));  // big_segments, huge_segments
-  LAUNCH(k_sort_small, dim3(grid_for(n_seg)), dim3(BLOCK), 0, st, seg_start, n_seg, carr, sort_key, big, nbig);
+  LAUNCH(k_sort_small<KEY>, dim3(grid_for(n_seg)), dim3(BLOCK), 0, st, seg_start, n_seg, carr, sort_key, big, nbig);
   // segments of 17..LDS_SORT_MAX: one workgroup each (huge ones are skipped there)
-  LAUNCH(k_sort_big, dim3(512), dim3(1024), 0, st, seg_start, big, nbig, carr, scratch, sort_key);
+  LAUNCH(k_sort_big<KEY>, dim3(512), dim3(1024), 0, st, seg_start, big, nbig, carr, scratch, sort_key);
   LAUNCH(k_sort_big_filter, dim3(16), dim3(BLOCK), 0, st, seg_start, big, nbig, huge, nhuge);
   uint32_t nh = 0;
   HIP_CHECK(hipMemcpyAsync(&nh, nhuge, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -352,11 +367,11 @@ int segmented_sort(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, ui
     uint32_t se[2];
     HIP_CHECK(hipMemcpy(se, seg_start + u, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
     const uint32_t b = se[0], len = se[1] - se[0];
-    LAUNCH(k_sort_chunks, dim3((len + LDS_SORT_MAX - 1) / LDS_SORT_MAX), dim3(1024), 0, st, carr, b, len, sort_key);
+    LAUNCH(k_sort_chunks<KEY>, dim3((len + LDS_SORT_MAX - 1) / LDS_SORT_MAX), dim3(1024), 0, st, carr, b, len, sort_key);
     uint32_t* src = carr + b;
     uint32_t* dst = scratch + b;
     for (uint32_t w = LDS_SORT_MAX; w < len; w <<= 1) {
-      LAUNCH(k_merge_pass, dim3((len + MERGE_TILE - 1) / MERGE_TILE), dim3(BLOCK), 0, st, src, dst, len, w,
+      LAUNCH(k_merge_pass<KEY>, dim3((len + MERGE_TILE - 1) / MERGE_TILE), dim3(BLOCK), 0, st, src, dst, len, w,
              sort_key);
       std::swap(src, dst);
     }
@@ -364,6 +379,16 @@ int segmented_sort(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, ui
       HIP_CHECK(hipMemcpyAsync(carr + b, src, len * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
   }
   return CRDTM_OK;
+}
+
+int segmented_sort(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items,
+                   const long long* sort_key, Arena& ws, hipStream_t st, DevResult* dres) {
+  return segmented_sort_t(seg_start, n_seg, carr, n_items, ArrKey{sort_key}, ws, st, dres);
+}
+
+int segmented_sort_desc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items, Arena& ws,
+                           hipStream_t st, DevResult* dres) {
+  return segmented_sort_t(seg_start, n_seg, carr, n_items, NegIdKey{}, ws, st, dres);
 }
 
 // ---------------------------------------------------------------------------
@@ -484,8 +509,179 @@ static int list_rank_level(const uint2* ent, const uint32_t* succ, const unsigne
   return CRDTM_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Local contraction (before the sublist ranking). Lists built over slot
+// numbering have strong memory locality: a typing run's Euler entries are
+// consecutive. A workgroup takes a tile of LC_T consecutive entries, finds
+// the pieces of the list that stay inside the tile (local chains) by
+// pointer jumping in LDS, and emits one contracted node per local chain
+// (weight = chain total, successor = the chain that follows its tail).
+// The contracted list (≈ LC_T / chains-per-tile times shorter) is ranked by
+// the sublist method; each entry's rank = its chain's rank + its prefix
+// inside the chain. A cycle inside a tile (never on a valid list) leaves
+// its entries unranked (~0), like entries off the list.
+// ---------------------------------------------------------------------------
+constexpr uint32_t LC_T = 1024;
+constexpr uint32_t LC_PER = LC_T / BLOCK;
+constexpr uint64_t LC_MIN = 1ULL << 16;  // shorter lists go straight to the sublist method
+
+__global__ void __launch_bounds__(BLOCK) k_lc_contract(const uint2* __restrict__ ent, uint64_t n,
+                                                       uint32_t* __restrict__ hidx,
+                                                       unsigned long long* __restrict__ pre,
+                                                       uint32_t* __restrict__ n_heads, uint32_t* __restrict__ rsucc,
+                                                       unsigned long long* __restrict__ rw) {
+  __shared__ uint32_t P[LC_T];
+  __shared__ unsigned long long V[LC_T];
+  __shared__ uint32_t W[LC_T];
+  __shared__ uint32_t hbase;
+  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * LC_T;
+#pragma unroll
+  for (uint32_t k = 0; k < LC_PER; ++k) P[threadIdx.x + k * BLOCK] = NONE;
+  __syncthreads();
+  uint32_t sc[LC_PER];
+#pragma unroll
+  for (uint32_t k = 0; k < LC_PER; ++k) {
+    const uint32_t l = threadIdx.x + k * BLOCK;
+    const uint64_t e = base + l;
+    const uint2 x = e < n ? ent[e] : make_uint2(ABSENT, 0u);
+    sc[k] = x.x;
+    W[l] = x.y;
+    if (x.x < n && x.x >= base && x.x < base + LC_T) P[x.x - base] = l;  // my successor's local predecessor
+  }
+  __syncthreads();
+  uint32_t p[LC_PER];
+  unsigned long long v[LC_PER];
+#pragma unroll
+  for (uint32_t k = 0; k < LC_PER; ++k) {
+    const uint32_t l = threadIdx.x + k * BLOCK;
+    p[k] = P[l];
+    v[k] = p[k] != NONE ? lr_weight(W[p[k]]) : 0ULL;
+    V[l] = v[k];
+  }
+  __syncthreads();
+  // Wyllie pointer jumping toward the chain head (<= log2(LC_T) rounds)
+  for (uint32_t round = 0; round <= 10; ++round) {
+    bool ch = false;
+#pragma unroll
+    for (uint32_t k = 0; k < LC_PER; ++k) {
+      if (p[k] == NONE) continue;
+      const uint32_t pp = P[p[k]];
+      if (pp != NONE) {
+        v[k] += V[p[k]];
+        p[k] = pp;
+        ch = true;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < LC_PER; ++k) {
+      const uint32_t l = threadIdx.x + k * BLOCK;
+      P[l] = p[k];
+      V[l] = v[k];
+    }
+    if (!__syncthreads_or(ch)) break;
+  }
+  // heads: present entries without a local predecessor; number them densely
+  uint32_t nh = 0;
+  bool head[LC_PER], cyc[LC_PER];
+#pragma unroll
+  for (uint32_t k = 0; k < LC_PER; ++k) {
+    const bool present = sc[k] != ABSENT;
+    cyc[k] = present && p[k] != NONE && P[p[k]] != NONE;  // still jumping: a cycle
+    head[k] = present && p[k] == NONE;
+    nh += head[k] ? 1u : 0u;
+  }
+  __syncthreads();
+  // block exclusive sum of nh (wave scan + LDS)
+  __shared__ uint32_t sw[BLOCK / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t inc = wave_incl_scan(nh);
+  if (lane == 63) sw[wave] = inc;
+  __syncthreads();
+  uint32_t off = inc - nh, tot = 0;
+  for (int w = 0; w < BLOCK / 64; ++w) {
+    if (w < wave) off += sw[w];
+    tot += sw[w];
+  }
+  if (threadIdx.x == 0) hbase = tot ? atomicAdd(n_heads, tot) : 0u;
+  __syncthreads();
+  // P[l] := hid of l when l is a head
+#pragma unroll
+  for (uint32_t k = 0; k < LC_PER; ++k) {
+    if (head[k]) P[threadIdx.x + k * BLOCK] = hbase + off++;
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < LC_PER; ++k) {
+    const uint32_t l = threadIdx.x + k * BLOCK;
+    const uint64_t e = base + l;
+    if (e >= n) continue;
+    if (sc[k] == ABSENT || cyc[k]) {
+      hidx[e] = NONE;
+      continue;
+    }
+    const uint32_t h = P[head[k] ? l : p[k]];
+    hidx[e] = h;
+    pre[e] = v[k];
+    const uint32_t s = sc[k];
+    if (!(s < n && s >= base && s < base + LC_T)) {  // tail of its local chain
+      rw[h] = v[k] + lr_weight(W[l]);
+      rsucc[h] = s;  // entry id of the next chain's head (or NONE); translated by k_lc_link
+    }
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_lc_link(const uint32_t* __restrict__ n_heads,
+                                                   const uint32_t* __restrict__ hidx, uint32_t* __restrict__ rsucc) {
+  const uint32_t H = *n_heads;
+  for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < H; h += gridDim.x * blockDim.x) {
+    const uint32_t s = rsucc[h];
+    rsucc[h] = s == NONE ? NONE : hidx[s];
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_lc_expand(uint64_t n, const uint32_t* __restrict__ hidx,
+                                                     const unsigned long long* __restrict__ pre,
+                                                     const unsigned long long* __restrict__ rexcl,
+                                                     unsigned long long* __restrict__ excl) {
+  for (uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; e < n;
+       e += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint32_t h = hidx[e];
+    unsigned long long r = ~0ULL;
+    if (h != NONE) {
+      const unsigned long long b = rexcl[h];
+      if (b != ~0ULL) r = b + pre[e];
+    }
+    excl[e] = r;
+  }
+}
+
 int list_rank(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws, hipStream_t st) {
-  return list_rank_level(ent, nullptr, nullptr, n, head, excl, ws, st, 0);
+  if (n < LC_MIN || n >= 0xFFFFFFF0ULL) return list_rank_level(ent, nullptr, nullptr, n, head, excl, ws, st, 0);
+  const uint64_t tiles = (n + LC_T - 1) / LC_T;
+  uint32_t* hidx = ws.alloc<uint32_t>(n);
+  unsigned long long* pre = ws.alloc<unsigned long long>(n);
+  // contracted list: at most one node per entry
+  uint32_t* rsucc = ws.alloc<uint32_t>(n + 1);
+  unsigned long long* rw = ws.alloc<unsigned long long>(n + 1);
+  uint32_t* cnt = ws.alloc<uint32_t>(2);  // [0] heads, [1] contracted head id
+  HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), st));
+  LAUNCH(k_lc_contract, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, ent, n, hidx, pre, cnt, rsucc, rw);
+  LAUNCH(k_lc_link, dim3(grid_for(n / 4 + 1)), dim3(BLOCK), 0, st, cnt, hidx, rsucc);
+  uint32_t hv[2] = {0, NONE};
+  HIP_CHECK(hipMemcpyAsync(&hv[0], cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipMemcpyAsync(&hv[1], hidx + head, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  const uint32_t H = hv[0], rhead = hv[1];
+  unsigned long long* rexcl = ws.alloc<unsigned long long>(static_cast<uint64_t>(H) + 1);
+  if (H == 0 || rhead == NONE) {
+    HIP_CHECK(hipMemsetAsync(excl, 0xFF, n * sizeof(unsigned long long), st));
+    return CRDTM_OK;
+  }
+  int r = list_rank_level(nullptr, rsucc, rw, H, rhead, rexcl, ws, st, 1);
+  if (r) return r;
+  LAUNCH(k_lc_expand, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, hidx, pre, rexcl, excl);
+  return CRDTM_OK;
 }
 
 }  // namespace crdtm
