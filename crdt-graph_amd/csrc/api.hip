@@ -90,7 +90,13 @@ void dump_dict(const HostTree& h, uint32_t d, int64_t depth, Sink& s) {
     s.put(nx != NONE ? h.key[nx] : 0);
     s.put(tomb ? 0 : static_cast<int64_t>(h.l_val[h.src[x]]));
     put_path(h, h.src[x], s);
-    if (!tomb && h.child[x] != NONE) dump_dict(h, h.child[x], depth + 1, s);
+    if (tomb) continue;
+    if (h.child[x] != NONE) {
+      dump_dict(h, h.child[x], depth + 1, s);
+    } else {  // implicit children {0: Tombstone [] Nothing}: its sentinel entry
+      const int64_t sent[] = {depth + 1, 0, 2, 0, 0, 0, 0};
+      for (int64_t w : sent) s.put(w);
+    }
   }
 }
 
@@ -106,6 +112,40 @@ void dump_visible(const HostTree& h, uint32_t d, int64_t depth, Sink& s) {
     if (h.child[nx] != NONE) dump_visible(h, h.child[nx], depth + 1, s);
     cur = nx;
   }
+}
+
+// The per-op kernels load 4 ops per lane with 16-byte vector loads; device
+// inputs that are not aligned for that are staged into the (aligned) arena.
+int align_ops(crdtm_ctx* c, OpsDev& o) {
+  auto mis = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) != 0; };
+  hipStream_t s = c->stream;
+  const uint64_t n = o.n;
+  if (mis(o.kind, 4)) {
+    auto* k = c->ws.alloc<uint8_t>(n + 1);
+    HIP_CHECK(hipMemcpyAsync(k, o.kind, n, hipMemcpyDeviceToDevice, s));
+    o.kind = k;
+  }
+  if (mis(o.ts, 16)) {
+    auto* t = c->ws.alloc<long long>(n + 1);
+    HIP_CHECK(hipMemcpyAsync(t, o.ts, n * 8, hipMemcpyDeviceToDevice, s));
+    o.ts = t;
+  }
+  if (mis(o.off, 16)) {
+    auto* f = c->ws.alloc<uint32_t>(n + 1);
+    HIP_CHECK(hipMemcpyAsync(f, o.off, (n + 1) * 4, hipMemcpyDeviceToDevice, s));
+    o.off = f;
+  }
+  if (mis(o.path, 16)) {
+    auto* p = c->ws.alloc<long long>(o.n_path + 1);
+    if (o.n_path) HIP_CHECK(hipMemcpyAsync(p, o.path, o.n_path * 8, hipMemcpyDeviceToDevice, s));
+    o.path = p;
+  }
+  if (mis(o.val, 16)) {
+    auto* v = c->ws.alloc<uint32_t>(n + 1);
+    HIP_CHECK(hipMemcpyAsync(v, o.val, n * 4, hipMemcpyDeviceToDevice, s));
+    o.val = v;
+  }
+  return CRDTM_OK;
 }
 
 uint64_t arena_need(uint64_t n, uint64_t np, const crdtm_tree* t) {
@@ -323,6 +363,7 @@ int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_b
         o.path = reinterpret_cast<const long long*>(ops->path);
         o.val = ops->val;
         st_dev = status_out;
+        if ((r = align_ops(c, o))) return r;
       } else {
         hipStream_t s = c->stream;
         auto* kind = c->ws.alloc<uint8_t>(n + 1);
@@ -518,6 +559,7 @@ int crdtm_forest_apply(crdtm_ctx* c, int64_t replica_id, const crdtm_ops* ops, c
       o.off = ops->path_off;
       o.path = reinterpret_cast<const long long*>(ops->path);
       o.val = ops->val;
+      if ((r = align_ops(c, o))) return r;
     } else {
       hipStream_t s = c->stream;
       auto* kind = c->ws.alloc<uint8_t>(n + 1);

@@ -62,6 +62,7 @@ struct DevResult {
   uint32_t n_split[8];      // list ranking level sizes
   uint32_t big_segments;
   uint32_t huge_segments;
+  uint32_t mid_segments;
   uint32_t last_add;        // 1 + index of the last applied Add
   uint32_t first_del;       // index of the first applied Delete
   uint32_t has_negative;    // some Add ts < 0 (dense index impossible)

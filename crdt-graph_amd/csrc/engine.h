@@ -42,7 +42,9 @@ constexpr uint32_t HOST_RANGES = 4096;  // replica ranges scanned on the host
 // slot of the entry named by its `next` key (Elm keeps the key; within a dict
 // the two are interchangeable); s_src is the op-log index of the Add whose
 // path and value the entry carries (a findInsertion copy carries the copied
-// node's source); s_child is the children dict of a live Node.
+// node's source); s_child is the children dict of a live Node,
+// or NONE for a live Node whose children are still the initial
+// {0: Tombstone} (implicit until something descends into it).
 struct TreeDev {
   long long* s_key = nullptr;
   uint32_t* s_next = nullptr;
@@ -101,11 +103,16 @@ namespace crdtm {
 int scan_excl_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* total, Arena& ws, hipStream_t st);
 int segmented_sort(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items,
                    const long long* sort_key, Arena& ws, hipStream_t st, DevResult* dres);
-// same, ordering items by descending id (timestamp-slot numbering)
+// same, ordering items by descending id (timestamp-slot numbering); segment
+// `skip` is left alone (the caller orders it)
 int segmented_sort_desc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items, Arena& ws,
-                           hipStream_t st, DevResult* dres);
-// ent[e] = {succ, wbits}: see primitives.hip
+                           hipStream_t st, DevResult* dres, uint32_t skip);
+// ent[e] = {succ, wbits}: see primitives.hip / listrank.h (list_rank_fused)
 int list_rank(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws, hipStream_t st);
+int list_rank_packed(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws,
+                     hipStream_t st);
+int list_rank_unpacked(const uint32_t* succ, const unsigned long long* w, uint64_t n, uint32_t head,
+                       unsigned long long* excl, Arena& ws, hipStream_t st);
 
 // Device view of one batch of ops.
 struct OpsDev {

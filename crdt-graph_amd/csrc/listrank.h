@@ -1,0 +1,229 @@
+// listrank.h — list ranking front end with local contraction, templated on
+// where the list entries come from (SRC) and where the ranks go (SINK), so a
+// caller can build its list on the fly and consume ranks without
+// materialising either array.
+//
+// SRC:  __device__ uint2 operator()(uint64_t e) const -> {succ, wbits}
+//       (succ: NONE = end of list, ABSENT = entry not in any list;
+//        wbits bit1 -> high word +1, bit0 -> low word +1)
+// SINK: __device__ void operator()(uint64_t e, unsigned long long rank) const,
+//       called once for every entry on the list (rank = exclusive prefix of
+//       the weights along the list from `head`). ExclSink also writes ~0 for
+//       entries off the list.
+#pragma once
+
+#include "engine.h"
+
+namespace crdtm {
+
+__device__ __forceinline__ unsigned long long lr_weight(uint32_t wbits) {
+  return (static_cast<unsigned long long>((wbits >> 1) & 1u) << 32) | (wbits & 1u);
+}
+
+struct PackedSrc {
+  const uint2* ent;
+  __device__ __forceinline__ uint2 operator()(uint64_t e) const { return ent[e]; }
+};
+
+struct ExclSink {
+  unsigned long long* excl;
+  static constexpr bool kOffList = true;  // also told about entries off the list
+  __device__ __forceinline__ void operator()(uint64_t e, unsigned long long r) const { excl[e] = r; }
+};
+
+// ---------------------------------------------------------------------------
+// Local contraction. Lists built over slot numbering have strong memory
+// locality: a typing run's Euler entries are consecutive. A workgroup takes
+// a tile of LC_T consecutive entries, finds the pieces of the list that stay
+// inside the tile (local chains) by pointer jumping in LDS, and emits one
+// contracted node per local chain (weight = chain total, successor = the
+// chain that follows its tail). The contracted list is ranked by the
+// sublist method; each entry's rank = its chain's rank + its prefix inside
+// the chain. A cycle inside a tile (never on a valid list) leaves its
+// entries unranked, like entries off the list.
+// ---------------------------------------------------------------------------
+constexpr uint32_t LC_T = 1024;
+constexpr uint32_t LC_PER = LC_T / BLOCK;
+constexpr uint64_t LC_MIN = 1ULL << 16;  // shorter lists: sublist method on a materialised list
+
+template <class SRC>
+__global__ void __launch_bounds__(BLOCK) k_lc_contract(SRC srcf, uint64_t n, uint32_t* __restrict__ hidx,
+                                                       unsigned long long* __restrict__ pre,
+                                                       uint32_t* __restrict__ n_heads, uint32_t* __restrict__ rsucc,
+                                                       unsigned long long* __restrict__ rw) {
+  __shared__ uint32_t P[LC_T];
+  __shared__ unsigned long long V[LC_T];
+  __shared__ uint32_t W[LC_T];
+  __shared__ uint32_t sw[BLOCK / 64];
+  __shared__ uint32_t hbase;
+  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * LC_T;
+#pragma unroll
+  for (uint32_t k = 0; k < LC_PER; ++k) P[threadIdx.x + k * BLOCK] = NONE;
+  __syncthreads();
+  uint32_t sc[LC_PER];
+#pragma unroll
+  for (uint32_t k = 0; k < LC_PER; ++k) {
+    const uint32_t l = threadIdx.x + k * BLOCK;
+    const uint64_t e = base + l;
+    const uint2 x = e < n ? srcf(e) : make_uint2(ABSENT, 0u);
+    sc[k] = x.x;
+    W[l] = x.y;
+    if (x.x < n && x.x >= base && x.x < base + LC_T) P[x.x - base] = l;  // my successor's local predecessor
+  }
+  __syncthreads();
+  uint32_t p[LC_PER];
+  unsigned long long v[LC_PER];
+#pragma unroll
+  for (uint32_t k = 0; k < LC_PER; ++k) {
+    const uint32_t l = threadIdx.x + k * BLOCK;
+    p[k] = P[l];
+    v[k] = p[k] != NONE ? lr_weight(W[p[k]]) : 0ULL;
+    V[l] = v[k];
+  }
+  __syncthreads();
+  // Wyllie pointer jumping toward the chain head (<= log2(LC_T) rounds)
+  for (uint32_t round = 0; round <= 10; ++round) {
+    bool ch = false;
+#pragma unroll
+    for (uint32_t k = 0; k < LC_PER; ++k) {
+      if (p[k] == NONE) continue;
+      const uint32_t pp = P[p[k]];
+      if (pp != NONE) {
+        v[k] += V[p[k]];
+        p[k] = pp;
+        ch = true;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < LC_PER; ++k) {
+      const uint32_t l = threadIdx.x + k * BLOCK;
+      P[l] = p[k];
+      V[l] = v[k];
+    }
+    if (!__syncthreads_or(ch)) break;
+  }
+  // heads: present entries without a local predecessor; number them densely
+  uint32_t nh = 0;
+  bool head[LC_PER], cyc[LC_PER];
+#pragma unroll
+  for (uint32_t k = 0; k < LC_PER; ++k) {
+    const bool present = sc[k] != ABSENT;
+    cyc[k] = present && p[k] != NONE && P[p[k]] != NONE;  // still jumping: a cycle
+    head[k] = present && p[k] == NONE;
+    nh += head[k] ? 1u : 0u;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t inc = wave_incl_scan(nh);
+  if (lane == 63) sw[wave] = inc;
+  __syncthreads();
+  uint32_t off = inc - nh, tot = 0;
+  for (int w = 0; w < BLOCK / 64; ++w) {
+    if (w < wave) off += sw[w];
+    tot += sw[w];
+  }
+  if (threadIdx.x == 0) hbase = tot ? atomicAdd(n_heads, tot) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < LC_PER; ++k) {
+    if (head[k]) P[threadIdx.x + k * BLOCK] = hbase + off++;  // P[head] := its contracted id
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < LC_PER; ++k) {
+    const uint32_t l = threadIdx.x + k * BLOCK;
+    const uint64_t e = base + l;
+    if (e >= n) continue;
+    if (sc[k] == ABSENT || cyc[k]) {
+      hidx[e] = NONE;
+      continue;
+    }
+    const uint32_t h = P[head[k] ? l : p[k]];
+    hidx[e] = h;
+    pre[e] = v[k];
+    const uint32_t s = sc[k];
+    if (!(s < n && s >= base && s < base + LC_T)) {  // tail of its local chain
+      rw[h] = v[k] + lr_weight(W[l]);
+      rsucc[h] = s;  // entry id of the next chain's head (or NONE); translated by k_lc_link
+    }
+  }
+}
+
+static __global__ void __launch_bounds__(BLOCK) k_lc_link(const uint32_t* __restrict__ n_heads,
+                                                   const uint32_t* __restrict__ hidx, uint32_t* __restrict__ rsucc) {
+  const uint32_t H = *n_heads;
+  for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < H; h += gridDim.x * blockDim.x) {
+    const uint32_t s = rsucc[h];
+    rsucc[h] = s == NONE ? NONE : hidx[s];
+  }
+}
+
+template <class SINK>
+__global__ void __launch_bounds__(BLOCK) k_lc_expand(uint64_t n, const uint32_t* __restrict__ hidx,
+                                                     const unsigned long long* __restrict__ pre,
+                                                     const unsigned long long* __restrict__ rexcl, SINK sink) {
+  for (uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; e < n;
+       e += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint32_t h = hidx[e];
+    const unsigned long long b = h != NONE ? rexcl[h] : ~0ULL;
+    if (b != ~0ULL) sink(e, b + pre[e]);
+    else if (SINK::kOffList) sink(e, ~0ULL);
+  }
+}
+
+template <class SRC>
+__global__ void __launch_bounds__(BLOCK) k_lr_materialise(SRC srcf, uint64_t n, uint2* ent) {
+  for (uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; e < n;
+       e += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    ent[e] = srcf(e);
+}
+
+template <class SINK>
+__global__ void __launch_bounds__(BLOCK) k_lr_sink(uint64_t n, const unsigned long long* __restrict__ excl,
+                                                   SINK sink) {
+  for (uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; e < n;
+       e += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const unsigned long long r = excl[e];
+    if (r != ~0ULL || SINK::kOffList) sink(e, r);
+  }
+}
+
+template <class SRC, class SINK>
+int list_rank_fused(SRC srcf, uint64_t n, uint32_t head, SINK sink, Arena& ws, hipStream_t st) {
+  if (n < LC_MIN || n >= 0xFFFFFFF0ULL) {
+    uint2* ent = ws.alloc<uint2>(n);
+    unsigned long long* excl = ws.alloc<unsigned long long>(n);
+    LAUNCH(k_lr_materialise<SRC>, dim3(grid_for(n)), dim3(BLOCK), 0, st, srcf, n, ent);
+    int r = list_rank_packed(ent, n, head, excl, ws, st);
+    if (r) return r;
+    LAUNCH(k_lr_sink<SINK>, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, excl, sink);
+    return CRDTM_OK;
+  }
+  const uint64_t tiles = (n + LC_T - 1) / LC_T;
+  uint32_t* hidx = ws.alloc<uint32_t>(n);
+  unsigned long long* pre = ws.alloc<unsigned long long>(n);
+  uint32_t* rsucc = ws.alloc<uint32_t>(n + 1);  // contracted list: at most one node per entry
+  unsigned long long* rw = ws.alloc<unsigned long long>(n + 1);
+  uint32_t* cnt = ws.alloc<uint32_t>(2);
+  HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), st));
+  LAUNCH(k_lc_contract<SRC>, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, srcf, n, hidx, pre, cnt, rsucc,
+         rw);
+  LAUNCH(k_lc_link, dim3(grid_for(n / 4 + 1)), dim3(BLOCK), 0, st, cnt, hidx, rsucc);
+  uint32_t hv[2] = {0, NONE};
+  HIP_CHECK(hipMemcpyAsync(&hv[0], cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipMemcpyAsync(&hv[1], hidx + head, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  const uint32_t H = hv[0], rhead = hv[1];
+  unsigned long long* rexcl = ws.alloc<unsigned long long>(static_cast<uint64_t>(H) + 1);
+  if (H == 0 || rhead == NONE) {
+    HIP_CHECK(hipMemsetAsync(rexcl, 0xFF, (static_cast<uint64_t>(H) + 1) * sizeof(unsigned long long), st));
+  } else {
+    int r = list_rank_unpacked(rsucc, rw, H, rhead, rexcl, ws, st);
+    if (r) return r;
+  }
+  LAUNCH(k_lc_expand<SINK>, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, hidx, pre, rexcl, sink);
+  return CRDTM_OK;
+}
+
+}  // namespace crdtm

@@ -15,6 +15,7 @@
 // DESIGN.md derives the closed form and its guard.
 
 #include "engine.h"
+#include "listrank.h"
 
 namespace crdtm {
 
@@ -33,6 +34,83 @@ struct Work {  // per-call device arrays of the closed form (sized by n ops)
 };
 
 __device__ __forceinline__ uint32_t op_len(const OpsDev& o, uint32_t i) { return o.off[i + 1] - o.off[i]; }
+
+// Four consecutive ops per lane, loaded with 16-byte vector loads (device
+// inputs are 16-byte aligned: api.hip align_ops); the tail quad falls back
+// to guarded scalar loads. Consecutive lanes take consecutive quads.
+struct Quad {
+  uint32_t cnt;  // valid ops (1..4)
+  uint8_t kind[4];
+  long long ts[4];
+  uint32_t off[5];
+};
+
+__device__ __forceinline__ void load_quad(const OpsDev& o, uint32_t i0, Quad& q) {
+  if (i0 + 4 <= o.n) {
+    q.cnt = 4;
+    const uchar4 k = *reinterpret_cast<const uchar4*>(o.kind + i0);
+    q.kind[0] = k.x;
+    q.kind[1] = k.y;
+    q.kind[2] = k.z;
+    q.kind[3] = k.w;
+    const longlong2 a = *reinterpret_cast<const longlong2*>(o.ts + i0);
+    const longlong2 b = *reinterpret_cast<const longlong2*>(o.ts + i0 + 2);
+    q.ts[0] = a.x;
+    q.ts[1] = a.y;
+    q.ts[2] = b.x;
+    q.ts[3] = b.y;
+    const uint4 f = *reinterpret_cast<const uint4*>(o.off + i0);
+    q.off[0] = f.x;
+    q.off[1] = f.y;
+    q.off[2] = f.z;
+    q.off[3] = f.w;
+    q.off[4] = o.off[i0 + 4];
+  } else {
+    q.cnt = o.n - i0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const bool v = k < q.cnt;
+      q.kind[k] = v ? o.kind[i0 + k] : 0;
+      q.ts[k] = v ? o.ts[i0 + k] : 0;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 5; ++k) q.off[k] = k <= q.cnt ? o.off[i0 + k] : 0;  // static indices: no scratch
+  }
+}
+
+__device__ __forceinline__ void store_quad_u8(uint8_t* p, uint32_t i0, uint32_t cnt, const uint8_t v[4]) {
+  if (cnt == 4) {
+    *reinterpret_cast<uchar4*>(p + i0) = make_uchar4(v[0], v[1], v[2], v[3]);
+  } else {
+    for (uint32_t k = 0; k < cnt; ++k) p[i0 + k] = v[k];
+  }
+}
+
+// Quads are strided over the grid: the blocks in flight cover one contiguous
+// front of ops, so the slot-space lines that the ops of one replica touch
+// (consecutive counters) are shared by concurrent blocks and stay cached.
+#define QUAD_LOOP(i0, n)                                                                           \
+  for (uint32_t i0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x); i0 < (n); i0 += 4 * gridDim.x * blockDim.x)
+
+// XCD-chunked variant for kernels that scatter into slot space: the front is
+// cut into 8 chunks, chunk j on the blocks with blockIdx % 8 == j % 8 (the
+// hardware's round-robin XCD placement; speed only). A replica's consecutive
+// ops within a chunk then write whole slot lines from ONE L2 instead of
+// leaving partial lines in eight (measured: 7x write amplification).
+#define QUAD_LOOP_XCD(i0, n)                                                                       \
+  const uint32_t nq_ = ((n) + 3) / 4;                                                              \
+  const bool x8_ = (gridDim.x & 7) == 0;                                                           \
+  const uint32_t xc_ = x8_ ? blockIdx.x & 7 : 0, xy_ = x8_ ? blockIdx.x >> 3 : blockIdx.x;         \
+  const uint32_t cq_ = (x8_ ? gridDim.x >> 3 : gridDim.x) * blockDim.x, xs_ = x8_ ? 8 : 1;         \
+  for (uint32_t j_ = xc_, qd_ = xc_ * cq_ + xy_ * blockDim.x + threadIdx.x, i0 = 4 * qd_;         \
+       j_ * cq_ < nq_; j_ += xs_, qd_ = j_ * cq_ + xy_ * blockDim.x + threadIdx.x, i0 = 4 * qd_)   \
+    if (qd_ < nq_)
+
+inline uint32_t quad_grid(uint64_t n) {
+  const uint64_t g = (((n + 3) / 4) + BLOCK - 1) / BLOCK;
+  if (g >= 2048) return 2048;
+  return g < 8 ? static_cast<uint32_t>(g ? g : 1) : static_cast<uint32_t>((g + 7) & ~7ULL);
+}
 
 // block-level OR/MAX reduction helpers (one atomic per block)
 __device__ __forceinline__ uint32_t block_max(uint32_t v) {
@@ -90,40 +168,45 @@ __global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint32_t* cmin, uint32_
   }
   __syncthreads();
   uint32_t mx = 0, bad = 0, neg = 0, ndel = 0, maxr = 0;
-  const uint32_t n = o.n;
-  const uint32_t chunk = (n + gridDim.x - 1) / gridDim.x;
-  const uint32_t b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
-  for (uint32_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
-    const uint32_t L = op_len(o, i);
-    mx = max(mx, L);
-    const bool add = o.kind[i] == CRDTM_ADD;
-    if (!add) {
-      ++ndel;
-      continue;
-    }
-    const long long ts = o.ts[i];
-    if (ts >= TWO53 || ts <= -TWO53) {
-      bad = 1;
-    } else if (ts < 0) {
-      neg = 1;
-    } else if (L >= 1 && ts != 0) {
-      const uint32_t r = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32), c = static_cast<uint32_t>(ts);
-      maxr = max(maxr, r);
-      if (r < REP_DIRECT) {
-        atomicMin(&rlo[r], c);
-        atomicMax(&rhi[r], c);
-      } else {
-        atomicMin(&cmin[r], c);
-        atomicMax(&cmax[r], c);
+  QUAD_LOOP(i0, o.n) {
+    Quad q;
+    load_quad(o, i0, q);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      if (k >= q.cnt) break;
+      const uint32_t L = q.off[k + 1] - q.off[k];
+      mx = max(mx, L);
+      if (q.kind[k] != CRDTM_ADD) {
+        ++ndel;
+        continue;
+      }
+      const long long ts = q.ts[k];
+      if (ts >= TWO53 || ts <= -TWO53) {
+        bad = 1;
+      } else if (ts < 0) {
+        neg = 1;
+      } else if (L >= 1 && ts != 0) {
+        const uint32_t r = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32), c = static_cast<uint32_t>(ts);
+        maxr = max(maxr, r);
+        if (r < REP_DIRECT) {
+          atomicMin(&rlo[r], c);
+          atomicMax(&rhi[r], c);
+        } else {
+          atomicMin(&cmin[r], c);
+          atomicMax(&cmax[r], c);
+        }
       }
     }
   }
-  // path elements (the same chunking over the path array)
-  const uint64_t np = o.n_path;
-  const uint64_t pchunk = (np + gridDim.x - 1) / gridDim.x;
-  const uint64_t p0 = blockIdx.x * pchunk, p1 = min(np, p0 + pchunk);
-  for (uint64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
-    const long long v = o.path[p];
+  // path elements: 16-byte loads over an even-aligned range
+  const uint64_t np = o.n_path, npair = np / 2;
+  for (uint64_t p = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; p < npair;
+       p += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const longlong2 v = *reinterpret_cast<const longlong2*>(o.path + 2 * p);
+    if (v.x >= TWO53 || v.x <= -TWO53 || v.y >= TWO53 || v.y <= -TWO53) bad = 1;
+  }
+  if ((np & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const long long v = o.path[np - 1];
     if (v >= TWO53 || v <= -TWO53) bad = 1;
   }
   __syncthreads();
@@ -179,20 +262,29 @@ __global__ void __launch_bounds__(BLOCK) k_index_insert(OpsDev o, TsIndex x) {
 // win takes an atomicMin, so the slot ends as the first Add of that
 // timestamp. Batches without duplicate timestamps pay no atomic at all.
 __global__ void __launch_bounds__(BLOCK) k_index_store(OpsDev o, TsIndex x) {
-  GRID_STRIDE(i, o.n) {
-    if (o.kind[i] != CRDTM_ADD || op_len(o, i) == 0) continue;
-    const long long ts = o.ts[i];
-    if (ts > 0) x.first[tsindex_slot(x, ts)] = i;
+  QUAD_LOOP_XCD(i0, o.n) {
+    Quad q;
+    load_quad(o, i0, q);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      if (k >= q.cnt) break;
+      if (q.kind[k] == CRDTM_ADD && q.off[k + 1] != q.off[k] && q.ts[k] > 0)
+        x.first[tsindex_slot(x, q.ts[k])] = i0 + k;
+    }
   }
 }
 
 __global__ void __launch_bounds__(BLOCK) k_index_fix(OpsDev o, TsIndex x) {
-  GRID_STRIDE(i, o.n) {
-    if (o.kind[i] != CRDTM_ADD || op_len(o, i) == 0) continue;
-    const long long ts = o.ts[i];
-    if (ts <= 0) continue;
-    uint32_t* f = &x.first[tsindex_slot(x, ts)];
-    if (*f != i) atomicMin(f, i);
+  QUAD_LOOP_XCD(i0, o.n) {
+    Quad q;
+    load_quad(o, i0, q);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      if (k >= q.cnt) break;
+      if (q.kind[k] != CRDTM_ADD || q.off[k + 1] == q.off[k] || q.ts[k] <= 0) continue;
+      uint32_t* f = &x.first[tsindex_slot(x, q.ts[k])];
+      if (*f != i0 + k) atomicMin(f, i0 + k);
+    }
   }
 }
 
@@ -792,6 +884,18 @@ struct Replayer {
     return d;
   }
 
+  // The children dict of live node s, created on first use: a dict holding
+  // only its sentinel (emptyChildren, src/Internal/Node.elm:46-48).
+  __device__ uint32_t materialise(uint32_t s) {
+    const uint32_t dd = new_dict(s);
+    if (dd == NONE) return NONE;
+    const uint32_t ss = new_slot(dd, 0, NONE, NONE, NONE, F_TOMB | F_SENT);
+    if (ss == NONE) return NONE;
+    a.T.d_sent[dd] = ss;
+    set_child(s, dd);
+    return dd;
+  }
+
   // Persistent copy of dict `src` (and every dict below it) into `dst`.
   __device__ void deep_copy(uint32_t src, uint32_t dst) {
     uint32_t qh = 0, qt = 0;
@@ -837,6 +941,10 @@ struct Replayer {
       if (s == NONE) return ST_INVALID;
       if (a.T.s_flags[s] & F_TOMB) return ST_ALREADY;
       d = a.T.s_child[s];
+      if (d == NONE) {  // an implicit empty children dict: materialise it
+        d = materialise(s);
+        if (d == NONE) return ST_PENDING;
+      }
     }
     const long long k = o.path[b + L - 1];
     if (o.kind[i] == CRDTM_DELETE) {  // deleteHelp
@@ -864,14 +972,10 @@ struct Replayer {
       nkey = rk;
       node = live;
     }
+    // the new Node's children {0: Tombstone} (src/Internal/Node.elm:85) stay
+    // implicit until something descends into it
     const uint32_t x = new_slot(d, ts, a.T.s_next[node], a.src_is_op ? i : a.log_base + applied, NONE, 0);
     if (x == NONE) return ST_PENDING;
-    const uint32_t dd = new_dict(x);
-    if (dd == NONE) return ST_PENDING;
-    a.T.s_child[x] = dd;
-    const uint32_t ss = new_slot(dd, 0, NONE, NONE, NONE, F_TOMB | F_SENT);
-    if (ss == NONE) return ST_PENDING;
-    a.T.d_sent[dd] = ss;
     const uint32_t ls = slothash_find(a.H, d, nkey);
     // x is reachable from the dict's sentinel iff its predecessor is (an Add
     // anchored at an orphan hangs off the chain)
@@ -1155,33 +1259,95 @@ __global__ void __launch_bounds__(64) k_forest(OpsDev o, ForestArgs f, const uin
 // ---------------------------------------------------------------------------
 
 // K1 (flat): status of every op; applied Adds record their anchor slot.
-__global__ void __launch_bounds__(BLOCK) k_fl_status(OpsDev o, uint8_t* st, TsIndex x, uint32_t Q, uint32_t* anc) {
-  GRID_STRIDE(i, o.n) {
-    const uint32_t L = op_len(o, i);
-    uint8_t s;
-    if (L == 0) {
-      s = ST_INVALID;  // update [] = InvalidPath (src/Internal/Node.elm:147-148)
-    } else {
-      const uint32_t q = tsindex_slot(x, o.ts[i]);
-      if (q == NONE || x.first[q] != i) {
-        s = ST_ALREADY;  // ts 0 is the sentinel's key / `child ts parent` exists (:63-65)
+// Fused with the batch accounting (k_stats) and the replicas fold: every
+// applied Add's replica keeps its last op index in a direct-mapped LDS table
+// (ids < REP_DIRECT), flushed once per block into the replica table.
+__global__ void __launch_bounds__(BLOCK) k_fl_status(OpsDev o, uint8_t* st, TsIndex x, uint32_t Q, uint32_t* anc,
+                                                     long long ts0, uint32_t* rtab, DevResult* dres) {
+  __shared__ uint32_t rv[REP_DIRECT];
+  for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) rv[j] = 0;
+  __syncthreads();
+  const long long id0 = replica_of(ts0);
+  uint32_t app = 0, alr = 0, own = 0, err = NONE;
+  QUAD_LOOP_XCD(i0, o.n) {
+    Quad qd;
+    load_quad(o, i0, qd);
+    uint8_t s4[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      if (k >= qd.cnt) break;
+      const uint32_t i = i0 + k;
+      uint8_t s;
+      const long long ts = qd.ts[k];
+      if (qd.off[k + 1] == qd.off[k]) {
+        s = ST_INVALID;  // update [] = InvalidPath (src/Internal/Node.elm:147-148)
       } else {
-        const long long k = o.path[o.off[i]];
-        uint32_t a = Q;  // anchor 0 = the dict's sentinel
-        if (k != 0) {
-          const uint32_t qa = tsindex_slot(x, k);
-          const uint32_t fa = qa == NONE ? NONE : x.first[qa];
-          a = (fa != NONE && fa < i) ? qa : NONE;  // anchor must exist before op i (:68-70)
-        }
-        if (a == NONE) {
-          s = ST_NOTFOUND;
+        const uint32_t q = tsindex_slot(x, ts);
+        if (q == NONE || x.first[q] != i) {
+          s = ST_ALREADY;  // ts 0 is the sentinel's key / `child ts parent` exists (:63-65)
         } else {
-          s = ST_APPLIED;
-          anc[q] = a;
+          const long long kk = o.path[qd.off[k]];
+          uint32_t a = Q;  // anchor 0 = the dict's sentinel
+          if (kk != 0) {
+            const uint32_t qa = tsindex_slot(x, kk);
+            const uint32_t fa = qa == NONE ? NONE : x.first[qa];
+            a = (fa != NONE && fa < i) ? qa : NONE;  // the anchor must exist before op i (:68-70)
+          }
+          if (a == NONE) {
+            s = ST_NOTFOUND;
+          } else {
+            s = ST_APPLIED;
+            anc[q] = a;
+          }
         }
       }
+      s4[k] = s;
+      if (s == ST_APPLIED) {
+        ++app;
+        const uint32_t r = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32);
+        if (r < REP_DIRECT) atomicMax(&rv[r], i + 1);
+        else atomicMax(&rtab[r + (1u << (REPLICA_BITS - 1))], i + 1);
+      } else if (s == ST_ALREADY) {
+        ++alr;
+      } else {
+        err = min(err, i);
+      }
+      // incrementTimestamp (src/CRDTree.elm:337-343): Ok Adds of the own replica
+      if ((s == ST_APPLIED || s == ST_ALREADY) && replica_of(ts) == id0) ++own;
     }
-    st[i] = s;
+    store_quad_u8(st, i0, qd.cnt, s4);
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x)
+    if (rv[j]) atomicMax(&rtab[j + (1u << (REPLICA_BITS - 1))], rv[j]);
+  app = block_sum(app);
+  alr = block_sum(alr);
+  own = block_sum(own);
+  err = block_min(err);
+  if (threadIdx.x == 0) {
+    if (app) {
+      atomicAdd(&dres->n_applied, app);
+      atomicAdd(&dres->n_adds_applied, app);
+    }
+    if (alr) atomicAdd(&dres->n_already, alr);
+    if (own) atomicAdd(&dres->own_ok_adds, own);
+    if (err != NONE) atomicMin(&dres->err_index, err);
+  }
+}
+
+// replicas[r] := ts of replica r's last applied Add (flat: Adds only, ids in
+// [0, max_replica]); clears the table entries it reads.
+__global__ void __launch_bounds__(BLOCK) k_fl_rep_collect(OpsDev o, uint32_t nr, uint32_t* rtab, long long* out,
+                                                          uint32_t* n_out) {
+  GRID_STRIDE(r, nr) {
+    uint32_t* e = &rtab[r + (1u << (REPLICA_BITS - 1))];
+    const uint32_t v = *e;
+    if (!v) continue;
+    *e = 0;
+    if (!out) continue;  // clear only (a merge that did not commit)
+    const uint32_t k = atomicAdd(n_out, 1u);
+    out[2 * k] = r;
+    out[2 * k + 1] = o.ts[v - 1];
   }
 }
 
@@ -1193,20 +1359,29 @@ __global__ void __launch_bounds__(BLOCK) k_fl_status(OpsDev o, uint8_t* st, TsIn
 // (flat10m: max walk 312 nodes -> 23 runs). anc[] is overwritten with ep as
 // walks finish; a concurrent reader then sees ep(h) instead of anchor(h),
 // which skips only nodes > h > x, so every walk stays exact.
-__global__ void __launch_bounds__(BLOCK) k_fl_ep(uint32_t Q, uint32_t* anc, const uint32_t* rh) {
+// Fused with the child count of each effective parent (the sentinel's count
+// aggregated per workgroup).
+__global__ void __launch_bounds__(BLOCK) k_fl_ep(uint32_t Q, uint32_t* anc, const uint32_t* rh, uint32_t* cnt) {
+  uint32_t hot = 0;
   GRID_STRIDE(x, Q) {
     uint32_t d = anc[x];
-    if (d == ABSENT || d == Q || d < x) continue;
-    while (d != Q && d > x) {
-      const uint32_t h = rh[d];
-      if (h < x) {
-        d = x - 1;
-        break;
+    if (d == ABSENT) continue;
+    if (d != Q && d > x) {
+      while (d != Q && d > x) {
+        const uint32_t h = rh[d];
+        if (h < x) {
+          d = x - 1;
+          break;
+        }
+        d = __hip_atomic_load(&anc[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      d = __hip_atomic_load(&anc[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&anc[x], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __hip_atomic_store(&anc[x], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == Q) ++hot;
+    else atomicAdd(&cnt[d], 1u);
   }
+  hot = block_sum(hot);
+  if (threadIdx.x == 0 && hot) atomicAdd(&cnt[Q], hot);
 }
 
 // Run heads: rh[q] = max{q' <= q : anc[q'] != q' - 1}, a three-phase
@@ -1277,42 +1452,45 @@ static int max_scan_incl(const uint32_t* anc, const uint32_t* in, uint32_t* out,
   return CRDTM_OK;
 }
 
-// K2b: children per parent (the sentinel's count aggregated per workgroup).
-__global__ void __launch_bounds__(BLOCK) k_fl_count(uint32_t Q, const uint32_t* anc, uint32_t* cnt) {
-  uint32_t hot = 0;
-  GRID_STRIDE(q, Q) {
-    const uint32_t p = anc[q];
-    if (p == ABSENT) continue;
-    if (p == Q) ++hot;
-    else atomicAdd(&cnt[p], 1u);
-  }
-  hot = block_sum(hot);
-  if (threadIdx.x == 0 && hot) atomicAdd(&cnt[Q], hot);
-}
-
 // Counting-sort scatter; single-child parents (the common case in a typing
-// stream) take a plain store.
+// stream) take a plain store. The root sentinel's children are placed by
+// k_fl_root_* instead (already in order, no sort).
 __global__ void __launch_bounds__(BLOCK) k_fl_scatter(uint32_t Q, const uint32_t* anc, const uint32_t* start,
                                                       uint32_t* fill, uint32_t* carr) {
-  __shared__ uint32_t blk_base;
-  uint32_t hot = 0;
-  GRID_STRIDE(q, Q) {
-    if (anc[q] == Q) ++hot;
-  }
-  uint32_t tot;
-  uint32_t mine = block_excl_sum(hot, &tot);
-  if (threadIdx.x == 0) blk_base = tot ? atomicAdd(&fill[Q], tot) : 0u;
-  __syncthreads();
-  mine += blk_base + start[Q];
   GRID_STRIDE(q, Q) {
     const uint32_t p = anc[q];
-    if (p == ABSENT) continue;
-    if (p == Q) {
-      carr[mine++] = q;
-    } else {
-      const uint32_t b = start[p];
-      carr[start[p + 1] - b == 1 ? b : b + atomicAdd(&fill[p], 1u)] = q;
-    }
+    if (p == ABSENT || p == Q) continue;
+    const uint32_t b = start[p];
+    carr[start[p + 1] - b == 1 ? b : b + atomicAdd(&fill[p], 1u)] = q;
+  }
+}
+
+// The root sentinel's children in descending slot order by an ordered
+// compaction: every workgroup owns a contiguous slot chunk, counts its root
+// children, and (after a scan of the counts) writes them in slot order from
+// the back of the segment.
+__global__ void __launch_bounds__(BLOCK) k_fl_root_count(uint32_t Q, const uint32_t* anc, uint32_t* bcnt) {
+  const uint32_t chunk = (Q + gridDim.x - 1) / gridDim.x;
+  const uint32_t b0 = blockIdx.x * chunk, b1 = min(Q, b0 + chunk);
+  uint32_t c = 0;
+  for (uint32_t q = b0 + threadIdx.x; q < b1; q += blockDim.x) c += anc[q] == Q ? 1u : 0u;
+  c = block_sum(c);
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = c;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_fl_root_place(uint32_t Q, const uint32_t* anc, const uint32_t* boff,
+                                                         const uint32_t* start, uint32_t* carr) {
+  const uint32_t chunk = (Q + gridDim.x - 1) / gridDim.x;
+  const uint32_t b0 = blockIdx.x * chunk, b1 = min(Q, b0 + chunk);
+  const uint32_t seg = start[Q], R = start[Q + 1] - seg;
+  uint32_t run = boff[blockIdx.x];
+  for (uint32_t t0 = b0; t0 < b1; t0 += blockDim.x) {
+    const uint32_t q = t0 + threadIdx.x;
+    const uint32_t f = (q < b1 && anc[q] == Q) ? 1u : 0u;
+    uint32_t tot;
+    const uint32_t j = run + block_excl_sum(f, &tot);
+    if (f) carr[seg + (R - 1 - j)] = q;
+    run += tot;
   }
 }
 
@@ -1325,56 +1503,95 @@ __global__ void __launch_bounds__(BLOCK) k_fl_links(const uint32_t* anc, const u
   }
 }
 
-// K4a: Euler tour, enter(u) = 2u, leave(u) = 2u + 1; enter of a node weighs
-// 1 (document rank). Both entries of u go out as one 16-byte store.
-__global__ void __launch_bounds__(BLOCK) k_fl_euler(uint32_t Q, const uint32_t* anc, const uint32_t* start,
-                                                    const uint32_t* carr, const uint32_t* ns, uint4* ent) {
-  GRID_STRIDE(u, Q + 1) {
+// K4: Euler tour entries computed on the fly for the list ranking:
+// enter(u) = 2u, leave(u) = 2u + 1; the enter of a node weighs 1, so a
+// node's rank is its document position. The ranks go straight into
+// order[rank] = node (no tour or rank arrays in HBM).
+struct FlatEulerSrc {
+  uint32_t Q;
+  const uint32_t* anc;    // ep per node, ABSENT = no node
+  const uint32_t* start;  // children segment of u: carr[start[u] .. start[u+1])
+  const uint32_t* carr;
+  const uint32_t* ns;     // next sibling
+  __device__ __forceinline__ uint2 operator()(uint64_t e) const {
+    const uint32_t u = static_cast<uint32_t>(e >> 1);
     const uint32_t p = u < Q ? anc[u] : Q;
-    if (p == ABSENT) {
-      ent[u] = make_uint4(ABSENT, 0u, ABSENT, 0u);
-      continue;
+    if (p == ABSENT) return make_uint2(ABSENT, 0u);
+    if (!(e & 1)) {
+      const uint32_t b = start[u], en = start[u + 1];
+      return make_uint2(b < en ? 2 * carr[b] : 2 * u + 1, u < Q ? 1u : 0u);
     }
-    const uint32_t b = start[u], e = start[u + 1];
-    const uint32_t enter = b < e ? 2 * carr[b] : 2 * u + 1;
-    uint32_t after = NONE;
-    if (u < Q) after = ns[u] != NONE ? 2 * ns[u] : 2 * p + 1;
-    ent[u] = make_uint4(enter, u < Q ? 1u : 0u, after, 0u);
+    if (u == Q) return make_uint2(NONE, 0u);
+    const uint32_t s = ns[u];
+    return make_uint2(s != NONE ? 2 * s : 2 * p + 1, 0u);
   }
-}
+};
 
-__global__ void __launch_bounds__(BLOCK) k_fl_order(uint32_t Q, const uint32_t* anc, const unsigned long long* excl,
-                                                    uint32_t* order) {
-  GRID_STRIDE(q, Q) {
-    if (anc[q] != ABSENT) order[static_cast<uint32_t>(excl[2 * q])] = q;
+// doc[rank] = the tree slot of the node (1 + its compacted slot index).
+struct FlatDocSink {
+  uint32_t Q;
+  uint32_t* doc;
+  const uint32_t* qc;  // exclusive scan of node presence, nullptr when slots have no holes
+  static constexpr bool kOffList = false;
+  __device__ __forceinline__ void operator()(uint64_t e, unsigned long long r) const {
+    if (e & 1) return;
+    const uint32_t u = static_cast<uint32_t>(e >> 1);
+    if (u < Q) doc[static_cast<uint32_t>(r)] = 1 + (qc ? qc[u] : u);
   }
-}
+};
 
-// Commit in document order: node of rank r -> slot 1 + r, its children
-// dict 1 + r with sentinel slot 1 + K + r. Within the root dict the raw
-// `next` chain is the document order (no tombstones).
-__global__ void __launch_bounds__(BLOCK) k_fl_commit(OpsDev o, TsIndex x, uint32_t K, const uint32_t* order,
-                                                     const uint32_t* logidx, TreeDev T) {
+// Commit. Node q -> tree slot 1 + qc(q) (slot order = timestamp order), its
+// children dict implicit (engine.h TreeDev). Within the root dict the raw
+// `next` chain is the document order (no tombstones): k_fl_next links
+// doc[r] -> doc[r + 1] and the root sentinel (slot 0) -> doc[0].
+__global__ void __launch_bounds__(BLOCK) k_fl_next(uint32_t K, const uint32_t* doc, TreeDev T) {
   GRID_STRIDE(r, K) {
-    const uint32_t q = order[r];
+    T.s_next[doc[r]] = r + 1 < K ? doc[r + 1] : NONE;
+    if (r == 0) T.s_next[0] = doc[0];
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_fl_present(uint32_t Q, const uint32_t* anc, uint32_t* f) {
+  GRID_STRIDE(q, Q) f[q] = anc[q] != ABSENT ? 1u : 0u;
+}
+
+// Node records in slot order. The key is recomputed from the slot: the
+// replica r with base[r] <= q (largest such r) and counter cmin[r] + q -
+// base[r] (tables in LDS when the replica ids fit, else the op's ts).
+__global__ void __launch_bounds__(BLOCK) k_fl_commit(OpsDev o, TsIndex x, uint32_t Q, uint32_t nrep,
+                                                     const uint32_t* anc, const uint32_t* qc, const uint32_t* logidx,
+                                                     TreeDev T) {
+  __shared__ uint32_t sb[HOST_RANGES];
+  __shared__ uint32_t sc[HOST_RANGES];
+  const bool lds = nrep <= HOST_RANGES;
+  if (lds) {
+    for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x) {
+      sb[j] = x.base[j];
+      sc[j] = x.cmin[j];
+    }
+  }
+  __syncthreads();
+  GRID_STRIDE(q, Q) {
+    if (anc[q] == ABSENT) continue;
+    const uint32_t slot = 1 + (qc ? qc[q] : q);
     const uint32_t i = x.first[q];
-    const uint32_t slot = 1 + r, ss = 1 + K + r, dd = 1 + r;
-    T.s_key[slot] = o.ts[i];
+    long long key;
+    if (lds) {
+      uint32_t lo = 0, hi = nrep;  // largest r with sb[r] <= q
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sb[mid] <= q) lo = mid;
+        else hi = mid;
+      }
+      key = (static_cast<long long>(lo) << 32) | static_cast<long long>(sc[lo] + (q - sb[lo]));
+    } else {
+      key = o.ts[i];
+    }
+    T.s_key[slot] = key;
     T.s_dict[slot] = 0;
-    T.s_next[slot] = r + 1 < K ? slot + 1 : NONE;
     T.s_src[slot] = logidx ? logidx[i] : i;
     T.s_flags[slot] = 0;
-    T.s_child[slot] = dd;
-    T.s_key[ss] = 0;
-    T.s_dict[ss] = dd;
-    T.s_next[ss] = NONE;
-    T.s_src[ss] = NONE;
-    T.s_child[ss] = NONE;
-    T.s_flags[ss] = F_TOMB | F_SENT;
-    T.d_sent[dd] = ss;
-    T.d_owner[dd] = slot;
-    T.doc[r] = slot;
-    if (r == 0) T.s_next[0] = slot;  // the root sentinel leads to the first node
+    T.s_child[slot] = NONE;
   }
 }
 
@@ -1602,7 +1819,7 @@ static int run_replay(crdtm_tree* t, const OpsDev& o, uint8_t* st, crdtm_result*
 
 // Flat closed form (see the k_fl_* kernels): the index `ix` is dense and
 // already built; Q = its slot range.
-static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_t Q, uint8_t* st,
+static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_t Q, uint32_t maxr, uint8_t* st,
                       uint8_t* st_out, crdtm_result* res) {
   crdtm_ctx* c = t->ctx;
   hipStream_t s = c->stream;
@@ -1612,11 +1829,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   const uint32_t g = grid_for(n);
   uint32_t* anc = ws.alloc<uint32_t>(static_cast<uint64_t>(Q) + 1);
   HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(anc), static_cast<int>(ABSENT), Q + 1, s));
-  LAUNCH(k_fl_status, dim3(g), dim3(BLOCK), 0, s, o, st, ix, Q, anc);
-  Work w{};
-  w.st = st;
-  HIP_CHECK(hipMemsetAsync(&dr->first_del, 0xFF, sizeof(uint32_t), s));
-  LAUNCH(k_stats, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, o, w, t->timestamp, dr);
+  LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, anc, t->timestamp, c->rtab, dr);
   int r;
   if ((r = sync_read(c))) return r;
   const DevResult h1 = *c->hres;
@@ -1624,6 +1837,8 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   const long long new_ts = t->timestamp + h1.own_ok_adds;
   if (replica_of(new_ts) != replica_of(t->timestamp)) guard |= G_REPLICA_DRIFT;
   res->guard = guard;
+  if (guard || h1.err_index != NONE)  // no commit: leave the replica table clean
+    LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr, nullptr);
   if (guard) {
     r = run_replay(t, o, st, res, guard);
     if (r == CRDTM_OK && st_out)
@@ -1645,8 +1860,8 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   const uint32_t K = h1.n_adds_applied;
   const bool all_applied = h1.n_applied == n;
   TreeCaps need = t->cap;
-  need.slots = std::max<uint64_t>(need.slots, 1 + 2ULL * K + 1);
-  need.dicts = std::max<uint64_t>(need.dicts, 1ULL + K + 1);
+  need.slots = std::max<uint64_t>(need.slots, 1ULL + K + 1);
+  need.dicts = std::max<uint64_t>(need.dicts, 2);
   need.log = std::max<uint64_t>(need.log, t->log_n + h1.n_applied + 1);
   need.lpath = std::max<uint64_t>(need.lpath, t->log_npath + o.n_path + 1);
   need.doc = std::max<uint64_t>(need.doc, 1ULL + K);
@@ -1666,22 +1881,31 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     const uint32_t gq = grid_for(Q);
     uint32_t* rh = ws.alloc<uint32_t>(Q);
     if ((r = max_scan_incl(anc, nullptr, rh, Q, ws, s))) return r;
-    LAUNCH(k_fl_ep, dim3(gq), dim3(BLOCK), 0, s, Q, anc, rh);
-    LAUNCH(k_fl_count, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, cnt);
+    LAUNCH(k_fl_ep, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, rh, cnt);
     uint32_t* n_child = &dr->n_sentinels;  // scratch word for the scan total
     if ((r = scan_excl_u32(cnt, cnt, U + 1, n_child, ws, s))) return r;
-    LAUNCH(k_fl_scatter, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, cnt, fill, carr);
-    if ((r = segmented_sort_desc_id(cnt, U, carr, U, ws, s, dr))) return r;
+    LAUNCH(k_fl_scatter, dim3(gq), dim3(BLOCK), 0, s, Q, anc, cnt, fill, carr);
+    {
+      const uint32_t gr = grid_for(Q, BLOCK, 2048);
+      uint32_t* bc = ws.alloc<uint32_t>(gr + 1);
+      LAUNCH(k_fl_root_count, dim3(gr), dim3(BLOCK), 0, s, Q, anc, bc);
+      if ((r = scan_excl_u32(bc, bc, gr, nullptr, ws, s))) return r;
+      LAUNCH(k_fl_root_place, dim3(gr), dim3(BLOCK), 0, s, Q, anc, bc, cnt, carr);
+    }
+    if ((r = segmented_sort_desc_id(cnt, U, carr, U, ws, s, dr, Q))) return r;
     LAUNCH(k_fl_links, dim3(gq), dim3(BLOCK), 0, s, anc, cnt, n_child, carr, ns);
-    // ---- K4: Euler tour + list ranking -> document rank ----
-    const uint64_t E = 2ULL * U;
-    uint4* ent = ws.alloc<uint4>(U);
-    unsigned long long* excl = ws.alloc<unsigned long long>(E);
-    LAUNCH(k_fl_euler, dim3(grid_for(U)), dim3(BLOCK), 0, s, Q, anc, cnt, carr, ns, ent);
-    if ((r = list_rank(reinterpret_cast<const uint2*>(ent), E, 2 * Q, excl, ws, s))) return r;
-    uint32_t* order = ws.alloc<uint32_t>(K);
-    LAUNCH(k_fl_order, dim3(gq), dim3(BLOCK), 0, s, Q, anc, excl, order);
-    // ---- commit in document order ----
+    // ---- K4: Euler tour + list ranking -> document order ----
+    uint32_t* qc = nullptr;
+    if (Q != K) {  // slots with no node: compact
+      qc = ws.alloc<uint32_t>(Q);
+      LAUNCH(k_fl_present, dim3(gq), dim3(BLOCK), 0, s, Q, anc, qc);
+      if ((r = scan_excl_u32(qc, qc, Q, nullptr, ws, s))) return r;
+    }
+    if ((r = list_rank_fused(FlatEulerSrc{Q, anc, cnt, carr, ns}, 2ULL * U, 2 * Q, FlatDocSink{Q, t->d.doc, qc}, ws,
+                             s)))
+      return r;
+    LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d);
+    // ---- commit ----
     uint32_t* logidx = nullptr;
     if (!all_applied) {
       logidx = ws.alloc<uint32_t>(n + 1);
@@ -1692,13 +1916,12 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
       LAUNCH(k_log, dim3(g), dim3(BLOCK), 0, s, o, st, t->d, 0u, 0u, logidx, plen);
       LAUNCH(k_log_tail, dim3(1), dim3(1), 0, s, t->d, 0u, &dr->log_n, 0u, &dr->log_npath);
     }
-    LAUNCH(k_fl_commit, dim3(grid_for(K)), dim3(BLOCK), 0, s, o, ix, K, order, logidx, t->d);
+    LAUNCH(k_fl_commit, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, o, ix, Q, maxr + 1, anc, qc, logidx, t->d);
   }
   if (all_applied) LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
-  long long* rep = ws.alloc<long long>(2 * static_cast<uint64_t>(n) + 2);
-  LAUNCH(k_rep_max, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, s, o, st, c->rtab);
-  LAUNCH(k_rep_out, dim3(g), dim3(BLOCK), 0, s, o, st, c->rtab, rep, &dr->n_replica_out);
-  LAUNCH(k_rep_reset, dim3(g), dim3(BLOCK), 0, s, o, st, c->rtab);
+  long long* rep = ws.alloc<long long>(2 * static_cast<uint64_t>(maxr) + 2);
+  LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, rep,
+         &dr->n_replica_out);
   if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, st, n, NONE, st_out);
   if ((r = sync_read(c))) return r;
   const DevResult& h2 = *c->hres;
@@ -1708,8 +1931,8 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     HIP_CHECK(hipMemcpy(hv.data(), rep, hv.size() * sizeof(long long), hipMemcpyDeviceToHost));
     for (uint32_t k = 0; k < nrep; ++k) t->replicas[hv[2 * k]] = hv[2 * k + 1];
   }
-  t->n_slots = 1 + 2ULL * K;
-  t->n_dicts = 1ULL + K;
+  t->n_slots = 1ULL + K;
+  t->n_dicts = 1;
   t->last_begin = t->log_n;
   t->log_n += h1.n_applied;
   t->log_npath += all_applied ? o.n_path : h2.log_npath;
@@ -1742,7 +1965,7 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   HIP_CHECK(hipMemsetAsync(&dr->err_index, 0xFF, sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(cmin, 0xFF, RID_SLOTS * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(cmax, 0, RID_SLOTS * sizeof(uint32_t), s));
-  LAUNCH(k_pre, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, o, cmin, cmax, dr);
+  LAUNCH(k_pre, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, cmin, cmax, dr);
   // the first HOST_RANGES replica ranges come back with the result block:
   // the dense index layout (exclusive scan of range sizes) is then a host loop
   HIP_CHECK(hipMemcpyAsync(c->hrange, cmin, HOST_RANGES * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -1788,9 +2011,9 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
     ix.first = ws.alloc<uint32_t>(range_total + 1);
     ix.h = TsHash{nullptr, nullptr, 0};
     HIP_CHECK(hipMemsetAsync(ix.first, 0xFF, (range_total + 1) * sizeof(uint32_t), s));
-    LAUNCH(k_index_store, dim3(g), dim3(BLOCK), 0, s, o, ix);
-    LAUNCH(k_index_fix, dim3(g), dim3(BLOCK), 0, s, o, ix);
-    if (flat) return apply_flat(t, o, ix, static_cast<uint32_t>(range_total), w.st, st_out, res);
+    LAUNCH(k_index_store, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix);
+    LAUNCH(k_index_fix, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix);
+    if (flat) return apply_flat(t, o, ix, static_cast<uint32_t>(range_total), maxr, w.st, st_out, res);
   } else {
     const uint32_t H = pow2_at_least(2 * static_cast<uint64_t>(n));
     ix.first = nullptr;

@@ -5,6 +5,7 @@
 // sort and (4) Euler-tour list ranking. Everything is integer, HBM-bound work.
 
 #include "engine.h"
+#include "listrank.h"
 
 namespace crdtm {
 
@@ -94,6 +95,7 @@ int scan_excl_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* total
 // bitonic in LDS up to LDS_SORT_MAX, else a workgroup merge sort in HBM.
 // ---------------------------------------------------------------------------
 constexpr uint32_t SMALL_SEG = 16;
+constexpr uint32_t MID_SEG = 512;
 constexpr uint32_t LDS_SORT_MAX = 4096;
 
 // Sort keys: an explicit per-item array, or the item id itself descending
@@ -108,32 +110,86 @@ struct NegIdKey {
 
 template <class KEY>
 __global__ void __launch_bounds__(BLOCK) k_sort_small(const uint32_t* __restrict__ seg_start, uint32_t n_seg,
-                                                      uint32_t* __restrict__ carr,
-                                                      KEY sort_key,
+                                                      uint32_t* __restrict__ carr, KEY sort_key, uint32_t skip,
+                                                      uint32_t* __restrict__ mid_list, uint32_t* __restrict__ n_mid,
                                                       uint32_t* __restrict__ big_list, uint32_t* __restrict__ n_big) {
   for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < n_seg; u += gridDim.x * blockDim.x) {
     const uint32_t b = seg_start[u], e = seg_start[u + 1];
     const uint32_t len = e - b;
-    if (len < 2) continue;
-    if (len > SMALL_SEG) {
-      big_list[atomicAdd(n_big, 1u)] = u;
-      continue;
-    }
-    uint32_t ids[SMALL_SEG];
-    long long keys[SMALL_SEG];
-    for (uint32_t j = 0; j < len; ++j) {
-      uint32_t v = carr[b + j];
-      long long k = sort_key(v);
-      uint32_t p = j;
-      while (p > 0 && keys[p - 1] > k) {
-        keys[p] = keys[p - 1];
-        ids[p] = ids[p - 1];
-        --p;
+    if (len < 2 || u == skip) continue;
+    if (len == 2) {
+      const uint32_t x = carr[b], y = carr[b + 1];
+      if (sort_key(y) < sort_key(x)) {
+        carr[b] = y;
+        carr[b + 1] = x;
       }
-      keys[p] = k;
-      ids[p] = v;
+    } else if (len <= SMALL_SEG) {
+      // insertion sort in place (the segment stays in L1/L2)
+      for (uint32_t j = b + 1; j < e; ++j) {
+        const uint32_t v = carr[j];
+        const long long k = sort_key(v);
+        uint32_t p = j;
+        while (p > b) {
+          const uint32_t w = carr[p - 1];
+          if (!(sort_key(w) > k)) break;
+          carr[p] = w;
+          --p;
+        }
+        carr[p] = v;
+      }
+    } else if (len <= MID_SEG) {
+      mid_list[atomicAdd(n_mid, 1u)] = u;
+    } else {
+      big_list[atomicAdd(n_big, 1u)] = u;
     }
-    for (uint32_t j = 0; j < len; ++j) carr[b + j] = ids[j];
+  }
+}
+
+// One wave per mid-size segment (17..MID_SEG): copy the keys to LDS; every
+// lane holds up to MID_SEG/64 items and counts the smaller keys (keys are
+// unique) in one sweep of broadcast 16-byte LDS reads, then writes each item
+// at its rank.
+template <class KEY>
+__global__ void __launch_bounds__(BLOCK) k_sort_mid(const uint32_t* __restrict__ seg_start,
+                                                    const uint32_t* __restrict__ mid_list,
+                                                    const uint32_t* __restrict__ n_mid, uint32_t* __restrict__ carr,
+                                                    KEY sort_key) {
+  constexpr uint32_t T = MID_SEG / 64;
+  __shared__ __attribute__((aligned(16))) long long skey[BLOCK / 64][MID_SEG + 2];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t nm = *n_mid;
+  const uint32_t waves = gridDim.x * (BLOCK / 64);
+  for (uint32_t mi = blockIdx.x * (BLOCK / 64) + wv; mi < nm; mi += waves) {
+    const uint32_t u = mid_list[mi];
+    const uint32_t b = seg_start[u], len = seg_start[u + 1] - b;
+    uint32_t id[T];
+    long long kk[T];
+    uint32_t rk[T];
+#pragma unroll
+    for (uint32_t t = 0; t < T; ++t) {
+      const uint32_t j = lane + 64 * t;
+      id[t] = j < len ? carr[b + j] : 0u;
+      kk[t] = j < len ? sort_key(id[t]) : 0x7fffffffffffffffLL;
+      rk[t] = 0;
+      if (j < len) skey[wv][j] = kk[t];
+    }
+    if (lane == 0) skey[wv][len] = 0x7fffffffffffffffLL;  // pad to an even count
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const longlong2* k2 = reinterpret_cast<const longlong2*>(skey[wv]);
+#pragma unroll 4
+    for (uint32_t m = 0; m < (len + 1) / 2; ++m) {
+      const longlong2 a = k2[m];
+#pragma unroll
+      for (uint32_t t = 0; t < T; ++t) rk[t] += (a.x < kk[t] ? 1u : 0u) + (a.y < kk[t] ? 1u : 0u);
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < T; ++t)
+      if (lane + 64 * t < len) carr[b + rk[t]] = id[t];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
@@ -346,16 +402,20 @@ __global__ void k_sort_big_filter(const uint32_t* __restrict__ seg_start, const 
 
 template <class KEY>
 static int segmented_sort_t(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items, KEY sort_key,
-                            Arena& ws, hipStream_t st, DevResult* dres) {
+                            Arena& ws, hipStream_t st, DevResult* dres, uint32_t skip) {
+  uint32_t* mid = ws.alloc<uint32_t>(n_seg + 1);
   uint32_t* big = ws.alloc<uint32_t>(n_seg + 1);
   uint32_t* huge = ws.alloc<uint32_t>(n_seg + 1);
   uint32_t* scratch = ws.alloc<uint32_t>(n_items + 1);
   uint32_t* nbig = &dres->big_segments;
   uint32_t* nhuge = &dres->huge_segments;
-  HIP_CHECK(hipMemsetAsync(nbig, 0, 2 * sizeof(uint32_t), st));  // big_segments, huge_segments
-  LAUNCH(k_sort_small<KEY>, dim3(grid_for(n_seg)), dim3(BLOCK), 0, st, seg_start, n_seg, carr, sort_key, big, nbig);
-  // segments of 17..LDS_SORT_MAX: one workgroup each (huge ones are skipped there)
-  LAUNCH(k_sort_big<KEY>, dim3(512), dim3(1024), 0, st, seg_start, big, nbig, carr, scratch, sort_key);
+  uint32_t* nmid = &dres->mid_segments;
+  HIP_CHECK(hipMemsetAsync(nbig, 0, 3 * sizeof(uint32_t), st));  // big_segments, huge_segments, mid_segments
+  LAUNCH(k_sort_small<KEY>, dim3(grid_for(n_seg)), dim3(BLOCK), 0, st, seg_start, n_seg, carr, sort_key, skip, mid,
+         nmid, big, nbig);
+  LAUNCH(k_sort_mid<KEY>, dim3(1024), dim3(BLOCK), 0, st, seg_start, mid, nmid, carr, sort_key);
+  // segments of MID_SEG+1..LDS_SORT_MAX: one workgroup each (huge ones are skipped there)
+  LAUNCH(k_sort_big<KEY>, dim3(256), dim3(1024), 0, st, seg_start, big, nbig, carr, scratch, sort_key);
   LAUNCH(k_sort_big_filter, dim3(16), dim3(BLOCK), 0, st, seg_start, big, nbig, huge, nhuge);
   uint32_t nh = 0;
   HIP_CHECK(hipMemcpyAsync(&nh, nhuge, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -383,12 +443,12 @@ static int segmented_sort_t(const uint32_t* seg_start, uint32_t n_seg, uint32_t*
 
 int segmented_sort(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items,
                    const long long* sort_key, Arena& ws, hipStream_t st, DevResult* dres) {
-  return segmented_sort_t(seg_start, n_seg, carr, n_items, ArrKey{sort_key}, ws, st, dres);
+  return segmented_sort_t(seg_start, n_seg, carr, n_items, ArrKey{sort_key}, ws, st, dres, NONE);
 }
 
 int segmented_sort_desc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items, Arena& ws,
-                           hipStream_t st, DevResult* dres) {
-  return segmented_sort_t(seg_start, n_seg, carr, n_items, NegIdKey{}, ws, st, dres);
+                           hipStream_t st, DevResult* dres, uint32_t skip) {
+  return segmented_sort_t(seg_start, n_seg, carr, n_items, NegIdKey{}, ws, st, dres, skip);
 }
 
 // ---------------------------------------------------------------------------
@@ -409,9 +469,6 @@ __host__ __device__ __forceinline__ uint64_t lr_cand(uint64_t b, uint32_t kbits)
   return (b << kbits) + (mix64(b * 0x9E3779B97F4A7C15ULL + 0x632BE59BD9B4E019ULL) & ((1ULL << kbits) - 1));
 }
 
-__device__ __forceinline__ unsigned long long lr_weight(uint32_t wbits) {
-  return (static_cast<unsigned long long>((wbits >> 1) & 1u) << 32) | (wbits & 1u);
-}
 
 template <bool PACKED>
 __global__ void __launch_bounds__(BLOCK) k_lr_walk(const uint2* __restrict__ ent, const uint32_t* __restrict__ succ,
@@ -509,179 +566,18 @@ static int list_rank_level(const uint2* ent, const uint32_t* succ, const unsigne
   return CRDTM_OK;
 }
 
-// ---------------------------------------------------------------------------
-// Local contraction (before the sublist ranking). Lists built over slot
-// numbering have strong memory locality: a typing run's Euler entries are
-// consecutive. A workgroup takes a tile of LC_T consecutive entries, finds
-// the pieces of the list that stay inside the tile (local chains) by
-// pointer jumping in LDS, and emits one contracted node per local chain
-// (weight = chain total, successor = the chain that follows its tail).
-// The contracted list (≈ LC_T / chains-per-tile times shorter) is ranked by
-// the sublist method; each entry's rank = its chain's rank + its prefix
-// inside the chain. A cycle inside a tile (never on a valid list) leaves
-// its entries unranked (~0), like entries off the list.
-// ---------------------------------------------------------------------------
-constexpr uint32_t LC_T = 1024;
-constexpr uint32_t LC_PER = LC_T / BLOCK;
-constexpr uint64_t LC_MIN = 1ULL << 16;  // shorter lists go straight to the sublist method
-
-__global__ void __launch_bounds__(BLOCK) k_lc_contract(const uint2* __restrict__ ent, uint64_t n,
-                                                       uint32_t* __restrict__ hidx,
-                                                       unsigned long long* __restrict__ pre,
-                                                       uint32_t* __restrict__ n_heads, uint32_t* __restrict__ rsucc,
-                                                       unsigned long long* __restrict__ rw) {
-  __shared__ uint32_t P[LC_T];
-  __shared__ unsigned long long V[LC_T];
-  __shared__ uint32_t W[LC_T];
-  __shared__ uint32_t hbase;
-  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * LC_T;
-#pragma unroll
-  for (uint32_t k = 0; k < LC_PER; ++k) P[threadIdx.x + k * BLOCK] = NONE;
-  __syncthreads();
-  uint32_t sc[LC_PER];
-#pragma unroll
-  for (uint32_t k = 0; k < LC_PER; ++k) {
-    const uint32_t l = threadIdx.x + k * BLOCK;
-    const uint64_t e = base + l;
-    const uint2 x = e < n ? ent[e] : make_uint2(ABSENT, 0u);
-    sc[k] = x.x;
-    W[l] = x.y;
-    if (x.x < n && x.x >= base && x.x < base + LC_T) P[x.x - base] = l;  // my successor's local predecessor
-  }
-  __syncthreads();
-  uint32_t p[LC_PER];
-  unsigned long long v[LC_PER];
-#pragma unroll
-  for (uint32_t k = 0; k < LC_PER; ++k) {
-    const uint32_t l = threadIdx.x + k * BLOCK;
-    p[k] = P[l];
-    v[k] = p[k] != NONE ? lr_weight(W[p[k]]) : 0ULL;
-    V[l] = v[k];
-  }
-  __syncthreads();
-  // Wyllie pointer jumping toward the chain head (<= log2(LC_T) rounds)
-  for (uint32_t round = 0; round <= 10; ++round) {
-    bool ch = false;
-#pragma unroll
-    for (uint32_t k = 0; k < LC_PER; ++k) {
-      if (p[k] == NONE) continue;
-      const uint32_t pp = P[p[k]];
-      if (pp != NONE) {
-        v[k] += V[p[k]];
-        p[k] = pp;
-        ch = true;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < LC_PER; ++k) {
-      const uint32_t l = threadIdx.x + k * BLOCK;
-      P[l] = p[k];
-      V[l] = v[k];
-    }
-    if (!__syncthreads_or(ch)) break;
-  }
-  // heads: present entries without a local predecessor; number them densely
-  uint32_t nh = 0;
-  bool head[LC_PER], cyc[LC_PER];
-#pragma unroll
-  for (uint32_t k = 0; k < LC_PER; ++k) {
-    const bool present = sc[k] != ABSENT;
-    cyc[k] = present && p[k] != NONE && P[p[k]] != NONE;  // still jumping: a cycle
-    head[k] = present && p[k] == NONE;
-    nh += head[k] ? 1u : 0u;
-  }
-  __syncthreads();
-  // block exclusive sum of nh (wave scan + LDS)
-  __shared__ uint32_t sw[BLOCK / 64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t inc = wave_incl_scan(nh);
-  if (lane == 63) sw[wave] = inc;
-  __syncthreads();
-  uint32_t off = inc - nh, tot = 0;
-  for (int w = 0; w < BLOCK / 64; ++w) {
-    if (w < wave) off += sw[w];
-    tot += sw[w];
-  }
-  if (threadIdx.x == 0) hbase = tot ? atomicAdd(n_heads, tot) : 0u;
-  __syncthreads();
-  // P[l] := hid of l when l is a head
-#pragma unroll
-  for (uint32_t k = 0; k < LC_PER; ++k) {
-    if (head[k]) P[threadIdx.x + k * BLOCK] = hbase + off++;
-  }
-  __syncthreads();
-#pragma unroll
-  for (uint32_t k = 0; k < LC_PER; ++k) {
-    const uint32_t l = threadIdx.x + k * BLOCK;
-    const uint64_t e = base + l;
-    if (e >= n) continue;
-    if (sc[k] == ABSENT || cyc[k]) {
-      hidx[e] = NONE;
-      continue;
-    }
-    const uint32_t h = P[head[k] ? l : p[k]];
-    hidx[e] = h;
-    pre[e] = v[k];
-    const uint32_t s = sc[k];
-    if (!(s < n && s >= base && s < base + LC_T)) {  // tail of its local chain
-      rw[h] = v[k] + lr_weight(W[l]);
-      rsucc[h] = s;  // entry id of the next chain's head (or NONE); translated by k_lc_link
-    }
-  }
+int list_rank_unpacked(const uint32_t* succ, const unsigned long long* w, uint64_t n, uint32_t head,
+                       unsigned long long* excl, Arena& ws, hipStream_t st) {
+  return list_rank_level(nullptr, succ, w, n, head, excl, ws, st, 1);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_lc_link(const uint32_t* __restrict__ n_heads,
-                                                   const uint32_t* __restrict__ hidx, uint32_t* __restrict__ rsucc) {
-  const uint32_t H = *n_heads;
-  for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < H; h += gridDim.x * blockDim.x) {
-    const uint32_t s = rsucc[h];
-    rsucc[h] = s == NONE ? NONE : hidx[s];
-  }
-}
-
-__global__ void __launch_bounds__(BLOCK) k_lc_expand(uint64_t n, const uint32_t* __restrict__ hidx,
-                                                     const unsigned long long* __restrict__ pre,
-                                                     const unsigned long long* __restrict__ rexcl,
-                                                     unsigned long long* __restrict__ excl) {
-  for (uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; e < n;
-       e += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    const uint32_t h = hidx[e];
-    unsigned long long r = ~0ULL;
-    if (h != NONE) {
-      const unsigned long long b = rexcl[h];
-      if (b != ~0ULL) r = b + pre[e];
-    }
-    excl[e] = r;
-  }
+int list_rank_packed(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws,
+                     hipStream_t st) {
+  return list_rank_level(ent, nullptr, nullptr, n, head, excl, ws, st, 0);
 }
 
 int list_rank(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws, hipStream_t st) {
-  if (n < LC_MIN || n >= 0xFFFFFFF0ULL) return list_rank_level(ent, nullptr, nullptr, n, head, excl, ws, st, 0);
-  const uint64_t tiles = (n + LC_T - 1) / LC_T;
-  uint32_t* hidx = ws.alloc<uint32_t>(n);
-  unsigned long long* pre = ws.alloc<unsigned long long>(n);
-  // contracted list: at most one node per entry
-  uint32_t* rsucc = ws.alloc<uint32_t>(n + 1);
-  unsigned long long* rw = ws.alloc<unsigned long long>(n + 1);
-  uint32_t* cnt = ws.alloc<uint32_t>(2);  // [0] heads, [1] contracted head id
-  HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), st));
-  LAUNCH(k_lc_contract, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, ent, n, hidx, pre, cnt, rsucc, rw);
-  LAUNCH(k_lc_link, dim3(grid_for(n / 4 + 1)), dim3(BLOCK), 0, st, cnt, hidx, rsucc);
-  uint32_t hv[2] = {0, NONE};
-  HIP_CHECK(hipMemcpyAsync(&hv[0], cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipMemcpyAsync(&hv[1], hidx + head, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipStreamSynchronize(st));
-  const uint32_t H = hv[0], rhead = hv[1];
-  unsigned long long* rexcl = ws.alloc<unsigned long long>(static_cast<uint64_t>(H) + 1);
-  if (H == 0 || rhead == NONE) {
-    HIP_CHECK(hipMemsetAsync(excl, 0xFF, n * sizeof(unsigned long long), st));
-    return CRDTM_OK;
-  }
-  int r = list_rank_level(nullptr, rsucc, rw, H, rhead, rexcl, ws, st, 1);
-  if (r) return r;
-  LAUNCH(k_lc_expand, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, hidx, pre, rexcl, excl);
-  return CRDTM_OK;
+  return list_rank_fused(PackedSrc{ent}, n, head, ExclSink{excl}, ws, st);
 }
 
 }  // namespace crdtm

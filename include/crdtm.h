@@ -71,7 +71,7 @@ typedef struct crdtm_result {
   uint64_t n_applied;
   uint64_t n_already;
   int64_t timestamp;  /* tree timestamp after the call */
-  uint64_t n_slots;   /* dict entries held by the tree (incl. sentinels) */
+  uint64_t n_slots;   /* slots held by the device state (empty children dicts are implicit) */
   uint32_t guard;     /* bit0 ts collision, bit1 delete-before-add in a dict, bit2 replica-id drift, bit3 non-fresh tree */
   uint32_t reserved;
 } crdtm_result;
