@@ -46,16 +46,21 @@ constexpr uint32_t LC_T = 1024;
 constexpr uint32_t LC_PER = LC_T / BLOCK;
 constexpr uint64_t LC_MIN = 1ULL << 16;  // shorter lists: sublist method on a materialised list
 
+// Contraction of one tile. Outputs: hidx[e] = the tile-local index of e's
+// chain (NONE: off every list), pre[e] = e's prefix inside its chain,
+// tcnt[tile] = chains in the tile; per chain, at sparse position
+// tile * LC_T + local: the successor entry of its tail (sp_succ) and its
+// total weight (sp_w). No global atomics: chain ids become dense after a
+// scan of tcnt (k_lc_link).
 template <class SRC>
 __global__ void __launch_bounds__(BLOCK) k_lc_contract(SRC srcf, uint64_t n, uint32_t* __restrict__ hidx,
                                                        unsigned long long* __restrict__ pre,
-                                                       uint32_t* __restrict__ n_heads, uint32_t* __restrict__ rsucc,
-                                                       unsigned long long* __restrict__ rw) {
+                                                       uint32_t* __restrict__ tcnt, uint32_t* __restrict__ sp_succ,
+                                                       unsigned long long* __restrict__ sp_w) {
   __shared__ uint32_t P[LC_T];
   __shared__ unsigned long long V[LC_T];
   __shared__ uint32_t W[LC_T];
   __shared__ uint32_t sw[BLOCK / 64];
-  __shared__ uint32_t hbase;
   const uint64_t base = static_cast<uint64_t>(blockIdx.x) * LC_T;
 #pragma unroll
   for (uint32_t k = 0; k < LC_PER; ++k) P[threadIdx.x + k * BLOCK] = NONE;
@@ -103,7 +108,7 @@ __global__ void __launch_bounds__(BLOCK) k_lc_contract(SRC srcf, uint64_t n, uin
     }
     if (!__syncthreads_or(ch)) break;
   }
-  // heads: present entries without a local predecessor; number them densely
+  // heads: present entries without a local predecessor, numbered in the tile
   uint32_t nh = 0;
   bool head[LC_PER], cyc[LC_PER];
 #pragma unroll
@@ -123,11 +128,10 @@ __global__ void __launch_bounds__(BLOCK) k_lc_contract(SRC srcf, uint64_t n, uin
     if (w < wave) off += sw[w];
     tot += sw[w];
   }
-  if (threadIdx.x == 0) hbase = tot ? atomicAdd(n_heads, tot) : 0u;
-  __syncthreads();
+  if (threadIdx.x == 0) tcnt[blockIdx.x] = tot;
 #pragma unroll
   for (uint32_t k = 0; k < LC_PER; ++k) {
-    if (head[k]) P[threadIdx.x + k * BLOCK] = hbase + off++;  // P[head] := its contracted id
+    if (head[k]) P[threadIdx.x + k * BLOCK] = off++;  // P[head] := its tile-local chain id
   }
   __syncthreads();
 #pragma unroll
@@ -144,29 +148,39 @@ __global__ void __launch_bounds__(BLOCK) k_lc_contract(SRC srcf, uint64_t n, uin
     pre[e] = v[k];
     const uint32_t s = sc[k];
     if (!(s < n && s >= base && s < base + LC_T)) {  // tail of its local chain
-      rw[h] = v[k] + lr_weight(W[l]);
-      rsucc[h] = s;  // entry id of the next chain's head (or NONE); translated by k_lc_link
+      sp_w[base + h] = v[k] + lr_weight(W[l]);
+      sp_succ[base + h] = s;  // entry id of the next chain's head (or NONE)
     }
   }
 }
 
-static __global__ void __launch_bounds__(BLOCK) k_lc_link(const uint32_t* __restrict__ n_heads,
-                                                   const uint32_t* __restrict__ hidx, uint32_t* __restrict__ rsucc) {
-  const uint32_t H = *n_heads;
-  for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < H; h += gridDim.x * blockDim.x) {
-    const uint32_t s = rsucc[h];
-    rsucc[h] = s == NONE ? NONE : hidx[s];
+// Dense contracted list: chain (tile t, local h) -> toff[t] + h; its
+// successor is the chain headed by entry s, i.e. toff[s / LC_T] + hidx[s].
+static __global__ void __launch_bounds__(BLOCK) k_lc_link(const uint32_t* __restrict__ toff,
+                                                          const uint32_t* __restrict__ hidx,
+                                                          const uint32_t* __restrict__ sp_succ,
+                                                          const unsigned long long* __restrict__ sp_w,
+                                                          uint32_t* __restrict__ rsucc,
+                                                          unsigned long long* __restrict__ rw) {
+  const uint32_t t = blockIdx.x;
+  const uint32_t b = toff[t], cnt = toff[t + 1] - b;
+  const uint64_t base = static_cast<uint64_t>(t) * LC_T;
+  for (uint32_t h = threadIdx.x; h < cnt; h += blockDim.x) {
+    const uint32_t s = sp_succ[base + h];
+    rsucc[b + h] = s == NONE ? NONE : toff[s / LC_T] + hidx[s];
+    rw[b + h] = sp_w[base + h];
   }
 }
 
 template <class SINK>
-__global__ void __launch_bounds__(BLOCK) k_lc_expand(uint64_t n, const uint32_t* __restrict__ hidx,
+__global__ void __launch_bounds__(BLOCK) k_lc_expand(uint64_t n, const uint32_t* __restrict__ toff,
+                                                     const uint32_t* __restrict__ hidx,
                                                      const unsigned long long* __restrict__ pre,
                                                      const unsigned long long* __restrict__ rexcl, SINK sink) {
   for (uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; e < n;
        e += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
     const uint32_t h = hidx[e];
-    const unsigned long long b = h != NONE ? rexcl[h] : ~0ULL;
+    const unsigned long long b = h != NONE ? rexcl[toff[e / LC_T] + h] : ~0ULL;
     if (b != ~0ULL) sink(e, b + pre[e]);
     else if (SINK::kOffList) sink(e, ~0ULL);
   }
@@ -203,26 +217,31 @@ int list_rank_fused(SRC srcf, uint64_t n, uint32_t head, SINK sink, Arena& ws, h
   const uint64_t tiles = (n + LC_T - 1) / LC_T;
   uint32_t* hidx = ws.alloc<uint32_t>(n);
   unsigned long long* pre = ws.alloc<unsigned long long>(n);
-  uint32_t* rsucc = ws.alloc<uint32_t>(n + 1);  // contracted list: at most one node per entry
-  unsigned long long* rw = ws.alloc<unsigned long long>(n + 1);
-  uint32_t* cnt = ws.alloc<uint32_t>(2);
-  HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), st));
-  LAUNCH(k_lc_contract<SRC>, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, srcf, n, hidx, pre, cnt, rsucc,
-         rw);
-  LAUNCH(k_lc_link, dim3(grid_for(n / 4 + 1)), dim3(BLOCK), 0, st, cnt, hidx, rsucc);
-  uint32_t hv[2] = {0, NONE};
-  HIP_CHECK(hipMemcpyAsync(&hv[0], cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  uint32_t* sp_succ = ws.alloc<uint32_t>(tiles * LC_T);
+  unsigned long long* sp_w = ws.alloc<unsigned long long>(tiles * LC_T);
+  uint32_t* toff = ws.alloc<uint32_t>(tiles + 1);
+  LAUNCH(k_lc_contract<SRC>, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, srcf, n, hidx, pre, toff,
+         sp_succ, sp_w);
+  HIP_CHECK(hipMemsetAsync(toff + tiles, 0, sizeof(uint32_t), st));
+  int r = scan_excl_u32(toff, toff, tiles + 1, nullptr, ws, st);
+  if (r) return r;
+  uint32_t hv[3] = {0, NONE, 0};
+  HIP_CHECK(hipMemcpyAsync(&hv[0], toff + tiles, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipMemcpyAsync(&hv[1], hidx + head, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipMemcpyAsync(&hv[2], toff + head / LC_T, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  uint32_t* rsucc = ws.alloc<uint32_t>(tiles * LC_T + 1);  // dense contracted list (H <= n)
+  unsigned long long* rw = ws.alloc<unsigned long long>(tiles * LC_T + 1);
+  LAUNCH(k_lc_link, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, toff, hidx, sp_succ, sp_w, rsucc, rw);
   HIP_CHECK(hipStreamSynchronize(st));
-  const uint32_t H = hv[0], rhead = hv[1];
+  const uint32_t H = hv[0], rhead = hv[1] == NONE ? NONE : hv[2] + hv[1];
   unsigned long long* rexcl = ws.alloc<unsigned long long>(static_cast<uint64_t>(H) + 1);
   if (H == 0 || rhead == NONE) {
     HIP_CHECK(hipMemsetAsync(rexcl, 0xFF, (static_cast<uint64_t>(H) + 1) * sizeof(unsigned long long), st));
   } else {
-    int r = list_rank_unpacked(rsucc, rw, H, rhead, rexcl, ws, st);
+    r = list_rank_unpacked(rsucc, rw, H, rhead, rexcl, ws, st);
     if (r) return r;
   }
-  LAUNCH(k_lc_expand<SINK>, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, hidx, pre, rexcl, sink);
+  LAUNCH(k_lc_expand<SINK>, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, toff, hidx, pre, rexcl, sink);
   return CRDTM_OK;
 }
 
