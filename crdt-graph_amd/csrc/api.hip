@@ -196,7 +196,13 @@ int crdtm_ctx_create(int device, void* stream, crdtm_ctx** out) {
   }
   HIP_CHECK(hipMalloc(&c->dres, sizeof(DevResult)));
   HIP_CHECK(hipHostMalloc(&c->hres, sizeof(DevResult), hipHostMallocDefault));
-  HIP_CHECK(hipHostMalloc(&c->hrange, 3 * HOST_RANGES * sizeof(uint32_t), hipHostMallocDefault));
+  HIP_CHECK(hipMalloc(&c->crange, RID_SLOTS * sizeof(uint2)));
+  HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->crange), -1, 2ULL * RID_SLOTS, c->stream));
+  HIP_CHECK(hipMemset2DAsync(reinterpret_cast<char*>(c->crange) + 4, 8, 0, 4, RID_SLOTS, c->stream));
+  c->ws.scan_cap = 1u << 20;
+  HIP_CHECK(hipMalloc(&c->ws.scan_status, (c->ws.scan_cap + 2) * sizeof(unsigned long long)));
+  HIP_CHECK(hipMemsetAsync(c->ws.scan_status, 0, (c->ws.scan_cap + 2) * sizeof(unsigned long long), c->stream));
+  c->ws.scan_ticket = reinterpret_cast<uint32_t*>(c->ws.scan_status + c->ws.scan_cap);
   HIP_CHECK(hipMalloc(&c->rtab, REPLICA_SLOTS * sizeof(uint32_t)));
   HIP_CHECK(hipMemsetAsync(c->rtab, 0, REPLICA_SLOTS * sizeof(uint32_t), c->stream));
   int r = ensure_arena(c, 64ULL << 20);
@@ -213,7 +219,8 @@ int crdtm_ctx_destroy(crdtm_ctx* c) {
   if (c->ws.base) hipFree(c->ws.base);
   hipFree(c->dres);
   hipHostFree(c->hres);
-  hipHostFree(c->hrange);
+  hipFree(c->crange);
+  hipFree(c->ws.scan_status);
   hipFree(c->rtab);
   if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;

@@ -69,6 +69,7 @@ struct DevResult {
   uint32_t n_del;           // Delete ops in the batch
   uint32_t range_total;     // dense index size
   uint32_t max_replica;     // largest replica id of an Add timestamp
+  uint32_t scan_err;        // a look-back scan gave up (never on a live device)
 };
 
 #define HIP_CHECK(x)                                                                         \

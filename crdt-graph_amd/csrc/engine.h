@@ -31,6 +31,12 @@ struct Arena {
     return p;
   }
   void reset() { used = 0; }
+  // single-pass scans (scan.h): status words tagged with a per-call epoch, so
+  // the pool is zeroed once at context creation and never again
+  unsigned long long* scan_status = nullptr;
+  uint64_t scan_cap = 0;
+  uint32_t* scan_ticket = nullptr;
+  uint32_t scan_epoch = 0;
 };
 
 enum : uint8_t { F_TOMB = 1, F_ORPHAN = 2, F_SENT = 4 };
@@ -78,7 +84,7 @@ struct crdtm_ctx {
   crdtm::DevResult* dres = nullptr;  // device
   crdtm::DevResult* hres = nullptr;  // pinned host
   uint32_t* rtab = nullptr;          // replica table [REPLICA_SLOTS], 0 = empty (kept clean between calls)
-  uint32_t* hrange = nullptr;        // pinned host: cmin/cmax/base of the first HOST_RANGES replicas
+  uint2* crange = nullptr;           // replica counter ranges [RID_SLOTS] {min, max}, kept clean between calls
   bool profile = false;
   std::vector<std::pair<std::string, hipEvent_t>> marks;
   std::vector<std::pair<std::string, double>> phases;

@@ -62,8 +62,7 @@ constexpr uint32_t RID_SLOTS = 1u << RID_BITS;
 struct TsIndex {
   uint32_t dense;
   TsHash h;
-  const uint32_t* cmin;  // [RID_SLOTS] per replica min counter (0xFFFFFFFF = no Add)
-  const uint32_t* cmax;  // [RID_SLOTS]
+  const uint2* rng;      // [RID_SLOTS] per replica {min counter, max counter}; min = 0xFFFFFFFF: no Add
   const uint32_t* base;  // [RID_SLOTS] exclusive scan of range sizes
   uint32_t* first;       // [total range] min op index, 0xFFFFFFFF = none
 };
@@ -73,9 +72,9 @@ __device__ __forceinline__ uint32_t tsindex_slot(const TsIndex& x, int64_t ts) {
   const uint64_t r = static_cast<uint64_t>(ts) >> 32;
   if (r >= RID_SLOTS) return NONE;
   const uint32_t c = static_cast<uint32_t>(ts);
-  const uint32_t lo = x.cmin[r];
-  if (lo == NONE || c < lo || c > x.cmax[r]) return NONE;
-  return x.base[r] + (c - lo);
+  const uint2 g = x.rng[r];
+  if (g.x == NONE || c < g.x || c > g.y) return NONE;
+  return x.base[r] + (c - g.x);
 }
 
 __device__ __forceinline__ uint32_t tsindex_find(const TsIndex& x, int64_t ts) {

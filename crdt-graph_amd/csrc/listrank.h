@@ -172,6 +172,14 @@ static __global__ void __launch_bounds__(BLOCK) k_lc_link(const uint32_t* __rest
   }
 }
 
+// {contracted list length, contracted id of the list head} in one word pair
+static __global__ void k_lc_meta(const uint32_t* toff, uint32_t tiles, const uint32_t* hidx, uint32_t head,
+                                 uint32_t* meta) {
+  meta[0] = toff[tiles];
+  const uint32_t h = hidx[head];
+  meta[1] = h == NONE ? NONE : toff[head / LC_T] + h;
+}
+
 template <class SINK>
 __global__ void __launch_bounds__(BLOCK) k_lc_expand(uint64_t n, const uint32_t* __restrict__ toff,
                                                      const uint32_t* __restrict__ hidx,
@@ -225,15 +233,15 @@ int list_rank_fused(SRC srcf, uint64_t n, uint32_t head, SINK sink, Arena& ws, h
   HIP_CHECK(hipMemsetAsync(toff + tiles, 0, sizeof(uint32_t), st));
   int r = scan_excl_u32(toff, toff, tiles + 1, nullptr, ws, st);
   if (r) return r;
-  uint32_t hv[3] = {0, NONE, 0};
-  HIP_CHECK(hipMemcpyAsync(&hv[0], toff + tiles, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipMemcpyAsync(&hv[1], hidx + head, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipMemcpyAsync(&hv[2], toff + head / LC_T, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  uint32_t* meta = ws.alloc<uint32_t>(2);
+  LAUNCH(k_lc_meta, dim3(1), dim3(1), 0, st, toff, static_cast<uint32_t>(tiles), hidx, head, meta);
+  uint32_t hv[2] = {0, NONE};
+  HIP_CHECK(hipMemcpyAsync(hv, meta, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   uint32_t* rsucc = ws.alloc<uint32_t>(tiles * LC_T + 1);  // dense contracted list (H <= n)
   unsigned long long* rw = ws.alloc<unsigned long long>(tiles * LC_T + 1);
   LAUNCH(k_lc_link, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, toff, hidx, sp_succ, sp_w, rsucc, rw);
   HIP_CHECK(hipStreamSynchronize(st));
-  const uint32_t H = hv[0], rhead = hv[1] == NONE ? NONE : hv[2] + hv[1];
+  const uint32_t H = hv[0], rhead = hv[1];
   unsigned long long* rexcl = ws.alloc<unsigned long long>(static_cast<uint64_t>(H) + 1);
   if (H == 0 || rhead == NONE) {
     HIP_CHECK(hipMemsetAsync(rexcl, 0xFF, (static_cast<uint64_t>(H) + 1) * sizeof(unsigned long long), st));

@@ -16,6 +16,7 @@
 
 #include "engine.h"
 #include "listrank.h"
+#include "scan.h"
 
 namespace crdtm {
 
@@ -159,7 +160,7 @@ __device__ __forceinline__ uint32_t block_min(uint32_t v) {
 // Replica ids below REP_DIRECT fold into a direct-mapped LDS table with
 // no-return LDS atomics; larger ids go straight to the global table.
 constexpr uint32_t REP_DIRECT = 4096;
-__global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint32_t* cmin, uint32_t* cmax, DevResult* dres) {
+__global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint2* rng, DevResult* dres) {
   __shared__ uint32_t rlo[REP_DIRECT];
   __shared__ uint32_t rhi[REP_DIRECT];
   for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) {
@@ -192,8 +193,8 @@ __global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint32_t* cmin, uint32_
           atomicMin(&rlo[r], c);
           atomicMax(&rhi[r], c);
         } else {
-          atomicMin(&cmin[r], c);
-          atomicMax(&cmax[r], c);
+          atomicMin(&rng[r].x, c);
+          atomicMax(&rng[r].y, c);
         }
       }
     }
@@ -212,8 +213,8 @@ __global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint32_t* cmin, uint32_
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) {
     if (rlo[j] != NONE) {
-      atomicMin(&cmin[j], rlo[j]);
-      atomicMax(&cmax[j], rhi[j]);
+      atomicMin(&rng[j].x, rlo[j]);
+      atomicMax(&rng[j].y, rhi[j]);
     }
   }
   mx = block_max(mx);
@@ -240,12 +241,51 @@ __global__ void __launch_bounds__(BLOCK) k_work_init(OpsDev o, Work w) {
   }
 }
 
-// range size per replica -> scan -> base (dense index layout)
-__global__ void __launch_bounds__(BLOCK) k_range_size(const uint32_t* cmin, const uint32_t* cmax, uint32_t* sz,
-                                                      uint32_t nr) {
-  GRID_STRIDE(r, nr) {
-    const uint32_t lo = cmin[r];
-    sz[r] = lo == NONE ? 0u : cmax[r] - lo + 1u;
+// Dense index layout: base[r] = exclusive scan of the range sizes over
+// replicas 0..max_replica, one workgroup (max_replica is read on the device,
+// so the host needs no copy of the ranges); the total goes to range_total.
+__global__ void __launch_bounds__(BLOCK) k_range_base(const uint2* rng, uint32_t* base, DevResult* dres) {
+  __shared__ uint32_t sw[BLOCK / 64];
+  const uint32_t nr = dres->max_replica + 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned long long carry = 0;
+  for (uint32_t r0 = 0; r0 < nr; r0 += BLOCK) {
+    const uint32_t r = r0 + threadIdx.x;
+    uint32_t sz = 0;
+    if (r < nr) {
+      const uint2 g = rng[r];
+      sz = g.x == NONE ? 0u : g.y - g.x + 1u;
+    }
+    const uint32_t inc = wave_incl_scan(sz);
+    if (lane == 63) sw[wave] = inc;
+    __syncthreads();
+    unsigned long long pre = carry + (inc - sz), tot = 0;
+    for (int w = 0; w < BLOCK / 64; ++w) {
+      if (w < wave) pre += sw[w];
+      tot += sw[w];
+    }
+    if (r < nr) base[r] = static_cast<uint32_t>(pre < NONE ? pre : NONE);
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dres->range_total = static_cast<uint32_t>(carry < NONE ? carry : NONE);
+}
+
+// The replica range table lives in the context and is kept clean between
+// calls: every merge resets the entries it touched (ids 0..max_replica).
+__global__ void __launch_bounds__(BLOCK) k_range_reset(uint2* rng, const DevResult* dres) {
+  const uint32_t nr = dres->max_replica + 1;
+  GRID_STRIDE(r, nr) rng[r] = make_uint2(NONE, 0u);
+}
+
+__global__ void k_dres_init(DevResult* d) {
+  const uint32_t nw = sizeof(DevResult) / sizeof(uint32_t);
+  uint32_t* w = reinterpret_cast<uint32_t*>(d);
+  for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) w[j] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    d->err_index = NONE;
+    d->first_del = NONE;
   }
 }
 
@@ -1249,7 +1289,7 @@ __global__ void __launch_bounds__(64) k_forest(OpsDev o, ForestArgs f, const uin
 // ---------------------------------------------------------------------------
 // Flat closed form in timestamp-slot space: a fresh tree, a single-level
 // Adds-only batch, and a dense timestamp index. Node q = the dense slot of
-// its timestamp (base[replica] + counter - cmin[replica]), so slot order IS
+// its timestamp (base[replica] + counter - min counter[replica]), so slot order IS
 // timestamp order (src/Internal/Node.elm:100 compares the Int key), and a
 // replica's typing run x_c -> x_{c+1} -> ... occupies consecutive slots: the
 // effective-parent chains, the child counting, the Euler tour and the
@@ -1384,73 +1424,30 @@ __global__ void __launch_bounds__(BLOCK) k_fl_ep(uint32_t Q, uint32_t* anc, cons
   if (threadIdx.x == 0 && hot) atomicAdd(&cnt[Q], hot);
 }
 
-// Run heads: rh[q] = max{q' <= q : anc[q'] != q' - 1}, a three-phase
-// inclusive max-scan (tiles of 2048 slots; tile maxima scanned recursively).
-constexpr int RH_ITEMS = 8;
-constexpr int RH_TILE = BLOCK * RH_ITEMS;
-
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-  const int lane = threadIdx.x & 63;
+// Run heads: rh[q] = max{q' <= q : anc[q'] != q' - 1}, an inclusive
+// max-scan over head flags (scan.h).
+struct RunHeadGen {
+  const uint32_t* anc;
+  __device__ __forceinline__ void load(uint64_t b, uint64_t n, uint32_t* v) const {
+    if (b + DS_ITEMS <= n) {
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = __shfl_up(v, o, 64);
-    if (lane >= o) v = max(v, t);
+      for (int j = 0; j < DS_ITEMS; j += 4) {
+        const uint4 x = *reinterpret_cast<const uint4*>(anc + b + j);
+        const uint32_t q = static_cast<uint32_t>(b) + j;
+        v[j] = (q == 0 || x.x != q - 1) ? q : 0u;
+        v[j + 1] = x.y != q ? q + 1 : 0u;
+        v[j + 2] = x.z != q + 1 ? q + 2 : 0u;
+        v[j + 3] = x.w != q + 2 ? q + 3 : 0u;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < DS_ITEMS; ++j) {
+        const uint64_t q = b + j;
+        v[j] = (q < n && (q == 0 || anc[q] != q - 1)) ? static_cast<uint32_t>(q) : 0u;
+      }
+    }
   }
-  return v;
-}
-
-// in == nullptr: values from anc (head flags); else a plain max-scan of in.
-__global__ void __launch_bounds__(BLOCK) k_rh_tiles(const uint32_t* anc, const uint32_t* in, uint32_t* out,
-                                                    uint32_t* tile_max, uint32_t n) {
-  __shared__ uint32_t lw[BLOCK / 64];
-  const uint32_t b = blockIdx.x * RH_TILE + threadIdx.x * RH_ITEMS;
-  uint32_t v[RH_ITEMS];
-  uint32_t m = 0;
-#pragma unroll
-  for (int j = 0; j < RH_ITEMS; ++j) {
-    const uint32_t q = b + j;
-    uint32_t x = 0;
-    if (q < n) x = in ? in[q] : ((q == 0 || anc[q] != q - 1) ? q : 0u);
-    m = max(m, x);
-    v[j] = m;
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t inc = wave_incl_max(m);
-  if (lane == 63) lw[wave] = inc;
-  __syncthreads();
-  uint32_t pre = __shfl_up(inc, 1, 64);
-  if (lane == 0) pre = 0;
-  for (int w = 0; w < wave; ++w) pre = max(pre, lw[w]);
-  uint32_t tot = 0;
-  for (int w = 0; w < BLOCK / 64; ++w) tot = max(tot, lw[w]);
-#pragma unroll
-  for (int j = 0; j < RH_ITEMS; ++j)
-    if (b + j < n) out[b + j] = max(v[j], pre);
-  if (threadIdx.x == 0) tile_max[blockIdx.x] = tot;
-}
-
-__global__ void __launch_bounds__(BLOCK) k_rh_add(uint32_t* out, const uint32_t* tile_incl, uint32_t n) {
-  if (blockIdx.x == 0) return;
-  const uint32_t add = tile_incl[blockIdx.x - 1];
-  const uint32_t b = blockIdx.x * RH_TILE + threadIdx.x * RH_ITEMS;
-#pragma unroll
-  for (int j = 0; j < RH_ITEMS; ++j)
-    if (b + j < n) out[b + j] = max(out[b + j], add);
-}
-
-// inclusive max-scan; anc != nullptr derives the values from run-head flags
-static int max_scan_incl(const uint32_t* anc, const uint32_t* in, uint32_t* out, uint32_t n, Arena& ws,
-                         hipStream_t st) {
-  const uint32_t tiles = (n + RH_TILE - 1) / RH_TILE;
-  uint32_t* tm = ws.alloc<uint32_t>(tiles + 1);
-  LAUNCH(k_rh_tiles, dim3(tiles), dim3(BLOCK), 0, st, anc, in, out, tm, n);
-  if (tiles > 1) {
-    int r = max_scan_incl(nullptr, tm, tm, tiles, ws, st);
-    if (r) return r;
-    LAUNCH(k_rh_add, dim3(tiles), dim3(BLOCK), 0, st, out, tm, n);
-  }
-  return CRDTM_OK;
-}
+};
 
 // Counting-sort scatter; single-child parents (the common case in a typing
 // stream) take a plain store. The root sentinel's children are placed by
@@ -1556,7 +1553,7 @@ __global__ void __launch_bounds__(BLOCK) k_fl_present(uint32_t Q, const uint32_t
 }
 
 // Node records in slot order. The key is recomputed from the slot: the
-// replica r with base[r] <= q (largest such r) and counter cmin[r] + q -
+// replica r with base[r] <= q (largest such r) and counter min[r] + q -
 // base[r] (tables in LDS when the replica ids fit, else the op's ts).
 __global__ void __launch_bounds__(BLOCK) k_fl_commit(OpsDev o, TsIndex x, uint32_t Q, uint32_t nrep,
                                                      const uint32_t* anc, const uint32_t* qc, const uint32_t* logidx,
@@ -1567,7 +1564,7 @@ __global__ void __launch_bounds__(BLOCK) k_fl_commit(OpsDev o, TsIndex x, uint32
   if (lds) {
     for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x) {
       sb[j] = x.base[j];
-      sc[j] = x.cmin[j];
+      sc[j] = x.rng[j].x;
     }
   }
   __syncthreads();
@@ -1817,6 +1814,24 @@ static int run_replay(crdtm_tree* t, const OpsDev& o, uint8_t* st, crdtm_result*
   return CRDTM_E_NOMEM;
 }
 
+__global__ void __launch_bounds__(BLOCK) k_fl_init(uint32_t Q, uint32_t* first, uint32_t* anc, uint32_t* cnt,
+                                                   uint32_t* fill) {
+  GRID_STRIDE(q, Q + 2) {
+    if (q <= Q) {
+      first[q] = NONE;
+      anc[q] = ABSENT;
+    }
+    cnt[q] = 0;
+    fill[q] = 0;
+  }
+}
+
+// Launches k_range_reset when a merge leaves apply_batch by any path.
+struct RangeReset {
+  crdtm_ctx* c;
+  ~RangeReset() { LAUNCH(k_range_reset, dim3(64), dim3(BLOCK), 0, c->stream, c->crange, c->dres); }
+};
+
 // Flat closed form (see the k_fl_* kernels): the index `ix` is dense and
 // already built; Q = its slot range.
 static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_t Q, uint32_t maxr, uint8_t* st,
@@ -1827,8 +1842,13 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   DevResult* dr = c->dres;
   const uint32_t n = o.n;
   const uint32_t g = grid_for(n);
-  uint32_t* anc = ws.alloc<uint32_t>(static_cast<uint64_t>(Q) + 1);
-  HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(anc), static_cast<int>(ABSENT), Q + 1, s));
+  const uint32_t U = Q + 1;  // nodes + the root sentinel
+  uint32_t* anc = ws.alloc<uint32_t>(U);
+  uint32_t* cnt = ws.alloc<uint32_t>(U + 1);
+  uint32_t* fill = ws.alloc<uint32_t>(U + 1);
+  LAUNCH(k_fl_init, dim3(grid_for(U + 1, BLOCK, 4096)), dim3(BLOCK), 0, s, Q, ix.first, anc, cnt, fill);
+  LAUNCH(k_index_store, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix);
+  LAUNCH(k_index_fix, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix);
   LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, anc, t->timestamp, c->rtab, dr);
   int r;
   if ((r = sync_read(c))) return r;
@@ -1871,16 +1891,11 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   }
   if (K > 0) {
     // ---- K2: effective parents, children lists in descending slot order ----
-    const uint32_t U = Q + 1;  // nodes + the root sentinel
-    uint32_t* cnt = ws.alloc<uint32_t>(U + 1);
-    uint32_t* fill = ws.alloc<uint32_t>(U + 1);
     uint32_t* carr = ws.alloc<uint32_t>(U);
     uint32_t* ns = ws.alloc<uint32_t>(U);
-    HIP_CHECK(hipMemsetAsync(cnt, 0, (U + 1) * sizeof(uint32_t), s));
-    HIP_CHECK(hipMemsetAsync(fill, 0, (U + 1) * sizeof(uint32_t), s));
     const uint32_t gq = grid_for(Q);
     uint32_t* rh = ws.alloc<uint32_t>(Q);
-    if ((r = max_scan_incl(anc, nullptr, rh, Q, ws, s))) return r;
+    if ((r = dscan<MaxOp, true>(RunHeadGen{anc}, rh, Q, nullptr, ws, s, &dr->scan_err))) return r;
     LAUNCH(k_fl_ep, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, rh, cnt);
     uint32_t* n_child = &dr->n_sentinels;  // scratch word for the scan total
     if ((r = scan_excl_u32(cnt, cnt, U + 1, n_child, ws, s))) return r;
@@ -1957,19 +1972,12 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   }
   Work w;
   w.st = ws.alloc<uint8_t>(n);
-  uint32_t* cmin = ws.alloc<uint32_t>(RID_SLOTS);
-  uint32_t* cmax = ws.alloc<uint32_t>(RID_SLOTS);
   uint32_t* rbase = ws.alloc<uint32_t>(RID_SLOTS + 1);
   DevResult* dr = c->dres;
-  HIP_CHECK(hipMemsetAsync(dr, 0, sizeof(DevResult), s));
-  HIP_CHECK(hipMemsetAsync(&dr->err_index, 0xFF, sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(cmin, 0xFF, RID_SLOTS * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(cmax, 0, RID_SLOTS * sizeof(uint32_t), s));
-  LAUNCH(k_pre, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, cmin, cmax, dr);
-  // the first HOST_RANGES replica ranges come back with the result block:
-  // the dense index layout (exclusive scan of range sizes) is then a host loop
-  HIP_CHECK(hipMemcpyAsync(c->hrange, cmin, HOST_RANGES * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipMemcpyAsync(c->hrange + HOST_RANGES, cmax, HOST_RANGES * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  LAUNCH(k_dres_init, dim3(1), dim3(64), 0, s, dr);
+  LAUNCH(k_pre, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, c->crange, dr);
+  LAUNCH(k_range_base, dim3(1), dim3(BLOCK), 0, s, c->crange, rbase, dr);
+  RangeReset keep_clean{c};  // resets the context's replica ranges on every exit
   int r;
   if ((r = sync_read(c))) return r;
   if (c->hres->bad_range) return CRDTM_E_RANGE;
@@ -1985,35 +1993,20 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
     return r;
   }
   const uint32_t maxr = c->hres->max_replica;
-  uint64_t range_total = 0;
-  if (maxr < HOST_RANGES) {
-    uint32_t* hb = c->hrange + 2 * HOST_RANGES;
-    for (uint32_t q = 0; q <= maxr; ++q) {
-      hb[q] = static_cast<uint32_t>(std::min<uint64_t>(range_total, NONE));
-      const uint32_t lo = c->hrange[q];
-      if (lo != NONE) range_total += static_cast<uint64_t>(c->hrange[HOST_RANGES + q]) - lo + 1;
-    }
-    HIP_CHECK(hipMemcpyAsync(rbase, hb, (maxr + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-  } else {
-    LAUNCH(k_range_size, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, cmin, cmax, rbase, maxr + 1);
-    if ((r = scan_excl_u32(rbase, rbase, maxr + 1, &dr->range_total, ws, s))) return r;
-    if ((r = sync_read(c))) return r;
-    range_total = c->hres->range_total;
-  }
+  const uint64_t range_total = c->hres->range_total;
   // ts index: dense per-replica runs when possible, else an open-addressing hash
   TsIndex ix;
-  ix.cmin = cmin;
-  ix.cmax = cmax;
+  ix.rng = c->crange;
   ix.base = rbase;
   ix.dense = (!c->hres->has_negative && range_total <= 4ULL * n + 65536) ? 1u : 0u;
   const bool flat = maxlen == 1 && c->hres->n_del == 0;
   if (ix.dense) {
     ix.first = ws.alloc<uint32_t>(range_total + 1);
     ix.h = TsHash{nullptr, nullptr, 0};
+    if (flat) return apply_flat(t, o, ix, static_cast<uint32_t>(range_total), maxr, w.st, st_out, res);
     HIP_CHECK(hipMemsetAsync(ix.first, 0xFF, (range_total + 1) * sizeof(uint32_t), s));
     LAUNCH(k_index_store, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix);
     LAUNCH(k_index_fix, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix);
-    if (flat) return apply_flat(t, o, ix, static_cast<uint32_t>(range_total), maxr, w.st, st_out, res);
   } else {
     const uint32_t H = pow2_at_least(2 * static_cast<uint64_t>(n));
     ix.first = nullptr;

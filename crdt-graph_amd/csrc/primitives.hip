@@ -6,86 +6,14 @@
 
 #include "engine.h"
 #include "listrank.h"
+#include "scan.h"
 
 namespace crdtm {
 
-// ---------------------------------------------------------------------------
-// Exclusive scan (u32), three-phase: per-block scan with block totals,
-// recursive scan of totals, uniform add. 256 threads x 8 items per block.
-// ---------------------------------------------------------------------------
-constexpr int SCAN_ITEMS = 8;
-constexpr int SCAN_TILE = BLOCK * SCAN_ITEMS;
-
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds_waves, uint32_t* total) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t inc = wave_incl_scan(v);
-  if (lane == 63) lds_waves[wave] = inc;
-  __syncthreads();
-  uint32_t wbase = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < BLOCK / 64; ++w) {
-    uint32_t s = lds_waves[w];
-    if (w < wave) wbase += s;
-    tot += s;
-  }
-  __syncthreads();
-  *total = tot;
-  return wbase + inc - v;
-}
-
-__global__ void __launch_bounds__(BLOCK) k_scan_tiles(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                      uint32_t* __restrict__ tile_sums, uint64_t n) {
-  __shared__ uint32_t lw[BLOCK / 64];
-  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
-  uint32_t v[SCAN_ITEMS];
-  uint32_t s = 0;
-#pragma unroll
-  for (int j = 0; j < SCAN_ITEMS; ++j) {
-    v[j] = (base + j < n) ? in[base + j] : 0u;
-    s += v[j];
-  }
-  uint32_t tot;
-  uint32_t ex = block_excl_scan(s, lw, &tot);
-#pragma unroll
-  for (int j = 0; j < SCAN_ITEMS; ++j) {
-    if (base + j < n) out[base + j] = ex;
-    ex += v[j];
-  }
-  if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
-}
-
-__global__ void __launch_bounds__(BLOCK) k_scan_add(uint32_t* __restrict__ out, const uint32_t* __restrict__ tile_off,
-                                                    uint64_t n) {
-  const uint32_t add = tile_off[blockIdx.x];
-  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
-#pragma unroll
-  for (int j = 0; j < SCAN_ITEMS; ++j)
-    if (base + j < n) out[base + j] += add;
-}
-
-__global__ void k_store_total(const uint32_t* in_last, const uint32_t* out_last, uint32_t* total) {
-  *total = *in_last + *out_last;
-}
-
 // out[i] = sum(in[0..i)); *total (device) = sum(in). in may alias out.
 int scan_excl_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* total, Arena& ws, hipStream_t st) {
-  if (n == 0) {
-    if (total) HIP_CHECK(hipMemsetAsync(total, 0, sizeof(uint32_t), st));
-    return CRDTM_OK;
-  }
-  const uint64_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
-  uint32_t* sums = ws.alloc<uint32_t>(tiles + 1);
-  // keep the last input element: `in` may alias `out`
-  uint32_t* last_in = ws.alloc<uint32_t>(1);
-  HIP_CHECK(hipMemcpyAsync(last_in, in + n - 1, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-  LAUNCH(k_scan_tiles, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, in, out, sums, n);
-  if (tiles > 1) {
-    int r = scan_excl_u32(sums, sums, tiles, nullptr, ws, st);
-    if (r) return r;
-    LAUNCH(k_scan_add, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, out, sums, n);
-  }
-  if (total) LAUNCH(k_store_total, dim3(1), dim3(1), 0, st, last_in, out + n - 1, total);
-  return CRDTM_OK;
+  uint32_t* err = ws.alloc<uint32_t>(1);  // a spin that never resolves (cannot happen on a live device)
+  return dscan<SumOp, false>(ArrGen{in}, out, n, total, ws, st, err);
 }
 
 // ---------------------------------------------------------------------------
@@ -410,7 +338,7 @@ static int segmented_sort_t(const uint32_t* seg_start, uint32_t n_seg, uint32_t*
   uint32_t* nbig = &dres->big_segments;
   uint32_t* nhuge = &dres->huge_segments;
   uint32_t* nmid = &dres->mid_segments;
-  HIP_CHECK(hipMemsetAsync(nbig, 0, 3 * sizeof(uint32_t), st));  // big_segments, huge_segments, mid_segments
+  // big_segments / huge_segments / mid_segments start at 0 (k_dres_init, once per merge)
   LAUNCH(k_sort_small<KEY>, dim3(grid_for(n_seg)), dim3(BLOCK), 0, st, seg_start, n_seg, carr, sort_key, skip, mid,
          nmid, big, nbig);
   LAUNCH(k_sort_mid<KEY>, dim3(1024), dim3(BLOCK), 0, st, seg_start, mid, nmid, carr, sort_key);

@@ -1,0 +1,181 @@
+// scan.h — single-pass device-wide scans (decoupled look-back) for crdtm.
+#pragma once
+
+#include "engine.h"
+
+namespace crdtm {
+
+// ---------------------------------------------------------------------------
+// Single-pass scan with decoupled look-back (u32, sum or max). A workgroup
+// takes the next tile by ticket (so every predecessor tile has started),
+// publishes its aggregate, and wave 0 looks back over up to 64 predecessors
+// at a time until it meets an inclusive prefix. Status words pack
+// {flag (1 = aggregate, 2 = prefix) : 2, epoch : 30, value : 32} and move
+// through agent-scope atomics (coherent across the XCDs' L2s); a word from an
+// earlier call carries an older epoch and reads as "not yet published", so
+// the status pool is never cleared. The workgroup that draws the last ticket
+// resets the ticket counter. Every element is read once and written once.
+// Spins are bounded; an exhausted spin sets err.
+// ---------------------------------------------------------------------------
+constexpr int DS_ITEMS = 16;
+constexpr int DS_TILE = BLOCK * DS_ITEMS;
+
+__device__ __forceinline__ unsigned long long ds_load(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ds_store(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr uint32_t DS_EPOCH_MASK = (1u << 30) - 1;
+
+template <class OP, bool INCL, class GEN>
+__global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* __restrict__ out, uint64_t n,
+                                                 unsigned long long* __restrict__ status, uint32_t* __restrict__ ticket,
+                                                 uint32_t ntiles, uint32_t epoch, uint32_t* __restrict__ total,
+                                                 uint32_t* __restrict__ err) {
+  __shared__ uint32_t s_tile, s_prefix;
+  __shared__ uint32_t sw[BLOCK / 64];
+  const unsigned long long ep = static_cast<unsigned long long>(epoch) << 32;
+  if (threadIdx.x == 0) {
+    s_tile = atomicAdd(ticket, 1u);
+    if (s_tile == ntiles - 1) atomicExch(ticket, 0u);  // every ticket is drawn: ready for the next scan
+  }
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint64_t b = static_cast<uint64_t>(tile) * DS_TILE + static_cast<uint64_t>(threadIdx.x) * DS_ITEMS;
+  uint32_t v[DS_ITEMS];
+  gen.load(b, n, v);
+  uint32_t acc = OP::id();
+#pragma unroll
+  for (int j = 0; j < DS_ITEMS; ++j) acc = OP::op(acc, v[j]);
+  // workgroup exclusive scan of the per-thread totals
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t inc = acc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc = OP::op(inc, t);
+  }
+  if (lane == 63) sw[wave] = inc;
+  __syncthreads();
+  uint32_t texcl = __shfl_up(inc, 1, 64);
+  if (lane == 0) texcl = OP::id();
+  uint32_t agg = OP::id();
+  for (int w = 0; w < BLOCK / 64; ++w) {
+    if (w < wave) texcl = OP::op(texcl, sw[w]);
+    agg = OP::op(agg, sw[w]);
+  }
+  if (wave == 0) {
+    uint32_t prefix = OP::id();
+    if (tile == 0) {
+      if (lane == 0) ds_store(&status[0], (2ULL << 62) | ep | agg);
+    } else {
+      if (lane == 0) ds_store(&status[tile], (1ULL << 62) | ep | agg);
+      long long j = static_cast<long long>(tile) - 1;
+      uint32_t spins = 0;
+      for (;;) {
+        const long long idx = j - lane;
+        const unsigned long long s = idx >= 0 ? ds_load(&status[idx]) : ((2ULL << 62) | ep | OP::id());
+        const uint32_t flag = ((s >> 32) & DS_EPOCH_MASK) == epoch ? static_cast<uint32_t>(s >> 62) : 0u;
+        const uint32_t val = static_cast<uint32_t>(s);
+        const unsigned long long pm = __ballot(flag == 2), im = __ballot(flag == 0);
+        uint32_t upto = 64;  // lanes that contribute
+        if (pm) upto = __ffsll(static_cast<long long>(pm));  // lowest prefix lane p -> lanes 0..p
+        const unsigned long long need = upto == 64 ? ~0ULL : ((1ULL << upto) - 1);
+        if (im & need) {
+          if (++spins > (1u << 24)) {  // bounded: never hang the device
+            if (lane == 0) atomicOr(err, 1u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        uint32_t c = static_cast<uint32_t>(lane) < upto ? val : OP::id();
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c = OP::op(c, __shfl_xor(c, o, 64));
+        prefix = OP::op(prefix, c);
+        if (pm) break;
+        j -= 64;
+      }
+      if (lane == 0) ds_store(&status[tile], (2ULL << 62) | ep | OP::op(prefix, agg));
+    }
+    if (lane == 0) {
+      s_prefix = prefix;
+      if (total && tile == ntiles - 1) *total = OP::op(prefix, agg);
+    }
+  }
+  __syncthreads();
+  uint32_t run = OP::op(s_prefix, texcl);
+#pragma unroll
+  for (int j = 0; j < DS_ITEMS; ++j) {
+    const uint32_t x = v[j];
+    if (INCL) {
+      run = OP::op(run, x);
+      v[j] = run;
+    } else {
+      v[j] = run;
+      run = OP::op(run, x);
+    }
+  }
+  if (b + DS_ITEMS <= n) {
+#pragma unroll
+    for (int j = 0; j < DS_ITEMS; j += 4)
+      *reinterpret_cast<uint4*>(out + b + j) = make_uint4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+  } else {
+    for (int j = 0; j < DS_ITEMS; ++j)
+      if (b + j < n) out[b + j] = v[j];
+  }
+}
+
+struct SumOp {
+  static __device__ __forceinline__ uint32_t id() { return 0u; }
+  static __device__ __forceinline__ uint32_t op(uint32_t a, uint32_t b) { return a + b; }
+};
+
+struct ArrGen {
+  const uint32_t* in;
+  __device__ __forceinline__ void load(uint64_t b, uint64_t n, uint32_t* v) const {
+    if (b + DS_ITEMS <= n && (reinterpret_cast<uintptr_t>(in + b) & 15) == 0) {
+#pragma unroll
+      for (int j = 0; j < DS_ITEMS; j += 4) {
+        const uint4 x = *reinterpret_cast<const uint4*>(in + b + j);
+        v[j] = x.x;
+        v[j + 1] = x.y;
+        v[j + 2] = x.z;
+        v[j + 3] = x.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < DS_ITEMS; ++j) v[j] = b + j < n ? in[b + j] : 0u;
+    }
+  }
+};
+
+template <class OP, bool INCL, class GEN>
+int dscan(GEN gen, uint32_t* out, uint64_t n, uint32_t* total, Arena& ws, hipStream_t st, uint32_t* err) {
+  if (n == 0) {
+    if (total) HIP_CHECK(hipMemsetAsync(total, 0, sizeof(uint32_t), st));
+    return CRDTM_OK;
+  }
+  const uint64_t tiles = (n + DS_TILE - 1) / DS_TILE;
+  ws.scan_epoch = (ws.scan_epoch % DS_EPOCH_MASK) + 1;  // 1..2^30-1; zeroed memory never matches
+  unsigned long long* status = ws.scan_status;
+  uint32_t* ticket = ws.scan_ticket;
+  if (!status || tiles > ws.scan_cap) {  // beyond the pool: a zeroed status array of its own
+    status = ws.alloc<unsigned long long>(tiles + 1);
+    ticket = reinterpret_cast<uint32_t*>(status + tiles);
+    HIP_CHECK(hipMemsetAsync(status, 0, (tiles + 1) * sizeof(unsigned long long), st));
+  }
+  auto* kfn = &k_dscan<OP, INCL, GEN>;
+  LAUNCH(kfn, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, gen, out, n, status, ticket,
+         static_cast<uint32_t>(tiles), ws.scan_epoch, total, err);
+  return CRDTM_OK;
+}
+
+struct MaxOp {
+  static __device__ __forceinline__ uint32_t id() { return 0u; }
+  static __device__ __forceinline__ uint32_t op(uint32_t a, uint32_t b) { return a > b ? a : b; }
+};
+
+}  // namespace crdtm
