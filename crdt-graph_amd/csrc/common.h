@@ -70,6 +70,7 @@ struct DevResult {
   uint32_t range_total;     // dense index size
   uint32_t max_replica;     // largest replica id of an Add timestamp
   uint32_t scan_err;        // a look-back scan gave up (never on a live device)
+  uint32_t dup_fix;         // flat status: a duplicate timestamp took its slot, decide again
 };
 
 #define HIP_CHECK(x)                                                                         \

@@ -1298,24 +1298,49 @@ __global__ void __launch_bounds__(64) k_forest(OpsDev o, ForestArgs f, const uin
 // Q. anc[q] = ABSENT marks a slot without an applied Add.
 // ---------------------------------------------------------------------------
 
-// K1 (flat): status of every op; applied Adds record their anchor slot.
-// Fused with the batch accounting (k_stats) and the replicas fold: every
+// K1 (flat). Slot records rec[q] = (index of the first Add of slot q) << 32
+// | (anchor slot of that Add: Q = the dict's sentinel, NONE = anchor key not
+// in the batch); REC_EMPTY = no Add. k_fl_store writes every Add's record
+// with one plain 8-byte store (an arbitrary duplicate wins); k_fl_status
+// then decides every op, and a smaller duplicate that lost the store race
+// takes the slot with a 64-bit atomicMin (op index in the high word) and
+// flags a second status pass.
+constexpr unsigned long long REC_EMPTY = ~0ULL;
+
+__global__ void __launch_bounds__(BLOCK) k_fl_store(OpsDev o, TsIndex x, uint32_t Q, unsigned long long* rec) {
+  QUAD_LOOP_XCD(i0, o.n) {
+    Quad qd;
+    load_quad(o, i0, qd);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      if (k >= qd.cnt || qd.off[k + 1] == qd.off[k] || qd.ts[k] <= 0) continue;
+      const uint32_t q = tsindex_slot(x, qd.ts[k]);
+      const long long kk = o.path[qd.off[k]];
+      const uint32_t qa = kk == 0 ? Q : tsindex_slot(x, kk);
+      rec[q] = (static_cast<unsigned long long>(i0 + k) << 32) | qa;
+    }
+  }
+}
+
+// Status of every op (update / addAfterHelp, src/Internal/Node.elm:56-90,
+// :138-163), fused with the batch accounting and the replicas fold: every
 // applied Add's replica keeps its last op index in a direct-mapped LDS table
-// (ids < REP_DIRECT), flushed once per block into the replica table.
-__global__ void __launch_bounds__(BLOCK) k_fl_status(OpsDev o, uint8_t* st, TsIndex x, uint32_t Q, uint32_t* anc,
-                                                     long long ts0, uint32_t* rtab, DevResult* dres) {
+// (ids < REP_DIRECT), flushed once per workgroup into the replica table.
+__global__ void __launch_bounds__(BLOCK) k_fl_status(OpsDev o, uint8_t* st, TsIndex x, uint32_t Q,
+                                                     unsigned long long* rec, long long ts0, uint32_t* rtab,
+                                                     DevResult* dres) {
   __shared__ uint32_t rv[REP_DIRECT];
   for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) rv[j] = 0;
   __syncthreads();
   const long long id0 = replica_of(ts0);
-  uint32_t app = 0, alr = 0, own = 0, err = NONE;
+  uint32_t app = 0, alr = 0, own = 0, err = NONE, dup = 0;
   QUAD_LOOP_XCD(i0, o.n) {
     Quad qd;
     load_quad(o, i0, qd);
     uint8_t s4[4] = {0, 0, 0, 0};
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
-      if (k >= qd.cnt) break;
+      if (k >= qd.cnt) continue;
       const uint32_t i = i0 + k;
       uint8_t s;
       const long long ts = qd.ts[k];
@@ -1323,30 +1348,33 @@ __global__ void __launch_bounds__(BLOCK) k_fl_status(OpsDev o, uint8_t* st, TsIn
         s = ST_INVALID;  // update [] = InvalidPath (src/Internal/Node.elm:147-148)
       } else {
         const uint32_t q = tsindex_slot(x, ts);
-        if (q == NONE || x.first[q] != i) {
-          s = ST_ALREADY;  // ts 0 is the sentinel's key / `child ts parent` exists (:63-65)
+        if (q == NONE) {
+          s = ST_ALREADY;  // ts 0 is the sentinel's key (:63-65)
         } else {
-          const long long kk = o.path[qd.off[k]];
-          uint32_t a = Q;  // anchor 0 = the dict's sentinel
-          if (kk != 0) {
-            const uint32_t qa = tsindex_slot(x, kk);
-            const uint32_t fa = qa == NONE ? NONE : x.first[qa];
-            a = (fa != NONE && fa < i) ? qa : NONE;  // the anchor must exist before op i (:68-70)
-          }
-          if (a == NONE) {
-            s = ST_NOTFOUND;
+          const unsigned long long r = rec[q];
+          const uint32_t fi = static_cast<uint32_t>(r >> 32);
+          if (fi != i) {
+            s = ST_ALREADY;  // `child ts parent` exists (:63-65)
+            if (i < fi) {    // lost the store race to a later duplicate: take the slot
+              const long long kk = o.path[qd.off[k]];
+              const uint32_t qa = kk == 0 ? Q : tsindex_slot(x, kk);
+              atomicMin(&rec[q], (static_cast<unsigned long long>(i) << 32) | qa);
+              dup = 1;
+            }
           } else {
-            s = ST_APPLIED;
-            anc[q] = a;
+            const uint32_t qa = static_cast<uint32_t>(r);
+            bool ok = qa == Q;  // anchored at the sentinel
+            if (!ok && qa != NONE) ok = static_cast<uint32_t>(rec[qa] >> 32) < i;  // anchor Added before (:68-70)
+            s = ok ? ST_APPLIED : ST_NOTFOUND;
           }
         }
       }
       s4[k] = s;
       if (s == ST_APPLIED) {
         ++app;
-        const uint32_t r = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32);
-        if (r < REP_DIRECT) atomicMax(&rv[r], i + 1);
-        else atomicMax(&rtab[r + (1u << (REPLICA_BITS - 1))], i + 1);
+        const uint32_t rr = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32);
+        if (rr < REP_DIRECT) atomicMax(&rv[rr], i + 1);
+        else atomicMax(&rtab[rr + (1u << (REPLICA_BITS - 1))], i + 1);
       } else if (s == ST_ALREADY) {
         ++alr;
       } else {
@@ -1364,6 +1392,7 @@ __global__ void __launch_bounds__(BLOCK) k_fl_status(OpsDev o, uint8_t* st, TsIn
   alr = block_sum(alr);
   own = block_sum(own);
   err = block_min(err);
+  dup = block_max(dup);
   if (threadIdx.x == 0) {
     if (app) {
       atomicAdd(&dres->n_applied, app);
@@ -1372,7 +1401,18 @@ __global__ void __launch_bounds__(BLOCK) k_fl_status(OpsDev o, uint8_t* st, TsIn
     if (alr) atomicAdd(&dres->n_already, alr);
     if (own) atomicAdd(&dres->own_ok_adds, own);
     if (err != NONE) atomicMin(&dres->err_index, err);
+    if (dup) atomicOr(&dres->dup_fix, 1u);
   }
+}
+
+// Before the second status pass: forget the first pass's accounting.
+__global__ void k_fl_stat_reset(DevResult* d) {
+  d->n_applied = 0;
+  d->n_adds_applied = 0;
+  d->n_already = 0;
+  d->own_ok_adds = 0;
+  d->err_index = NONE;
+  d->dup_fix = 0;
 }
 
 // replicas[r] := ts of replica r's last applied Add (flat: Adds only, ids in
@@ -1427,23 +1467,38 @@ __global__ void __launch_bounds__(BLOCK) k_fl_ep(uint32_t Q, uint32_t* anc, cons
 // Run heads: rh[q] = max{q' <= q : anc[q'] != q' - 1}, an inclusive
 // max-scan over head flags (scan.h).
 struct RunHeadGen {
-  const uint32_t* anc;
+  const unsigned long long* rec;
+  uint32_t* anc;  // side output: anchor slot per slot (ABSENT = no node)
+  __device__ __forceinline__ uint32_t anchor(unsigned long long r) const {
+    return r == REC_EMPTY ? ABSENT : static_cast<uint32_t>(r);
+  }
   __device__ __forceinline__ void load(uint64_t b, uint64_t n, uint32_t* v) const {
     if (b + DS_ITEMS <= n) {
+      uint32_t a[DS_ITEMS];
 #pragma unroll
-      for (int j = 0; j < DS_ITEMS; j += 4) {
-        const uint4 x = *reinterpret_cast<const uint4*>(anc + b + j);
+      for (int j = 0; j < DS_ITEMS; j += 2) {
+        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(rec + b + j);
+        a[j] = anchor(x.x);
+        a[j + 1] = anchor(x.y);
+      }
+#pragma unroll
+      for (int j = 0; j < DS_ITEMS; j += 4)
+        *reinterpret_cast<uint4*>(anc + b + j) = make_uint4(a[j], a[j + 1], a[j + 2], a[j + 3]);
+#pragma unroll
+      for (int j = 0; j < DS_ITEMS; ++j) {
         const uint32_t q = static_cast<uint32_t>(b) + j;
-        v[j] = (q == 0 || x.x != q - 1) ? q : 0u;
-        v[j + 1] = x.y != q ? q + 1 : 0u;
-        v[j + 2] = x.z != q + 1 ? q + 2 : 0u;
-        v[j + 3] = x.w != q + 2 ? q + 3 : 0u;
+        v[j] = (q == 0 || a[j] != q - 1) ? q : 0u;
       }
     } else {
 #pragma unroll
       for (int j = 0; j < DS_ITEMS; ++j) {
         const uint64_t q = b + j;
-        v[j] = (q < n && (q == 0 || anc[q] != q - 1)) ? static_cast<uint32_t>(q) : 0u;
+        uint32_t a = ABSENT;
+        if (q < n) {
+          a = anchor(rec[q]);
+          anc[q] = a;
+        }
+        v[j] = (q < n && (q == 0 || a != q - 1)) ? static_cast<uint32_t>(q) : 0u;
       }
     }
   }
@@ -1556,8 +1611,8 @@ __global__ void __launch_bounds__(BLOCK) k_fl_present(uint32_t Q, const uint32_t
 // replica r with base[r] <= q (largest such r) and counter min[r] + q -
 // base[r] (tables in LDS when the replica ids fit, else the op's ts).
 __global__ void __launch_bounds__(BLOCK) k_fl_commit(OpsDev o, TsIndex x, uint32_t Q, uint32_t nrep,
-                                                     const uint32_t* anc, const uint32_t* qc, const uint32_t* logidx,
-                                                     TreeDev T) {
+                                                     const uint32_t* anc, const unsigned long long* rec,
+                                                     const uint32_t* qc, const uint32_t* logidx, TreeDev T) {
   __shared__ uint32_t sb[HOST_RANGES];
   __shared__ uint32_t sc[HOST_RANGES];
   const bool lds = nrep <= HOST_RANGES;
@@ -1571,7 +1626,7 @@ __global__ void __launch_bounds__(BLOCK) k_fl_commit(OpsDev o, TsIndex x, uint32
   GRID_STRIDE(q, Q) {
     if (anc[q] == ABSENT) continue;
     const uint32_t slot = 1 + (qc ? qc[q] : q);
-    const uint32_t i = x.first[q];
+    const uint32_t i = static_cast<uint32_t>(rec[q] >> 32);
     long long key;
     if (lds) {
       uint32_t lo = 0, hi = nrep;  // largest r with sb[r] <= q
@@ -1814,13 +1869,10 @@ static int run_replay(crdtm_tree* t, const OpsDev& o, uint8_t* st, crdtm_result*
   return CRDTM_E_NOMEM;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_fl_init(uint32_t Q, uint32_t* first, uint32_t* anc, uint32_t* cnt,
+__global__ void __launch_bounds__(BLOCK) k_fl_init(uint32_t Q, unsigned long long* rec, uint32_t* cnt,
                                                    uint32_t* fill) {
   GRID_STRIDE(q, Q + 2) {
-    if (q <= Q) {
-      first[q] = NONE;
-      anc[q] = ABSENT;
-    }
+    if (q < Q) rec[q] = REC_EMPTY;
     cnt[q] = 0;
     fill[q] = 0;
   }
@@ -1843,15 +1895,21 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   const uint32_t n = o.n;
   const uint32_t g = grid_for(n);
   const uint32_t U = Q + 1;  // nodes + the root sentinel
+  unsigned long long* rec = ws.alloc<unsigned long long>(Q + 1);
   uint32_t* anc = ws.alloc<uint32_t>(U);
   uint32_t* cnt = ws.alloc<uint32_t>(U + 1);
   uint32_t* fill = ws.alloc<uint32_t>(U + 1);
-  LAUNCH(k_fl_init, dim3(grid_for(U + 1, BLOCK, 4096)), dim3(BLOCK), 0, s, Q, ix.first, anc, cnt, fill);
-  LAUNCH(k_index_store, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix);
-  LAUNCH(k_index_fix, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix);
-  LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, anc, t->timestamp, c->rtab, dr);
+  LAUNCH(k_fl_init, dim3(grid_for(U + 1, BLOCK, 4096)), dim3(BLOCK), 0, s, Q, rec, cnt, fill);
+  LAUNCH(k_fl_store, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix, Q, rec);
+  LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, rec, t->timestamp, c->rtab, dr);
   int r;
   if ((r = sync_read(c))) return r;
+  if (c->hres->dup_fix) {  // duplicate timestamps: the records are final now, decide again
+    LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr, nullptr);
+    LAUNCH(k_fl_stat_reset, dim3(1), dim3(1), 0, s, dr);
+    LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, rec, t->timestamp, c->rtab, dr);
+    if ((r = sync_read(c))) return r;
+  }
   const DevResult h1 = *c->hres;
   uint32_t guard = 0;
   const long long new_ts = t->timestamp + h1.own_ok_adds;
@@ -1895,7 +1953,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     uint32_t* ns = ws.alloc<uint32_t>(U);
     const uint32_t gq = grid_for(Q);
     uint32_t* rh = ws.alloc<uint32_t>(Q);
-    if ((r = dscan<MaxOp, true>(RunHeadGen{anc}, rh, Q, nullptr, ws, s, &dr->scan_err))) return r;
+    if ((r = dscan<MaxOp, true>(RunHeadGen{rec, anc}, rh, Q, nullptr, ws, s, &dr->scan_err))) return r;
     LAUNCH(k_fl_ep, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, rh, cnt);
     uint32_t* n_child = &dr->n_sentinels;  // scratch word for the scan total
     if ((r = scan_excl_u32(cnt, cnt, U + 1, n_child, ws, s))) return r;
@@ -1931,7 +1989,8 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
       LAUNCH(k_log, dim3(g), dim3(BLOCK), 0, s, o, st, t->d, 0u, 0u, logidx, plen);
       LAUNCH(k_log_tail, dim3(1), dim3(1), 0, s, t->d, 0u, &dr->log_n, 0u, &dr->log_npath);
     }
-    LAUNCH(k_fl_commit, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, o, ix, Q, maxr + 1, anc, qc, logidx, t->d);
+    LAUNCH(k_fl_commit, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, o, ix, Q, maxr + 1, anc, rec, qc, logidx,
+           t->d);
   }
   if (all_applied) LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
   long long* rep = ws.alloc<long long>(2 * static_cast<uint64_t>(maxr) + 2);
@@ -2001,9 +2060,10 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   ix.dense = (!c->hres->has_negative && range_total <= 4ULL * n + 65536) ? 1u : 0u;
   const bool flat = maxlen == 1 && c->hres->n_del == 0;
   if (ix.dense) {
-    ix.first = ws.alloc<uint32_t>(range_total + 1);
     ix.h = TsHash{nullptr, nullptr, 0};
+    ix.first = nullptr;
     if (flat) return apply_flat(t, o, ix, static_cast<uint32_t>(range_total), maxr, w.st, st_out, res);
+    ix.first = ws.alloc<uint32_t>(range_total + 1);
     HIP_CHECK(hipMemsetAsync(ix.first, 0xFF, (range_total + 1) * sizeof(uint32_t), s));
     LAUNCH(k_index_store, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix);
     LAUNCH(k_index_fix, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix);
