@@ -55,6 +55,20 @@ def head(s, m):
                 path_off=off[:m + 1].copy(), path=s["path"][:off[m]].copy())
 
 
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary
+    of this workload (profiles/*_pmc.json, written by tools/pmc_summary.py from
+    separate FETCH_SIZE and WRITE_SIZE passes of `bench.py`; FETCH_SIZE doubled
+    per the gfx950 correction). None when no summary covers the kernel."""
+    path = os.path.join(ROOT, "profiles", f"r1_{workload}_pmc.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    e = d.get(kernel.split("<")[0])
+    return None if not e or "hbm_bytes_corrected" not in e else e["hbm_bytes_corrected"]
+
+
 def cpu_baseline(s, m):
     """Oracle restatement (oracle/, test infrastructure) on the first m ops, one core."""
     from oracle.oracle import lib as olib, _ptr
@@ -161,14 +175,19 @@ def main():
     per_step = {}
     for nm, v in acc.items():
         per_step[nm] = sum(v) / max(1, args.profile_steps)
-    dominant = max(per_step, key=per_step.get)
-    # average duration of one launch of the dominant kernel
-    launches = len(acc[dominant]) / max(1, args.profile_steps)
-    t_dom = per_step[dominant] / launches / 1e3
+    # Roofline kernel: the longest kernel that processes the whole batch in
+    # one launch (its units = every op of the batch); kernels
+    # launched several times per step work on sub-problems (list-ranking
+    # levels, scan recursion) whose units are not ops.
+    single = {nm: t for nm, t in per_step.items() if len(acc[nm]) == max(1, args.profile_steps)}
+    dominant = max(single or per_step, key=(single or per_step).get)
+    t_dom = per_step[dominant] / 1e3
+    kernels_ms = sum(per_step.values())
 
     ms_step = elapsed / args.steps * 1e3
     value = world * n * args.steps / elapsed
     achieved = B_alg / t_dom / 1e9
+    traffic = pmc_traffic(args.workload, dominant)
     line = {
         "metric": "merged ops/sec (whole node) on 10M-op batch",
         "value": value,
@@ -187,8 +206,8 @@ def main():
                    "path": {1: "closed-form", 2: "replay"}.get(path_taken, "?"),
                    "parallelism": f"documents sharded by id over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "alg_bytes_per_launch": B_alg, "kernel_ms": t_dom * 1e3,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "alg_bytes_per_launch": B_alg, "kernel_ms": t_dom * 1e3, "kernels_ms_per_step": kernels_ms,
                      "merge_frac": B_alg / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS},
     }
     if args.verbose and rank == 0:
@@ -285,8 +304,11 @@ def run_trees(args, rank, world, local_rank):
     k = L.crdtm_ctx_phase_times(ctx, names, len(names), ms, 64)
     labels = names.raw.split(b"\0")
     L.crdtm_ctx_profile(ctx, 0)
-    per_k = {labels[j].decode(): ms[j] for j in range(min(k, 64))}
+    per_k = {}
+    for j in range(min(k, 64)):
+        per_k[labels[j].decode()] = per_k.get(labels[j].decode(), 0.0) + ms[j]
     dominant = max(per_k, key=per_k.get)
+    kernels_ms = sum(per_k.values())
     ot = state["ops_t"]
     kinds = ot["kind"].cpu().numpy()
     B_alg = int(np.sum(np.where(kinds == 0, 57, 17)))  # flat documents: L = 1
@@ -302,7 +324,7 @@ def run_trees(args, rank, world, local_rank):
                    "parallelism": f"documents sharded by id over {world} GPU(s); op logs all-gathered (RCCL)"},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": B_alg / t_dom / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": B_alg / t_dom / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                     "alg_bytes_per_launch": B_alg, "kernel_ms": t_dom * 1e3,
+                     "alg_bytes_per_launch": B_alg, "kernel_ms": t_dom * 1e3, "kernels_ms_per_step": kernels_ms,
                      "merge_frac": B_alg / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS},
     }
     if args.verbose and rank == 0:

@@ -215,7 +215,7 @@ int crdtm_ctx_create(int device, void* stream, crdtm_ctx** out) {
 int crdtm_ctx_destroy(crdtm_ctx* c) {
   if (!c) return CRDTM_OK;
   hipStreamSynchronize(c->stream);
-  for (auto& m : c->marks) hipEventDestroy(m.second);
+  c->clear_marks();
   if (c->ws.base) hipFree(c->ws.base);
   hipFree(c->dres);
   hipHostFree(c->hres);
@@ -348,8 +348,7 @@ int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_b
   if (ops->n_ops >= 0x7FFFFFF0ULL) return CRDTM_E_ARG;
   crdtm_ctx* c = t->ctx;
   HIP_CHECK(hipSetDevice(c->device));
-  for (auto& m : c->marks) hipEventDestroy(m.second);
-  c->marks.clear();
+  c->clear_marks();
   const uint64_t n = ops->n_ops;
   uint64_t np = ops->n_path;
   if (!ops_on_device && n) np = ops->path_off[n];
@@ -393,7 +392,6 @@ int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_b
         if (status_out) st_dev = c->ws.alloc<uint8_t>(n + 1);
       }
       g_prof = c->profile ? c : nullptr;
-      mark(c, "start");
       r = apply_batch(t, o, st_dev, res);
       g_prof = nullptr;
       if (r == CRDTM_OK && status_out && !ops_on_device && n) {
@@ -419,12 +417,7 @@ int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_b
   res->n_slots = t->n_slots;
   if (c->profile) {
     HIP_CHECK(hipStreamSynchronize(c->stream));
-    c->phases.clear();
-    for (size_t k = 1; k < c->marks.size(); ++k) {
-      float ms = 0;
-      hipEventElapsedTime(&ms, c->marks[k - 1].second, c->marks[k].second);
-      c->phases.emplace_back(c->marks[k].first, ms);
-    }
+    c->collect_phases();
   }
   return res->code < 0 ? res->code : CRDTM_OK;
 }
@@ -554,8 +547,7 @@ int crdtm_forest_apply(crdtm_ctx* c, int64_t replica_id, const crdtm_ops* ops, c
   int r = ensure_arena(c, forest_ws_bytes(doc_off, n_docs, n, np));
   if (r) return r;
   c->ws.reset();
-  for (auto& m : c->marks) hipEventDestroy(m.second);
-  c->marks.clear();
+  c->clear_marks();
   try {
     OpsDev o;
     o.n = static_cast<uint32_t>(n);
@@ -588,7 +580,6 @@ int crdtm_forest_apply(crdtm_ctx* c, int64_t replica_id, const crdtm_ops* ops, c
       o.val = val;
     }
     g_prof = c->profile ? c : nullptr;
-    mark(c, "start");
     r = forest_apply(c, replica_id, o, doc_off, n_docs, doc_code, doc_err, doc_applied, doc_hash, doc_words,
                      doc_timestamp);
     g_prof = nullptr;
@@ -597,12 +588,7 @@ int crdtm_forest_apply(crdtm_ctx* c, int64_t replica_id, const crdtm_ops* ops, c
   }
   if (c->profile) {
     HIP_CHECK(hipStreamSynchronize(c->stream));
-    c->phases.clear();
-    for (size_t k = 1; k < c->marks.size(); ++k) {
-      float ms = 0;
-      hipEventElapsedTime(&ms, c->marks[k - 1].second, c->marks[k].second);
-      c->phases.emplace_back(c->marks[k].first, ms);
-    }
+    c->collect_phases();
   }
   return r;
 }

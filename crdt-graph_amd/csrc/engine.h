@@ -86,8 +86,31 @@ struct crdtm_ctx {
   uint32_t* rtab = nullptr;          // replica table [REPLICA_SLOTS], 0 = empty (kept clean between calls)
   uint2* crange = nullptr;           // replica counter ranges [RID_SLOTS] {min, max}, kept clean between calls
   bool profile = false;
-  std::vector<std::pair<std::string, hipEvent_t>> marks;
+  // profiling: one {name, begin, end} event pair per kernel launch
+  struct Mark {
+    std::string name;
+    hipEvent_t begin, end;
+  };
+  std::vector<Mark> marks;
+  hipEvent_t pending = nullptr;  // begin event of the launch in flight
   std::vector<std::pair<std::string, double>> phases;
+  void clear_marks() {
+    for (auto& m : marks) {
+      hipEventDestroy(m.begin);
+      hipEventDestroy(m.end);
+    }
+    marks.clear();
+    if (pending) hipEventDestroy(pending);
+    pending = nullptr;
+  }
+  void collect_phases() {  // after a stream synchronisation
+    phases.clear();
+    for (auto& m : marks) {
+      float ms = 0;
+      hipEventElapsedTime(&ms, m.begin, m.end);
+      phases.emplace_back(m.name, ms);
+    }
+  }
 };
 
 struct crdtm_tree {
@@ -138,15 +161,21 @@ int linearize(crdtm_tree* t);  // fills t->d.doc / t->doc_n from the tree state
 int forest_apply(crdtm_ctx* c, int64_t replica_id, const OpsDev& o, const uint32_t* doc_off_host, uint64_t n_docs,
                  int32_t* code, int64_t* err, uint32_t* applied, uint64_t* vhash, uint64_t* vwords, int64_t* tstamp);
 uint64_t forest_ws_bytes(const uint32_t* doc_off_host, uint64_t n_docs, uint64_t n_ops, uint64_t n_path);
+void mark_begin(crdtm_ctx* c);
 void mark(crdtm_ctx* c, const char* name);
-// Profiling hook: when the current context profiles, every launch records a
-// HIP event on the launch stream so each kernel's device time is measurable.
+// Profiling hook: when the current context profiles, every launch is
+// bracketed by two HIP events on the launch stream, so each kernel's device
+// time is measured on its own (no host gaps between launches).
 extern thread_local crdtm_ctx* g_prof;
+inline void prof_begin() {
+  if (g_prof) mark_begin(g_prof);
+}
 inline void prof_mark(const char* name) {
   if (g_prof) mark(g_prof, name);
 }
 #define LAUNCH(k, grid, block, shm, st, ...)                    \
   do {                                                          \
+    ::crdtm::prof_begin();                                      \
     hipLaunchKernelGGL(k, grid, block, shm, st, __VA_ARGS__);   \
     ::crdtm::prof_mark(#k);                                     \
   } while (0)

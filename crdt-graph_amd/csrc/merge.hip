@@ -1668,12 +1668,23 @@ __global__ void __launch_bounds__(BLOCK) k_fl_log_copy(OpsDev o, TreeDev T) {
 // ---------------------------------------------------------------------------
 thread_local crdtm_ctx* g_prof = nullptr;
 
-void mark(crdtm_ctx* c, const char* name) {
+void mark_begin(crdtm_ctx* c) {
   if (!c->profile) return;
+  if (c->pending) hipEventDestroy(c->pending);
+  c->pending = nullptr;
   hipEvent_t e;
   if (hipEventCreate(&e) != hipSuccess) return;
   hipEventRecord(e, c->stream);
-  c->marks.emplace_back(name, e);
+  c->pending = e;
+}
+
+void mark(crdtm_ctx* c, const char* name) {
+  if (!c->profile || !c->pending) return;
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return;
+  hipEventRecord(e, c->stream);
+  c->marks.push_back({name, c->pending, e});
+  c->pending = nullptr;
 }
 
 template <class T>
@@ -1771,7 +1782,6 @@ static int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& w
   LAUNCH(k_rep_max, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, s, o, st, c->rtab);
   LAUNCH(k_rep_out, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab, rep, &dr->n_replica_out);
   LAUNCH(k_rep_reset, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab);
-  mark(c, "log+replicas");
   if ((r = sync_read(c))) return r;
   const uint32_t nrep = c->hres->n_replica_out;
   if (nrep) {
@@ -1840,7 +1850,6 @@ static int run_replay(crdtm_tree* t, const OpsDev& o, uint8_t* st, crdtm_result*
     a.src_is_op = 0;
     HIP_CHECK(hipMemsetAsync(c->dres, 0, sizeof(DevResult), s));
     LAUNCH(k_replay, dim3(1), dim3(64), 0, s, o, a, st, c->dres);
-    mark(c, "replay");
     if ((r = sync_read(c))) return r;
     const DevResult& h = *c->hres;
     if (h.replay_overflow) {

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel summary of rocprofv3 --pmc CSVs (one pass per directory).
 
-    python tools/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_sq
+    python tools/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_sq [--json out.json]
 
 FETCH_SIZE / WRITE_SIZE are in KB per dispatch. On gfx950 FETCH_SIZE counts
 half the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md, HBM);
@@ -26,7 +26,18 @@ def load(d):
     return out, meta
 
 
-def main(dirs):
+def base_name(k):
+    """crdtm::k_lc_contract<crdtm::FlatEulerSrc> -> k_lc_contract (the name bench.py's HIP-event marks use)."""
+    return k.split("<")[0].split("::")[-1]
+
+
+def main(args):
+    out_json = None
+    if "--json" in args:
+        i = args.index("--json")
+        out_json = args[i + 1]
+        args = args[:i] + args[i + 2:]
+    dirs = args
     agg = defaultdict(dict)
     meta = {}
     for d in dirs:
@@ -42,6 +53,19 @@ def main(dirs):
         f = agg[k].get("FETCH_SIZE", (0, 0))[0]
         w = agg[k].get("WRITE_SIZE", (0, 0))[0]
         print(k[:40].ljust(40), " ".join(meta.get(k, ("?", "?", "?"))).ljust(12), vals, f"{(2 * f + w) / 1024:9.1f}")
+    if out_json:
+        import json
+        res = {}
+        for k, cs in agg.items():
+            b = base_name(k)
+            e = {c: v[0] for c, v in cs.items()}
+            e["dispatches"] = max(v[1] for v in cs.values())
+            if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
+                # bytes per dispatch; FETCH_SIZE doubled (gfx950 counts half of wide streaming reads)
+                e["hbm_bytes_corrected"] = (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
+                e["hbm_bytes_raw"] = (e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
+            res.setdefault(b, e)
+        json.dump(res, open(out_json, "w"), indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
