@@ -106,6 +106,10 @@ def main():
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    # One explicit stream shared by torch and the engine (crdtm_ctx_create on
+    # its handle): the default stream's handle is 0, which the C ABI reads as
+    # "engine-owned stream" and which would not be ordered with torch's work.
+    torch.cuda.set_stream(torch.cuda.Stream(device=local_rank))
 
     from crdtm import _native as N
     L = N.lib()

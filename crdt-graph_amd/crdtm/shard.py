@@ -79,27 +79,31 @@ def all_gather_records(local: torch.Tensor, group=None) -> torch.Tensor:
     return torch.cat(parts, 0)
 
 
+_ARANGE = {}
+
+
 def assemble(records: torch.Tensor, rank, world, n_docs, per_doc):
     """Records of every replica -> SoA ops of this rank's documents in causal order.
     Documents owned: t = rank, rank + world, ... (local index t // world);
-    every document holds exactly per_doc ops."""
+    every document holds exactly per_doc ops. Sync-free: records of other
+    ranks' documents are scattered into a spill slot at index n."""
     doc = records[:, 0] >> 32
+    seq = records[:, 0] & 0xFFFFFFFF
     keep = (doc % world) == rank
-    r = records[keep]
-    doc = r[:, 0] >> 32
-    seq = r[:, 0] & 0xFFFFFFFF
     n_mine = (n_docs - rank + world - 1) // world
-    dst = (doc // world) * per_doc + seq
     n = n_mine * per_doc
+    dst = torch.where(keep, (doc // world) * per_doc + seq, torch.full_like(doc, n))
     dev = records.device
-    kind = torch.zeros(n, dtype=torch.uint8, device=dev)
-    val = torch.zeros(n, dtype=torch.int32, device=dev)
-    ts = torch.zeros(n, dtype=torch.int64, device=dev)
-    path = torch.zeros(n, dtype=torch.int64, device=dev)
-    kind[dst] = (r[:, 1] >> 32).to(torch.uint8)
-    val[dst] = (r[:, 1] & 0xFFFFFFFF).to(torch.int32)
-    ts[dst] = r[:, 2]
-    path[dst] = r[:, 3]
-    path_off = torch.arange(n + 1, dtype=torch.int32, device=dev)
+    kind = torch.zeros(n + 1, dtype=torch.uint8, device=dev)
+    val = torch.zeros(n + 1, dtype=torch.int32, device=dev)
+    ts = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    path = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    kind[dst] = (records[:, 1] >> 32).to(torch.uint8)
+    val[dst] = (records[:, 1] & 0xFFFFFFFF).to(torch.int32)
+    ts[dst] = records[:, 2]
+    path[dst] = records[:, 3]
+    key = (str(dev), n)
+    if key not in _ARANGE:
+        _ARANGE[key] = torch.arange(n + 1, dtype=torch.int32, device=dev)
     doc_off = np.arange(n_mine + 1, dtype=np.uint32) * per_doc
-    return dict(kind=kind, ts=ts, path_off=path_off, path=path, val=val), doc_off, int(keep.sum().item())
+    return dict(kind=kind, ts=ts, path_off=_ARANGE[key], path=path, val=val), doc_off, keep

@@ -18,11 +18,8 @@ struct Sink {
   uint64_t h = FNV_OFF;
   void put(int64_t w) {
     if (out && n < cap) out[n] = w;
-    uint64_t u = static_cast<uint64_t>(w);
-    for (int i = 0; i < 8; ++i) {
-      h ^= (u >> (8 * i)) & 0xff;
-      h *= FNV_PRIME;
-    }
+    h ^= static_cast<uint64_t>(w);  // word-wise FNV-1a over 64-bit words (same as the oracle)
+    h *= FNV_PRIME;
     ++n;
   }
 };

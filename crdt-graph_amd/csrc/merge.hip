@@ -1190,19 +1190,233 @@ __host__ __device__ __forceinline__ uint32_t forest_hash_cap(uint32_t nops) {
 struct Fnv {
   unsigned long long h = 1469598103934665603ULL, n = 0;
   __device__ void put(long long w) {
-    const unsigned long long u = static_cast<unsigned long long>(w);
-    for (int k = 0; k < 8; ++k) {
-      h ^= (u >> (8 * k)) & 0xff;
-      h *= 1099511628211ULL;
-    }
+    h ^= static_cast<unsigned long long>(w);  // word-wise FNV-1a over 64-bit words
+    h *= 1099511628211ULL;
     ++n;
   }
 };
 
+// ---------------------------------------------------------------------------
+// Forest fast path for flat documents (every op's path has length <= 1) of
+// at most FL_MAXOPS ops, in two kernels (one wave per document each).
+// k_forest_prep (64 lanes): the document's Add keys and the sentinel key 0
+// are sorted in LDS (bitonic); a key's slot = the index of its first
+// occurrence, so slot order is key order (findInsertion's `ts > key` becomes
+// a slot comparison) and every op's target / anchor slot is one binary
+// search. Result: one packed word per op in HBM.
+// k_forest_replay (one lane, 4 KB of LDS per document, so 32 documents per
+// CU): the literal sequential replay of addAfterHelp / findInsertion /
+// deleteHelp (src/Internal/Node.elm:56-122) on one packed word per slot
+// {next, source op, present, tombstone, orphan}, including the copy quirk (a
+// flat node's children are always the initial empty dict, so a copy is the
+// slot's own fields); then the visible document is hashed like k_forest and
+// the oracle. Documents that do not fit are left to k_forest (fb[d] = 1).
+// ---------------------------------------------------------------------------
+constexpr uint32_t FL_MAXOPS = 1023;  // + the sentinel key: 1024 sort slots
+constexpr uint32_t FL_SLOTS = 1024;
+constexpr uint32_t FL_N = 0x7FF;  // 11-bit "none"
+// per-op word: tslot | aslot << 11 | DEL << 22 | INVALID << 23 | OWN << 24
+constexpr uint32_t FO_DEL = 1u << 22, FO_INV = 1u << 23, FO_OWN = 1u << 24;
+// per-slot word: next | src << 11 | PRESENT << 21 | TOMB << 22 | ORPHAN << 23
+constexpr uint32_t FS_PRESENT = 1u << 21, FS_TOMB = 1u << 22, FS_ORPHAN = 1u << 23;
+
+__device__ __forceinline__ uint32_t fl_lower(const long long* k, long long x) {
+  uint32_t lo = 0, hi = FL_SLOTS;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (k[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(64) k_forest_prep(OpsDev o, const uint32_t* doc_off, uint32_t n_docs, long long ts0,
+                                                    uint32_t* opw, uint16_t* sent, uint8_t* fb) {
+  __shared__ long long skey[FL_SLOTS];
+  const uint32_t d = blockIdx.x;
+  if (d >= n_docs) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t ob = doc_off[d], nops = doc_off[d + 1] - ob;
+  if (nops > FL_MAXOPS) {
+    if (lane == 0) fb[d] = 1;
+    return;
+  }
+  constexpr long long INF = 0x7fffffffffffffffLL;
+  const long long own = replica_of(ts0);
+  uint32_t bad = 0;
+  for (uint32_t j = lane; j < FL_SLOTS; j += 64) {
+    long long key = INF;
+    if (j < nops) {
+      const uint32_t i = ob + j;
+      const uint32_t L = o.off[i + 1] - o.off[i];
+      if (L > 1) bad = 1;
+      if (o.kind[i] == CRDTM_ADD && L == 1) key = o.ts[i];
+    } else if (j == nops) {
+      key = 0;  // the root dict's sentinel
+    }
+    skey[j] = key;
+  }
+  if (__any(bad)) {
+    if (lane == 0) fb[d] = 1;
+    return;
+  }
+  __syncthreads();
+  for (uint32_t k = 2; k <= FL_SLOTS; k <<= 1) {
+    for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+      for (uint32_t i = lane; i < FL_SLOTS; i += 64) {
+        const uint32_t ixj = i ^ jj;
+        if (ixj > i) {
+          const long long a = skey[i], b = skey[ixj];
+          if ((a > b) == ((i & k) == 0)) {
+            skey[i] = b;
+            skey[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t j = lane; j < nops; j += 64) {
+    const uint32_t i = ob + j;
+    const uint32_t L = o.off[i + 1] - o.off[i];
+    uint32_t w;
+    if (L == 0) {
+      w = FO_INV | FL_N | (FL_N << 11);
+    } else {
+      const long long k0 = o.path[o.off[i]];
+      const uint32_t p = fl_lower(skey, k0);
+      const uint32_t ps = (p < FL_SLOTS && skey[p] == k0) ? p : FL_N;
+      if (o.kind[i] != CRDTM_ADD) {
+        w = FO_DEL | ps | (FL_N << 11);
+      } else {
+        const long long t = o.ts[i];
+        w = fl_lower(skey, t) | (ps << 11) | (replica_of(t) == own ? FO_OWN : 0u);
+      }
+    }
+    opw[i] = w;
+  }
+  if (lane == 0) sent[d] = static_cast<uint16_t>(fl_lower(skey, 0));
+}
+
+__global__ void __launch_bounds__(64) k_forest_replay(OpsDev o, const uint32_t* doc_off, uint32_t n_docs,
+                                                      long long ts0, const uint32_t* opw, const uint16_t* sent,
+                                                      const uint8_t* fb, int32_t* code_out, uint32_t* err_out,
+                                                      uint32_t* applied_out, unsigned long long* vhash,
+                                                      unsigned long long* vwords, long long* tstamp,
+                                                      uint32_t* overflow) {
+  __shared__ uint32_t sl[FL_SLOTS];
+  const uint32_t d = blockIdx.x;
+  if (d >= n_docs || fb[d]) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t ob = doc_off[d], nops = doc_off[d + 1] - ob;
+  const uint32_t s0 = sent[d];
+  for (uint32_t j = lane; j < FL_SLOTS; j += 64) sl[j] = j == s0 ? (FL_N | FS_PRESENT | FS_TOMB) : FL_N;
+  __syncthreads();
+  if (lane != 0) return;
+  // Fresh documents start at counter 0 of their replica, so no run of at most
+  // FL_MAXOPS own Adds can cross into the next replica id: the OWN bit of
+  // each op (computed against ts0) is the reference's per-op comparison.
+  long long ts = ts0;
+  uint32_t applied = 0, err = NONE;
+  int32_t code = CRDTM_OK;
+  for (uint32_t j = 0; j < nops; ++j) {
+    const uint32_t w = opw[ob + j];
+    if (w & FO_INV) {  // update [] = InvalidPath
+      err = j;
+      code = CRDTM_INVALID_PATH;
+      break;
+    }
+    const uint32_t t = w & FL_N;
+    if (w & FO_DEL) {  // deleteHelp (:112-122)
+      const uint32_t st = t == FL_N ? 0u : sl[t];
+      if (!(st & FS_PRESENT)) {
+        err = j;
+        code = CRDTM_OPERATION_FAILED;
+        break;
+      }
+      if (!(st & FS_TOMB)) {
+        sl[t] = st | FS_TOMB;
+        ++applied;
+      }
+      continue;
+    }
+    const uint32_t x = t;
+    if (sl[x] & FS_PRESENT) {  // `child ts parent` exists: AlreadyApplied
+      if (w & FO_OWN) ++ts;
+      continue;
+    }
+    const uint32_t a = (w >> 11) & FL_N;
+    const uint32_t sa = a == FL_N ? 0u : sl[a];
+    if (!(sa & FS_PRESENT)) {  // anchor missing: NotFound
+      err = j;
+      code = CRDTM_OPERATION_FAILED;
+      break;
+    }
+    uint32_t nk = a, node = a, sn = sa;  // findInsertion (:93-104)
+    for (;;) {
+      const uint32_t rn = sn & FL_N;
+      if (rn == FL_N) break;
+      uint32_t live = rn, sl_live = sl[rn];
+      while (sl_live & FS_TOMB) {
+        live = sl_live & FL_N;
+        if (live == FL_N) break;
+        sl_live = sl[live];
+      }
+      if (live == FL_N || x > rn) break;
+      nk = rn;
+      node = live;
+      sn = sl_live;
+    }
+    const uint32_t snk = nk == node ? sn : sl[nk];
+    sl[x] = (sn & FL_N) | (j << 11) | FS_PRESENT | (snk & FS_ORPHAN);
+    if (nk == node) {
+      sl[node] = (sn & ~FL_N) | x;
+    } else {  // copy quirk: slot nk := copy of node with next = x
+      if (!(snk & FS_ORPHAN)) {
+        for (uint32_t q = snk & FL_N; q != FL_N;) {
+          const uint32_t sq = sl[q];
+          sl[q] = sq | FS_ORPHAN;
+          if (q == node) break;
+          q = sq & FL_N;
+        }
+      }
+      sl[nk] = x | (sn & (0x3FFu << 11)) | FS_PRESENT | (snk & FS_ORPHAN);
+    }
+    ++applied;
+    if (w & FO_OWN) ++ts;  // incrementTimestamp (src/CRDTree.elm:337-343)
+  }
+  code_out[d] = code;
+  err_out[d] = err;
+  applied_out[d] = applied;
+  tstamp[d] = ts;
+  overflow[d] = 0;
+  Fnv h;
+  if (code == CRDTM_OK) {
+    uint32_t cur = s0;
+    for (;;) {
+      uint32_t nx = sl[cur] & FL_N;
+      while (nx != FL_N && (sl[nx] & FS_TOMB)) nx = sl[nx] & FL_N;
+      if (nx == FL_N) break;
+      const uint32_t i = ob + ((sl[nx] >> 11) & 0x3FFu);
+      h.put(0);
+      h.put(static_cast<long long>(o.val[i]));
+      h.put(1);
+      h.put(o.ts[i]);
+      cur = nx;
+    }
+  }
+  vhash[d] = h.h;
+  vwords[d] = h.n;
+}
+
 __global__ void __launch_bounds__(64) k_forest(OpsDev o, ForestArgs f, const uint64_t* sbase, const uint64_t* dbase,
-                                               const uint64_t* hbase) {
+                                               const uint64_t* hbase, const uint8_t* fb) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= f.n_docs) return;
+  if (d >= f.n_docs || !fb[d]) return;  // served by k_forest_prep / k_forest_replay
+  {
+    uint32_t* hs = f.hslot + hbase[d];  // this document's hash region starts empty
+    for (uint32_t p = 0, H = forest_hash_cap(f.doc_off[d + 1] - f.doc_off[d]); p < H; ++p) hs[p] = NONE;
+  }
   const uint32_t ob = f.doc_off[d], oe = f.doc_off[d + 1], nops = oe - ob;
   const uint32_t s0 = static_cast<uint32_t>(sbase[d]), d0 = static_cast<uint32_t>(dbase[d]);
   const uint32_t H = forest_hash_cap(nops);
@@ -2328,8 +2542,14 @@ int forest_apply(crdtm_ctx* c, int64_t replica_id, const OpsDev& o, const uint32
   HIP_CHECK(hipMemcpyAsync(dsb, sb.data(), (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemcpyAsync(ddb, db.data(), (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemcpyAsync(dhb, hb.data(), (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
-  HIP_CHECK(hipMemsetAsync(f.hslot, 0xFF, Hn * sizeof(uint32_t), s));
-  LAUNCH(k_forest, dim3(static_cast<uint32_t>((n_docs + 63) / 64)), dim3(64), 0, s, o, f, dsb, ddb, dhb);
+  uint8_t* fb = ws.alloc<uint8_t>(n_docs);
+  HIP_CHECK(hipMemsetAsync(fb, 0, n_docs, s));
+  uint32_t* opw = ws.alloc<uint32_t>(o.n + 1);
+  uint16_t* sent = ws.alloc<uint16_t>(n_docs);
+  LAUNCH(k_forest_prep, dim3(static_cast<uint32_t>(n_docs)), dim3(64), 0, s, o, doff, f.n_docs, f.ts0, opw, sent, fb);
+  LAUNCH(k_forest_replay, dim3(static_cast<uint32_t>(n_docs)), dim3(64), 0, s, o, doff, f.n_docs, f.ts0, opw, sent, fb,
+         f.code, f.err, f.applied, f.vhash, f.vwords, f.tstamp, f.overflow);
+  LAUNCH(k_forest, dim3(static_cast<uint32_t>((n_docs + 63) / 64)), dim3(64), 0, s, o, f, dsb, ddb, dhb, fb);
   std::vector<uint32_t> e(n_docs), ov(n_docs);
   HIP_CHECK(hipMemcpyAsync(code, f.code, n_docs * 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipMemcpyAsync(e.data(), f.err, n_docs * 4, hipMemcpyDeviceToHost, s));

@@ -82,7 +82,10 @@ typedef struct crdtm_tree crdtm_tree; /* one replica's CRDTree state, resident i
 /* ---- context ---- */
 int crdtm_version(void);
 int crdtm_device_count(int *count);
-/* stream: an existing hipStream_t (as void*) to launch on, or NULL for an engine-owned stream. */
+/* stream: an existing hipStream_t (as void*) to launch on, or NULL for an engine-owned stream.
+ * Device inputs produced on another stream must be complete before crdtm_apply /
+ * crdtm_forest_apply is called (synchronise, or create the context on that stream;
+ * note that the legacy default stream's handle is NULL, i.e. "engine-owned"). */
 int crdtm_ctx_create(int device, void *stream, crdtm_ctx **out);
 int crdtm_ctx_destroy(crdtm_ctx *ctx);
 void *crdtm_ctx_stream(crdtm_ctx *ctx);
@@ -120,7 +123,8 @@ int crdtm_tree_ops(const crdtm_tree *t, int which, crdtm_ops *out, int *is_batch
 
 /* Canonical dumps shared with the oracle: which 0 = every dict entry (structure),
  * 1 = visible document order. Writes up to cap words (out may be NULL), the
- * word count and a 64-bit FNV-1a hash of the words. Host-side read API. */
+ * word count and a 64-bit word-wise FNV-1a hash of the words (h ^= w; h *= 0x100000001b3
+ * per 64-bit word, from 0xcbf29ce484222325). Host-side read API. */
 int crdtm_tree_canonical(const crdtm_tree *t, int which, int64_t *out, uint64_t cap, uint64_t *n_words,
                          uint64_t *hash);
 
@@ -134,7 +138,7 @@ int crdtm_tree_document(const crdtm_tree *t, uint32_t *vals, uint64_t cap, uint6
  * Every document starts as `init replica_id` and takes `apply (Batch ops_d)`
  * with the exact sequential semantics. Per-document host outputs (any may be
  * NULL except doc_code): CRDTree.Error code, local err index (-1), applied
- * count, FNV-1a hash + word count of the visible-document canonical dump
+ * count, word-wise FNV-1a hash + word count of the visible-document canonical dump
  * (same words as crdtm_tree_canonical(which = 1)), final timestamp.
  * Replaces: CRDTree.apply (src/CRDTree.elm:265-269) over many trees. */
 int crdtm_forest_apply(crdtm_ctx *ctx, int64_t replica_id, const crdtm_ops *ops, const uint32_t *doc_off,

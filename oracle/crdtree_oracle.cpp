@@ -300,8 +300,8 @@ struct Sink {
   uint64_t n = 0;
   void put(int64_t w) {
     if (out) out->push_back(w);
-    uint64_t u = static_cast<uint64_t>(w);
-    for (int i = 0; i < 8; ++i) { h ^= (u >> (8 * i)) & 0xff; h *= FNV_PRIME; }
+    h ^= static_cast<uint64_t>(w);  // word-wise FNV-1a over 64-bit words
+    h *= FNV_PRIME;
     ++n;
   }
 };

@@ -29,13 +29,16 @@ def _worker(rank, world, port, n_docs, per_doc, q):
     doc_off = np.arange(n_docs + 1, dtype=np.uint32) * per_doc
     local = torch.from_numpy(shard.local_log(s, doc_off, rank, world, replicas=8))
     allrec = shard.all_gather_records(local)
-    ops, my_off, n_kept = shard.assemble(allrec, rank, world, n_docs, per_doc)
+    ops, my_off, keep = shard.assemble(allrec, rank, world, n_docs, per_doc)
+    n_kept = int(keep.sum())
     # expected: the owned documents' streams, sliced directly from the generator output
     mine = [t for t in range(n_docs) if t % world == rank]
     idx = np.concatenate([np.arange(t * per_doc, (t + 1) * per_doc) for t in mine])
-    ok = (np.array_equal(ops["kind"].numpy(), s["kind"][idx]) and np.array_equal(ops["ts"].numpy(), s["ts"][idx])
-          and np.array_equal(ops["path"].numpy(), s["path"][idx])
-          and np.array_equal(ops["val"].numpy().astype(np.uint32), s["val"][idx]) and n_kept == len(idx))
+    m = len(idx)  # arrays carry one spill slot at the end
+    ok = (np.array_equal(ops["kind"].numpy()[:m], s["kind"][idx]) and np.array_equal(ops["ts"].numpy()[:m], s["ts"][idx])
+          and np.array_equal(ops["path"].numpy()[:m], s["path"][idx])
+          and np.array_equal(ops["val"].numpy()[:m].astype(np.uint32), s["val"][idx]) and n_kept == m
+          and int(my_off[-1]) == m)
     q.put((rank, bool(ok), int(local.shape[0]), int(allrec.shape[0])))
     dist.barrier()
     dist.destroy_process_group()
