@@ -35,8 +35,14 @@ WORKLOADS = {
     # depth <= 12, <= 8 children, 6.67M adds then deletes of half the nodes
     "deep10m": dict(n_ops=10_000_000, replicas=16, p_delete=1 / 3, max_depth=12, max_children=8, deletes_last=1,
                     seed=0xC0FFEE04),
+    # one tree, 1M ops (80/20 interleaved), 16 replicas, branches, depth <= 4
+    # (Deletes interleaved before later inserts: the exact sequential replay)
+    "cfg2": dict(n_ops=1_000_000, replicas=16, window=64, p_delete=0.2, p_branch=0.1, max_depth=4,
+                 seed=0xC0FFEE02),
+    # SURVEY.md §8d config 1 shape: 2 replicas, 10k ops, 70/30 interleaved, depth <= 3
+    "cfg1": dict(n_ops=10_000, replicas=2, window=8, p_delete=0.3, p_branch=0.05, max_depth=3, seed=0xC0FFEE01),
 }
-CPU_SAMPLE = {"flat10m": 150_000, "deep10m": 2_000_000, "trees": 2_000_000}
+CPU_SAMPLE = {"flat10m": 150_000, "deep10m": 2_000_000, "trees": 2_000_000, "cfg2": 100_000, "cfg1": 10_000}
 # 100k documents x 1k ops (80/20), 8 replicas, sharded by
 # document id; 12.5k documents per GPU (100k at 8 GPUs), weak scaling.
 TREES = dict(per_doc=1000, docs_per_gpu=12_500, replicas=8, window=16, p_delete=0.2, seed=0xC0FFEE05)
