@@ -213,7 +213,7 @@ def main():
         "data": "synthetic (deterministic generator, SURVEY.md §8d)",
         "config": {"workload": f"{args.workload}: {n} ops per GPU, one document per GPU",
                    "replicas": spec.get("replicas"), "window": spec.get("window", 0),
-                   "path": {1: "closed-form", 2: "replay"}.get(path_taken, "?"),
+                   "path": {1: "closed-form", 2: "replay", 3: "per-dict replay"}.get(path_taken, "?"),
                    "parallelism": f"documents sharded by id over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libcrdtm.so")
 CRDTM_OK = 0
 PATH_CLOSED_FORM = 1
 PATH_REPLAY = 2
+PATH_DICT_REPLAY = 3
 CODES = {0: "Ok", 1: "InvalidPath", 2: "NotFound", 3: "OperationFailed", -1: "E_ARG", -2: "E_HIP", -3: "E_NOMEM",
          -4: "E_RANGE", -5: "E_NODEVICE", -6: "E_PARSE"}
 

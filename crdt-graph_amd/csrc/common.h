@@ -15,6 +15,9 @@ namespace crdtm {
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;     // absent index / list end
 constexpr uint32_t ABSENT = 0xFFFFFFFEu;   // entry not part of a list
+constexpr uint32_t PDR_REACHED = 0xFFFFFFFDu;  // K1 tag: the op's path resolved to its leaf dict
+constexpr uint32_t SENT_T = 0xFFFFFFFDu;       // K1 leaf target: the dict's sentinel (key 0)
+constexpr uint32_t MISS_T = 0xFFFFFFFCu;       // K1 leaf target: key not in the dict
 constexpr int64_t TWO53 = 9007199254740992LL;
 constexpr int64_t TWO32 = 4294967296LL;
 constexpr int REPLICA_BITS = 22;           // replica ids in (-2^21, 2^21) when |ts| < 2^53
@@ -71,6 +74,11 @@ struct DevResult {
   uint32_t max_replica;     // largest replica id of an Add timestamp
   uint32_t scan_err;        // a look-back scan gave up (never on a live device)
   uint32_t dup_fix;         // flat status: a duplicate timestamp took its slot, decide again
+  uint32_t pdr_conflict;    // per-dict replay: a path crossed a key the copy quirk refilled
+  uint32_t pdr_jobs;        // per-dict replay: snapshot dicts created so far
+  uint32_t pdr_overflow;    // per-dict replay: snapshot room exhausted
+  uint32_t pdr_dicts;       // per-dict replay: dicts of the new state
+  uint32_t pdr_slots;       // per-dict replay: slots of the new state
 };
 
 #define HIP_CHECK(x)                                                                         \

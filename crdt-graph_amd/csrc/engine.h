@@ -136,6 +136,9 @@ int segmented_sort(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, ui
 // `skip` is left alone (the caller orders it)
 int segmented_sort_desc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items, Arena& ws,
                            hipStream_t st, DevResult* dres, uint32_t skip);
+// same, ascending op index (per-dict op lists of pdr.hip)
+int segmented_sort_asc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items, Arena& ws,
+                          hipStream_t st, DevResult* dres);
 // ent[e] = {succ, wbits}: see primitives.hip / listrank.h (list_rank_fused)
 int list_rank(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws, hipStream_t st);
 int list_rank_packed(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws,
@@ -154,6 +157,21 @@ struct OpsDev {
   const uint32_t* val = nullptr;
 };
 
+// K1 results handed to the per-dict replay (pdr.hip)
+struct PdrIn {
+  TsIndex ix;
+  const uint32_t* tag;     // PDR_REACHED, the tombstoned node the path stopped at, or NONE
+  const uint32_t* cur;     // leaf dict owner (n = root)
+  const uint32_t* leaf;    // leaf target: node, SENT_T or MISS_T
+  const uint32_t* addpar;  // Adds: dict owner
+  uint32_t maxlen;
+};
+
+// merge.hip
+int sync_read(crdtm_ctx* c);
+int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& ws);
+// pdr.hip
+int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdtm_result* res, bool* handled);
 // merge.hip
 int grow_tree(crdtm_tree* t, const TreeCaps& need);
 int apply_batch(crdtm_tree* t, const OpsDev& ops, uint8_t* status_dev, crdtm_result* res);

@@ -171,4 +171,39 @@ __device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long lon
   return v;
 }
 
+// block-level OR/MAX reduction helpers (one atomic per block)
+__device__ __forceinline__ uint32_t block_max(uint32_t v) {
+  __shared__ uint32_t s[BLOCK / 64];
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t r = 0;
+  for (int w = 0; w < BLOCK / 64; ++w) r = max(r, s[w]);
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ uint32_t block_sum(uint32_t v) {
+  __shared__ uint32_t s[BLOCK / 64];
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t r = 0;
+  for (int w = 0; w < BLOCK / 64; ++w) r += s[w];
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ uint32_t block_min(uint32_t v) {
+  __shared__ uint32_t s[BLOCK / 64];
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t r = NONE;
+  for (int w = 0; w < BLOCK / 64; ++w) r = min(r, s[w]);
+  __syncthreads();
+  return r;
+}
+
+#define GRID_STRIDE(i, n) \
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += gridDim.x * blockDim.x)
+
 }  // namespace crdtm

@@ -20,8 +20,6 @@
 
 namespace crdtm {
 
-constexpr uint32_t SENT_T = 0xFFFFFFFDu;  // leaf target: the dict's sentinel (key 0)
-constexpr uint32_t MISS_T = 0xFFFFFFFCu;  // leaf target: key not in the dict
 
 struct Work {  // per-call device arrays of the closed form (sized by n ops)
   uint8_t* st;
@@ -32,6 +30,7 @@ struct Work {  // per-call device arrays of the closed form (sized by n ops)
   uint32_t* dtime;
   uint8_t* dead;
   uint32_t* maxadd;
+  uint32_t* tag;  // per op: PDR_REACHED, or the tombstoned node its path stopped at, or NONE (pdr.hip)
 };
 
 __device__ __forceinline__ uint32_t op_len(const OpsDev& o, uint32_t i) { return o.off[i + 1] - o.off[i]; }
@@ -113,40 +112,6 @@ inline uint32_t quad_grid(uint64_t n) {
   return g < 8 ? static_cast<uint32_t>(g ? g : 1) : static_cast<uint32_t>((g + 7) & ~7ULL);
 }
 
-// block-level OR/MAX reduction helpers (one atomic per block)
-__device__ __forceinline__ uint32_t block_max(uint32_t v) {
-  __shared__ uint32_t s[BLOCK / 64];
-  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
-  __syncthreads();
-  uint32_t r = 0;
-  for (int w = 0; w < BLOCK / 64; ++w) r = max(r, s[w]);
-  __syncthreads();
-  return r;
-}
-__device__ __forceinline__ uint32_t block_sum(uint32_t v) {
-  __shared__ uint32_t s[BLOCK / 64];
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
-  __syncthreads();
-  uint32_t r = 0;
-  for (int w = 0; w < BLOCK / 64; ++w) r += s[w];
-  __syncthreads();
-  return r;
-}
-__device__ __forceinline__ uint32_t block_min(uint32_t v) {
-  __shared__ uint32_t s[BLOCK / 64];
-  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
-  __syncthreads();
-  uint32_t r = NONE;
-  for (int w = 0; w < BLOCK / 64; ++w) r = min(r, s[w]);
-  __syncthreads();
-  return r;
-}
-
-#define GRID_STRIDE(i, n) \
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += gridDim.x * blockDim.x)
 
 // ---------------------------------------------------------------------------
 // K1 — per-op status under sequential semantics (src/Internal/Node.elm:138-163,
@@ -238,6 +203,7 @@ __global__ void __launch_bounds__(BLOCK) k_work_init(OpsDev o, Work w) {
     w.cur[i] = o.n;
     w.addpar[i] = NONE;
     w.dtime[i] = NONE;
+    w.tag[i] = NONE;
   }
 }
 
@@ -423,9 +389,14 @@ __global__ void __launch_bounds__(BLOCK) k_lvl_fin(OpsDev o, Work w, TsIndex h, 
     const uint32_t L = op_len(o, i);
     if (L > lvl) {
       const uint32_t x = w.nxt[i];
-      if (w.dtime[x] < i) w.st[i] = ST_ALREADY;  // descending into a Tombstone
-      else w.cur[i] = x;
+      if (w.dtime[x] < i) {
+        w.st[i] = ST_ALREADY;  // descending into a Tombstone
+        w.tag[i] = x;
+      } else {
+        w.cur[i] = x;
+      }
     } else if (L == lvl) {
+      w.tag[i] = PDR_REACHED;
       if (o.kind[i] == CRDTM_DELETE) {
         w.st[i] = (w.dtime[w.leaf[i]] == i) ? ST_APPLIED : ST_ALREADY;
       } else {
@@ -1961,7 +1932,7 @@ static uint32_t pow2_at_least(uint64_t x) {
   return static_cast<uint32_t>(p);
 }
 
-static int sync_read(crdtm_ctx* c) {
+int sync_read(crdtm_ctx* c) {
   HIP_CHECK(hipMemcpyAsync(c->hres, c->dres, sizeof(DevResult), hipMemcpyDeviceToHost, c->stream));
   HIP_CHECK(hipStreamSynchronize(c->stream));
   return CRDTM_OK;
@@ -1976,7 +1947,7 @@ __global__ void __launch_bounds__(BLOCK) k_post_flags(OpsDev o, const uint8_t* s
 }
 
 // Append the applied ops to the log and fold replicas; shared by both paths.
-static int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& ws) {
+int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& ws) {
   crdtm_ctx* c = t->ctx;
   hipStream_t s = c->stream;
   const uint32_t n = o.n;
@@ -2307,6 +2278,7 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   w.dtime = ws.alloc<uint32_t>(n);
   w.dead = ws.alloc<uint8_t>(n);
   w.maxadd = ws.alloc<uint32_t>(n + 1);
+  w.tag = ws.alloc<uint32_t>(n);
   uint32_t* anc = ws.alloc<uint32_t>(n);
   LAUNCH(k_work_init, dim3(g), dim3(BLOCK), 0, s, o, w);
   if (flat) {
@@ -2335,6 +2307,25 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   const long long new_ts = t->timestamp + h1.own_ok_adds;
   if (replica_of(new_ts) != id0) guard |= G_REPLICA_DRIFT;
   res->guard = guard;
+  if (guard == G_DEL_BEFORE_ADD) {
+    // one lane per children dict (pdr.hip); conflicts fall through to the replay
+    PdrIn pin;
+    pin.ix = ix;
+    pin.tag = w.tag;
+    pin.cur = w.cur;
+    pin.leaf = w.leaf;
+    pin.addpar = w.addpar;
+    pin.maxlen = maxlen;
+    bool handled = false;
+    if ((r = pdr_apply(t, o, pin, w.st, res, &handled))) return r;
+    if (handled) {
+      res->guard = guard;
+      if (st_out)
+        LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n,
+               res->err_index >= 0 ? static_cast<uint32_t>(res->err_index) : NONE, st_out);
+      return CRDTM_OK;
+    }
+  }
   if (guard) {
     // exact sequential replay decides statuses (and errors) itself
     r = run_replay(t, o, w.st, res, guard);

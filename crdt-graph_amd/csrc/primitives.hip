@@ -32,6 +32,9 @@ struct ArrKey {
   const long long* k;
   __device__ __forceinline__ long long operator()(uint32_t v) const { return k[v]; }
 };
+struct IdKey {
+  __device__ __forceinline__ long long operator()(uint32_t v) const { return static_cast<long long>(v); }
+};
 struct NegIdKey {
   __device__ __forceinline__ long long operator()(uint32_t v) const { return -static_cast<long long>(v); }
 };
@@ -377,6 +380,11 @@ int segmented_sort(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, ui
 int segmented_sort_desc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items, Arena& ws,
                            hipStream_t st, DevResult* dres, uint32_t skip) {
   return segmented_sort_t(seg_start, n_seg, carr, n_items, NegIdKey{}, ws, st, dres, skip);
+}
+
+int segmented_sort_asc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items, Arena& ws,
+                          hipStream_t st, DevResult* dres) {
+  return segmented_sort_t(seg_start, n_seg, carr, n_items, IdKey{}, ws, st, dres, NONE);
 }
 
 // ---------------------------------------------------------------------------

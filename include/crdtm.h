@@ -51,6 +51,7 @@ extern "C" {
 /* ---- which merge path served a call */
 #define CRDTM_PATH_CLOSED_FORM 1 /* parallel closed form, guard held */
 #define CRDTM_PATH_REPLAY 2      /* exact sequential replay on the GPU */
+#define CRDTM_PATH_DICT_REPLAY 3 /* exact replay, one lane per children dict */
 
 /* Packed op batch, structure of arrays (host or device memory; see crdtm_apply). */
 typedef struct crdtm_ops {

@@ -86,6 +86,31 @@ def test_synthetic_streams(name):
         assert res.path_taken == N.PATH_CLOSED_FORM, f"expected the closed form, guard={res.guard}"
 
 
+@pytest.mark.parametrize("chunk", range(8))
+def test_adversarial_streams(chunk):
+    """Interleaved Deletes and tombstone walks (copy quirks, nested dicts):
+    the per-dict replay, its conflict fallback and the sequential replay all
+    match the oracle."""
+    from adversarial import adversarial
+    paths = {}
+    for seed in range(16 * chunk, 16 * chunk + 16):
+        n = [40, 120, 400, 1500][seed % 4]
+        ops = adversarial(seed, n, replicas=2 + seed % 3, max_depth=1 + seed % 4)
+        arrs = pack(ops)
+        ot, rc, oerr = oracle_apply_arrays(arrs, n)
+        et = CRDTree.init(0)
+        res = et.apply_arrays(arrs, n)
+        paths[res.path_taken] = paths.get(res.path_taken, 0) + 1
+        assert res.code == rc, (seed, res.code, rc)
+        if rc != 0:
+            assert res.err_index == oerr, seed
+            continue
+        assert engine_summary(et) == oracle_summary(ot), seed
+        assert engine_log(et, 0) == oracle_log(ot, 0), seed
+        assert np.array_equal(et.document_handles(), oracle_visible_vals(ot)), seed
+    assert paths.get(N.PATH_DICT_REPLAY, 0) > 0, paths
+
+
 def test_incremental_batches():
     """Successive applies of chunks equal one apply of the whole stream's chunks on the oracle."""
     s, n = synth_case(n_ops=20000, replicas=8, window=16, p_delete=0.2, p_branch=0.1, max_depth=3, seed=5)
