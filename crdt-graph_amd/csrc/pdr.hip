@@ -12,184 +12,108 @@
 //  1. K1 (merge.hip, level-synchronous lookup) resolves every path as if no
 //     slot were ever re-filled, and tags each op with "reached its leaf dict"
 //     or the tombstoned node where the path stopped (Work.tag);
-//  2. one lane per children dict replays that dict's reached ops in batch
+//  2. one wave per children dict replays that dict's reached ops in batch
 //     order with the reference's literal addAfter/findInsertion/delete
-//     semantics (P2), recording when each key's slot was first re-filled;
+//     semantics, on a slot state held in LDS (P2);
 //  3. an op whose path stopped at a key re-filled before it ran would have
 //     descended into the copy: conflict, and the batch goes to the sequential
 //     replay (P3). Otherwise every status is exact;
 //  4. assembly (P5): the surviving dicts are the original dicts whose owner
 //     chain is live and un-copied, plus one snapshot per copied slot — the
-//     deep copy (Replayer::deep_copy) of the source dict as of the copy time,
-//     rebuilt by replaying the source dict's op prefix (nested level by
-//     level). Slots are numbered by scans and written into TreeDev.
+//     deep copy (Replayer::deep_copy, merge.hip) of the source dict as of the
+//     copy time, rebuilt by replaying the source dict's op prefix (nested
+//     level by level). Slots are numbered by scans and written into TreeDev.
 //
-// Region layout: original dict D (D = owner op index, n = root) owns the
-// slot range [rbase[D], rbase[D+1]) = 1 sentinel + one slot per reached op;
-// olist holds the dict's ops in batch order at [rbase[D], rbase[D+1]-1), its
-// last position a NONE pad (the sort needs unique keys). Snapshot regions
-// follow the originals.
+// Slot numbering inside a dict: the dict's keys are the timestamps of the
+// Adds that reach it first (no collision: one dict per timestamp), so slot r
+// = rank of the key among them (sentinel = 0) and findInsertion's key test
+// `ts > key(rn)` becomes `r > rn`. A slot is one 32-bit word: next slot (24
+// bits) | flags (8 bits). What a copy carries (source node, children view)
+// lives in side arrays written only when the quirk fires.
+//
+// Regions: original dict D (D = owner op index, n = root) owns positions
+// [rbase[D], rbase[D+1]): olist holds the dict's ops in batch order there (a
+// NONE pad last, the sort needs unique keys); rop[rbase[D] + r] is the Add
+// that created slot r; the slot words of rank r live at base[I] + r for each
+// instance I of D (the original, then its snapshots).
 
 #include "engine.h"
 
 namespace crdtm {
 
-enum : uint8_t { P_TOMB = 1, P_ORPHAN = 2, P_COPY = 4 };
-
-struct PdrRegion {     // per replay slot (originals, then snapshots)
-  long long* key;
-  uint32_t* next;      // local index in the same region
-  uint32_t* src;       // op whose node the slot holds (NONE: sentinel)
-  uint32_t* cd;        // children: original dict (owner op) ...
-  uint32_t* cb;        // ... as of op index cb (NONE: current)
-  uint32_t* ch;        // assembly: snapshot instance of the children
-  uint32_t* inst;      // instance owning the slot (NONE: unused room)
-  uint8_t* fl;
-};
+constexpr uint32_t PM = 0xFFFFFFu;  // slot index mask; PM = end of chain
+enum : uint32_t { SF_TOMB = 1u << 24, SF_ORPHAN = 2u << 24, SF_COPY = 4u << 24, SF_MADE = 8u << 24 };
+constexpr uint32_t OW_NF = PM;           // op word code: the target/anchor is missing (NotFound)
+constexpr uint32_t PDR_SMALL = 4096;     // slots per dict held in static LDS
 
 struct PdrInst {       // per instance: originals 0..n (n = root), snapshots n+1+j
-  uint32_t* base;
-  uint32_t* used;
+  uint32_t* base;      // first slot position
   uint32_t* src;       // snapshots: source original dict
   uint32_t* bound;     // snapshots: replay the ops < bound
   uint32_t* pi;        // snapshots: parent instance
-  uint32_t* pl;        // snapshots: parent local slot
+  uint32_t* pl;        // snapshots: parent slot (rank)
 };
 
 struct PdrCtx {
   OpsDev o;
   TsIndex ix;
   const uint32_t* leaf;
-  const uint32_t* rbase;  // [n + 2]
-  const uint32_t* olist;
-  uint32_t* lidx;         // op -> local slot in its original dict
-  uint32_t* tcopy;        // node op -> first op whose copy quirk re-filled its key's slot
-  PdrRegion R;
+  const uint32_t* rbase;   // [n + 2]
+  const uint32_t* cbase;   // [n + 2] key counts, scanned: K_D = cbase[D+1] - cbase[D]
+  const uint32_t* olist;   // per region position: op index (batch order)
+  const unsigned long long* opw;  // per region position: op word
+  uint32_t* rankof;        // per op: slot (rank) of the Add's key in its dict, 0 = not a key
+  uint32_t* rop;           // per region position: Add op of rank r
+  uint32_t* tcopy;         // node op -> first op whose copy quirk re-filled its key's slot
+  uint32_t* S;             // per slot position: next | flags
+  uint32_t* qsrc;          // per slot position, COPY slots: node carried
+  uint32_t* qcd;           // ... its children: original dict
+  uint32_t* qcb;           // ... as of op index (NONE: current)
+  uint32_t* ch;            // assembly: snapshot instance of a slot's children
+  uint32_t* inst;          // per slot position: instance (NONE: unused room)
   PdrInst I;
 };
+
+__device__ __forceinline__ uint32_t pdr_kcount(const PdrCtx& p, uint32_t D) { return p.cbase[D + 1] - p.cbase[D]; }
 
 __device__ __forceinline__ uint32_t pdr_first_op(const PdrCtx& p, uint32_t D) {
   const uint32_t b = p.rbase[D];
   return p.rbase[D + 1] - b > 1 ? p.olist[b] : NONE;
 }
 
-// Replay original dict D's ops (ORIG, statuses written) or the op prefix
-// < bound of a snapshot, into the region at `base`. Literal semantics of
-// Replayer::op's leaf step (merge.hip) on the region.
-template <bool ORIG>
-__device__ void pdr_replay(const PdrCtx& p, uint8_t* st, uint32_t D, uint32_t bound, uint32_t base, uint32_t inst) {
-  const OpsDev& o = p.o;
-  const PdrRegion& R = p.R;
-  R.key[base] = 0;
-  R.next[base] = NONE;
-  R.src[base] = NONE;
-  R.cd[base] = NONE;
-  R.cb[base] = NONE;
-  R.ch[base] = NONE;
-  R.inst[base] = inst;
-  R.fl[base] = P_TOMB;
-  uint32_t m = 1;
-  const uint32_t ob = p.rbase[D], oe = p.rbase[D + 1] - 1;
-  for (uint32_t k = ob; k < oe; ++k) {
-    const uint32_t i = p.olist[k];
-    if (i >= bound) break;
-    uint8_t s;
-    if (o.kind[i] == CRDTM_DELETE) {  // deleteHelp
-      const uint32_t tg = p.leaf[i];
-      if (tg == SENT_T) {
-        s = ST_ALREADY;
-      } else {
-        const uint32_t l = (tg == MISS_T || tg >= i) ? NONE : p.lidx[tg];
-        if (l == NONE) {
-          s = ST_NOTFOUND;
-        } else if (R.fl[base + l] & P_TOMB) {
-          s = ST_ALREADY;
-        } else {
-          R.fl[base + l] |= P_TOMB;
-          R.cd[base + l] = NONE;  // Tombstone drops the children
-          s = ST_APPLIED;
-        }
-      }
-    } else {  // addAfterHelp: no collision, so the dict holds ts iff an earlier Add of ts reached it
-      const long long ts = o.ts[i];
-      if (ts == 0 || tsindex_find(p.ix, ts) != i) {
-        s = ST_ALREADY;
-      } else {
-        const uint32_t a = p.leaf[i];
-        const uint32_t al = a == SENT_T ? 0u : ((a == MISS_T || a >= i) ? NONE : p.lidx[a]);
-        if (al == NONE) {
-          s = ST_NOTFOUND;
-        } else {
-          uint32_t node = al, nk = al;  // findInsertion
-          for (;;) {
-            const uint32_t rn = R.next[base + node];
-            if (rn == NONE) break;
-            uint32_t live = rn;
-            while (live != NONE && (R.fl[base + live] & P_TOMB)) live = R.next[base + live];
-            if (live == NONE) break;
-            if (ts > R.key[base + rn]) break;
-            nk = rn;
-            node = live;
-          }
-          const uint32_t x = m++;
-          const uint32_t gx = base + x;
-          R.key[gx] = ts;
-          R.next[gx] = R.next[base + node];
-          R.src[gx] = i;
-          R.cd[gx] = i;
-          R.cb[gx] = ORIG ? NONE : bound;
-          R.ch[gx] = NONE;
-          R.inst[gx] = inst;
-          R.fl[gx] = R.fl[base + nk] & P_ORPHAN;
-          if (nk == node) {
-            R.next[base + node] = x;
-          } else {
-            // copy quirk: slot nk := copy of node, next = x; the entries after
-            // nk up to node drop off the chain when nk was on it
-            if (!(R.fl[base + nk] & P_ORPHAN)) {
-              for (uint32_t q = R.next[base + nk]; q != NONE; q = R.next[base + q]) {
-                R.fl[base + q] |= P_ORPHAN;
-                if (q == node) break;
-              }
-            }
-            R.src[base + nk] = R.src[base + node];
-            R.fl[base + nk] = (R.fl[base + node] & ~P_ORPHAN) | (R.fl[base + nk] & P_ORPHAN) | P_COPY;
-            R.cd[base + nk] = R.cd[base + node];
-            R.cb[base + nk] = min(R.cb[base + node], i);
-            R.next[base + nk] = x;
-            if (ORIG) atomicMin(&p.tcopy[tsindex_find(p.ix, R.key[base + nk])], i);
-          }
-          if (ORIG) p.lidx[i] = x;
-          s = ST_APPLIED;
-        }
-      }
-    }
-    if (ORIG) st[i] = s;
-  }
-  p.I.used[inst] = m;
-}
-
 // ---- P1: group the reached ops by leaf dict ----
-__global__ void __launch_bounds__(BLOCK) k_pdr_init(uint32_t n, uint32_t* cnt, uint32_t* fill, uint32_t* lidx,
-                                                    uint32_t* tcopy) {
+__global__ void __launch_bounds__(BLOCK) k_pdr_init(uint32_t n, uint32_t* cnt, uint32_t* fill, uint32_t* ccnt,
+                                                    uint32_t* cfill, uint32_t* rankof, uint32_t* tcopy) {
   GRID_STRIDE(i, n + 2) {
     cnt[i] = 0;
     fill[i] = 0;
+    ccnt[i] = 0;
+    cfill[i] = 0;
     if (i < n) {
-      lidx[i] = NONE;
+      rankof[i] = 0;
       tcopy[i] = NONE;
     }
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_pdr_count(OpsDev o, const uint32_t* tag, const uint32_t* cur,
-                                                     uint32_t* cnt) {
+__device__ __forceinline__ bool pdr_is_key(const OpsDev& o, const TsIndex& ix, uint32_t i) {
+  if (o.kind[i] != CRDTM_ADD) return false;
+  const long long ts = o.ts[i];
+  return ts != 0 && tsindex_find(ix, ts) == i;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_pdr_count(OpsDev o, TsIndex ix, const uint32_t* tag, const uint32_t* cur,
+                                                     uint32_t* cnt, uint32_t* ccnt) {
   GRID_STRIDE(i, o.n) {
-    if (tag[i] == PDR_REACHED) atomicAdd(&cnt[cur[i]], 1u);
+    if (tag[i] != PDR_REACHED) continue;
+    const uint32_t d = cur[i];
+    atomicAdd(&cnt[d], 1u);
+    if (pdr_is_key(o, ix, i)) atomicAdd(&ccnt[d], 1u);
   }
 }
 
-// region size: sentinel + one slot per reached op; the root dict always exists
+// region size: one position per reached op + 1 (sentinel slot / list pad);
+// the root dict always exists
 __global__ void __launch_bounds__(BLOCK) k_pdr_size(uint32_t n, uint32_t* cnt) {
   GRID_STRIDE(d, n + 1) {
     const uint32_t c = cnt[d];
@@ -197,24 +121,200 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_size(uint32_t n, uint32_t* cnt) {
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_pdr_scatter(OpsDev o, const uint32_t* tag, const uint32_t* cur,
-                                                       const uint32_t* rbase, uint32_t* fill, uint32_t* olist) {
+__global__ void __launch_bounds__(BLOCK) k_pdr_scatter(OpsDev o, TsIndex ix, const uint32_t* tag, const uint32_t* cur,
+                                                       const uint32_t* rbase, uint32_t* fill, uint32_t* olist,
+                                                       const uint32_t* cbase, uint32_t* cfill, uint32_t* carr) {
   GRID_STRIDE(i, o.n) {
     if (tag[i] != PDR_REACHED) continue;
     const uint32_t d = cur[i];
     olist[rbase[d] + atomicAdd(&fill[d], 1u)] = i;  // the pad (NONE) stays last
+    if (pdr_is_key(o, ix, i)) carr[cbase[d] + atomicAdd(&cfill[d], 1u)] = i;
   }
 }
 
-// ---- P2: one lane per original dict ----
-__global__ void __launch_bounds__(64) k_pdr_replay_orig(PdrCtx p, uint8_t* st) {
+// keys sorted by ts within each dict -> ranks
+__global__ void __launch_bounds__(BLOCK) k_pdr_rank(uint32_t kt, const uint32_t* carr, const uint32_t* cur,
+                                                    const uint32_t* cbase, const uint32_t* rbase, uint32_t* rankof,
+                                                    uint32_t* rop) {
+  GRID_STRIDE(k, kt) {
+    const uint32_t i = carr[k];
+    const uint32_t d = cur[i];
+    const uint32_t r = k - cbase[d] + 1;
+    rankof[i] = r;
+    rop[rbase[d] + r] = i;
+  }
+}
+
+// op word: bit 63 = Delete; Add: anchor code << 24 | own rank (0 = key
+// already present -> AlreadyApplied); Delete: target code (0 = the sentinel
+// -> AlreadyApplied). Codes: 0 sentinel, OW_NF missing, else a rank.
+__global__ void __launch_bounds__(BLOCK) k_pdr_opw(uint32_t R0, const uint32_t* olist, OpsDev o,
+                                                   const uint32_t* leaf, const uint32_t* rankof,
+                                                   unsigned long long* opw) {
+  GRID_STRIDE(k, R0) {
+    const uint32_t i = olist[k];
+    if (i == NONE) continue;
+    const uint32_t a = leaf[i];
+    uint32_t code;
+    if (a == SENT_T) code = 0;
+    else if (a == MISS_T || a >= i) code = OW_NF;
+    else code = rankof[a];  // a node of the same dict that came first: a key
+    unsigned long long w;
+    if (o.kind[i] == CRDTM_DELETE) w = (1ULL << 63) | code;
+    else w = (static_cast<unsigned long long>(code) << 24) | rankof[i];
+    opw[k] = w;
+  }
+}
+
+// ---- P2: the serial replay of one dict (instance) on one wave ----
+// All lanes run the loop with identical values (wave-uniform control flow,
+// broadcast LDS reads); S points to LDS (or to the region for huge dicts).
+template <bool ORIG>
+__device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t D = ORIG ? I : p.I.src[I];
+  const uint32_t bound = ORIG ? NONE : p.I.bound[I];
+  const uint32_t base = p.I.base[I];
+  const uint32_t K = pdr_kcount(p, D);
+  const uint32_t rb = p.rbase[D];
+  for (uint32_t r = lane; r <= K; r += 64) S[r] = r == 0 ? (PM | SF_TOMB | SF_MADE) : PM;
+  __syncthreads();
+  const uint32_t ob = rb, oe = p.rbase[D + 1] - 1;
+  bool done = false;
+  for (uint32_t k0 = ob; k0 < oe && !done; k0 += 64) {
+    const uint32_t kk = k0 + lane;
+    const uint32_t my_i = kk < oe ? p.olist[kk] : NONE;
+    const unsigned long long my_w = kk < oe ? p.opw[kk] : 0ULL;
+    const uint32_t cnt = min(64u, oe - k0);
+    for (uint32_t j = 0; j < cnt; ++j) {
+      const uint32_t i = __builtin_amdgcn_readlane(my_i, j);
+      const uint32_t wlo = __builtin_amdgcn_readlane(static_cast<uint32_t>(my_w), j);
+      const uint32_t whi = __builtin_amdgcn_readlane(static_cast<uint32_t>(my_w >> 32), j);
+      if (i >= bound) {
+        done = true;
+        break;
+      }
+      uint8_t s;
+      if (whi >> 31) {  // deleteHelp
+        const uint32_t t = wlo & PM;
+        if (t == 0) {
+          s = ST_ALREADY;
+        } else if (t == OW_NF || !(S[t] & SF_MADE)) {
+          s = ST_NOTFOUND;
+        } else if (S[t] & SF_TOMB) {
+          s = ST_ALREADY;
+        } else {
+          S[t] |= SF_TOMB;
+          s = ST_APPLIED;
+        }
+      } else {  // addAfterHelp
+        const uint32_t x = wlo & PM;
+        const uint32_t an = ((wlo >> 24) | (whi << 8)) & PM;
+        if (x == 0) {
+          s = ST_ALREADY;
+        } else if (an == OW_NF || !(S[an] & SF_MADE)) {
+          s = ST_NOTFOUND;
+        } else {
+          uint32_t node = an, nk = an;  // findInsertion
+          uint32_t wn = S[node];
+          for (;;) {
+            const uint32_t rn = wn & PM;
+            if (rn == PM) break;
+            uint32_t live = rn, wl = S[rn];
+            while (wl & SF_TOMB) {
+              live = wl & PM;
+              if (live == PM) break;
+              wl = S[live];
+            }
+            if (live == PM) break;
+            if (x > rn) break;  // ts > key(rn)
+            nk = rn;
+            node = live;
+            wn = wl;
+          }
+          const uint32_t wk = nk == node ? wn : S[nk];
+          S[x] = (wn & PM) | (wk & SF_ORPHAN) | SF_MADE;
+          if (nk == node) {
+            S[node] = (wn & ~PM) | x;
+          } else {
+            // copy quirk: slot nk := copy of node, next = x; the entries after
+            // nk up to node drop off the chain when nk was on it
+            if (!(wk & SF_ORPHAN)) {
+              for (uint32_t q = wk & PM; q != PM;) {
+                const uint32_t wq = S[q];
+                S[q] = wq | SF_ORPHAN;
+                if (q == node) break;
+                q = wq & PM;
+              }
+              wn |= SF_ORPHAN;
+            }
+            S[nk] = x | (wn & ~PM & ~SF_ORPHAN) | (wk & SF_ORPHAN) | SF_COPY;
+            uint32_t cs, cd, cb;
+            if (wn & SF_COPY) {
+              cs = p.qsrc[base + node];
+              cd = p.qcd[base + node];
+              cb = p.qcb[base + node];
+            } else {
+              cs = cd = p.rop[rb + node];
+              cb = bound;
+            }
+            p.qsrc[base + nk] = cs;
+            p.qcd[base + nk] = cd;
+            p.qcb[base + nk] = min(cb, i);
+            if (ORIG && lane == 0) atomicMin(&p.tcopy[p.rop[rb + nk]], i);
+          }
+          s = ST_APPLIED;
+        }
+      }
+      if (ORIG && lane == 0) st[i] = s;
+    }
+  }
+  __syncthreads();
+  if (S != p.S + base) {
+    for (uint32_t r = lane; r <= K; r += 64) p.S[base + r] = S[r];
+  }
+  for (uint32_t r = lane; r <= K; r += 64) p.inst[base + r] = I;
+}
+
+template <bool ORIG>
+__global__ void __launch_bounds__(64) k_pdr_small(PdrCtx p, const uint32_t* list, uint8_t* st) {
+  __shared__ uint32_t S[PDR_SMALL];
+  pdr_serial<ORIG>(p, st, list[blockIdx.x], S);
+}
+
+template <bool ORIG>
+__global__ void __launch_bounds__(64) k_pdr_big(PdrCtx p, const uint32_t* list, uint8_t* st) {
+  extern __shared__ uint32_t S_dyn[];
+  pdr_serial<ORIG>(p, st, list[blockIdx.x], S_dyn);
+}
+
+template <bool ORIG>
+__global__ void __launch_bounds__(64) k_pdr_huge(PdrCtx p, const uint32_t* list, uint8_t* st) {
+  const uint32_t I = list[blockIdx.x];
+  pdr_serial<ORIG>(p, st, I, p.S + p.I.base[I]);
+}
+
+// Sort instances [i0, i1) into three size tiers: static LDS, dynamic LDS,
+// global memory. count = {tier sizes, largest slot count of tier 1}.
+struct PdrTiers {
+  uint32_t* list[3];
+  uint32_t* count;
+};
+
+__global__ void __launch_bounds__(BLOCK) k_pdr_tier(PdrCtx p, uint32_t i0, uint32_t i1, uint32_t big_cap,
+                                                    PdrTiers tt) {
   const uint32_t n = p.o.n;
-  const uint32_t D = blockIdx.x * blockDim.x + threadIdx.x;
-  if (D > n) return;
-  const uint32_t b = p.rbase[D];
-  if (p.rbase[D + 1] == b) return;
-  p.I.base[D] = b;
-  pdr_replay<true>(p, st, D, NONE, b, D);
+  GRID_STRIDE(k, i1 - i0) {
+    const uint32_t I = i0 + k;
+    uint32_t D = I;
+    if (I > n) D = p.I.src[I];
+    else if (p.rbase[I + 1] == p.rbase[I]) continue;  // a dict no op reached
+    if (I <= n) p.I.base[I] = p.rbase[I];
+    const uint32_t slots = pdr_kcount(p, D) + 1;
+    const uint32_t t = slots <= PDR_SMALL ? 0u : (slots <= big_cap ? 1u : 2u);
+    tt.list[t][atomicAdd(&tt.count[t], 1u)] = I;
+    if (t == 1) atomicMax(&tt.count[3], slots);
+  }
 }
 
 // ---- P3: conflicts ----
@@ -261,12 +361,12 @@ __global__ void k_pdr_stats_reset(DevResult* d) {
   d->err_index = NONE;
   d->pdr_jobs = 0;
   d->pdr_overflow = 0;
+  d->pdr_conflict = 0;
 }
 
 // ---- P5: assembly ----
-// alive[D]: original dict D is reachable in the final state (its owner is a
-// live, un-copied node of an alive dict). ok/up pointer jumping as in
-// k_dict_alive_*.
+// ok[D]: original dict D is reachable in the final state (its owner is a
+// live, un-copied node of a reachable dict); pointer jumping over owners.
 __global__ void __launch_bounds__(BLOCK) k_pdr_alive_init(PdrCtx p, const uint32_t* addpar, uint8_t* ok,
                                                           uint32_t* up) {
   const uint32_t n = p.o.n;
@@ -280,8 +380,8 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_alive_init(PdrCtx p, const uint32
     uint32_t P = n;
     if (p.rbase[d + 1] != p.rbase[d]) {
       P = addpar[d];
-      const uint32_t l = p.lidx[d];
-      v = (l != NONE && !(p.R.fl[p.rbase[P] + l] & (P_TOMB | P_COPY))) ? 1 : 0;
+      const uint32_t w = p.S[p.rbase[P] + p.rankof[d]];
+      v = (w & SF_MADE) && !(w & (SF_TOMB | SF_COPY)) ? 1 : 0;
     }
     ok[d] = v;
     up[d] = P;
@@ -296,20 +396,30 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_alive_jump(uint32_t n, uint8_t* o
   }
 }
 
+__device__ __forceinline__ uint32_t pdr_src_dict(const PdrCtx& p, uint32_t I) { return I > p.o.n ? p.I.src[I] : I; }
+
 // A live slot whose children are a frozen (dict, bound) view gets a snapshot
-// job when that view is non-empty. Slots [s0, s1) of the last replayed regions.
+// job when that view is non-empty. Slot positions [s0, s1).
 __global__ void __launch_bounds__(BLOCK) k_pdr_jobs(PdrCtx p, const uint8_t* ok, uint32_t s0, uint32_t s1,
-                                                    uint32_t jcap, uint32_t scap_left, DevResult* dres) {
+                                                    uint32_t jcap, DevResult* dres) {
   const uint32_t n = p.o.n;
   GRID_STRIDE(k, s1 - s0) {
     const uint32_t g = s0 + k;
-    const uint32_t I = p.R.inst[g];
+    const uint32_t I = p.inst[g];
     if (I == NONE) continue;
-    if (I <= n && !ok[I]) continue;  // a dead original dict
-    const uint8_t f = p.R.fl[g];
-    if (f & P_TOMB) continue;        // (sentinels too)
-    if (I <= n && !(f & P_COPY)) continue;  // children = the live original dict
-    const uint32_t cd = p.R.cd[g], cb = p.R.cb[g];
+    if (I <= n && !ok[I]) continue;  // an unreachable original dict
+    const uint32_t w = p.S[g];
+    if (!(w & SF_MADE) || (w & SF_TOMB)) continue;  // (sentinels too)
+    if (I <= n && !(w & SF_COPY)) continue;         // children = the live original dict
+    uint32_t cd, cb;
+    const uint32_t r = g - p.I.base[I];
+    if (w & SF_COPY) {
+      cd = p.qcd[g];
+      cb = p.qcb[g];
+    } else {
+      cd = p.rop[p.rbase[pdr_src_dict(p, I)] + r];
+      cb = p.I.bound[I];
+    }
     const uint32_t f0 = pdr_first_op(p, cd);
     if (f0 == NONE || f0 >= cb) continue;  // the copy is an empty dict (implicit)
     const uint32_t j = atomicAdd(&dres->pdr_jobs, 1u);
@@ -321,93 +431,103 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_jobs(PdrCtx p, const uint8_t* ok,
     p.I.src[J] = cd;
     p.I.bound[J] = cb;
     p.I.pi[J] = I;
-    p.I.pl[J] = g - p.I.base[I];
-    p.R.ch[g] = J;
+    p.I.pl[J] = r;
+    p.ch[g] = J;
   }
-  (void)scap_left;
 }
 
 __global__ void __launch_bounds__(BLOCK) k_pdr_job_size(PdrCtx p, uint32_t j0, uint32_t j1, uint32_t* sz) {
   const uint32_t n = p.o.n;
   GRID_STRIDE(k, j1 - j0 + 1) {
-    if (k == j1 - j0) {
-      sz[k] = 0;
-      continue;
-    }
-    const uint32_t d = p.I.src[n + 1 + j0 + k];
-    sz[k] = p.rbase[d + 1] - p.rbase[d];
+    sz[k] = k == j1 - j0 ? 0u : pdr_kcount(p, p.I.src[n + 1 + j0 + k]) + 1;
   }
 }
 
-__global__ void __launch_bounds__(64) k_pdr_replay_snap(PdrCtx p, uint32_t j0, uint32_t j1, const uint32_t* off,
+__global__ void __launch_bounds__(BLOCK) k_pdr_job_base(PdrCtx p, uint32_t j0, uint32_t j1, const uint32_t* off,
                                                         uint32_t s0) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= j1 - j0) return;
-  const uint32_t J = p.o.n + 1 + j0 + k;
-  const uint32_t b = s0 + off[k];
-  p.I.base[J] = b;
-  pdr_replay<false>(p, nullptr, p.I.src[J], p.I.bound[J], b, J);
+  const uint32_t n = p.o.n;
+  GRID_STRIDE(k, j1 - j0) p.I.base[n + 1 + j0 + k] = s0 + off[k];
 }
 
 // instance order: root first, then originals 0..n-1, then snapshots
 __device__ __forceinline__ uint32_t pdr_pos(uint32_t I, uint32_t n) { return I == n ? 0u : (I < n ? I + 1 : I); }
 
 __global__ void __launch_bounds__(BLOCK) k_pdr_inst_flags(PdrCtx p, const uint8_t* ok, uint32_t njobs,
-                                                          uint32_t* dflag, uint32_t* dsize) {
+                                                          uint32_t* dflag) {
   const uint32_t n = p.o.n;
   GRID_STRIDE(I, n + 1 + njobs + 1) {
     if (I == n + 1 + njobs) {  // scan tail
       dflag[I] = 0;
-      dsize[I] = 0;
       continue;
     }
     const bool inst = I > n || (ok[I] && p.rbase[I + 1] != p.rbase[I]);
-    const uint32_t q = pdr_pos(I, n);
-    dflag[q] = inst ? 1u : 0u;
-    dsize[q] = inst ? p.I.used[I] : 0u;
+    dflag[pdr_pos(I, n)] = inst ? 1u : 0u;
+  }
+}
+
+// Final slot numbering runs over positions with the root region first, so
+// the root sentinel is slot 0 (api.hip tree reset, linearize).
+__device__ __forceinline__ uint32_t pdr_u_of_g(const PdrCtx& p, uint32_t g) {
+  const uint32_t rb = p.rbase[p.o.n], r0 = p.rbase[p.o.n + 1];
+  return g >= r0 ? g : (g >= rb ? g - rb : g + (r0 - rb));
+}
+__device__ __forceinline__ uint32_t pdr_g_of_u(const PdrCtx& p, uint32_t u) {
+  const uint32_t rb = p.rbase[p.o.n], r0 = p.rbase[p.o.n + 1];
+  return u >= r0 ? u : (u < r0 - rb ? rb + u : u - (r0 - rb));
+}
+
+__global__ void __launch_bounds__(BLOCK) k_pdr_slot_flags(PdrCtx p, const uint8_t* ok, uint32_t S1, uint32_t* f) {
+  const uint32_t n = p.o.n;
+  GRID_STRIDE(u, S1 + 1) {
+    uint32_t v = 0;
+    if (u < S1) {
+      const uint32_t g = pdr_g_of_u(p, u);
+      const uint32_t I = p.inst[g];
+      if (I != NONE && (I > n || ok[I]) && (p.S[g] & SF_MADE)) v = 1;
+    }
+    f[u] = v;
   }
 }
 
 __global__ void __launch_bounds__(BLOCK) k_pdr_write(PdrCtx p, const uint8_t* ok, const uint32_t* addpar,
-                                                     const uint32_t* did, const uint32_t* sbase,
-                                                     const uint32_t* logidx, uint32_t S, TreeDev T) {
+                                                     const uint32_t* did, const uint32_t* fpos,
+                                                     const uint32_t* logidx, uint32_t S1, TreeDev T) {
   const uint32_t n = p.o.n;
-  GRID_STRIDE(g, S) {
-    const uint32_t I = p.R.inst[g];
+  GRID_STRIDE(g, S1) {
+    const uint32_t I = p.inst[g];
     if (I == NONE) continue;
-    if (I <= n && !(ok[I])) continue;
-    const uint32_t q = pdr_pos(I, n);
-    const uint32_t l = g - p.I.base[I];
-    const uint32_t sb = sbase[q];
-    const uint32_t d = did[q];
-    const uint32_t s = sb + l;
-    const uint8_t f = p.R.fl[g];
-    const uint32_t nx = p.R.next[g];
-    T.s_key[s] = p.R.key[g];
+    if (I <= n && !ok[I]) continue;
+    const uint32_t w = p.S[g];
+    if (!(w & SF_MADE)) continue;
+    const uint32_t base = p.I.base[I];
+    const uint32_t r = g - base;
+    const uint32_t rb = p.rbase[pdr_src_dict(p, I)];
+    const uint32_t d = did[pdr_pos(I, n)];
+    const uint32_t s = fpos[pdr_u_of_g(p, g)];
+    const uint32_t nx = w & PM;
     T.s_dict[s] = d;
-    T.s_next[s] = nx == NONE ? NONE : sb + nx;
+    T.s_next[s] = nx == PM ? NONE : fpos[pdr_u_of_g(p, base + nx)];
     uint32_t child = NONE;
-    if (l == 0) {
+    if (r == 0) {
+      T.s_key[s] = 0;
       T.s_src[s] = NONE;
       T.s_flags[s] = F_TOMB | F_SENT;
       T.d_sent[d] = s;
       uint32_t owner = NONE;
-      if (I > n) {
-        owner = sbase[pdr_pos(p.I.pi[I], n)] + p.I.pl[I];
-      } else if (I < n) {
-        owner = sbase[pdr_pos(addpar[I], n)] + p.lidx[I];
-      }
+      if (I > n) owner = fpos[pdr_u_of_g(p, p.I.base[p.I.pi[I]] + p.I.pl[I])];
+      else if (I < n) owner = fpos[pdr_u_of_g(p, p.rbase[addpar[I]] + p.rankof[I])];
       T.d_owner[d] = owner;
     } else {
-      T.s_src[s] = logidx[p.R.src[g]];
-      T.s_flags[s] = ((f & P_TOMB) ? F_TOMB : 0) | ((f & P_ORPHAN) ? F_ORPHAN : 0);
-      if (!(f & P_TOMB)) {
-        if (I > n || (f & P_COPY)) {
-          const uint32_t J = p.R.ch[g];
+      const uint32_t y = p.rop[rb + r];
+      T.s_key[s] = p.o.ts[y];
+      T.s_src[s] = logidx[(w & SF_COPY) ? p.qsrc[g] : y];
+      T.s_flags[s] = ((w & SF_TOMB) ? F_TOMB : 0) | ((w & SF_ORPHAN) ? F_ORPHAN : 0);
+      if (!(w & SF_TOMB)) {
+        if (I > n || (w & SF_COPY)) {
+          const uint32_t J = p.ch[g];
           if (J != NONE) child = did[pdr_pos(J, n)];
-        } else {
-          const uint32_t y = p.R.src[g];  // a live original node: its own dict
-          if (p.rbase[y + 1] != p.rbase[y]) child = did[pdr_pos(y, n)];
+        } else if (p.rbase[y + 1] != p.rbase[y]) {
+          child = did[pdr_pos(y, n)];  // a live original node: its own dict
         }
       }
     }
@@ -417,6 +537,48 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_write(PdrCtx p, const uint8_t* ok
 
 __global__ void __launch_bounds__(BLOCK) k_pdr_logidx(OpsDev o, const uint8_t* st, uint32_t* a) {
   GRID_STRIDE(i, o.n) a[i] = st[i] == ST_APPLIED ? 1u : 0u;
+}
+
+static int pdr_run_tiers(crdtm_ctx* c, const PdrCtx& p, uint32_t i0, uint32_t i1, bool orig, uint8_t* st,
+                         const PdrTiers& tt, uint32_t big_cap, uint32_t* hcount) {
+  hipStream_t s = c->stream;
+  if (i1 <= i0) return CRDTM_OK;
+  HIP_CHECK(hipMemsetAsync(tt.count, 0, 4 * sizeof(uint32_t), s));
+  LAUNCH(k_pdr_tier, dim3(grid_for(i1 - i0)), dim3(BLOCK), 0, s, p, i0, i1, big_cap, tt);
+  HIP_CHECK(hipMemcpyAsync(hcount, tt.count, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  const uint32_t* h = hcount;
+  if (h[0]) {
+    if (orig) LAUNCH(k_pdr_small<true>, dim3(h[0]), dim3(64), 0, s, p, tt.list[0], st);
+    else LAUNCH(k_pdr_small<false>, dim3(h[0]), dim3(64), 0, s, p, tt.list[0], st);
+  }
+  if (h[1]) {
+    const size_t lds = static_cast<size_t>(h[3]) * sizeof(uint32_t);
+    if (orig) LAUNCH(k_pdr_big<true>, dim3(h[1]), dim3(64), lds, s, p, tt.list[1], st);
+    else LAUNCH(k_pdr_big<false>, dim3(h[1]), dim3(64), lds, s, p, tt.list[1], st);
+  }
+  if (h[2]) {
+    if (orig) LAUNCH(k_pdr_huge<true>, dim3(h[2]), dim3(64), 0, s, p, tt.list[2], st);
+    else LAUNCH(k_pdr_huge<false>, dim3(h[2]), dim3(64), 0, s, p, tt.list[2], st);
+  }
+  return CRDTM_OK;
+}
+
+// slots a workgroup can hold in dynamic LDS (the per-block maximum)
+static uint32_t pdr_big_cap(int device) {
+  static int cached = -1;
+  if (cached < 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess || v <= 0)
+      v = 64 * 1024;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pdr_big<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, v) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pdr_big<false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, v) != hipSuccess)
+      v = 64 * 1024;
+    cached = v;
+  }
+  return static_cast<uint32_t>(cached) / sizeof(uint32_t);
 }
 
 // Host driver. *handled = false: conflict or no room, the caller replays
@@ -431,6 +593,8 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   *handled = false;
   const size_t arena_mark = ws.used;
   int r;
+  const uint32_t big_cap = pdr_big_cap(c->device);
+  uint32_t hcount[4];
 
   PdrCtx p;
   p.o = o;
@@ -438,59 +602,64 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   p.leaf = in.leaf;
   uint32_t* rbase = ws.alloc<uint32_t>(n + 2);
   uint32_t* fill = ws.alloc<uint32_t>(n + 2);
-  p.lidx = ws.alloc<uint32_t>(n);
+  uint32_t* cbase = ws.alloc<uint32_t>(n + 2);
+  uint32_t* cfill = ws.alloc<uint32_t>(n + 2);
+  p.rankof = ws.alloc<uint32_t>(n);
   p.tcopy = ws.alloc<uint32_t>(n);
-  LAUNCH(k_pdr_init, dim3(grid_for(n + 2)), dim3(BLOCK), 0, s, n, rbase, fill, p.lidx, p.tcopy);
-  LAUNCH(k_pdr_count, dim3(g), dim3(BLOCK), 0, s, o, in.tag, in.cur, rbase);
+  LAUNCH(k_pdr_init, dim3(grid_for(n + 2)), dim3(BLOCK), 0, s, n, rbase, fill, cbase, cfill, p.rankof, p.tcopy);
+  LAUNCH(k_pdr_count, dim3(g), dim3(BLOCK), 0, s, o, in.ix, in.tag, in.cur, rbase, cbase);
   LAUNCH(k_pdr_size, dim3(grid_for(n + 1)), dim3(BLOCK), 0, s, n, rbase);
-  uint32_t* rtot = &dr->pdr_slots;
-  if ((r = scan_excl_u32(rbase, rbase, n + 2, rtot, ws, s))) return r;
+  if ((r = scan_excl_u32(rbase, rbase, n + 2, &dr->pdr_slots, ws, s))) return r;
+  if ((r = scan_excl_u32(cbase, cbase, n + 2, &dr->pdr_dicts, ws, s))) return r;
   if ((r = sync_read(c))) return r;
   const uint32_t R0 = c->hres->pdr_slots;  // original regions
+  const uint32_t KT = c->hres->pdr_dicts;  // keys over all dicts
+  if (R0 >= PM) return CRDTM_OK;           // slot indices are 24-bit: sequential replay
   p.rbase = rbase;
+  p.cbase = cbase;
   uint32_t* olist = ws.alloc<uint32_t>(R0);
+  uint32_t* carr = ws.alloc<uint32_t>(KT + 1);
   p.olist = olist;
   HIP_CHECK(hipMemsetAsync(olist, 0xFF, static_cast<size_t>(R0) * sizeof(uint32_t), s));
-  LAUNCH(k_pdr_scatter, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, in.tag, in.cur, rbase, fill, olist);
+  LAUNCH(k_pdr_scatter, dim3(g), dim3(BLOCK), 0, s, o, in.ix, in.tag, in.cur, rbase, fill, olist, cbase, cfill, carr);
   if ((r = segmented_sort_asc_id(rbase, n + 1, olist, R0, ws, s, dr))) return r;
+  if ((r = segmented_sort(cbase, n + 1, carr, KT, o.ts, ws, s, dr))) return r;
+  p.rop = ws.alloc<uint32_t>(R0);
+  LAUNCH(k_pdr_rank, dim3(grid_for(KT)), dim3(BLOCK), 0, s, KT, carr, in.cur, cbase, rbase, p.rankof, p.rop);
+  unsigned long long* opw = ws.alloc<unsigned long long>(R0);
+  LAUNCH(k_pdr_opw, dim3(grid_for(R0)), dim3(BLOCK), 0, s, R0, olist, o, in.leaf, p.rankof, opw);
+  p.opw = opw;
 
   // slot room: originals + snapshots (bounded; overflow -> sequential replay)
-  const uint64_t scap64 = std::min<uint64_t>(2ULL * R0 + 4096, 0xF0000000ULL);
-  const uint32_t SCAP = static_cast<uint32_t>(scap64);
+  const uint32_t SCAP = static_cast<uint32_t>(std::min<uint64_t>(2ULL * R0 + 4096, PM - 1));
   const uint32_t JCAP = std::max<uint32_t>(1024u, n);
-  PdrRegion& R = p.R;
-  R.key = ws.alloc<long long>(SCAP);
-  R.next = ws.alloc<uint32_t>(SCAP);
-  R.src = ws.alloc<uint32_t>(SCAP);
-  R.cd = ws.alloc<uint32_t>(SCAP);
-  R.cb = ws.alloc<uint32_t>(SCAP);
-  R.ch = ws.alloc<uint32_t>(SCAP);
-  R.inst = ws.alloc<uint32_t>(SCAP);
-  R.fl = ws.alloc<uint8_t>(SCAP);
+  p.S = ws.alloc<uint32_t>(SCAP);
+  p.qsrc = ws.alloc<uint32_t>(SCAP);
+  p.qcd = ws.alloc<uint32_t>(SCAP);
+  p.qcb = ws.alloc<uint32_t>(SCAP);
+  p.ch = ws.alloc<uint32_t>(SCAP);
+  p.inst = ws.alloc<uint32_t>(SCAP);
   const uint64_t ICAP = static_cast<uint64_t>(n) + 1 + JCAP;
-  PdrInst& I = p.I;
-  I.base = ws.alloc<uint32_t>(ICAP);
-  I.used = ws.alloc<uint32_t>(ICAP);
-  I.src = ws.alloc<uint32_t>(ICAP);
-  I.bound = ws.alloc<uint32_t>(ICAP);
-  I.pi = ws.alloc<uint32_t>(ICAP);
-  I.pl = ws.alloc<uint32_t>(ICAP);
-  HIP_CHECK(hipMemsetAsync(R.inst, 0xFF, static_cast<size_t>(SCAP) * sizeof(uint32_t), s));
+  p.I.base = ws.alloc<uint32_t>(ICAP);
+  p.I.src = ws.alloc<uint32_t>(ICAP);
+  p.I.bound = ws.alloc<uint32_t>(ICAP);
+  p.I.pi = ws.alloc<uint32_t>(ICAP);
+  p.I.pl = ws.alloc<uint32_t>(ICAP);
+  PdrTiers tt;
+  for (int k = 0; k < 3; ++k) tt.list[k] = ws.alloc<uint32_t>(ICAP);
+  tt.count = ws.alloc<uint32_t>(4);
+  HIP_CHECK(hipMemsetAsync(p.inst, 0xFF, static_cast<size_t>(SCAP) * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(p.ch, 0xFF, static_cast<size_t>(SCAP) * sizeof(uint32_t), s));
 
   // ---- P2 + P3 ----
-  LAUNCH(k_pdr_replay_orig, dim3((n + 1 + 63) / 64), dim3(64), 0, s, p, st);
+  if ((r = pdr_run_tiers(c, p, 0, n + 1, true, st, tt, big_cap, hcount))) return r;
   LAUNCH(k_pdr_stats_reset, dim3(1), dim3(1), 0, s, dr);
-  HIP_CHECK(hipMemsetAsync(&dr->pdr_conflict, 0, sizeof(uint32_t), s));
   LAUNCH(k_pdr_conflict, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, n, in.tag, p.tcopy, dr);
   LAUNCH(k_pdr_stats, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, o, st, t->timestamp, dr);
   if ((r = sync_read(c))) return r;
   const DevResult h1 = *c->hres;
-  if (h1.pdr_conflict) {
-    ws.used = arena_mark;
-    return CRDTM_OK;
-  }
   const long long new_ts = t->timestamp + h1.own_ok_adds;
-  if (replica_of(new_ts) != replica_of(t->timestamp)) {
+  if (h1.pdr_conflict || replica_of(new_ts) != replica_of(t->timestamp)) {
     ws.used = arena_mark;
     return CRDTM_OK;
   }
@@ -506,7 +675,7 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   res->n_applied = h1.n_applied;
   res->n_already = h1.n_already;
 
-  // ---- P5: alive originals, snapshot jobs level by level ----
+  // ---- P5: reachable originals, snapshot jobs level by level ----
   uint8_t* ok = ws.alloc<uint8_t>(n + 1);
   uint32_t* up = ws.alloc<uint32_t>(n + 1);
   LAUNCH(k_pdr_alive_init, dim3(grid_for(n + 1)), dim3(BLOCK), 0, s, p, in.addpar, ok, up);
@@ -515,7 +684,7 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   uint32_t s0 = 0, s1 = R0, j0 = 0;
   uint32_t* joff = ws.alloc<uint32_t>(JCAP + 1);
   for (uint32_t level = 0;; ++level) {
-    LAUNCH(k_pdr_jobs, dim3(grid_for(s1 - s0)), dim3(BLOCK), 0, s, p, ok, s0, s1, JCAP, SCAP - s1, dr);
+    LAUNCH(k_pdr_jobs, dim3(grid_for(s1 - s0)), dim3(BLOCK), 0, s, p, ok, s0, s1, JCAP, dr);
     if ((r = sync_read(c))) return r;
     if (c->hres->pdr_overflow || level > in.maxlen + 1) {  // no room: sequential replay
       *handled = false;
@@ -533,7 +702,8 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
       ws.used = arena_mark;
       return CRDTM_OK;
     }
-    LAUNCH(k_pdr_replay_snap, dim3((j1 - j0 + 63) / 64), dim3(64), 0, s, p, j0, j1, joff, s1);
+    LAUNCH(k_pdr_job_base, dim3(grid_for(j1 - j0)), dim3(BLOCK), 0, s, p, j0, j1, joff, s1);
+    if ((r = pdr_run_tiers(c, p, n + 1 + j0, n + 1 + j1, false, st, tt, big_cap, hcount))) return r;
     s0 = s1;
     s1 = static_cast<uint32_t>(need);
     j0 = j1;
@@ -543,10 +713,11 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   // ---- numbering ----
   const uint32_t NI = n + 1 + nj;
   uint32_t* did = ws.alloc<uint32_t>(NI + 1);
-  uint32_t* sbase = ws.alloc<uint32_t>(NI + 1);
-  LAUNCH(k_pdr_inst_flags, dim3(grid_for(NI + 1)), dim3(BLOCK), 0, s, p, ok, nj, did, sbase);
+  uint32_t* fpos = ws.alloc<uint32_t>(static_cast<uint64_t>(s1) + 1);
+  LAUNCH(k_pdr_inst_flags, dim3(grid_for(NI + 1)), dim3(BLOCK), 0, s, p, ok, nj, did);
   if ((r = scan_excl_u32(did, did, NI + 1, &dr->pdr_dicts, ws, s))) return r;
-  if ((r = scan_excl_u32(sbase, sbase, NI + 1, &dr->pdr_slots, ws, s))) return r;
+  LAUNCH(k_pdr_slot_flags, dim3(grid_for(s1 + 1)), dim3(BLOCK), 0, s, p, ok, s1, fpos);
+  if ((r = scan_excl_u32(fpos, fpos, s1 + 1, &dr->pdr_slots, ws, s))) return r;
   uint32_t* logidx = ws.alloc<uint32_t>(n + 1);
   LAUNCH(k_pdr_logidx, dim3(g), dim3(BLOCK), 0, s, o, st, logidx);
   if ((r = scan_excl_u32(logidx, logidx, n, nullptr, ws, s))) return r;
@@ -560,7 +731,7 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   if (need.slots > t->cap.slots || need.dicts > t->cap.dicts || need.log > t->cap.log || need.lpath > t->cap.lpath) {
     if ((r = grow_tree(t, need))) return r;
   }
-  LAUNCH(k_pdr_write, dim3(grid_for(s1)), dim3(BLOCK), 0, s, p, ok, in.addpar, did, sbase, logidx, s1, t->d);
+  LAUNCH(k_pdr_write, dim3(grid_for(s1)), dim3(BLOCK), 0, s, p, ok, in.addpar, did, fpos, logidx, s1, t->d);
   if ((r = post_pass(t, o, st, ws))) return r;
   t->n_slots = n_slots;
   t->n_dicts = n_dicts;

@@ -341,7 +341,7 @@ static int segmented_sort_t(const uint32_t* seg_start, uint32_t n_seg, uint32_t*
   uint32_t* nbig = &dres->big_segments;
   uint32_t* nhuge = &dres->huge_segments;
   uint32_t* nmid = &dres->mid_segments;
-  // big_segments / huge_segments / mid_segments start at 0 (k_dres_init, once per merge)
+  // big_segments / huge_segments / mid_segments are 0 on entry (k_dres_init; reset on exit)
   LAUNCH(k_sort_small<KEY>, dim3(grid_for(n_seg)), dim3(BLOCK), 0, st, seg_start, n_seg, carr, sort_key, skip, mid,
          nmid, big, nbig);
   LAUNCH(k_sort_mid<KEY>, dim3(1024), dim3(BLOCK), 0, st, seg_start, mid, nmid, carr, sort_key);
@@ -351,6 +351,11 @@ static int segmented_sort_t(const uint32_t* seg_start, uint32_t n_seg, uint32_t*
   uint32_t nh = 0;
   HIP_CHECK(hipMemcpyAsync(&nh, nhuge, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));
+  // leave the three counters at 0 for the next sort of this merge
+  static_assert(offsetof(DevResult, huge_segments) == offsetof(DevResult, big_segments) + 4 &&
+                    offsetof(DevResult, mid_segments) == offsetof(DevResult, big_segments) + 8,
+                "sort counters are contiguous");
+  HIP_CHECK(hipMemsetAsync(nbig, 0, 3 * sizeof(uint32_t), st));
   if (nh == 0) return CRDTM_OK;
   std::vector<uint32_t> hh(nh);
   HIP_CHECK(hipMemcpy(hh.data(), huge, nh * sizeof(uint32_t), hipMemcpyDeviceToHost));
