@@ -55,6 +55,23 @@ def alg_bytes(s):
     return int(np.sum(np.where(add, 49 + 8 * L, 9 + 8 * L)))
 
 
+def stream_copy_gbs(dev, nbytes=1 << 30, reps=5):
+    """Measured device-copy ceiling (read + write bytes / time), SURVEY.md §8d."""
+    import torch
+    a = torch.empty(nbytes // 4, dtype=torch.int32, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2 * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del a, b
+    return gbs
+
+
 def head(s, m):
     off = s["path_off"]
     return dict(kind=s["kind"][:m].copy(), ts=s["ts"][:m].copy(), val=s["val"][:m].copy(),
@@ -166,6 +183,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     path_taken = res.path_taken
+    guard = res.guard
 
     # Per-kernel device time (HIP events recorded on the launch stream) over a
     # few extra, untimed steps.
@@ -214,12 +232,17 @@ def main():
         "config": {"workload": f"{args.workload}: {n} ops per GPU, one document per GPU",
                    "replicas": spec.get("replicas"), "window": spec.get("window", 0),
                    "path": {1: "closed-form", 2: "replay", 3: "per-dict replay"}.get(path_taken, "?"),
+                   "guard": guard,
                    "parallelism": f"documents sharded by id over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "alg_bytes_per_launch": B_alg, "kernel_ms": t_dom * 1e3, "kernels_ms_per_step": kernels_ms,
                      "merge_frac": B_alg / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS},
     }
+    if rank == 0:
+        sc = stream_copy_gbs(dev)
+        line["roofline"]["stream_copy_gbs"] = sc
+        line["roofline"]["frac_of_stream"] = achieved / sc
     if args.verbose and rank == 0:
         for nm, v in sorted(per_step.items(), key=lambda kv: -kv[1]):
             print(f"  {nm:28s} {v:9.3f} ms/step ({len(acc[nm]) // max(1, args.profile_steps)} launches)",

@@ -55,6 +55,7 @@ SIGNATURES = [
     ("crdtm_tree_timestamp", C.c_int, [P, C.POINTER(C.c_int64)]),
     ("crdtm_tree_replicas", C.c_int, [P, P, P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("crdtm_tree_ops", C.c_int, [P, C.c_int, C.POINTER(Ops), C.POINTER(C.c_int)]),
+    ("crdtm_tree_ops_since", C.c_int, [P, C.c_int64, C.POINTER(Ops)]),
     ("crdtm_tree_canonical", C.c_int, [P, C.c_int, P, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("crdtm_tree_document", C.c_int, [P, P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("crdtm_forest_apply", C.c_int, [P, C.c_int64, C.POINTER(Ops), P, C.c_uint64, C.c_int, P, P, P, P, P, P]),

@@ -226,10 +226,17 @@ class CRDTree:
         """CRDTree.lastReplicaTimestamp (src/CRDTree.elm:637-639)."""
         return self.replicas().get(rid, 0)
 
-    def _ops(self, which):
+    def _ops(self, which, since=None):
         o = N.Ops()
-        isb = C.c_int()
-        N.check(N.lib().crdtm_tree_ops(self._h, which, C.byref(o), C.byref(isb)))
+        isb = C.c_int(1)
+
+        def fetch(ops):
+            if since is None:
+                N.check(N.lib().crdtm_tree_ops(self._h, which, C.byref(ops), C.byref(isb)))
+            else:
+                N.check(N.lib().crdtm_tree_ops_since(self._h, since, C.byref(ops)))
+
+        fetch(o)
         n, npth = o.n_ops, o.n_path
         kind = np.zeros(n + 1, np.uint8)
         ts = np.zeros(n + 1, np.int64)
@@ -237,7 +244,7 @@ class CRDTree:
         path = np.zeros(npth + 1, np.int64)
         val = np.zeros(n + 1, np.uint32)
         o2 = N.Ops(n, npth, _ptr(kind), _ptr(ts), _ptr(off), _ptr(path), _ptr(val), None)
-        N.check(N.lib().crdtm_tree_ops(self._h, which, C.byref(o2), C.byref(isb)))
+        fetch(o2)
         out = []
         for i in range(n):
             p = [int(x) for x in path[off[i]:off[i + 1]]]
@@ -257,16 +264,9 @@ class CRDTree:
         return Batch(ops) if isb else ops[0]
 
     def operations_since(self, ts: int) -> Batch:
-        """CRDTree.operationsSince (src/CRDTree.elm:408-418)."""
-        log = self.operations()
-        if ts == 0:
-            return Batch(log)
-        acc = []
-        for o in reversed(log):
-            acc.insert(0, o)
-            if o.kind == "add" and o.ts == ts:
-                return Batch(acc)
-        return Batch([])
+        """CRDTree.operationsSince (src/CRDTree.elm:408-418): inclusive of the
+        newest logged Add with that ts, [] when absent (crdtm_tree_ops_since)."""
+        return Batch(self._ops(0, since=ts)[0])
 
     def canonical(self, which=0, full=True):
         n = C.c_uint64()

@@ -439,11 +439,8 @@ int crdtm_tree_replicas(const crdtm_tree* t, int64_t* ids, int64_t* tss, uint64_
   return CRDTM_OK;
 }
 
-int crdtm_tree_ops(const crdtm_tree* t, int which, crdtm_ops* out, int* is_batch) {
-  if (!t || !out) return CRDTM_E_ARG;
-  const uint64_t b = which == 0 ? 0 : t->last_begin;
-  const uint64_t e = which == 0 ? t->log_n : t->last_end;
-  if (is_batch) *is_batch = which == 0 ? 1 : t->last_is_batch;
+// Copy log entries [b, e) out as a crdtm_ops (sizes only when out->kind is NULL).
+static int copy_log_range(const crdtm_tree* t, uint64_t b, uint64_t e, crdtm_ops* out) {
   const uint64_t n = e - b;
   std::vector<uint32_t> off(n + 1);
   HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
@@ -461,6 +458,38 @@ int crdtm_tree_ops(const crdtm_tree* t, int which, crdtm_ops* out, int* is_batch
   for (uint64_t i = 0; i <= n; ++i) out->path_off[i] = off[i] - static_cast<uint32_t>(pb);
   if (pe > pb) HIP_CHECK(hipMemcpy(out->path, t->d.l_path + pb, (pe - pb) * 8, hipMemcpyDeviceToHost));
   return CRDTM_OK;
+}
+
+int crdtm_tree_ops(const crdtm_tree* t, int which, crdtm_ops* out, int* is_batch) {
+  if (!t || !out) return CRDTM_E_ARG;
+  const uint64_t b = which == 0 ? 0 : t->last_begin;
+  const uint64_t e = which == 0 ? t->log_n : t->last_end;
+  if (is_batch) *is_batch = which == 0 ? 1 : t->last_is_batch;
+  return copy_log_range(t, b, e, out);
+}
+
+// since (src/Internal/Operation.elm:25-53): the newest logged Add with this ts
+__global__ void k_since(const uint8_t* kind, const long long* ts, uint64_t n, long long want, uint32_t* end) {
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    if (kind[i] == CRDTM_ADD && ts[i] == want) atomicMax(end, static_cast<uint32_t>(i + 1));
+}
+
+int crdtm_tree_ops_since(const crdtm_tree* t, int64_t ts, crdtm_ops* out) {
+  if (!t || !out) return CRDTM_E_ARG;
+  crdtm_ctx* c = t->ctx;
+  HIP_CHECK(hipSetDevice(c->device));
+  if (ts == 0) return copy_log_range(t, 0, t->log_n, out);  // operationsSince 0: the whole log
+  uint32_t* end = &c->dres->since_end;
+  HIP_CHECK(hipMemsetAsync(end, 0, sizeof(uint32_t), c->stream));
+  if (t->log_n)
+    hipLaunchKernelGGL(k_since, dim3(grid_for(t->log_n)), dim3(BLOCK), 0, c->stream, t->d.l_kind, t->d.l_ts,
+                       t->log_n, static_cast<long long>(ts), end);
+  uint32_t h = 0;
+  HIP_CHECK(hipMemcpyAsync(&h, end, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(hipStreamSynchronize(c->stream));
+  if (h == 0) return copy_log_range(t, 0, 0, out);  // no such Add: []
+  return copy_log_range(t, h - 1, t->log_n, out);
 }
 
 int crdtm_tree_canonical(const crdtm_tree* t, int which, int64_t* out, uint64_t cap, uint64_t* n_words,

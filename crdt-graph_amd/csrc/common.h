@@ -79,6 +79,7 @@ struct DevResult {
   uint32_t pdr_overflow;    // per-dict replay: snapshot room exhausted
   uint32_t pdr_dicts;       // per-dict replay: dicts of the new state
   uint32_t pdr_slots;       // per-dict replay: slots of the new state
+  uint32_t since_end;       // operationsSince: 1 + log index of the newest Add with the asked ts
 };
 
 #define HIP_CHECK(x)                                                                         \

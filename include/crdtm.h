@@ -121,6 +121,11 @@ int crdtm_tree_replicas(const crdtm_tree *t, int64_t *ids, int64_t *tss, uint64_
  * op list when which == 1 (*is_batch = 0 means lastOperation is that single op).
  * Host arrays; call with NULL arrays to size (n_ops, n_path). */
 int crdtm_tree_ops(const crdtm_tree *t, int which, crdtm_ops *out, int *is_batch);
+/* operationsSince ts (src/CRDTree.elm:408-418 -> since, src/Internal/Operation.elm:25-53):
+ * the log oldest-first from the newest logged Add whose ts == ts (inclusive) to the end;
+ * no such Add -> no ops; ts == 0 -> the whole log. The search runs on the device.
+ * Host arrays; NULL arrays to size, like crdtm_tree_ops. */
+int crdtm_tree_ops_since(const crdtm_tree *t, int64_t ts, crdtm_ops *out);
 
 /* Canonical dumps shared with the oracle: which 0 = every dict entry (structure),
  * 1 = visible document order. Writes up to cap words (out may be NULL), the

@@ -51,12 +51,32 @@ def log_tuples(kind, ts, off, path, val, n):
              int(val[i]) if kind[i] == 0 else 0) for i in range(n)]
 
 
-def engine_log(tree, which=0):
+def oracle_since(t, ts):
+    """Operation.since (src/Internal/Operation.elm:25-53) over the oracle's log:
+    newest-first walk, inclusive of the first Add with that ts; [] when absent;
+    operationsSince 0 = the whole log (src/CRDTree.elm:408-418)."""
+    log, _ = oracle_log(t, 0)
+    if ts == 0:
+        return log
+    for j in range(len(log) - 1, -1, -1):
+        if log[j][0] == 0 and log[j][1] == ts:
+            return log[j:]
+    return []
+
+
+def engine_log(tree, which=0, since=None):
     import crdtm._native as N
     from crdtm.tree import _ptr
     o = N.Ops()
-    isb = C.c_int()
-    N.check(N.lib().crdtm_tree_ops(tree._h, which, C.byref(o), C.byref(isb)))
+    isb = C.c_int(1)
+
+    def fetch(ops):
+        if since is None:
+            N.check(N.lib().crdtm_tree_ops(tree._h, which, C.byref(ops), C.byref(isb)))
+        else:
+            N.check(N.lib().crdtm_tree_ops_since(tree._h, since, C.byref(ops)))
+
+    fetch(o)
     n, npth = o.n_ops, o.n_path
     kind = np.zeros(n + 1, np.uint8)
     ts = np.zeros(n + 1, np.int64)
@@ -64,7 +84,7 @@ def engine_log(tree, which=0):
     path = np.zeros(npth + 1, np.int64)
     val = np.zeros(n + 1, np.uint32)
     o2 = N.Ops(n, npth, _ptr(kind), _ptr(ts), _ptr(off), _ptr(path), _ptr(val), None)
-    N.check(N.lib().crdtm_tree_ops(tree._h, which, C.byref(o2), C.byref(isb)))
+    fetch(o2)
     return log_tuples(kind, ts, off, path, val, n), bool(isb.value)
 
 

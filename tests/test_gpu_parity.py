@@ -14,8 +14,8 @@ from crdtm import _native as N  # noqa: E402
 from crdtm.operation import flatten  # noqa: E402
 from crdtm.tree import CRDTree, pack  # noqa: E402
 from kat_cases import SCENARIOS  # noqa: E402
-from parity_util import (engine_log, engine_summary, oracle_apply_arrays, oracle_log, oracle_summary,  # noqa: E402
-                         oracle_visible_vals)
+from parity_util import (engine_log, engine_summary, oracle_apply_arrays, oracle_log, oracle_since,  # noqa: E402
+                         oracle_summary, oracle_visible_vals)
 
 
 def run_both(replica, calls):
@@ -109,6 +109,27 @@ def test_adversarial_streams(chunk):
         assert engine_log(et, 0) == oracle_log(ot, 0), seed
         assert np.array_equal(et.document_handles(), oracle_visible_vals(ot)), seed
     assert paths.get(N.PATH_DICT_REPLAY, 0) > 0, paths
+
+
+def test_operations_since_matches_oracle():
+    """operationsSince through the device search (crdtm_tree_ops_since) against
+    the oracle's newest-first walk (src/Internal/Operation.elm:25-53), incl. the
+    reference test's vectors (tests/CRDTreeTest.elm:592-658)."""
+    replica, calls = SCENARIOS["operations_since"]
+    ot, et, results = run_both(replica, calls)
+    full = tuple(et.operations())
+    assert et.operations_since(0).ops == full
+    assert et.operations_since(2).ops == full[1:]
+    assert et.operations_since(6).ops == full[-1:]
+    assert et.operations_since(10).ops == ()
+    s, n = synth_case(n_ops=5000, replicas=4, window=16, p_delete=0.2, p_branch=0.1, max_depth=3, seed=21)
+    ot, rc, _ = oracle_apply_arrays(s, n)
+    et = CRDTree.init(0)
+    assert et.apply_arrays(s, n).code == rc == 0
+    rng = np.random.default_rng(3)
+    adds = s["ts"][s["kind"] == 0]
+    for want in list(rng.choice(adds, 16)) + [0, 12345]:
+        assert engine_log(et, since=int(want))[0] == oracle_since(ot, int(want)), int(want)
 
 
 def test_incremental_batches():
