@@ -16,6 +16,7 @@ namespace crdtm {
 constexpr uint32_t NONE = 0xFFFFFFFFu;     // absent index / list end
 constexpr uint32_t ABSENT = 0xFFFFFFFEu;   // entry not part of a list
 constexpr uint32_t PDR_REACHED = 0xFFFFFFFDu;  // K1 tag: the op's path resolved to its leaf dict
+constexpr uint32_t TAG_LAZY = 0xFFFFFFFBu;     // K1 tag: stopped at a Tombstone of the chain ending at cur
 constexpr uint32_t SENT_T = 0xFFFFFFFDu;       // K1 leaf target: the dict's sentinel (key 0)
 constexpr uint32_t MISS_T = 0xFFFFFFFCu;       // K1 leaf target: key not in the dict
 constexpr int64_t TWO53 = 9007199254740992LL;
@@ -39,6 +40,7 @@ enum : uint32_t {
   G_DEL_BEFORE_ADD = 2u,// a dict saw a Delete before a later Add (tombstones in the skip walk)
   G_REPLICA_DRIFT = 4u, // own replica id changes during the batch (timestamp crosses 2^32)
   G_NOT_FRESH = 8u,     // tree already holds state (incremental merge)
+  G_DEEP_PATH = 16u,    // a path longer than the length buckets of K1
 };
 
 // Small device-side result block (one copy back per phase).

@@ -160,10 +160,11 @@ struct OpsDev {
 // K1 results handed to the per-dict replay (pdr.hip)
 struct PdrIn {
   TsIndex ix;
-  const uint32_t* tag;     // PDR_REACHED, the tombstoned node the path stopped at, or NONE
+  const uint32_t* tag;     // PDR_REACHED, the tombstoned node the path stopped at, TAG_LAZY, or NONE
   const uint32_t* cur;     // leaf dict owner (n = root)
   const uint32_t* leaf;    // leaf target: node, SENT_T or MISS_T
   const uint32_t* addpar;  // Adds: dict owner
+  const uint32_t* dtime;   // node -> first Delete that tombstoned it
   uint32_t maxlen;
 };
 

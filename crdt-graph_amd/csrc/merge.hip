@@ -24,7 +24,6 @@ namespace crdtm {
 struct Work {  // per-call device arrays of the closed form (sized by n ops)
   uint8_t* st;
   uint32_t* cur;
-  uint32_t* nxt;
   uint32_t* leaf;
   uint32_t* addpar;
   uint32_t* dtime;
@@ -324,25 +323,17 @@ __global__ void __launch_bounds__(BLOCK) k_flat_status(OpsDev o, Work w, TsIndex
   }
 }
 
-// Adds whose path has length lvl record their dict owner (resolved prefix).
-__global__ void __launch_bounds__(BLOCK) k_lvl_addpar(OpsDev o, Work w, uint32_t lvl) {
-  GRID_STRIDE(i, o.n) {
-    if (o.kind[i] == CRDTM_ADD && w.st[i] == ST_PENDING && op_len(o, i) == lvl) w.addpar[i] = w.cur[i];
-  }
-}
-
-// The closed form names a node by its timestamp alone; the same ts added under
-// two different parents breaks that and routes the batch to the replay.
-__global__ void __launch_bounds__(BLOCK) k_lvl_collide(OpsDev o, Work w, TsIndex h, uint32_t lvl, DevResult* dres) {
-  GRID_STRIDE(i, o.n) {
-    if (o.kind[i] != CRDTM_ADD || op_len(o, i) != lvl || w.addpar[i] == NONE) continue;
-    const long long ts = o.ts[i];
-    if (ts == 0) continue;
-    const uint32_t f = tsindex_find(h, ts);
-    if (f != i && (op_len(o, f) != lvl || w.addpar[f] != w.addpar[i])) atomicOr(&dres->guard, G_COLLISION);
-  }
-}
-
+// K1 by path length. Ops are bucketed by |path| and level j handles only the
+// ops of length j, after every shorter op is final: their dict owner (L1),
+// the leaf lookup, collisions and Delete times (L2), then statuses and each
+// new node's chain death time (L3). Path resolution (src/Internal/Node.elm:
+// 138-163) descends through keys; with timestamps unique per dict (the
+// collision guard) the node of key k is tsindex_find(k), so the prefix
+// [k1..k(j-1)] of op i names the node g = find(k(j-1)) exactly when g's own
+// parent path equals [k1..k(j-2)]: then i's ancestors are g's, and i reaches
+// g's children iff g was applied and no node of that chain was deleted before
+// i (dtc[g] = first Delete time over the chain). Anything else takes the
+// literal walk, one lookup per level.
 __device__ __forceinline__ uint32_t lookup_child(const OpsDev& o, const Work& w, const TsIndex& h, uint32_t parent,
                                                  long long k, uint32_t lvl) {
   if (k == 0) return SENT_T;
@@ -351,69 +342,172 @@ __device__ __forceinline__ uint32_t lookup_child(const OpsDev& o, const Work& w,
   return f;
 }
 
-// Resolve path element lvl (1-based) of every pending op.
-__global__ void __launch_bounds__(BLOCK) k_lvl_resolve(OpsDev o, Work w, TsIndex h, uint32_t lvl) {
-  GRID_STRIDE(i, o.n) {
+struct LevelLists {
+  uint32_t* ops;          // op indices grouped by |path|
+  uint32_t* fill;         // [MAXLV_BUCKET + 1] scatter cursors
+};
+constexpr uint32_t MAXLV_BUCKET = 64;  // longer paths: the per-level fallback
+
+__global__ void __launch_bounds__(BLOCK) k_len_count(OpsDev o, uint32_t maxlen, uint32_t* cnt) {
+  __shared__ uint32_t hist[MAXLV_BUCKET + 1];
+  for (uint32_t j = threadIdx.x; j <= maxlen; j += blockDim.x) hist[j] = 0;
+  __syncthreads();
+  GRID_STRIDE(i, o.n) atomicAdd(&hist[op_len(o, i)], 1u);
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j <= maxlen; j += blockDim.x)
+    if (hist[j]) atomicAdd(&cnt[j], hist[j]);
+}
+
+// one global atomic per (block, length): the block reserves its range, then
+// ranks its ops in LDS (order inside a level does not matter)
+struct LevelStart {
+  uint32_t v[MAXLV_BUCKET + 1];
+};
+
+__global__ void __launch_bounds__(BLOCK) k_len_scatter(OpsDev o, uint32_t maxlen, LevelStart start,
+                                                       uint32_t* fill, uint32_t* lists) {
+  __shared__ uint32_t hist[MAXLV_BUCKET + 1];
+  __shared__ uint32_t base[MAXLV_BUCKET + 1];
+  const uint32_t n = o.n;
+  const uint32_t chunk = BLOCK * 8;
+  for (uint32_t c0 = blockIdx.x * chunk; c0 < n; c0 += gridDim.x * chunk) {
+    for (uint32_t j = threadIdx.x; j <= maxlen; j += blockDim.x) hist[j] = 0;
+    __syncthreads();
+    uint32_t L[8], r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t i = c0 + u * BLOCK + threadIdx.x;
+      L[u] = i < n ? op_len(o, i) : NONE;
+      r[u] = (L[u] != NONE) ? atomicAdd(&hist[L[u]], 1u) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j <= maxlen; j += blockDim.x)
+      base[j] = hist[j] ? start.v[j] + atomicAdd(&fill[j], hist[j]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t i = c0 + u * BLOCK + threadIdx.x;
+      if (L[u] != NONE) lists[base[L[u]] + r[u]] = i;
+    }
+    __syncthreads();
+  }
+}
+
+// L1: the dict of every op of length j (fast prefix check, else the walk).
+__global__ void __launch_bounds__(BLOCK) k_lv_dict(OpsDev o, Work w, TsIndex h, const uint32_t* list, uint32_t cnt,
+                                                   uint32_t j, const uint32_t* dtc) {
+  const uint32_t n = o.n;
+  GRID_STRIDE(q, cnt) {
+    const uint32_t i = list[q];
+    const uint32_t b = o.off[i];
+    uint32_t cur = n;
+    uint8_t s = ST_PENDING;
+    if (j > 1) {
+      const long long kp = o.path[b + j - 2];
+      const uint32_t g = kp == 0 ? NONE : tsindex_find(h, kp);
+      bool fast = g != NONE && g < i;
+      if (fast) {
+        // independent loads (no early exit) so they issue together
+        const uint32_t bg = o.off[g], eg = o.off[g + 1];
+        const uint8_t sg = w.st[g];
+        unsigned long long diff = 0;
+        for (uint32_t l = 0; l + 2 < j; ++l) diff |= static_cast<unsigned long long>(o.path[bg + l] ^ o.path[b + l]);
+        fast = eg - bg == j - 1 && sg == ST_APPLIED && diff == 0;
+      }
+      if (fast && dtc[g] < i) {
+        // the chain holds a node deleted before i: the descent stops at the
+        // topmost such Tombstone (AlreadyApplied); which one is only needed
+        // by the per-dict replay, which resolves TAG_LAZY from cur = g
+        w.st[i] = ST_ALREADY;
+        w.tag[i] = TAG_LAZY;
+        w.cur[i] = g;
+        continue;
+      }
+      if (fast) {
+        cur = g;
+      } else {  // the literal descent (k_lvl semantics, one level at a time)
+        for (uint32_t l = 1; l < j; ++l) {
+          const uint32_t tgt = lookup_child(o, w, h, cur, o.path[b + l - 1], l);
+          if (tgt == MISS_T || (tgt != SENT_T && tgt >= i)) {  // child missing -> InvalidPath
+            s = ST_INVALID;
+            break;
+          }
+          if (tgt == SENT_T) {  // descending into the sentinel Tombstone
+            s = ST_ALREADY;
+            break;
+          }
+          if (w.dtime[tgt] < i) {  // descending into a Tombstone
+            s = ST_ALREADY;
+            w.tag[i] = tgt;
+            break;
+          }
+          cur = tgt;
+        }
+      }
+    }
+    if (s != ST_PENDING) {
+      w.st[i] = s;
+      continue;
+    }
+    w.cur[i] = cur;
+    if (o.kind[i] == CRDTM_ADD) w.addpar[i] = cur;
+  }
+}
+
+// L2: leaf lookup; collisions (the closed form names a node by its ts alone);
+// the first Delete of a node that reaches it while its dict is live
+// (deleteHelp, src/Internal/Node.elm:112-122).
+__global__ void __launch_bounds__(BLOCK) k_lv_leaf(OpsDev o, Work w, TsIndex h, const uint32_t* list, uint32_t cnt,
+                                                   uint32_t j, DevResult* dres) {
+  GRID_STRIDE(q, cnt) {
+    const uint32_t i = list[q];
     if (w.st[i] != ST_PENDING) continue;
-    const uint32_t L = op_len(o, i);
-    if (L < lvl) continue;
-    const long long k = o.path[o.off[i] + lvl - 1];
-    const uint32_t tgt = lookup_child(o, w, h, w.cur[i], k, lvl);
-    if (L > lvl) {
-      // update: child k missing -> InvalidPath; found Tombstone (the sentinel) -> AlreadyApplied
-      if (tgt == MISS_T || (tgt != SENT_T && tgt >= i)) w.st[i] = ST_INVALID;
-      else if (tgt == SENT_T) w.st[i] = ST_ALREADY;
-      else w.nxt[i] = tgt;
+    const uint32_t cur = w.cur[i];
+    const uint32_t tgt = lookup_child(o, w, h, cur, o.path[o.off[i] + j - 1], j);
+    w.leaf[i] = tgt;
+    if (o.kind[i] == CRDTM_ADD) {
+      const long long ts = o.ts[i];
+      if (ts != 0) {
+        const uint32_t f = tsindex_find(h, ts);
+        if (f != i && (op_len(o, f) != j || w.addpar[f] != cur)) atomicOr(&dres->guard, G_COLLISION);
+      }
+    } else if (tgt == SENT_T) {
+      w.st[i] = ST_ALREADY;
+    } else if (tgt == MISS_T || tgt > i) {
+      w.st[i] = ST_NOTFOUND;
     } else {
-      w.leaf[i] = tgt;
+      atomicMin(&w.dtime[tgt], i);
     }
   }
 }
 
-// Deletes at this level: deleteHelp (src/Internal/Node.elm:112-122). The first
-// Delete of a node that reaches it while its dict is live tombstones it.
-__global__ void __launch_bounds__(BLOCK) k_lvl_del(OpsDev o, Work w, uint32_t lvl) {
-  GRID_STRIDE(i, o.n) {
-    if (o.kind[i] != CRDTM_DELETE || w.st[i] != ST_PENDING || op_len(o, i) != lvl) continue;
-    const uint32_t t = w.leaf[i];
-    if (t == SENT_T) w.st[i] = ST_ALREADY;
-    else if (t == MISS_T || t > i) w.st[i] = ST_NOTFOUND;
-    else atomicMin(&w.dtime[t], i);
-  }
-}
-
-__global__ void __launch_bounds__(BLOCK) k_lvl_fin(OpsDev o, Work w, TsIndex h, uint32_t lvl) {
+// L3: statuses of the ops that reached their dict; the chain death time of
+// each new node (its own first Delete, or an ancestor's).
+__global__ void __launch_bounds__(BLOCK) k_lv_fin(OpsDev o, Work w, TsIndex h, const uint32_t* list, uint32_t cnt,
+                                                  uint32_t* dtc) {
   const uint32_t n = o.n;
-  GRID_STRIDE(i, n) {
+  GRID_STRIDE(q, cnt) {
+    const uint32_t i = list[q];
     if (w.st[i] != ST_PENDING) continue;
-    const uint32_t L = op_len(o, i);
-    if (L > lvl) {
-      const uint32_t x = w.nxt[i];
-      if (w.dtime[x] < i) {
-        w.st[i] = ST_ALREADY;  // descending into a Tombstone
-        w.tag[i] = x;
-      } else {
-        w.cur[i] = x;
-      }
-    } else if (L == lvl) {
-      w.tag[i] = PDR_REACHED;
-      if (o.kind[i] == CRDTM_DELETE) {
-        w.st[i] = (w.dtime[w.leaf[i]] == i) ? ST_APPLIED : ST_ALREADY;
-      } else {
-        const long long ts = o.ts[i];
-        uint8_t s;
-        if (ts == 0) s = ST_ALREADY;                         // key 0 = the sentinel
-        else if (tsindex_find(h, ts) != i) s = ST_ALREADY;    // child ts parent exists
-        else {
-          const uint32_t a = w.leaf[i];
-          s = (a == SENT_T || (a != MISS_T && a < i)) ? ST_APPLIED : ST_NOTFOUND;
-        }
-        w.st[i] = s;
-        if (s == ST_APPLIED) {
-          const uint32_t p = w.addpar[i];
-          w.dead[i] = (w.dtime[i] != NONE || (p != n && w.dead[p])) ? 1 : 0;
-        }
-      }
+    w.tag[i] = PDR_REACHED;
+    if (o.kind[i] == CRDTM_DELETE) {
+      w.st[i] = (w.dtime[w.leaf[i]] == i) ? ST_APPLIED : ST_ALREADY;
+      continue;
+    }
+    const long long ts = o.ts[i];
+    uint8_t s;
+    if (ts == 0) s = ST_ALREADY;                         // key 0 = the sentinel
+    else if (tsindex_find(h, ts) != i) s = ST_ALREADY;    // child ts parent exists
+    else {
+      const uint32_t a = w.leaf[i];
+      s = (a == SENT_T || (a != MISS_T && a < i)) ? ST_APPLIED : ST_NOTFOUND;
+    }
+    w.st[i] = s;
+    if (s == ST_APPLIED) {
+      const uint32_t p = w.addpar[i];
+      const uint32_t dt = w.dtime[i];
+      w.dead[i] = (dt != NONE || (p != n && w.dead[p])) ? 1 : 0;
+      dtc[i] = p == n ? dt : min(dt, dtc[p]);
     }
   }
 }
@@ -484,9 +578,12 @@ __global__ void __launch_bounds__(BLOCK) k_guard_del(OpsDev o, Work w, DevResult
 // findInsertion (src/Internal/Node.elm:93-104) puts x after the subtree of its
 // effective parent ep(x) = first node on x's anchor chain with a smaller ts
 // (the dict's sentinel acts as -inf), among ep's children in descending ts.
-// Unified tree: node x -> x; sentinel of dict P -> n + P (root dict: 2n);
-// super root 2n + 1. A sentinel is the first child of its owner, so a node's
-// sub-document precedes its following siblings.
+// While jumping, the sentinel of dict P is the marker n + P (root dict: 2n).
+// Document tree (uids 0..n+1): node x -> x, root sentinel -> n, super root
+// -> n + 1. A node's children are first the roots of its own children dict
+// (group 0: its sub-document) and then its ep-children in its parent's dict
+// (group 1), each group in descending ts — the sentinel of a dict merged into
+// its owner.
 // ---------------------------------------------------------------------------
 
 __device__ __forceinline__ uint32_t sent_uid(uint32_t owner, uint32_t n) { return owner == n ? 2 * n : n + owner; }
@@ -516,22 +613,28 @@ __global__ void __launch_bounds__(BLOCK) k_ep_jump(OpsDev o, Work w, uint32_t* a
   }
 }
 
-__device__ __forceinline__ bool uni_present(const OpsDev& o, const Work& w, const uint8_t* sp, uint32_t v) {
+__device__ __forceinline__ bool doc_present(const OpsDev& o, const Work& w, const uint8_t* sp, uint32_t v) {
   const uint32_t n = o.n;
   if (v < n) return o.kind[v] == CRDTM_ADD && w.st[v] == ST_APPLIED;
-  if (v <= 2 * n) return sp[v - n] != 0;
-  return v == 2 * n + 1;
+  if (v == n) return sp[n] != 0;  // root sentinel: present when the root dict has nodes
+  return v == n + 1;
 }
 
-__device__ __forceinline__ uint32_t uni_up(const OpsDev& o, const uint32_t* anc, uint32_t v) {
+// parent uid of a present v != super root
+__device__ __forceinline__ uint32_t doc_up(const OpsDev& o, const uint32_t* anc, uint32_t v) {
   const uint32_t n = o.n;
-  if (v < n) return anc[v];
-  if (v < 2 * n) return v - n;
-  return 2 * n + 1;  // root sentinel -> super root
+  if (v == n) return n + 1;
+  const uint32_t a = anc[v];
+  if (a < n) return a;         // ep-child (group 1)
+  return a == 2 * n ? n : a - n;  // a root of dict P: child of P (group 0) / of the root sentinel
 }
 
-// Child counting and placement. The root dict's sentinel (uid 2n) can own a
-// large share of all nodes (every node whose anchor chain holds no smaller
+__device__ __forceinline__ bool doc_group1(const OpsDev& o, const uint32_t* anc, uint32_t v) {
+  return v < o.n && anc[v] < o.n;
+}
+
+// Child counting and placement. The root sentinel (uid n) can own a large
+// share of all nodes (every node whose anchor chain holds no smaller
 // timestamp), so its counter is aggregated per workgroup instead of taking
 // one same-address atomic per child.
 __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* total) {
@@ -550,16 +653,17 @@ __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* total) 
   return base + inc - v;
 }
 
+// sort key: group 0 before group 1, then descending ts (|ts| < 2^53)
 __global__ void __launch_bounds__(BLOCK) k_up_count(OpsDev o, Work w, const uint32_t* anc, const uint8_t* sp,
                                                     uint32_t* cnt, long long* skey) {
-  const uint32_t n = o.n, U = 2 * n + 1, H = 2 * n;  // super root excluded (no parent)
+  const uint32_t n = o.n, U = n + 1, H = n;  // super root excluded (no parent)
   uint32_t hot = 0;
   GRID_STRIDE(v, U) {
-    if (!uni_present(o, w, sp, v)) continue;
-    const uint32_t u = uni_up(o, anc, v);
+    if (!doc_present(o, w, sp, v)) continue;
+    const uint32_t u = doc_up(o, anc, v);
     if (u == H) ++hot;
     else atomicAdd(&cnt[u], 1u);
-    skey[v] = v < n ? -o.ts[v] : (long long)0x8000000000000000LL;
+    skey[v] = v < n ? (doc_group1(o, anc, v) ? (1LL << 60) : 0LL) + (TWO53 - o.ts[v]) : 0LL;
   }
   hot = block_sum(hot);
   if (threadIdx.x == 0 && hot) atomicAdd(&cnt[H], hot);
@@ -568,10 +672,10 @@ __global__ void __launch_bounds__(BLOCK) k_up_count(OpsDev o, Work w, const uint
 __global__ void __launch_bounds__(BLOCK) k_scatter(OpsDev o, Work w, const uint32_t* anc, const uint8_t* sp,
                                                    const uint32_t* start, uint32_t* fill, uint32_t* carr) {
   __shared__ uint32_t blk_base;
-  const uint32_t n = o.n, U = 2 * n + 1, H = 2 * n;
+  const uint32_t n = o.n, U = n + 1, H = n;
   uint32_t hot = 0;
   GRID_STRIDE(v, U) {
-    if (uni_present(o, w, sp, v) && uni_up(o, anc, v) == H) ++hot;
+    if (doc_present(o, w, sp, v) && doc_up(o, anc, v) == H) ++hot;
   }
   uint32_t tot;
   uint32_t mine = block_excl_sum(hot, &tot);
@@ -579,21 +683,24 @@ __global__ void __launch_bounds__(BLOCK) k_scatter(OpsDev o, Work w, const uint3
   __syncthreads();
   mine += blk_base + start[H];
   GRID_STRIDE(v, U) {
-    if (!uni_present(o, w, sp, v)) continue;
-    const uint32_t u = uni_up(o, anc, v);
+    if (!doc_present(o, w, sp, v)) continue;
+    const uint32_t u = doc_up(o, anc, v);
     if (u == H) carr[mine++] = v;
     else carr[start[u] + atomicAdd(&fill[u], 1u)] = v;
   }
 }
 
+// fc = first child, ns = next sibling, f1 = first ep-child (group 1)
 __global__ void __launch_bounds__(BLOCK) k_links(OpsDev o, const uint32_t* anc, const uint32_t* start,
                                                  const uint32_t* total, const uint32_t* carr, uint32_t* fc,
-                                                 uint32_t* ns) {
+                                                 uint32_t* ns, uint32_t* f1) {
   const uint32_t tot = *total;
   GRID_STRIDE(p, tot) {
     const uint32_t v = carr[p];
-    const uint32_t u = uni_up(o, anc, v);
-    if (p == start[u]) fc[u] = v;
+    const uint32_t u = doc_up(o, anc, v);
+    const bool first = p == start[u];
+    if (first) fc[u] = v;
+    if (doc_group1(o, anc, v) && (first || !doc_group1(o, anc, carr[p - 1]))) f1[u] = v;
     ns[v] = (p + 1 < start[u + 1]) ? carr[p + 1] : NONE;
   }
 }
@@ -603,17 +710,17 @@ __global__ void __launch_bounds__(BLOCK) k_links(OpsDev o, const uint32_t* anc, 
 // (pre-order rank), the low word counts visible nodes (document rank).
 __global__ void __launch_bounds__(BLOCK) k_euler(OpsDev o, Work w, const uint32_t* anc, const uint8_t* sp,
                                                  const uint32_t* fc, const uint32_t* ns, uint2* ent) {
-  const uint32_t n = o.n, U = 2 * n + 2;
+  const uint32_t n = o.n, U = n + 2;
   GRID_STRIDE(v, U) {
-    if (!uni_present(o, w, sp, v)) {
+    if (!doc_present(o, w, sp, v)) {
       ent[2 * v] = make_uint2(ABSENT, 0u);
       ent[2 * v + 1] = make_uint2(ABSENT, 0u);
       continue;
     }
     uint32_t after;
-    if (ns[v] != NONE) after = 2 * ns[v];
-    else if (v == 2 * n + 1) after = NONE;
-    else after = 2 * uni_up(o, anc, v) + 1;
+    if (v == n + 1) after = NONE;
+    else if (ns[v] != NONE) after = 2 * ns[v];
+    else after = 2 * doc_up(o, anc, v) + 1;
     uint32_t vis = 0;
     if (v < n) {
       const uint32_t p = w.addpar[v];
@@ -626,28 +733,28 @@ __global__ void __launch_bounds__(BLOCK) k_euler(OpsDev o, Work w, const uint32_
 
 __global__ void __launch_bounds__(BLOCK) k_order(OpsDev o, Work w, const uint8_t* sp,
                                                  const unsigned long long* excl, uint32_t* order) {
-  const uint32_t n = o.n, U = 2 * n + 2;
+  const uint32_t n = o.n, U = n + 2;
   GRID_STRIDE(v, U) {
-    if (!uni_present(o, w, sp, v)) continue;
+    if (!doc_present(o, w, sp, v)) continue;
     order[static_cast<uint32_t>(excl[2 * v] >> 32)] = v;
   }
 }
 
-// next(x) within its dict = the pre-order successor after x's own sub-document
-// when that node lives in the same dict (DESIGN.md "Raw next chains").
-__global__ void __launch_bounds__(BLOCK) k_next(OpsDev o, Work w, const uint8_t* sp, const unsigned long long* excl,
-                                                const uint32_t* order, uint32_t* nextn) {
+// next(x) within its dict (DESIGN.md "Raw next chains"): the first ep-child
+// of x, else the pre-order successor of x's whole subtree when that node
+// lives in the same dict.
+__global__ void __launch_bounds__(BLOCK) k_next(OpsDev o, Work w, const unsigned long long* excl,
+                                                const uint32_t* order, const uint32_t* f1, uint32_t* nextn) {
   const uint32_t n = o.n;
   // tour nodes = enter-weights before leave(super root)
-  const uint32_t total = static_cast<uint32_t>(excl[2 * (2 * n + 1) + 1] >> 32);
+  const uint32_t total = static_cast<uint32_t>(excl[2 * (n + 1) + 1] >> 32);
   GRID_STRIDE(x, n) {
     if (o.kind[x] != CRDTM_ADD || w.st[x] != ST_APPLIED) continue;
-    uint32_t j = static_cast<uint32_t>(excl[2 * x] >> 32) + 1;
-    if (sp[x]) {
-      const uint32_t s = n + x;
-      j += static_cast<uint32_t>(excl[2 * s + 1] >> 32) - static_cast<uint32_t>(excl[2 * s] >> 32);
+    uint32_t y = f1[x];
+    if (y == NONE) {
+      const uint32_t j = static_cast<uint32_t>(excl[2 * x + 1] >> 32);
+      y = j < total ? order[j] : NONE;
     }
-    uint32_t y = j < total ? order[j] : NONE;
     nextn[x] = (y < n && w.addpar[y] == w.addpar[x]) ? y : NONE;
   }
 }
@@ -703,8 +810,8 @@ __global__ void __launch_bounds__(BLOCK) k_commit_nodes(OpsDev o, Work w, TreeDe
       T.s_child[slot] = dd;
       T.s_key[ss] = 0;
       T.s_dict[ss] = dd;
-      const uint32_t f = fc[n + x];
-      T.s_next[ss] = f != NONE ? a.base_slot + kslot[f] : NONE;
+      const uint32_t f = fc[x];  // first root of x's own dict (group 0), if any
+      T.s_next[ss] = (f != NONE && w.addpar[f] == x) ? a.base_slot + kslot[f] : NONE;
       T.s_src[ss] = NONE;
       T.s_child[ss] = NONE;
       T.s_flags[ss] = F_TOMB | F_SENT;
@@ -718,24 +825,53 @@ __global__ void __launch_bounds__(BLOCK) k_commit_nodes(OpsDev o, Work w, TreeDe
 }
 
 __global__ void k_commit_root(OpsDev o, TreeDev T, const uint32_t* kslot, const uint32_t* fc, uint32_t base_slot) {
-  const uint32_t f = fc[2 * o.n];
+  const uint32_t f = fc[o.n];  // root sentinel's first child
   T.s_next[0] = f != NONE ? base_slot + kslot[f] : NONE;
 }
 
 // Append applied ops to the log (operations, src/CRDTree.elm:311).
+// One block per chunk of BLOCK ops: the op records first, then the chunk's
+// path elements (contiguous in the input) one per thread, each finding its op
+// by a binary search over the chunk's offsets in LDS (coalesced reads; writes
+// contiguous across applied ops).
 __global__ void __launch_bounds__(BLOCK) k_log(OpsDev o, const uint8_t* st, TreeDev T, uint32_t log_base,
                                                uint32_t lpath_base, const uint32_t* logidx, const uint32_t* lpoff) {
-  GRID_STRIDE(i, o.n) {
-    if (st[i] != ST_APPLIED) continue;
-    const uint32_t li = log_base + logidx[i];
-    const bool add = o.kind[i] == CRDTM_ADD;
-    T.l_kind[li] = o.kind[i];
-    T.l_ts[li] = add ? o.ts[i] : 0;
-    T.l_val[li] = add ? o.val[i] : 0;
-    const uint32_t b = lpath_base + lpoff[i];
-    T.l_off[li] = b;
-    const uint32_t s = o.off[i], L = o.off[i + 1] - s;
-    for (uint32_t j = 0; j < L; ++j) T.l_path[b + j] = o.path[s + j];
+  __shared__ uint32_t soff[BLOCK + 1];
+  __shared__ uint32_t sdst[BLOCK];
+  const uint32_t n = o.n;
+  const uint32_t chunks = (n + BLOCK - 1) / BLOCK;
+  for (uint32_t c = blockIdx.x; c < chunks; c += gridDim.x) {
+    const uint32_t i0 = c * BLOCK, cnt = min(static_cast<uint32_t>(BLOCK), n - i0);
+    const uint32_t t = threadIdx.x;
+    if (t < cnt) {
+      const uint32_t i = i0 + t;
+      soff[t] = o.off[i];
+      uint32_t dst = NONE;
+      if (st[i] == ST_APPLIED) {
+        const uint32_t li = log_base + logidx[i];
+        const bool add = o.kind[i] == CRDTM_ADD;
+        T.l_kind[li] = o.kind[i];
+        T.l_ts[li] = add ? o.ts[i] : 0;
+        T.l_val[li] = add ? o.val[i] : 0;
+        dst = lpath_base + lpoff[i];
+        T.l_off[li] = dst;
+      }
+      sdst[t] = dst;
+    }
+    if (t == 0) soff[cnt] = o.off[i0 + cnt];
+    __syncthreads();
+    const uint32_t p0 = soff[0], p1 = soff[cnt];
+    for (uint32_t p = p0 + t; p < p1; p += BLOCK) {
+      uint32_t lo = 0, hi = cnt;  // last op j with soff[j] <= p
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (soff[mid] <= p) lo = mid;
+        else hi = mid;
+      }
+      const uint32_t d = sdst[lo];
+      if (d != NONE) T.l_path[d + (p - soff[lo])] = o.path[p];
+    }
+    __syncthreads();
   }
 }
 
@@ -2272,7 +2408,6 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
     LAUNCH(k_index_insert, dim3(g), dim3(BLOCK), 0, s, o, ix);
   }
   w.cur = ws.alloc<uint32_t>(n);
-  w.nxt = ws.alloc<uint32_t>(n);
   w.leaf = ws.alloc<uint32_t>(n);
   w.addpar = ws.alloc<uint32_t>(n);
   w.dtime = ws.alloc<uint32_t>(n);
@@ -2285,12 +2420,38 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
     LAUNCH(k_flat_status, dim3(g), dim3(BLOCK), 0, s, o, w, ix, anc);
   } else {
     HIP_CHECK(hipMemsetAsync(w.maxadd, 0, (n + 1) * sizeof(uint32_t), s));
+    if (maxlen > MAXLV_BUCKET) {  // paths this deep are not bucketed: exact replay
+      r = run_replay(t, o, w.st, res, G_DEEP_PATH);
+      if (r == CRDTM_OK && st_out)
+        LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n,
+               res->err_index >= 0 ? static_cast<uint32_t>(res->err_index) : NONE, st_out);
+      return r;
+    }
+    // bucket the ops by |path| (one small copy back for the level sizes)
+    uint32_t* lcnt = ws.alloc<uint32_t>(2 * (MAXLV_BUCKET + 1));
+    uint32_t* lfill = lcnt + (MAXLV_BUCKET + 1);
+    uint32_t* lists = ws.alloc<uint32_t>(n);
+    uint32_t* dtc = ws.alloc<uint32_t>(n);
+    HIP_CHECK(hipMemsetAsync(lcnt, 0, 2 * (MAXLV_BUCKET + 1) * sizeof(uint32_t), s));
+    LAUNCH(k_len_count, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, s, o, maxlen, lcnt);
+    uint32_t hc[MAXLV_BUCKET + 1];
+    HIP_CHECK(hipMemcpyAsync(hc, lcnt, (maxlen + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    LevelStart hs{};
+    uint32_t acc = 0;
+    for (uint32_t j = 0; j <= maxlen; ++j) {
+      hs.v[j] = acc;
+      acc += hc[j];
+    }
+    LAUNCH(k_len_scatter, dim3(grid_for(n, BLOCK * 8, 2048)), dim3(BLOCK), 0, s, o, maxlen, hs, lfill, lists);
     for (uint32_t lvl = 1; lvl <= maxlen; ++lvl) {
-      LAUNCH(k_lvl_addpar, dim3(g), dim3(BLOCK), 0, s, o, w, lvl);
-      LAUNCH(k_lvl_collide, dim3(g), dim3(BLOCK), 0, s, o, w, ix, lvl, dr);
-      LAUNCH(k_lvl_resolve, dim3(g), dim3(BLOCK), 0, s, o, w, ix, lvl);
-      LAUNCH(k_lvl_del, dim3(g), dim3(BLOCK), 0, s, o, w, lvl);
-      LAUNCH(k_lvl_fin, dim3(g), dim3(BLOCK), 0, s, o, w, ix, lvl);
+      const uint32_t c = hc[lvl];
+      if (!c) continue;
+      const uint32_t* lst = lists + hs.v[lvl];
+      const uint32_t gl = grid_for(c);
+      LAUNCH(k_lv_dict, dim3(gl), dim3(BLOCK), 0, s, o, w, ix, lst, c, lvl, dtc);
+      LAUNCH(k_lv_leaf, dim3(gl), dim3(BLOCK), 0, s, o, w, ix, lst, c, lvl, dr);
+      LAUNCH(k_lv_fin, dim3(gl), dim3(BLOCK), 0, s, o, w, ix, lst, c, dtc);
     }
   }
   HIP_CHECK(hipMemsetAsync(&dr->first_del, 0xFF, sizeof(uint32_t), s));
@@ -2315,6 +2476,7 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
     pin.cur = w.cur;
     pin.leaf = w.leaf;
     pin.addpar = w.addpar;
+    pin.dtime = w.dtime;
     pin.maxlen = maxlen;
     bool handled = false;
     if ((r = pdr_apply(t, o, pin, w.st, res, &handled))) return r;
@@ -2347,8 +2509,8 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   res->n_applied = h1.n_applied;
   res->n_already = h1.n_already;
 
-  // ---- K2: effective parents, unified tree, sibling sort ----
-  const uint32_t U = 2 * n + 2;
+  // ---- K2: effective parents, document tree, sibling sort ----
+  const uint32_t U = n + 2;
   uint8_t* sp = ws.alloc<uint8_t>(n + 1);
   uint32_t* cnt = ws.alloc<uint32_t>(U + 1);
   uint32_t* fill = ws.alloc<uint32_t>(U + 1);
@@ -2356,11 +2518,13 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   uint32_t* carr = ws.alloc<uint32_t>(U);
   uint32_t* fc = ws.alloc<uint32_t>(U);
   uint32_t* ns = ws.alloc<uint32_t>(U);
+  uint32_t* f1 = ws.alloc<uint32_t>(U);
   HIP_CHECK(hipMemsetAsync(sp, 0, n + 1, s));
   HIP_CHECK(hipMemsetAsync(cnt, 0, (U + 1) * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(fill, 0, (U + 1) * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(fc, 0xFF, U * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(ns, 0xFF, U * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(f1, 0xFF, U * sizeof(uint32_t), s));
   if (!flat) LAUNCH(k_ep_init, dim3(g), dim3(BLOCK), 0, s, o, w, anc);
   LAUNCH(k_ep_jump, dim3(g), dim3(BLOCK), 0, s, o, w, anc, sp);
   const uint32_t gU = grid_for(U);
@@ -2369,18 +2533,18 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   if ((r = scan_excl_u32(cnt, cnt, U + 1, n_child_total, ws, s))) return r;
   LAUNCH(k_scatter, dim3(grid_for(U, BLOCK, 2048)), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, fill, carr);
   if ((r = segmented_sort(cnt, U, carr, U, skey, ws, s, dr))) return r;
-  LAUNCH(k_links, dim3(gU), dim3(BLOCK), 0, s, o, anc, cnt, n_child_total, carr, fc, ns);
+  LAUNCH(k_links, dim3(gU), dim3(BLOCK), 0, s, o, anc, cnt, n_child_total, carr, fc, ns, f1);
 
   // ---- K4: Euler tour + list ranking ----
   const uint64_t E = 2ULL * U;
   uint2* ent = ws.alloc<uint2>(E);
   unsigned long long* excl = ws.alloc<unsigned long long>(E);
   LAUNCH(k_euler, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, fc, ns, ent);
-  if ((r = list_rank(ent, E, 2 * (2 * n + 1), excl, ws, s))) return r;
+  if ((r = list_rank(ent, E, 2 * (n + 1), excl, ws, s))) return r;
   uint32_t* order = ws.alloc<uint32_t>(U);
   uint32_t* nextn = ws.alloc<uint32_t>(n);
   LAUNCH(k_order, dim3(gU), dim3(BLOCK), 0, s, o, w, sp, excl, order);
-  LAUNCH(k_next, dim3(g), dim3(BLOCK), 0, s, o, w, sp, excl, order, nextn);
+  LAUNCH(k_next, dim3(g), dim3(BLOCK), 0, s, o, w, excl, order, f1, nextn);
 
   // ---- K3 + commit ----
   uint32_t* appl = ws.alloc<uint32_t>(n + 1);

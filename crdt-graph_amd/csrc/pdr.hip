@@ -318,10 +318,20 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_tier(PdrCtx p, uint32_t i0, uint3
 }
 
 // ---- P3: conflicts ----
-__global__ void __launch_bounds__(BLOCK) k_pdr_conflict(uint32_t n, const uint32_t* tag, const uint32_t* tcopy,
-                                                        DevResult* dres) {
+// An op whose path stopped at a Tombstone that the copy quirk re-filled
+// before the op ran would have descended into the copy. K1 left the stop
+// node implicit (TAG_LAZY) on its fast path: it is the topmost node of the
+// chain ending at cur[i] deleted before i.
+__global__ void __launch_bounds__(BLOCK) k_pdr_conflict(uint32_t n, const uint32_t* tag, const uint32_t* cur,
+                                                        const uint32_t* addpar, const uint32_t* dtime,
+                                                        const uint32_t* tcopy, DevResult* dres) {
   GRID_STRIDE(i, n) {
-    const uint32_t x = tag[i];
+    uint32_t x = tag[i];
+    if (x == TAG_LAZY) {
+      x = NONE;
+      for (uint32_t y = cur[i]; y != n; y = addpar[y])
+        if (dtime[y] < i) x = y;
+    }
     if (x < n && tcopy[x] < i) atomicOr(&dres->pdr_conflict, 1u);  // rare
   }
 }
@@ -654,7 +664,8 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   // ---- P2 + P3 ----
   if ((r = pdr_run_tiers(c, p, 0, n + 1, true, st, tt, big_cap, hcount))) return r;
   LAUNCH(k_pdr_stats_reset, dim3(1), dim3(1), 0, s, dr);
-  LAUNCH(k_pdr_conflict, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, n, in.tag, p.tcopy, dr);
+  LAUNCH(k_pdr_conflict, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, n, in.tag, in.cur, in.addpar, in.dtime,
+         p.tcopy, dr);
   LAUNCH(k_pdr_stats, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, o, st, t->timestamp, dr);
   if ((r = sync_read(c))) return r;
   const DevResult h1 = *c->hres;
