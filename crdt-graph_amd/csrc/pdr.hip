@@ -166,6 +166,12 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_opw(uint32_t R0, const uint32_t* 
   }
 }
 
+// A slot word read by the whole wave (same address): moved to a scalar
+// register, so the walk's tests and branches are scalar instructions.
+__device__ __forceinline__ uint32_t ld_uniform(const uint32_t* S, uint32_t k) {
+  return __builtin_amdgcn_readfirstlane(S[k]);
+}
+
 // ---- P2: the serial replay of one dict (instance) on one wave ----
 // All lanes run the loop with identical values (wave-uniform control flow,
 // broadcast LDS reads); S points to LDS (or to the region for huge dicts).
@@ -199,32 +205,35 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
         const uint32_t t = wlo & PM;
         if (t == 0) {
           s = ST_ALREADY;
-        } else if (t == OW_NF || !(S[t] & SF_MADE)) {
-          s = ST_NOTFOUND;
-        } else if (S[t] & SF_TOMB) {
-          s = ST_ALREADY;
         } else {
-          S[t] |= SF_TOMB;
-          s = ST_APPLIED;
+          const uint32_t wt = t == OW_NF ? 0u : ld_uniform(S, t);
+          if (!(wt & SF_MADE)) {
+            s = ST_NOTFOUND;
+          } else if (wt & SF_TOMB) {
+            s = ST_ALREADY;
+          } else {
+            S[t] = wt | SF_TOMB;
+            s = ST_APPLIED;
+          }
         }
       } else {  // addAfterHelp
         const uint32_t x = wlo & PM;
         const uint32_t an = ((wlo >> 24) | (whi << 8)) & PM;
         if (x == 0) {
           s = ST_ALREADY;
-        } else if (an == OW_NF || !(S[an] & SF_MADE)) {
+        } else if (an == OW_NF || !(ld_uniform(S, an) & SF_MADE)) {
           s = ST_NOTFOUND;
         } else {
           uint32_t node = an, nk = an;  // findInsertion
-          uint32_t wn = S[node];
+          uint32_t wn = ld_uniform(S, node);
           for (;;) {
             const uint32_t rn = wn & PM;
             if (rn == PM) break;
-            uint32_t live = rn, wl = S[rn];
+            uint32_t live = rn, wl = ld_uniform(S, rn);
             while (wl & SF_TOMB) {
               live = wl & PM;
               if (live == PM) break;
-              wl = S[live];
+              wl = ld_uniform(S, live);
             }
             if (live == PM) break;
             if (x > rn) break;  // ts > key(rn)
@@ -232,7 +241,7 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
             node = live;
             wn = wl;
           }
-          const uint32_t wk = nk == node ? wn : S[nk];
+          const uint32_t wk = nk == node ? wn : ld_uniform(S, nk);
           S[x] = (wn & PM) | (wk & SF_ORPHAN) | SF_MADE;
           if (nk == node) {
             S[node] = (wn & ~PM) | x;
@@ -241,7 +250,7 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
             // nk up to node drop off the chain when nk was on it
             if (!(wk & SF_ORPHAN)) {
               for (uint32_t q = wk & PM; q != PM;) {
-                const uint32_t wq = S[q];
+                const uint32_t wq = ld_uniform(S, q);
                 S[q] = wq | SF_ORPHAN;
                 if (q == node) break;
                 q = wq & PM;

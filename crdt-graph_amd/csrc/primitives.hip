@@ -249,14 +249,35 @@ __global__ void __launch_bounds__(1024) k_sort_big(const uint32_t* __restrict__ 
   }
 }
 
-// Huge segments (> LDS_SORT_MAX): chunk-sort in LDS, then merge passes with
-// merge-path partitioning, every pass spread over many workgroups.
+// Huge segments (> LDS_SORT_MAX), all of them at once: a table of the huge
+// segments {begin, length, first chunk, first merge tile}; chunk-sort in LDS,
+// then merge passes with merge-path partitioning, one launch per width for
+// every segment (a segment already merged at this width is copied through).
+struct HugeTable {
+  uint32_t* b;     // segment begin
+  uint32_t* len;   // segment length
+  uint32_t* cpre;  // [nh + 1] exclusive prefix of LDS chunks
+  uint32_t* tpre;  // [nh + 1] exclusive prefix of merge tiles
+  uint32_t nh;
+};
+
+__device__ __forceinline__ uint32_t huge_find(const uint32_t* pre, uint32_t nh, uint32_t x) {
+  uint32_t lo = 0, hi = nh;  // last k with pre[k] <= x
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pre[mid] <= x) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
 template <class KEY>
-__global__ void __launch_bounds__(1024) k_sort_chunks(uint32_t* __restrict__ carr, uint32_t b, uint32_t len,
-                                                       KEY sort_key) {
+__global__ void __launch_bounds__(1024) k_sort_chunks(uint32_t* __restrict__ carr, HugeTable ht, KEY sort_key) {
   __shared__ long long skey[LDS_SORT_MAX];
   __shared__ uint32_t sid[LDS_SORT_MAX];
-  const uint32_t r0 = blockIdx.x * LDS_SORT_MAX;
+  const uint32_t seg = huge_find(ht.cpre, ht.nh, blockIdx.x);
+  const uint32_t b = ht.b[seg], len = ht.len[seg];
+  const uint32_t r0 = (blockIdx.x - ht.cpre[seg]) * LDS_SORT_MAX;
   const uint32_t rl = min(LDS_SORT_MAX, len - r0);
   for (uint32_t j = threadIdx.x; j < LDS_SORT_MAX; j += blockDim.x) {
     if (j < rl) {
@@ -295,10 +316,14 @@ constexpr uint32_t MERGE_PER_THREAD = 8;
 constexpr uint32_t MERGE_TILE = BLOCK * MERGE_PER_THREAD;  // 2048 outputs per workgroup
 
 template <class KEY>
-__global__ void __launch_bounds__(BLOCK) k_merge_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
-                                                      uint32_t len, uint32_t width,
+__global__ void __launch_bounds__(BLOCK) k_merge_pass(const uint32_t* __restrict__ src_base,
+                                                      uint32_t* __restrict__ dst_base, HugeTable ht, uint32_t width,
                                                       KEY sort_key) {
-  const uint32_t d0 = blockIdx.x * MERGE_TILE + threadIdx.x * MERGE_PER_THREAD;
+  const uint32_t seg = huge_find(ht.tpre, ht.nh, blockIdx.x);
+  const uint32_t len = ht.len[seg];
+  const uint32_t* __restrict__ src = src_base + ht.b[seg];
+  uint32_t* __restrict__ dst = dst_base + ht.b[seg];
+  const uint32_t d0 = (blockIdx.x - ht.tpre[seg]) * MERGE_TILE + threadIdx.x * MERGE_PER_THREAD;
   if (d0 >= len) return;
   const uint32_t pair = d0 / (2 * width);
   const uint32_t a0 = pair * 2 * width, a1 = min(a0 + width, len), b1 = min(a0 + 2 * width, len);
@@ -331,6 +356,67 @@ __global__ void k_sort_big_filter(const uint32_t* __restrict__ seg_start, const 
   }
 }
 
+// One workgroup: fill the huge table from the huge segment list and publish
+// {chunks, tiles, longest} for the host.
+__global__ void __launch_bounds__(BLOCK) k_huge_meta(const uint32_t* __restrict__ seg_start,
+                                                     const uint32_t* __restrict__ huge, HugeTable ht,
+                                                     uint32_t* __restrict__ out) {
+  __shared__ uint32_t sc[BLOCK / 64], stl[BLOCK / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t carry_c = 0, carry_t = 0, mx = 0;
+  for (uint32_t k0 = 0; k0 < ht.nh; k0 += BLOCK) {
+    const uint32_t k = k0 + threadIdx.x;
+    uint32_t c = 0, tl = 0;
+    if (k < ht.nh) {
+      const uint32_t u = huge[k];
+      const uint32_t b = seg_start[u], len = seg_start[u + 1] - b;
+      ht.b[k] = b;
+      ht.len[k] = len;
+      c = (len + LDS_SORT_MAX - 1) / LDS_SORT_MAX;
+      tl = (len + MERGE_TILE - 1) / MERGE_TILE;
+      mx = max(mx, len);
+    }
+    const uint32_t ic = wave_incl_scan(c), it = wave_incl_scan(tl);
+    if (lane == 63) {
+      sc[wave] = ic;
+      stl[wave] = it;
+    }
+    __syncthreads();
+    uint32_t pc = carry_c, pt = carry_t, tc = 0, tt = 0;
+    for (int w = 0; w < BLOCK / 64; ++w) {
+      if (w < wave) {
+        pc += sc[w];
+        pt += stl[w];
+      }
+      tc += sc[w];
+      tt += stl[w];
+    }
+    if (k < ht.nh) {
+      ht.cpre[k] = pc + ic - c;
+      ht.tpre[k] = pt + it - tl;
+    }
+    carry_c += tc;
+    carry_t += tt;
+    __syncthreads();
+  }
+  mx = block_max(mx);
+  if (threadIdx.x == 0) {
+    ht.cpre[ht.nh] = carry_c;
+    ht.tpre[ht.nh] = carry_t;
+    out[0] = carry_c;
+    out[1] = carry_t;
+    out[2] = mx;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_huge_copy(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                     HugeTable ht) {
+  const uint32_t seg = huge_find(ht.tpre, ht.nh, blockIdx.x);
+  const uint32_t b = ht.b[seg], len = ht.len[seg];
+  const uint32_t t0 = (blockIdx.x - ht.tpre[seg]) * MERGE_TILE;
+  for (uint32_t q = t0 + threadIdx.x; q < min(t0 + MERGE_TILE, len); q += BLOCK) dst[b + q] = src[b + q];
+}
+
 template <class KEY>
 static int segmented_sort_t(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items, KEY sort_key,
                             Arena& ws, hipStream_t st, DevResult* dres, uint32_t skip) {
@@ -357,23 +443,25 @@ static int segmented_sort_t(const uint32_t* seg_start, uint32_t n_seg, uint32_t*
                 "sort counters are contiguous");
   HIP_CHECK(hipMemsetAsync(nbig, 0, 3 * sizeof(uint32_t), st));
   if (nh == 0) return CRDTM_OK;
-  std::vector<uint32_t> hh(nh);
-  HIP_CHECK(hipMemcpy(hh.data(), huge, nh * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  for (uint32_t u : hh) {
-    uint32_t se[2];
-    HIP_CHECK(hipMemcpy(se, seg_start + u, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    const uint32_t b = se[0], len = se[1] - se[0];
-    LAUNCH(k_sort_chunks<KEY>, dim3((len + LDS_SORT_MAX - 1) / LDS_SORT_MAX), dim3(1024), 0, st, carr, b, len, sort_key);
-    uint32_t* src = carr + b;
-    uint32_t* dst = scratch + b;
-    for (uint32_t w = LDS_SORT_MAX; w < len; w <<= 1) {
-      LAUNCH(k_merge_pass<KEY>, dim3((len + MERGE_TILE - 1) / MERGE_TILE), dim3(BLOCK), 0, st, src, dst, len, w,
-             sort_key);
-      std::swap(src, dst);
-    }
-    if (src != carr + b)
-      HIP_CHECK(hipMemcpyAsync(carr + b, src, len * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+  HugeTable ht;
+  ht.nh = nh;
+  ht.b = ws.alloc<uint32_t>(nh);
+  ht.len = ws.alloc<uint32_t>(nh);
+  ht.cpre = ws.alloc<uint32_t>(nh + 1);
+  ht.tpre = ws.alloc<uint32_t>(nh + 1);
+  uint32_t* meta = ws.alloc<uint32_t>(4);
+  LAUNCH(k_huge_meta, dim3(1), dim3(BLOCK), 0, st, seg_start, huge, ht, meta);
+  uint32_t hm[3];
+  HIP_CHECK(hipMemcpyAsync(hm, meta, sizeof(hm), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  LAUNCH(k_sort_chunks<KEY>, dim3(hm[0]), dim3(1024), 0, st, carr, ht, sort_key);
+  uint32_t* src = carr;
+  uint32_t* dst = scratch;
+  for (uint32_t w = LDS_SORT_MAX; w < hm[2]; w <<= 1) {
+    LAUNCH(k_merge_pass<KEY>, dim3(hm[1]), dim3(BLOCK), 0, st, src, dst, ht, w, sort_key);
+    std::swap(src, dst);
   }
+  if (src != carr) LAUNCH(k_huge_copy, dim3(hm[1]), dim3(BLOCK), 0, st, src, carr, ht);
   return CRDTM_OK;
 }
 
