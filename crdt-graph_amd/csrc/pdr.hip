@@ -37,6 +37,8 @@
 // that created slot r; the slot words of rank r live at base[I] + r for each
 // instance I of D (the original, then its snapshots).
 
+#include <cstdlib>
+
 #include "engine.h"
 
 namespace crdtm {
@@ -71,8 +73,18 @@ struct PdrCtx {
   uint32_t* qcb;           // ... as of op index (NONE: current)
   uint32_t* ch;            // assembly: snapshot instance of a slot's children
   uint32_t* inst;          // per slot position: instance (NONE: unused room)
+  uint4* log;              // per original dict (4 entries per region position): slot writes in op order
+  uint32_t* logn;          // per dict: entries logged, NONE = no log (small dict or room exhausted)
+  uint32_t* ilog;          // per instance: snapshots rebuilt from the log -> prefix length, else NONE
+  uint32_t log_min;        // slots a dict needs to keep a change log
   PdrInst I;
 };
+
+// Change log of an original dict's replay: {op, slot | kind << 30, a, b};
+// kind 0: slot word := a; kind 1: copy payload (node carried a, children dict
+// b); kind 2: children as-of op a. A snapshot as of op b is the last write per
+// slot among the entries with op < b, found in parallel (k_pdr_snap_*).
+constexpr uint32_t PDR_LOG_MIN = 512;  // smaller dicts re-replay their snapshots (env CRDTM_PDR_LOG_MIN)
 
 __device__ __forceinline__ uint32_t pdr_kcount(const PdrCtx& p, uint32_t D) { return p.cbase[D + 1] - p.cbase[D]; }
 
@@ -187,6 +199,17 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
   __syncthreads();
   const uint32_t ob = rb, oe = p.rbase[D + 1] - 1;
   bool done = false;
+  // change log (original dicts big enough to be worth rebuilding snapshots from)
+  const bool logging = ORIG && p.log != nullptr && K + 1 >= p.log_min;
+  const uint32_t lcap = 4 * (oe + 1 - rb);
+  uint4* const lg = logging ? p.log + 4ULL * rb : nullptr;
+  uint32_t ln = 0;
+  auto logw = [&](uint32_t i, uint32_t k, uint32_t kind, uint32_t a, uint32_t b) {
+    if (logging) {
+      if (ln < lcap) lg[ln] = make_uint4(i, k | (kind << 30), a, b);  // uniform store (no divergence)
+      ++ln;
+    }
+  };
   for (uint32_t k0 = ob; k0 < oe && !done; k0 += 64) {
     const uint32_t kk = k0 + lane;
     const uint32_t my_i = kk < oe ? p.olist[kk] : NONE;
@@ -213,6 +236,7 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
             s = ST_ALREADY;
           } else {
             S[t] = wt | SF_TOMB;
+            logw(i, t, 0, wt | SF_TOMB, 0);
             s = ST_APPLIED;
           }
         }
@@ -243,8 +267,10 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
           }
           const uint32_t wk = nk == node ? wn : ld_uniform(S, nk);
           S[x] = (wn & PM) | (wk & SF_ORPHAN) | SF_MADE;
+          logw(i, x, 0, (wn & PM) | (wk & SF_ORPHAN) | SF_MADE, 0);
           if (nk == node) {
             S[node] = (wn & ~PM) | x;
+            logw(i, node, 0, (wn & ~PM) | x, 0);
           } else {
             // copy quirk: slot nk := copy of node, next = x; the entries after
             // nk up to node drop off the chain when nk was on it
@@ -252,12 +278,14 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
               for (uint32_t q = wk & PM; q != PM;) {
                 const uint32_t wq = ld_uniform(S, q);
                 S[q] = wq | SF_ORPHAN;
+                logw(i, q, 0, wq | SF_ORPHAN, 0);
                 if (q == node) break;
                 q = wq & PM;
               }
               wn |= SF_ORPHAN;
             }
             S[nk] = x | (wn & ~PM & ~SF_ORPHAN) | (wk & SF_ORPHAN) | SF_COPY;
+            logw(i, nk, 0, x | (wn & ~PM & ~SF_ORPHAN) | (wk & SF_ORPHAN) | SF_COPY, 0);
             uint32_t cs, cd, cb;
             if (wn & SF_COPY) {
               cs = p.qsrc[base + node];
@@ -270,14 +298,17 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
             p.qsrc[base + nk] = cs;
             p.qcd[base + nk] = cd;
             p.qcb[base + nk] = min(cb, i);
+            logw(i, nk, 1, cs, cd);
+            logw(i, nk, 2, min(cb, i), 0);
             if (ORIG && lane == 0) atomicMin(&p.tcopy[p.rop[rb + nk]], i);
           }
           s = ST_APPLIED;
         }
       }
-      if (ORIG && lane == 0) st[i] = s;
+      if (ORIG) st[i] = s;  // uniform store
     }
   }
+  if (ORIG && lane == 0) p.logn[D] = (logging && ln <= lcap) ? ln : NONE;
   __syncthreads();
   if (S != p.S + base) {
     for (uint32_t r = lane; r <= K; r += 64) p.S[base + r] = S[r];
@@ -316,8 +347,12 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_tier(PdrCtx p, uint32_t i0, uint3
   GRID_STRIDE(k, i1 - i0) {
     const uint32_t I = i0 + k;
     uint32_t D = I;
-    if (I > n) D = p.I.src[I];
-    else if (p.rbase[I + 1] == p.rbase[I]) continue;  // a dict no op reached
+    if (I > n) {
+      if (p.ilog[I] != NONE) continue;  // rebuilt from the source dict's change log
+      D = p.I.src[I];
+    } else if (p.rbase[I + 1] == p.rbase[I]) {
+      continue;  // a dict no op reached
+    }
     if (I <= n) p.I.base[I] = p.rbase[I];
     const uint32_t slots = pdr_kcount(p, D) + 1;
     const uint32_t t = slots <= PDR_SMALL ? 0u : (slots <= big_cap ? 1u : 2u);
@@ -466,6 +501,82 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_job_base(PdrCtx p, uint32_t j0, u
                                                         uint32_t s0) {
   const uint32_t n = p.o.n;
   GRID_STRIDE(k, j1 - j0) p.I.base[n + 1 + j0 + k] = s0 + off[k];
+}
+
+// Snapshots from change logs. plan: prefix length (entries with op < bound)
+// per job whose source dict kept a log; ecnt = that length (0 otherwise).
+__global__ void __launch_bounds__(BLOCK) k_pdr_snap_plan(PdrCtx p, uint32_t j0, uint32_t j1, uint32_t* ecnt) {
+  const uint32_t n = p.o.n;
+  GRID_STRIDE(k, j1 - j0 + 1) {
+    if (k == j1 - j0) {
+      ecnt[k] = 0;
+      continue;
+    }
+    const uint32_t J = n + 1 + j0 + k;
+    const uint32_t D = p.I.src[J], b = p.I.bound[J];
+    const uint32_t m = p.logn[D];
+    uint32_t e = 0;
+    if (m != NONE) {
+      const uint4* lg = p.log + 4ULL * p.rbase[D];
+      uint32_t lo = 0, hi = m;  // first entry with op >= bound
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (lg[mid].x < b) lo = mid + 1;
+        else hi = mid;
+      }
+      e = lo;
+      p.ilog[J] = lo;
+    } else {
+      p.ilog[J] = NONE;
+    }
+    ecnt[k] = e;
+  }
+}
+
+__device__ __forceinline__ uint32_t pdr_find(const uint32_t* pre, uint32_t cnt, uint32_t x) {
+  uint32_t lo = 0, hi = cnt;  // last k with pre[k] <= x
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pre[mid] <= x) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// last writer per (slot, kind) among each job's log prefix (entry index + 1)
+__global__ void __launch_bounds__(BLOCK) k_pdr_snap_apply(PdrCtx p, uint32_t j0, uint32_t nj, const uint32_t* epre,
+                                                          uint32_t etot, uint32_t* last) {
+  const uint32_t n = p.o.n;
+  GRID_STRIDE(x, etot) {
+    const uint32_t k = pdr_find(epre, nj, x);
+    const uint32_t J = n + 1 + j0 + k;
+    const uint32_t e = x - epre[k];
+    const uint4 en = p.log[4ULL * p.rbase[p.I.src[J]] + e];
+    const uint32_t kind = en.y >> 30, slot = en.y & 0x3FFFFFFFu;
+    atomicMax(&last[3ULL * (p.I.base[J] + slot) + kind], e + 1);
+  }
+}
+
+// slot positions [s0, s1) of this level's snapshot regions (joff: region
+// offsets relative to s0 per job)
+__global__ void __launch_bounds__(BLOCK) k_pdr_snap_fill(PdrCtx p, uint32_t j0, uint32_t nj, const uint32_t* joff,
+                                                         uint32_t s0, uint32_t s1, const uint32_t* last) {
+  const uint32_t n = p.o.n;
+  GRID_STRIDE(u, s1 - s0) {
+    const uint32_t k = pdr_find(joff, nj, u);
+    const uint32_t J = n + 1 + j0 + k;
+    if (p.ilog[J] == NONE) continue;  // replayed by the tiers
+    const uint32_t g = s0 + u, r = u - joff[k];
+    const uint4* lg = p.log + 4ULL * p.rbase[p.I.src[J]];
+    const uint32_t l0 = last[3ULL * g], l1 = last[3ULL * g + 1], l2 = last[3ULL * g + 2];
+    p.S[g] = l0 ? lg[l0 - 1].z : (r == 0 ? (PM | SF_TOMB | SF_MADE) : PM);
+    if (l1) {
+      p.qsrc[g] = lg[l1 - 1].z;
+      p.qcd[g] = lg[l1 - 1].w;
+    }
+    if (l2) p.qcb[g] = lg[l2 - 1].z;
+    p.inst[g] = J;
+  }
 }
 
 // instance order: root first, then originals 0..n-1, then snapshots
@@ -664,6 +775,14 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   p.I.bound = ws.alloc<uint32_t>(ICAP);
   p.I.pi = ws.alloc<uint32_t>(ICAP);
   p.I.pl = ws.alloc<uint32_t>(ICAP);
+  p.log = ws.alloc<uint4>(4ULL * R0);
+  p.log_min = PDR_LOG_MIN;
+  if (const char* e = getenv("CRDTM_PDR_LOG_MIN")) p.log_min = static_cast<uint32_t>(strtoul(e, nullptr, 10));
+  p.logn = ws.alloc<uint32_t>(n + 1);
+  p.ilog = ws.alloc<uint32_t>(ICAP);
+  uint32_t* last = ws.alloc<uint32_t>(3ULL * SCAP);
+  HIP_CHECK(hipMemsetAsync(last, 0, 3ULL * SCAP * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(p.ilog, 0xFF, ICAP * sizeof(uint32_t), s));
   PdrTiers tt;
   for (int k = 0; k < 3; ++k) tt.list[k] = ws.alloc<uint32_t>(ICAP);
   tt.count = ws.alloc<uint32_t>(4);
@@ -703,6 +822,7 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
     LAUNCH(k_pdr_alive_jump, dim3(grid_for(n + 1)), dim3(BLOCK), 0, s, n, ok, up);
   uint32_t s0 = 0, s1 = R0, j0 = 0;
   uint32_t* joff = ws.alloc<uint32_t>(JCAP + 1);
+  uint32_t* epre = ws.alloc<uint32_t>(JCAP + 1);
   for (uint32_t level = 0;; ++level) {
     LAUNCH(k_pdr_jobs, dim3(grid_for(s1 - s0)), dim3(BLOCK), 0, s, p, ok, s0, s1, JCAP, dr);
     if ((r = sync_read(c))) return r;
@@ -723,7 +843,16 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
       return CRDTM_OK;
     }
     LAUNCH(k_pdr_job_base, dim3(grid_for(j1 - j0)), dim3(BLOCK), 0, s, p, j0, j1, joff, s1);
+    // snapshots of logged dicts: rebuilt in parallel; the rest re-replay
+    LAUNCH(k_pdr_snap_plan, dim3(grid_for(j1 - j0 + 1)), dim3(BLOCK), 0, s, p, j0, j1, epre);
+    if ((r = scan_excl_u32(epre, epre, j1 - j0 + 1, &dr->pdr_dicts, ws, s))) return r;
     if ((r = pdr_run_tiers(c, p, n + 1 + j0, n + 1 + j1, false, st, tt, big_cap, hcount))) return r;
+    if ((r = sync_read(c))) return r;
+    const uint32_t etot = c->hres->pdr_dicts;
+    if (etot)
+      LAUNCH(k_pdr_snap_apply, dim3(grid_for(etot)), dim3(BLOCK), 0, s, p, j0, j1 - j0, epre, etot, last);
+    LAUNCH(k_pdr_snap_fill, dim3(grid_for(static_cast<uint32_t>(need - s1))), dim3(BLOCK), 0, s, p, j0, j1 - j0,
+           joff, s1, static_cast<uint32_t>(need), last);
     s0 = s1;
     s1 = static_cast<uint32_t>(need);
     j0 = j1;

@@ -111,6 +111,28 @@ def test_adversarial_streams(chunk):
     assert paths.get(N.PATH_DICT_REPLAY, 0) > 0, paths
 
 
+def test_snapshots_from_change_logs(monkeypatch):
+    """Copy-quirk snapshots rebuilt from every dict's change log (forced on
+    for all dict sizes) match the oracle like the re-replayed ones."""
+    from adversarial import adversarial
+    monkeypatch.setenv("CRDTM_PDR_LOG_MIN", "1")
+    for seed in range(0, 128, 3):
+        n = [40, 120, 400, 1500][seed % 4]
+        ops = adversarial(seed, n, replicas=2 + seed % 3, max_depth=1 + seed % 4)
+        arrs = pack(ops)
+        ot, rc, oerr = oracle_apply_arrays(arrs, n)
+        et = CRDTree.init(0)
+        res = et.apply_arrays(arrs, n)
+        assert res.code == rc, seed
+        if rc == 0:
+            assert engine_summary(et) == oracle_summary(ot), seed
+    s, n = synth_case(**CASES["cfg2_small"])
+    ot, rc, _ = oracle_apply_arrays(s, n)
+    et = CRDTree.init(0)
+    assert et.apply_arrays(s, n).code == rc == 0
+    assert engine_summary(et) == oracle_summary(ot)
+
+
 def test_operations_since_matches_oracle():
     """operationsSince through the device search (crdtm_tree_ops_since) against
     the oracle's newest-first walk (src/Internal/Operation.elm:25-53), incl. the
