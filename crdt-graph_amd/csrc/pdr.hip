@@ -264,6 +264,23 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
             nk = rn;
             node = live;
             wn = wl;
+            // Typing run: node, node+1, node+2, ... chained in rank order and
+            // all live. Every later comparison passes (x <= node < node+1 <
+            // ...), so the walk crosses the run in one step: lane l checks
+            // the link node+l -> node+l+1 (two contiguous LDS reads).
+            if (rn == live && (wn & PM) == node + 1) {
+              const uint32_t e = node + lane;
+              const bool in = e + 1 <= K;
+              const uint32_t a = in ? S[e] : 0u, b = in ? S[e + 1] : 0u;
+              const bool ok = in && (a & PM) == e + 1 && (b & SF_MADE) && !(b & SF_TOMB);
+              const unsigned long long bal = __ballot(ok);
+              const uint32_t m = bal == ~0ULL ? 64u : static_cast<uint32_t>(__builtin_ctzll(~bal));
+              if (m > 0) {
+                node += m;
+                nk = node;
+                wn = __builtin_amdgcn_readlane(b, m - 1);
+              }
+            }
           }
           const uint32_t wk = nk == node ? wn : ld_uniform(S, nk);
           S[x] = (wn & PM) | (wk & SF_ORPHAN) | SF_MADE;
