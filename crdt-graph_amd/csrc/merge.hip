@@ -29,6 +29,7 @@ struct Work {  // per-call device arrays of the closed form (sized by n ops)
   uint32_t* dtime;
   uint8_t* dead;
   uint32_t* maxadd;
+  uint4* nrec;    // per op, one line per lookup: {path begin, len | status << 16 | dead << 24, dict owner, chain death}
   uint32_t* tag;  // per op: PDR_REACHED, or the tombstoned node its path stopped at, or NONE (pdr.hip)
 };
 
@@ -206,6 +207,17 @@ __global__ void __launch_bounds__(BLOCK) k_work_init(OpsDev o, Work w) {
   }
 }
 
+// K1 node records (levels): written once per op here, then by its level
+__global__ void __launch_bounds__(BLOCK) k_nrec_init(OpsDev o, Work w) {
+  GRID_STRIDE(i, o.n) {
+    const uint32_t b = o.off[i], L = o.off[i + 1] - b;
+    w.nrec[i] = make_uint4(b, L | (static_cast<uint32_t>(ST_PENDING) << 16), NONE, NONE);
+  }
+}
+__device__ __forceinline__ uint32_t nrec_len(const uint4& r) { return r.y & 0xFFFFu; }
+__device__ __forceinline__ uint32_t nrec_st(const uint4& r) { return (r.y >> 16) & 0xFFu; }
+__device__ __forceinline__ bool nrec_dead(const uint4& r) { return (r.y >> 24) & 1u; }
+
 // Dense index layout: base[r] = exclusive scan of the range sizes over
 // replicas 0..max_replica, one workgroup (max_replica is read on the device,
 // so the host needs no copy of the ranges); the total goes to range_total.
@@ -332,13 +344,15 @@ __global__ void __launch_bounds__(BLOCK) k_flat_status(OpsDev o, Work w, TsIndex
 // [k1..k(j-1)] of op i names the node g = find(k(j-1)) exactly when g's own
 // parent path equals [k1..k(j-2)]: then i's ancestors are g's, and i reaches
 // g's children iff g was applied and no node of that chain was deleted before
-// i (dtc[g] = first Delete time over the chain). Anything else takes the
+// i (dtc = first Delete time over the chain, in the node record). Anything else takes the
 // literal walk, one lookup per level.
 __device__ __forceinline__ uint32_t lookup_child(const OpsDev& o, const Work& w, const TsIndex& h, uint32_t parent,
                                                  long long k, uint32_t lvl) {
   if (k == 0) return SENT_T;
   const uint32_t f = tsindex_find(h, k);
-  if (f == NONE || op_len(o, f) != lvl || w.addpar[f] != parent) return MISS_T;
+  if (f == NONE) return MISS_T;
+  const uint4 r = w.nrec[f];
+  if (nrec_len(r) != lvl || r.z != parent) return MISS_T;
   return f;
 }
 
@@ -395,7 +409,7 @@ __global__ void __launch_bounds__(BLOCK) k_len_scatter(OpsDev o, uint32_t maxlen
 
 // L1: the dict of every op of length j (fast prefix check, else the walk).
 __global__ void __launch_bounds__(BLOCK) k_lv_dict(OpsDev o, Work w, TsIndex h, const uint32_t* list, uint32_t cnt,
-                                                   uint32_t j, const uint32_t* dtc) {
+                                                   uint32_t j) {
   const uint32_t n = o.n;
   GRID_STRIDE(q, cnt) {
     const uint32_t i = list[q];
@@ -406,15 +420,17 @@ __global__ void __launch_bounds__(BLOCK) k_lv_dict(OpsDev o, Work w, TsIndex h, 
       const long long kp = o.path[b + j - 2];
       const uint32_t g = kp == 0 ? NONE : tsindex_find(h, kp);
       bool fast = g != NONE && g < i;
+      uint32_t dg = NONE;
       if (fast) {
+        const uint4 r = w.nrec[g];
+        const uint32_t bg = r.x;
+        dg = r.w;
         // independent loads (no early exit) so they issue together
-        const uint32_t bg = o.off[g], eg = o.off[g + 1];
-        const uint8_t sg = w.st[g];
         unsigned long long diff = 0;
         for (uint32_t l = 0; l + 2 < j; ++l) diff |= static_cast<unsigned long long>(o.path[bg + l] ^ o.path[b + l]);
-        fast = eg - bg == j - 1 && sg == ST_APPLIED && diff == 0;
+        fast = nrec_len(r) == j - 1 && nrec_st(r) == ST_APPLIED && diff == 0;
       }
-      if (fast && dtc[g] < i) {
+      if (fast && dg < i) {
         // the chain holds a node deleted before i: the descent stops at the
         // topmost such Tombstone (AlreadyApplied); which one is only needed
         // by the per-dict replay, which resolves TAG_LAZY from cur = g
@@ -450,7 +466,10 @@ __global__ void __launch_bounds__(BLOCK) k_lv_dict(OpsDev o, Work w, TsIndex h, 
       continue;
     }
     w.cur[i] = cur;
-    if (o.kind[i] == CRDTM_ADD) w.addpar[i] = cur;
+    if (o.kind[i] == CRDTM_ADD) {
+      w.addpar[i] = cur;
+      w.nrec[i].z = cur;
+    }
   }
 }
 
@@ -469,7 +488,10 @@ __global__ void __launch_bounds__(BLOCK) k_lv_leaf(OpsDev o, Work w, TsIndex h, 
       const long long ts = o.ts[i];
       if (ts != 0) {
         const uint32_t f = tsindex_find(h, ts);
-        if (f != i && (op_len(o, f) != j || w.addpar[f] != cur)) atomicOr(&dres->guard, G_COLLISION);
+        if (f != i) {
+          const uint4 r = w.nrec[f];
+          if (nrec_len(r) != j || r.z != cur) atomicOr(&dres->guard, G_COLLISION);
+        }
       }
     } else if (tgt == SENT_T) {
       w.st[i] = ST_ALREADY;
@@ -484,7 +506,7 @@ __global__ void __launch_bounds__(BLOCK) k_lv_leaf(OpsDev o, Work w, TsIndex h, 
 // L3: statuses of the ops that reached their dict; the chain death time of
 // each new node (its own first Delete, or an ancestor's).
 __global__ void __launch_bounds__(BLOCK) k_lv_fin(OpsDev o, Work w, TsIndex h, const uint32_t* list, uint32_t cnt,
-                                                  uint32_t* dtc) {
+                                                  uint32_t j) {
   const uint32_t n = o.n;
   GRID_STRIDE(q, cnt) {
     const uint32_t i = list[q];
@@ -503,12 +525,22 @@ __global__ void __launch_bounds__(BLOCK) k_lv_fin(OpsDev o, Work w, TsIndex h, c
       s = (a == SENT_T || (a != MISS_T && a < i)) ? ST_APPLIED : ST_NOTFOUND;
     }
     w.st[i] = s;
+    uint32_t dead = 0, dc = NONE;
     if (s == ST_APPLIED) {
       const uint32_t p = w.addpar[i];
       const uint32_t dt = w.dtime[i];
-      w.dead[i] = (dt != NONE || (p != n && w.dead[p])) ? 1 : 0;
-      dtc[i] = p == n ? dt : min(dt, dtc[p]);
+      if (p == n) {
+        dead = dt != NONE;
+        dc = dt;
+      } else {
+        const uint4 rp = w.nrec[p];
+        dead = (dt != NONE || nrec_dead(rp)) ? 1u : 0u;
+        dc = min(dt, rp.w);
+      }
+      w.dead[i] = static_cast<uint8_t>(dead);
     }
+    w.nrec[i].y = j | (static_cast<uint32_t>(s) << 16) | (dead << 24);
+    w.nrec[i].w = dc;
   }
 }
 
@@ -2431,7 +2463,8 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
     uint32_t* lcnt = ws.alloc<uint32_t>(2 * (MAXLV_BUCKET + 1));
     uint32_t* lfill = lcnt + (MAXLV_BUCKET + 1);
     uint32_t* lists = ws.alloc<uint32_t>(n);
-    uint32_t* dtc = ws.alloc<uint32_t>(n);
+    w.nrec = ws.alloc<uint4>(n);
+    LAUNCH(k_nrec_init, dim3(g), dim3(BLOCK), 0, s, o, w);
     HIP_CHECK(hipMemsetAsync(lcnt, 0, 2 * (MAXLV_BUCKET + 1) * sizeof(uint32_t), s));
     LAUNCH(k_len_count, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, s, o, maxlen, lcnt);
     uint32_t hc[MAXLV_BUCKET + 1];
@@ -2449,9 +2482,9 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
       if (!c) continue;
       const uint32_t* lst = lists + hs.v[lvl];
       const uint32_t gl = grid_for(c);
-      LAUNCH(k_lv_dict, dim3(gl), dim3(BLOCK), 0, s, o, w, ix, lst, c, lvl, dtc);
+      LAUNCH(k_lv_dict, dim3(gl), dim3(BLOCK), 0, s, o, w, ix, lst, c, lvl);
       LAUNCH(k_lv_leaf, dim3(gl), dim3(BLOCK), 0, s, o, w, ix, lst, c, lvl, dr);
-      LAUNCH(k_lv_fin, dim3(gl), dim3(BLOCK), 0, s, o, w, ix, lst, c, dtc);
+      LAUNCH(k_lv_fin, dim3(gl), dim3(BLOCK), 0, s, o, w, ix, lst, c, lvl);
     }
   }
   HIP_CHECK(hipMemsetAsync(&dr->first_del, 0xFF, sizeof(uint32_t), s));
