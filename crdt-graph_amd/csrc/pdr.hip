@@ -210,10 +210,16 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
       ++ln;
     }
   };
+  // op words stream through registers 64 at a time; the next chunk is loaded
+  // while this one replays (the loads do not depend on the slot state)
+  uint32_t nx_i = ob + lane < oe ? p.olist[ob + lane] : NONE;
+  unsigned long long nx_w = ob + lane < oe ? p.opw[ob + lane] : 0ULL;
   for (uint32_t k0 = ob; k0 < oe && !done; k0 += 64) {
-    const uint32_t kk = k0 + lane;
-    const uint32_t my_i = kk < oe ? p.olist[kk] : NONE;
-    const unsigned long long my_w = kk < oe ? p.opw[kk] : 0ULL;
+    const uint32_t my_i = nx_i;
+    const unsigned long long my_w = nx_w;
+    const uint32_t kn = k0 + 64 + lane;
+    nx_i = kn < oe ? p.olist[kn] : NONE;
+    nx_w = kn < oe ? p.opw[kn] : 0ULL;
     const uint32_t cnt = min(64u, oe - k0);
     for (uint32_t j = 0; j < cnt; ++j) {
       const uint32_t i = __builtin_amdgcn_readlane(my_i, j);
