@@ -16,6 +16,9 @@ CRDTM_OK = 0
 PATH_CLOSED_FORM = 1
 PATH_REPLAY = 2
 PATH_DICT_REPLAY = 3
+REF_NONE = 2 ** 64 - 1
+REF_ROOT = 2 ** 64 - 2
+REL_PARENT, REL_NEXT, REL_PREV, REL_HEAD = 0, 1, 2, 3
 CODES = {0: "Ok", 1: "InvalidPath", 2: "NotFound", 3: "OperationFailed", -1: "E_ARG", -2: "E_HIP", -3: "E_NOMEM",
          -4: "E_RANGE", -5: "E_NODEVICE", -6: "E_PARSE"}
 
@@ -56,6 +59,12 @@ SIGNATURES = [
     ("crdtm_tree_replicas", C.c_int, [P, P, P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("crdtm_tree_ops", C.c_int, [P, C.c_int, C.POINTER(Ops), C.POINTER(C.c_int)]),
     ("crdtm_tree_ops_since", C.c_int, [P, C.c_int64, C.POINTER(Ops)]),
+    ("crdtm_tree_get", C.c_int, [P, P, C.c_uint64, C.POINTER(C.c_uint64)]),
+    ("crdtm_node_info", C.c_int, [P, C.c_uint64, C.POINTER(C.c_int32), C.POINTER(C.c_uint32), C.POINTER(C.c_int32),
+                                  C.POINTER(C.c_int64), P, C.c_uint64, C.POINTER(C.c_uint64)]),
+    ("crdtm_tree_relative", C.c_int, [P, C.c_uint64, C.c_int, C.POINTER(C.c_uint64)]),
+    ("crdtm_node_children", C.c_int, [P, C.c_uint64, P, C.c_uint64, C.POINTER(C.c_uint64)]),
+    ("crdtm_tree_walk", C.c_int, [P, C.c_uint64, P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("crdtm_tree_canonical", C.c_int, [P, C.c_int, P, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("crdtm_tree_document", C.c_int, [P, P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("crdtm_forest_apply", C.c_int, [P, C.c_int64, C.POINTER(Ops), P, C.c_uint64, C.c_int, P, P, P, P, P, P]),

@@ -72,6 +72,20 @@ class Values:
 VALUES = Values()
 
 
+
+class NodeView:
+    """A node of CRDTree a as the reference exposes it (src/Internal/Node.elm:29-32)."""
+    __slots__ = ("ref", "kind", "value", "path", "next")
+
+    def __init__(self, ref, kind, value, path, next_):
+        self.ref, self.kind, self.value, self.path, self.next = ref, kind, value, path, next_
+
+    def key(self):
+        return (self.kind, self.value, tuple(self.path), self.next)
+
+    def __repr__(self):
+        return f"NodeView({self.kind}, {self.value!r}, {self.path}, next={self.next})"
+
 def pack(leaves, values=VALUES):
     """Flattened Add/Delete leaves -> SoA numpy arrays (crdtm_ops layout)."""
     n = len(leaves)
@@ -267,6 +281,86 @@ class CRDTree:
         """CRDTree.operationsSince (src/CRDTree.elm:408-418): inclusive of the
         newest logged Add with that ts, [] when absent (crdtm_tree_ops_since)."""
         return Batch(self._ops(0, since=ts)[0])
+
+    # ---- traversal (src/CRDTree.elm:421-625, src/CRDTree/Node.elm:96-174) ----
+    # Nodes are returned as NodeView(ref, kind, value, path, next); refs stay
+    # valid until the next apply.
+    def _view(self, ref):
+        if ref == N.REF_NONE:
+            return None
+        kind = C.c_int32()
+        val = C.c_uint32()
+        hn = C.c_int32()
+        nx = C.c_int64()
+        pl = C.c_uint64()
+        buf = np.zeros(64, np.int64)
+        N.check(N.lib().crdtm_node_info(self._h, ref, C.byref(kind), C.byref(val), C.byref(hn), C.byref(nx),
+                                        _ptr(buf), 64, C.byref(pl)), "crdtm_node_info")
+        if pl.value > 64:
+            buf = np.zeros(pl.value, np.int64)
+            N.check(N.lib().crdtm_node_info(self._h, ref, None, None, None, None, _ptr(buf), pl.value, C.byref(pl)))
+        k = {1: "node", 2: "tombstone", 3: "root"}[kind.value]
+        return NodeView(ref, k, VALUES.value(val.value) if k == "node" else None,
+                        [int(x) for x in buf[:pl.value]], int(nx.value) if hn.value else None)
+
+    def get(self, path):
+        """CRDTree.get (src/CRDTree.elm:468-470): the Node / Tombstone at path, or None."""
+        ref = C.c_uint64()
+        p = np.array(list(path) or [0], np.int64)
+        N.check(N.lib().crdtm_tree_get(self._h, _ptr(p), len(path), C.byref(ref)), "crdtm_tree_get")
+        return self._view(ref.value)
+
+    def get_value(self, path):
+        """CRDTree.getValue (src/CRDTree.elm:486-488)."""
+        v = self.get(path)
+        return v.value if v is not None and v.kind == "node" else None
+
+    def root(self):
+        return self._view(N.REF_ROOT)
+
+    def _rel(self, node, which):
+        out = C.c_uint64()
+        N.check(N.lib().crdtm_tree_relative(self._h, node.ref, which, C.byref(out)), "crdtm_tree_relative")
+        return self._view(out.value)
+
+    def parent(self, node):
+        """CRDTree.parent (src/CRDTree.elm:425-441)."""
+        return self._rel(node, N.REL_PARENT)
+
+    def next(self, node):
+        """CRDTree.next (src/CRDTree.elm:560-566)."""
+        return self._rel(node, N.REL_NEXT)
+
+    def prev(self, node):
+        """CRDTree.prev (src/CRDTree.elm:569-575)."""
+        return self._rel(node, N.REL_PREV)
+
+    def head(self, node):
+        """CRDTree.Node.head (src/CRDTree/Node.elm:165-167)."""
+        return self._rel(node, N.REL_HEAD)
+
+    def _refs(self, fn, ref):
+        n = C.c_uint64()
+        N.check(fn(self._h, ref, None, 0, C.byref(n)))
+        buf = np.zeros(max(n.value, 1), np.uint64)
+        N.check(fn(self._h, ref, _ptr(buf), n.value, C.byref(n)))
+        return [self._view(int(r)) for r in buf[:n.value]]
+
+    def children(self, node):
+        """CRDTree.Node.children (src/CRDTree/Node.elm:96-98): live children in order."""
+        return self._refs(N.lib().crdtm_node_children, node.ref)
+
+    def walk(self, func, acc, start=None):
+        """CRDTree.walk (src/CRDTree.elm:583-625): func(node, acc) -> ("take", acc) | ("done", acc)."""
+        for node in self._refs(N.lib().crdtm_tree_walk, N.REF_NONE if start is None else start.ref):
+            step, acc = func(node, acc)
+            if step == "done":
+                return acc
+        return acc
+
+    def walk_nodes(self, start=None):
+        """The visit order of walk when func always Takes."""
+        return self._refs(N.lib().crdtm_tree_walk, N.REF_NONE if start is None else start.ref)
 
     def canonical(self, which=0, full=True):
         n = C.c_uint64()

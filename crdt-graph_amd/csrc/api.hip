@@ -2,6 +2,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <unordered_map>
 
 #include "engine.h"
 
@@ -285,6 +286,7 @@ int crdtm_tree_reset(crdtm_tree* t, int64_t replica_id) {
   t->replicas.clear();
   t->last_begin = t->last_end = 0;
   t->last_is_batch = 1;
+  ++t->version;
   return CRDTM_OK;
 }
 
@@ -339,6 +341,7 @@ int crdtm_tree_clone(const crdtm_tree* t, crdtm_tree** out) {
 int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_batch, uint8_t* status_out,
                 crdtm_result* res) {
   if (!t || !ops || !res) return CRDTM_E_ARG;
+  ++t->version;
   std::memset(res, 0, sizeof(*res));
   res->err_index = -1;
   if (!is_batch && ops->n_ops != 1) return CRDTM_E_ARG;
@@ -620,5 +623,260 @@ int crdtm_forest_apply(crdtm_ctx* c, int64_t replica_id, const crdtm_ops* ops, c
 }
 
 void crdtm_free(void* p) { std::free(p); }
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Traversal API (src/CRDTree.elm:421-625, src/CRDTree/Node.elm:96-174), served
+// from a host copy of the device state fetched once per tree version. Node
+// references: a slot index of the current state, CRDTM_REF_ROOT, or the
+// implicit sentinel of a live node's still-empty children dict
+// (CRDTM_REF_VSENT | slot). References stay valid until the next apply.
+// Semantics follow the reference literally: a node's parent is found from its
+// *path* (a dict sentinel's path is [] so its parent is the root), `next`
+// follows next *keys* in that parent's children skipping Tombstones, `prev`
+// scans the parent's chain from its sentinel (Tombstones included), `walk`
+// starts after its start node and after the head of every node it descends
+// into.
+// ---------------------------------------------------------------------------
+namespace {
+
+struct PairHash {
+  size_t operator()(const std::pair<uint32_t, long long>& p) const {
+    return std::hash<long long>()(p.second * 0x9E3779B97F4A7C15LL ^ static_cast<long long>(p.first));
+  }
+};
+
+struct TravCache {
+  uint64_t version = ~0ULL;
+  HostTree h;
+  std::unordered_map<std::pair<uint32_t, long long>, uint32_t, PairHash> index;  // (dict, key) -> slot
+};
+
+constexpr uint64_t REF_NONE = CRDTM_REF_NONE, REF_ROOT = CRDTM_REF_ROOT, REF_VSENT = CRDTM_REF_VSENT;
+
+int trav_cache(const crdtm_tree* tc, TravCache*& out) {
+  auto* t = const_cast<crdtm_tree*>(tc);
+  auto* c = static_cast<TravCache*>(t->trav.get());
+  if (!c) {
+    t->trav = std::make_shared<TravCache>();
+    c = static_cast<TravCache*>(t->trav.get());
+  }
+  if (c->version != t->version) {
+    c->h = HostTree();
+    int r = fetch(t, c->h, false);
+    if (r) return r;
+    c->index.clear();
+    c->index.reserve(c->h.key.size() * 2);
+    for (uint32_t sl = 0; sl < c->h.key.size(); ++sl) c->index[{c->h.dict[sl], c->h.key[sl]}] = sl;
+    c->version = t->version;
+  }
+  out = c;
+  return CRDTM_OK;
+}
+
+bool ref_ok(const TravCache& c, uint64_t r) {
+  if (r == REF_ROOT) return true;
+  if (r & REF_VSENT) {
+    const uint64_t s = r & ~REF_VSENT;
+    return s < c.h.key.size() && !(c.h.flags[s] & F_TOMB) && c.h.child[s] == NONE;
+  }
+  return r < c.h.key.size();
+}
+
+bool is_tomb(const TravCache& c, uint64_t r) { return r != REF_ROOT && ((r & REF_VSENT) || (c.h.flags[r] & F_TOMB)); }
+
+// children dict of a node: kind 0 = empty (Tombstone), 1 = dict id, 2 = implicit {0: sentinel} of owner slot
+struct DictRef {
+  int kind;
+  uint64_t v;
+};
+
+DictRef children_of(const TravCache& c, uint64_t r) {
+  if (r == REF_ROOT) return {1, 0};
+  if (is_tomb(c, r)) return {0, 0};
+  const uint32_t ch = c.h.child[r];
+  return ch == NONE ? DictRef{2, r} : DictRef{1, ch};
+}
+
+uint64_t lookup(const TravCache& c, const DictRef& d, long long key) {
+  if (d.kind == 0) return REF_NONE;
+  if (d.kind == 2) return key == 0 ? (REF_VSENT | d.v) : REF_NONE;
+  auto it = c.index.find({static_cast<uint32_t>(d.v), key});
+  return it == c.index.end() ? REF_NONE : it->second;
+}
+
+bool next_key(const TravCache& c, uint64_t r, long long* k) {
+  if (r == REF_ROOT || (r & REF_VSENT)) return false;
+  const uint32_t nx = c.h.next[r];
+  if (nx == NONE) return false;
+  *k = c.h.key[nx];
+  return true;
+}
+
+void node_path(const TravCache& c, uint64_t r, std::vector<long long>& p) {
+  p.clear();
+  if (r == REF_ROOT || (r & REF_VSENT)) return;
+  const uint32_t src = c.h.src[r];
+  if (src == NONE) return;  // a sentinel: Tombstone [] _
+  const uint32_t b = c.h.l_off[src], e = c.h.l_off[src + 1];
+  for (uint32_t j = b; j + 1 < e; ++j) p.push_back(c.h.l_path[j]);
+  p.push_back(c.h.l_ts[src]);
+}
+
+// nextNode (src/Internal/Node.elm:257-268) in dict d
+uint64_t next_node(const TravCache& c, uint64_t r, const DictRef& d) {
+  long long k;
+  for (uint64_t x = r;;) {
+    if (!next_key(c, x, &k)) return REF_NONE;
+    x = lookup(c, d, k);
+    if (x == REF_NONE) return REF_NONE;
+    if (!is_tomb(c, x)) return x;
+  }
+}
+
+uint64_t descend(const TravCache& c, const int64_t* p, uint64_t n) {  // Node.descendant (src/Internal/Node.elm:289-299)
+  if (n == 0) return REF_NONE;
+  uint64_t r = REF_ROOT;
+  for (uint64_t j = 0; j < n && r != REF_NONE; ++j) r = lookup(c, children_of(c, r), p[j]);
+  return r;
+}
+
+uint64_t parent_of(const TravCache& c, uint64_t r) {  // src/CRDTree.elm:425-441
+  std::vector<long long> p;
+  node_path(c, r, p);
+  if (!p.empty()) p.pop_back();
+  if (p.empty()) return REF_ROOT;
+  return descend(c, reinterpret_cast<const int64_t*>(p.data()), p.size());
+}
+
+uint64_t next_of(const TravCache& c, uint64_t r) {  // src/CRDTree.elm:560-566
+  const uint64_t par = parent_of(c, r);
+  if (par == REF_NONE) return REF_NONE;
+  return next_node(c, r, children_of(c, par));
+}
+
+uint64_t prev_of(const TravCache& c, uint64_t r) {  // src/CRDTree.elm:569-575 (Node.find, identity for ==)
+  const uint64_t par = parent_of(c, r);
+  if (par == REF_NONE) return REF_NONE;
+  const DictRef d = children_of(c, par);
+  uint64_t left = lookup(c, d, 0);
+  long long k;
+  while (left != REF_NONE && next_key(c, left, &k)) {
+    const uint64_t x = lookup(c, d, k);
+    if (x == REF_NONE) return REF_NONE;
+    if (next_of(c, x) == r) return x;
+    left = x;
+  }
+  return REF_NONE;
+}
+
+uint64_t head_of(const TravCache& c, uint64_t r) {  // src/CRDTree/Node.elm:165-167
+  const DictRef d = children_of(c, r);
+  const uint64_t s0 = lookup(c, d, 0);
+  return s0 == REF_NONE ? REF_NONE : next_node(c, s0, d);
+}
+
+// walkHelp (src/CRDTree.elm:602-625) with a function that always Takes; an
+// explicit stack instead of recursion (documents nest arbitrarily deep)
+void walk_from(const TravCache& c, uint64_t left, const DictRef& sib, std::vector<uint64_t>& out) {
+  std::vector<std::pair<uint64_t, DictRef>> st{{left, sib}};
+  while (!st.empty()) {
+    auto [l, d] = st.back();
+    st.pop_back();
+    const uint64_t node = next_node(c, l, d);
+    if (node == REF_NONE) continue;
+    out.push_back(node);
+    st.push_back({node, d});  // then the siblings after node
+    const uint64_t h = head_of(c, node);
+    if (h != REF_NONE) st.push_back({h, children_of(c, node)});  // first: node's children after its head
+  }
+}
+
+int put_refs(const std::vector<uint64_t>& v, uint64_t* out, uint64_t cap, uint64_t* n) {
+  for (uint64_t k = 0; out && k < v.size() && k < cap; ++k) out[k] = v[k];
+  if (n) *n = v.size();
+  return CRDTM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int crdtm_tree_get(const crdtm_tree* t, const int64_t* path, uint64_t len, uint64_t* ref) {
+  if (!t || !ref || (len && !path)) return CRDTM_E_ARG;
+  TravCache* c;
+  int r = trav_cache(t, c);
+  if (r) return r;
+  *ref = descend(*c, path, len);
+  return CRDTM_OK;
+}
+
+int crdtm_node_info(const crdtm_tree* t, uint64_t ref, int32_t* kind, uint32_t* val, int32_t* has_next,
+                    int64_t* next, int64_t* path, uint64_t cap, uint64_t* path_len) {
+  if (!t) return CRDTM_E_ARG;
+  TravCache* c;
+  int r = trav_cache(t, c);
+  if (r) return r;
+  if (!ref_ok(*c, ref)) return CRDTM_E_ARG;
+  const bool tomb = is_tomb(*c, ref);
+  if (kind) *kind = ref == REF_ROOT ? 3 : (tomb ? 2 : 1);
+  if (val) *val = (ref == REF_ROOT || tomb) ? 0u : c->h.l_val[c->h.src[ref]];
+  long long k = 0;
+  const bool hn = next_key(*c, ref, &k);
+  if (has_next) *has_next = hn ? 1 : 0;
+  if (next) *next = hn ? k : 0;
+  std::vector<long long> p;
+  node_path(*c, ref, p);
+  for (uint64_t j = 0; path && j < p.size() && j < cap; ++j) path[j] = p[j];
+  if (path_len) *path_len = p.size();
+  return CRDTM_OK;
+}
+
+int crdtm_tree_relative(const crdtm_tree* t, uint64_t ref, int which, uint64_t* out) {
+  if (!t || !out) return CRDTM_E_ARG;
+  TravCache* c;
+  int r = trav_cache(t, c);
+  if (r) return r;
+  if (!ref_ok(*c, ref)) return CRDTM_E_ARG;
+  switch (which) {
+    case CRDTM_REL_PARENT: *out = parent_of(*c, ref); break;
+    case CRDTM_REL_NEXT: *out = next_of(*c, ref); break;
+    case CRDTM_REL_PREV: *out = prev_of(*c, ref); break;
+    case CRDTM_REL_HEAD: *out = head_of(*c, ref); break;
+    default: return CRDTM_E_ARG;
+  }
+  return CRDTM_OK;
+}
+
+int crdtm_node_children(const crdtm_tree* t, uint64_t ref, uint64_t* out, uint64_t cap, uint64_t* n) {
+  if (!t) return CRDTM_E_ARG;
+  TravCache* c;
+  int r = trav_cache(t, c);
+  if (r) return r;
+  if (!ref_ok(*c, ref)) return CRDTM_E_ARG;
+  std::vector<uint64_t> v;
+  const DictRef d = children_of(*c, ref);
+  const uint64_t s0 = lookup(*c, d, 0);
+  for (uint64_t x = s0 == REF_NONE ? REF_NONE : next_node(*c, s0, d); x != REF_NONE; x = next_node(*c, x, d))
+    v.push_back(x);
+  return put_refs(v, out, cap, n);
+}
+
+int crdtm_tree_walk(const crdtm_tree* t, uint64_t start, uint64_t* out, uint64_t cap, uint64_t* n) {
+  if (!t) return CRDTM_E_ARG;
+  TravCache* c;
+  int r = trav_cache(t, c);
+  if (r) return r;
+  std::vector<uint64_t> v;
+  uint64_t s = start;
+  if (s == REF_NONE) s = head_of(*c, REF_ROOT);  // walk ... Nothing: from the root's head
+  else if (!ref_ok(*c, s)) return CRDTM_E_ARG;
+  if (s != REF_NONE) {
+    const uint64_t par = parent_of(*c, s);
+    if (par != REF_NONE) walk_from(*c, s, children_of(*c, par), v);
+  }
+  return put_refs(v, out, cap, n);
+}
 
 }  // extern "C"

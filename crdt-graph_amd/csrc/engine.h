@@ -2,6 +2,7 @@
 // and the host-side launch entry points of each kernel family.
 #pragma once
 
+#include <memory>
 #include <stdexcept>
 
 #include "kernels.h"
@@ -124,6 +125,8 @@ struct crdtm_tree {
   std::map<int64_t, int64_t> replicas;
   uint64_t last_begin = 0, last_end = 0;
   int last_is_batch = 1;
+  uint64_t version = 0;              // bumped by every state change (apply, reset)
+  std::shared_ptr<void> trav;        // traversal cache (api.hip), valid for `version`
 };
 
 namespace crdtm {

@@ -127,6 +127,31 @@ int crdtm_tree_ops(const crdtm_tree *t, int which, crdtm_ops *out, int *is_batch
  * Host arrays; NULL arrays to size, like crdtm_tree_ops. */
 int crdtm_tree_ops_since(const crdtm_tree *t, int64_t ts, crdtm_ops *out);
 
+/* ---- traversal (CRDTree.get/parent/next/prev/walk, src/CRDTree.elm:421-625;
+ *      CRDTree.Node.children/head, src/CRDTree/Node.elm:96-174). Host-side
+ *      reads of the device state (copied once per tree version). A node
+ *      reference is valid until the next apply/reset of the tree. */
+#define CRDTM_REF_NONE UINT64_MAX                 /* Nothing */
+#define CRDTM_REF_ROOT (UINT64_MAX - 1)           /* the Root node */
+#define CRDTM_REF_VSENT (1ULL << 62)              /* | slot: sentinel of a live node's empty children */
+#define CRDTM_REL_PARENT 0
+#define CRDTM_REL_NEXT 1
+#define CRDTM_REL_PREV 2
+#define CRDTM_REL_HEAD 3
+/* get path tree (Node.descendant from the root): *ref = node or CRDTM_REF_NONE. */
+int crdtm_tree_get(const crdtm_tree *t, const int64_t *path, uint64_t len, uint64_t *ref);
+/* kind 1 Node, 2 Tombstone, 3 Root; value handle (Node); next key; Node.path (up to cap words). */
+int crdtm_node_info(const crdtm_tree *t, uint64_t ref, int32_t *kind, uint32_t *val, int32_t *has_next,
+                    int64_t *next, int64_t *path, uint64_t cap, uint64_t *path_len);
+/* parent / next / prev (src/CRDTree.elm:425-441, :560-575) and Node.head: *out or CRDTM_REF_NONE. */
+int crdtm_tree_relative(const crdtm_tree *t, uint64_t ref, int which, uint64_t *out);
+/* CRDTree.Node.children: the live children in chain order (head = first, last = last). */
+int crdtm_node_children(const crdtm_tree *t, uint64_t ref, uint64_t *out, uint64_t cap, uint64_t *n);
+/* The nodes CRDTree.walk visits, in order, when its function always Takes
+ * (start = CRDTM_REF_NONE: walk ... Nothing); a walk that stops with Done
+ * visits a prefix of this order. */
+int crdtm_tree_walk(const crdtm_tree *t, uint64_t start, uint64_t *out, uint64_t cap, uint64_t *n);
+
 /* Canonical dumps shared with the oracle: which 0 = every dict entry (structure),
  * 1 = visible document order. Writes up to cap words (out may be NULL), the
  * word count and a 64-bit word-wise FNV-1a hash of the words (h ^= w; h *= 0x100000001b3

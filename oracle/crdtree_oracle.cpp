@@ -469,6 +469,146 @@ uint64_t orc_get_path(orc_tree* o, const int64_t* p, uint64_t n, int64_t* out, u
   return d->path.size();
 }
 
+}  // extern "C"
+
+// ---- traversal (src/CRDTree.elm:421-625, src/CRDTree/Node.elm:96-174) ----
+// Results are node descriptors written as words: kind (1 Node, 2 Tombstone,
+// 3 Root), value handle (Node; else 0), has_next, next, path length, path.
+
+static void putNode(const Node* d, std::vector<int64_t>& out) {
+  out.push_back(d->kind == ROOT ? 3 : d->kind);
+  out.push_back(d->kind == NODE ? d->val : 0);
+  out.push_back(d->kind != ROOT && d->has_next ? 1 : 0);
+  out.push_back(d->kind != ROOT && d->has_next ? d->next : 0);
+  out.push_back(static_cast<int64_t>(d->path.size()));
+  for (int64_t k : d->path) out.push_back(k);
+}
+
+static uint64_t emit(const std::vector<int64_t>& w, int64_t* out, uint64_t cap) {
+  for (uint64_t i = 0; out && i < w.size() && i < cap; ++i) out[i] = w[i];
+  return w.size();
+}
+
+// parent (src/CRDTree.elm:425-441): path minus its last key; [] -> the root
+static Node* parentOf(Tree& t, Node* node) {
+  std::vector<int64_t> pp = node->path;
+  if (!pp.empty()) pp.pop_back();  // Array.slice 0 -1
+  if (pp.empty()) return &t.root;
+  return descendant(pp.data(), pp.size(), t.root);
+}
+
+static Dict kEmpty;
+static Dict& childrenOf(Node* n) { return n->kind == TOMB ? kEmpty : n->children; }  // src/Internal/Node.elm:231-241
+
+// next (src/CRDTree.elm:560-566)
+static Node* nextOf(Tree& t, Node* node) {
+  Node* par = parentOf(t, node);
+  if (!par) return nullptr;
+  return nextNode(node, childrenOf(par));
+}
+
+// Elm structural equality on Node values
+static bool nodeEq(const Node& a, const Node& b) {
+  if (a.kind != b.kind || a.path != b.path) return false;
+  if (a.kind == NODE && a.val != b.val) return false;
+  const bool an = a.kind != ROOT && a.has_next, bn = b.kind != ROOT && b.has_next;
+  if (an != bn || (an && a.next != b.next)) return false;
+  if (a.children.size() != b.children.size()) return false;
+  for (auto ia = a.children.begin(), ib = b.children.begin(); ia != a.children.end(); ++ia, ++ib)
+    if (ia->first != ib->first || !nodeEq(ia->second, ib->second)) return false;
+  return true;
+}
+
+// prev (src/CRDTree.elm:569-575): Node.find over the parent's chain from its
+// sentinel, Tombstones included (findHelp, src/Internal/Node.elm:170-182)
+static Node* prevOf(Tree& t, Node* node) {
+  Node* par = parentOf(t, node);
+  if (!par) return nullptr;
+  Dict& c = childrenOf(par);
+  auto it = c.find(0);
+  if (it == c.end()) return nullptr;
+  Node* left = &it->second;
+  for (;;) {
+    if (left->kind == ROOT || !left->has_next) return nullptr;
+    auto jt = c.find(left->next);
+    if (jt == c.end()) return nullptr;
+    Node* n = &jt->second;
+    Node* nn = nextOf(t, n);
+    if (nn && nodeEq(*nn, *node)) return n;
+    left = n;
+  }
+}
+
+// head (src/CRDTree/Node.elm:165-167): first live child
+static Node* headOf(Node* node) {
+  Dict& c = childrenOf(node);
+  auto it = c.find(0);
+  if (it == c.end()) return nullptr;
+  return nextNode(&it->second, c);
+}
+
+// walkHelp (src/CRDTree.elm:602-625) with a function that always Takes
+static void walkHelp(Node* left, Dict& siblings, std::vector<int64_t>& out) {
+  for (;;) {
+    Node* node = nextNode(left, siblings);
+    if (!node) return;
+    putNode(node, out);
+    Node* h = headOf(node);
+    if (h) walkHelp(h, childrenOf(node), out);
+    left = node;
+  }
+}
+
+extern "C" {
+
+// get (src/CRDTree.elm:468-470) -> one descriptor, or 0 words (Nothing)
+uint64_t orc_node_get(orc_tree* o, const int64_t* p, uint64_t n, int64_t* out, uint64_t cap) {
+  std::vector<int64_t> w;
+  Node* d = descendant(p, n, o->t.root);
+  if (d) putNode(d, w);
+  return emit(w, out, cap);
+}
+
+// which: 0 parent, 1 next, 2 prev, 3 CRDTree.Node.children (live, chain order),
+// 4 walk from the node (Just node), 5 walk from the start (Nothing; p ignored)
+uint64_t orc_node_query(orc_tree* o, int which, const int64_t* p, uint64_t n, int64_t* out, uint64_t cap) {
+  std::vector<int64_t> w;
+  Tree& t = o->t;
+  Node* d = which == 5 ? nullptr : (n == 0 ? &t.root : descendant(p, n, t.root));
+  if (which != 5 && !d) return emit(w, out, cap);
+  Node* r = nullptr;
+  switch (which) {
+    case 0: r = parentOf(t, d); break;
+    case 1: r = nextOf(t, d); break;
+    case 2: r = prevOf(t, d); break;
+    case 3: {
+      Dict& c = childrenOf(d);
+      auto it = c.find(0);
+      for (Node* x = it == c.end() ? nullptr : nextNode(&it->second, c); x; x = nextNode(x, c)) putNode(x, w);
+      return emit(w, out, cap);
+    }
+    case 4: {
+      Node* par = parentOf(t, d);
+      if (par) walkHelp(d, childrenOf(par), w);
+      return emit(w, out, cap);
+    }
+    case 5: {
+      Node* h = headOf(&t.root);
+      if (h) {
+        Node* par = parentOf(t, h);
+        if (par) walkHelp(h, childrenOf(par), w);
+      }
+      return emit(w, out, cap);
+    }
+  }
+  if (r) putNode(r, w);
+  return emit(w, out, cap);
+}
+
+}  // extern "C"
+
+extern "C" {
+
 // lastOperation := Batch [] (the reset `batch` performs, src/CRDTree.elm:231)
 void orc_reset_last(orc_tree* o) { o->t.last_is_batch = true; o->t.last.clear(); }
 

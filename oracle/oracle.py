@@ -58,6 +58,10 @@ def lib():
         L.orc_get_value.argtypes = [P, P, C.c_uint64, P, P]
         L.orc_get_path.restype = C.c_uint64
         L.orc_get_path.argtypes = [P, P, C.c_uint64, P, C.c_uint64]
+        L.orc_node_get.restype = C.c_uint64
+        L.orc_node_get.argtypes = [P, P, C.c_uint64, P, C.c_uint64]
+        L.orc_node_query.restype = C.c_uint64
+        L.orc_node_query.argtypes = [P, C.c_int, P, C.c_uint64, P, C.c_uint64]
         L.orc_reset_last.argtypes = [P]
         L.orc_merge_last.argtypes = [P, P]
         _lib = L
@@ -192,6 +196,40 @@ class OTree:
             lib().orc_merge_last(nxt._h, cur._h)
             cur = nxt
         return "Ok", cur
+
+    # ---- traversal (src/CRDTree.elm:421-625): node descriptors
+    #      (kind, value, path tuple, next) with kind in node/tombstone/root ----
+    raw_values = False  # True: descriptors carry value handles (engine parity tests)
+
+    def _nodes(self, words):
+        out, k = [], 0
+        while k < len(words):
+            kind, val, hn, nx, pl = (int(x) for x in words[k:k + 5])
+            path = tuple(int(x) for x in words[k + 5:k + 5 + pl])
+            kd = {1: "node", 2: "tombstone", 3: "root"}[kind]
+            v = (val if self.raw_values else VALUES.value(val)) if kd == "node" else None
+            out.append((kd, v, path, nx if hn else None))
+            k += 5 + pl
+        return out
+
+    def _words(self, fn, *args):
+        n = fn(self._h, *args, None, 0)
+        buf = np.zeros(max(n, 1), np.int64)
+        fn(self._h, *args, _ptr(buf), n)
+        return buf[:n]
+
+    def node(self, path):
+        """get path tree -> descriptor or None."""
+        p = np.array(list(path) or [0], np.int64)
+        r = self._nodes(self._words(lib().orc_node_get, _ptr(p), len(path)))
+        return r[0] if r else None
+
+    def node_query(self, which, path=None):
+        """which: parent, next, prev, children, walk (from the node at path), walk_start."""
+        code = {"parent": 0, "next": 1, "prev": 2, "children": 3, "walk": 4, "walk_start": 5}[which]
+        p = np.array(list(path or []) or [0], np.int64)
+        r = self._nodes(self._words(lib().orc_node_query, code, _ptr(p), len(path or [])))
+        return r if which in ("children", "walk", "walk_start") else (r[0] if r else None)
 
     # ---- queries ----
     def timestamp(self):

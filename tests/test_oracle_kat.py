@@ -245,3 +245,45 @@ def children_of(recs, key):
         elif inside and r["depth"] == 1:
             kids.append(r["key"])
     return kids
+
+
+# ---------------- traversal: the reference's documented examples ----------------
+# (src/CRDTree.elm:447-466: get / getValue on treeA = batch [addBranch "a",
+# addBranch "b", add "c"] with replica 1; the walk order follows A.8)
+
+class TestTraversal:
+    def tree_a(self):
+        return ok(OTree(1).batch([lambda t: t.add_branch("a"), lambda t: t.add_branch("b"), lambda t: t.add("c")]))
+
+    def test_get_doc_examples(self):  # src/CRDTree.elm:447-466
+        t = self.tree_a()
+        o = T32
+        assert t.node([o + 1])[:3] == ("node", "a", (o + 1,))
+        assert t.node([o + 1, o + 2])[:3] == ("node", "b", (o + 1, o + 2))
+        assert t.node([o + 1, o + 2, o + 3])[:3] == ("node", "c", (o + 1, o + 2, o + 3))
+        assert t.node([4]) is None
+        assert t.node([]) is None
+        # a dict sentinel exists: Tombstone [] Nothing, whose parent is the root (path [])
+        assert t.node([o + 1, 0]) == ("tombstone", None, (), o + 2)
+        assert t.node_query("parent", [o + 1, 0])[0] == "root"
+
+    def test_next_prev_children_walk(self):
+        t = ok(OTree(1).batch([lambda t: t.add("a"), lambda t: t.add("b"), lambda t: t.add("c")]))
+        o = T32
+        ch = t.node_query("children", [])  # the root's children: a, b, c in chain order
+        assert [c[1] for c in ch] == ["a", "b", "c"]
+        assert t.node_query("next", [o + 1])[1] == "b"
+        assert t.node_query("prev", [o + 3])[1] == "b"
+        assert t.node_query("prev", [o + 1]) is None
+        assert t.node_query("next", [o + 3]) is None
+        # walk ... Nothing starts after the root's head: b, c
+        assert [n[1] for n in t.node_query("walk_start")] == ["b", "c"]
+        t2 = ok(t.delete([o + 2]))
+        assert t2.node_query("next", [o + 1])[1] == "c"  # skips the Tombstone
+        assert t2.node_query("prev", [o + 3])[1] == "a"
+
+    def test_walk_skips_each_head(self):  # A.8
+        t = ok(OTree(1).batch([lambda t: t.add("a"), lambda t: t.add_branch("b"), lambda t: t.add("b1"),
+                               lambda t: t.add("b2")]))
+        # root: a, b; b's children: b1, b2. walk Nothing: after head a -> b, then b's children after b1 -> b2
+        assert [n[1] for n in t.node_query("walk_start")] == ["b", "b2"]

@@ -1,0 +1,91 @@
+"""Traversal API (CRDTree.get/parent/next/prev/walk, CRDTree.Node.children/head;
+src/CRDTree.elm:421-625, src/CRDTree/Node.elm:96-174) served from the device
+state, against the oracle's literal restatement — on trees with tombstones,
+copy-quirk slots, orphans and implicit sentinels (tests/adversarial.py)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from crdtm.operation import flatten  # noqa: E402
+from crdtm.tree import CRDTree, pack  # noqa: E402
+from kat_cases import SCENARIOS  # noqa: E402
+from parity_util import oracle_apply_arrays  # noqa: E402
+
+
+def _oracle(handle):
+    from oracle.oracle import OTree
+    t = OTree(_h=handle)
+    t.raw_values = True
+    return t
+
+
+def _key(v):
+    return None if v is None else (v.kind, v.value, tuple(v.path), v.next)
+
+
+def check_tree(et, ot, paths):
+    import crdtm.tree as T
+    orig = T.VALUES.value
+    T.VALUES.value = lambda h: h
+    try:
+        assert [_key(v) for v in et.walk_nodes()] == ot.node_query("walk_start")
+        assert [_key(v) for v in et.children(et.root())] == ot.node_query("children", [])
+        for p in paths:
+            v = et.get(p)
+            assert _key(v) == ot.node(p), p
+            if v is None:
+                continue
+            assert _key(et.parent(v)) == ot.node_query("parent", p), p
+            assert _key(et.next(v)) == ot.node_query("next", p), p
+            assert _key(et.prev(v)) == ot.node_query("prev", p), p
+            assert [_key(c) for c in et.children(v)] == ot.node_query("children", p), p
+            assert [_key(w) for w in et.walk_nodes(v)] == ot.node_query("walk", p), p
+    finally:
+        T.VALUES.value = orig
+
+
+def query_paths(leaves, rng):
+    paths = set()
+    for o in leaves:
+        if o.kind == "add":
+            node = tuple(o.path[:-1]) + (o.ts,)
+            paths.add(node)
+            paths.add(node + (0,))            # its children's sentinel
+            paths.add(tuple(o.path))          # its anchor
+        else:
+            paths.add(tuple(o.path))
+    paths = sorted(paths)
+    extra = [p + (int(rng.integers(1, 1 << 40)),) for p in paths[:20]] + [(0,), (12345,)]
+    return [list(p) for p in paths + extra]
+
+
+@pytest.mark.parametrize("name", sorted(SCENARIOS))
+def test_traversal_scenarios(name):
+    replica, calls = SCENARIOS[name]
+    from oracle.oracle import lib as olib
+    ot = olib().orc_init(replica)
+    et = CRDTree.init(replica)
+    leaves_all = []
+    for op in calls:
+        leaves = flatten(op) if op.kind == "batch" else [op]
+        arrs = pack(leaves)
+        oracle_apply_arrays(arrs, len(leaves), is_batch=op.kind == "batch", tree=ot)
+        et.apply_arrays(arrs, len(leaves), is_batch=op.kind == "batch")
+        leaves_all += leaves
+    check_tree(et, _oracle(ot), query_paths(leaves_all, np.random.default_rng(1)))
+
+
+@pytest.mark.parametrize("seed", range(0, 64, 4))
+def test_traversal_adversarial(seed):
+    from adversarial import adversarial
+    n = [40, 120, 400, 1500][seed % 4]
+    ops = adversarial(seed, n, replicas=2 + seed % 3, max_depth=1 + seed % 4)
+    arrs = pack(ops)
+    ot, rc, _ = oracle_apply_arrays(arrs, n)
+    et = CRDTree.init(0)
+    assert et.apply_arrays(arrs, n).code == rc
+    if rc != 0:
+        return
+    paths = query_paths(ops, np.random.default_rng(seed))
+    check_tree(et, _oracle(ot), paths[:400])
