@@ -42,7 +42,8 @@ struct ExclSink {
 // the chain. A cycle inside a tile (never on a valid list) leaves its
 // entries unranked, like entries off the list.
 // ---------------------------------------------------------------------------
-constexpr uint32_t LC_T = 1024;
+constexpr uint32_t LC_LOG = 10;
+constexpr uint32_t LC_T = 1u << LC_LOG;
 constexpr uint32_t LC_PER = LC_T / BLOCK;
 constexpr uint64_t LC_MIN = 1ULL << 16;  // shorter lists: sublist method on a materialised list
 
@@ -87,7 +88,7 @@ __global__ void __launch_bounds__(BLOCK) k_lc_contract(SRC srcf, uint64_t n, uin
   }
   __syncthreads();
   // Wyllie pointer jumping toward the chain head (<= log2(LC_T) rounds)
-  for (uint32_t round = 0; round <= 10; ++round) {
+  for (uint32_t round = 0; round <= LC_LOG; ++round) {
     bool ch = false;
 #pragma unroll
     for (uint32_t k = 0; k < LC_PER; ++k) {
