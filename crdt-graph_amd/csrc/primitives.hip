@@ -492,7 +492,7 @@ int segmented_sort_asc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* c
 // per block, + the head) is ranked recursively, serially once it is short,
 // and a last pass adds each splitter's prefix to its sublist. No atomics.
 // ---------------------------------------------------------------------------
-constexpr uint64_t LR_SERIAL = 2048;
+constexpr uint64_t LR_SERIAL = 64;
 
 __host__ __device__ __forceinline__ uint64_t lr_cand(uint64_t b, uint32_t kbits) {
   return (b << kbits) + (mix64(b * 0x9E3779B97F4A7C15ULL + 0x632BE59BD9B4E019ULL) & ((1ULL << kbits) - 1));
@@ -568,7 +568,7 @@ __global__ void __launch_bounds__(BLOCK) k_lr_apply(uint64_t n, const uint32_t* 
 
 static int list_rank_level(const uint2* ent, const uint32_t* succ, const unsigned long long* w, uint64_t n,
                            uint32_t head, unsigned long long* excl, Arena& ws, hipStream_t st, int level) {
-  const uint32_t kbits = level == 0 ? 5u : 4u;
+  const uint32_t kbits = level == 0 ? 5u : 3u;
   const uint64_t nb = (n + (1ULL << kbits) - 1) >> kbits;
   const uint64_t head_id = (lr_cand(head >> kbits, kbits) == head) ? (head >> kbits) : nb;
   uint32_t* owner = ws.alloc<uint32_t>(n);
