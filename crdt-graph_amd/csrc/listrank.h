@@ -44,22 +44,31 @@ struct ExclSink {
 // ---------------------------------------------------------------------------
 constexpr uint32_t LC_LOG = 10;
 constexpr uint32_t LC_T = 1u << LC_LOG;
+static_assert(LC_T < 0xFFFFu, "tile-local chain ids and prefixes are 16-bit");
 constexpr uint32_t LC_PER = LC_T / BLOCK;
 constexpr uint64_t LC_MIN = 1ULL << 16;  // shorter lists: sublist method on a materialised list
 
+// Inside a tile both weight counters stay below 2^16, so a weight travels as
+// one 32-bit word {tour nodes:16 | visible:16} (the halves never carry).
+__device__ __forceinline__ uint32_t lc_pw(uint32_t wbits) { return (((wbits >> 1) & 1u) << 16) | (wbits & 1u); }
+__device__ __forceinline__ unsigned long long lc_unpack(uint32_t pw) {
+  return (static_cast<unsigned long long>(pw >> 16) << 32) | (pw & 0xFFFFu);
+}
+constexpr uint16_t LC_NONE = 0xFFFFu;
+
 // Contraction of one tile. Outputs: hidx[e] = the tile-local index of e's
-// chain (NONE: off every list), pre[e] = e's prefix inside its chain,
+// chain (LC_NONE: off every list), pre[e] = e's packed prefix inside its chain,
 // tcnt[tile] = chains in the tile; per chain, at sparse position
 // tile * LC_T + local: the successor entry of its tail (sp_succ) and its
 // total weight (sp_w). No global atomics: chain ids become dense after a
 // scan of tcnt (k_lc_link).
 template <class SRC>
-__global__ void __launch_bounds__(BLOCK) k_lc_contract(SRC srcf, uint64_t n, uint32_t* __restrict__ hidx,
-                                                       unsigned long long* __restrict__ pre,
+__global__ void __launch_bounds__(BLOCK) k_lc_contract(SRC srcf, uint64_t n, uint16_t* __restrict__ hidx,
+                                                       uint32_t* __restrict__ pre,
                                                        uint32_t* __restrict__ tcnt, uint32_t* __restrict__ sp_succ,
                                                        unsigned long long* __restrict__ sp_w) {
   __shared__ uint32_t P[LC_T];
-  __shared__ unsigned long long V[LC_T];
+  __shared__ uint32_t V[LC_T];
   __shared__ uint32_t W[LC_T];
   __shared__ uint32_t sw[BLOCK / 64];
   const uint64_t base = static_cast<uint64_t>(blockIdx.x) * LC_T;
@@ -78,12 +87,12 @@ __global__ void __launch_bounds__(BLOCK) k_lc_contract(SRC srcf, uint64_t n, uin
   }
   __syncthreads();
   uint32_t p[LC_PER];
-  unsigned long long v[LC_PER];
+  uint32_t v[LC_PER];
 #pragma unroll
   for (uint32_t k = 0; k < LC_PER; ++k) {
     const uint32_t l = threadIdx.x + k * BLOCK;
     p[k] = P[l];
-    v[k] = p[k] != NONE ? lr_weight(W[p[k]]) : 0ULL;
+    v[k] = p[k] != NONE ? lc_pw(W[p[k]]) : 0u;
     V[l] = v[k];
   }
   __syncthreads();
@@ -141,15 +150,15 @@ __global__ void __launch_bounds__(BLOCK) k_lc_contract(SRC srcf, uint64_t n, uin
     const uint64_t e = base + l;
     if (e >= n) continue;
     if (sc[k] == ABSENT || cyc[k]) {
-      hidx[e] = NONE;
+      hidx[e] = LC_NONE;
       continue;
     }
     const uint32_t h = P[head[k] ? l : p[k]];
-    hidx[e] = h;
+    hidx[e] = static_cast<uint16_t>(h);
     pre[e] = v[k];
     const uint32_t s = sc[k];
     if (!(s < n && s >= base && s < base + LC_T)) {  // tail of its local chain
-      sp_w[base + h] = v[k] + lr_weight(W[l]);
+      sp_w[base + h] = lc_unpack(v[k] + lc_pw(W[l]));
       sp_succ[base + h] = s;  // entry id of the next chain's head (or NONE)
     }
   }
@@ -158,7 +167,7 @@ __global__ void __launch_bounds__(BLOCK) k_lc_contract(SRC srcf, uint64_t n, uin
 // Dense contracted list: chain (tile t, local h) -> toff[t] + h; its
 // successor is the chain headed by entry s, i.e. toff[s / LC_T] + hidx[s].
 static __global__ void __launch_bounds__(BLOCK) k_lc_link(const uint32_t* __restrict__ toff,
-                                                          const uint32_t* __restrict__ hidx,
+                                                          const uint16_t* __restrict__ hidx,
                                                           const uint32_t* __restrict__ sp_succ,
                                                           const unsigned long long* __restrict__ sp_w,
                                                           uint32_t* __restrict__ rsucc,
@@ -174,23 +183,23 @@ static __global__ void __launch_bounds__(BLOCK) k_lc_link(const uint32_t* __rest
 }
 
 // {contracted list length, contracted id of the list head} in one word pair
-static __global__ void k_lc_meta(const uint32_t* toff, uint32_t tiles, const uint32_t* hidx, uint32_t head,
+static __global__ void k_lc_meta(const uint32_t* toff, uint32_t tiles, const uint16_t* hidx, uint32_t head,
                                  uint32_t* meta) {
   meta[0] = toff[tiles];
   const uint32_t h = hidx[head];
-  meta[1] = h == NONE ? NONE : toff[head / LC_T] + h;
+  meta[1] = h == LC_NONE ? NONE : toff[head / LC_T] + h;
 }
 
 template <class SINK>
 __global__ void __launch_bounds__(BLOCK) k_lc_expand(uint64_t n, const uint32_t* __restrict__ toff,
-                                                     const uint32_t* __restrict__ hidx,
-                                                     const unsigned long long* __restrict__ pre,
+                                                     const uint16_t* __restrict__ hidx,
+                                                     const uint32_t* __restrict__ pre,
                                                      const unsigned long long* __restrict__ rexcl, SINK sink) {
   for (uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; e < n;
        e += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
     const uint32_t h = hidx[e];
-    const unsigned long long b = h != NONE ? rexcl[toff[e / LC_T] + h] : ~0ULL;
-    if (b != ~0ULL) sink(e, b + pre[e]);
+    const unsigned long long b = h != LC_NONE ? rexcl[toff[e / LC_T] + h] : ~0ULL;
+    if (b != ~0ULL) sink(e, b + lc_unpack(pre[e]));
     else if (SINK::kOffList) sink(e, ~0ULL);
   }
 }
@@ -224,8 +233,8 @@ int list_rank_fused(SRC srcf, uint64_t n, uint32_t head, SINK sink, Arena& ws, h
     return CRDTM_OK;
   }
   const uint64_t tiles = (n + LC_T - 1) / LC_T;
-  uint32_t* hidx = ws.alloc<uint32_t>(n);
-  unsigned long long* pre = ws.alloc<unsigned long long>(n);
+  uint16_t* hidx = ws.alloc<uint16_t>(n);
+  uint32_t* pre = ws.alloc<uint32_t>(n);
   uint32_t* sp_succ = ws.alloc<uint32_t>(tiles * LC_T);
   unsigned long long* sp_w = ws.alloc<unsigned long long>(tiles * LC_T);
   uint32_t* toff = ws.alloc<uint32_t>(tiles + 1);
