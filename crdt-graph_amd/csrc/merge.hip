@@ -2573,7 +2573,7 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   uint2* ent = ws.alloc<uint2>(E);
   unsigned long long* excl = ws.alloc<unsigned long long>(E);
   LAUNCH(k_euler, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, fc, ns, ent);
-  if ((r = list_rank(ent, E, 2 * (n + 1), excl, ws, s))) return r;
+  if ((r = list_rank_packed(ent, E, 2 * (n + 1), excl, ws, s))) return r;
   uint32_t* order = ws.alloc<uint32_t>(U);
   uint32_t* nextn = ws.alloc<uint32_t>(n);
   LAUNCH(k_order, dim3(gU), dim3(BLOCK), 0, s, o, w, sp, excl, order);

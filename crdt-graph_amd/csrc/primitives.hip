@@ -568,7 +568,7 @@ __global__ void __launch_bounds__(BLOCK) k_lr_apply(uint64_t n, const uint32_t* 
 
 static int list_rank_level(const uint2* ent, const uint32_t* succ, const unsigned long long* w, uint64_t n,
                            uint32_t head, unsigned long long* excl, Arena& ws, hipStream_t st, int level) {
-  const uint32_t kbits = level == 0 ? 5u : 3u;
+  const uint32_t kbits = level == 0 ? 4u : 3u;
   const uint64_t nb = (n + (1ULL << kbits) - 1) >> kbits;
   const uint64_t head_id = (lr_cand(head >> kbits, kbits) == head) ? (head >> kbits) : nb;
   uint32_t* owner = ws.alloc<uint32_t>(n);
