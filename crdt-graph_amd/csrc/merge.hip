@@ -1437,6 +1437,14 @@ __global__ void __launch_bounds__(64) k_forest_prep(OpsDev o, const uint32_t* do
   if (lane == 0) sent[d] = static_cast<uint16_t>(fl_lower(skey, 0));
 }
 
+// The whole wave runs the replay with identical values (wave-uniform control
+// flow, broadcast LDS reads moved to scalar registers): op words stream
+// through registers 64 at a time, and the hash inputs of the visible
+// document are gathered 64 at a time by all lanes.
+__device__ __forceinline__ uint32_t fl_ld(const uint32_t* sl, uint32_t k) {
+  return __builtin_amdgcn_readfirstlane(sl[k]);
+}
+
 __global__ void __launch_bounds__(64) k_forest_replay(OpsDev o, const uint32_t* doc_off, uint32_t n_docs,
                                                       long long ts0, const uint32_t* opw, const uint16_t* sent,
                                                       const uint8_t* fb, int32_t* code_out, uint32_t* err_out,
@@ -1451,101 +1459,136 @@ __global__ void __launch_bounds__(64) k_forest_replay(OpsDev o, const uint32_t* 
   const uint32_t s0 = sent[d];
   for (uint32_t j = lane; j < FL_SLOTS; j += 64) sl[j] = j == s0 ? (FL_N | FS_PRESENT | FS_TOMB) : FL_N;
   __syncthreads();
-  if (lane != 0) return;
   // Fresh documents start at counter 0 of their replica, so no run of at most
   // FL_MAXOPS own Adds can cross into the next replica id: the OWN bit of
   // each op (computed against ts0) is the reference's per-op comparison.
   long long ts = ts0;
   uint32_t applied = 0, err = NONE;
   int32_t code = CRDTM_OK;
-  for (uint32_t j = 0; j < nops; ++j) {
-    const uint32_t w = opw[ob + j];
-    if (w & FO_INV) {  // update [] = InvalidPath
-      err = j;
-      code = CRDTM_INVALID_PATH;
-      break;
-    }
-    const uint32_t t = w & FL_N;
-    if (w & FO_DEL) {  // deleteHelp (:112-122)
-      const uint32_t st = t == FL_N ? 0u : sl[t];
-      if (!(st & FS_PRESENT)) {
+  uint32_t nxw = lane < nops ? opw[ob + lane] : 0u;
+  bool stop = false;
+  for (uint32_t j0 = 0; j0 < nops && !stop; j0 += 64) {
+    const uint32_t myw = nxw;
+    nxw = j0 + 64 + lane < nops ? opw[ob + j0 + 64 + lane] : 0u;
+    const uint32_t cnt = min(64u, nops - j0);
+    for (uint32_t jj = 0; jj < cnt; ++jj) {
+      const uint32_t j = j0 + jj;
+      const uint32_t w = __builtin_amdgcn_readlane(myw, jj);
+      if (w & FO_INV) {  // update [] = InvalidPath
         err = j;
-        code = CRDTM_OPERATION_FAILED;
+        code = CRDTM_INVALID_PATH;
+        stop = true;
         break;
       }
-      if (!(st & FS_TOMB)) {
-        sl[t] = st | FS_TOMB;
-        ++applied;
-      }
-      continue;
-    }
-    const uint32_t x = t;
-    if (sl[x] & FS_PRESENT) {  // `child ts parent` exists: AlreadyApplied
-      if (w & FO_OWN) ++ts;
-      continue;
-    }
-    const uint32_t a = (w >> 11) & FL_N;
-    const uint32_t sa = a == FL_N ? 0u : sl[a];
-    if (!(sa & FS_PRESENT)) {  // anchor missing: NotFound
-      err = j;
-      code = CRDTM_OPERATION_FAILED;
-      break;
-    }
-    uint32_t nk = a, node = a, sn = sa;  // findInsertion (:93-104)
-    for (;;) {
-      const uint32_t rn = sn & FL_N;
-      if (rn == FL_N) break;
-      uint32_t live = rn, sl_live = sl[rn];
-      while (sl_live & FS_TOMB) {
-        live = sl_live & FL_N;
-        if (live == FL_N) break;
-        sl_live = sl[live];
-      }
-      if (live == FL_N || x > rn) break;
-      nk = rn;
-      node = live;
-      sn = sl_live;
-    }
-    const uint32_t snk = nk == node ? sn : sl[nk];
-    sl[x] = (sn & FL_N) | (j << 11) | FS_PRESENT | (snk & FS_ORPHAN);
-    if (nk == node) {
-      sl[node] = (sn & ~FL_N) | x;
-    } else {  // copy quirk: slot nk := copy of node with next = x
-      if (!(snk & FS_ORPHAN)) {
-        for (uint32_t q = snk & FL_N; q != FL_N;) {
-          const uint32_t sq = sl[q];
-          sl[q] = sq | FS_ORPHAN;
-          if (q == node) break;
-          q = sq & FL_N;
+      const uint32_t t = w & FL_N;
+      if (w & FO_DEL) {  // deleteHelp (:112-122)
+        const uint32_t st = t == FL_N ? 0u : fl_ld(sl, t);
+        if (!(st & FS_PRESENT)) {
+          err = j;
+          code = CRDTM_OPERATION_FAILED;
+          stop = true;
+          break;
         }
+        if (!(st & FS_TOMB)) {
+          sl[t] = st | FS_TOMB;
+          ++applied;
+        }
+        continue;
       }
-      sl[nk] = x | (sn & (0x3FFu << 11)) | FS_PRESENT | (snk & FS_ORPHAN);
+      const uint32_t x = t;
+      if (fl_ld(sl, x) & FS_PRESENT) {  // `child ts parent` exists: AlreadyApplied
+        if (w & FO_OWN) ++ts;
+        continue;
+      }
+      const uint32_t a = (w >> 11) & FL_N;
+      const uint32_t sa = a == FL_N ? 0u : fl_ld(sl, a);
+      if (!(sa & FS_PRESENT)) {  // anchor missing: NotFound
+        err = j;
+        code = CRDTM_OPERATION_FAILED;
+        stop = true;
+        break;
+      }
+      uint32_t nk = a, node = a, sn = sa;  // findInsertion (:93-104)
+      for (;;) {
+        const uint32_t rn = sn & FL_N;
+        if (rn == FL_N) break;
+        uint32_t live = rn, sl_live = fl_ld(sl, rn);
+        while (sl_live & FS_TOMB) {
+          live = sl_live & FL_N;
+          if (live == FL_N) break;
+          sl_live = fl_ld(sl, live);
+        }
+        if (live == FL_N || x > rn) break;
+        nk = rn;
+        node = live;
+        sn = sl_live;
+      }
+      const uint32_t snk = nk == node ? sn : fl_ld(sl, nk);
+      sl[x] = (sn & FL_N) | (j << 11) | FS_PRESENT | (snk & FS_ORPHAN);
+      if (nk == node) {
+        sl[node] = (sn & ~FL_N) | x;
+      } else {  // copy quirk: slot nk := copy of node with next = x
+        if (!(snk & FS_ORPHAN)) {
+          for (uint32_t q = snk & FL_N; q != FL_N;) {
+            const uint32_t sq = fl_ld(sl, q);
+            sl[q] = sq | FS_ORPHAN;
+            if (q == node) break;
+            q = sq & FL_N;
+          }
+        }
+        sl[nk] = x | (sn & (0x3FFu << 11)) | FS_PRESENT | (snk & FS_ORPHAN);
+      }
+      ++applied;
+      if (w & FO_OWN) ++ts;  // incrementTimestamp (src/CRDTree.elm:337-343)
     }
-    ++applied;
-    if (w & FO_OWN) ++ts;  // incrementTimestamp (src/CRDTree.elm:337-343)
   }
-  code_out[d] = code;
-  err_out[d] = err;
-  applied_out[d] = applied;
-  tstamp[d] = ts;
-  overflow[d] = 0;
+  if (lane == 0) {
+    code_out[d] = code;
+    err_out[d] = err;
+    applied_out[d] = applied;
+    tstamp[d] = ts;
+    overflow[d] = 0;
+  }
+  // hash of the visible document: walk 64 visible nodes (LDS), gather their
+  // values and timestamps with one load per lane, hash them in order
   Fnv h;
   if (code == CRDTM_OK) {
     uint32_t cur = s0;
-    for (;;) {
-      uint32_t nx = sl[cur] & FL_N;
-      while (nx != FL_N && (sl[nx] & FS_TOMB)) nx = sl[nx] & FL_N;
-      if (nx == FL_N) break;
-      const uint32_t i = ob + ((sl[nx] >> 11) & 0x3FFu);
-      h.put(0);
-      h.put(static_cast<long long>(o.val[i]));
-      h.put(1);
-      h.put(o.ts[i]);
-      cur = nx;
+    bool more = true;
+    while (more) {
+      uint32_t mine = NONE, cntv = 0;
+      while (cntv < 64) {
+        uint32_t nx = fl_ld(sl, cur) & FL_N;
+        while (nx != FL_N && (fl_ld(sl, nx) & FS_TOMB)) nx = fl_ld(sl, nx) & FL_N;
+        if (nx == FL_N) {
+          more = false;
+          break;
+        }
+        if (lane == cntv) mine = ob + ((fl_ld(sl, nx) >> 11) & 0x3FFu);
+        ++cntv;
+        cur = nx;
+      }
+      uint32_t v = 0;
+      long long tv = 0;
+      if (mine != NONE) {
+        v = o.val[mine];
+        tv = o.ts[mine];
+      }
+      for (uint32_t k = 0; k < cntv; ++k) {
+        const uint32_t vk = __builtin_amdgcn_readlane(v, k);
+        const uint32_t tlo = __builtin_amdgcn_readlane(static_cast<uint32_t>(tv), k);
+        const uint32_t thi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<unsigned long long>(tv) >> 32), k);
+        h.put(0);
+        h.put(static_cast<long long>(vk));
+        h.put(1);
+        h.put(static_cast<long long>((static_cast<unsigned long long>(thi) << 32) | tlo));
+      }
     }
   }
-  vhash[d] = h.h;
-  vwords[d] = h.n;
+  if (lane == 0) {
+    vhash[d] = h.h;
+    vwords[d] = h.n;
+  }
 }
 
 __global__ void __launch_bounds__(64) k_forest(OpsDev o, ForestArgs f, const uint64_t* sbase, const uint64_t* dbase,
