@@ -298,7 +298,7 @@ def run_trees(args, rank, world, local_rank):
 
     def step():
         allrec = shard.all_gather_records(local)
-        ops_t, doc_off, _ = shard.assemble(allrec, rank, world, n_docs, per)
+        ops_t, doc_off, _ = shard.assemble(allrec, rank, world, n_docs, per, ctx=ctx)
         n = int(doc_off[-1])
         ops = N.Ops(n, n, ops_t["kind"].data_ptr(), ops_t["ts"].data_ptr(), ops_t["path_off"].data_ptr(),
                     ops_t["path"].data_ptr(), ops_t["val"].data_ptr(), None)

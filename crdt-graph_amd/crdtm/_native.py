@@ -59,6 +59,7 @@ SIGNATURES = [
     ("crdtm_tree_replicas", C.c_int, [P, P, P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("crdtm_tree_ops", C.c_int, [P, C.c_int, C.POINTER(Ops), C.POINTER(C.c_int)]),
     ("crdtm_tree_ops_since", C.c_int, [P, C.c_int64, C.POINTER(Ops)]),
+    ("crdtm_shard_assemble", C.c_int, [P, P, C.c_uint64, C.c_int32, C.c_int32, C.c_uint64, C.POINTER(Ops)]),
     ("crdtm_tree_get", C.c_int, [P, P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("crdtm_node_info", C.c_int, [P, C.c_uint64, C.POINTER(C.c_int32), C.POINTER(C.c_uint32), C.POINTER(C.c_int32),
                                   C.POINTER(C.c_int64), P, C.c_uint64, C.POINTER(C.c_uint64)]),

@@ -82,16 +82,33 @@ def all_gather_records(local: torch.Tensor, group=None) -> torch.Tensor:
 _ARANGE = {}
 
 
-def assemble(records: torch.Tensor, rank, world, n_docs, per_doc):
+def assemble(records: torch.Tensor, rank, world, n_docs, per_doc, ctx=None):
     """Records of every replica -> SoA ops of this rank's documents in causal order.
     Documents owned: t = rank, rank + world, ... (local index t // world);
     every document holds exactly per_doc ops. Sync-free: records of other
     ranks' documents are scattered into a spill slot at index n."""
+    n_mine = (n_docs - rank + world - 1) // world
+    n = n_mine * per_doc
+    doc_off = np.arange(n_mine + 1, dtype=np.uint32) * per_doc
+    if ctx is not None and records.device.type == "cuda":
+        # one HIP pass (crdtm_shard_assemble) on the engine's stream
+        import ctypes as C
+        from . import _native as N
+        dev = records.device
+        out = dict(kind=torch.zeros(n + 1, dtype=torch.uint8, device=dev),
+                   ts=torch.zeros(n + 1, dtype=torch.int64, device=dev),
+                   path_off=torch.empty(n + 1, dtype=torch.int32, device=dev),
+                   path=torch.zeros(n + 1, dtype=torch.int64, device=dev),
+                   val=torch.zeros(n + 1, dtype=torch.int32, device=dev))
+        records = records.contiguous()
+        ops = N.Ops(n, n, out["kind"].data_ptr(), out["ts"].data_ptr(), out["path_off"].data_ptr(),
+                    out["path"].data_ptr(), out["val"].data_ptr(), None)
+        N.check(N.lib().crdtm_shard_assemble(ctx, C.c_void_p(records.data_ptr()), records.shape[0], rank, world,
+                                             per_doc, C.byref(ops)), "crdtm_shard_assemble")
+        return out, doc_off, None
     doc = records[:, 0] >> 32
     seq = records[:, 0] & 0xFFFFFFFF
     keep = (doc % world) == rank
-    n_mine = (n_docs - rank + world - 1) // world
-    n = n_mine * per_doc
     dst = torch.where(keep, (doc // world) * per_doc + seq, torch.full_like(doc, n))
     dev = records.device
     kind = torch.zeros(n + 1, dtype=torch.uint8, device=dev)
@@ -105,5 +122,4 @@ def assemble(records: torch.Tensor, rank, world, n_docs, per_doc):
     key = (str(dev), n)
     if key not in _ARANGE:
         _ARANGE[key] = torch.arange(n + 1, dtype=torch.int32, device=dev)
-    doc_off = np.arange(n_mine + 1, dtype=np.uint32) * per_doc
     return dict(kind=kind, ts=ts, path_off=_ARANGE[key], path=path, val=val), doc_off, keep

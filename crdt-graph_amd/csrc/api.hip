@@ -880,3 +880,49 @@ int crdtm_tree_walk(const crdtm_tree* t, uint64_t start, uint64_t* out, uint64_t
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Sharding glue (config 5): after the all-gather of the
+// replicas' op logs, put every record of a document this rank owns at its
+// place in the document's causal stream, as packed ops (one pass).
+// ---------------------------------------------------------------------------
+namespace {
+__global__ void __launch_bounds__(BLOCK) k_shard_assemble(const long long* __restrict__ rec, uint64_t n_rec,
+                                                          uint32_t rank, uint32_t world, uint64_t per_doc,
+                                                          uint64_t n_out, uint8_t* kind, uint32_t* val, long long* ts,
+                                                          long long* path, uint32_t* path_off) {
+  for (uint64_t r = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; r < n_rec;
+       r += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const longlong2 a = reinterpret_cast<const longlong2*>(rec)[2 * r];
+    const longlong2 b = reinterpret_cast<const longlong2*>(rec)[2 * r + 1];
+    const uint64_t doc = static_cast<uint64_t>(a.x) >> 32, seq = static_cast<uint64_t>(a.x) & 0xFFFFFFFFull;
+    if (doc % world != rank || seq >= per_doc) continue;
+    const uint64_t dst = (doc / world) * per_doc + seq;
+    if (dst >= n_out) continue;
+    kind[dst] = static_cast<uint8_t>(static_cast<uint64_t>(a.y) >> 32);
+    val[dst] = static_cast<uint32_t>(a.y);
+    ts[dst] = b.x;
+    path[dst] = b.y;
+  }
+  for (uint64_t q = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; q <= n_out;
+       q += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    path_off[q] = static_cast<uint32_t>(q);  // flat documents: one path element per op
+}
+}  // namespace
+
+extern "C" {
+
+int crdtm_shard_assemble(crdtm_ctx* c, const int64_t* records, uint64_t n_rec, int32_t rank, int32_t world,
+                         uint64_t per_doc, crdtm_ops* out) {
+  if (!c || !out || world <= 0 || rank < 0 || rank >= world || (n_rec && !records)) return CRDTM_E_ARG;
+  if ((reinterpret_cast<uintptr_t>(records) & 15) != 0) return CRDTM_E_ARG;
+  HIP_CHECK(hipSetDevice(c->device));
+  hipLaunchKernelGGL(k_shard_assemble, dim3(grid_for(std::max<uint64_t>(n_rec, out->n_ops + 1))), dim3(BLOCK), 0,
+                     c->stream, reinterpret_cast<const long long*>(records), n_rec, static_cast<uint32_t>(rank),
+                     static_cast<uint32_t>(world), per_doc, out->n_ops, out->kind, out->val,
+                     reinterpret_cast<long long*>(out->ts), reinterpret_cast<long long*>(out->path), out->path_off);
+  HIP_CHECK(hipGetLastError());
+  return CRDTM_OK;
+}
+
+}  // extern "C"

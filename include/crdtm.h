@@ -176,6 +176,14 @@ int crdtm_forest_apply(crdtm_ctx *ctx, int64_t replica_id, const crdtm_ops *ops,
                        uint64_t n_docs, int on_device, int32_t *doc_code, int64_t *doc_err, uint32_t *doc_applied,
                        uint64_t *doc_hash, uint64_t *doc_words, int64_t *doc_timestamp);
 
+/* ---- sharding glue (config 5): records [doc << 32 | seq, kind << 32 | val, ts, anchor]
+ * (int64 x 4, device, 16-byte aligned) of every replica -> the packed ops of the
+ * documents this rank owns (t mod world == rank), document t at
+ * [(t / world) * per_doc, ...) in causal order. out: device arrays of
+ * out->n_ops (+1 for path_off) entries; records of other ranks are skipped. */
+int crdtm_shard_assemble(crdtm_ctx *ctx, const int64_t *records, uint64_t n_rec, int32_t rank, int32_t world,
+                         uint64_t per_doc, crdtm_ops *out);
+
 /* ---- synthetic op streams ---- */
 typedef struct crdtm_synth_params {
   uint64_t n_ops;       /* per document */
