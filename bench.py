@@ -42,7 +42,7 @@ WORKLOADS = {
     # SURVEY.md §8d config 1 shape: 2 replicas, 10k ops, 70/30 interleaved, depth <= 3
     "cfg1": dict(n_ops=10_000, replicas=2, window=8, p_delete=0.3, p_branch=0.05, max_depth=3, seed=0xC0FFEE01),
 }
-CPU_SAMPLE = {"flat10m": 150_000, "deep10m": 2_000_000, "trees": 2_000_000, "cfg2": 100_000, "cfg1": 10_000}
+CPU_SAMPLE = {"flat10m": 100_000, "deep10m": 500_000, "trees": 2_000_000, "cfg2": 100_000, "cfg1": 10_000}
 # 100k documents x 1k ops (80/20), 8 replicas, sharded by
 # document id; 12.5k documents per GPU (100k at 8 GPUs), weak scaling.
 TREES = dict(per_doc=1000, docs_per_gpu=12_500, replicas=8, window=16, p_delete=0.2, seed=0xC0FFEE05)
@@ -92,20 +92,54 @@ def pmc_traffic(workload, kernel):
     return None if not e or "hbm_bytes_corrected" not in e else e["hbm_bytes_corrected"]
 
 
-def cpu_baseline(s, m):
-    """Oracle restatement (oracle/, test infrastructure) on the first m ops, one core."""
+def cpu_baseline(s, m, doc_off=None, workers=1, batch_cut=20_000):
+    """CPU baseline: the Elm-compiled-to-JS cost model —
+    oracle/crdtree.js (persistent red-black Dicts, cons Lists; test
+    infrastructure) run by `node` on this host, ops pre-decoded, timed around
+    `apply` with process.hrtime. Value = `apply op` one op at a time over the
+    first m ops (same final tree as one Batch, without the O(N^2)
+    lastOperation accumulator); the reference's own `apply (Batch ops)` is
+    timed beside it up to `batch_cut` ops. The C++ restatement
+    (oracle/crdtree_oracle.cpp, mutable maps) is timed on the same sample."""
+    import tempfile
+    from oracle import jsoracle
     from oracle.oracle import lib as olib, _ptr
-    sub = head(s, m)
-    L = olib()
-    t = L.orc_init(0)
-    err = C.c_int64(-1)
-    t0 = time.perf_counter()
-    rc = L.orc_apply(t, 1, 0, m, _ptr(sub["kind"]), _ptr(sub["ts"]), _ptr(sub["path_off"]), _ptr(sub["path"]),
-                     _ptr(sub["val"]), C.byref(err))
-    dt = time.perf_counter() - t0
-    L.orc_free(t)
-    assert rc == 0
-    return m / dt, dt
+    sub = head(s, m) if doc_off is None else s
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        f = os.path.join(td, "batch.bin")
+        jsoracle.write_batch(f, sub, m, doc_off=doc_off)
+        js = jsoracle.run(f, mode="op", workers=workers, timeout=900)
+        out["js"] = js
+        if doc_off is None and batch_cut:
+            out["js_batch"] = jsoracle.run(f, mode="batch", limit=min(batch_cut, m), timeout=900)
+    if doc_off is None:
+        L = olib()
+        t = L.orc_init(0)
+        err = C.c_int64(-1)
+        t0 = time.perf_counter()
+        rc = L.orc_apply(t, 1, 0, m, _ptr(sub["kind"]), _ptr(sub["ts"]), _ptr(sub["path_off"]), _ptr(sub["path"]),
+                         _ptr(sub["val"]), C.byref(err))
+        out["cpp"] = (m / (time.perf_counter() - t0))
+        L.orc_free(t)
+        assert rc == 0
+    return out
+
+
+def cpu_line(cb, what):
+    js = cb["js"]
+    d = {"value": js["ops_per_s"], "unit": "ops/s", "cores": js["workers"], "kind": "port",
+         "sample": f"{what}: oracle/crdtree.js (Elm-compiled-to-JS cost model: persistent RB Dicts, cons Lists), "
+                   f"`apply op` per op, node {js['node']}, {js['workers']} worker(s) on {js['cpu_count']} x "
+                   f"{js['cpu_model']}, --max-old-space-size {js['max_old_space_mb']} MB, {js['seconds']:.1f} s"}
+    if "js_batch" in cb:
+        b = cb["js_batch"]
+        d["reference_batch_mode"] = {"value": b["ops_per_s"], "ops": b["ops"],
+                                     "note": "apply (Batch ops) in one call: O(N^2) lastOperation accumulator "
+                                             "(src/CRDTree.elm:224-232), cut off at this size"}
+    if "cpp" in cb:
+        d["cpp_restatement"] = {"value": cb["cpp"], "note": "oracle/crdtree_oracle.cpp (mutable maps), same sample"}
+    return d
 
 
 def main():
@@ -251,10 +285,8 @@ def main():
         m = args.cpu_sample if args.cpu_sample >= 0 else CPU_SAMPLE[args.workload]
         if m > 0:
             m = min(m, n)
-            ops_s, dt = cpu_baseline(s, m)
-            line["cpu_baseline"] = {"value": ops_s, "unit": "ops/s", "cores": 1, "kind": "port",
-                                    "sample": f"first {m} ops of the same batch, oracle/ C++ restatement, "
-                                              f"{dt:.1f} s (cost grows with the batch: skip walks)"}
+            line["cpu_baseline"] = cpu_line(cpu_baseline(s, m),
+                                            f"first {m} ops of the same batch (cost grows with the batch)")
     if rank == 0:
         print(json.dumps(line), flush=True)
     L.crdtm_tree_destroy(tree)
@@ -366,25 +398,15 @@ def run_trees(args, rank, world, local_rank):
     if rank == 0 and world == 1:
         m = args.cpu_sample if args.cpu_sample >= 0 else CPU_SAMPLE["trees"]
         if m > 0:
-            from oracle.oracle import lib as olib, _ptr
-            Lo = olib()
             host = {k: v.cpu().numpy() for k, v in ot.items()}
-            host["val"] = host["val"].astype(np.uint32)
-            host["path_off"] = host["path_off"].astype(np.uint32)
             ndoc = max(1, min(n_mine, m // per))
-            t0 = time.perf_counter()
-            for d in range(ndoc):
-                a, b = d * per, (d + 1) * per
-                sub = dict(kind=host["kind"][a:b].copy(), ts=host["ts"][a:b].copy(), val=host["val"][a:b].copy(),
-                           path_off=np.arange(per + 1, dtype=np.uint32), path=host["path"][a:b].copy())
-                t = Lo.orc_init(0)
-                err = C.c_int64(-1)
-                Lo.orc_apply(t, 1, 0, per, _ptr(sub["kind"]), _ptr(sub["ts"]), _ptr(sub["path_off"]),
-                             _ptr(sub["path"]), _ptr(sub["val"]), C.byref(err))
-                Lo.orc_free(t)
-            dt = time.perf_counter() - t0
-            line["cpu_baseline"] = {"value": ndoc * per / dt, "unit": "ops/s", "cores": 1, "kind": "port",
-                                    "sample": f"{ndoc} documents x {per} ops, oracle/ C++ restatement, {dt:.1f} s"}
+            sub = dict(kind=host["kind"][:ndoc * per], ts=host["ts"][:ndoc * per],
+                       val=host["val"][:ndoc * per].astype(np.uint32),
+                       path_off=np.arange(ndoc * per + 1, dtype=np.uint32), path=host["path"][:ndoc * per])
+            workers = min(16, os.cpu_count() or 1)
+            cb = cpu_baseline(sub, ndoc * per, doc_off=np.arange(ndoc + 1, dtype=np.uint32) * per, workers=workers)
+            line["cpu_baseline"] = cpu_line(cb, f"{ndoc} documents x {per} ops, documents round-robin over "
+                                                f"worker_threads")
     if rank == 0:
         print(json.dumps(line), flush=True)
     L.crdtm_ctx_destroy(ctx)
