@@ -82,6 +82,9 @@ struct DevResult {
   uint32_t pdr_dicts;       // per-dict replay: dicts of the new state
   uint32_t pdr_slots;       // per-dict replay: slots of the new state
   uint32_t since_end;       // operationsSince: 1 + log index of the newest Add with the asked ts
+  uint32_t fl_keys;         // flat: Adds with a timestamp slot
+  uint32_t fl_slow;         // flat: ops that need per-op statuses (empty path, ts 0)
+  uint32_t fl_part[16 * 32];  // flat: slots holding an Add, 16 partial counts one cache line apart
 };
 
 #define HIP_CHECK(x)                                                                         \

@@ -183,23 +183,23 @@ int linearize(crdtm_tree* t);  // fills t->d.doc / t->doc_n from the tree state
 int forest_apply(crdtm_ctx* c, int64_t replica_id, const OpsDev& o, const uint32_t* doc_off_host, uint64_t n_docs,
                  int32_t* code, int64_t* err, uint32_t* applied, uint64_t* vhash, uint64_t* vwords, int64_t* tstamp);
 uint64_t forest_ws_bytes(const uint32_t* doc_off_host, uint64_t n_docs, uint64_t n_ops, uint64_t n_path);
-void mark_begin(crdtm_ctx* c);
-void mark(crdtm_ctx* c, const char* name);
+void mark_begin(crdtm_ctx* c, hipStream_t st);
+void mark(crdtm_ctx* c, const char* name, hipStream_t st);
 // Profiling hook: when the current context profiles, every launch is
 // bracketed by two HIP events on the launch stream, so each kernel's device
 // time is measured on its own (no host gaps between launches).
 extern thread_local crdtm_ctx* g_prof;
-inline void prof_begin() {
-  if (g_prof) mark_begin(g_prof);
+inline void prof_begin(hipStream_t st) {
+  if (g_prof) mark_begin(g_prof, st);
 }
-inline void prof_mark(const char* name) {
-  if (g_prof) mark(g_prof, name);
+inline void prof_mark(const char* name, hipStream_t st) {
+  if (g_prof) mark(g_prof, name, st);
 }
 #define LAUNCH(k, grid, block, shm, st, ...)                    \
   do {                                                          \
-    ::crdtm::prof_begin();                                      \
+    ::crdtm::prof_begin(st);                                    \
     hipLaunchKernelGGL(k, grid, block, shm, st, __VA_ARGS__);   \
-    ::crdtm::prof_mark(#k);                                     \
+    ::crdtm::prof_mark(#k, st);                                 \
   } while (0)
 
 }  // namespace crdtm

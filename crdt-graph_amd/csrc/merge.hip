@@ -1696,30 +1696,72 @@ __global__ void __launch_bounds__(64) k_forest(OpsDev o, ForestArgs f, const uin
 
 // K1 (flat). Slot records rec[q] = (index of the first Add of slot q) << 32
 // | (anchor slot of that Add: Q = the dict's sentinel, NONE = anchor key not
-// in the batch); REC_EMPTY = no Add. k_fl_store writes every Add's record
-// with one plain 8-byte store (an arbitrary duplicate wins); k_fl_status
-// then decides every op, and a smaller duplicate that lost the store race
-// takes the slot with a 64-bit atomicMin (op index in the high word) and
-// flags a second status pass.
+// in the batch); REC_EMPTY = no Add.
 constexpr unsigned long long REC_EMPTY = ~0ULL;
 
-__global__ void __launch_bounds__(BLOCK) k_fl_store(OpsDev o, TsIndex x, uint32_t Q, unsigned long long* rec) {
+// K1 (flat), one pass over the ops: every Add writes its slot record with
+// one plain 8-byte store (an arbitrary duplicate wins), and the pass folds
+// what the batch accounting needs when every op applies — the last Add
+// index per replica (replicas table), the own-replica Add count
+// (incrementTimestamp), the Adds with a slot, and the ops that would not
+// apply on their own (empty path: InvalidPath, its smallest index to
+// err_index; ts 0: the sentinel's key, AlreadyApplied). k_fl_check then
+// checks every slot's Add against its anchor and counts the slots: as many
+// slots as keyed Adds means no duplicate timestamps. Only a batch where some
+// op does not apply runs the per-op k_fl_status.
+__global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_t Q, unsigned long long* rec,
+                                                    long long ts0, uint32_t* rtab, DevResult* dres) {
+  __shared__ uint32_t rv[REP_DIRECT];
+  for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) rv[j] = 0;
+  __syncthreads();
+  const long long id0 = replica_of(ts0);
+  uint32_t keys = 0, own = 0, slow = 0, err = NONE;
   QUAD_LOOP_XCD(i0, o.n) {
     Quad qd;
     load_quad(o, i0, qd);
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
-      if (k >= qd.cnt || qd.off[k + 1] == qd.off[k] || qd.ts[k] <= 0) continue;
-      const uint32_t q = tsindex_slot(x, qd.ts[k]);
+      if (k >= qd.cnt) continue;
+      const uint32_t i = i0 + k;
+      if (qd.off[k + 1] == qd.off[k]) {  // update [] = InvalidPath (src/Internal/Node.elm:147-148)
+        ++slow;
+        err = min(err, i);
+        continue;
+      }
+      const long long ts = qd.ts[k];
+      if (replica_of(ts) == id0) ++own;
+      const uint32_t q = tsindex_slot(x, ts);
+      if (q == NONE) {  // ts 0: the sentinel's key (AlreadyApplied)
+        ++slow;
+        continue;
+      }
+      ++keys;
       const long long kk = o.path[qd.off[k]];
       const uint32_t qa = kk == 0 ? Q : tsindex_slot(x, kk);
-      rec[q] = (static_cast<unsigned long long>(i0 + k) << 32) | qa;
+      rec[q] = (static_cast<unsigned long long>(i) << 32) | qa;
+      const uint32_t rr = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32);
+      if (rr < REP_DIRECT) atomicMax(&rv[rr], i + 1);
+      else atomicMax(&rtab[rr + (1u << (REPLICA_BITS - 1))], i + 1);
     }
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x)
+    if (rv[j]) atomicMax(&rtab[j + (1u << (REPLICA_BITS - 1))], rv[j]);
+  keys = block_sum(keys);
+  own = block_sum(own);
+  slow = block_sum(slow);
+  err = block_min(err);
+  if (threadIdx.x == 0) {
+    if (keys) atomicAdd(&dres->fl_keys, keys);
+    if (own) atomicAdd(&dres->own_ok_adds, own);
+    if (slow) atomicAdd(&dres->fl_slow, slow);
+    if (err != NONE) atomicMin(&dres->err_index, err);
   }
 }
 
 // Status of every op (update / addAfterHelp, src/Internal/Node.elm:56-90,
-// :138-163), fused with the batch accounting and the replicas fold: every
+// :138-163) when some op does not apply (k_fl_claim's records are final by
+// then), fused with the batch accounting and the replicas fold: every
 // applied Add's replica keeps its last op index in a direct-mapped LDS table
 // (ids < REP_DIRECT), flushed once per workgroup into the replica table.
 __global__ void __launch_bounds__(BLOCK) k_fl_status(OpsDev o, uint8_t* st, TsIndex x, uint32_t Q,
@@ -1900,6 +1942,35 @@ struct RunHeadGen {
   }
 };
 
+// Per-slot check of k_fl_claim's records (addAfterHelp,
+// src/Internal/Node.elm:68-70): the Add of slot q applies iff its anchor is
+// the sentinel or a slot whose Add comes earlier in the batch, else it fails
+// (NotFound -> OperationFailed); the smallest failing index goes to
+// err_index. Counts the slots holding an Add (fl_part[0]).
+__global__ void __launch_bounds__(BLOCK) k_fl_check(uint32_t Q, const unsigned long long* rec, DevResult* dres) {
+  uint32_t present = 0, err = NONE;
+  const uint32_t npair = Q / 2;
+  GRID_STRIDE(k, npair + (Q & 1)) {
+    const bool pair = k < npair;
+    const ulonglong2 x = pair ? *reinterpret_cast<const ulonglong2*>(rec + 2 * k) : make_ulonglong2(rec[Q - 1], REC_EMPTY);
+    const unsigned long long r2[2] = {x.x, x.y};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const unsigned long long r = r2[j];
+      if (r == REC_EMPTY) continue;
+      ++present;
+      const uint32_t fi = static_cast<uint32_t>(r >> 32), qa = static_cast<uint32_t>(r);
+      if (qa != Q && (qa == NONE || static_cast<uint32_t>(rec[qa] >> 32) >= fi)) err = min(err, fi);
+    }
+  }
+  present = block_sum(present);
+  err = block_min(err);
+  if (threadIdx.x == 0) {
+    if (present) atomicAdd(&dres->fl_part[32 * (blockIdx.x & 15)], present);
+    if (err != NONE) atomicMin(&dres->err_index, err);
+  }
+}
+
 // Counting-sort scatter; single-child parents (the common case in a typing
 // stream) take a plain store. The root sentinel's children are placed by
 // k_fl_root_* instead (already in order, no sort).
@@ -2064,21 +2135,21 @@ __global__ void __launch_bounds__(BLOCK) k_fl_log_copy(OpsDev o, TreeDev T) {
 // ---------------------------------------------------------------------------
 thread_local crdtm_ctx* g_prof = nullptr;
 
-void mark_begin(crdtm_ctx* c) {
+void mark_begin(crdtm_ctx* c, hipStream_t st) {
   if (!c->profile) return;
   if (c->pending) hipEventDestroy(c->pending);
   c->pending = nullptr;
   hipEvent_t e;
   if (hipEventCreate(&e) != hipSuccess) return;
-  hipEventRecord(e, c->stream);
+  hipEventRecord(e, st);
   c->pending = e;
 }
 
-void mark(crdtm_ctx* c, const char* name) {
+void mark(crdtm_ctx* c, const char* name, hipStream_t st) {
   if (!c->profile || !c->pending) return;
   hipEvent_t e;
   if (hipEventCreate(&e) != hipSuccess) return;
-  hipEventRecord(e, c->stream);
+  hipEventRecord(e, st);
   c->marks.push_back({name, c->pending, e});
   c->pending = nullptr;
 }
@@ -2305,15 +2376,32 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   uint32_t* cnt = ws.alloc<uint32_t>(U + 1);
   uint32_t* fill = ws.alloc<uint32_t>(U + 1);
   LAUNCH(k_fl_init, dim3(grid_for(U + 1, BLOCK, 4096)), dim3(BLOCK), 0, s, Q, rec, cnt, fill);
-  LAUNCH(k_fl_store, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix, Q, rec);
-  LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, rec, t->timestamp, c->rtab, dr);
+  LAUNCH(k_fl_claim, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix, Q, rec, t->timestamp, c->rtab, dr);
+  LAUNCH(k_fl_check, dim3(grid_for(Q / 2 + 1, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, rec, dr);
   int r;
   if ((r = sync_read(c))) return r;
-  if (c->hres->dup_fix) {  // duplicate timestamps: the records are final now, decide again
-    LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr, nullptr);
-    LAUNCH(k_fl_stat_reset, dim3(1), dim3(1), 0, s, dr);
-    LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, rec, t->timestamp, c->rtab, dr);
-    if ((r = sync_read(c))) return r;
+  {
+    const DevResult& h0 = *c->hres;
+    uint32_t present = 0;
+    for (int k = 0; k < 16; ++k) present += h0.fl_part[32 * k];
+    const bool every = h0.err_index == NONE && h0.fl_slow == 0 && present == h0.fl_keys && h0.fl_keys == n;
+    if (every) {  // every op is the only Add of its timestamp and applies
+      c->hres->n_applied = n;
+      c->hres->n_adds_applied = n;
+      c->hres->n_already = 0;
+    } else {  // per-op statuses: duplicates, ts 0, errors
+      LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr, nullptr);
+      LAUNCH(k_fl_stat_reset, dim3(1), dim3(1), 0, s, dr);
+      LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, rec, t->timestamp, c->rtab, dr);
+      if ((r = sync_read(c))) return r;
+      if (c->hres->dup_fix) {  // a smaller duplicate took its slot: the records are final now, decide again
+        LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr,
+               nullptr);
+        LAUNCH(k_fl_stat_reset, dim3(1), dim3(1), 0, s, dr);
+        LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, rec, t->timestamp, c->rtab, dr);
+        if ((r = sync_read(c))) return r;
+      }
+    }
   }
   const DevResult h1 = *c->hres;
   uint32_t guard = 0;
@@ -2372,20 +2460,14 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     }
     if ((r = segmented_sort_desc_id(cnt, U, carr, U, ws, s, dr, Q))) return r;
     LAUNCH(k_fl_links, dim3(gq), dim3(BLOCK), 0, s, anc, cnt, n_child, carr, ns);
-    // ---- K4: Euler tour + list ranking -> document order ----
     uint32_t* qc = nullptr;
     if (Q != K) {  // slots with no node: compact
       qc = ws.alloc<uint32_t>(Q);
       LAUNCH(k_fl_present, dim3(gq), dim3(BLOCK), 0, s, Q, anc, qc);
       if ((r = scan_excl_u32(qc, qc, Q, nullptr, ws, s))) return r;
     }
-    if ((r = list_rank_fused(FlatEulerSrc{Q, anc, cnt, carr, ns}, 2ULL * U, 2 * Q, FlatDocSink{Q, t->d.doc, qc}, ws,
-                             s)))
-      return r;
-    LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d);
-    // ---- commit ----
     uint32_t* logidx = nullptr;
-    if (!all_applied) {
+    if (!all_applied) {  // compacted log (its scans share the ctx scan pool: main stream)
       logidx = ws.alloc<uint32_t>(n + 1);
       uint32_t* plen = ws.alloc<uint32_t>(n + 1);
       LAUNCH(k_post_flags, dim3(g), dim3(BLOCK), 0, s, o, st, logidx, plen);
@@ -2394,10 +2476,21 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
       LAUNCH(k_log, dim3(g), dim3(BLOCK), 0, s, o, st, t->d, 0u, 0u, logidx, plen);
       LAUNCH(k_log_tail, dim3(1), dim3(1), 0, s, t->d, 0u, &dr->log_n, 0u, &dr->log_npath);
     }
+    // ---- commit ----
+    // (Measured: running the commit and the log copy on the ctx side stream
+    // while the list ranking runs does not shorten the merge — the ranking
+    // kernels keep every CU busy, the copies just stretch — so one stream.)
     LAUNCH(k_fl_commit, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, o, ix, Q, maxr + 1, anc, rec, qc, logidx,
            t->d);
+    if (all_applied) LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
+    // ---- K4: Euler tour + list ranking -> document order ----
+    if ((r = list_rank_fused(FlatEulerSrc{Q, anc, cnt, carr, ns}, 2ULL * U, 2 * Q, FlatDocSink{Q, t->d.doc, qc}, ws,
+                             s)))
+      return r;
+    LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d);
+  } else if (all_applied) {
+    LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
   }
-  if (all_applied) LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
   long long* rep = ws.alloc<long long>(2 * static_cast<uint64_t>(maxr) + 2);
   LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, rep,
          &dr->n_replica_out);

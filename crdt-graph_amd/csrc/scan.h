@@ -168,10 +168,10 @@ int dscan(GEN gen, uint32_t* out, uint64_t n, uint32_t* total, Arena& ws, hipStr
     HIP_CHECK(hipMemsetAsync(status, 0, (tiles + 1) * sizeof(unsigned long long), st));
   }
   auto* kfn = &k_dscan<OP, INCL, GEN>;
-  prof_begin();
+  prof_begin(st);
   hipLaunchKernelGGL(kfn, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, gen, out, n, status, ticket,
                      static_cast<uint32_t>(tiles), ws.scan_epoch, total, err);
-  prof_mark("k_dscan");
+  prof_mark("k_dscan", st);
   return CRDTM_OK;
 }
 

@@ -217,3 +217,52 @@ def test_forest_matches_oracle_per_document():
     et.apply_arrays(sub, b - a)
     _, nw, hh = et.canonical(1, full=False)
     assert (nw, hh) == (int(out["words"][d]), int(out["hash"][d]))
+
+
+def _flat_variant(s, edits):
+    """Rebuild a flat stream (path length 1) with edits: ('ins', k, ts, anchor)
+    inserts an Add at position k; ('empty', k) inserts an Add with path []."""
+    n = len(s["kind"])
+    rows = [(int(s["ts"][i]), [int(s["path"][s["path_off"][i]])], int(s["val"][i])) for i in range(n)]
+    for e in sorted(edits, key=lambda e: -e[1]):
+        if e[0] == "ins":
+            rows.insert(e[1], (e[2], [e[3]], 7))
+        else:
+            rows.insert(e[1], (e[2], [], 7))
+    m = len(rows)
+    off = np.zeros(m + 1, np.uint32)
+    off[1:] = np.cumsum([len(r[1]) for r in rows])
+    path = np.array([x for r in rows for x in r[1]] + [0], np.int64)
+    return dict(kind=np.zeros(m, np.uint8), ts=np.array([r[0] for r in rows], np.int64), path_off=off, path=path,
+                val=np.array([r[2] for r in rows], np.uint32)), m
+
+
+@pytest.mark.parametrize("case", ["dup_later", "dup_earlier", "ts_zero", "empty_path", "anchor_later",
+                                  "anchor_missing", "clean"])
+def test_flat_closed_form_edges(case):
+    """The flat closed form's one-pass claim + per-slot anchor check, and its
+    per-op fallback (duplicates, ts 0, errors), against the oracle."""
+    s, n = synth_case(n_ops=20000, replicas=16, window=64, seed=0xC0FFEE03)
+    ts, anc = s["ts"], s["path"]
+    edits = {
+        "clean": [],
+        "dup_later": [("ins", 15000, int(ts[100]), int(anc[100])), ("ins", 18000, int(ts[9000]), 0)],
+        "dup_earlier": [("ins", 12000, int(ts[15000]), int(ts[50]))],
+        "ts_zero": [("ins", 500, 0, 0)],
+        "empty_path": [("empty", 7000, int(ts[3]))],
+        "anchor_later": [("ins", 4000, (40 << 32) + 5, (41 << 32) + 5), ("ins", 9000, (41 << 32) + 5, 0)],
+        "anchor_missing": [("ins", 11000, (42 << 32) + 1, (43 << 32) + 9)],
+    }[case]
+    v, m = _flat_variant(s, edits)
+    ot, rc, oerr = oracle_apply_arrays(v, m)
+    et = CRDTree.init(0)
+    res = et.apply_arrays(v, m)
+    assert res.path_taken == N.PATH_CLOSED_FORM
+    assert res.code == rc, (case, res.code, rc)
+    if rc != 0:
+        assert res.err_index == oerr
+        return
+    assert (res.n_applied, res.n_already) == (len(oracle_log(ot, 0)[0]), m - len(oracle_log(ot, 0)[0]))
+    assert engine_summary(et) == oracle_summary(ot)
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
