@@ -388,7 +388,8 @@ def run_trees(args, rank, world, local_rank):
                    "replicas": TREES["replicas"], "documents_ok": ok_docs,
                    "parallelism": f"documents sharded by id over {world} GPU(s); op logs all-gathered (RCCL)"},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": B_alg / t_dom / 1e9, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": B_alg / t_dom / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": B_alg / t_dom / 1e9 / HBM_PEAK_GBS,
+                     "traffic": pmc_traffic("trees", dominant),
                      "alg_bytes_per_launch": B_alg, "kernel_ms": t_dom * 1e3, "kernels_ms_per_step": kernels_ms,
                      "merge_frac": B_alg / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS},
     }

@@ -12,6 +12,9 @@
 //       entries off the list.
 #pragma once
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "engine.h"
 
 namespace crdtm {
@@ -252,6 +255,8 @@ int list_rank_fused(SRC srcf, uint64_t n, uint32_t head, SINK sink, Arena& ws, h
   LAUNCH(k_lc_link, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, toff, hidx, sp_succ, sp_w, rsucc, rw);
   HIP_CHECK(hipStreamSynchronize(st));
   const uint32_t H = hv[0], rhead = hv[1];
+  if (std::getenv("CRDTM_LR_STATS")) std::fprintf(stderr, "crdtm list ranking: %llu entries -> %u chains\n",
+                                                  static_cast<unsigned long long>(n), H);
   unsigned long long* rexcl = ws.alloc<unsigned long long>(static_cast<uint64_t>(H) + 1);
   if (H == 0 || rhead == NONE) {
     HIP_CHECK(hipMemsetAsync(rexcl, 0xFF, (static_cast<uint64_t>(H) + 1) * sizeof(unsigned long long), st));
