@@ -378,8 +378,17 @@ struct LevelStart {
   uint32_t v[MAXLV_BUCKET + 1];
 };
 
+// A level-list entry carries what the level kernels would otherwise fetch
+// through dependent loads: the op, its path offset and its parent key
+// (path[L-2], 0 for |path| < 2), written by the streaming k_len_scatter.
+struct LvEnt {
+  uint32_t i, b;
+  long long kp;
+};
+static_assert(sizeof(LvEnt) == 16, "one 16-byte load per entry");
+
 __global__ void __launch_bounds__(BLOCK) k_len_scatter(OpsDev o, uint32_t maxlen, LevelStart start,
-                                                       uint32_t* fill, uint32_t* lists) {
+                                                       uint32_t* fill, LvEnt* lists) {
   __shared__ uint32_t hist[MAXLV_BUCKET + 1];
   __shared__ uint32_t base[MAXLV_BUCKET + 1];
   const uint32_t n = o.n;
@@ -387,11 +396,12 @@ __global__ void __launch_bounds__(BLOCK) k_len_scatter(OpsDev o, uint32_t maxlen
   for (uint32_t c0 = blockIdx.x * chunk; c0 < n; c0 += gridDim.x * chunk) {
     for (uint32_t j = threadIdx.x; j <= maxlen; j += blockDim.x) hist[j] = 0;
     __syncthreads();
-    uint32_t L[8], r[8];
+    uint32_t L[8], r[8], b[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const uint32_t i = c0 + u * BLOCK + threadIdx.x;
-      L[u] = i < n ? op_len(o, i) : NONE;
+      b[u] = i < n ? o.off[i] : 0u;
+      L[u] = i < n ? o.off[i + 1] - b[u] : NONE;
       r[u] = (L[u] != NONE) ? atomicAdd(&hist[L[u]], 1u) : 0u;
     }
     __syncthreads();
@@ -401,23 +411,38 @@ __global__ void __launch_bounds__(BLOCK) k_len_scatter(OpsDev o, uint32_t maxlen
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const uint32_t i = c0 + u * BLOCK + threadIdx.x;
-      if (L[u] != NONE) lists[base[L[u]] + r[u]] = i;
+      if (L[u] != NONE) {
+        LvEnt e;
+        e.i = i;
+        e.b = b[u];
+        e.kp = L[u] >= 2 ? o.path[b[u] + L[u] - 2] : 0;
+        *reinterpret_cast<uint4*>(&lists[base[L[u]] + r[u]]) = *reinterpret_cast<const uint4*>(&e);
+      }
     }
     __syncthreads();
   }
 }
 
 // L1: the dict of every op of length j (fast prefix check, else the walk).
-__global__ void __launch_bounds__(BLOCK) k_lv_dict(OpsDev o, Work w, TsIndex h, const uint32_t* list, uint32_t cnt,
+// The prefix compare of paths up to LV_UNROLL keys is unrolled with
+// level-uniform predicates, so the op's own keys load before the parent
+// lookup resolves and the parent's keys load together.
+constexpr uint32_t LV_UNROLL = 14;
+__global__ void __launch_bounds__(BLOCK) k_lv_dict(OpsDev o, Work w, TsIndex h, const LvEnt* list, uint32_t cnt,
                                                    uint32_t j) {
   const uint32_t n = o.n;
   GRID_STRIDE(q, cnt) {
-    const uint32_t i = list[q];
-    const uint32_t b = o.off[i];
+    const uint4 ev = *reinterpret_cast<const uint4*>(&list[q]);
+    const uint32_t i = ev.x, b = ev.y;
     uint32_t cur = n;
     uint8_t s = ST_PENDING;
     if (j > 1) {
-      const long long kp = o.path[b + j - 2];
+      const long long kp = static_cast<long long>((static_cast<unsigned long long>(ev.w) << 32) | ev.z);
+      long long own[LV_UNROLL];
+      if (j - 2 <= LV_UNROLL) {
+#pragma unroll
+        for (uint32_t l = 0; l < LV_UNROLL; ++l) own[l] = l + 2 < j ? o.path[b + l] : 0;
+      }
       const uint32_t g = kp == 0 ? NONE : tsindex_find(h, kp);
       bool fast = g != NONE && g < i;
       uint32_t dg = NONE;
@@ -427,7 +452,14 @@ __global__ void __launch_bounds__(BLOCK) k_lv_dict(OpsDev o, Work w, TsIndex h, 
         dg = r.w;
         // independent loads (no early exit) so they issue together
         unsigned long long diff = 0;
-        for (uint32_t l = 0; l + 2 < j; ++l) diff |= static_cast<unsigned long long>(o.path[bg + l] ^ o.path[b + l]);
+        if (j - 2 <= LV_UNROLL) {
+#pragma unroll
+          for (uint32_t l = 0; l < LV_UNROLL; ++l)
+            if (l + 2 < j) diff |= static_cast<unsigned long long>(o.path[bg + l] ^ own[l]);
+        } else {
+          for (uint32_t l = 0; l + 2 < j; ++l)
+            diff |= static_cast<unsigned long long>(o.path[bg + l] ^ o.path[b + l]);
+        }
         fast = nrec_len(r) == j - 1 && nrec_st(r) == ST_APPLIED && diff == 0;
       }
       if (fast && dg < i) {
@@ -476,13 +508,14 @@ __global__ void __launch_bounds__(BLOCK) k_lv_dict(OpsDev o, Work w, TsIndex h, 
 // L2: leaf lookup; collisions (the closed form names a node by its ts alone);
 // the first Delete of a node that reaches it while its dict is live
 // (deleteHelp, src/Internal/Node.elm:112-122).
-__global__ void __launch_bounds__(BLOCK) k_lv_leaf(OpsDev o, Work w, TsIndex h, const uint32_t* list, uint32_t cnt,
+__global__ void __launch_bounds__(BLOCK) k_lv_leaf(OpsDev o, Work w, TsIndex h, const LvEnt* list, uint32_t cnt,
                                                    uint32_t j, DevResult* dres) {
   GRID_STRIDE(q, cnt) {
-    const uint32_t i = list[q];
+    const uint2 ev = *reinterpret_cast<const uint2*>(&list[q]);
+    const uint32_t i = ev.x;
     if (w.st[i] != ST_PENDING) continue;
     const uint32_t cur = w.cur[i];
-    const uint32_t tgt = lookup_child(o, w, h, cur, o.path[o.off[i] + j - 1], j);
+    const uint32_t tgt = lookup_child(o, w, h, cur, o.path[ev.y + j - 1], j);
     w.leaf[i] = tgt;
     if (o.kind[i] == CRDTM_ADD) {
       const long long ts = o.ts[i];
@@ -505,11 +538,11 @@ __global__ void __launch_bounds__(BLOCK) k_lv_leaf(OpsDev o, Work w, TsIndex h, 
 
 // L3: statuses of the ops that reached their dict; the chain death time of
 // each new node (its own first Delete, or an ancestor's).
-__global__ void __launch_bounds__(BLOCK) k_lv_fin(OpsDev o, Work w, TsIndex h, const uint32_t* list, uint32_t cnt,
+__global__ void __launch_bounds__(BLOCK) k_lv_fin(OpsDev o, Work w, TsIndex h, const LvEnt* list, uint32_t cnt,
                                                   uint32_t j) {
   const uint32_t n = o.n;
   GRID_STRIDE(q, cnt) {
-    const uint32_t i = list[q];
+    const uint32_t i = list[q].i;
     if (w.st[i] != ST_PENDING) continue;
     w.tag[i] = PDR_REACHED;
     if (o.kind[i] == CRDTM_DELETE) {
@@ -2598,7 +2631,7 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
     // bucket the ops by |path| (one small copy back for the level sizes)
     uint32_t* lcnt = ws.alloc<uint32_t>(2 * (MAXLV_BUCKET + 1));
     uint32_t* lfill = lcnt + (MAXLV_BUCKET + 1);
-    uint32_t* lists = ws.alloc<uint32_t>(n);
+    LvEnt* lists = ws.alloc<LvEnt>(n);
     w.nrec = ws.alloc<uint4>(n);
     LAUNCH(k_nrec_init, dim3(g), dim3(BLOCK), 0, s, o, w);
     HIP_CHECK(hipMemsetAsync(lcnt, 0, 2 * (MAXLV_BUCKET + 1) * sizeof(uint32_t), s));
@@ -2616,7 +2649,7 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
     for (uint32_t lvl = 1; lvl <= maxlen; ++lvl) {
       const uint32_t c = hc[lvl];
       if (!c) continue;
-      const uint32_t* lst = lists + hs.v[lvl];
+      const LvEnt* lst = lists + hs.v[lvl];
       const uint32_t gl = grid_for(c);
       LAUNCH(k_lv_dict, dim3(gl), dim3(BLOCK), 0, s, o, w, ix, lst, c, lvl);
       LAUNCH(k_lv_leaf, dim3(gl), dim3(BLOCK), 0, s, o, w, ix, lst, c, lvl, dr);
