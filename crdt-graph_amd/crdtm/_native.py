@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcrdtm.so")
+# CRDTM_LIB: load another build of the engine (same-box A/B measurements)
+LIB_PATH = os.environ.get("CRDTM_LIB") or os.path.join(_HERE, "libcrdtm.so")
 
 CRDTM_OK = 0
 PATH_CLOSED_FORM = 1

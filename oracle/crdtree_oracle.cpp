@@ -18,6 +18,7 @@
 // Pinned by: the 83 reference tests transcribed in tests/test_oracle_kat.py
 // and the hand-traced vectors of SURVEY.md Appendix C.
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -622,3 +623,138 @@ void orc_merge_last(orc_tree* o, const orc_tree* prev) {
 }
 
 }  // extern "C"
+
+// ---- flat fast restatement (test infrastructure) ----
+// The same findInsertion / addAfterHelp semantics (src/Internal/Node.elm:56-104)
+// specialised to an Adds-only batch on a fresh tree whose paths all have
+// length 1 (one dict, no Tombstone besides the sentinel, so no copy quirk):
+// the dict is an array of keys in ascending order with a `next` link per
+// key, so a 10M-op batch replays in seconds instead of the general
+// restatement's minutes. Used for full-size parity of config 3; pinned
+// against orc_apply by tests/test_oracle_kat.py. Returns 0 (Ok), 3
+// (OperationFailed) with *err_index, or -1 when the batch is outside the
+// specialisation (a Delete, a path of length != 1). hash[0..1] / words[0..1]
+// receive the canonical structure and visible-order digests (orc_canonical).
+extern "C" int orc_flat_replay(uint64_t n, const uint8_t* kind, const int64_t* ts, const uint32_t* path_off,
+                               const int64_t* path, const uint32_t* val, int64_t* err_index, uint64_t* hash,
+                               uint64_t* words, uint64_t* n_applied) {
+  std::vector<int64_t> keys;
+  keys.reserve(n + 1);
+  keys.push_back(0);
+  for (uint64_t i = 0; i < n; ++i) {
+    if (kind[i] != 0 || path_off[i + 1] - path_off[i] != 1) return -1;
+    keys.push_back(ts[i]);
+  }
+  std::sort(keys.begin(), keys.end());
+  keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+  const size_t K = keys.size();
+  auto slot = [&](int64_t k) -> int64_t {
+    auto it = std::lower_bound(keys.begin(), keys.end(), k);
+    return (it != keys.end() && *it == k) ? it - keys.begin() : -1;
+  };
+  constexpr uint32_t NIL = 0xFFFFFFFFu;
+  std::vector<uint32_t> nxt(K, NIL), v(K, 0);
+  std::vector<uint8_t> made(K, 0);
+  const int64_t z = slot(0);
+  made[z] = 1;  // the sentinel 0 -> Tombstone [] Nothing
+  uint64_t applied = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    const int64_t x = slot(ts[i]);  // always found
+    if (made[x]) continue;          // child ts parent exists: AlreadyApplied (the sentinel too)
+    const int64_t a = slot(path[path_off[i]]);
+    if (a < 0 || !made[a]) {        // anchor missing: NotFound -> OperationFailed
+      *err_index = static_cast<int64_t>(i);
+      return 3;
+    }
+    // findInsertion: slot order is key order, and no node but the sentinel is a Tombstone
+    uint32_t node = static_cast<uint32_t>(a);
+    for (;;) {
+      const uint32_t rn = nxt[node];
+      if (rn == NIL || x > static_cast<int64_t>(rn)) break;
+      node = rn;
+    }
+    nxt[x] = nxt[node];
+    nxt[node] = static_cast<uint32_t>(x);
+    v[x] = val[i];
+    made[x] = 1;
+    ++applied;
+  }
+  *n_applied = applied;
+  // canonical dumps, same words as dumpDict / dumpVisible
+  Sink s0{nullptr}, s1{nullptr};
+  for (size_t q = 0; q < K; ++q) {
+    if (!made[q]) continue;
+    const bool hn = nxt[q] != NIL;
+    s0.put(0);
+    s0.put(keys[q]);
+    s0.put(static_cast<int64_t>(q) == z ? TOMB : NODE);
+    s0.put(hn ? 1 : 0);
+    s0.put(hn ? keys[nxt[q]] : 0);
+    s0.put(static_cast<int64_t>(q) == z ? 0 : static_cast<int64_t>(v[q]));
+    if (static_cast<int64_t>(q) == z) {
+      s0.put(0);
+      continue;
+    }
+    s0.put(1);
+    s0.put(keys[q]);
+    // its children: emptyChildren = {0: Tombstone [] Nothing}
+    s0.put(1); s0.put(0); s0.put(TOMB); s0.put(0); s0.put(0); s0.put(0); s0.put(0);
+  }
+  for (uint32_t q = nxt[z]; q != NIL; q = nxt[q]) {
+    s1.put(0);
+    s1.put(static_cast<int64_t>(v[q]));
+    s1.put(1);
+    s1.put(keys[q]);
+  }
+  hash[0] = s0.h;
+  hash[1] = s1.h;
+  words[0] = s0.n;
+  words[1] = s1.n;
+  return 0;
+}
+
+// ---- full-size property check of a flat merge (test infrastructure) ----
+// For an Adds-only batch with paths of length 1 on a fresh tree, every
+// findInsertion walk (src/Internal/Node.elm:93-104) skips only keys larger
+// than the inserted one, and a later insertion lands between an anchor and
+// x only if it is larger than x (induction on the batch); so in the final
+// document order: (1) every applied key appears once, (2) each key comes
+// after its anchor, (3) every key strictly between the anchor and the key
+// is larger than the key, i.e. the nearest smaller key to its left is at or
+// before the anchor (the sentinel sits before position 0). O(n log n).
+// Returns the number of violations (0 = the order has all three properties).
+extern "C" uint64_t orc_flat_check(uint64_t n_doc, const int64_t* doc_keys, uint64_t n, const int64_t* ts,
+                                   const uint32_t* path_off, const int64_t* path) {
+  std::vector<std::pair<int64_t, int64_t>> kp(n_doc);
+  for (uint64_t p = 0; p < n_doc; ++p) kp[p] = {doc_keys[p], static_cast<int64_t>(p)};
+  std::sort(kp.begin(), kp.end());
+  uint64_t bad = 0;
+  for (uint64_t p = 1; p < n_doc; ++p)
+    if (kp[p].first == kp[p - 1].first) ++bad;  // a key twice
+  auto pos = [&](int64_t k) -> int64_t {
+    auto it = std::lower_bound(kp.begin(), kp.end(), std::make_pair(k, INT64_MIN));
+    return (it != kp.end() && it->first == k) ? it->second : -2;
+  };
+  std::vector<int64_t> ps(n_doc), st;  // nearest smaller key to the left (monotonic stack)
+  st.reserve(1024);
+  for (uint64_t p = 0; p < n_doc; ++p) {
+    while (!st.empty() && doc_keys[st.back()] > doc_keys[p]) st.pop_back();
+    ps[p] = st.empty() ? -1 : st.back();
+    st.push_back(static_cast<int64_t>(p));
+  }
+  uint64_t seen = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (path_off[i + 1] - path_off[i] != 1) return ~0ULL;
+    const int64_t px = pos(ts[i]);
+    if (px < 0) {
+      ++bad;  // an applied key missing from the document
+      continue;
+    }
+    ++seen;
+    const int64_t a = path[path_off[i]];
+    const int64_t pa = a == 0 ? -1 : pos(a);
+    if (pa == -2 || pa >= px || ps[px] > pa) ++bad;
+  }
+  if (seen != n_doc) ++bad;
+  return bad;
+}

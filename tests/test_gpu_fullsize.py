@@ -1,0 +1,61 @@
+"""Full-size GPU checks (BASELINE.json config 3: 10M flat inserts, 64
+replicas) through size-independent properties, where the general CPU
+restatement would take hours (its findInsertion walks grow with the
+document).
+
+* every op applies, the document holds each key once, the visible-order
+  walk of the committed `next` chain (host) and the device linearisation
+  (`doc`) give the same values;
+* the RGA order properties of oracle/crdtree_oracle.cpp `orc_flat_check`:
+  each key after its anchor, every key between them larger (what every
+  findInsertion walk guarantees for an Adds-only flat batch);
+* the first 1M ops of the same stream: canonical structure and visible
+  digests equal the fast flat restatement's (`orc_flat_replay`, pinned
+  against the general restatement in tests/test_oracle_kat.py).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from crdtm import _native as N  # noqa: E402
+from crdtm.tree import CRDTree  # noqa: E402
+from oracle.oracle import _ptr, lib as olib  # noqa: E402
+
+CFG3 = dict(replicas=64, window=256, seed=0xC0FFEE03)
+
+
+def test_flat10m_order_properties():
+    n = 10_000_000
+    s = N.synth(n_ops=n, **CFG3)
+    t = CRDTree.init(0)
+    res = t.apply_arrays(s, n)
+    assert res.code == 0 and res.path_taken == N.PATH_CLOSED_FORM
+    assert res.n_applied == n
+    words, nw, _ = t.canonical(1, full=True)
+    assert nw == 4 * n
+    keys = words[3::4].copy()
+    assert np.array_equal(words[2::4], np.ones(n, np.int64)) and not words[0::4].any()
+    # device linearisation == host walk of the next chain
+    assert np.array_equal(t.document_handles().astype(np.int64), words[1::4])
+    bad = olib().orc_flat_check(n, _ptr(keys), n, _ptr(s["ts"]), _ptr(s["path_off"]), _ptr(s["path"]))
+    assert bad == 0, bad
+
+
+def test_flat1m_matches_fast_restatement():
+    m = 1_000_000
+    s = N.synth(n_ops=m, **CFG3)
+    t = CRDTree.init(0)
+    assert t.apply_arrays(s, m).code == 0
+    h = np.zeros(2, np.uint64)
+    w = np.zeros(2, np.uint64)
+    err = C.c_int64(-1)
+    na = C.c_uint64()
+    rc = olib().orc_flat_replay(m, _ptr(s["kind"]), _ptr(s["ts"]), _ptr(s["path_off"]), _ptr(s["path"]),
+                                _ptr(s["val"]), C.byref(err), _ptr(h), _ptr(w), C.byref(na))
+    assert rc == 0 and na.value == m
+    for which in (0, 1):
+        _, enw, eh = t.canonical(which, full=False)
+        assert (enw, eh) == (int(w[which]), int(h[which])), which

@@ -287,3 +287,38 @@ class TestTraversal:
                                lambda t: t.add("b2")]))
         # root: a, b; b's children: b1, b2. walk Nothing: after head a -> b, then b's children after b1 -> b2
         assert [n[1] for n in t.node_query("walk_start")] == ["b", "b2"]
+
+
+@pytest.mark.parametrize("seed", [0xC0FFEE03, 5, 6])
+def test_flat_fast_restatement_matches_general(seed):
+    """orc_flat_replay (the flat, Adds-only specialisation) gives the general
+    restatement's canonical dumps; orc_flat_check accepts that order and
+    rejects a perturbed one."""
+    import ctypes as C
+    import numpy as np
+    from crdtm import _native as N
+    from oracle.oracle import lib, _ptr
+    L = lib()
+    m = 30000
+    s = N.synth(n_ops=m, replicas=8 + seed % 64, window=64, seed=seed)
+    h = np.zeros(2, np.uint64)
+    w = np.zeros(2, np.uint64)
+    err = C.c_int64(-1)
+    na = C.c_uint64()
+    args = (_ptr(s["kind"]), _ptr(s["ts"]), _ptr(s["path_off"]), _ptr(s["path"]), _ptr(s["val"]))
+    assert L.orc_flat_replay(m, *args, C.byref(err), _ptr(h), _ptr(w), C.byref(na)) == 0
+    t = L.orc_init(0)
+    e2 = C.c_int64(-1)
+    assert L.orc_apply(t, 1, 0, m, *args, C.byref(e2)) == 0
+    for which in (0, 1):
+        hh = C.c_uint64()
+        assert (L.orc_canonical(t, which, None, 0, C.byref(hh)), hh.value) == (int(w[which]), int(h[which]))
+    nw = L.orc_canonical(t, 1, None, 0, None)
+    buf = np.zeros(nw, np.int64)
+    L.orc_canonical(t, 1, _ptr(buf), nw, None)
+    L.orc_free(t)
+    keys = buf[3::4].copy()
+    chk = (_ptr(s["ts"]), _ptr(s["path_off"]), _ptr(s["path"]))
+    assert L.orc_flat_check(len(keys), _ptr(keys), m, *chk) == 0
+    keys[100], keys[101] = keys[101], keys[100]
+    assert L.orc_flat_check(len(keys), _ptr(keys), m, *chk) > 0
