@@ -126,11 +126,11 @@ inline uint32_t quad_grid(uint64_t n) {
 // no-return LDS atomics; larger ids go straight to the global table.
 constexpr uint32_t REP_DIRECT = 4096;
 __global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint2* rng, DevResult* dres) {
-  __shared__ uint32_t rlo[REP_DIRECT];
-  __shared__ uint32_t rhi[REP_DIRECT];
-  for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) {
-    rlo[j] = NONE;
-    rhi[j] = 0;
+  __shared__ __attribute__((aligned(16))) uint32_t rlo[REP_DIRECT];
+  __shared__ __attribute__((aligned(16))) uint32_t rhi[REP_DIRECT];
+  for (uint32_t j = threadIdx.x; j < REP_DIRECT / 4; j += blockDim.x) {
+    reinterpret_cast<uint4*>(rlo)[j] = make_uint4(NONE, NONE, NONE, NONE);
+    reinterpret_cast<uint4*>(rhi)[j] = make_uint4(0u, 0u, 0u, 0u);
   }
   __syncthreads();
   uint32_t mx = 0, bad = 0, neg = 0, ndel = 0, maxr = 0;
@@ -155,8 +155,11 @@ __global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint2* rng, DevResult* 
         const uint32_t r = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32), c = static_cast<uint32_t>(ts);
         maxr = max(maxr, r);
         if (r < REP_DIRECT) {
-          atomicMin(&rlo[r], c);
-          atomicMax(&rhi[r], c);
+          // the table only narrows towards the answer: a plain read that
+          // already covers c makes the atomic unnecessary (same-address
+          // reads broadcast, same-address atomics serialise)
+          if (c < rlo[r]) atomicMin(&rlo[r], c);
+          if (c > rhi[r]) atomicMax(&rhi[r], c);
         } else {
           atomicMin(&rng[r].x, c);
           atomicMax(&rng[r].y, c);
@@ -175,8 +178,8 @@ __global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint2* rng, DevResult* 
     const long long v = o.path[np - 1];
     if (v >= TWO53 || v <= -TWO53) bad = 1;
   }
-  __syncthreads();
-  for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) {
+  maxr = block_max(maxr);  // (synchronises the block) only ids <= maxr were touched
+  for (uint32_t j = threadIdx.x; j <= maxr && j < REP_DIRECT; j += blockDim.x) {
     if (rlo[j] != NONE) {
       atomicMin(&rng[j].x, rlo[j]);
       atomicMax(&rng[j].y, rhi[j]);
@@ -185,7 +188,6 @@ __global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint2* rng, DevResult* 
   mx = block_max(mx);
   bad = block_max(bad);
   neg = block_max(neg);
-  maxr = block_max(maxr);
   ndel = block_sum(ndel);
   if (threadIdx.x == 0) {
     if (mx) atomicMax(&dres->max_len, mx);
@@ -1744,11 +1746,12 @@ constexpr unsigned long long REC_EMPTY = ~0ULL;
 // op does not apply runs the per-op k_fl_status.
 __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_t Q, unsigned long long* rec,
                                                     long long ts0, uint32_t* rtab, DevResult* dres) {
-  __shared__ uint32_t rv[REP_DIRECT];
-  for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) rv[j] = 0;
+  __shared__ __attribute__((aligned(16))) uint32_t rv[REP_DIRECT];
+  for (uint32_t j = threadIdx.x; j < REP_DIRECT / 4; j += blockDim.x)
+    reinterpret_cast<uint4*>(rv)[j] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
   const long long id0 = replica_of(ts0);
-  uint32_t keys = 0, own = 0, slow = 0, err = NONE;
+  uint32_t keys = 0, own = 0, slow = 0, err = NONE, mr = 0;
   QUAD_LOOP_XCD(i0, o.n) {
     Quad qd;
     load_quad(o, i0, qd);
@@ -1773,12 +1776,16 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
       const uint32_t qa = kk == 0 ? Q : tsindex_slot(x, kk);
       rec[q] = (static_cast<unsigned long long>(i) << 32) | qa;
       const uint32_t rr = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32);
-      if (rr < REP_DIRECT) atomicMax(&rv[rr], i + 1);
-      else atomicMax(&rtab[rr + (1u << (REPLICA_BITS - 1))], i + 1);
+      if (rr < REP_DIRECT) {
+        atomicMax(&rv[rr], i + 1);
+        mr = max(mr, rr);
+      } else {
+        atomicMax(&rtab[rr + (1u << (REPLICA_BITS - 1))], i + 1);
+      }
     }
   }
-  __syncthreads();
-  for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x)
+  mr = block_max(mr);  // (synchronises the block) only ids <= mr were touched
+  for (uint32_t j = threadIdx.x; j <= mr; j += blockDim.x)
     if (rv[j]) atomicMax(&rtab[j + (1u << (REPLICA_BITS - 1))], rv[j]);
   keys = block_sum(keys);
   own = block_sum(own);

@@ -39,40 +39,70 @@ struct NegIdKey {
   __device__ __forceinline__ long long operator()(uint32_t v) const { return -static_cast<long long>(v); }
 };
 
+// Segments of 2 swap in place; tiny ones (3..SMALL_SEG) sort in place too:
+// the lane's items load together into registers and each item's rank
+// (smaller keys, ties by position: stable) comes from static-index compares
+// bounded by the wave's longest tiny segment (a scalar bound, so the steps
+// beyond it are skipped) — no dependent loads and no list of tiny segments
+// (a list append per tiny segment serialises on its counter: ~10^5 of them
+// in a 10M-op flat merge). Mid and big segments go to their lists with
+// wave-aggregated appends.
 template <class KEY>
 __global__ void __launch_bounds__(BLOCK) k_sort_small(const uint32_t* __restrict__ seg_start, uint32_t n_seg,
                                                       uint32_t* __restrict__ carr, KEY sort_key, uint32_t skip,
                                                       uint32_t* __restrict__ mid_list, uint32_t* __restrict__ n_mid,
                                                       uint32_t* __restrict__ big_list, uint32_t* __restrict__ n_big) {
-  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < n_seg; u += gridDim.x * blockDim.x) {
-    const uint32_t b = seg_start[u], e = seg_start[u + 1];
-    const uint32_t len = e - b;
-    if (len < 2 || u == skip) continue;
-    if (len == 2) {
-      const uint32_t x = carr[b], y = carr[b + 1];
-      if (sort_key(y) < sort_key(x)) {
-        carr[b] = y;
-        carr[b + 1] = x;
-      }
-    } else if (len <= SMALL_SEG) {
-      // insertion sort in place (the segment stays in L1/L2)
-      for (uint32_t j = b + 1; j < e; ++j) {
-        const uint32_t v = carr[j];
-        const long long k = sort_key(v);
-        uint32_t p = j;
-        while (p > b) {
-          const uint32_t w = carr[p - 1];
-          if (!(sort_key(w) > k)) break;
-          carr[p] = w;
-          --p;
+  // the loop bound is uniform per workgroup, so every lane reaches the wave steps
+  for (uint32_t u0 = blockIdx.x * blockDim.x; u0 < n_seg; u0 += gridDim.x * blockDim.x) {
+    const uint32_t u = u0 + threadIdx.x;
+    uint32_t len = 0, b = 0;
+    if (u < n_seg && u != skip) {
+      b = seg_start[u];
+      len = seg_start[u + 1] - b;
+      if (len == 2) {
+        const uint32_t x = carr[b], y = carr[b + 1];
+        if (sort_key(y) < sort_key(x)) {
+          carr[b] = y;
+          carr[b + 1] = x;
         }
-        carr[p] = v;
       }
-    } else if (len <= MID_SEG) {
-      mid_list[atomicAdd(n_mid, 1u)] = u;
-    } else {
-      big_list[atomicAdd(n_big, 1u)] = u;
     }
+    const uint32_t tl = len > 2 && len <= SMALL_SEG ? len : 0u;
+    uint32_t wl = tl;
+    for (int o = 32; o > 0; o >>= 1) wl = max(wl, static_cast<uint32_t>(__shfl_xor(static_cast<int>(wl), o, 64)));
+    wl = __builtin_amdgcn_readfirstlane(wl);
+    if (wl) {
+      uint32_t v[SMALL_SEG];
+      long long k[SMALL_SEG];
+#pragma unroll
+      for (uint32_t t = 0; t < SMALL_SEG; ++t) {
+        v[t] = 0;
+        k[t] = 0x7fffffffffffffffLL;
+        if (t < wl && t < tl) {
+          v[t] = carr[b + t];
+          k[t] = sort_key(v[t]);
+        }
+      }
+#pragma unroll
+      for (uint32_t t = 0; t < SMALL_SEG; ++t) {
+        if (t < wl) {
+          uint32_t rk = 0;
+#pragma unroll
+          for (uint32_t j = 0; j < SMALL_SEG; ++j) {
+            if (j < wl) {
+              if (j < t) rk += k[j] <= k[t] ? 1u : 0u;
+              else if (j > t) rk += k[j] < k[t] ? 1u : 0u;
+            }
+          }
+          if (t < tl) carr[b + rk] = v[t];
+        }
+      }
+    }
+    // wave-aggregated appends: one atomic per wave and list
+    const bool mi = len > SMALL_SEG && len <= MID_SEG, bi = len > MID_SEG;
+    const uint32_t km = wave_ticket(n_mid, mi), kb = wave_ticket(n_big, bi);
+    if (mi) mid_list[km] = u;
+    if (bi) big_list[kb] = u;
   }
 }
 
@@ -427,16 +457,21 @@ static int segmented_sort_t(const uint32_t* seg_start, uint32_t n_seg, uint32_t*
   uint32_t* nbig = &dres->big_segments;
   uint32_t* nhuge = &dres->huge_segments;
   uint32_t* nmid = &dres->mid_segments;
-  // big_segments / huge_segments / mid_segments are 0 on entry (k_dres_init; reset on exit)
+  // big / huge / mid segment counters are 0 on entry (k_dres_init; reset on exit)
   LAUNCH(k_sort_small<KEY>, dim3(grid_for(n_seg)), dim3(BLOCK), 0, st, seg_start, n_seg, carr, sort_key, skip, mid,
          nmid, big, nbig);
   LAUNCH(k_sort_mid<KEY>, dim3(1024), dim3(BLOCK), 0, st, seg_start, mid, nmid, carr, sort_key);
   // segments of MID_SEG+1..LDS_SORT_MAX: one workgroup each (huge ones are skipped there)
   LAUNCH(k_sort_big<KEY>, dim3(256), dim3(1024), 0, st, seg_start, big, nbig, carr, scratch, sort_key);
   LAUNCH(k_sort_big_filter, dim3(16), dim3(BLOCK), 0, st, seg_start, big, nbig, huge, nhuge);
-  uint32_t nh = 0;
-  HIP_CHECK(hipMemcpyAsync(&nh, nhuge, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  uint32_t cn[3] = {0, 0, 0};  // big, huge, mid
+  HIP_CHECK(hipMemcpyAsync(cn, nbig, sizeof(cn), hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));
+  const uint32_t nh = cn[1];
+  static const bool stats = getenv("CRDTM_SORT_STATS") != nullptr;
+  if (stats)
+    fprintf(stderr, "[crdtm] segmented sort: %u segments, %u mid (%u..%u), %u big (..%u), %u huge\n", n_seg, cn[2],
+            SMALL_SEG + 1, MID_SEG, cn[0], LDS_SORT_MAX, cn[1]);
   // leave the three counters at 0 for the next sort of this merge
   static_assert(offsetof(DevResult, huge_segments) == offsetof(DevResult, big_segments) + 4 &&
                     offsetof(DevResult, mid_segments) == offsetof(DevResult, big_segments) + 8,

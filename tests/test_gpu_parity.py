@@ -266,3 +266,33 @@ def test_flat_closed_form_edges(case):
     assert engine_summary(et) == oracle_summary(ot)
     assert engine_log(et, 0) == oracle_log(ot, 0)
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+
+
+@pytest.mark.gpu
+def test_flat_sibling_fans():
+    """Sibling-sort tiers (tiny 3..16, mid ..512, big ..4096, huge beyond):
+    fans of concurrent inserts that all anchor after one node, children of
+    each fan spread over 60 replicas and shuffled, against the oracle."""
+    rng = np.random.default_rng(0xFA45)
+    sizes = [3, 5, 16, 17, 300, 512, 513, 2000, 4096, 4097, 9000]
+    heads = [((1 << 32) + k + 1, 0) for k in range(len(sizes))]
+    ctr = {}
+    kids = []
+    for k, K in enumerate(sizes):
+        for j in range(K):
+            r = 2 + int(rng.integers(0, 60))
+            ctr[r] = ctr.get(r, 0) + 1
+            kids.append(((r << 32) + ctr[r], heads[k][0]))
+    kids = [kids[i] for i in rng.permutation(len(kids))]
+    rows = heads + kids
+    m = len(rows)
+    v = dict(kind=np.zeros(m, np.uint8), ts=np.array([a for a, _ in rows], np.int64),
+             path_off=np.arange(m + 1, dtype=np.uint32), path=np.array([b for _, b in rows] + [0], np.int64),
+             val=np.arange(m, dtype=np.uint32))
+    ot, rc, _ = oracle_apply_arrays(v, m)
+    assert rc == 0
+    et = CRDTree.init(0)
+    res = et.apply_arrays(v, m)
+    assert res.code == 0 and res.path_taken == N.PATH_CLOSED_FORM
+    assert engine_summary(et) == oracle_summary(ot)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
