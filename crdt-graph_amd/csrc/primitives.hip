@@ -29,13 +29,16 @@ constexpr uint32_t LDS_SORT_MAX = 4096;
 // Sort keys: an explicit per-item array, or the item id itself descending
 // (timestamp-slot numbering: slot order == timestamp order).
 struct ArrKey {
+  static constexpr bool kFromId = false;  // the key is a gather: k_sort_big keeps keys in LDS
   const long long* k;
   __device__ __forceinline__ long long operator()(uint32_t v) const { return k[v]; }
 };
 struct IdKey {
+  static constexpr bool kFromId = true;  // the key is arithmetic on the id: k_sort_big keeps ids only
   __device__ __forceinline__ long long operator()(uint32_t v) const { return static_cast<long long>(v); }
 };
 struct NegIdKey {
+  static constexpr bool kFromId = true;
   __device__ __forceinline__ long long operator()(uint32_t v) const { return -static_cast<long long>(v); }
 };
 
@@ -154,128 +157,66 @@ __global__ void __launch_bounds__(BLOCK) k_sort_mid(const uint32_t* __restrict__
   }
 }
 
-// One workgroup per large segment. Bitonic sort over the next power of two
-// in LDS (keys padded with +inf) when it fits; otherwise an in-HBM merge sort
-// with ping-pong through `scratch` (same offsets as carr).
+// One workgroup per large segment (MID_SEG+1..LDS_SORT_MAX): bitonic sort
+// over the next power of two in LDS (padding sorts last). Every step is one
+// compare-exchange per pair, pairs spread over all threads (pair q works on
+// i = q with a zero bit inserted at jj, and i | jj). The network is LDS
+// bandwidth bound, so when the key is arithmetic on the id (IdKey /
+// NegIdKey) only the 4-byte ids live in LDS and keys are recomputed.
+template <class KEY>
+__device__ __forceinline__ long long big_key(KEY sort_key, uint32_t v) {
+  return v == NONE ? 0x7fffffffffffffffLL : sort_key(v);
+}
+
 template <class KEY>
 __global__ void __launch_bounds__(1024) k_sort_big(const uint32_t* __restrict__ seg_start,
                                                     const uint32_t* __restrict__ big_list,
                                                     const uint32_t* __restrict__ n_big, uint32_t* __restrict__ carr,
-                                                    uint32_t* __restrict__ scratch,
                                                     KEY sort_key) {
-  __shared__ long long skey[LDS_SORT_MAX];
+  constexpr bool FROM_ID = KEY::kFromId;
+  __shared__ long long skey[FROM_ID ? 1 : LDS_SORT_MAX];
   __shared__ uint32_t sid[LDS_SORT_MAX];
   const uint32_t nb = *n_big;
   for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
     const uint32_t u = big_list[bi];
     const uint32_t b = seg_start[u], len = seg_start[u + 1] - b;
     if (len > LDS_SORT_MAX) continue;  // huge: multi-workgroup path (segmented_sort)
-    if (len <= LDS_SORT_MAX) {
-      uint32_t p2 = 1;
-      while (p2 < len) p2 <<= 1;
-      for (uint32_t j = threadIdx.x; j < p2; j += blockDim.x) {
-        if (j < len) {
-          uint32_t v = carr[b + j];
-          sid[j] = v;
-          skey[j] = sort_key(v);
-        } else {
-          sid[j] = NONE;
-          skey[j] = 0x7fffffffffffffffLL;
-        }
-      }
-      __syncthreads();
-      for (uint32_t k = 2; k <= p2; k <<= 1) {
-        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-          for (uint32_t i = threadIdx.x; i < p2; i += blockDim.x) {
-            uint32_t ixj = i ^ jj;
-            if (ixj > i) {
-              bool up = (i & k) == 0;
-              long long a = skey[i], c = skey[ixj];
-              if ((a > c) == up) {
-                skey[i] = c;
-                skey[ixj] = a;
-                uint32_t t = sid[i];
-                sid[i] = sid[ixj];
-                sid[ixj] = t;
-              }
-            }
-          }
-          __syncthreads();
-        }
-      }
-      for (uint32_t j = threadIdx.x; j < len; j += blockDim.x) carr[b + j] = sid[j];
-      __syncthreads();
-    } else {
-      // 1) sort runs of LDS_SORT_MAX in LDS
-      for (uint32_t r0 = 0; r0 < len; r0 += LDS_SORT_MAX) {
-        const uint32_t rl = min(LDS_SORT_MAX, len - r0);
-        for (uint32_t j = threadIdx.x; j < LDS_SORT_MAX; j += blockDim.x) {
-          if (j < rl) {
-            uint32_t v = carr[b + r0 + j];
-            sid[j] = v;
-            skey[j] = sort_key(v);
-          } else {
-            sid[j] = NONE;
-            skey[j] = 0x7fffffffffffffffLL;
-          }
-        }
-        __syncthreads();
-        for (uint32_t k = 2; k <= LDS_SORT_MAX; k <<= 1) {
-          for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            for (uint32_t i = threadIdx.x; i < LDS_SORT_MAX; i += blockDim.x) {
-              uint32_t ixj = i ^ jj;
-              if (ixj > i) {
-                bool up = (i & k) == 0;
-                long long a = skey[i], c = skey[ixj];
-                if ((a > c) == up) {
-                  skey[i] = c;
-                  skey[ixj] = a;
-                  uint32_t t = sid[i];
-                  sid[i] = sid[ixj];
-                  sid[ixj] = t;
-                }
-              }
-            }
-            __syncthreads();
-          }
-        }
-        for (uint32_t j = threadIdx.x; j < rl; j += blockDim.x) carr[b + r0 + j] = sid[j];
-        __syncthreads();
-      }
-      // 2) merge passes (merge-path partition per thread)
-      uint32_t* src = carr + b;
-      uint32_t* dst = scratch + b;
-      for (uint32_t width = LDS_SORT_MAX; width < len; width <<= 1) {
-        for (uint32_t m0 = 0; m0 < len; m0 += 2 * width) {
-          const uint32_t a0 = m0, a1 = min(m0 + width, len), b1 = min(m0 + 2 * width, len);
-          const uint32_t na = a1 - a0, nbb = b1 - a1, tot = na + nbb;
-          const uint32_t per = (tot + blockDim.x - 1) / blockDim.x;
-          const uint32_t d0 = min(threadIdx.x * per, tot), d1 = min(d0 + per, tot);
-          // merge path: find i in A, j in B with i + j = d0
-          uint32_t lo = d0 > nbb ? d0 - nbb : 0, hi = min(d0, na);
-          while (lo < hi) {
-            uint32_t mid = (lo + hi) >> 1;
-            if (sort_key(src[a0 + mid]) < sort_key(src[a1 + d0 - mid - 1])) lo = mid + 1;
-            else hi = mid;
-          }
-          uint32_t i = lo, j = d0 - lo;
-          for (uint32_t d = d0; d < d1; ++d) {
-            bool takeA;
-            if (i >= na) takeA = false;
-            else if (j >= nbb) takeA = true;
-            else takeA = sort_key(src[a0 + i]) < sort_key(src[a1 + j]);
-            dst[m0 + d] = takeA ? src[a0 + i++] : src[a1 + j++];
-          }
-        }
-        __syncthreads();
-        uint32_t* t = src;
-        src = dst;
-        dst = t;
-      }
-      if (src != carr + b)
-        for (uint32_t j = threadIdx.x; j < len; j += blockDim.x) carr[b + j] = src[j];
-      __syncthreads();
+    uint32_t p2 = 1;
+    while (p2 < len) p2 <<= 1;
+    for (uint32_t j = threadIdx.x; j < p2; j += blockDim.x) {
+      const uint32_t v = j < len ? carr[b + j] : NONE;
+      sid[j] = v;
+      if constexpr (!FROM_ID) skey[j] = big_key(sort_key, v);
     }
+    __syncthreads();
+    for (uint32_t k = 2; k <= p2; k <<= 1) {
+      for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+        for (uint32_t q = threadIdx.x; q < p2 / 2; q += blockDim.x) {
+          const uint32_t i = ((q & ~(jj - 1)) << 1) | (q & (jj - 1)), ixj = i | jj;
+          const bool up = (i & k) == 0;
+          const uint32_t va = sid[i], vc = sid[ixj];
+          long long a, c;
+          if constexpr (FROM_ID) {
+            a = big_key(sort_key, va);
+            c = big_key(sort_key, vc);
+          } else {
+            a = skey[i];
+            c = skey[ixj];
+          }
+          if ((a > c) == up) {
+            sid[i] = vc;
+            sid[ixj] = va;
+            if constexpr (!FROM_ID) {
+              skey[i] = c;
+              skey[ixj] = a;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    for (uint32_t j = threadIdx.x; j < len; j += blockDim.x) carr[b + j] = sid[j];
+    __syncthreads();
   }
 }
 
@@ -462,7 +403,7 @@ static int segmented_sort_t(const uint32_t* seg_start, uint32_t n_seg, uint32_t*
          nmid, big, nbig);
   LAUNCH(k_sort_mid<KEY>, dim3(1024), dim3(BLOCK), 0, st, seg_start, mid, nmid, carr, sort_key);
   // segments of MID_SEG+1..LDS_SORT_MAX: one workgroup each (huge ones are skipped there)
-  LAUNCH(k_sort_big<KEY>, dim3(256), dim3(1024), 0, st, seg_start, big, nbig, carr, scratch, sort_key);
+  LAUNCH(k_sort_big<KEY>, dim3(256), dim3(1024), 0, st, seg_start, big, nbig, carr, sort_key);
   LAUNCH(k_sort_big_filter, dim3(16), dim3(BLOCK), 0, st, seg_start, big, nbig, huge, nhuge);
   uint32_t cn[3] = {0, 0, 0};  // big, huge, mid
   HIP_CHECK(hipMemcpyAsync(cn, nbig, sizeof(cn), hipMemcpyDeviceToHost, st));
