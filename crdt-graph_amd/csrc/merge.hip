@@ -2120,8 +2120,9 @@ __global__ void __launch_bounds__(BLOCK) k_fl_present(uint32_t Q, const uint32_t
 __global__ void __launch_bounds__(BLOCK) k_fl_commit(OpsDev o, TsIndex x, uint32_t Q, uint32_t nrep,
                                                      const uint32_t* anc, const unsigned long long* rec,
                                                      const uint32_t* qc, const uint32_t* logidx, TreeDev T) {
-  __shared__ uint32_t sb[HOST_RANGES];
-  __shared__ uint32_t sc[HOST_RANGES];
+  extern __shared__ uint32_t sbc[];  // dynamic: 2 * nrep words when the tables fit (HOST_RANGES)
+  uint32_t* sb = sbc;
+  uint32_t* sc = sbc + nrep;
   const bool lds = nrep <= HOST_RANGES;
   if (lds) {
     for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x) {
@@ -2520,8 +2521,9 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     // (Measured: running the commit and the log copy on the ctx side stream
     // while the list ranking runs does not shorten the merge — the ranking
     // kernels keep every CU busy, the copies just stretch — so one stream.)
-    LAUNCH(k_fl_commit, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, o, ix, Q, maxr + 1, anc, rec, qc, logidx,
-           t->d);
+    LAUNCH(k_fl_commit, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK),
+           maxr + 1 <= HOST_RANGES ? 2 * (maxr + 1) * sizeof(uint32_t) : 0, s, o, ix, Q, maxr + 1, anc, rec, qc,
+           logidx, t->d);
     if (all_applied) LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
     // ---- K4: Euler tour + list ranking -> document order ----
     if ((r = list_rank_fused(FlatEulerSrc{Q, anc, cnt, carr, ns}, 2ULL * U, 2 * Q, FlatDocSink{Q, t->d.doc, qc}, ws,
