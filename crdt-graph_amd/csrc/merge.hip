@@ -834,8 +834,8 @@ __global__ void __launch_bounds__(BLOCK) k_commit_flags(OpsDev o, Work w, uint32
   const uint32_t n = o.n;
   GRID_STRIDE(i, n) {
     const bool a = w.st[i] == ST_APPLIED;
-    appl[i] = a;
-    plen[i] = a ? op_len(o, i) : 0;
+    if (appl) appl[i] = a;  // (null when every op applied: the log is the batch)
+    if (plen) plen[i] = a ? op_len(o, i) : 0;
     uint32_t k = 0, l = 0;
     if (a && o.kind[i] == CRDTM_ADD) {
       const uint32_t p = w.addpar[i];
@@ -869,7 +869,7 @@ __global__ void __launch_bounds__(BLOCK) k_commit_nodes(OpsDev o, Work w, TreeDe
     T.s_key[slot] = o.ts[x];
     T.s_dict[slot] = p == n ? 0u : a.base_dict + lslot[p];
     T.s_next[slot] = nextn[x] != NONE ? a.base_slot + kslot[nextn[x]] : NONE;
-    T.s_src[slot] = a.log_base + logidx[x];
+    T.s_src[slot] = a.log_base + (logidx ? logidx[x] : x);
     T.s_flags[slot] = tomb ? F_TOMB : 0;
     if (!tomb) {
       const uint32_t dd = a.base_dict + lslot[x];
@@ -915,12 +915,14 @@ __global__ void __launch_bounds__(BLOCK) k_log(OpsDev o, const uint8_t* st, Tree
       soff[t] = o.off[i];
       uint32_t dst = NONE;
       if (st[i] == ST_APPLIED) {
-        const uint32_t li = log_base + logidx[i];
+        // logidx / lpoff null: every op applied, log index = op index and
+        // path offsets = the batch's (off[0] == 0)
+        const uint32_t li = log_base + (logidx ? logidx[i] : i);
         const bool add = o.kind[i] == CRDTM_ADD;
         T.l_kind[li] = o.kind[i];
         T.l_ts[li] = add ? o.ts[i] : 0;
         T.l_val[li] = add ? o.val[i] : 0;
-        dst = lpath_base + lpoff[i];
+        dst = lpath_base + (lpoff ? lpoff[i] : soff[t]);
         T.l_off[li] = dst;
       }
       sdst[t] = dst;
@@ -940,6 +942,11 @@ __global__ void __launch_bounds__(BLOCK) k_log(OpsDev o, const uint8_t* st, Tree
     }
     __syncthreads();
   }
+}
+
+__global__ void k_log_totals(DevResult* d, uint32_t n, uint32_t npath) {
+  d->log_n = n;
+  d->log_npath = npath;
 }
 
 __global__ void k_log_tail(TreeDev T, uint32_t log_base, const uint32_t* n_app, uint32_t lpath_base,
@@ -2762,11 +2769,21 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   uint32_t* plen = ws.alloc<uint32_t>(n + 1);
   uint32_t* kept = ws.alloc<uint32_t>(n + 1);
   uint32_t* live = ws.alloc<uint32_t>(n + 1);
+  // every op applied: the log is the batch (identity log index, the batch's
+  // path offsets), so the two log scans are skipped
+  const bool every = h1.n_applied == n;
+  if (every) {
+    appl = nullptr;
+    plen = nullptr;
+    LAUNCH(k_log_totals, dim3(1), dim3(1), 0, s, dr, n, static_cast<uint32_t>(o.n_path));
+  }
   LAUNCH(k_commit_flags, dim3(g), dim3(BLOCK), 0, s, o, w, appl, plen, kept, live);
   if ((r = scan_excl_u32(kept, kept, n, &dr->n_nodes_kept, ws, s))) return r;
   if ((r = scan_excl_u32(live, live, n, &dr->n_live_kept, ws, s))) return r;
-  if ((r = scan_excl_u32(appl, appl, n, &dr->log_n, ws, s))) return r;
-  if ((r = scan_excl_u32(plen, plen, n, &dr->log_npath, ws, s))) return r;
+  if (!every) {
+    if ((r = scan_excl_u32(appl, appl, n, &dr->log_n, ws, s))) return r;
+    if ((r = scan_excl_u32(plen, plen, n, &dr->log_npath, ws, s))) return r;
+  }
   TreeCaps need = t->cap;
   need.slots = std::max<uint64_t>(need.slots, 1 + 2ULL * h1.n_adds_applied + 1);
   need.dicts = std::max<uint64_t>(need.dicts, 1 + h1.n_adds_applied + 1);
