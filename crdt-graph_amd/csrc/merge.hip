@@ -1952,6 +1952,9 @@ __global__ void __launch_bounds__(BLOCK) k_fl_ep(uint32_t Q, uint32_t* anc, cons
 // Run heads: rh[q] = max{q' <= q : anc[q'] != q' - 1}, an inclusive
 // max-scan over head flags (scan.h).
 struct RunHeadGen {
+  static constexpr bool kStriped = false;  // loads through load() (it writes anc as a side output)
+  __device__ __forceinline__ bool aligned(uint64_t) const { return false; }
+  __device__ __forceinline__ uint4 load4(uint64_t) const { return make_uint4(0u, 0u, 0u, 0u); }
   const unsigned long long* rec;
   uint32_t* anc;  // side output: anchor slot per slot (ABSENT = no node)
   __device__ __forceinline__ uint32_t anchor(unsigned long long r) const {

@@ -36,6 +36,10 @@ __global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* __restrict__
                                                  uint32_t* __restrict__ err) {
   __shared__ uint32_t s_tile, s_prefix;
   __shared__ uint32_t sw[BLOCK / 64];
+  // full tiles move through LDS so that HBM sees lane-contiguous 16-byte
+  // accesses (a lane's DS_ITEMS consecutive items would otherwise make every
+  // vector load/store instruction touch one 16-byte piece of 64 lines)
+  __shared__ __attribute__((aligned(16))) uint32_t sx[DS_TILE];
   const unsigned long long ep = static_cast<unsigned long long>(epoch) << 32;
   if (threadIdx.x == 0) {
     s_tile = atomicAdd(ticket, 1u);
@@ -45,7 +49,26 @@ __global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* __restrict__
   const uint32_t tile = s_tile;
   const uint64_t b = static_cast<uint64_t>(tile) * DS_TILE + static_cast<uint64_t>(threadIdx.x) * DS_ITEMS;
   uint32_t v[DS_ITEMS];
-  gen.load(b, n, v);
+  const uint64_t tb = static_cast<uint64_t>(tile) * DS_TILE;
+  const bool full = tb + DS_TILE <= n;
+  if (GEN::kStriped && full && gen.aligned(tb)) {
+#pragma unroll
+    for (int j = 0; j < DS_ITEMS / 4; ++j) {
+      const uint32_t x = (j * BLOCK + threadIdx.x) * 4;
+      *reinterpret_cast<uint4*>(sx + x) = gen.load4(tb + x);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < DS_ITEMS; j += 4) {
+      const uint4 y = *reinterpret_cast<const uint4*>(sx + threadIdx.x * DS_ITEMS + j);
+      v[j] = y.x;
+      v[j + 1] = y.y;
+      v[j + 2] = y.z;
+      v[j + 3] = y.w;
+    }
+  } else {
+    gen.load(b, n, v);
+  }
   uint32_t acc = OP::id();
 #pragma unroll
   for (int j = 0; j < DS_ITEMS; ++j) acc = OP::op(acc, v[j]);
@@ -118,7 +141,18 @@ __global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* __restrict__
       run = OP::op(run, x);
     }
   }
-  if (b + DS_ITEMS <= n) {
+  if (full && (reinterpret_cast<uintptr_t>(out + tb) & 15) == 0) {
+    // (every lane finished reading sx: the look-back's __syncthreads lie between)
+#pragma unroll
+    for (int j = 0; j < DS_ITEMS; j += 4)
+      *reinterpret_cast<uint4*>(sx + threadIdx.x * DS_ITEMS + j) = make_uint4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < DS_ITEMS / 4; ++j) {
+      const uint32_t x = (j * BLOCK + threadIdx.x) * 4;
+      *reinterpret_cast<uint4*>(out + tb + x) = *reinterpret_cast<const uint4*>(sx + x);
+    }
+  } else if (b + DS_ITEMS <= n) {
 #pragma unroll
     for (int j = 0; j < DS_ITEMS; j += 4)
       *reinterpret_cast<uint4*>(out + b + j) = make_uint4(v[j], v[j + 1], v[j + 2], v[j + 3]);
@@ -134,7 +168,10 @@ struct SumOp {
 };
 
 struct ArrGen {
+  static constexpr bool kStriped = true;  // k_dscan may load full tiles lane-contiguously
   const uint32_t* in;
+  __device__ __forceinline__ bool aligned(uint64_t b) const { return (reinterpret_cast<uintptr_t>(in + b) & 15) == 0; }
+  __device__ __forceinline__ uint4 load4(uint64_t b) const { return *reinterpret_cast<const uint4*>(in + b); }
   __device__ __forceinline__ void load(uint64_t b, uint64_t n, uint32_t* v) const {
     if (b + DS_ITEMS <= n && (reinterpret_cast<uintptr_t>(in + b) & 15) == 0) {
 #pragma unroll
