@@ -17,7 +17,7 @@ namespace crdtm {
 // resets the ticket counter. Every element is read once and written once.
 // Spins are bounded; an exhausted spin sets err.
 // ---------------------------------------------------------------------------
-constexpr int DS_ITEMS = 16;
+constexpr int DS_ITEMS = 32;
 constexpr int DS_TILE = BLOCK * DS_ITEMS;
 
 __device__ __forceinline__ unsigned long long ds_load(const unsigned long long* p) {
