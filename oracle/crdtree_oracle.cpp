@@ -758,3 +758,35 @@ extern "C" uint64_t orc_flat_check(uint64_t n_doc, const int64_t* doc_keys, uint
   if (seen != n_doc) ++bad;
   return bad;
 }
+
+// ---- many independent documents (test infrastructure; config 5) ----
+// Document d = ops [doc_off[d], doc_off[d+1]) applied as `apply (Batch ops_d)`
+// to a fresh `init replica` (src/CRDTree.elm:130-139, :265-269), exactly like
+// orc_init + orc_apply + orc_canonical(which = 1) + orc_timestamp per document,
+// without a host round trip per document. Per-document outputs: error code,
+// local err index (-1), visible-order digest and word count, final timestamp.
+extern "C" void orc_forest_apply(uint64_t n_docs, const uint32_t* doc_off, int64_t replica, const uint8_t* kind,
+                                 const int64_t* ts, const uint32_t* path_off, const int64_t* path,
+                                 const uint32_t* val, int32_t* code, int64_t* err, uint64_t* vhash,
+                                 uint64_t* vwords, int64_t* tstamp) {
+  for (uint64_t d = 0; d < n_docs; ++d) {
+    const uint32_t a = doc_off[d], b = doc_off[d + 1];
+    Tree t;
+    initTree(t, replica);
+    Op top;
+    top.kind = OP_BATCH;
+    top.ops.reserve(b - a);
+    for (uint32_t i = a; i < b; ++i)
+      top.ops.push_back(makeOp(kind[i], ts[i], path + path_off[i], path_off[i + 1] - path_off[i], val[i],
+                               static_cast<int64_t>(i - a)));
+    t.err_index = -1;
+    const int r = apply(top, t);
+    code[d] = r;
+    err[d] = r == T_OK ? -1 : t.err_index;
+    Sink s{nullptr};
+    if (r == T_OK) dumpVisible(t.root.children, 0, s);
+    vhash[d] = s.h;
+    vwords[d] = s.n;
+    tstamp[d] = t.timestamp;
+  }
+}

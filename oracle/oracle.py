@@ -68,6 +68,8 @@ def lib():
         L.orc_flat_check.argtypes = [C.c_uint64, P, C.c_uint64, P, P, P]
         L.orc_reset_last.argtypes = [P]
         L.orc_merge_last.argtypes = [P, P]
+        L.orc_forest_apply.restype = None
+        L.orc_forest_apply.argtypes = [C.c_uint64, P, C.c_int64, P, P, P, P, P, P, P, P, P, P]
         _lib = L
     return _lib
 
