@@ -78,18 +78,65 @@ def head(s, m):
                 path_off=off[:m + 1].copy(), path=s["path"][:off[m]].copy())
 
 
-def pmc_traffic(workload, kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary
-    of this workload (profiles/*_pmc.json, written by tools/pmc_summary.py from
-    separate FETCH_SIZE and WRITE_SIZE passes of `bench.py`; FETCH_SIZE doubled
-    per the gfx950 correction). None when no summary covers the kernel."""
-    path = os.path.join(ROOT, "profiles", f"r1_{workload}_pmc.json")
-    try:
-        d = json.load(open(path))
-    except (OSError, ValueError):
-        return None
-    e = d.get(kernel.split("<")[0])
-    return None if not e or "hbm_bytes_corrected" not in e else e["hbm_bytes_corrected"]
+def pmc_table(workload):
+    """Per-kernel HBM bytes per dispatch from the newest committed rocprofv3
+    --pmc summary of this workload (profiles/r<N>_<workload>_pmc.json, written
+    by tools/pmc_summary.py from separate FETCH_SIZE and WRITE_SIZE passes of
+    this bench). `hbm_bytes` applies the gfx950 FETCH_SIZE x2 correction only to
+    the kernels whose reads are calibrated wide streams (MI355X_MICROARCH.md,
+    HBM); the others carry the raw counter bytes."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc.json")),
+                   key=lambda f: int(os.path.basename(f)[1:].split("_")[0]))
+    for f in reversed(files):
+        try:
+            return json.load(open(f)), os.path.basename(f)
+        except (OSError, ValueError):
+            continue
+    return {}, None
+
+
+def roofline(workload, per_step, launches, B_alg, ms_step, steps_profiled):
+    """SURVEY.md §8d roofline of the whole merge (one crdtm_apply / forest
+    step): achieved = algorithmic bytes / merge time, against the 8 TB/s HBM
+    peak; traffic = the merge's HBM bytes summed over its kernels' PMC counts
+    (bytes per dispatch x dispatches per step). The dominant kernel (largest
+    device-time share) is reported beside it with its own counter bandwidth."""
+    pmc, src = pmc_table(workload)
+
+    def kbytes(nm, key="hbm_bytes"):
+        e = pmc.get(nm.split("<")[0])
+        if e and key not in e and key == "hbm_bytes" and "hbm_bytes_corrected" in e:
+            key = "hbm_bytes_corrected"  # (round-1 summaries)
+        return None if not e or key not in e else e[key]
+
+    merge_s = ms_step / 1e3
+    achieved = B_alg / merge_s / 1e9
+    traffic, traffic_raw, covered = 0.0, 0.0, True
+    for nm in per_step:
+        b, braw = kbytes(nm), kbytes(nm, "hbm_bytes_raw")
+        if b is None or braw is None:
+            covered = False
+            continue
+        traffic += b * launches[nm] / steps_profiled
+        traffic_raw += braw * launches[nm] / steps_profiled
+    kernels = []
+    for nm, t in sorted(per_step.items(), key=lambda kv: -kv[1])[:8]:
+        b = kbytes(nm)
+        per = launches[nm] / steps_profiled
+        e = {"name": nm, "ms_per_step": t, "launches_per_step": per}
+        if b is not None:
+            e["hbm_bytes_per_step"] = b * per
+            e["hbm_gbs"] = b * per / (t / 1e3) / 1e9
+            e["hbm_frac"] = e["hbm_gbs"] / HBM_PEAK_GBS
+        kernels.append(e)
+    return {"bound": "hbm", "scope": "whole merge (every kernel of one step)", "achieved": achieved,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            "traffic": (traffic if covered and pmc else None),
+            "traffic_lower": (traffic_raw if covered and pmc else None), "traffic_source": src,
+            "traffic_over_alg": (traffic / B_alg if covered and pmc else None),
+            "alg_bytes": B_alg, "kernels_ms_per_step": sum(per_step.values()),
+            "dominant_kernel": kernels[0] if kernels else None, "top_kernels": kernels}
 
 
 def cpu_baseline(s, m, doc_off=None, workers=1, batch_cut=20_000):
@@ -234,22 +281,12 @@ def main():
             acc.setdefault(nm, []).append(ms[j])
     L.crdtm_ctx_profile(ctx, 0)
     # a kernel launched several times per step is summed within the step
-    per_step = {}
-    for nm, v in acc.items():
-        per_step[nm] = sum(v) / max(1, args.profile_steps)
-    # Roofline kernel: the longest kernel that processes the whole batch in
-    # one launch (its units = every op of the batch); kernels
-    # launched several times per step work on sub-problems (list-ranking
-    # levels, scan recursion) whose units are not ops.
-    single = {nm: t for nm, t in per_step.items() if len(acc[nm]) == max(1, args.profile_steps)}
-    dominant = max(single or per_step, key=(single or per_step).get)
-    t_dom = per_step[dominant] / 1e3
-    kernels_ms = sum(per_step.values())
+    ps = max(1, args.profile_steps)
+    per_step = {nm: sum(v) / ps for nm, v in acc.items()}
+    launches = {nm: len(v) for nm, v in acc.items()}
 
     ms_step = elapsed / args.steps * 1e3
     value = world * n * args.steps / elapsed
-    achieved = B_alg / t_dom / 1e9
-    traffic = pmc_traffic(args.workload, dominant)
     line = {
         "metric": "merged ops/sec (whole node) on 10M-op batch",
         "value": value,
@@ -268,15 +305,12 @@ def main():
                    "path": {1: "closed-form", 2: "replay", 3: "per-dict replay"}.get(path_taken, "?"),
                    "guard": guard,
                    "parallelism": f"documents sharded by id over {world} GPU(s)"},
-        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "alg_bytes_per_launch": B_alg, "kernel_ms": t_dom * 1e3, "kernels_ms_per_step": kernels_ms,
-                     "merge_frac": B_alg / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS},
+        "roofline": roofline(args.workload, per_step, launches, B_alg, ms_step, ps),
     }
     if rank == 0:
         sc = stream_copy_gbs(dev)
         line["roofline"]["stream_copy_gbs"] = sc
-        line["roofline"]["frac_of_stream"] = achieved / sc
+        line["roofline"]["frac_of_stream"] = line["roofline"]["achieved"] / sc
     if args.verbose and rank == 0:
         for nm, v in sorted(per_step.items(), key=lambda kv: -kv[1]):
             print(f"  {nm:28s} {v:9.3f} ms/step ({len(acc[nm]) // max(1, args.profile_steps)} launches)",
@@ -361,6 +395,8 @@ def run_trees(args, rank, world, local_rank):
         elapsed = float(t.item())
     n = state["n"]
     ok_docs = int(np.sum(code == 0))
+    if ok_docs != n_mine:  # every generated document merges; anything else is a regression
+        raise RuntimeError(f"forest merge: {n_mine - ok_docs} of {n_mine} documents returned an error")
     # dominant kernel time (HIP events on the launch stream)
     L.crdtm_ctx_profile(ctx, 1)
     step()
@@ -369,15 +405,14 @@ def run_trees(args, rank, world, local_rank):
     k = L.crdtm_ctx_phase_times(ctx, names, len(names), ms, 64)
     labels = names.raw.split(b"\0")
     L.crdtm_ctx_profile(ctx, 0)
-    per_k = {}
+    per_k, launches = {}, {}
     for j in range(min(k, 64)):
-        per_k[labels[j].decode()] = per_k.get(labels[j].decode(), 0.0) + ms[j]
-    dominant = max(per_k, key=per_k.get)
-    kernels_ms = sum(per_k.values())
+        nm = labels[j].decode()
+        per_k[nm] = per_k.get(nm, 0.0) + ms[j]
+        launches[nm] = launches.get(nm, 0) + 1
     ot = state["ops_t"]
     kinds = ot["kind"].cpu().numpy()
     B_alg = int(np.sum(np.where(kinds == 0, 57, 17)))  # flat documents: L = 1
-    t_dom = per_k[dominant] / 1e3
     ms_step = elapsed / args.steps * 1e3
     line = {
         "metric": "merged ops/sec (whole node) on 10M-op batch",
@@ -387,11 +422,7 @@ def run_trees(args, rank, world, local_rank):
         "config": {"workload": f"trees: {n_mine} documents x {per} ops per GPU ({n} ops), {n_docs} documents total",
                    "replicas": TREES["replicas"], "documents_ok": ok_docs,
                    "parallelism": f"documents sharded by id over {world} GPU(s); op logs all-gathered (RCCL)"},
-        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": B_alg / t_dom / 1e9, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": B_alg / t_dom / 1e9 / HBM_PEAK_GBS,
-                     "traffic": pmc_traffic("trees", dominant),
-                     "alg_bytes_per_launch": B_alg, "kernel_ms": t_dom * 1e3, "kernels_ms_per_step": kernels_ms,
-                     "merge_frac": B_alg / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS},
+        "roofline": roofline("trees", per_k, launches, B_alg, ms_step, 1),
     }
     if args.verbose and rank == 0:
         for nm, v in sorted(per_k.items(), key=lambda kv: -kv[1])[:12]:

@@ -201,6 +201,8 @@ int crdtm_ctx_create(int device, void* stream, crdtm_ctx** out) {
   HIP_CHECK(hipMalloc(&c->ws.scan_status, (c->ws.scan_cap + 2) * sizeof(unsigned long long)));
   HIP_CHECK(hipMemsetAsync(c->ws.scan_status, 0, (c->ws.scan_cap + 2) * sizeof(unsigned long long), c->stream));
   c->ws.scan_ticket = reinterpret_cast<uint32_t*>(c->ws.scan_status + c->ws.scan_cap);
+  c->ws.scan_err = &c->dres->scan_err;
+  HIP_CHECK(hipMemsetAsync(c->dres, 0, sizeof(DevResult), c->stream));
   HIP_CHECK(hipMalloc(&c->rtab, REPLICA_SLOTS * sizeof(uint32_t)));
   HIP_CHECK(hipMemsetAsync(c->rtab, 0, REPLICA_SLOTS * sizeof(uint32_t), c->stream));
   int r = ensure_arena(c, 64ULL << 20);
@@ -352,6 +354,10 @@ int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_b
   const uint64_t n = ops->n_ops;
   uint64_t np = ops->n_path;
   if (!ops_on_device && n) np = ops->path_off[n];
+  // a fresh tree (the closed form and the per-dict replay only run on one)
+  // is restored on an engine error; other paths commit after their last check
+  const bool fresh = t->n_slots == 1 && t->log_n == 0;
+  const int64_t ts_before = t->timestamp;
   int r = CRDTM_OK;
   for (int attempt = 0; attempt < 4; ++attempt) {
     r = ensure_arena(c, arena_need(n, np, t) << attempt);
@@ -405,6 +411,7 @@ int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_b
     }
   }
   if (r != CRDTM_OK) {
+    if (fresh && crdtm_tree_reset(t, replica_of(ts_before)) == CRDTM_OK) t->timestamp = ts_before;
     res->code = r;
     return r;
   }

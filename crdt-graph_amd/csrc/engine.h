@@ -38,6 +38,7 @@ struct Arena {
   uint64_t scan_cap = 0;
   uint32_t* scan_ticket = nullptr;
   uint32_t scan_epoch = 0;
+  uint32_t* scan_err = nullptr;  // device word every scan reports an exhausted look-back to (DevResult::scan_err)
 };
 
 enum : uint8_t { F_TOMB = 1, F_ORPHAN = 2, F_SENT = 4 };

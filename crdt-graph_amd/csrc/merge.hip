@@ -2265,9 +2265,15 @@ static uint32_t pow2_at_least(uint64_t x) {
   return static_cast<uint32_t>(p);
 }
 
+// Reads the device result block. A scan whose look-back gave up has written
+// partial prefixes: report it as an engine error before anything is used.
 int sync_read(crdtm_ctx* c) {
   HIP_CHECK(hipMemcpyAsync(c->hres, c->dres, sizeof(DevResult), hipMemcpyDeviceToHost, c->stream));
   HIP_CHECK(hipStreamSynchronize(c->stream));
+  if (c->hres->scan_err) {
+    std::fprintf(stderr, "crdtm: a device scan's look-back did not resolve\n");
+    return CRDTM_E_HIP;
+  }
   return CRDTM_OK;
 }
 
@@ -2497,7 +2503,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     uint32_t* ns = ws.alloc<uint32_t>(U);
     const uint32_t gq = grid_for(Q);
     uint32_t* rh = ws.alloc<uint32_t>(Q);
-    if ((r = dscan<MaxOp, true>(RunHeadGen{rec, anc}, rh, Q, nullptr, ws, s, &dr->scan_err))) return r;
+    if ((r = dscan<MaxOp, true>(RunHeadGen{rec, anc}, rh, Q, nullptr, ws, s, nullptr))) return r;
     LAUNCH(k_fl_ep, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, rh, cnt);
     uint32_t* n_child = &dr->n_sentinels;  // scratch word for the scan total
     if ((r = scan_excl_u32(cnt, cnt, U + 1, n_child, ws, s))) return r;

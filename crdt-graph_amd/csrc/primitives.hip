@@ -12,8 +12,7 @@ namespace crdtm {
 
 // out[i] = sum(in[0..i)); *total (device) = sum(in). in may alias out.
 int scan_excl_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* total, Arena& ws, hipStream_t st) {
-  uint32_t* err = ws.alloc<uint32_t>(1);  // a spin that never resolves (cannot happen on a live device)
-  return dscan<SumOp, false>(ArrGen{in}, out, n, total, ws, st, err);
+  return dscan<SumOp, false>(ArrGen{in}, out, n, total, ws, st, nullptr);  // errors: ws.scan_err
 }
 
 // ---------------------------------------------------------------------------

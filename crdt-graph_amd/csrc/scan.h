@@ -15,7 +15,9 @@ namespace crdtm {
 // earlier call carries an older epoch and reads as "not yet published", so
 // the status pool is never cleared. The workgroup that draws the last ticket
 // resets the ticket counter. Every element is read once and written once.
-// Spins are bounded; an exhausted spin sets err.
+// Spins are bounded; an exhausted spin sets *err (by default the context's
+// DevResult::scan_err, which sync_read turns into CRDTM_E_HIP before any
+// result is used). `out` may alias the input (in-place scans): no restrict.
 // ---------------------------------------------------------------------------
 constexpr int DS_ITEMS = 32;
 constexpr int DS_TILE = BLOCK * DS_ITEMS;
@@ -30,7 +32,7 @@ __device__ __forceinline__ void ds_store(unsigned long long* p, unsigned long lo
 constexpr uint32_t DS_EPOCH_MASK = (1u << 30) - 1;
 
 template <class OP, bool INCL, class GEN>
-__global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* __restrict__ out, uint64_t n,
+__global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* out, uint64_t n,
                                                  unsigned long long* __restrict__ status, uint32_t* __restrict__ ticket,
                                                  uint32_t ntiles, uint32_t epoch, uint32_t* __restrict__ total,
                                                  uint32_t* __restrict__ err) {
@@ -204,6 +206,7 @@ int dscan(GEN gen, uint32_t* out, uint64_t n, uint32_t* total, Arena& ws, hipStr
     ticket = reinterpret_cast<uint32_t*>(status + tiles);
     HIP_CHECK(hipMemsetAsync(status, 0, (tiles + 1) * sizeof(unsigned long long), st));
   }
+  if (!err) err = ws.scan_err;
   auto* kfn = &k_dscan<OP, INCL, GEN>;
   prof_begin(st);
   hipLaunchKernelGGL(kfn, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, gen, out, n, status, ticket,

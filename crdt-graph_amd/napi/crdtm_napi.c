@@ -32,12 +32,18 @@
 
 #include "crdtm.h"
 
+struct job;
+
 typedef struct {
   crdtm_tree *t;
   char *vb;          /* value bytes (canonical JSON texts, concatenated) */
   uint64_t vb_len, vb_cap;
   uint64_t *vo;      /* handle h -> [vo[h], vo[h+1]) */
   uint64_t nv, vo_cap;
+  /* async applies of this tree run one at a time in call order (the
+   * reference's applies are sequential): a FIFO touched only on the JS thread */
+  struct job *qhead, *qtail;
+  int busy;
 } tree_h;
 
 static crdtm_ctx *g_ctx = NULL;
@@ -85,8 +91,10 @@ static int vt_reserve(tree_h *h, uint64_t more_bytes, uint64_t more_vals) {
 
 /* ---- one merge: decode, remap value handles into the tree's table, apply,
  *      encode lastOperation ---- */
-typedef struct {
+typedef struct job {
   tree_h *h;
+  napi_ref tree_ref; /* async: keeps the tree external alive until the job is done */
+  struct job *next;  /* the tree's FIFO */
   char *json;
   size_t len;
   int rc;            /* engine error (< 0) */
@@ -95,7 +103,8 @@ typedef struct {
   size_t last_len;
   napi_async_work work;
   napi_deferred def;
-} job_t;
+} job;
+typedef job job_t;
 
 static int encode_log(tree_h *h, int which, int64_t since, int use_since, char **out, size_t *out_len) {
   crdtm_ops o;
@@ -209,7 +218,11 @@ static void tree_finalize(napi_env env, void *data, void *hint) {
   (void)env;
   (void)hint;
   tree_h *h = data;
+  /* (no job can be in flight: every queued job holds a reference to the external) */
+  pthread_mutex_lock(&g_mu);
   if (h->t) crdtm_tree_destroy(h->t);
+  h->t = NULL;
+  pthread_mutex_unlock(&g_mu);
   free(h->vb);
   free(h->vo);
   free(h);
@@ -264,6 +277,11 @@ static job_t *make_job(napi_env env, napi_callback_info info) {
 static napi_value js_apply_sync(napi_env env, napi_callback_info info) {
   job_t *j = make_job(env, info);
   if (!j) return NULL;
+  if (j->h->busy) {  /* would overtake queued async applies of this tree */
+    job_free(j);
+    napi_throw_error(env, "E_BUSY", "crdtm: applySync while async applies of this tree are pending");
+    return NULL;
+  }
   run_merge(j);
   if (j->rc) {
     const int rc = j->rc;
@@ -280,8 +298,11 @@ static void async_exec(napi_env env, void *data) {
   run_merge(data);
 }
 
+static void start_next(napi_env env, tree_h *h);
+
 static void async_done(napi_env env, napi_status status, void *data) {
   job_t *j = data;
+  tree_h *h = j->h;
   if (status != napi_ok || j->rc) {
     napi_value err, msg;
     char m[128];
@@ -293,17 +314,39 @@ static void async_done(napi_env env, napi_status status, void *data) {
     napi_resolve_deferred(env, j->def, result_object(env, j));
   }
   napi_delete_async_work(env, j->work);
+  napi_ref ref = j->tree_ref;
   job_free(j);
+  h->busy = 0;
+  start_next(env, h);          /* the next queued apply of this tree, if any */
+  napi_delete_reference(env, ref);  /* (last: may let the tree be collected) */
+}
+
+/* Queue the tree's oldest pending job on the libuv pool (JS thread only). */
+static void start_next(napi_env env, tree_h *h) {
+  if (h->busy || !h->qhead) return;
+  job_t *j = h->qhead;
+  h->qhead = j->next;
+  if (!h->qhead) h->qtail = NULL;
+  h->busy = 1;
+  napi_queue_async_work(env, j->work);
 }
 
 static napi_value js_apply(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  napi_get_cb_info(env, info, &argc, argv, NULL, NULL);
   job_t *j = make_job(env, info);
   if (!j) return NULL;
   napi_value promise, name;
+  napi_create_reference(env, argv[0], 1, &j->tree_ref);
   napi_create_promise(env, &j->def, &promise);
   napi_create_string_utf8(env, "crdtm.apply", NAPI_AUTO_LENGTH, &name);
   napi_create_async_work(env, NULL, name, async_exec, async_done, j, &j->work);
-  napi_queue_async_work(env, j->work);
+  tree_h *h = j->h;
+  if (h->qtail) h->qtail->next = j;
+  else h->qhead = j;
+  h->qtail = j;
+  start_next(env, h);
   return promise;
 }
 
@@ -421,6 +464,10 @@ static napi_value js_release(napi_env env, napi_callback_info info) {
   napi_get_cb_info(env, info, &argc, argv, NULL, NULL);
   tree_h *h = argc > 0 ? get_tree(env, argv[0]) : NULL;
   if (!h) return NULL;
+  if (h->busy || h->qhead) {
+    napi_throw_error(env, "E_BUSY", "crdtm: release while async applies of this tree are pending");
+    return NULL;
+  }
   pthread_mutex_lock(&g_mu);
   crdtm_tree_destroy(h->t);
   h->t = NULL;

@@ -72,27 +72,47 @@ def test_addon_matches_oracle(tmp_path):
     cases.append({"replica": 0, "calls": [encoder(big)], "since": [adds[10], adds[-1], 12345]})
     expect.append((0, [big]))
 
+    # the same scenarios again with every apply queued before the first is
+    # awaited (the addon's per-tree FIFO keeps the reference's call order)
+    for (replica, calls), case in list(zip(expect, cases))[:len(SCENARIOS)]:
+        if len(calls) > 1:
+            cases.append(dict(case, queued=True))
+            expect.append((replica, calls))
+
+    # oracle side first: the expected lastOperation of every call (its JSON
+    # bytes are produced by Node's JSON.stringify in napi_run.js, not by this
+    # package's encoder)
+    from crdtm.tree import VALUES
+    from oracle.oracle import lib as olib
+    oracle_runs = []
+    for (replica, calls), case in zip(expect, cases):
+        ot = olib().orc_init(replica)
+        per_call = []
+        for op in calls:
+            leaves = flatten(op) if op.kind == "batch" else [op]
+            _, rc, oerr = oracle_apply_arrays(pack(leaves), len(leaves), is_batch=op.kind == "batch", tree=ot)
+            last = None
+            if rc == 0:
+                olast, oisb = oracle_log(ot, 1)
+                last = {"isBatch": oisb, "ops": [[k, t, list(p), VALUES.value(v) if k == 0 else None]
+                                                 for k, t, p, v in olast]}
+            per_call.append((rc, oerr))
+            case.setdefault("expectLast", []).append(last)
+        oracle_runs.append((ot, per_call))
+
     fin, fout = tmp_path / "in.json", tmp_path / "out.json"
     fin.write_text(json.dumps(cases))
     subprocess.run([NODE, os.path.join(ROOT, "tests", "napi_run.js"), str(fin), str(fout)], check=True, timeout=300)
     got = json.loads(fout.read_text())
 
-    from oracle.oracle import lib as olib
-    for (replica, calls), case, res in zip(expect, cases, got):
-        ot = olib().orc_init(replica)
-        for op, text, r in zip(calls, case["calls"], res["results"]):
-            leaves = flatten(op) if op.kind == "batch" else [op]
-            _, rc, oerr = oracle_apply_arrays(pack(leaves), len(leaves), is_batch=op.kind == "batch", tree=ot)
+    for (ot, per_call), case, res in zip(oracle_runs, cases, got):
+        for (rc, oerr), text, r, want in zip(per_call, case["calls"], res["results"], res["expectLast"]):
             assert r["code"] == rc, (text[:80], r, rc)
             if rc != 0:
                 assert r["errIndex"] == oerr
                 continue
-            # lastOperation: same ops as the oracle's, and the JSON is the encoder's bytes
-            olast, oisb = oracle_log(ot, 1)
-            dec = decoder(r["lastOperation"])
-            dl = flatten(dec) if dec.kind == "batch" else [dec]
-            assert len(dl) == len(olast)
-            assert r["lastOperation"] == encoder(dec)
+            # lastOperation: byte-identical to Encode.encode 0 of the oracle's lastOperation
+            assert r["lastOperation"] == want, (r["lastOperation"][:200], want[:200])
         # full log and visible document against the oracle
         log = decoder(res["log"])
         olog, _ = oracle_log(ot, 0)

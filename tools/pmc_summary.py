@@ -3,10 +3,14 @@
 
     python tools/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_sq [--json out.json]
 
-FETCH_SIZE / WRITE_SIZE are in KB per dispatch. On gfx950 FETCH_SIZE counts
-half the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md, HBM);
-the `hbm_MB` column applies that x2 correction to FETCH_SIZE, so it is an
-upper bound for kernels whose reads are not wide streams.
+FETCH_SIZE / WRITE_SIZE are in KB per dispatch. Calibration on this box
+(tools/pmc_calibrate.hip -> profiles/r2_pmc_calibration.txt): coalesced reads
+of 4, 8 and 16 B per lane count exactly half their bytes in FETCH_SIZE;
+WRITE_SIZE counts writes exactly; a random 4 B gather counts 64 B per access,
+which is the true transfer (half-line request) or half of it (full line). So
+every kernel gets two figures: `raw_MB` = F + W (a lower bound of its HBM
+bytes) and `hbm_MB` = 2F + W (exact for streaming reads, an upper bound for
+gather-heavy kernels).
 """
 import csv
 import os
@@ -47,12 +51,14 @@ def main(args):
             for c, v in cs.items():
                 agg[k][c] = (sum(v) / len(v), len(v))
     cols = sorted({c for k in agg for c in agg[k]})
-    print("kernel".ljust(40), "vgpr lds scr", " ".join(c[:14].rjust(14) for c in cols), "hbm_MB".rjust(9))
+    print("kernel".ljust(40), "vgpr lds scr", " ".join(c[:14].rjust(14) for c in cols), "raw_MB".rjust(9),
+          "hbm_MB".rjust(9))
     for k in sorted(agg, key=lambda k: -agg[k].get("FETCH_SIZE", (0, 0))[0] - agg[k].get("WRITE_SIZE", (0, 0))[0]):
         vals = " ".join(f"{agg[k][c][0]:14.1f}" if c in agg[k] else " " * 14 for c in cols)
         f = agg[k].get("FETCH_SIZE", (0, 0))[0]
         w = agg[k].get("WRITE_SIZE", (0, 0))[0]
-        print(k[:40].ljust(40), " ".join(meta.get(k, ("?", "?", "?"))).ljust(12), vals, f"{(2 * f + w) / 1024:9.1f}")
+        print(k[:40].ljust(40), " ".join(meta.get(k, ("?", "?", "?"))).ljust(12), vals, f"{(f + w) / 1024:9.1f}",
+              f"{(2 * f + w) / 1024:9.1f}")
     if out_json:
         import json
         res = {}
@@ -61,8 +67,8 @@ def main(args):
             e = {c: v[0] for c, v in cs.items()}
             e["dispatches"] = max(v[1] for v in cs.values())
             if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
-                # bytes per dispatch; FETCH_SIZE doubled (gfx950 counts half of wide streaming reads)
-                e["hbm_bytes_corrected"] = (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
+                # bytes per dispatch: [raw, corrected] = [F + W, 2F + W] (see the module docstring)
+                e["hbm_bytes"] = (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
                 e["hbm_bytes_raw"] = (e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
             res.setdefault(b, e)
         json.dump(res, open(out_json, "w"), indent=1, sort_keys=True)
