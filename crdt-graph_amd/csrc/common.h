@@ -85,6 +85,10 @@ struct DevResult {
   uint32_t fl_keys;         // flat: Adds with a timestamp slot
   uint32_t fl_slow;         // flat: ops that need per-op statuses (empty path, ts 0)
   uint32_t fl_part[16 * 32];  // flat: slots holding an Add, 16 partial counts one cache line apart
+  uint32_t run_count;       // flat order: ep-runs (scan total)
+  uint32_t run_fail;        // flat order: the run tree is deeper than RUN_MAXD (generic list ranking instead)
+  uint32_t run_maxd;        // flat order: deepest run
+  uint32_t run_lhist[64];   // flat order: runs per depth
 };
 
 #define HIP_CHECK(x)                                                                         \

@@ -1924,30 +1924,7 @@ __global__ void __launch_bounds__(BLOCK) k_fl_rep_collect(OpsDev o, uint32_t nr,
 // (flat10m: max walk 312 nodes -> 23 runs). anc[] is overwritten with ep as
 // walks finish; a concurrent reader then sees ep(h) instead of anchor(h),
 // which skips only nodes > h > x, so every walk stays exact.
-// Fused with the child count of each effective parent (the sentinel's count
-// aggregated per workgroup).
-__global__ void __launch_bounds__(BLOCK) k_fl_ep(uint32_t Q, uint32_t* anc, const uint32_t* rh, uint32_t* cnt) {
-  uint32_t hot = 0;
-  GRID_STRIDE(x, Q) {
-    uint32_t d = anc[x];
-    if (d == ABSENT) continue;
-    if (d != Q && d > x) {
-      while (d != Q && d > x) {
-        const uint32_t h = rh[d];
-        if (h < x) {
-          d = x - 1;
-          break;
-        }
-        d = __hip_atomic_load(&anc[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __hip_atomic_store(&anc[x], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (d == Q) ++hot;
-    else atomicAdd(&cnt[d], 1u);
-  }
-  hot = block_sum(hot);
-  if (threadIdx.x == 0 && hot) atomicAdd(&cnt[Q], hot);
-}
+// (k_fl_ep_runs, with the K4 run decomposition below.)
 
 // Run heads: rh[q] = max{q' <= q : anc[q'] != q' - 1}, an inclusive
 // max-scan over head flags (scan.h).
@@ -2182,6 +2159,232 @@ __global__ void __launch_bounds__(BLOCK) k_fl_log_copy(OpsDev o, TreeDev T) {
 }
 
 // ---------------------------------------------------------------------------
+// K4 (flat): the document order by ep-run decomposition. An ep-run is a
+// maximal interval of present slots [h, h + len) with ep(q) = q - 1 inside.
+// A node's children all have larger slots (an effective parent has the
+// smaller timestamp), so q + 1 is the smallest, i.e. the LAST child of q in
+// the descending order (src/Internal/Node.elm:93-104 via the closed form,
+// DESIGN.md): the pre-order visits q, then q's other ("side") children's
+// subtrees, then q + 1. With side(q) = the sizes of q's side children's
+// subtrees and P(q) = sum over the run's slots before q of (1 + side), a
+// slot's document rank is pos(head) + P(q), the subtree of run r has
+// T(r) = P(end) and a side child run r of slot j starts at
+// pos(j) + 1 + (the subtrees of j's side children with a larger slot).
+// Runs form a shallow tree (flat10m: 1.0M runs, depth <= 11): T comes
+// bottom-up level by level, pos(head) top-down as a sum along the run's
+// ancestor chain. Every per-slot pass streams through slot order; only the
+// 1M-run passes gather. A run tree deeper than RUN_MAXD takes the generic
+// Euler-tour list ranking instead (run_fail).
+// ---------------------------------------------------------------------------
+constexpr uint32_t RUN_MAXD = 64;
+
+// K2a (see above); hflag[q] = q heads an ep-run.
+__global__ void __launch_bounds__(BLOCK) k_fl_ep_runs(uint32_t Q, uint32_t* anc, const uint32_t* rh, uint32_t* hflag) {
+  GRID_STRIDE(x, Q) {
+    uint32_t d = anc[x];
+    if (d == ABSENT) {
+      hflag[x] = 0;
+      continue;
+    }
+    if (d != Q && d > x) {
+      while (d != Q && d > x) {
+        const uint32_t h = rh[d];
+        if (h < x) {
+          d = x - 1;
+          break;
+        }
+        d = __hip_atomic_load(&anc[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __hip_atomic_store(&anc[x], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    hflag[x] = (x == 0 || d != x - 1) ? 1u : 0u;
+  }
+}
+
+// heads[run] = its first slot (rid = inclusive count of heads); side[] := 0
+__global__ void __launch_bounds__(BLOCK) k_run_heads(uint32_t Q, const uint32_t* ep, const uint32_t* rid,
+                                                     uint32_t* heads, uint32_t* side) {
+  GRID_STRIDE(q, Q) {
+    const uint32_t e = ep[q];
+    side[q] = 0;
+    if (e != ABSENT && (q == 0 || e != q - 1)) heads[rid[q] - 1] = q;
+  }
+}
+
+struct RunArr {
+  const uint32_t* nR;        // device: number of runs
+  uint32_t* heads;
+  uint32_t* par;             // parent run (NONE: a child of the root sentinel)
+  uint32_t* len;
+  uint32_t* nch;             // child runs
+  unsigned long long* ca;    // children arrived << 32 | their subtree sizes
+  uint32_t* T;               // subtree size
+  uint32_t* w;               // top-down increment along the chain
+  uint32_t* posh;            // document rank of the head
+};
+
+#define RUN_LOOP(r) for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x, nr_ = *a.nR; r < nr_; r += gridDim.x * blockDim.x)
+
+// parent run and length of every run; the sibling sort's input (key =
+// attach slot, the root sentinel = Q) listed in descending run order, so the
+// stable sort leaves siblings at one slot in descending slot order
+__global__ void __launch_bounds__(BLOCK) k_run_par(RunArr a, uint32_t Q, uint32_t K, const uint32_t* ep,
+                                                   const uint32_t* rid, const uint32_t* qc, uint32_t* skey,
+                                                   uint32_t* sval) {
+  const uint32_t R = *a.nR;
+  RUN_LOOP(r) {
+    const uint32_t h = a.heads[r];
+    const uint32_t hn = r + 1 < R ? a.heads[r + 1] : Q;
+    const uint32_t ln = qc ? (r + 1 < R ? qc[hn] : K) - qc[h] : hn - h;
+    const uint32_t p = ep[h];
+    a.par[r] = p == Q ? NONE : rid[p] - 1;
+    a.len[r] = ln;
+    a.nch[r] = 0;
+    a.ca[r] = 0;
+    skey[R - 1 - r] = p;
+    sval[R - 1 - r] = r;
+  }
+}
+
+// children per parent run: the last sibling of every attach slot's group adds
+// the group's size (one atomic per group, not per child)
+__global__ void __launch_bounds__(BLOCK) k_run_nch(RunArr a, uint32_t Q, const uint32_t* pk, const uint32_t* sarr,
+                                                   const uint32_t* sgs) {
+  const uint32_t R = *a.nR;
+  RUN_LOOP(k) {
+    const uint32_t p = pk[k];
+    if (p != Q && (k + 1 == R || pk[k + 1] != p)) atomicAdd(&a.nch[a.par[sarr[k]]], k - sgs[k] + 1);
+  }
+}
+
+// Bottom-up subtree sizes in one launch: every leaf run climbs its chain of
+// ancestors; a child announces its size with ONE 64-bit device-scope atomic
+// {arrivals += 1, sizes += T} (memory-side, coherent across the XCDs), and
+// the child that arrives last holds the sum of all its siblings' sizes in
+// the returned value, so it finalises the parent and climbs on. Any depth;
+// a parent with c children serialises c atomics (~12 ns each).
+__global__ void __launch_bounds__(BLOCK) k_run_tree_up(RunArr a) {
+  RUN_LOOP(r) {
+    if (a.nch[r] != 0) continue;  // an inner run: finalised by its last child
+    uint32_t x = r, t = a.len[r];
+    for (;;) {
+      a.T[x] = t;
+      const uint32_t p = a.par[x];
+      if (p == NONE) break;
+      const unsigned long long old = atomicAdd(&a.ca[p], (1ULL << 32) | t);
+      if (static_cast<uint32_t>(old >> 32) + 1u != a.nch[p]) break;
+      t = a.len[p] + static_cast<uint32_t>(old) + t;
+      x = p;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_run_gather(RunArr a, const uint32_t* sarr, uint32_t* tk) {
+  RUN_LOOP(k) tk[k] = a.T[sarr[k]];
+}
+
+// inclusive max-scan input: k where a new attach slot starts
+struct SubgroupGen {
+  static constexpr bool kStriped = false;
+  const uint32_t* pk;
+  __device__ __forceinline__ bool aligned(uint64_t) const { return false; }
+  __device__ __forceinline__ uint4 load4(uint64_t) const { return make_uint4(0u, 0u, 0u, 0u); }
+  __device__ __forceinline__ void load(uint64_t b, uint64_t n, uint32_t* v) const {
+#pragma unroll
+    for (int j = 0; j < DS_ITEMS; ++j) {
+      const uint64_t k = b + j;
+      v[j] = (k < n && (k == 0 || pk[k] != pk[k - 1])) ? static_cast<uint32_t>(k) : 0u;
+    }
+  }
+};
+
+// side(p) = the subtree sizes of the runs hanging from slot p: the last
+// sibling of each slot's group stores the group's sum (no atomics)
+__global__ void __launch_bounds__(BLOCK) k_run_side(RunArr a, uint32_t Q, const uint32_t* pk, const uint32_t* tk,
+                                                    const uint32_t* xs, const uint32_t* sgs, uint32_t* side) {
+  const uint32_t R = *a.nR;
+  RUN_LOOP(k) {
+    const uint32_t p = pk[k];
+    if (p != Q && (k + 1 == R || pk[k + 1] != p)) side[p] = xs[k] + tk[k] - xs[sgs[k]];
+  }
+}
+
+// G(q) = exclusive prefix of (1 + side(q)) over present slots: a slot's rank
+// inside its run is G(q) - G(head)
+struct SideGen {
+  static constexpr bool kStriped = false;
+  const uint32_t* ep;
+  const uint32_t* side;
+  __device__ __forceinline__ bool aligned(uint64_t) const { return false; }
+  __device__ __forceinline__ uint4 load4(uint64_t) const { return make_uint4(0u, 0u, 0u, 0u); }
+  __device__ __forceinline__ void load(uint64_t b, uint64_t n, uint32_t* v) const {
+    if (b + DS_ITEMS <= n) {
+#pragma unroll
+      for (int j = 0; j < DS_ITEMS; j += 4) {
+        const uint4 e = *reinterpret_cast<const uint4*>(ep + b + j);
+        const uint4 s = *reinterpret_cast<const uint4*>(side + b + j);
+        v[j] = e.x != ABSENT ? 1u + s.x : 0u;
+        v[j + 1] = e.y != ABSENT ? 1u + s.y : 0u;
+        v[j + 2] = e.z != ABSENT ? 1u + s.z : 0u;
+        v[j + 3] = e.w != ABSENT ? 1u + s.w : 0u;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < DS_ITEMS; ++j) v[j] = (b + j < n && ep[b + j] != ABSENT) ? 1u + side[b + j] : 0u;
+    }
+  }
+};
+
+// w(r): the head's rank minus its parent run head's rank (root children:
+// the rank itself)
+__global__ void __launch_bounds__(BLOCK) k_run_w(RunArr a, uint32_t Q, const uint32_t* sarr, const uint32_t* pk,
+                                                 const uint32_t* xs, const uint32_t* sgs, const uint32_t* G) {
+  RUN_LOOP(k) {
+    const uint32_t r = sarr[k], p = pk[k];
+    const uint32_t off = xs[k] - xs[sgs[k]];  // siblings hanging from p with a larger slot
+    a.w[r] = p == Q ? off : G[p] - G[a.heads[a.par[r]]] + 1u + off;
+  }
+}
+
+// head ranks: the sum of w along the ancestor chain; a chain longer than
+// RUN_MAXD flags the generic path instead (quadratic walks on deep trees)
+__global__ void __launch_bounds__(BLOCK) k_run_pos(RunArr a, DevResult* dres) {
+  RUN_LOOP(r) {
+    uint32_t s = a.w[r], d = 0;
+    for (uint32_t x = a.par[r]; x != NONE; x = a.par[x]) {
+      if (++d > RUN_MAXD) {
+        atomicOr(&dres->run_fail, 1u);
+        break;
+      }
+      s += a.w[x];
+    }
+    a.posh[r] = s;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, const uint32_t* ep, const uint32_t* rid,
+                                                      const uint32_t* G, const uint32_t* qc, uint32_t* doc) {
+  GRID_STRIDE(q, Q) {
+    if (ep[q] == ABSENT) continue;
+    const uint32_t r = rid[q] - 1;
+    doc[a.posh[r] + G[q] - G[a.heads[r]]] = 1 + (qc ? qc[q] : q);
+  }
+}
+
+// child counts of every node (the generic K2b/K4 fallback)
+__global__ void __launch_bounds__(BLOCK) k_fl_count(uint32_t Q, const uint32_t* ep, uint32_t* cnt) {
+  uint32_t hot = 0;
+  GRID_STRIDE(x, Q) {
+    const uint32_t d = ep[x];
+    if (d == ABSENT) continue;
+    if (d == Q) ++hot;
+    else atomicAdd(&cnt[d], 1u);
+  }
+  hot = block_sum(hot);
+  if (threadIdx.x == 0 && hot) atomicAdd(&cnt[Q], hot);
+}
+
+// ---------------------------------------------------------------------------
 // Host orchestration
 // ---------------------------------------------------------------------------
 thread_local crdtm_ctx* g_prof = nullptr;
@@ -2402,13 +2605,8 @@ static int run_replay(crdtm_tree* t, const OpsDev& o, uint8_t* st, crdtm_result*
   return CRDTM_E_NOMEM;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_fl_init(uint32_t Q, unsigned long long* rec, uint32_t* cnt,
-                                                   uint32_t* fill) {
-  GRID_STRIDE(q, Q + 2) {
-    if (q < Q) rec[q] = REC_EMPTY;
-    cnt[q] = 0;
-    fill[q] = 0;
-  }
+__global__ void __launch_bounds__(BLOCK) k_fl_init(uint32_t Q, unsigned long long* rec) {
+  GRID_STRIDE(q, Q) rec[q] = REC_EMPTY;
 }
 
 // Launches k_range_reset when a merge leaves apply_batch by any path.
@@ -2432,7 +2630,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   uint32_t* anc = ws.alloc<uint32_t>(U);
   uint32_t* cnt = ws.alloc<uint32_t>(U + 1);
   uint32_t* fill = ws.alloc<uint32_t>(U + 1);
-  LAUNCH(k_fl_init, dim3(grid_for(U + 1, BLOCK, 4096)), dim3(BLOCK), 0, s, Q, rec, cnt, fill);
+  LAUNCH(k_fl_init, dim3(grid_for(Q, BLOCK, 4096)), dim3(BLOCK), 0, s, Q, rec);
   LAUNCH(k_fl_claim, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix, Q, rec, t->timestamp, c->rtab, dr);
   LAUNCH(k_fl_check, dim3(grid_for(Q / 2 + 1, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, rec, dr);
   int r;
@@ -2498,31 +2696,55 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     if ((r = grow_tree(t, need))) return r;
   }
   if (K > 0) {
-    // ---- K2: effective parents, children lists in descending slot order ----
-    uint32_t* carr = ws.alloc<uint32_t>(U);
-    uint32_t* ns = ws.alloc<uint32_t>(U);
+    // ---- K2a: effective parents (run-skipping walk over the anchor runs) ----
     const uint32_t gq = grid_for(Q);
     uint32_t* rh = ws.alloc<uint32_t>(Q);
     if ((r = dscan<MaxOp, true>(RunHeadGen{rec, anc}, rh, Q, nullptr, ws, s, nullptr))) return r;
-    LAUNCH(k_fl_ep, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, rh, cnt);
-    uint32_t* n_child = &dr->n_sentinels;  // scratch word for the scan total
-    if ((r = scan_excl_u32(cnt, cnt, U + 1, n_child, ws, s))) return r;
-    LAUNCH(k_fl_scatter, dim3(gq), dim3(BLOCK), 0, s, Q, anc, cnt, fill, carr);
-    {
-      const uint32_t gr = grid_for(Q, BLOCK, 2048);
-      uint32_t* bc = ws.alloc<uint32_t>(gr + 1);
-      LAUNCH(k_fl_root_count, dim3(gr), dim3(BLOCK), 0, s, Q, anc, bc);
-      if ((r = scan_excl_u32(bc, bc, gr, nullptr, ws, s))) return r;
-      LAUNCH(k_fl_root_place, dim3(gr), dim3(BLOCK), 0, s, Q, anc, bc, cnt, carr);
-    }
-    if ((r = segmented_sort_desc_id(cnt, U, carr, U, ws, s, dr, Q))) return r;
-    LAUNCH(k_fl_links, dim3(gq), dim3(BLOCK), 0, s, anc, cnt, n_child, carr, ns);
+    uint32_t* rid = ws.alloc<uint32_t>(Q);  // ep-run head flags, then inclusive head counts
+    LAUNCH(k_fl_ep_runs, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, rh, rid);
+    if ((r = dscan<SumOp, true>(ArrGen{rid}, rid, Q, &dr->run_count, ws, s, nullptr))) return r;
     uint32_t* qc = nullptr;
     if (Q != K) {  // slots with no node: compact
       qc = ws.alloc<uint32_t>(Q);
       LAUNCH(k_fl_present, dim3(gq), dim3(BLOCK), 0, s, Q, anc, qc);
       if ((r = scan_excl_u32(qc, qc, Q, nullptr, ws, s))) return r;
     }
+    // ---- K4: ep-runs, parent runs, sibling order (stable radix sort by attach slot) ----
+    RunArr ra;
+    ra.nR = &dr->run_count;
+    ra.heads = ws.alloc<uint32_t>(K + 1);
+    ra.par = ws.alloc<uint32_t>(K + 1);
+    ra.len = ws.alloc<uint32_t>(K + 1);
+    ra.nch = ws.alloc<uint32_t>(K + 1);
+    ra.ca = ws.alloc<unsigned long long>(K + 1);
+    ra.T = ws.alloc<uint32_t>(K + 1);
+    ra.w = ws.alloc<uint32_t>(K + 1);
+    ra.posh = ws.alloc<uint32_t>(K + 1);
+    uint32_t* side = ws.alloc<uint32_t>(Q + 1);  // side(q), then G(q)
+    uint32_t* sk[2] = {ws.alloc<uint32_t>(K + 1), ws.alloc<uint32_t>(K + 1)};
+    uint32_t* sv[2] = {ws.alloc<uint32_t>(K + 1), ws.alloc<uint32_t>(K + 1)};
+    uint32_t* xs = ws.alloc<uint32_t>(K + 1);
+    uint32_t* sgs = ws.alloc<uint32_t>(K + 1);
+    const uint32_t gr = grid_for(K, BLOCK, 2048);
+    LAUNCH(k_run_heads, dim3(gq), dim3(BLOCK), 0, s, Q, anc, rid, ra.heads, side);
+    LAUNCH(k_run_par, dim3(gr), dim3(BLOCK), 0, s, ra, Q, K, anc, rid, qc, sk[0], sv[0]);
+    uint32_t sbits = 8;
+    while (sbits < 32 && (static_cast<uint64_t>(Q) >> sbits) != 0) sbits += 8;
+    uint32_t *pk = nullptr, *sarr = nullptr;  // attach slot, run: siblings grouped by slot, slots ascending
+    if ((r = radix_sort_pairs(sk[0], sv[0], sk[1], sv[1], ra.nR, K, sbits, ws, s, &pk, &sarr))) return r;
+    uint32_t* tk = pk == sk[0] ? sk[1] : sk[0];  // (free after the sort)
+    if ((r = dscan<MaxOp, true>(SubgroupGen{pk}, sgs, K, nullptr, ws, s, nullptr, ra.nR))) return r;
+    LAUNCH(k_run_nch, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, sarr, sgs);
+    // ---- subtree sizes (one launch), slot ranks inside runs, head ranks ----
+    LAUNCH(k_run_tree_up, dim3(gr), dim3(BLOCK), 0, s, ra);
+    LAUNCH(k_run_gather, dim3(gr), dim3(BLOCK), 0, s, ra, sarr, tk);
+    if ((r = dscan<SumOp, false>(ArrGen{tk}, xs, K, nullptr, ws, s, nullptr, ra.nR))) return r;
+    LAUNCH(k_run_side, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, tk, xs, sgs, side);
+    if ((r = dscan<SumOp, false>(SideGen{anc, side}, side, Q, nullptr, ws, s, nullptr))) return r;
+    LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, sgs, side);
+    LAUNCH(k_run_pos, dim3(gr), dim3(BLOCK), 0, s, ra, dr);
+    LAUNCH(k_run_expand, dim3(gq), dim3(BLOCK), 0, s, ra, Q, anc, rid, side, qc, t->d.doc);
+    LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d);
     uint32_t* logidx = nullptr;
     if (!all_applied) {  // compacted log (its scans share the ctx scan pool: main stream)
       logidx = ws.alloc<uint32_t>(n + 1);
@@ -2534,18 +2756,35 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
       LAUNCH(k_log_tail, dim3(1), dim3(1), 0, s, t->d, 0u, &dr->log_n, 0u, &dr->log_npath);
     }
     // ---- commit ----
-    // (Measured: running the commit and the log copy on the ctx side stream
-    // while the list ranking runs does not shorten the merge — the ranking
-    // kernels keep every CU busy, the copies just stretch — so one stream.)
     LAUNCH(k_fl_commit, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK),
            maxr + 1 <= HOST_RANGES ? 2 * (maxr + 1) * sizeof(uint32_t) : 0, s, o, ix, Q, maxr + 1, anc, rec, qc,
            logidx, t->d);
     if (all_applied) LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
-    // ---- K4: Euler tour + list ranking -> document order ----
-    if ((r = list_rank_fused(FlatEulerSrc{Q, anc, cnt, carr, ns}, 2ULL * U, 2 * Q, FlatDocSink{Q, t->d.doc, qc}, ws,
-                             s)))
-      return r;
-    LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d);
+    if ((r = sync_read(c))) return r;
+    if (c->hres->run_fail) {
+      // ---- a run tree deeper than RUN_MAXD: children of every node, Euler tour + list ranking ----
+      uint32_t* carr = ws.alloc<uint32_t>(U);
+      uint32_t* ns = ws.alloc<uint32_t>(U);
+      HIP_CHECK(hipMemsetAsync(cnt, 0, (U + 1) * sizeof(uint32_t), s));
+      HIP_CHECK(hipMemsetAsync(fill, 0, (U + 1) * sizeof(uint32_t), s));
+      LAUNCH(k_fl_count, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, cnt);
+      uint32_t* n_child = &dr->n_sentinels;  // scratch word for the scan total
+      if ((r = scan_excl_u32(cnt, cnt, U + 1, n_child, ws, s))) return r;
+      LAUNCH(k_fl_scatter, dim3(gq), dim3(BLOCK), 0, s, Q, anc, cnt, fill, carr);
+      {
+        const uint32_t gb = grid_for(Q, BLOCK, 2048);
+        uint32_t* bc = ws.alloc<uint32_t>(gb + 1);
+        LAUNCH(k_fl_root_count, dim3(gb), dim3(BLOCK), 0, s, Q, anc, bc);
+        if ((r = scan_excl_u32(bc, bc, gb, nullptr, ws, s))) return r;
+        LAUNCH(k_fl_root_place, dim3(gb), dim3(BLOCK), 0, s, Q, anc, bc, cnt, carr);
+      }
+      if ((r = segmented_sort_desc_id(cnt, U, carr, U, ws, s, dr, Q))) return r;
+      LAUNCH(k_fl_links, dim3(gq), dim3(BLOCK), 0, s, anc, cnt, n_child, carr, ns);
+      if ((r = list_rank_fused(FlatEulerSrc{Q, anc, cnt, carr, ns}, 2ULL * U, 2 * Q, FlatDocSink{Q, t->d.doc, qc},
+                               ws, s)))
+        return r;
+      LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d);
+    }
   } else if (all_applied) {
     LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
   }

@@ -4,6 +4,8 @@
 // These are the building blocks of north-star kernels (2) segmented sibling
 // sort and (4) Euler-tour list ranking. Everything is integer, HBM-bound work.
 
+#include <algorithm>
+
 #include "engine.h"
 #include "listrank.h"
 #include "scan.h"
@@ -445,6 +447,11 @@ int segmented_sort(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, ui
   return segmented_sort_t(seg_start, n_seg, carr, n_items, ArrKey{sort_key}, ws, st, dres, NONE);
 }
 
+int segmented_sort_skip(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items,
+                        const long long* sort_key, Arena& ws, hipStream_t st, DevResult* dres, uint32_t skip) {
+  return segmented_sort_t(seg_start, n_seg, carr, n_items, ArrKey{sort_key}, ws, st, dres, skip);
+}
+
 int segmented_sort_desc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items, Arena& ws,
                            hipStream_t st, DevResult* dres, uint32_t skip) {
   return segmented_sort_t(seg_start, n_seg, carr, n_items, NegIdKey{}, ws, st, dres, skip);
@@ -453,6 +460,111 @@ int segmented_sort_desc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* 
 int segmented_sort_asc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* carr, uint32_t n_items, Arena& ws,
                           hipStream_t st, DevResult* dres) {
   return segmented_sort_t(seg_start, n_seg, carr, n_items, IdKey{}, ws, st, dres, NONE);
+}
+
+// ---------------------------------------------------------------------------
+// Stable LSD radix sort of (u32 key, u32 value) pairs, 8 bits per pass. The
+// item count may live on the device (n_dev: read by every kernel); the host
+// gives an upper bound for the grid. Per pass: per-tile digit histograms
+// (digit-major, so one exclusive scan gives every (digit, tile) its output
+// base), then every tile ranks its items stably — within a wave by digit
+// match masks from 8 ballots, across the workgroup's waves and rounds by
+// LDS digit counters — and scatters them. No global atomics: a digit shared
+// by many items costs nothing extra (counting sorts by parent pay a
+// serialised device-scope atomic per item on a hot parent, ~12 ns each).
+// ---------------------------------------------------------------------------
+constexpr uint32_t RS_ITEMS = 8;
+constexpr uint32_t RS_TILE = BLOCK * RS_ITEMS;
+
+__global__ void __launch_bounds__(BLOCK) k_rs_hist(const uint32_t* __restrict__ keys, const uint32_t* n_dev,
+                                                   uint32_t shift, uint32_t ntiles, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[256];
+  const uint32_t n = *n_dev;
+  for (uint32_t j = threadIdx.x; j < 256; j += BLOCK) h[j] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * RS_TILE;
+#pragma unroll
+  for (uint32_t j = 0; j < RS_ITEMS; ++j) {
+    const uint32_t i = base + j * BLOCK + threadIdx.x;
+    if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < 256; d += BLOCK) hist[d * ntiles + blockIdx.x] = h[d];
+}
+
+__global__ void __launch_bounds__(BLOCK) k_rs_scatter(const uint32_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ vals, const uint32_t* n_dev,
+                                                      uint32_t shift, uint32_t ntiles, const uint32_t* __restrict__ off,
+                                                      uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
+  constexpr uint32_t NW = BLOCK / 64;
+  __shared__ uint32_t run[256];
+  __shared__ uint32_t wc[NW][256];
+  const uint32_t n = *n_dev;
+  const uint32_t base = blockIdx.x * RS_TILE;
+  if (base >= n) return;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (uint32_t d = threadIdx.x; d < 256; d += BLOCK) run[d] = off[d * ntiles + blockIdx.x];
+  for (uint32_t d = lane; d < 256; d += 64) wc[wv][d] = 0;  // kept all-zero between rounds
+  const unsigned long long lt = (1ULL << lane) - 1ULL;
+  __syncthreads();
+  for (uint32_t j = 0; j < RS_ITEMS; ++j) {
+    const uint32_t i = base + j * BLOCK + threadIdx.x;
+    const bool valid = i < n;
+    const uint32_t k = valid ? keys[i] : 0u;
+    const uint32_t v = valid ? vals[i] : 0u;
+    const uint32_t d = (k >> shift) & 255u;
+    unsigned long long m = __ballot(valid);
+#pragma unroll
+    for (uint32_t b = 0; b < 8; ++b) {
+      const unsigned long long bb = __ballot((d >> b) & 1u);
+      m &= ((d >> b) & 1u) ? bb : ~bb;
+    }
+    const uint32_t lr = static_cast<uint32_t>(__popcll(m & lt));
+    const bool leader = valid && lr == 0;  // one lane per digit present in the wave
+    if (leader) wc[wv][d] = static_cast<uint32_t>(__popcll(m));
+    __syncthreads();
+    uint32_t pre = 0;
+    for (uint32_t w = 0; w < wv; ++w) pre += wc[w][d];
+    const uint32_t pos = run[d] + pre + lr;
+    __syncthreads();  // every lane has read run[] and wc[]
+    for (uint32_t dd = threadIdx.x; dd < 256; dd += BLOCK) {
+      uint32_t t = 0;
+      for (uint32_t w = 0; w < NW; ++w) t += wc[w][dd];
+      run[dd] += t;
+    }
+    __syncthreads();  // run[] advanced, wc[] read
+    if (leader) wc[wv][d] = 0;
+    if (valid) {
+      kout[pos] = k;
+      vout[pos] = v;
+    }
+  }
+}
+
+// Sorts n_dev (<= n_max) pairs by the low `bits` bits of the keys, stably.
+// The result lands in (k0, v0) when the pass count is even, else in (k1, v1):
+// *out_k / *out_v point to it.
+// *hist_out (optional): the last pass's scanned histogram, digit d's first
+// output position at [d * *ntiles_out].
+int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, const uint32_t* n_dev, uint32_t n_max,
+                     uint32_t bits, Arena& ws, hipStream_t st, uint32_t** out_k, uint32_t** out_v, uint32_t** hist_out,
+                     uint32_t* ntiles_out) {
+  const uint32_t ntiles = std::max<uint32_t>(1, (n_max + RS_TILE - 1) / RS_TILE);
+  uint32_t* hist = ws.alloc<uint32_t>(256ULL * ntiles + 1);
+  if (hist_out) *hist_out = hist;
+  if (ntiles_out) *ntiles_out = ntiles;
+  uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
+  for (uint32_t shift = 0; shift < bits; shift += 8) {
+    LAUNCH(k_rs_hist, dim3(ntiles), dim3(BLOCK), 0, st, ki, n_dev, shift, ntiles, hist);
+    int r = scan_excl_u32(hist, hist, 256ULL * ntiles, nullptr, ws, st);
+    if (r) return r;
+    LAUNCH(k_rs_scatter, dim3(ntiles), dim3(BLOCK), 0, st, ki, vi, n_dev, shift, ntiles, hist, ko, vo);
+    std::swap(ki, ko);
+    std::swap(vi, vo);
+  }
+  *out_k = ki;
+  *out_v = vi;
+  return CRDTM_OK;
 }
 
 // ---------------------------------------------------------------------------

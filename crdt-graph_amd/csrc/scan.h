@@ -35,7 +35,7 @@ template <class OP, bool INCL, class GEN>
 __global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* out, uint64_t n,
                                                  unsigned long long* __restrict__ status, uint32_t* __restrict__ ticket,
                                                  uint32_t ntiles, uint32_t epoch, uint32_t* __restrict__ total,
-                                                 uint32_t* __restrict__ err) {
+                                                 uint32_t* __restrict__ err, const uint32_t* n_dev) {
   __shared__ uint32_t s_tile, s_prefix;
   __shared__ uint32_t sw[BLOCK / 64];
   // full tiles move through LDS so that HBM sees lane-contiguous 16-byte
@@ -49,6 +49,13 @@ __global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* out, uint64_
   }
   __syncthreads();
   const uint32_t tile = s_tile;
+  // a device-side item count (<= n): tiles past it only draw their ticket
+  if (n_dev && *n_dev < n) {
+    n = *n_dev;
+    const uint32_t last = n ? static_cast<uint32_t>((n - 1) / DS_TILE) : 0u;
+    if (tile > last) return;
+    ntiles = last + 1;
+  }
   const uint64_t b = static_cast<uint64_t>(tile) * DS_TILE + static_cast<uint64_t>(threadIdx.x) * DS_ITEMS;
   uint32_t v[DS_ITEMS];
   const uint64_t tb = static_cast<uint64_t>(tile) * DS_TILE;
@@ -191,8 +198,10 @@ struct ArrGen {
   }
 };
 
+// n_dev (optional): the item count on the device, at most n (the grid covers n).
 template <class OP, bool INCL, class GEN>
-int dscan(GEN gen, uint32_t* out, uint64_t n, uint32_t* total, Arena& ws, hipStream_t st, uint32_t* err) {
+int dscan(GEN gen, uint32_t* out, uint64_t n, uint32_t* total, Arena& ws, hipStream_t st, uint32_t* err,
+          const uint32_t* n_dev = nullptr) {
   if (n == 0) {
     if (total) HIP_CHECK(hipMemsetAsync(total, 0, sizeof(uint32_t), st));
     return CRDTM_OK;
@@ -210,7 +219,7 @@ int dscan(GEN gen, uint32_t* out, uint64_t n, uint32_t* total, Arena& ws, hipStr
   auto* kfn = &k_dscan<OP, INCL, GEN>;
   prof_begin(st);
   hipLaunchKernelGGL(kfn, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, gen, out, n, status, ticket,
-                     static_cast<uint32_t>(tiles), ws.scan_epoch, total, err);
+                     static_cast<uint32_t>(tiles), ws.scan_epoch, total, err, n_dev);
   prof_mark("k_dscan", st);
   return CRDTM_OK;
 }

@@ -296,3 +296,37 @@ def test_flat_sibling_fans():
     assert res.code == 0 and res.path_taken == N.PATH_CLOSED_FORM
     assert engine_summary(et) == oracle_summary(ot)
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+
+
+@pytest.mark.parametrize("depth", [3, 62, 63, 64, 65, 150])
+def test_flat_run_tree_depth(depth):
+    """The flat order by ep-run decomposition walks the tree of runs (a run
+    hangs from the slot of its head's effective parent); chains of runs up
+    to RUN_MAXD deep take it, deeper ones the generic Euler-tour list
+    ranking. Replica k's first node anchors after replica k-1's first node
+    (one run deeper each), its second after the sentinel, plus a typing
+    stream around them; against the oracle."""
+    rows = []
+    for k in range(1, depth + 1):
+        a = ((k - 1) << 32) + 1 if k > 1 else 0
+        rows.append(((k << 32) + 1, a))
+        rows.append(((k << 32) + 2, 0))
+    rng = np.random.default_rng(depth)
+    last = {}
+    for j in range(3000):
+        r = depth + 1 + int(rng.integers(0, 8))
+        c = last.get(r, 0) + 1
+        anc = ((r << 32) + c - 1) if c > 1 and rng.random() < 0.9 else rows[int(rng.integers(0, len(rows)))][0]
+        rows.append(((r << 32) + c, anc))
+        last[r] = c
+    m = len(rows)
+    v = dict(kind=np.zeros(m, np.uint8), ts=np.array([a for a, _ in rows], np.int64),
+             path_off=np.arange(m + 1, dtype=np.uint32), path=np.array([b for _, b in rows] + [0], np.int64),
+             val=np.arange(m, dtype=np.uint32))
+    ot, rc, _ = oracle_apply_arrays(v, m)
+    assert rc == 0
+    et = CRDTree.init(0)
+    res = et.apply_arrays(v, m)
+    assert res.code == 0 and res.path_taken == N.PATH_CLOSED_FORM
+    assert engine_summary(et) == oracle_summary(ot)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
