@@ -274,9 +274,9 @@ int crdtm_tree_reset(crdtm_tree* t, int64_t replica_id) {
   if (!t) return CRDTM_E_ARG;
   // slot 0 / dict 0 / l_off[0] keep their init values: only the root
   // sentinel's `next` can change, and only to a slot we now drop.
-  const uint32_t none = NONE;
-  HIP_CHECK(hipMemcpyAsync(t->d.s_next, &none, 4, hipMemcpyHostToDevice, t->ctx->stream));
-  HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+  // (stream-ordered, no host wait: every later read of the state synchronises)
+  hipLaunchKernelGGL(k_reset_root, dim3(1), dim3(1), 0, t->ctx->stream, t->d.s_next);
+  HIP_CHECK(hipGetLastError());
   t->n_slots = 1;
   t->n_dicts = 1;
   t->log_n = 0;

@@ -44,6 +44,8 @@ enum : uint32_t {
 };
 
 // Small device-side result block (one copy back per phase).
+constexpr uint32_t REP_INLINE = 256;  // replica entries returned inside the result block
+
 struct DevResult {
   uint32_t err_index;       // atomicMin over erroring ops
   uint32_t guard;           // G_* bits
@@ -89,6 +91,7 @@ struct DevResult {
   uint32_t run_fail;        // flat order: the run tree is deeper than RUN_MAXD (generic list ranking instead)
   uint32_t run_maxd;        // flat order: deepest run
   uint32_t run_lhist[64];   // flat order: runs per depth
+  long long rep_inline[2 * REP_INLINE];  // replicas table entries collected by a commit (the first REP_INLINE)
 };
 
 #define HIP_CHECK(x)                                                                         \

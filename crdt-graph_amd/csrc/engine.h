@@ -181,6 +181,7 @@ struct PdrIn {
 
 // merge.hip
 int sync_read(crdtm_ctx* c);
+__global__ void k_reset_root(uint32_t* s_next);
 int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& ws);
 // pdr.hip
 int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdtm_result* res, bool* handled);

@@ -994,7 +994,7 @@ __global__ void __launch_bounds__(BLOCK) k_rep_max(OpsDev o, const uint8_t* st, 
 }
 
 __global__ void __launch_bounds__(BLOCK) k_rep_out(OpsDev o, const uint8_t* st, const uint32_t* rtab,
-                                                   long long* out, uint32_t* n_out) {
+                                                   long long* out, uint32_t* n_out, long long* inl) {
   GRID_STRIDE(i, o.n) {
     if (st[i] != ST_APPLIED) continue;
     const long long t = op_t(o, i);
@@ -1003,6 +1003,10 @@ __global__ void __launch_bounds__(BLOCK) k_rep_out(OpsDev o, const uint8_t* st, 
       const uint32_t k = atomicAdd(n_out, 1u);
       out[2 * k] = replica_of(t);
       out[2 * k + 1] = t;
+      if (k < REP_INLINE) {
+        inl[2 * k] = replica_of(t);
+        inl[2 * k + 1] = t;
+      }
     }
   }
 }
@@ -1014,9 +1018,10 @@ __global__ void __launch_bounds__(BLOCK) k_rep_reset(OpsDev o, const uint8_t* st
   }
 }
 
+// st == nullptr: every op applied (the flat speculation writes no statuses)
 __global__ void __launch_bounds__(BLOCK) k_status_out(const uint8_t* st, uint32_t n, uint32_t err, uint8_t* out) {
   GRID_STRIDE(i, n) {
-    uint8_t s = st[i];
+    uint8_t s = st ? st[i] : static_cast<uint8_t>(ST_APPLIED);
     if (i > err) s = CRDTM_ST_UNREACHED;
     else if (s == ST_INVALID || s == ST_NOTFOUND) s = CRDTM_ST_ERROR;
     out[i] = s;
@@ -1751,11 +1756,17 @@ constexpr unsigned long long REC_EMPTY = ~0ULL;
 // checks every slot's Add against its anchor and counts the slots: as many
 // slots as keyed Adds means no duplicate timestamps. Only a batch where some
 // op does not apply runs the per-op k_fl_status.
+// track_rep = 0: k_fl_check folds the replicas table from the records instead
+// (slot order: a thread's slots stay inside one replica's range, no per-op
+// LDS atomics).
 __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_t Q, unsigned long long* rec,
-                                                    long long ts0, uint32_t* rtab, DevResult* dres) {
+                                                    long long ts0, uint32_t* rtab, DevResult* dres,
+                                                    uint32_t track_rep) {
   __shared__ __attribute__((aligned(16))) uint32_t rv[REP_DIRECT];
-  for (uint32_t j = threadIdx.x; j < REP_DIRECT / 4; j += blockDim.x)
-    reinterpret_cast<uint4*>(rv)[j] = make_uint4(0u, 0u, 0u, 0u);
+  if (track_rep) {
+    for (uint32_t j = threadIdx.x; j < REP_DIRECT / 4; j += blockDim.x)
+      reinterpret_cast<uint4*>(rv)[j] = make_uint4(0u, 0u, 0u, 0u);
+  }
   __syncthreads();
   const long long id0 = replica_of(ts0);
   uint32_t keys = 0, own = 0, slow = 0, err = NONE, mr = 0;
@@ -1782,18 +1793,21 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
       const long long kk = o.path[qd.off[k]];
       const uint32_t qa = kk == 0 ? Q : tsindex_slot(x, kk);
       rec[q] = (static_cast<unsigned long long>(i) << 32) | qa;
-      const uint32_t rr = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32);
-      if (rr < REP_DIRECT) {
-        atomicMax(&rv[rr], i + 1);
-        mr = max(mr, rr);
-      } else {
-        atomicMax(&rtab[rr + (1u << (REPLICA_BITS - 1))], i + 1);
+      if (track_rep) {
+        const uint32_t rr = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32);
+        if (rr < REP_DIRECT) {
+          atomicMax(&rv[rr], i + 1);
+          mr = max(mr, rr);
+        } else {
+          atomicMax(&rtab[rr + (1u << (REPLICA_BITS - 1))], i + 1);
+        }
       }
     }
   }
   mr = block_max(mr);  // (synchronises the block) only ids <= mr were touched
-  for (uint32_t j = threadIdx.x; j <= mr; j += blockDim.x)
-    if (rv[j]) atomicMax(&rtab[j + (1u << (REPLICA_BITS - 1))], rv[j]);
+  if (track_rep)
+    for (uint32_t j = threadIdx.x; j <= mr; j += blockDim.x)
+      if (rv[j]) atomicMax(&rtab[j + (1u << (REPLICA_BITS - 1))], rv[j]);
   keys = block_sum(keys);
   own = block_sum(own);
   slow = block_sum(slow);
@@ -1890,6 +1904,16 @@ __global__ void __launch_bounds__(BLOCK) k_fl_status(OpsDev o, uint8_t* st, TsIn
   }
 }
 
+// Before a second commit: forget the speculative one's order and collection words.
+__global__ void k_fl_commit_reset(DevResult* d) {
+  d->run_fail = 0;
+  d->n_replica_out = 0;
+}
+
+// A fresh tree's root sentinel points nowhere (crdtm_tree_reset, and after an
+// unconfirmed speculative commit).
+__global__ void k_reset_root(uint32_t* s_next) { s_next[0] = NONE; }
+
 // Before the second status pass: forget the first pass's accounting.
 __global__ void k_fl_stat_reset(DevResult* d) {
   d->n_applied = 0;
@@ -1903,7 +1927,7 @@ __global__ void k_fl_stat_reset(DevResult* d) {
 // replicas[r] := ts of replica r's last applied Add (flat: Adds only, ids in
 // [0, max_replica]); clears the table entries it reads.
 __global__ void __launch_bounds__(BLOCK) k_fl_rep_collect(OpsDev o, uint32_t nr, uint32_t* rtab, long long* out,
-                                                          uint32_t* n_out) {
+                                                          uint32_t* n_out, long long* inl) {
   GRID_STRIDE(r, nr) {
     uint32_t* e = &rtab[r + (1u << (REPLICA_BITS - 1))];
     const uint32_t v = *e;
@@ -1913,6 +1937,10 @@ __global__ void __launch_bounds__(BLOCK) k_fl_rep_collect(OpsDev o, uint32_t nr,
     const uint32_t k = atomicAdd(n_out, 1u);
     out[2 * k] = r;
     out[2 * k + 1] = o.ts[v - 1];
+    if (k < REP_INLINE) {  // (the host reads these with the result block)
+      inl[2 * k] = r;
+      inl[2 * k + 1] = o.ts[v - 1];
+    }
   }
 }
 
@@ -1933,9 +1961,15 @@ struct RunHeadGen {
   __device__ __forceinline__ bool aligned(uint64_t) const { return false; }
   __device__ __forceinline__ uint4 load4(uint64_t) const { return make_uint4(0u, 0u, 0u, 0u); }
   const unsigned long long* rec;
+  uint32_t Q;
   uint32_t* anc;  // side output: anchor slot per slot (ABSENT = no node)
+  // A missing anchor (NONE) only occurs in a batch that fails (NotFound),
+  // which the flat speculation discards: it reads as the sentinel so that
+  // the speculative walks stay in bounds.
   __device__ __forceinline__ uint32_t anchor(unsigned long long r) const {
-    return r == REC_EMPTY ? ABSENT : static_cast<uint32_t>(r);
+    if (r == REC_EMPTY) return ABSENT;
+    const uint32_t a = static_cast<uint32_t>(r);
+    return a == NONE ? Q : a;
   }
   __device__ __forceinline__ void load(uint64_t b, uint64_t n, uint32_t* v) const {
     if (b + DS_ITEMS <= n) {
@@ -1974,11 +2008,28 @@ struct RunHeadGen {
 // the sentinel or a slot whose Add comes earlier in the batch, else it fails
 // (NotFound -> OperationFailed); the smallest failing index goes to
 // err_index. Counts the slots holding an Add (fl_part[0]).
-__global__ void __launch_bounds__(BLOCK) k_fl_check(uint32_t Q, const unsigned long long* rec, DevResult* dres) {
+// With nrep > 0 (replica ids < nrep, base table in LDS) it also folds the
+// replicas table: every workgroup checks one contiguous slot chunk, so a
+// thread's slots run through few replica ranges; it keeps the largest op
+// index of the current replica in a register and touches LDS only when the
+// range changes (replicas[r] = the last applied Add of r, src/CRDTree.elm:313).
+__global__ void __launch_bounds__(BLOCK) k_fl_check(uint32_t Q, const unsigned long long* rec, DevResult* dres,
+                                                    const uint32_t* base, uint32_t nrep, uint32_t* rtab) {
+  extern __shared__ uint32_t sck[];  // [nrep] range bases, [nrep] largest index + 1
+  uint32_t* sb = sck;
+  uint32_t* rv = sck + nrep;
+  for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x) {
+    sb[j] = base[j];
+    rv[j] = 0;
+  }
+  __syncthreads();
   uint32_t present = 0, err = NONE;
-  const uint32_t npair = Q / 2;
-  GRID_STRIDE(k, npair + (Q & 1)) {
-    const bool pair = k < npair;
+  const uint32_t npair = (Q + 1) / 2;
+  const uint32_t chunk = (npair + gridDim.x - 1) / gridDim.x;
+  const uint32_t k0 = blockIdx.x * chunk, k1 = min(npair, k0 + chunk);
+  uint32_t cr = NONE, cmax = 0, rlo = 0, rhi = 0;  // current replica, its [lo, hi) slot range
+  for (uint32_t k = k0 + threadIdx.x; k < k1; k += blockDim.x) {
+    const bool pair = 2 * k + 1 < Q;
     const ulonglong2 x = pair ? *reinterpret_cast<const ulonglong2*>(rec + 2 * k) : make_ulonglong2(rec[Q - 1], REC_EMPTY);
     const unsigned long long r2[2] = {x.x, x.y};
 #pragma unroll
@@ -1988,10 +2039,30 @@ __global__ void __launch_bounds__(BLOCK) k_fl_check(uint32_t Q, const unsigned l
       ++present;
       const uint32_t fi = static_cast<uint32_t>(r >> 32), qa = static_cast<uint32_t>(r);
       if (qa != Q && (qa == NONE || static_cast<uint32_t>(rec[qa] >> 32) >= fi)) err = min(err, fi);
+      if (nrep) {
+        const uint32_t q = 2 * k + j;
+        if (q < rlo || q >= rhi) {
+          if (cmax) atomicMax(&rv[cr], cmax);
+          uint32_t lo = 0, hi = nrep;  // largest replica whose range starts at or below q
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (sb[mid] <= q) lo = mid;
+            else hi = mid;
+          }
+          cr = lo;
+          rlo = sb[lo];
+          rhi = lo + 1 < nrep ? sb[lo + 1] : NONE;
+          cmax = 0;
+        }
+        cmax = max(cmax, fi + 1);
+      }
     }
   }
-  present = block_sum(present);
+  if (cmax) atomicMax(&rv[cr], cmax);
+  present = block_sum(present);  // (synchronises the block)
   err = block_min(err);
+  for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x)
+    if (rv[j]) atomicMax(&rtab[j + (1u << (REPLICA_BITS - 1))], rv[j]);
   if (threadIdx.x == 0) {
     if (present) atomicAdd(&dres->fl_part[32 * (blockIdx.x & 15)], present);
     if (err != NONE) atomicMin(&dres->err_index, err);
@@ -2090,9 +2161,13 @@ struct FlatDocSink {
 // children dict implicit (engine.h TreeDev). Within the root dict the raw
 // `next` chain is the document order (no tombstones): k_fl_next links
 // doc[r] -> doc[r + 1] and the root sentinel (slot 0) -> doc[0].
-__global__ void __launch_bounds__(BLOCK) k_fl_next(uint32_t K, const uint32_t* doc, TreeDev T) {
+// (The flat speculation may run this over more ranks than slots when its
+// guess fails: entries past the document are then stale, and `cap` keeps
+// the stores inside the slot arrays; the result is discarded.)
+__global__ void __launch_bounds__(BLOCK) k_fl_next(uint32_t K, const uint32_t* doc, TreeDev T, uint64_t cap) {
   GRID_STRIDE(r, K) {
-    T.s_next[doc[r]] = r + 1 < K ? doc[r + 1] : NONE;
+    const uint32_t d = doc[r];
+    if (d < cap) T.s_next[d] = r + 1 < K ? doc[r + 1] : NONE;
     if (r == 0) T.s_next[0] = doc[0];
   }
 }
@@ -2186,16 +2261,29 @@ __global__ void __launch_bounds__(BLOCK) k_fl_ep_runs(uint32_t Q, uint32_t* anc,
       hflag[x] = 0;
       continue;
     }
-    if (d != Q && d > x) {
-      while (d != Q && d > x) {
+    if (d < Q && d > x) {
+      // (a valid batch's anchors form a forest of present slots; a failing
+      // batch run by the flat speculation may anchor at a slot without a node
+      // or hold a cycle: those walks end at the sentinel, which keeps every
+      // walk finite and in bounds, and the speculation is discarded)
+      for (uint32_t steps = 0; d < Q && d > x; ++steps) {
         const uint32_t h = rh[d];
         if (h < x) {
           d = x - 1;
           break;
         }
+        if (steps > Q) {
+          d = Q;
+          break;
+        }
         d = __hip_atomic_load(&anc[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      if (d >= Q || (d != x - 1 && __hip_atomic_load(&anc[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ABSENT))
+        d = Q;
       __hip_atomic_store(&anc[x], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (d != Q && (d >= x || anc[d] == ABSENT)) {  // (self-anchored / nodeless anchor: a failing batch)
+      d = Q;
+      anc[x] = d;
     }
     hflag[x] = (x == 0 || d != x - 1) ? 1u : 0u;
   }
@@ -2249,11 +2337,11 @@ __global__ void __launch_bounds__(BLOCK) k_run_par(RunArr a, uint32_t Q, uint32_
 // children per parent run: the last sibling of every attach slot's group adds
 // the group's size (one atomic per group, not per child)
 __global__ void __launch_bounds__(BLOCK) k_run_nch(RunArr a, uint32_t Q, const uint32_t* pk, const uint32_t* sarr,
-                                                   const uint32_t* sgs) {
+                                                   const uint32_t* gstart) {
   const uint32_t R = *a.nR;
   RUN_LOOP(k) {
     const uint32_t p = pk[k];
-    if (p != Q && (k + 1 == R || pk[k + 1] != p)) atomicAdd(&a.nch[a.par[sarr[k]]], k - sgs[k] + 1);
+    if (p != Q && (k + 1 == R || pk[k + 1] != p)) atomicAdd(&a.nch[a.par[sarr[k]]], k - gstart[p] + 1);
   }
 }
 
@@ -2283,29 +2371,22 @@ __global__ void __launch_bounds__(BLOCK) k_run_gather(RunArr a, const uint32_t* 
   RUN_LOOP(k) tk[k] = a.T[sarr[k]];
 }
 
-// inclusive max-scan input: k where a new attach slot starts
-struct SubgroupGen {
-  static constexpr bool kStriped = false;
-  const uint32_t* pk;
-  __device__ __forceinline__ bool aligned(uint64_t) const { return false; }
-  __device__ __forceinline__ uint4 load4(uint64_t) const { return make_uint4(0u, 0u, 0u, 0u); }
-  __device__ __forceinline__ void load(uint64_t b, uint64_t n, uint32_t* v) const {
-#pragma unroll
-    for (int j = 0; j < DS_ITEMS; ++j) {
-      const uint64_t k = b + j;
-      v[j] = (k < n && (k == 0 || pk[k] != pk[k - 1])) ? static_cast<uint32_t>(k) : 0u;
-    }
+// gstart[p] = the first position of slot p's sibling group in the sorted list
+__global__ void __launch_bounds__(BLOCK) k_run_gstart(RunArr a, const uint32_t* pk, uint32_t* gstart) {
+  RUN_LOOP(k) {
+    const uint32_t p = pk[k];
+    if (k == 0 || pk[k - 1] != p) gstart[p] = k;
   }
-};
+}
 
 // side(p) = the subtree sizes of the runs hanging from slot p: the last
 // sibling of each slot's group stores the group's sum (no atomics)
 __global__ void __launch_bounds__(BLOCK) k_run_side(RunArr a, uint32_t Q, const uint32_t* pk, const uint32_t* tk,
-                                                    const uint32_t* xs, const uint32_t* sgs, uint32_t* side) {
+                                                    const uint32_t* xs, const uint32_t* gstart, uint32_t* side) {
   const uint32_t R = *a.nR;
   RUN_LOOP(k) {
     const uint32_t p = pk[k];
-    if (p != Q && (k + 1 == R || pk[k + 1] != p)) side[p] = xs[k] + tk[k] - xs[sgs[k]];
+    if (p != Q && (k + 1 == R || pk[k + 1] != p)) side[p] = xs[k] + tk[k] - xs[gstart[p]];
   }
 }
 
@@ -2338,10 +2419,10 @@ struct SideGen {
 // w(r): the head's rank minus its parent run head's rank (root children:
 // the rank itself)
 __global__ void __launch_bounds__(BLOCK) k_run_w(RunArr a, uint32_t Q, const uint32_t* sarr, const uint32_t* pk,
-                                                 const uint32_t* xs, const uint32_t* sgs, const uint32_t* G) {
+                                                 const uint32_t* xs, const uint32_t* gstart, const uint32_t* G) {
   RUN_LOOP(k) {
     const uint32_t r = sarr[k], p = pk[k];
-    const uint32_t off = xs[k] - xs[sgs[k]];  // siblings hanging from p with a larger slot
+    const uint32_t off = xs[k] - xs[gstart[p]];  // siblings hanging from p with a larger slot
     a.w[r] = p == Q ? off : G[p] - G[a.heads[a.par[r]]] + 1u + off;
   }
 }
@@ -2480,6 +2561,23 @@ int sync_read(crdtm_ctx* c) {
   return CRDTM_OK;
 }
 
+// Replicas table entries collected by the commit (inline in the result
+// block when they fit, else one copy).
+static int take_replicas(crdtm_tree* t, const long long* rep_dev) {
+  const DevResult& h = *t->ctx->hres;
+  const uint32_t nrep = h.n_replica_out;
+  if (!nrep) return CRDTM_OK;
+  const long long* hv = h.rep_inline;
+  std::vector<long long> big;
+  if (nrep > REP_INLINE) {
+    big.resize(2 * static_cast<size_t>(nrep));
+    HIP_CHECK(hipMemcpy(big.data(), rep_dev, big.size() * sizeof(long long), hipMemcpyDeviceToHost));
+    hv = big.data();
+  }
+  for (uint32_t k = 0; k < nrep; ++k) t->replicas[hv[2 * k]] = hv[2 * k + 1];
+  return CRDTM_OK;
+}
+
 __global__ void __launch_bounds__(BLOCK) k_post_flags(OpsDev o, const uint8_t* st, uint32_t* appl, uint32_t* plen) {
   GRID_STRIDE(i, o.n) {
     const bool a = st[i] == ST_APPLIED;
@@ -2507,15 +2605,10 @@ int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& ws) {
                      static_cast<uint32_t>(t->log_npath), &dr->log_npath);
   HIP_CHECK(hipMemsetAsync(&dr->n_replica_out, 0, sizeof(uint32_t), s));
   LAUNCH(k_rep_max, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, s, o, st, c->rtab);
-  LAUNCH(k_rep_out, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab, rep, &dr->n_replica_out);
+  LAUNCH(k_rep_out, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab, rep, &dr->n_replica_out, dr->rep_inline);
   LAUNCH(k_rep_reset, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab);
   if ((r = sync_read(c))) return r;
-  const uint32_t nrep = c->hres->n_replica_out;
-  if (nrep) {
-    std::vector<long long> h(2 * static_cast<size_t>(nrep));
-    HIP_CHECK(hipMemcpy(h.data(), rep, h.size() * sizeof(long long), hipMemcpyDeviceToHost));
-    for (uint32_t k = 0; k < nrep; ++k) t->replicas[h[2 * k]] = h[2 * k + 1];
-  }
+  if ((r = take_replicas(t, rep))) return r;
   t->last_begin = t->log_n;
   t->log_n += c->hres->log_n;
   t->log_npath += c->hres->log_npath;
@@ -2615,97 +2708,42 @@ struct RangeReset {
   ~RangeReset() { LAUNCH(k_range_reset, dim3(64), dim3(BLOCK), 0, c->stream, c->crange, c->dres); }
 };
 
-// Flat closed form (see the k_fl_* kernels): the index `ix` is dense and
-// already built; Q = its slot range.
-static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_t Q, uint32_t maxr, uint8_t* st,
-                      uint8_t* st_out, crdtm_result* res) {
+// Flat closed form: launches K2/K4 (the order), the commit and the replica
+// collection for K nodes; nothing synchronises. The flat order's run tree
+// may be too deep (DevResult::run_fail, read with the final result): then
+// flat_order_fallback recomputes `doc` and the chain.
+struct FlatBufs {
+  unsigned long long* rec;
+  uint32_t* anc;
+  uint32_t* cnt;
+  uint32_t* fill;
+  uint32_t* qc;
+  long long* rep;
+};
+
+static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_t Q, uint32_t maxr,
+                             const uint8_t* st, uint32_t K, bool all_applied, FlatBufs& fb) {
   crdtm_ctx* c = t->ctx;
   hipStream_t s = c->stream;
   Arena& ws = c->ws;
   DevResult* dr = c->dres;
   const uint32_t n = o.n;
   const uint32_t g = grid_for(n);
-  const uint32_t U = Q + 1;  // nodes + the root sentinel
-  unsigned long long* rec = ws.alloc<unsigned long long>(Q + 1);
-  uint32_t* anc = ws.alloc<uint32_t>(U);
-  uint32_t* cnt = ws.alloc<uint32_t>(U + 1);
-  uint32_t* fill = ws.alloc<uint32_t>(U + 1);
-  LAUNCH(k_fl_init, dim3(grid_for(Q, BLOCK, 4096)), dim3(BLOCK), 0, s, Q, rec);
-  LAUNCH(k_fl_claim, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix, Q, rec, t->timestamp, c->rtab, dr);
-  LAUNCH(k_fl_check, dim3(grid_for(Q / 2 + 1, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, rec, dr);
+  unsigned long long* rec = fb.rec;
+  uint32_t* anc = fb.anc;
   int r;
-  if ((r = sync_read(c))) return r;
-  {
-    const DevResult& h0 = *c->hres;
-    uint32_t present = 0;
-    for (int k = 0; k < 16; ++k) present += h0.fl_part[32 * k];
-    const bool every = h0.err_index == NONE && h0.fl_slow == 0 && present == h0.fl_keys && h0.fl_keys == n;
-    if (every) {  // every op is the only Add of its timestamp and applies
-      c->hres->n_applied = n;
-      c->hres->n_adds_applied = n;
-      c->hres->n_already = 0;
-    } else {  // per-op statuses: duplicates, ts 0, errors
-      LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr, nullptr);
-      LAUNCH(k_fl_stat_reset, dim3(1), dim3(1), 0, s, dr);
-      LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, rec, t->timestamp, c->rtab, dr);
-      if ((r = sync_read(c))) return r;
-      if (c->hres->dup_fix) {  // a smaller duplicate took its slot: the records are final now, decide again
-        LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr,
-               nullptr);
-        LAUNCH(k_fl_stat_reset, dim3(1), dim3(1), 0, s, dr);
-        LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, rec, t->timestamp, c->rtab, dr);
-        if ((r = sync_read(c))) return r;
-      }
-    }
-  }
-  const DevResult h1 = *c->hres;
-  uint32_t guard = 0;
-  const long long new_ts = t->timestamp + h1.own_ok_adds;
-  if (replica_of(new_ts) != replica_of(t->timestamp)) guard |= G_REPLICA_DRIFT;
-  res->guard = guard;
-  if (guard || h1.err_index != NONE)  // no commit: leave the replica table clean
-    LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr, nullptr);
-  if (guard) {
-    r = run_replay(t, o, st, res, guard);
-    if (r == CRDTM_OK && st_out)
-      LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, st, n,
-             res->err_index >= 0 ? static_cast<uint32_t>(res->err_index) : NONE, st_out);
-    return r;
-  }
-  res->path_taken = CRDTM_PATH_CLOSED_FORM;
-  if (h1.err_index != NONE) {
-    uint8_t est = 0;
-    HIP_CHECK(hipMemcpy(&est, st + h1.err_index, 1, hipMemcpyDeviceToHost));
-    res->code = est == ST_INVALID ? CRDTM_INVALID_PATH : CRDTM_OPERATION_FAILED;
-    res->err_index = h1.err_index;
-    if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, st, n, h1.err_index, st_out);
-    return CRDTM_OK;
-  }
-  res->n_applied = h1.n_applied;
-  res->n_already = h1.n_already;
-  const uint32_t K = h1.n_adds_applied;
-  const bool all_applied = h1.n_applied == n;
-  TreeCaps need = t->cap;
-  need.slots = std::max<uint64_t>(need.slots, 1ULL + K + 1);
-  need.dicts = std::max<uint64_t>(need.dicts, 2);
-  need.log = std::max<uint64_t>(need.log, t->log_n + h1.n_applied + 1);
-  need.lpath = std::max<uint64_t>(need.lpath, t->log_npath + o.n_path + 1);
-  need.doc = std::max<uint64_t>(need.doc, 1ULL + K);
-  if (need.slots > t->cap.slots || need.dicts > t->cap.dicts || need.log > t->cap.log ||
-      need.lpath > t->cap.lpath || need.doc > t->cap.doc) {
-    if ((r = grow_tree(t, need))) return r;
-  }
+  fb.qc = nullptr;
   if (K > 0) {
     // ---- K2a: effective parents (run-skipping walk over the anchor runs) ----
     const uint32_t gq = grid_for(Q);
     uint32_t* rh = ws.alloc<uint32_t>(Q);
-    if ((r = dscan<MaxOp, true>(RunHeadGen{rec, anc}, rh, Q, nullptr, ws, s, nullptr))) return r;
+    if ((r = dscan<MaxOp, true>(RunHeadGen{rec, Q, anc}, rh, Q, nullptr, ws, s, nullptr))) return r;
     uint32_t* rid = ws.alloc<uint32_t>(Q);  // ep-run head flags, then inclusive head counts
     LAUNCH(k_fl_ep_runs, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, rh, rid);
     if ((r = dscan<SumOp, true>(ArrGen{rid}, rid, Q, &dr->run_count, ws, s, nullptr))) return r;
     uint32_t* qc = nullptr;
     if (Q != K) {  // slots with no node: compact
-      qc = ws.alloc<uint32_t>(Q);
+      qc = fb.qc = ws.alloc<uint32_t>(Q);
       LAUNCH(k_fl_present, dim3(gq), dim3(BLOCK), 0, s, Q, anc, qc);
       if ((r = scan_excl_u32(qc, qc, Q, nullptr, ws, s))) return r;
     }
@@ -2724,7 +2762,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     uint32_t* sk[2] = {ws.alloc<uint32_t>(K + 1), ws.alloc<uint32_t>(K + 1)};
     uint32_t* sv[2] = {ws.alloc<uint32_t>(K + 1), ws.alloc<uint32_t>(K + 1)};
     uint32_t* xs = ws.alloc<uint32_t>(K + 1);
-    uint32_t* sgs = ws.alloc<uint32_t>(K + 1);
+    uint32_t* gstart = fb.cnt;  // [Q + 1] (the generic order's child counts; unused here)
     const uint32_t gr = grid_for(K, BLOCK, 2048);
     LAUNCH(k_run_heads, dim3(gq), dim3(BLOCK), 0, s, Q, anc, rid, ra.heads, side);
     LAUNCH(k_run_par, dim3(gr), dim3(BLOCK), 0, s, ra, Q, K, anc, rid, qc, sk[0], sv[0]);
@@ -2733,18 +2771,18 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     uint32_t *pk = nullptr, *sarr = nullptr;  // attach slot, run: siblings grouped by slot, slots ascending
     if ((r = radix_sort_pairs(sk[0], sv[0], sk[1], sv[1], ra.nR, K, sbits, ws, s, &pk, &sarr))) return r;
     uint32_t* tk = pk == sk[0] ? sk[1] : sk[0];  // (free after the sort)
-    if ((r = dscan<MaxOp, true>(SubgroupGen{pk}, sgs, K, nullptr, ws, s, nullptr, ra.nR))) return r;
-    LAUNCH(k_run_nch, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, sarr, sgs);
+    LAUNCH(k_run_gstart, dim3(gr), dim3(BLOCK), 0, s, ra, pk, gstart);
+    LAUNCH(k_run_nch, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, sarr, gstart);
     // ---- subtree sizes (one launch), slot ranks inside runs, head ranks ----
     LAUNCH(k_run_tree_up, dim3(gr), dim3(BLOCK), 0, s, ra);
     LAUNCH(k_run_gather, dim3(gr), dim3(BLOCK), 0, s, ra, sarr, tk);
     if ((r = dscan<SumOp, false>(ArrGen{tk}, xs, K, nullptr, ws, s, nullptr, ra.nR))) return r;
-    LAUNCH(k_run_side, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, tk, xs, sgs, side);
+    LAUNCH(k_run_side, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, tk, xs, gstart, side);
     if ((r = dscan<SumOp, false>(SideGen{anc, side}, side, Q, nullptr, ws, s, nullptr))) return r;
-    LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, sgs, side);
+    LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, gstart, side);
     LAUNCH(k_run_pos, dim3(gr), dim3(BLOCK), 0, s, ra, dr);
     LAUNCH(k_run_expand, dim3(gq), dim3(BLOCK), 0, s, ra, Q, anc, rid, side, qc, t->d.doc);
-    LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d);
+    LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d, t->cap.slots);
     uint32_t* logidx = nullptr;
     if (!all_applied) {  // compacted log (its scans share the ctx scan pool: main stream)
       logidx = ws.alloc<uint32_t>(n + 1);
@@ -2760,56 +2798,177 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
            maxr + 1 <= HOST_RANGES ? 2 * (maxr + 1) * sizeof(uint32_t) : 0, s, o, ix, Q, maxr + 1, anc, rec, qc,
            logidx, t->d);
     if (all_applied) LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
-    if ((r = sync_read(c))) return r;
-    if (c->hres->run_fail) {
-      // ---- a run tree deeper than RUN_MAXD: children of every node, Euler tour + list ranking ----
-      uint32_t* carr = ws.alloc<uint32_t>(U);
-      uint32_t* ns = ws.alloc<uint32_t>(U);
-      HIP_CHECK(hipMemsetAsync(cnt, 0, (U + 1) * sizeof(uint32_t), s));
-      HIP_CHECK(hipMemsetAsync(fill, 0, (U + 1) * sizeof(uint32_t), s));
-      LAUNCH(k_fl_count, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, cnt);
-      uint32_t* n_child = &dr->n_sentinels;  // scratch word for the scan total
-      if ((r = scan_excl_u32(cnt, cnt, U + 1, n_child, ws, s))) return r;
-      LAUNCH(k_fl_scatter, dim3(gq), dim3(BLOCK), 0, s, Q, anc, cnt, fill, carr);
-      {
-        const uint32_t gb = grid_for(Q, BLOCK, 2048);
-        uint32_t* bc = ws.alloc<uint32_t>(gb + 1);
-        LAUNCH(k_fl_root_count, dim3(gb), dim3(BLOCK), 0, s, Q, anc, bc);
-        if ((r = scan_excl_u32(bc, bc, gb, nullptr, ws, s))) return r;
-        LAUNCH(k_fl_root_place, dim3(gb), dim3(BLOCK), 0, s, Q, anc, bc, cnt, carr);
-      }
-      if ((r = segmented_sort_desc_id(cnt, U, carr, U, ws, s, dr, Q))) return r;
-      LAUNCH(k_fl_links, dim3(gq), dim3(BLOCK), 0, s, anc, cnt, n_child, carr, ns);
-      if ((r = list_rank_fused(FlatEulerSrc{Q, anc, cnt, carr, ns}, 2ULL * U, 2 * Q, FlatDocSink{Q, t->d.doc, qc},
-                               ws, s)))
-        return r;
-      LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d);
-    }
   } else if (all_applied) {
     LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
   }
-  long long* rep = ws.alloc<long long>(2 * static_cast<uint64_t>(maxr) + 2);
-  LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, rep,
-         &dr->n_replica_out);
+  fb.rep = ws.alloc<long long>(2 * static_cast<uint64_t>(maxr) + 2);
+  LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, fb.rep,
+         &dr->n_replica_out, dr->rep_inline);
+  return CRDTM_OK;
+}
+
+// The generic order for a run tree deeper than RUN_MAXD: children of every
+// node, Euler tour + list ranking, then the chain.
+static int flat_order_fallback(crdtm_tree* t, uint32_t Q, uint32_t K, FlatBufs& fb) {
+  crdtm_ctx* c = t->ctx;
+  hipStream_t s = c->stream;
+  Arena& ws = c->ws;
+  DevResult* dr = c->dres;
+  const uint32_t U = Q + 1;
+  const uint32_t gq = grid_for(Q);
+  uint32_t* anc = fb.anc;
+  uint32_t* cnt = fb.cnt;
+  uint32_t* fill = fb.fill;
+  uint32_t* qc = fb.qc;
+  int r;
+  // ---- a run tree deeper than RUN_MAXD: children of every node, Euler tour + list ranking ----
+  uint32_t* carr = ws.alloc<uint32_t>(U);
+  uint32_t* ns = ws.alloc<uint32_t>(U);
+  HIP_CHECK(hipMemsetAsync(cnt, 0, (U + 1) * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(fill, 0, (U + 1) * sizeof(uint32_t), s));
+  LAUNCH(k_fl_count, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, cnt);
+  uint32_t* n_child = &dr->n_sentinels;  // scratch word for the scan total
+  if ((r = scan_excl_u32(cnt, cnt, U + 1, n_child, ws, s))) return r;
+  LAUNCH(k_fl_scatter, dim3(gq), dim3(BLOCK), 0, s, Q, anc, cnt, fill, carr);
+  {
+    const uint32_t gb = grid_for(Q, BLOCK, 2048);
+    uint32_t* bc = ws.alloc<uint32_t>(gb + 1);
+    LAUNCH(k_fl_root_count, dim3(gb), dim3(BLOCK), 0, s, Q, anc, bc);
+    if ((r = scan_excl_u32(bc, bc, gb, nullptr, ws, s))) return r;
+    LAUNCH(k_fl_root_place, dim3(gb), dim3(BLOCK), 0, s, Q, anc, bc, cnt, carr);
+  }
+  if ((r = segmented_sort_desc_id(cnt, U, carr, U, ws, s, dr, Q))) return r;
+  LAUNCH(k_fl_links, dim3(gq), dim3(BLOCK), 0, s, anc, cnt, n_child, carr, ns);
+  if ((r = list_rank_fused(FlatEulerSrc{Q, anc, cnt, carr, ns}, 2ULL * U, 2 * Q, FlatDocSink{Q, t->d.doc, qc},
+                           ws, s)))
+    return r;
+  LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d, t->cap.slots);
+  return CRDTM_OK;
+}
+
+// Flat closed form (see the k_fl_* kernels): the index `ix` is dense and
+// already built; Q = its slot range. The common case — every op is the only
+// Add of its timestamp and applies — is speculated: its order and commit are
+// queued right behind the claim, and the claim's own counters, read with the
+// final result, confirm it (one host round trip for the whole merge). A
+// batch where some op does not apply is then decided op by op and committed
+// again (the tree is fresh: its root sentinel is restored in between).
+static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_t Q, uint32_t maxr, uint8_t* st,
+                      uint8_t* st_out, crdtm_result* res) {
+  crdtm_ctx* c = t->ctx;
+  hipStream_t s = c->stream;
+  Arena& ws = c->ws;
+  DevResult* dr = c->dres;
+  const uint32_t n = o.n;
+  const uint32_t g = grid_for(n);
+  const uint32_t U = Q + 1;  // nodes + the root sentinel
+  FlatBufs fb{};
+  fb.rec = ws.alloc<unsigned long long>(Q + 1);
+  fb.anc = ws.alloc<uint32_t>(U);
+  fb.cnt = ws.alloc<uint32_t>(U + 1);
+  fb.fill = ws.alloc<uint32_t>(U + 1);
+  LAUNCH(k_fl_init, dim3(grid_for(Q, BLOCK, 4096)), dim3(BLOCK), 0, s, Q, fb.rec);
+  // replicas table: folded by the check over slot order when the range table fits in LDS
+  const uint32_t nrep = maxr + 1 <= HOST_RANGES ? maxr + 1 : 0u;
+  LAUNCH(k_fl_claim, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix, Q, fb.rec, t->timestamp, c->rtab, dr,
+         nrep ? 0u : 1u);
+  LAUNCH(k_fl_check, dim3(grid_for(Q / 2 + 1, BLOCK, 2048)), dim3(BLOCK), 2 * nrep * sizeof(uint32_t), s, Q,
+         fb.rec, dr, ix.base, nrep, c->rtab);
+  int r;
+  auto grow_for = [&](uint32_t K, uint32_t applied) -> int {
+    TreeCaps need = t->cap;
+    need.slots = std::max<uint64_t>(need.slots, 1ULL + K + 1);
+    need.dicts = std::max<uint64_t>(need.dicts, 2);
+    need.log = std::max<uint64_t>(need.log, t->log_n + applied + 1);
+    need.lpath = std::max<uint64_t>(need.lpath, t->log_npath + o.n_path + 1);
+    need.doc = std::max<uint64_t>(need.doc, 1ULL + K);
+    if (need.slots > t->cap.slots || need.dicts > t->cap.dicts || need.log > t->cap.log ||
+        need.lpath > t->cap.lpath || need.doc > t->cap.doc)
+      return grow_tree(t, need);
+    return CRDTM_OK;
+  };
+  auto finish = [&](uint32_t K, uint32_t applied, uint32_t already, uint64_t npath, long long new_ts) -> int {
+    int rr = take_replicas(t, fb.rep);
+    if (rr) return rr;
+    res->path_taken = CRDTM_PATH_CLOSED_FORM;
+    res->n_applied = applied;
+    res->n_already = already;
+    t->n_slots = 1ULL + K;
+    t->n_dicts = 1;
+    t->last_begin = t->log_n;
+    t->log_n += applied;
+    t->log_npath += npath;
+    t->last_end = t->log_n;
+    t->timestamp = new_ts;
+    t->doc_n = K;
+    t->doc_valid = true;
+    return CRDTM_OK;
+  };
+  // ---- speculation: every op applies ----
+  if (Q >= n) {
+    if ((r = grow_for(n, n))) return r;
+    if ((r = flat_order_commit(t, o, ix, Q, maxr, st, n, true, fb))) return r;
+    if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, nullptr, n, NONE, st_out);
+    if ((r = sync_read(c))) return r;
+    const DevResult& h = *c->hres;
+    uint32_t present = 0;
+    for (int k = 0; k < 16; ++k) present += h.fl_part[32 * k];
+    const long long new_ts = t->timestamp + h.own_ok_adds;
+    const bool every = h.err_index == NONE && h.fl_slow == 0 && present == h.fl_keys && h.fl_keys == n;
+    if (every && replica_of(new_ts) == replica_of(t->timestamp)) {
+      if (h.run_fail && (r = flat_order_fallback(t, Q, n, fb))) return r;
+      res->guard = 0;
+      return finish(n, n, 0, o.n_path, new_ts);
+    }
+    // not confirmed: the fresh tree's only reachable change is its root sentinel's `next`
+    LAUNCH(k_reset_root, dim3(1), dim3(1), 0, s, t->d.s_next);
+  }
+  // ---- per-op statuses: duplicates, ts 0, errors ----
+  LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr, nullptr,
+         nullptr);
+  LAUNCH(k_fl_stat_reset, dim3(1), dim3(1), 0, s, dr);
+  LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, fb.rec, t->timestamp, c->rtab, dr);
+  if ((r = sync_read(c))) return r;
+  if (c->hres->dup_fix) {  // a smaller duplicate took its slot: the records are final now, decide again
+    LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr, nullptr,
+           nullptr);
+    LAUNCH(k_fl_stat_reset, dim3(1), dim3(1), 0, s, dr);
+    LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, fb.rec, t->timestamp, c->rtab, dr);
+    if ((r = sync_read(c))) return r;
+  }
+  const DevResult h1 = *c->hres;
+  uint32_t guard = 0;
+  const long long new_ts = t->timestamp + h1.own_ok_adds;
+  if (replica_of(new_ts) != replica_of(t->timestamp)) guard |= G_REPLICA_DRIFT;
+  res->guard = guard;
+  if (guard || h1.err_index != NONE)  // no commit: leave the replica table clean
+    LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr, nullptr,
+           nullptr);
+  if (guard) {
+    r = run_replay(t, o, st, res, guard);
+    if (r == CRDTM_OK && st_out)
+      LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, st, n,
+             res->err_index >= 0 ? static_cast<uint32_t>(res->err_index) : NONE, st_out);
+    return r;
+  }
+  res->path_taken = CRDTM_PATH_CLOSED_FORM;
+  if (h1.err_index != NONE) {
+    uint8_t est = 0;
+    HIP_CHECK(hipMemcpy(&est, st + h1.err_index, 1, hipMemcpyDeviceToHost));
+    res->code = est == ST_INVALID ? CRDTM_INVALID_PATH : CRDTM_OPERATION_FAILED;
+    res->err_index = h1.err_index;
+    if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, st, n, h1.err_index, st_out);
+    return CRDTM_OK;
+  }
+  const uint32_t K = h1.n_adds_applied;
+  const bool all_applied = h1.n_applied == n;
+  if ((r = grow_for(K, h1.n_applied))) return r;
+  LAUNCH(k_fl_commit_reset, dim3(1), dim3(1), 0, s, dr);
+  if ((r = flat_order_commit(t, o, ix, Q, maxr, st, K, all_applied, fb))) return r;
   if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, st, n, NONE, st_out);
   if ((r = sync_read(c))) return r;
-  const DevResult& h2 = *c->hres;
-  const uint32_t nrep = h2.n_replica_out;
-  if (nrep) {
-    std::vector<long long> hv(2 * static_cast<size_t>(nrep));
-    HIP_CHECK(hipMemcpy(hv.data(), rep, hv.size() * sizeof(long long), hipMemcpyDeviceToHost));
-    for (uint32_t k = 0; k < nrep; ++k) t->replicas[hv[2 * k]] = hv[2 * k + 1];
-  }
-  t->n_slots = 1ULL + K;
-  t->n_dicts = 1;
-  t->last_begin = t->log_n;
-  t->log_n += h1.n_applied;
-  t->log_npath += all_applied ? o.n_path : h2.log_npath;
-  t->last_end = t->log_n;
-  t->timestamp = new_ts;
-  t->doc_n = K;
-  t->doc_valid = true;
-  return CRDTM_OK;
+  if (c->hres->run_fail && (r = flat_order_fallback(t, Q, K, fb))) return r;
+  return finish(K, h1.n_applied, h1.n_already, all_applied ? o.n_path : c->hres->log_npath, new_ts);
 }
 
 int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res) {
@@ -3059,17 +3218,12 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   LAUNCH(k_log_tail, dim3(1), dim3(1), 0, s, t->d, static_cast<uint32_t>(t->log_n), &dr->log_n,
                      static_cast<uint32_t>(t->log_npath), &dr->log_npath);
   LAUNCH(k_rep_max, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, s, o, w.st, c->rtab);
-  LAUNCH(k_rep_out, dim3(g), dim3(BLOCK), 0, s, o, w.st, c->rtab, rep, &dr->n_replica_out);
+  LAUNCH(k_rep_out, dim3(g), dim3(BLOCK), 0, s, o, w.st, c->rtab, rep, &dr->n_replica_out, dr->rep_inline);
   LAUNCH(k_rep_reset, dim3(g), dim3(BLOCK), 0, s, o, w.st, c->rtab);
   if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n, NONE, st_out);
   if ((r = sync_read(c))) return r;
   const DevResult& h2 = *c->hres;
-  const uint32_t nrep = h2.n_replica_out;
-  if (nrep) {
-    std::vector<long long> hv(2 * static_cast<size_t>(nrep));
-    HIP_CHECK(hipMemcpy(hv.data(), rep, hv.size() * sizeof(long long), hipMemcpyDeviceToHost));
-    for (uint32_t k = 0; k < nrep; ++k) t->replicas[hv[2 * k]] = hv[2 * k + 1];
-  }
+  if ((r = take_replicas(t, rep))) return r;
   t->n_slots = 1 + static_cast<uint64_t>(h2.n_nodes_kept) + h2.n_live_kept;
   t->n_dicts = 1 + static_cast<uint64_t>(h2.n_live_kept);
   t->last_begin = t->log_n;

@@ -238,7 +238,7 @@ def _flat_variant(s, edits):
 
 
 @pytest.mark.parametrize("case", ["dup_later", "dup_earlier", "ts_zero", "empty_path", "anchor_later",
-                                  "anchor_missing", "clean"])
+                                  "anchor_missing", "anchor_cycle", "anchor_self", "anchor_gap", "clean"])
 def test_flat_closed_form_edges(case):
     """The flat closed form's one-pass claim + per-slot anchor check, and its
     per-op fallback (duplicates, ts 0, errors), against the oracle."""
@@ -252,6 +252,10 @@ def test_flat_closed_form_edges(case):
         "empty_path": [("empty", 7000, int(ts[3]))],
         "anchor_later": [("ins", 4000, (40 << 32) + 5, (41 << 32) + 5), ("ins", 9000, (41 << 32) + 5, 0)],
         "anchor_missing": [("ins", 11000, (42 << 32) + 1, (43 << 32) + 9)],
+        # (the flat path speculates that every op applies; these fail and must not derail its walks)
+        "anchor_cycle": [("ins", 6000, (44 << 32) + 1, (44 << 32) + 2), ("ins", 6001, (44 << 32) + 2, (44 << 32) + 1)],
+        "anchor_self": [("ins", 8000, (45 << 32) + 1, (45 << 32) + 1)],
+        "anchor_gap": [("ins", 3000, (46 << 32) + 1, 0), ("ins", 3001, (46 << 32) + 5, (46 << 32) + 3)],
     }[case]
     v, m = _flat_variant(s, edits)
     ot, rc, oerr = oracle_apply_arrays(v, m)
