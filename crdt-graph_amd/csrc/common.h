@@ -84,9 +84,10 @@ struct DevResult {
   uint32_t pdr_dicts;       // per-dict replay: dicts of the new state
   uint32_t pdr_slots;       // per-dict replay: slots of the new state
   uint32_t since_end;       // operationsSince: 1 + log index of the newest Add with the asked ts
-  uint32_t fl_keys;         // flat: Adds with a timestamp slot
-  uint32_t fl_slow;         // flat: ops that need per-op statuses (empty path, ts 0)
-  uint32_t fl_part[16 * 32];  // flat: slots holding an Add, 16 partial counts one cache line apart
+  // flat claim/check counters, 16 shards one cache line apart (shard k at
+  // [32 k]): +0 slots holding an Add, +1 Adds with a timestamp slot, +2 Adds
+  // of the own replica, +3 ops that need per-op statuses (empty path, ts 0)
+  uint32_t fl_part[16 * 32];
   uint32_t run_count;       // flat order: ep-runs (scan total)
   uint32_t run_fail;        // flat order: the run tree is deeper than RUN_MAXD (generic list ranking instead)
   uint32_t run_maxd;        // flat order: deepest run

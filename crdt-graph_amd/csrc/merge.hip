@@ -1761,13 +1761,32 @@ constexpr unsigned long long REC_EMPTY = ~0ULL;
 // LDS atomics).
 __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_t Q, unsigned long long* rec,
                                                     long long ts0, uint32_t* rtab, DevResult* dres,
-                                                    uint32_t track_rep) {
-  __shared__ __attribute__((aligned(16))) uint32_t rv[REP_DIRECT];
-  if (track_rep) {
-    for (uint32_t j = threadIdx.x; j < REP_DIRECT / 4; j += blockDim.x)
-      reinterpret_cast<uint4*>(rv)[j] = make_uint4(0u, 0u, 0u, 0u);
+                                                    uint32_t track_rep, uint32_t nrep) {
+  // dynamic LDS: the replica range table (nrep ids: base, min, max counter)
+  // when it fits, else lookups go to the global table; rv when track_rep
+  extern __shared__ __attribute__((aligned(16))) uint32_t scl[];
+  uint32_t* sbase = scl;
+  uint32_t* smin = scl + nrep;
+  uint32_t* smax = scl + 2 * nrep;
+  uint32_t* rv = scl + 3 * nrep;
+  for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x) {
+    sbase[j] = x.base[j];
+    const uint2 g = x.rng[j];
+    smin[j] = g.x;
+    smax[j] = g.y;
   }
+  if (track_rep)
+    for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) rv[j] = 0;
   __syncthreads();
+  auto slot = [&](long long ts) -> uint32_t {
+    if (!nrep) return tsindex_slot(x, ts);
+    if (ts <= 0) return NONE;
+    const uint64_t r = static_cast<uint64_t>(ts) >> 32;
+    if (r >= nrep) return NONE;
+    const uint32_t c = static_cast<uint32_t>(ts), lo = smin[r];
+    if (lo == NONE || c < lo || c > smax[r]) return NONE;
+    return sbase[r] + (c - lo);
+  };
   const long long id0 = replica_of(ts0);
   uint32_t keys = 0, own = 0, slow = 0, err = NONE, mr = 0;
   QUAD_LOOP_XCD(i0, o.n) {
@@ -1784,14 +1803,14 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
       }
       const long long ts = qd.ts[k];
       if (replica_of(ts) == id0) ++own;
-      const uint32_t q = tsindex_slot(x, ts);
+      const uint32_t q = slot(ts);
       if (q == NONE) {  // ts 0: the sentinel's key (AlreadyApplied)
         ++slow;
         continue;
       }
       ++keys;
       const long long kk = o.path[qd.off[k]];
-      const uint32_t qa = kk == 0 ? Q : tsindex_slot(x, kk);
+      const uint32_t qa = kk == 0 ? Q : slot(kk);
       rec[q] = (static_cast<unsigned long long>(i) << 32) | qa;
       if (track_rep) {
         const uint32_t rr = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32);
@@ -1812,10 +1831,11 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
   own = block_sum(own);
   slow = block_sum(slow);
   err = block_min(err);
-  if (threadIdx.x == 0) {
-    if (keys) atomicAdd(&dres->fl_keys, keys);
-    if (own) atomicAdd(&dres->own_ok_adds, own);
-    if (slow) atomicAdd(&dres->fl_slow, slow);
+  if (threadIdx.x == 0) {  // 16 shards a line apart: ~12 ns per atomic on one word
+    uint32_t* sh = dres->fl_part + 32 * (blockIdx.x & 15);
+    if (keys) atomicAdd(&sh[1], keys);
+    if (own) atomicAdd(&sh[2], own);
+    if (slow) atomicAdd(&sh[3], slow);
     if (err != NONE) atomicMin(&dres->err_index, err);
   }
 }
@@ -2349,20 +2369,51 @@ __global__ void __launch_bounds__(BLOCK) k_run_nch(RunArr a, uint32_t Q, const u
 // ancestors; a child announces its size with ONE 64-bit device-scope atomic
 // {arrivals += 1, sizes += T} (memory-side, coherent across the XCDs), and
 // the child that arrives last holds the sum of all its siblings' sizes in
-// the returned value, so it finalises the parent and climbs on. Any depth;
-// a parent with c children serialises c atomics (~12 ns each).
-__global__ void __launch_bounds__(BLOCK) k_run_tree_up(RunArr a) {
-  RUN_LOOP(r) {
-    if (a.nch[r] != 0) continue;  // an inner run: finalised by its last child
-    uint32_t x = r, t = a.len[r];
-    for (;;) {
-      a.T[x] = t;
-      const uint32_t p = a.par[x];
-      if (p == NONE) break;
-      const unsigned long long old = atomicAdd(&a.ca[p], (1ULL << 32) | t);
-      if (static_cast<uint32_t>(old >> 32) + 1u != a.nch[p]) break;
-      t = a.len[p] + static_cast<uint32_t>(old) + t;
-      x = p;
+// the returned value, so it finalises the parent and climbs on. Any depth.
+// Leaves are taken in sibling order, where a parent's children sit side by
+// side: a wave sums its leaves per parent first (one atomic per wave and
+// parent; a parent with thousands of children would otherwise serialise
+// thousands of atomics on one word, ~12 ns each).
+__device__ __forceinline__ void run_climb(RunArr& a, uint32_t x, uint32_t t) {
+  for (;;) {
+    a.T[x] = t;
+    const uint32_t p = a.par[x];
+    if (p == NONE) return;
+    const unsigned long long old = atomicAdd(&a.ca[p], (1ULL << 32) | t);
+    if (static_cast<uint32_t>(old >> 32) + 1u != a.nch[p]) return;
+    t = a.len[p] + static_cast<uint32_t>(old) + t;
+    x = p;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_run_tree_up(RunArr a, const uint32_t* sarr) {
+  const uint32_t R = *a.nR;
+  const int lane = threadIdx.x & 63;
+  for (uint32_t k0 = blockIdx.x * blockDim.x; k0 < R; k0 += gridDim.x * blockDim.x) {
+    const uint32_t k = k0 + threadIdx.x;
+    uint32_t key = NONE - 1 - static_cast<uint32_t>(lane);  // (distinct per idle lane)
+    unsigned long long v = 0;                                // leaves << 32 | their sizes
+    if (k < R) {
+      const uint32_t r = sarr[k];
+      key = a.par[r];
+      if (a.nch[r] == 0) {
+        const uint32_t t = a.len[r];
+        a.T[r] = t;
+        v = (1ULL << 32) | t;
+      }
+    }
+    // segmented inclusive sum over lanes with the same parent (contiguous)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long ov = __shfl_up(v, o, 64);
+      const uint32_t ok = __shfl_up(key, o, 64);
+      if (lane >= o && ok == key) v += ov;
+    }
+    const uint32_t nk = __shfl_down(key, 1, 64);
+    if ((lane == 63 || nk != key) && key < NONE - 64 && (v >> 32)) {
+      const unsigned long long old = atomicAdd(&a.ca[key], v);
+      if (static_cast<uint32_t>(old >> 32) + static_cast<uint32_t>(v >> 32) == a.nch[key])
+        run_climb(a, key, a.len[key] + static_cast<uint32_t>(old) + static_cast<uint32_t>(v));
     }
   }
 }
@@ -2774,7 +2825,7 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     LAUNCH(k_run_gstart, dim3(gr), dim3(BLOCK), 0, s, ra, pk, gstart);
     LAUNCH(k_run_nch, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, sarr, gstart);
     // ---- subtree sizes (one launch), slot ranks inside runs, head ranks ----
-    LAUNCH(k_run_tree_up, dim3(gr), dim3(BLOCK), 0, s, ra);
+    LAUNCH(k_run_tree_up, dim3(gr), dim3(BLOCK), 0, s, ra, sarr);
     LAUNCH(k_run_gather, dim3(gr), dim3(BLOCK), 0, s, ra, sarr, tk);
     if ((r = dscan<SumOp, false>(ArrGen{tk}, xs, K, nullptr, ws, s, nullptr, ra.nR))) return r;
     LAUNCH(k_run_side, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, tk, xs, gstart, side);
@@ -2870,8 +2921,8 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   LAUNCH(k_fl_init, dim3(grid_for(Q, BLOCK, 4096)), dim3(BLOCK), 0, s, Q, fb.rec);
   // replicas table: folded by the check over slot order when the range table fits in LDS
   const uint32_t nrep = maxr + 1 <= HOST_RANGES ? maxr + 1 : 0u;
-  LAUNCH(k_fl_claim, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix, Q, fb.rec, t->timestamp, c->rtab, dr,
-         nrep ? 0u : 1u);
+  LAUNCH(k_fl_claim, dim3(quad_grid(n)), dim3(BLOCK), (3 * nrep + (nrep ? 0 : REP_DIRECT)) * sizeof(uint32_t), s,
+         o, ix, Q, fb.rec, t->timestamp, c->rtab, dr, nrep ? 0u : 1u, nrep);
   LAUNCH(k_fl_check, dim3(grid_for(Q / 2 + 1, BLOCK, 2048)), dim3(BLOCK), 2 * nrep * sizeof(uint32_t), s, Q,
          fb.rec, dr, ix.base, nrep, c->rtab);
   int r;
@@ -2911,10 +2962,15 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, nullptr, n, NONE, st_out);
     if ((r = sync_read(c))) return r;
     const DevResult& h = *c->hres;
-    uint32_t present = 0;
-    for (int k = 0; k < 16; ++k) present += h.fl_part[32 * k];
-    const long long new_ts = t->timestamp + h.own_ok_adds;
-    const bool every = h.err_index == NONE && h.fl_slow == 0 && present == h.fl_keys && h.fl_keys == n;
+    uint32_t present = 0, keys = 0, own = 0, slow = 0;  // (k_fl_check / k_fl_claim shards)
+    for (int k = 0; k < 16; ++k) {
+      present += h.fl_part[32 * k];
+      keys += h.fl_part[32 * k + 1];
+      own += h.fl_part[32 * k + 2];
+      slow += h.fl_part[32 * k + 3];
+    }
+    const long long new_ts = t->timestamp + own;
+    const bool every = h.err_index == NONE && slow == 0 && present == keys && keys == n;
     if (every && replica_of(new_ts) == replica_of(t->timestamp)) {
       if (h.run_fail && (r = flat_order_fallback(t, Q, n, fb))) return r;
       res->guard = 0;
@@ -2988,7 +3044,9 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   uint32_t* rbase = ws.alloc<uint32_t>(RID_SLOTS + 1);
   DevResult* dr = c->dres;
   LAUNCH(k_dres_init, dim3(1), dim3(64), 0, s, dr);
-  LAUNCH(k_pre, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, c->crange, dr);
+  // (512 workgroups: each flushes its replica ranges and counters with
+  // device-scope atomics that serialise per word, ~12 ns each)
+  LAUNCH(k_pre, dim3(std::min<uint32_t>(quad_grid(n), 512)), dim3(BLOCK), 0, s, o, c->crange, dr);
   LAUNCH(k_range_base, dim3(1), dim3(BLOCK), 0, s, c->crange, rbase, dr);
   RangeReset keep_clean{c};  // resets the context's replica ranges on every exit
   int r;
