@@ -184,6 +184,38 @@ __device__ __forceinline__ uint32_t ld_uniform(const uint32_t* S, uint32_t k) {
   return __builtin_amdgcn_readfirstlane(S[k]);
 }
 
+// nextNode's tombstone skip (src/Internal/Node.elm:257-268) from chain entry
+// p (slot word wp): the first live entry from p on, or PM; *wp becomes its
+// word. Tombstone runs through consecutive ranks are crossed 64 ranks at a
+// time (wave-uniform: every lane runs it with the same p).
+__device__ __forceinline__ uint32_t pdr_next_live(const uint32_t* S, uint32_t K, uint32_t lane, uint32_t p,
+                                                  uint32_t& wp) {
+  while (p != PM && (wp & SF_TOMB)) {
+    const uint32_t q = wp & PM;
+    if (q == p + 1) {
+      const uint32_t e = p + lane;
+      const bool in = e <= K;
+      const uint32_t a = in ? S[e] : 0u;
+      const unsigned long long lb = __ballot(in && (a & PM) == e + 1);
+      const unsigned long long vb = __ballot(in && (a & SF_MADE) && !(a & SF_TOMB));
+      const uint32_t m = lb == ~0ULL ? 64u : static_cast<uint32_t>(__builtin_ctzll(~lb));
+      const uint32_t M = m < 63u ? m : 63u;
+      const unsigned long long lv = vb & ((M == 63u ? ~0ULL : ((2ULL << M) - 1ULL)) & ~1ULL);
+      if (lv) {
+        const uint32_t j = static_cast<uint32_t>(__builtin_ctzll(lv));
+        wp = __builtin_amdgcn_readlane(a, j);
+        return p + j;
+      }
+      p = __builtin_amdgcn_readlane(a, M) & PM;
+    } else {
+      p = q;
+    }
+    if (p == PM) break;
+    wp = __builtin_amdgcn_readfirstlane(S[p]);
+  }
+  return p;
+}
+
 // ---- P2: the serial replay of one dict (instance) on one wave ----
 // All lanes run the loop with identical values (wave-uniform control flow,
 // broadcast LDS reads); S points to LDS (or to the region for huge dicts).
@@ -259,34 +291,46 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
           for (;;) {
             const uint32_t rn = wn & PM;
             if (rn == PM) break;
-            uint32_t live = rn, wl = ld_uniform(S, rn);
-            while (wl & SF_TOMB) {
-              live = wl & PM;
-              if (live == PM) break;
-              wl = ld_uniform(S, live);
+            if (rn == node + 1 && x < rn) {
+              // Window step. The chain runs through consecutive ranks from
+              // node (node -> node+1 -> ...), so every key ahead is larger
+              // than x: the walk visits each live entry of the run and goes
+              // on (nextNode skips the run's tombstones); lane l reads rank
+              // node+l. Afterwards node = the last visited entry and the
+              // copy quirk's n = the rank after the entry visited before it.
+              const uint32_t e = node + lane;
+              const bool in = e <= K;
+              const uint32_t a = in ? S[e] : 0u;
+              const unsigned long long lb = __ballot(in && (a & PM) == e + 1);
+              const unsigned long long vb = __ballot(in && (a & SF_MADE) && !(a & SF_TOMB));
+              const uint32_t m = lb == ~0ULL ? 64u : static_cast<uint32_t>(__builtin_ctzll(~lb));  // >= 1
+              const uint32_t M = m < 63u ? m : 63u;  // ranks node..node+M are chained
+              const unsigned long long vis = vb & ((M == 63u ? ~0ULL : ((2ULL << M) - 1ULL)) & ~1ULL);
+              if (vis) {
+                const uint32_t vs = 63u - static_cast<uint32_t>(__builtin_clzll(vis));
+                const unsigned long long rest = (vis & ~(1ULL << vs)) | 1ULL;
+                nk = node + (63u - static_cast<uint32_t>(__builtin_clzll(rest))) + 1u;
+                wn = __builtin_amdgcn_readlane(a, vs);
+                node += vs;
+                continue;
+              }
+              // ranks node+1..node+M are tombstones: the next live entry lies past them
+              uint32_t p = __builtin_amdgcn_readlane(a, M) & PM;
+              uint32_t wl = p == PM ? 0u : ld_uniform(S, p);
+              p = pdr_next_live(S, K, lane, p, wl);
+              if (p == PM) break;  // only tombstones follow: stop here
+              nk = node + 1u;      // (x < node + 1: the walk goes on)
+              node = p;
+              wn = wl;
+              continue;
             }
+            uint32_t wl = ld_uniform(S, rn);
+            const uint32_t live = pdr_next_live(S, K, lane, rn, wl);
             if (live == PM) break;
             if (x > rn) break;  // ts > key(rn)
             nk = rn;
             node = live;
             wn = wl;
-            // Typing run: node, node+1, node+2, ... chained in rank order and
-            // all live. Every later comparison passes (x <= node < node+1 <
-            // ...), so the walk crosses the run in one step: lane l checks
-            // the link node+l -> node+l+1 (two contiguous LDS reads).
-            if (rn == live && (wn & PM) == node + 1) {
-              const uint32_t e = node + lane;
-              const bool in = e + 1 <= K;
-              const uint32_t a = in ? S[e] : 0u, b = in ? S[e + 1] : 0u;
-              const bool ok = in && (a & PM) == e + 1 && (b & SF_MADE) && !(b & SF_TOMB);
-              const unsigned long long bal = __ballot(ok);
-              const uint32_t m = bal == ~0ULL ? 64u : static_cast<uint32_t>(__builtin_ctzll(~bal));
-              if (m > 0) {
-                node += m;
-                nk = node;
-                wn = __builtin_amdgcn_readlane(b, m - 1);
-              }
-            }
           }
           const uint32_t wk = nk == node ? wn : ld_uniform(S, nk);
           S[x] = (wn & PM) | (wk & SF_ORPHAN) | SF_MADE;
