@@ -200,6 +200,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=-1, help="oracle sample ops (0 = skip)")
     ap.add_argument("--profile-steps", type=int, default=3)
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--exchange", choices=("auto", "on", "off"), default="auto",
+                    help="also run config 5 (op-log all-gather + sharded merge) after a single-document "
+                         "workload and attach its line as 'exchange' (auto: when N > 1)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -218,7 +221,12 @@ def main():
     from crdtm import _native as N
     L = N.lib()
     if args.workload == "trees":
-        return run_trees(args, rank, world, local_rank)
+        line = run_trees(args, rank, world, local_rank)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     spec = dict(WORKLOADS[args.workload])
     if args.n_ops:
@@ -321,15 +329,24 @@ def main():
             m = min(m, n)
             line["cpu_baseline"] = cpu_line(cpu_baseline(s, m),
                                             f"first {m} ops of the same batch (cost grows with the batch)")
-    if rank == 0:
-        print(json.dumps(line), flush=True)
     L.crdtm_tree_destroy(tree)
     L.crdtm_ctx_destroy(ctx)
+    del tens
+    # The single-document workloads exchange nothing between ranks; config 5 is
+    # the path with the RCCL all-gather, so a multi-GPU run measures it too and
+    # carries its line (same clocks, same contract) under "exchange".
+    if args.exchange == "on" or (args.exchange == "auto" and world > 1):
+        ex = run_trees(args, rank, world, local_rank, cpu=False)
+        line["exchange"] = {k: ex[k] for k in ("metric", "value", "unit", "ms_per_step", "config")}
+        line["exchange"]["roofline_frac"] = ex["roofline"]["frac"]
+        line["exchange"]["all_gather_ms"] = ex["all_gather_ms"]
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def run_trees(args, rank, world, local_rank):
+def run_trees(args, rank, world, local_rank, cpu=True):
     """Config 5: all-gather of the simulated replicas' op logs (RCCL), then every
     rank merges the documents it owns (document t -> rank t mod world)."""
     import torch
@@ -354,6 +371,7 @@ def run_trees(args, rank, world, local_rank):
         logs.append(rec)
     local = torch.from_numpy(np.concatenate(logs)).to(dev)
     del logs
+    ex = shard.Exchange(local)  # counts gathered once; persistent padded buffers
     ctx = C.c_void_p()
     stream = torch.cuda.current_stream()
     N.check(L.crdtm_ctx_create(local_rank, C.c_void_p(stream.cuda_stream), C.byref(ctx)), "ctx")
@@ -363,7 +381,7 @@ def run_trees(args, rank, world, local_rank):
     state = {}
 
     def step():
-        allrec = shard.all_gather_records(local)
+        allrec = ex.gather()
         ops_t, doc_off, _ = shard.assemble(allrec, rank, world, n_docs, per, ctx=ctx)
         n = int(doc_off[-1])
         ops = N.Ops(n, n, ops_t["kind"].data_ptr(), ops_t["ts"].data_ptr(), ops_t["path_off"].data_ptr(),
@@ -410,8 +428,20 @@ def run_trees(args, rank, world, local_rank):
         nm = labels[j].decode()
         per_k[nm] = per_k.get(nm, 0.0) + ms[j]
         launches[nm] = launches.get(nm, 0) + 1
+    # the all-gather alone (RCCL over xGMI), timed the same way
+    ag_ms = 0.0
+    if world > 1:
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            ex.gather()
+        torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ag_ms = float(t.item()) / args.steps * 1e3
     ot = state["ops_t"]
-    kinds = ot["kind"].cpu().numpy()
+    kinds = ot["kind"][:n].cpu().numpy()
     B_alg = int(np.sum(np.where(kinds == 0, 57, 17)))  # flat documents: L = 1
     ms_step = elapsed / args.steps * 1e3
     line = {
@@ -423,11 +453,12 @@ def run_trees(args, rank, world, local_rank):
                    "replicas": TREES["replicas"], "documents_ok": ok_docs,
                    "parallelism": f"documents sharded by id over {world} GPU(s); op logs all-gathered (RCCL)"},
         "roofline": roofline("trees", per_k, launches, B_alg, ms_step, 1),
+        "all_gather_ms": ag_ms,
     }
     if args.verbose and rank == 0:
         for nm, v in sorted(per_k.items(), key=lambda kv: -kv[1])[:12]:
             print(f"  {nm:28s} {v:9.3f} ms", file=sys.stderr)
-    if rank == 0 and world == 1:
+    if cpu and rank == 0 and world == 1:
         m = args.cpu_sample if args.cpu_sample >= 0 else CPU_SAMPLE["trees"]
         if m > 0:
             host = {k: v.cpu().numpy() for k, v in ot.items()}
@@ -439,11 +470,8 @@ def run_trees(args, rank, world, local_rank):
             cb = cpu_baseline(sub, ndoc * per, doc_off=np.arange(ndoc + 1, dtype=np.uint32) * per, workers=workers)
             line["cpu_baseline"] = cpu_line(cb, f"{ndoc} documents x {per} ops, documents round-robin over "
                                                 f"worker_threads")
-    if rank == 0:
-        print(json.dumps(line), flush=True)
     L.crdtm_ctx_destroy(ctx)
-    if world > 1:
-        dist.destroy_process_group()
+    return line
 
 
 if __name__ == "__main__":

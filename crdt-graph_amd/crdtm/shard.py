@@ -54,6 +54,40 @@ def local_log(s, doc_off, rank, world, replicas):
     return pack_records(s, doc_off, mine)
 
 
+class Exchange:
+    """The op-log all-gather of one step, with its buffers kept across steps.
+
+    Each rank's log for the step's documents has a fixed record count, so the
+    counts are gathered once (no host sync in the step). The local records sit
+    at the head of a persistent send block padded to the largest count with
+    rows of -1 (document id 0xFFFFFFFF, never owned: crdtm_shard_assemble and
+    `assemble` skip them); `gather()` is one all_gather_into_tensor into a
+    persistent receive buffer of world x block rows, which the assembly reads
+    as it is (no per-rank slicing, no concatenation)."""
+
+    def __init__(self, local: torch.Tensor, group=None):
+        self.group = group
+        self.dist = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        self.world = dist.get_world_size(group) if self.dist else 1
+        if not self.dist:
+            self.recv = local
+            return
+        cnt = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
+        cnts = torch.zeros(self.world, dtype=torch.int64, device=local.device)
+        dist.all_gather_into_tensor(cnts, cnt, group=group)
+        self.counts = [int(c) for c in cnts.cpu()]  # once, at setup
+        self.block = max(self.counts)
+        self.send = torch.full((self.block, REC_W), -1, dtype=torch.int64, device=local.device)
+        self.send[:local.shape[0]] = local
+        self.recv = torch.empty((self.world * self.block, REC_W), dtype=torch.int64, device=local.device)
+
+    def gather(self) -> torch.Tensor:
+        """Every rank's records (padding rows included) in the receive buffer."""
+        if self.dist:
+            dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
+        return self.recv
+
+
 def all_gather_records(local: torch.Tensor, group=None) -> torch.Tensor:
     """All-gather variable-length record blocks: counts first, then padded blocks."""
     if not (dist.is_available() and dist.is_initialized()):
@@ -80,6 +114,7 @@ def all_gather_records(local: torch.Tensor, group=None) -> torch.Tensor:
 
 
 _ARANGE = {}
+_SOA = {}
 
 
 def assemble(records: torch.Tensor, rank, world, n_docs, per_doc, ctx=None):
@@ -95,11 +130,16 @@ def assemble(records: torch.Tensor, rank, world, n_docs, per_doc, ctx=None):
         import ctypes as C
         from . import _native as N
         dev = records.device
-        out = dict(kind=torch.zeros(n + 1, dtype=torch.uint8, device=dev),
-                   ts=torch.zeros(n + 1, dtype=torch.int64, device=dev),
-                   path_off=torch.empty(n + 1, dtype=torch.int32, device=dev),
-                   path=torch.zeros(n + 1, dtype=torch.int64, device=dev),
-                   val=torch.zeros(n + 1, dtype=torch.int32, device=dev))
+        key = ("soa", str(dev), n, ctx.value if hasattr(ctx, "value") else id(ctx))
+        out = _SOA.get(key)
+        if out is None:  # every slot is rewritten each step: kept across steps
+            out = dict(kind=torch.zeros(n + 1, dtype=torch.uint8, device=dev),
+                       ts=torch.zeros(n + 1, dtype=torch.int64, device=dev),
+                       path_off=torch.empty(n + 1, dtype=torch.int32, device=dev),
+                       path=torch.zeros(n + 1, dtype=torch.int64, device=dev),
+                       val=torch.zeros(n + 1, dtype=torch.int32, device=dev))
+            _SOA.clear()
+            _SOA[key] = out
         records = records.contiguous()
         ops = N.Ops(n, n, out["kind"].data_ptr(), out["ts"].data_ptr(), out["path_off"].data_ptr(),
                     out["path"].data_ptr(), out["val"].data_ptr(), None)
@@ -108,7 +148,7 @@ def assemble(records: torch.Tensor, rank, world, n_docs, per_doc, ctx=None):
         return out, doc_off, None
     doc = records[:, 0] >> 32
     seq = records[:, 0] & 0xFFFFFFFF
-    keep = (doc % world) == rank
+    keep = (doc >= 0) & ((doc % world) == rank) & (seq < per_doc)  # padding rows carry -1
     dst = torch.where(keep, (doc // world) * per_doc + seq, torch.full_like(doc, n))
     dev = records.device
     kind = torch.zeros(n + 1, dtype=torch.uint8, device=dev)

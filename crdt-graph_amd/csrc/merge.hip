@@ -1384,27 +1384,26 @@ struct Fnv {
 
 // ---------------------------------------------------------------------------
 // Forest fast path for flat documents (every op's path has length <= 1) of
-// at most FL_MAXOPS ops, in two kernels (one wave per document each).
-// k_forest_prep (64 lanes): the document's Add keys and the sentinel key 0
+// at most FL_MAXOPS ops, in two kernels.
+// k_forest_prep (one 256-thread workgroup per document): the document's Add
+// keys and the sentinel key 0
 // are sorted in LDS (bitonic); a key's slot = the index of its first
 // occurrence, so slot order is key order (findInsertion's `ts > key` becomes
 // a slot comparison) and every op's target / anchor slot is one binary
 // search. Result: one packed word per op in HBM.
-// k_forest_replay (one lane, 4 KB of LDS per document, so 32 documents per
-// CU): the literal sequential replay of addAfterHelp / findInsertion /
-// deleteHelp (src/Internal/Node.elm:56-122) on one packed word per slot
-// {next, source op, present, tombstone, orphan}, including the copy quirk (a
-// flat node's children are always the initial empty dict, so a copy is the
-// slot's own fields); then the visible document is hashed like k_forest and
-// the oracle. Documents that do not fit are left to k_forest (fb[d] = 1).
+// k_forest_lanes (one lane per document): the literal sequential replay of
+// addAfterHelp / findInsertion / deleteHelp (src/Internal/Node.elm:56-122) on
+// one packed word per slot {next, present, tombstone, orphan}, including the
+// copy quirk (a flat node's children are always the initial empty dict, so a
+// copy is the slot's own fields); then the visible document is hashed like
+// k_forest and the oracle. Documents that do not fit are left to k_forest
+// (fb[d] = 1).
 // ---------------------------------------------------------------------------
 constexpr uint32_t FL_MAXOPS = 1023;  // + the sentinel key: 1024 sort slots
 constexpr uint32_t FL_SLOTS = 1024;
 constexpr uint32_t FL_N = 0x7FF;  // 11-bit "none"
 // per-op word: tslot | aslot << 11 | DEL << 22 | INVALID << 23 | OWN << 24
 constexpr uint32_t FO_DEL = 1u << 22, FO_INV = 1u << 23, FO_OWN = 1u << 24;
-// per-slot word: next | src << 11 | PRESENT << 21 | TOMB << 22 | ORPHAN << 23
-constexpr uint32_t FS_PRESENT = 1u << 21, FS_TOMB = 1u << 22, FS_ORPHAN = 1u << 23;
 
 __device__ __forceinline__ uint32_t fl_lower(const long long* k, long long x) {
   uint32_t lo = 0, hi = FL_SLOTS;
@@ -1416,9 +1415,12 @@ __device__ __forceinline__ uint32_t fl_lower(const long long* k, long long x) {
   return lo;
 }
 
-__global__ void __launch_bounds__(64) k_forest_prep(OpsDev o, const uint32_t* doc_off, uint32_t n_docs, long long ts0,
-                                                    uint32_t* opw, uint16_t* sent, uint8_t* fb) {
+constexpr uint32_t FPREP_THREADS = 256;  // one workgroup (4 waves) per document
+
+__global__ void __launch_bounds__(FPREP_THREADS) k_forest_prep(OpsDev o, const uint32_t* doc_off, uint32_t n_docs, long long ts0,
+                                                    uint32_t* opw, uint16_t* sent, uint8_t* fb, longlong2* vt) {
   __shared__ long long skey[FL_SLOTS];
+  __shared__ uint32_t cre[FL_SLOTS];  // slot -> its first Add (the one that can create it)
   const uint32_t d = blockIdx.x;
   if (d >= n_docs) return;
   const uint32_t lane = threadIdx.x;
@@ -1430,7 +1432,7 @@ __global__ void __launch_bounds__(64) k_forest_prep(OpsDev o, const uint32_t* do
   constexpr long long INF = 0x7fffffffffffffffLL;
   const long long own = replica_of(ts0);
   uint32_t bad = 0;
-  for (uint32_t j = lane; j < FL_SLOTS; j += 64) {
+  for (uint32_t j = lane; j < FL_SLOTS; j += FPREP_THREADS) {
     long long key = INF;
     if (j < nops) {
       const uint32_t i = ob + j;
@@ -1441,15 +1443,15 @@ __global__ void __launch_bounds__(64) k_forest_prep(OpsDev o, const uint32_t* do
       key = 0;  // the root dict's sentinel
     }
     skey[j] = key;
+    cre[j] = NONE;
   }
-  if (__any(bad)) {
+  if (__syncthreads_or(bad)) {
     if (lane == 0) fb[d] = 1;
     return;
   }
-  __syncthreads();
   for (uint32_t k = 2; k <= FL_SLOTS; k <<= 1) {
     for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-      for (uint32_t i = lane; i < FL_SLOTS; i += 64) {
+      for (uint32_t i = lane; i < FL_SLOTS; i += FPREP_THREADS) {
         const uint32_t ixj = i ^ jj;
         if (ixj > i) {
           const long long a = skey[i], b = skey[ixj];
@@ -1462,7 +1464,7 @@ __global__ void __launch_bounds__(64) k_forest_prep(OpsDev o, const uint32_t* do
       __syncthreads();
     }
   }
-  for (uint32_t j = lane; j < nops; j += 64) {
+  for (uint32_t j = lane; j < nops; j += FPREP_THREADS) {
     const uint32_t i = ob + j;
     const uint32_t L = o.off[i + 1] - o.off[i];
     uint32_t w;
@@ -1480,168 +1482,205 @@ __global__ void __launch_bounds__(64) k_forest_prep(OpsDev o, const uint32_t* do
       }
     }
     opw[i] = w;
+    if (o.kind[i] == CRDTM_ADD && L == 1) atomicMin(&cre[w & FL_N], j);
   }
   if (lane == 0) sent[d] = static_cast<uint16_t>(fl_lower(skey, 0));
-}
-
-// The whole wave runs the replay with identical values (wave-uniform control
-// flow, broadcast LDS reads moved to scalar registers): op words stream
-// through registers 64 at a time, and the hash inputs of the visible
-// document are gathered 64 at a time by all lanes.
-__device__ __forceinline__ uint32_t fl_ld(const uint32_t* sl, uint32_t k) {
-  return __builtin_amdgcn_readfirstlane(sl[k]);
-}
-
-__global__ void __launch_bounds__(64) k_forest_replay(OpsDev o, const uint32_t* doc_off, uint32_t n_docs,
-                                                      long long ts0, const uint32_t* opw, const uint16_t* sent,
-                                                      const uint8_t* fb, int32_t* code_out, uint32_t* err_out,
-                                                      uint32_t* applied_out, unsigned long long* vhash,
-                                                      unsigned long long* vwords, long long* tstamp,
-                                                      uint32_t* overflow) {
-  __shared__ uint32_t sl[FL_SLOTS];
-  const uint32_t d = blockIdx.x;
-  if (d >= n_docs || fb[d]) return;
-  const uint32_t lane = threadIdx.x;
-  const uint32_t ob = doc_off[d], nops = doc_off[d + 1] - ob;
-  const uint32_t s0 = sent[d];
-  for (uint32_t j = lane; j < FL_SLOTS; j += 64) sl[j] = j == s0 ? (FL_N | FS_PRESENT | FS_TOMB) : FL_N;
+  if (!vt) return;
   __syncthreads();
-  // Fresh documents start at counter 0 of their replica, so no run of at most
-  // FL_MAXOPS own Adds can cross into the next replica id: the OWN bit of
-  // each op (computed against ts0) is the reference's per-op comparison.
-  long long ts = ts0;
-  uint32_t applied = 0, err = NONE;
+  // hash inputs per slot: value and timestamp of the Add that creates it
+  longlong2* v = vt + static_cast<uint64_t>(d) * FL_SLOTS;
+  for (uint32_t j = lane; j < FL_SLOTS; j += FPREP_THREADS) {
+    const uint32_t c = cre[j];
+    if (c != NONE) v[j] = make_longlong2(static_cast<long long>(o.val[ob + c]), o.ts[ob + c]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Lane-per-document replay (the literal addAfterHelp / findInsertion /
+// deleteHelp, src/Internal/Node.elm:56-122, copy quirk included): lane m < D
+// of a workgroup replays document blockIdx.x * D + m on a 16-bit word per slot {next:11, present, tombstone, orphan} in LDS. A
+// wave-uniform replay puts every step on the CU's scalar unit (~123k scalar
+// instructions per 1,000-op document); here each step is a handful of vector
+// instructions, and small D leaves many waves per SIMD to hide the dependent
+// LDS latency of the walks. The op words reach LDS 64 per document at a time,
+// loaded coalesced by the whole wave. What a slot carries for the hash (value,
+// timestamp of its Add; a copy takes the copied node's) lives in `vt`, written
+// by k_forest_prep and updated on the (rare) copy quirk.
+// ---------------------------------------------------------------------------
+constexpr uint16_t FW_PRESENT = 1u << 11, FW_TOMB = 1u << 12, FW_ORPHAN = 1u << 13;
+// slot words cover indices [0, FL_N]: slot FL_N ("none") stays 0 (absent, not
+// a tombstone), so lookups of "none" need no test and tombstone runs end there
+constexpr uint32_t FLANE_REGION = FL_N + 1;
+
+// slot j of lane m at j * D + m: each lane keeps to its own banks
+template <uint32_t D>
+struct LaneSlots {
+  uint16_t* base;
+  __device__ __forceinline__ uint32_t operator[](uint32_t j) const { return base[j * D]; }
+  __device__ __forceinline__ void set(uint32_t j, uint32_t w) const { base[j * D] = static_cast<uint16_t>(w); }
+};
+
+template <uint32_t D>
+__global__ void __launch_bounds__(64) k_forest_lanes(const uint32_t* doc_off, uint32_t n_docs, long long ts0,
+                                                     const uint32_t* opw, const uint16_t* sent, const uint8_t* fb,
+                                                     longlong2* vt, int32_t* code_out, uint32_t* err_out,
+                                                     uint32_t* applied_out, unsigned long long* vhash,
+                                                     unsigned long long* vwords, long long* tstamp,
+                                                     uint32_t* overflow) {
+  extern __shared__ uint16_t slw[];  // [FLANE_REGION][D] slot words, then [64][D] op words
+  uint32_t* lops = reinterpret_cast<uint32_t*>(slw + FLANE_REGION * D);
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t j = lane; j < FLANE_REGION * D / 8; j += 64) reinterpret_cast<uint4*>(slw)[j] = make_uint4(0, 0, 0, 0);
+  const uint32_t d0 = blockIdx.x * D;
+  uint32_t obm[D], nm[D], cmax = 0;
+#pragma unroll
+  for (uint32_t m = 0; m < D; ++m) {
+    const uint32_t dm = d0 + m;
+    obm[m] = nm[m] = 0;
+    if (dm < n_docs && !fb[dm]) {
+      obm[m] = doc_off[dm];
+      nm[m] = doc_off[dm + 1] - obm[m];
+    }
+    cmax = max(cmax, nm[m]);
+  }
+  const uint32_t d = d0 + lane;
+  const bool act = lane < D && d < n_docs && !fb[d];
+  const uint32_t nops = act ? doc_off[d + 1] - doc_off[d] : 0u;
+  const LaneSlots<D> sl{slw + (lane < D ? lane : 0u)};
+  __syncthreads();
+  const uint32_t s0 = act ? sent[d] : 0u;
+  if (act) sl.set(s0, FL_N | FW_PRESENT | FW_TOMB);
+  // (fresh documents start at counter 0 of their replica: no run of at most
+  // FL_MAXOPS own Adds crosses into the next replica id, so the OWN bit of each
+  // op is the reference's per-op comparison)
+  uint32_t own = 0, applied = 0, err = NONE;
   int32_t code = CRDTM_OK;
-  uint32_t nxw = lane < nops ? opw[ob + lane] : 0u;
-  bool stop = false;
-  for (uint32_t j0 = 0; j0 < nops && !stop; j0 += 64) {
-    const uint32_t myw = nxw;
-    nxw = j0 + 64 + lane < nops ? opw[ob + j0 + 64 + lane] : 0u;
-    const uint32_t cnt = min(64u, nops - j0);
-    for (uint32_t jj = 0; jj < cnt; ++jj) {
-      const uint32_t j = j0 + jj;
-      const uint32_t w = __builtin_amdgcn_readlane(myw, jj);
-      if (w & FO_INV) {  // update [] = InvalidPath
-        err = j;
-        code = CRDTM_INVALID_PATH;
-        stop = true;
-        break;
-      }
-      const uint32_t t = w & FL_N;
-      if (w & FO_DEL) {  // deleteHelp (:112-122)
-        const uint32_t st = t == FL_N ? 0u : fl_ld(sl, t);
-        if (!(st & FS_PRESENT)) {
-          err = j;
+  bool run = act;
+  for (uint32_t c0 = 0; c0 < cmax; c0 += 64) {
+#pragma unroll
+    for (uint32_t m = 0; m < D; ++m) lops[lane * D + m] = c0 + lane < nm[m] ? opw[obm[m] + c0 + lane] : 0u;
+    __syncthreads();
+    if (run) {
+      const uint32_t kend = min(64u, nops - min(nops, c0));
+      for (uint32_t k = 0; k < kend; ++k) {
+        const uint32_t w = lops[k * D + lane];
+        const uint32_t t = w & FL_N;
+        const uint32_t st = sl[t];
+        if (w & (FO_DEL | FO_INV)) {
+          if ((w & FO_INV) || !(st & FW_PRESENT)) {  // InvalidPath / deleteHelp NotFound (:112-122)
+            err = c0 + k;
+            code = (w & FO_INV) ? CRDTM_INVALID_PATH : CRDTM_OPERATION_FAILED;
+            run = false;
+            break;
+          }
+          if (!(st & FW_TOMB)) {
+            sl.set(t, st | FW_TOMB);
+            ++applied;
+          }
+          continue;
+        }
+        const uint32_t ownb = (w >> 24) & 1u;
+        if (st & FW_PRESENT) {  // `child ts parent` exists: AlreadyApplied
+          own += ownb;
+          continue;
+        }
+        const uint32_t a = (w >> 11) & FL_N;
+        const uint32_t sa = sl[a];
+        if (!(sa & FW_PRESENT)) {  // anchor missing: NotFound
+          err = c0 + k;
           code = CRDTM_OPERATION_FAILED;
-          stop = true;
+          run = false;
           break;
         }
-        if (!(st & FS_TOMB)) {
-          sl[t] = st | FS_TOMB;
-          ++applied;
-        }
-        continue;
-      }
-      const uint32_t x = t;
-      if (fl_ld(sl, x) & FS_PRESENT) {  // `child ts parent` exists: AlreadyApplied
-        if (w & FO_OWN) ++ts;
-        continue;
-      }
-      const uint32_t a = (w >> 11) & FL_N;
-      const uint32_t sa = a == FL_N ? 0u : fl_ld(sl, a);
-      if (!(sa & FS_PRESENT)) {  // anchor missing: NotFound
-        err = j;
-        code = CRDTM_OPERATION_FAILED;
-        stop = true;
-        break;
-      }
-      uint32_t nk = a, node = a, sn = sa;  // findInsertion (:93-104)
-      for (;;) {
-        const uint32_t rn = sn & FL_N;
-        if (rn == FL_N) break;
-        uint32_t live = rn, sl_live = fl_ld(sl, rn);
-        while (sl_live & FS_TOMB) {
-          live = sl_live & FL_N;
-          if (live == FL_N) break;
-          sl_live = fl_ld(sl, live);
-        }
-        if (live == FL_N || x > rn) break;
-        nk = rn;
-        node = live;
-        sn = sl_live;
-      }
-      const uint32_t snk = nk == node ? sn : fl_ld(sl, nk);
-      sl[x] = (sn & FL_N) | (j << 11) | FS_PRESENT | (snk & FS_ORPHAN);
-      if (nk == node) {
-        sl[node] = (sn & ~FL_N) | x;
-      } else {  // copy quirk: slot nk := copy of node with next = x
-        if (!(snk & FS_ORPHAN)) {
-          for (uint32_t q = snk & FL_N; q != FL_N;) {
-            const uint32_t sq = fl_ld(sl, q);
-            sl[q] = sq | FS_ORPHAN;
-            if (q == node) break;
-            q = sq & FL_N;
+        const uint32_t x = t;
+        uint32_t nk = a, node = a, sn = sa;  // findInsertion (:93-104)
+        for (;;) {
+          const uint32_t rn = sn & FL_N;
+          uint32_t live = rn, wl = sl[rn];
+          while (wl & FW_TOMB) {  // nextNode: the first live node after next
+            live = wl & FL_N;
+            wl = sl[live];
           }
+          if (live == FL_N || x > rn) break;
+          nk = rn;
+          node = live;
+          sn = wl;
         }
-        sl[nk] = x | (sn & (0x3FFu << 11)) | FS_PRESENT | (snk & FS_ORPHAN);
+        const uint32_t snk = nk == node ? sn : sl[nk];
+        sl.set(x, (sn & FL_N) | FW_PRESENT | (snk & FW_ORPHAN));
+        if (nk == node) {
+          sl.set(node, (sn & ~FL_N) | x);
+        } else {  // copy quirk: slot nk := copy of node with next = x
+          if (!(snk & FW_ORPHAN)) {
+            for (uint32_t q = snk & FL_N; q != FL_N;) {
+              const uint32_t sq = sl[q];
+              sl.set(q, sq | FW_ORPHAN);
+              if (q == node) break;
+              q = sq & FL_N;
+            }
+          }
+          sl.set(nk, x | FW_PRESENT | (snk & FW_ORPHAN));
+          longlong2* v = vt + static_cast<uint64_t>(d) * FL_SLOTS;
+          v[nk] = v[node];
+        }
+        ++applied;
+        own += ownb;  // incrementTimestamp (src/CRDTree.elm:337-343)
       }
-      ++applied;
-      if (w & FO_OWN) ++ts;  // incrementTimestamp (src/CRDTree.elm:337-343)
     }
+    __syncthreads();
   }
-  if (lane == 0) {
-    code_out[d] = code;
-    err_out[d] = err;
-    applied_out[d] = applied;
-    tstamp[d] = ts;
-    overflow[d] = 0;
-  }
-  // hash of the visible document: walk 64 visible nodes (LDS), gather their
-  // values and timestamps with one load per lane, hash them in order
+  if (!act) return;
+  code_out[d] = code;
+  err_out[d] = err;
+  applied_out[d] = applied;
+  tstamp[d] = ts0 + own;
+  overflow[d] = 0;
+  // the visible document's hash (the oracle's dumpVisible words), its
+  // (value, timestamp) loads issued 8 entries ahead of the hash chain
   Fnv h;
   if (code == CRDTM_OK) {
-    uint32_t cur = s0;
+    const longlong2* v = vt + static_cast<uint64_t>(d) * FL_SLOTS;
+    uint32_t wc = sl[s0];
     bool more = true;
     while (more) {
-      uint32_t mine = NONE, cntv = 0;
-      while (cntv < 64) {
-        uint32_t nx = fl_ld(sl, cur) & FL_N;
-        while (nx != FL_N && (fl_ld(sl, nx) & FS_TOMB)) nx = fl_ld(sl, nx) & FL_N;
+      uint32_t sv[8];
+      uint32_t c = 0;
+      for (; c < 8; ++c) {
+        uint32_t nx = wc & FL_N, wn = sl[nx];
+        while (wn & FW_TOMB) {
+          nx = wn & FL_N;
+          wn = sl[nx];
+        }
         if (nx == FL_N) {
           more = false;
           break;
         }
-        if (lane == cntv) mine = ob + ((fl_ld(sl, nx) >> 11) & 0x3FFu);
-        ++cntv;
-        cur = nx;
+        sv[c] = nx;
+        wc = wn;
       }
-      uint32_t v = 0;
-      long long tv = 0;
-      if (mine != NONE) {
-        v = o.val[mine];
-        tv = o.ts[mine];
-      }
-      for (uint32_t k = 0; k < cntv; ++k) {
-        const uint32_t vk = __builtin_amdgcn_readlane(v, k);
-        const uint32_t tlo = __builtin_amdgcn_readlane(static_cast<uint32_t>(tv), k);
-        const uint32_t thi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<unsigned long long>(tv) >> 32), k);
-        h.put(0);
-        h.put(static_cast<long long>(vk));
-        h.put(1);
-        h.put(static_cast<long long>((static_cast<unsigned long long>(thi) << 32) | tlo));
+      longlong2 e[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k)
+        if (k < c) e[k] = v[sv[k]];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) {
+        if (k < c) {
+          h.put(0);
+          h.put(e[k].x);
+          h.put(1);
+          h.put(e[k].y);
+        }
       }
     }
   }
-  if (lane == 0) {
-    vhash[d] = h.h;
-    vwords[d] = h.n;
-  }
+  vhash[d] = h.h;
+  vwords[d] = h.n;
 }
 
 __global__ void __launch_bounds__(64) k_forest(OpsDev o, ForestArgs f, const uint64_t* sbase, const uint64_t* dbase,
                                                const uint64_t* hbase, const uint8_t* fb) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= f.n_docs || !fb[d]) return;  // served by k_forest_prep / k_forest_replay
+  if (d >= f.n_docs || !fb[d]) return;  // served by k_forest_prep / k_forest_lanes
   {
     uint32_t* hs = f.hslot + hbase[d];  // this document's hash region starts empty
     for (uint32_t p = 0, H = forest_hash_cap(f.doc_off[d + 1] - f.doc_off[d]); p < H; ++p) hs[p] = NONE;
@@ -3389,8 +3428,15 @@ int forest_apply(crdtm_ctx* c, int64_t replica_id, const OpsDev& o, const uint32
   HIP_CHECK(hipMemsetAsync(fb, 0, n_docs, s));
   uint32_t* opw = ws.alloc<uint32_t>(o.n + 1);
   uint16_t* sent = ws.alloc<uint16_t>(n_docs);
-  LAUNCH(k_forest_prep, dim3(static_cast<uint32_t>(n_docs)), dim3(64), 0, s, o, doff, f.n_docs, f.ts0, opw, sent, fb);
-  LAUNCH(k_forest_replay, dim3(static_cast<uint32_t>(n_docs)), dim3(64), 0, s, o, doff, f.n_docs, f.ts0, opw, sent, fb,
+  longlong2* vt = ws.alloc<longlong2>(n_docs * FL_SLOTS);
+  LAUNCH(k_forest_prep, dim3(static_cast<uint32_t>(n_docs)), dim3(FPREP_THREADS), 0, s, o, doff, f.n_docs, f.ts0, opw,
+         sent, fb, vt);
+  // one document per wave measured fastest (1, 2, 4, 8 per wave: 2.70, 2.95,
+  // 3.80, 5.70 ms on 12.5k config-5 documents): lanes of one wave diverge on
+  // every walk, and one document per wave gives the most waves to hide latency
+  constexpr uint32_t DPW = 1;
+  LAUNCH(k_forest_lanes<DPW>, dim3(static_cast<uint32_t>((n_docs + DPW - 1) / DPW)), dim3(64),
+         DPW * (FLANE_REGION * sizeof(uint16_t) + 64 * sizeof(uint32_t)), s, doff, f.n_docs, f.ts0, opw, sent, fb, vt,
          f.code, f.err, f.applied, f.vhash, f.vwords, f.tstamp, f.overflow);
   LAUNCH(k_forest, dim3(static_cast<uint32_t>((n_docs + 63) / 64)), dim3(64), 0, s, o, f, dsb, ddb, dhb, fb);
   std::vector<uint32_t> e(n_docs), ov(n_docs);
@@ -3421,7 +3467,7 @@ uint64_t forest_ws_bytes(const uint32_t* doc_off_host, uint64_t n_docs, uint64_t
     D += forest_dict_cap(nops);
     H += forest_hash_cap(nops);
   }
-  return S * 29 + D * 20 + H * 16 + n_docs * 96 + n_ops * 32 + n_path * 8 + (64ULL << 20);
+  return S * 29 + D * 20 + H * 16 + n_docs * (96 + 16 * FL_SLOTS) + n_ops * 32 + n_path * 8 + (64ULL << 20);
 }
 
 }  // namespace crdtm

@@ -13,7 +13,9 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/crdtm.h"
@@ -237,17 +239,52 @@ extern "C" int crdtm_synth(const crdtm_synth_params* p, crdtm_ops** out) {
   try {
     Out o;
     const uint64_t docs = p->n_docs ? p->n_docs : 1;
-    o.kind.reserve(p->n_ops * docs);
-    o.ts.reserve(p->n_ops * docs);
-    o.val.reserve(p->n_ops * docs);
-    o.off.reserve(p->n_ops * docs + 1);
-    o.tree.reserve(p->n_ops * docs);
-    for (uint64_t d = 0; d < docs; ++d) {
-      const uint64_t id = p->doc_base + d;
-      const uint64_t seed = p->seed ^ (0xD1B54A32D192ED03ULL * (id + 1));
-      const bool single = docs == 1 && p->doc_base == 0;
-      if (p->max_children > 0) genDeep(*p, single ? p->seed : seed, static_cast<uint32_t>(id), o);
-      else genTyping(*p, single ? p->seed : seed, static_cast<uint32_t>(id), o);
+    auto gen = [p, docs](uint64_t d0, uint64_t d1, Out& out) {
+      out.kind.reserve(p->n_ops * (d1 - d0));
+      out.ts.reserve(p->n_ops * (d1 - d0));
+      out.val.reserve(p->n_ops * (d1 - d0));
+      out.off.reserve(p->n_ops * (d1 - d0) + 1);
+      out.tree.reserve(p->n_ops * (d1 - d0));
+      for (uint64_t d = d0; d < d1; ++d) {
+        const uint64_t id = p->doc_base + d;
+        const uint64_t seed = p->seed ^ (0xD1B54A32D192ED03ULL * (id + 1));
+        const bool single = docs == 1 && p->doc_base == 0;
+        if (p->max_children > 0) genDeep(*p, single ? p->seed : seed, static_cast<uint32_t>(id), out);
+        else genTyping(*p, single ? p->seed : seed, static_cast<uint32_t>(id), out);
+      }
+    };
+    // documents are independent streams (their own seeds): many documents are
+    // generated on up to 16 threads and concatenated in document order
+    const uint64_t nt = std::min<uint64_t>({16, std::max(1u, std::thread::hardware_concurrency()),
+                                             docs * p->n_ops >= (1u << 20) ? docs : 1});
+    if (nt <= 1) {
+      gen(0, docs, o);
+    } else {
+      std::vector<Out> part(nt);
+      std::vector<std::thread> th;
+      std::vector<int> failed(nt, 0);
+      for (uint64_t t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+          try {
+            gen(docs * t / nt, docs * (t + 1) / nt, part[t]);
+          } catch (const std::bad_alloc&) {
+            failed[t] = 1;
+          }
+        });
+      for (auto& x : th) x.join();
+      for (int f : failed)
+        if (f) throw std::bad_alloc();
+      for (auto& q : part) {
+        const uint32_t base = static_cast<uint32_t>(o.path.size());
+        o.kind.insert(o.kind.end(), q.kind.begin(), q.kind.end());
+        o.ts.insert(o.ts.end(), q.ts.begin(), q.ts.end());
+        o.val.insert(o.val.end(), q.val.begin(), q.val.end());
+        o.tree.insert(o.tree.end(), q.tree.begin(), q.tree.end());
+        o.path.insert(o.path.end(), q.path.begin(), q.path.end());
+        for (size_t i = 1; i < q.off.size(); ++i) o.off.push_back(base + q.off[i]);
+        Out().kind.swap(q.kind);
+        q = Out();
+      }
     }
     auto* r = static_cast<crdtm_ops*>(std::calloc(1, sizeof(crdtm_ops)));
     if (!r) return CRDTM_E_NOMEM;

@@ -1,5 +1,9 @@
 """Multi-process (world_size 2, gloo on CPU) checks of the document sharding
-and op-log exchange used by bench.py --workload trees (RCCL on the GPU node)."""
+and op-log exchange used by bench.py --workload trees (RCCL on the GPU node):
+the persistent padded all-gather (shard.Exchange), the assembly of each
+rank's documents, and the merge of the assembled documents on the oracle
+(orc_forest_apply, oracle/crdtree_oracle.cpp) against the single-process
+stream's documents."""
 import os
 import socket
 import sys
@@ -17,8 +21,25 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _oracle_forest(ops, n_docs, per_doc):
+    import numpy as np
+    from oracle.oracle import _ptr, lib as olib
+    n = n_docs * per_doc
+    a = dict(kind=np.ascontiguousarray(ops["kind"][:n], np.uint8), ts=np.ascontiguousarray(ops["ts"][:n], np.int64),
+             path=np.ascontiguousarray(ops["path"][:n], np.int64), val=np.ascontiguousarray(ops["val"][:n], np.uint32))
+    off = np.arange(n_docs + 1, dtype=np.uint32) * per_doc
+    path_off = np.arange(n + 1, dtype=np.uint32)
+    out = dict(code=np.zeros(n_docs, np.int32), err=np.zeros(n_docs, np.int64), hash=np.zeros(n_docs, np.uint64),
+               words=np.zeros(n_docs, np.uint64), ts=np.zeros(n_docs, np.int64))
+    olib().orc_forest_apply(n_docs, _ptr(off), 0, _ptr(a["kind"]), _ptr(a["ts"]), _ptr(path_off), _ptr(a["path"]),
+                            _ptr(a["val"]), _ptr(out["code"]), _ptr(out["err"]), _ptr(out["hash"]),
+                            _ptr(out["words"]), _ptr(out["ts"]))
+    return out
+
+
 def _worker(rank, world, port, n_docs, per_doc, q):
     sys.path.insert(0, os.path.join(ROOT, "crdt-graph_amd"))
+    sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
     from crdtm import _native as N
@@ -28,7 +49,10 @@ def _worker(rank, world, port, n_docs, per_doc, q):
     s = N.synth(n_ops=per_doc, n_docs=n_docs, replicas=8, window=16, p_delete=0.2, seed=0xC0FFEE05)
     doc_off = np.arange(n_docs + 1, dtype=np.uint32) * per_doc
     local = torch.from_numpy(shard.local_log(s, doc_off, rank, world, replicas=8))
-    allrec = shard.all_gather_records(local)
+    ex = shard.Exchange(local)
+    for _ in range(2):  # the buffers are reused step after step
+        allrec = ex.gather()
+    assert allrec.shape[0] == world * ex.block and ex.counts[rank] == local.shape[0]
     ops, my_off, keep = shard.assemble(allrec, rank, world, n_docs, per_doc)
     n_kept = int(keep.sum())
     # expected: the owned documents' streams, sliced directly from the generator output
@@ -39,7 +63,11 @@ def _worker(rank, world, port, n_docs, per_doc, q):
           and np.array_equal(ops["path"].numpy()[:m], s["path"][idx])
           and np.array_equal(ops["val"].numpy()[:m].astype(np.uint32), s["val"][idx]) and n_kept == m
           and int(my_off[-1]) == m)
-    q.put((rank, bool(ok), int(local.shape[0]), int(allrec.shape[0])))
+    # the assembled documents merge exactly as the generator's own streams do
+    got = _oracle_forest({k: v.numpy() for k, v in ops.items()}, len(mine), per_doc)
+    want = _oracle_forest({k: s[k][idx] for k in ("kind", "ts", "path", "val")}, len(mine), per_doc)
+    merged = all(np.array_equal(got[k], want[k]) for k in got) and bool(np.all(got["code"] == 0))
+    q.put((rank, bool(ok and merged), int(local.shape[0]), int(n_kept)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -58,6 +86,6 @@ def test_oplog_exchange_world2():
         assert p.exitcode == 0
     res.sort()
     assert all(ok for _, ok, _, _ in res), res
-    # every op travels in exactly one rank's log; everyone receives all of them
+    # every op travels in exactly one rank's log; every op is kept by exactly one rank
     assert sum(r[2] for r in res) == n_docs * per_doc
-    assert all(r[3] == n_docs * per_doc for r in res)
+    assert sum(r[3] for r in res) == n_docs * per_doc
