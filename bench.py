@@ -45,6 +45,8 @@ WORKLOADS = {
 CPU_SAMPLE = {"flat10m": 100_000, "deep10m": 500_000, "trees": 2_000_000, "cfg2": 100_000, "cfg1": 10_000}
 # 100k documents x 1k ops (80/20), 8 replicas, sharded by
 # document id; 12.5k documents per GPU (100k at 8 GPUs), weak scaling.
+# Incremental merges: a 10M-node document, then successive 10k-op batches of the same stream
+INCR = dict(base=10_000_000, batch=10_000, batches=100)
 TREES = dict(per_doc=1000, docs_per_gpu=12_500, replicas=8, window=16, p_delete=0.2, seed=0xC0FFEE05)
 
 
@@ -194,7 +196,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="flat10m", choices=sorted(WORKLOADS) + ["trees"])
+    ap.add_argument("--workload", default="flat10m", choices=sorted(WORKLOADS) + ["trees", "incr"])
     ap.add_argument("--docs-per-gpu", type=int, default=0, help="trees workload: override documents per GPU")
     ap.add_argument("--n-ops", type=int, default=0, help="override the batch size (parity/debug only)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="oracle sample ops (0 = skip)")
@@ -220,8 +222,8 @@ def main():
 
     from crdtm import _native as N
     L = N.lib()
-    if args.workload == "trees":
-        line = run_trees(args, rank, world, local_rank)
+    if args.workload in ("trees", "incr"):
+        line = (run_trees if args.workload == "trees" else run_incr)(args, rank, world, local_rank)
         if rank == 0:
             print(json.dumps(line), flush=True)
         if world > 1:
@@ -273,6 +275,7 @@ def main():
         elapsed = float(t.item())
     path_taken = res.path_taken
     guard = res.guard
+    serial = {"ops": int(res.serial_ops), "dicts": int(res.serial_dicts), "largest": int(res.serial_max)}
 
     # Per-kernel device time (HIP events recorded on the launch stream) over a
     # few extra, untimed steps.
@@ -295,6 +298,12 @@ def main():
 
     ms_step = elapsed / args.steps * 1e3
     value = world * n * args.steps / elapsed
+    # SURVEY.md 8d (config 2): how much of the merge ran as in-order replay, and its device-time share
+    serial_ms = sum(v for nm, v in per_step.items() if nm.startswith(("k_pdr_small", "k_pdr_big", "k_pdr_huge",
+                                                                        "k_replay<", "k_replay")))
+    serial_ms -= per_step.get("k_replay_index", 0.0)
+    serial["time_share"] = serial_ms / max(1e-9, sum(per_step.values()))
+    serial["fraction_of_ops"] = serial["ops"] / n
     line = {
         "metric": "merged ops/sec (whole node) on 10M-op batch",
         "value": value,
@@ -311,7 +320,7 @@ def main():
         "config": {"workload": f"{args.workload}: {n} ops per GPU, one document per GPU",
                    "replicas": spec.get("replicas"), "window": spec.get("window", 0),
                    "path": {1: "closed-form", 2: "replay", 3: "per-dict replay"}.get(path_taken, "?"),
-                   "guard": guard,
+                   "guard": guard, "serial_replay": serial,
                    "parallelism": f"documents sharded by id over {world} GPU(s)"},
         "roofline": roofline(args.workload, per_step, launches, B_alg, ms_step, ps),
     }
@@ -344,6 +353,115 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def run_incr(args, rank, world, local_rank):
+    """Incremental merges (src/CRDTree.elm:265-269 on a tree that holds state):
+    a 10M-node flat document (config 3's stream, merged untimed), then one
+    step = 100 successive 10k-op batches of the same stream applied to it.
+    Each step is bracketed by its own synchronisations; the base is rebuilt
+    (reset + merge, untimed) between steps so every step sees the same
+    document. Single document per rank (replicas only)."""
+    import torch
+    from crdtm import _native as N
+    L = N.lib()
+    base, bsz, nb = INCR["base"], INCR["batch"], INCR["batches"]
+    if args.n_ops:
+        base = args.n_ops
+    spec = dict(WORKLOADS["flat10m"])
+    spec["n_ops"] = base + bsz * nb
+    spec["seed"] = spec["seed"] + rank
+    s = N.synth(**spec)
+    n = len(s["kind"])
+    assert n == base + bsz * nb and int(s["path_off"][n]) == n  # flat: one path element per op
+    dev = torch.device("cuda", local_rank)
+    tens = {k: torch.from_numpy(s[k]).to(dev) for k in ("kind", "ts", "path", "val")}
+    offs = torch.arange(max(base, bsz) + 1, dtype=torch.int32, device=dev)  # flat batches: path_off = 0..m
+
+    def ops_at(a, m):
+        return N.Ops(m, m, tens["kind"].data_ptr() + a, tens["ts"].data_ptr() + 8 * a, offs.data_ptr(),
+                     tens["path"].data_ptr() + 8 * a, tens["val"].data_ptr() + 4 * a, None)
+
+    base_ops = ops_at(0, base)
+    batches = [ops_at(base + j * bsz, bsz) for j in range(nb)]
+    stream = torch.cuda.current_stream()
+    ctx = C.c_void_p()
+    N.check(L.crdtm_ctx_create(local_rank, C.c_void_p(stream.cuda_stream), C.byref(ctx)), "ctx")
+    tree = C.c_void_p()
+    N.check(L.crdtm_tree_create(ctx, 0, C.byref(tree)), "tree")
+    res = N.Result()
+    acct = {"remerge": 0, "paths": {}}
+
+    def apply(o):
+        N.check(L.crdtm_apply(tree, C.byref(o), 1, 1, None, C.byref(res)), "apply")
+        if res.code != 0:
+            raise RuntimeError(f"merge failed: code {res.code} at op {res.err_index}")
+
+    def rebuild():
+        N.check(L.crdtm_tree_reset(tree, 0), "reset")
+        apply(base_ops)
+
+    def step():
+        for o in batches:
+            apply(o)
+            acct["remerge"] += bool(res.flags & N.FLAG_REMERGE)
+            acct["paths"][res.path_taken] = acct["paths"].get(res.path_taken, 0) + 1
+
+    for _ in range(args.warmup):
+        rebuild()
+        step()
+    elapsed = 0.0
+    for _ in range(args.steps):
+        rebuild()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        elapsed += time.perf_counter() - t0
+    # per-kernel device time of one incremental batch (the last one of a step)
+    rebuild()
+    for o in batches[:-1]:
+        apply(o)
+    L.crdtm_ctx_profile(ctx, 1)
+    apply(batches[-1])
+    names = C.create_string_buffer(1 << 16)
+    ms = (C.c_double * 512)()
+    k = L.crdtm_ctx_phase_times(ctx, names, len(names), ms, 512)
+    labels = names.raw.split(b"\0")
+    L.crdtm_ctx_profile(ctx, 0)
+    per_k, launches = {}, {}
+    for j in range(min(k, 512)):
+        nm = labels[j].decode()
+        per_k[nm] = per_k.get(nm, 0.0) + ms[j]
+        launches[nm] = launches.get(nm, 0) + 1
+    ms_step = elapsed / args.steps * 1e3
+    B_alg = 57 * bsz  # SURVEY.md 8d: flat Add = 57 B; one batch
+    line = {
+        "metric": "merged ops/sec (whole node) on 10M-op batch",
+        "value": world * bsz * nb * args.steps / elapsed, "unit": "ops/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int64", "data": "synthetic (deterministic generator, SURVEY.md §8d)",
+        "config": {"workload": f"incr: {nb} successive {bsz}-op batches into a {base}-op flat document "
+                               f"(config 3 stream), per GPU",
+                   "replicas": spec["replicas"], "window": spec["window"],
+                   "batches_remerged": acct["remerge"], "batches": nb * (args.steps + args.warmup),
+                   "paths": {({1: "closed-form", 2: "replay", 3: "per-dict replay"}).get(p_, "?"): c_
+                             for p_, c_ in acct["paths"].items()},
+                   "ms_per_batch": ms_step / nb,
+                   "parallelism": f"one document per GPU ({world} GPU(s)), replicas only"},
+        "roofline": roofline("incr", per_k, launches, B_alg, ms_step / nb, 1),
+    }
+    line["roofline"]["note"] = ("achieved = the batch's own algorithmic bytes / time per batch; the re-merge "
+                                "re-reads the whole log, so this is far below the per-kernel fractions")
+    if rank == 0 and world == 1:
+        m = args.cpu_sample if args.cpu_sample >= 0 else CPU_SAMPLE["flat10m"]
+        if m > 0:
+            line["cpu_baseline"] = cpu_line(cpu_baseline(s, min(m, n)),
+                                            f"first {min(m, n)} ops of the same stream, one op at a time (a CPU "
+                                            f"replica merges incrementally at this per-op cost or worse)")
+    L.crdtm_tree_destroy(tree)
+    L.crdtm_ctx_destroy(ctx)
+    return line
 
 
 def run_trees(args, rank, world, local_rank, cpu=True):

@@ -17,6 +17,7 @@ CRDTM_OK = 0
 PATH_CLOSED_FORM = 1
 PATH_REPLAY = 2
 PATH_DICT_REPLAY = 3
+FLAG_REMERGE = 1  # non-fresh tree merged as init ++ log ++ batch on the parallel paths
 REF_NONE = 2 ** 64 - 1
 REF_ROOT = 2 ** 64 - 2
 REL_PARENT, REL_NEXT, REL_PREV, REL_HEAD = 0, 1, 2, 3
@@ -32,7 +33,8 @@ class Ops(C.Structure):
 class Result(C.Structure):
     _fields_ = [("code", C.c_int32), ("path_taken", C.c_int32), ("err_index", C.c_int64),
                 ("n_applied", C.c_uint64), ("n_already", C.c_uint64), ("timestamp", C.c_int64),
-                ("n_slots", C.c_uint64), ("guard", C.c_uint32), ("reserved", C.c_uint32)]
+                ("n_slots", C.c_uint64), ("guard", C.c_uint32), ("flags", C.c_uint32),
+                ("serial_ops", C.c_uint64), ("serial_dicts", C.c_uint64), ("serial_max", C.c_uint64)]
 
 
 class SynthParams(C.Structure):

@@ -359,8 +359,10 @@ int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_b
   const bool fresh = t->n_slots == 1 && t->log_n == 0;
   const int64_t ts_before = t->timestamp;
   int r = CRDTM_OK;
+  // an incremental merge may run over log ++ batch (merge.hip apply_batch)
+  const uint64_t n_need = fresh ? n : n + t->log_n, np_need = fresh ? np : np + t->log_npath;
   for (int attempt = 0; attempt < 4; ++attempt) {
-    r = ensure_arena(c, arena_need(n, np, t) << attempt);
+    r = ensure_arena(c, arena_need(n_need, np_need, t) << attempt);
     if (r) return r;
     c->ws.reset();
     try {

@@ -127,6 +127,12 @@ struct crdtm_tree {
   uint64_t last_begin = 0, last_end = 0;
   int last_is_batch = 1;
   uint64_t version = 0;              // bumped by every state change (apply, reset)
+  // incremental re-merge (merge.hip apply_batch): while set, the engine runs
+  // the fresh-tree paths over log ++ batch; own-replica Adds of the log are
+  // not counted again (own_bias), and no path may write the state before its
+  // last check (no speculation, no sequential replay: R_INCR instead)
+  bool remerge = false;
+  int64_t own_bias = 0;
   std::shared_ptr<void> trav;        // traversal cache (api.hip), valid for `version`
 };
 
@@ -178,6 +184,10 @@ struct PdrIn {
   const uint32_t* dtime;   // node -> first Delete that tombstoned it
   uint32_t maxlen;
 };
+
+// internal: a path that cannot run inside an incremental re-merge asks the
+// caller to replay the batch incrementally on the untouched state instead
+constexpr int R_INCR = 1 << 20;
 
 // merge.hip
 int sync_read(crdtm_ctx* c);

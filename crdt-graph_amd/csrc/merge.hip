@@ -14,6 +14,8 @@
 //    including the findInsertion copy quirk, with an undo log for atomicity.
 // DESIGN.md derives the closed form and its guard.
 
+#include <cstring>
+
 #include "engine.h"
 #include "listrank.h"
 #include "scan.h"
@@ -2707,6 +2709,7 @@ int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& ws) {
 }
 
 static int run_replay(crdtm_tree* t, const OpsDev& o, uint8_t* st, crdtm_result* res, uint32_t guard) {
+  if (t->remerge) return R_INCR;  // replay the batch alone on the untouched state instead
   crdtm_ctx* c = t->ctx;
   hipStream_t s = c->stream;
   uint64_t nadd = o.n;  // upper bound on new nodes
@@ -2775,6 +2778,9 @@ static int run_replay(crdtm_tree* t, const OpsDev& o, uint8_t* st, crdtm_result*
     }
     res->n_applied = h.n_applied;
     res->n_already = h.n_already;
+    res->serial_ops = o.n;  // the whole batch in order on one lane
+    res->serial_dicts = 1;
+    res->serial_max = o.n;
     const long long new_ts = h.replay_timestamp;
     const uint32_t new_slots = h.replay_slots, new_dicts = h.replay_dicts;
     if ((r = post_pass(t, o, st, ws))) return r;
@@ -2994,8 +3000,9 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     t->doc_valid = true;
     return CRDTM_OK;
   };
-  // ---- speculation: every op applies ----
-  if (Q >= n) {
+  // ---- speculation: every op applies (writes the state before the check,
+  // so never inside an incremental re-merge) ----
+  if (Q >= n && !t->remerge) {
     if ((r = grow_for(n, n))) return r;
     if ((r = flat_order_commit(t, o, ix, Q, maxr, st, n, true, fb))) return r;
     if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, nullptr, n, NONE, st_out);
@@ -3008,7 +3015,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
       own += h.fl_part[32 * k + 2];
       slow += h.fl_part[32 * k + 3];
     }
-    const long long new_ts = t->timestamp + own;
+    const long long new_ts = t->timestamp + own - t->own_bias;
     const bool every = h.err_index == NONE && slow == 0 && present == keys && keys == n;
     if (every && replica_of(new_ts) == replica_of(t->timestamp)) {
       if (h.run_fail && (r = flat_order_fallback(t, Q, n, fb))) return r;
@@ -3033,7 +3040,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   }
   const DevResult h1 = *c->hres;
   uint32_t guard = 0;
-  const long long new_ts = t->timestamp + h1.own_ok_adds;
+  const long long new_ts = t->timestamp + h1.own_ok_adds - t->own_bias;
   if (replica_of(new_ts) != replica_of(t->timestamp)) guard |= G_REPLICA_DRIFT;
   res->guard = guard;
   if (guard || h1.err_index != NONE)  // no commit: leave the replica table clean
@@ -3066,7 +3073,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   return finish(K, h1.n_applied, h1.n_already, all_applied ? o.n_path : c->hres->log_npath, new_ts);
 }
 
-int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res) {
+static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res) {
   crdtm_ctx* c = t->ctx;
   hipStream_t s = c->stream;
   Arena& ws = c->ws;  // reset by the caller (inputs may live in it)
@@ -3187,7 +3194,7 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   DevResult h1 = *c->hres;
   uint32_t guard = h1.guard;
   const long long id0 = replica_of(t->timestamp);
-  const long long new_ts = t->timestamp + h1.own_ok_adds;
+  const long long new_ts = t->timestamp + h1.own_ok_adds - t->own_bias;
   if (replica_of(new_ts) != id0) guard |= G_REPLICA_DRIFT;
   res->guard = guard;
   if (guard == G_DEL_BEFORE_ADD) {
@@ -3330,6 +3337,167 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   t->timestamp = new_ts;
   t->doc_n = h2.n_live_kept;  // visible nodes = kept live nodes
   t->doc_valid = true;
+  return CRDTM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Incremental merges: apply into a tree that already holds state
+// (src/CRDTree.elm:265-269 on any tree; the steady state of a replica that
+// applies remote batches). The state is a pure function of its log: every
+// logged op was Applied, in log order, and every op that was not logged
+// (AlreadyApplied) changed nothing. So `apply batch state` equals
+// `apply (log ++ batch) init` with the log's ops all Applied again, and that
+// runs on the parallel fresh-tree paths (closed form, per-dict replay)
+// instead of the one-lane replay over a rebuilt slot index. The outputs
+// that are not a function of the log are carried over: the timestamp (the
+// log's own-replica Adds are not counted again; AlreadyApplied ones never
+// reached the log), lastOperation (the log suffix) and the statuses (the
+// batch part). Nothing writes the state before the batch's last check (no
+// flat speculation), so an error or a path that needs the sequential replay
+// (R_INCR) leaves the state untouched and the batch is replayed alone.
+// Cost: O(log + batch) parallel work per call, against O(batch) serial
+// dependent steps plus an O(state) index rebuild for the replay.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(BLOCK) k_cat_ops(OpsDev lg, OpsDev b, uint32_t L, uint32_t LP, uint8_t* kind,
+                                                   long long* ts, uint32_t* off, uint32_t* val) {
+  GRID_STRIDE(i, L + b.n + 1) {
+    if (i < L) {
+      kind[i] = lg.kind[i];
+      ts[i] = lg.ts[i];
+      val[i] = lg.val[i];
+      off[i] = lg.off[i];
+    } else {
+      const uint32_t j = i - L;
+      if (j < b.n) {
+        kind[i] = b.kind[j];
+        ts[i] = b.ts[j];
+        val[i] = b.val[j];
+      }
+      off[i] = LP + b.off[j];
+    }
+  }
+}
+
+// own-replica Adds of the log (incrementTimestamp, src/CRDTree.elm:337-343)
+__global__ void __launch_bounds__(BLOCK) k_own_log(const uint8_t* kind, const long long* ts, uint32_t L, long long rid,
+                                                   unsigned long long* out) {
+  uint32_t c = 0;
+  GRID_STRIDE(i, L) c += (kind[i] == CRDTM_ADD && replica_of(ts[i]) == rid) ? 1u : 0u;
+  c = block_sum(c);
+  if (threadIdx.x == 0 && c) atomicAdd(out, static_cast<unsigned long long>(c));
+}
+
+static bool remerge_wanted(const crdtm_tree* t, uint32_t n) {
+  if (t->log_n + static_cast<uint64_t>(n) >= 0x7FFFFFF0ULL || t->max_depth > MAXLV_BUCKET) return false;
+  const char* e = getenv("CRDTM_INCREMENTAL");
+  if (e && !strcmp(e, "replay")) return false;
+  if (e && !strcmp(e, "remerge")) return true;
+  // parallel work over log + batch (~0.1-1 ns per op) against ~5 us of
+  // dependent device accesses per replayed op
+  return t->log_n <= 4096ULL * n;
+}
+
+int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res) {
+  const bool fresh = t->n_slots == 1 && t->log_n == 0;
+  if (fresh || o.n == 0 || !remerge_wanted(t, o.n)) return apply_core(t, o, st_out, res);
+  crdtm_ctx* c = t->ctx;
+  hipStream_t s = c->stream;
+  Arena& ws = c->ws;
+  const size_t mark0 = ws.used;
+  const uint32_t L = static_cast<uint32_t>(t->log_n);
+  const uint64_t LP = t->log_npath;
+  OpsDev lg;
+  lg.n = L;
+  lg.kind = t->d.l_kind;
+  lg.ts = t->d.l_ts;
+  lg.off = t->d.l_off;
+  lg.val = t->d.l_val;
+  OpsDev m;
+  m.n = L + o.n;
+  m.n_path = LP + o.n_path;
+  auto* kind = ws.alloc<uint8_t>(m.n + 1);
+  auto* ts = ws.alloc<long long>(m.n + 1);
+  auto* off = ws.alloc<uint32_t>(m.n + 1);
+  auto* path = ws.alloc<long long>(m.n_path + 1);
+  auto* val = ws.alloc<uint32_t>(m.n + 1);
+  auto* own = ws.alloc<unsigned long long>(1);
+  uint8_t* st2 = st_out ? ws.alloc<uint8_t>(m.n + 1) : nullptr;
+  LAUNCH(k_cat_ops, dim3(grid_for(m.n + 1)), dim3(BLOCK), 0, s, lg, o, L, static_cast<uint32_t>(LP), kind, ts, off,
+         val);
+  if (LP) HIP_CHECK(hipMemcpyAsync(path, t->d.l_path, LP * 8, hipMemcpyDeviceToDevice, s));
+  if (o.n_path) HIP_CHECK(hipMemcpyAsync(path + LP, o.path, o.n_path * 8, hipMemcpyDeviceToDevice, s));
+  HIP_CHECK(hipMemsetAsync(own, 0, sizeof(*own), s));
+  LAUNCH(k_own_log, dim3(grid_for(L, BLOCK, 1024)), dim3(BLOCK), 0, s, kind, ts, L, replica_of(t->timestamp), own);
+  unsigned long long own_h = 0;
+  HIP_CHECK(hipMemcpyAsync(&own_h, own, sizeof(own_h), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  m.kind = kind;
+  m.ts = ts;
+  m.off = off;
+  m.path = path;
+  m.val = val;
+  // the host-side state the fresh paths overwrite; restored unless the batch commits
+  struct Saved {
+    uint64_t n_slots, n_dicts, log_n, log_npath, doc_n, last_begin, last_end;
+    bool doc_valid;
+    uint32_t max_depth;
+    int64_t timestamp;
+  } sv{t->n_slots, t->n_dicts, t->log_n, t->log_npath, t->doc_n, t->last_begin, t->last_end,
+       t->doc_valid, t->max_depth, t->timestamp};
+  auto restore = [&]() {
+    t->n_slots = sv.n_slots;
+    t->n_dicts = sv.n_dicts;
+    t->log_n = sv.log_n;
+    t->log_npath = sv.log_npath;
+    t->doc_n = sv.doc_n;
+    t->last_begin = sv.last_begin;
+    t->last_end = sv.last_end;
+    t->doc_valid = sv.doc_valid;
+    t->max_depth = sv.max_depth;
+    t->timestamp = sv.timestamp;
+    t->remerge = false;
+    t->own_bias = 0;
+  };
+  t->n_slots = 1;
+  t->n_dicts = 1;
+  t->log_n = 0;
+  t->log_npath = 0;
+  t->remerge = true;
+  t->own_bias = static_cast<int64_t>(own_h);
+  int r;
+  try {
+    r = apply_core(t, m, st2, res);
+  } catch (...) {
+    restore();
+    throw;
+  }
+  t->remerge = false;
+  t->own_bias = 0;
+  if (r == R_INCR || (r == CRDTM_OK && res->code != CRDTM_OK && res->err_index < static_cast<int64_t>(L))) {
+    // a sequential path (or, defensively, a log op that did not re-apply):
+    // the state is untouched; replay the batch alone on it
+    restore();
+    ws.used = mark0;
+    std::memset(res, 0, sizeof(*res));
+    res->err_index = -1;
+    return apply_core(t, o, st_out, res);
+  }
+  if (r != CRDTM_OK) return r;
+  res->flags |= CRDTM_FLAG_REMERGE;
+  if (res->code != CRDTM_OK) {
+    restore();
+    res->err_index -= L;
+  } else {
+    res->n_applied -= L;
+    t->last_begin = sv.log_n;
+    t->last_end = t->log_n;
+    if (t->log_n != sv.log_n + res->n_applied) {
+      std::fprintf(stderr, "crdtm: incremental re-merge log mismatch\n");
+      return CRDTM_E_HIP;
+    }
+    if (t->max_depth < sv.max_depth) t->max_depth = sv.max_depth;
+  }
+  if (st_out) HIP_CHECK(hipMemcpyAsync(st_out, st2 + L, o.n, hipMemcpyDeviceToDevice, s));
   return CRDTM_OK;
 }
 

@@ -425,6 +425,7 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_tier(PdrCtx p, uint32_t i0, uint3
     const uint32_t t = slots <= PDR_SMALL ? 0u : (slots <= big_cap ? 1u : 2u);
     tt.list[t][atomicAdd(&tt.count[t], 1u)] = I;
     if (t == 1) atomicMax(&tt.count[3], slots);
+    if (I <= n) atomicMax(&tt.count[4], p.rbase[I + 1] - p.rbase[I]);  // ops replayed by this dict's wave
   }
 }
 
@@ -740,9 +741,9 @@ static int pdr_run_tiers(crdtm_ctx* c, const PdrCtx& p, uint32_t i0, uint32_t i1
                          const PdrTiers& tt, uint32_t big_cap, uint32_t* hcount) {
   hipStream_t s = c->stream;
   if (i1 <= i0) return CRDTM_OK;
-  HIP_CHECK(hipMemsetAsync(tt.count, 0, 4 * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(tt.count, 0, 5 * sizeof(uint32_t), s));
   LAUNCH(k_pdr_tier, dim3(grid_for(i1 - i0)), dim3(BLOCK), 0, s, p, i0, i1, big_cap, tt);
-  HIP_CHECK(hipMemcpyAsync(hcount, tt.count, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(hcount, tt.count, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
   const uint32_t* h = hcount;
   if (h[0]) {
@@ -791,7 +792,7 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   const size_t arena_mark = ws.used;
   int r;
   const uint32_t big_cap = pdr_big_cap(c->device);
-  uint32_t hcount[4];
+  uint32_t hcount[5];
 
   PdrCtx p;
   p.o = o;
@@ -852,19 +853,22 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   HIP_CHECK(hipMemsetAsync(p.ilog, 0xFF, ICAP * sizeof(uint32_t), s));
   PdrTiers tt;
   for (int k = 0; k < 3; ++k) tt.list[k] = ws.alloc<uint32_t>(ICAP);
-  tt.count = ws.alloc<uint32_t>(4);
+  tt.count = ws.alloc<uint32_t>(5);
   HIP_CHECK(hipMemsetAsync(p.inst, 0xFF, static_cast<size_t>(SCAP) * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(p.ch, 0xFF, static_cast<size_t>(SCAP) * sizeof(uint32_t), s));
 
   // ---- P2 + P3 ----
   if ((r = pdr_run_tiers(c, p, 0, n + 1, true, st, tt, big_cap, hcount))) return r;
+  res->serial_dicts = static_cast<uint64_t>(hcount[0]) + hcount[1] + hcount[2];
+  res->serial_ops = n;  // every op, in order within its dict
+  res->serial_max = hcount[4];
   LAUNCH(k_pdr_stats_reset, dim3(1), dim3(1), 0, s, dr);
   LAUNCH(k_pdr_conflict, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, n, in.tag, in.cur, in.addpar, in.dtime,
          p.tcopy, dr);
   LAUNCH(k_pdr_stats, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, o, st, t->timestamp, dr);
   if ((r = sync_read(c))) return r;
   const DevResult h1 = *c->hres;
-  const long long new_ts = t->timestamp + h1.own_ok_adds;
+  const long long new_ts = t->timestamp + h1.own_ok_adds - t->own_bias;
   if (h1.pdr_conflict || replica_of(new_ts) != replica_of(t->timestamp)) {
     ws.used = arena_mark;
     return CRDTM_OK;

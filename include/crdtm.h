@@ -74,8 +74,17 @@ typedef struct crdtm_result {
   int64_t timestamp;  /* tree timestamp after the call */
   uint64_t n_slots;   /* slots held by the device state (empty children dicts are implicit) */
   uint32_t guard;     /* bit0 ts collision, bit1 delete-before-add in a dict, bit2 replica-id drift, bit3 non-fresh tree */
-  uint32_t reserved;
+  uint32_t flags;     /* CRDTM_FLAG_* */
+  /* serial-work accounting: ops and dicts that went through an
+   * exact in-order replay (one wave per dict, or one lane for the whole batch),
+   * and the op count of the largest such replay (the merge's serial critical path) */
+  uint64_t serial_ops;
+  uint64_t serial_dicts;
+  uint64_t serial_max;
 } crdtm_result;
+
+/* crdtm_result.flags */
+#define CRDTM_FLAG_REMERGE 1 /* non-fresh tree: merged as init ++ log ++ batch on the parallel paths */
 
 typedef struct crdtm_ctx crdtm_ctx;   /* device + stream + workspace */
 typedef struct crdtm_tree crdtm_tree; /* one replica's CRDTree state, resident in HBM */

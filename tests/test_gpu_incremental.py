@@ -1,0 +1,92 @@
+"""GPU parity of incremental merges: successive applies into a tree that
+already holds state (src/CRDTree.elm:265-269 on a non-fresh tree — a replica
+applying remote batches), chained against `orc_apply` on one oracle tree.
+
+Both incremental paths are pinned: the re-merge of log ++ batch on the
+parallel fresh-tree paths (merge.hip apply_batch, CRDTM_FLAG_REMERGE) and the
+one-lane sequential replay on the existing state (CRDTM_INCREMENTAL=replay).
+Every step compares the dict structure, the visible document, timestamp,
+replicas, lastOperation and the applied count; a failing batch in the middle
+must leave everything unchanged (transactional, src/CRDTree.elm:224-232).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from crdtm import _native as N  # noqa: E402
+from crdtm.tree import CRDTree  # noqa: E402
+from parity_util import (engine_log, engine_summary, oracle_apply_arrays, oracle_log, oracle_summary,  # noqa: E402
+                         oracle_visible_vals)
+
+STREAMS = {
+    # adds only, flat, 16 typing replicas: every re-merge is the flat closed form
+    "flat_adds": dict(n_ops=60000, replicas=16, window=64, seed=31),
+    # config-2 shape: interleaved deletes, branches -> per-dict replay / replay
+    "nested_interleaved": dict(n_ops=30000, replicas=8, window=16, p_delete=0.2, p_branch=0.1, max_depth=3, seed=5),
+    # config-4 shape: depth 12, deletes after adds -> nested closed form
+    "deep_deletes_last": dict(n_ops=40000, replicas=16, p_delete=1 / 3, max_depth=12, max_children=8,
+                              deletes_last=1, seed=9),
+}
+
+
+def sub(s, a, b):
+    off = s["path_off"]
+    return dict(kind=s["kind"][a:b].copy(), ts=s["ts"][a:b].copy(), val=s["val"][a:b].copy(),
+                path_off=(off[a:b + 1] - off[a]).astype(np.uint32), path=s["path"][off[a]:off[b]].copy())
+
+
+def failing_batch(s, a):
+    """[the next op of the stream, an Add anchored at a key that does not exist]."""
+    one = sub(s, a, a + 1)
+    bad = dict(kind=np.zeros(1, np.uint8), ts=np.array([(63 << 32) + 7], np.int64), val=np.zeros(1, np.uint32),
+               path_off=np.array([0, 1], np.uint32), path=np.array([(62 << 32) + 99991], np.int64))
+    return dict(kind=np.concatenate([one["kind"], bad["kind"]]), ts=np.concatenate([one["ts"], bad["ts"]]),
+                val=np.concatenate([one["val"], bad["val"]]),
+                path_off=np.concatenate([one["path_off"], one["path_off"][-1] + bad["path_off"][1:]]).astype(np.uint32),
+                path=np.concatenate([one["path"], bad["path"]]))
+
+
+@pytest.mark.parametrize("mode", ["remerge", "replay"])
+@pytest.mark.parametrize("name", sorted(STREAMS))
+def test_incremental_chain(name, mode, monkeypatch):
+    monkeypatch.setenv("CRDTM_INCREMENTAL", mode)
+    s = N.synth(**STREAMS[name])
+    n = len(s["kind"])
+    rng = np.random.default_rng(len(name))
+    # a large first batch, then batches of varied size (1 op .. a few thousand)
+    cuts = [0, n // 2]
+    while cuts[-1] < n:
+        cuts.append(min(n, cuts[-1] + int(rng.choice([1, 7, 300, 2500, 6000]))))
+    from oracle.oracle import lib as olib
+    ot = olib().orc_init(0)
+    et = CRDTree.init(0)
+    remerged = 0
+    for k, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        if k == 3:  # a failing batch in the middle: Err, nothing changes
+            before = engine_summary(et)
+            fb = failing_batch(s, a)
+            _, rc, oerr = oracle_apply_arrays(fb, 2, tree=ot)
+            st = np.full(2, 9, np.uint8)
+            res = et.apply_arrays(fb, 2, status=st)
+            assert (res.code, res.err_index) == (rc, oerr) == (3, 1)  # OperationFailed
+            assert st[1] == 2  # CRDTM_ST_ERROR
+            assert engine_summary(et) == before == oracle_summary(ot)
+        chunk = sub(s, a, b)
+        n_log0 = len(oracle_log(ot, 0)[0])
+        _, rc, _ = oracle_apply_arrays(chunk, b - a, tree=ot)
+        st = np.full(b - a, 9, np.uint8)
+        res = et.apply_arrays(chunk, b - a, status=st)
+        assert res.code == rc == 0, (k, res.code, rc)
+        if k and mode == "remerge" and res.flags & N.FLAG_REMERGE:
+            remerged += 1
+        if k and mode == "replay":
+            assert res.path_taken == N.PATH_REPLAY and not res.flags & N.FLAG_REMERGE
+        assert res.n_applied == len(oracle_log(ot, 0)[0]) - n_log0 == int(np.sum(st == 0)), k
+        assert engine_summary(et) == oracle_summary(ot), (k, a, b)
+        assert engine_log(et, 1) == oracle_log(ot, 1), k
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+    if mode == "remerge" and name != "nested_interleaved":
+        assert remerged == len(cuts) - 2  # every incremental step took the parallel paths
+    olib().orc_free(ot)
