@@ -235,19 +235,7 @@ int crdtm_ctx_sync(crdtm_ctx* c) {
   return CRDTM_OK;
 }
 
-int crdtm_tree_create(crdtm_ctx* c, int64_t replica_id, crdtm_tree** out) {
-  if (!c || !out) return CRDTM_E_ARG;
-  HIP_CHECK(hipSetDevice(c->device));
-  auto* t = new crdtm_tree;
-  t->ctx = c;
-  TreeCaps need;
-  need.slots = 1024;
-  need.dicts = 512;
-  need.log = 1024;
-  need.lpath = 4096;
-  need.doc = 1024;
-  int r = grow_tree(t, need);
-  if (r) return r;
+static int init_root(crdtm_tree* t) {
   // init: Root {0: Tombstone [] Nothing} (src/Internal/Node.elm:41-48)
   const long long k0 = 0;
   const uint32_t none = NONE, zero = 0;
@@ -261,6 +249,22 @@ int crdtm_tree_create(crdtm_ctx* c, int64_t replica_id, crdtm_tree** out) {
   HIP_CHECK(hipMemcpy(t->d.d_sent, &zero, 4, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(t->d.d_owner, &none, 4, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(t->d.l_off, &zero, 4, hipMemcpyHostToDevice));
+  return CRDTM_OK;
+}
+
+int crdtm_tree_create(crdtm_ctx* c, int64_t replica_id, crdtm_tree** out) {
+  if (!c || !out) return CRDTM_E_ARG;
+  HIP_CHECK(hipSetDevice(c->device));
+  auto* t = new crdtm_tree;
+  t->ctx = c;
+  TreeCaps need;
+  need.slots = 1024;
+  need.dicts = 512;
+  need.log = 1024;
+  need.lpath = 4096;
+  need.doc = 1024;
+  int r = grow_tree(t, need);
+  if (r || (r = init_root(t))) return r;
   t->n_slots = 1;
   t->n_dicts = 1;
   t->timestamp = replica_id * TWO32;  // replicaId * 2 ^ 32 (src/CRDTree.elm:137)
@@ -272,6 +276,10 @@ int crdtm_tree_create(crdtm_ctx* c, int64_t replica_id, crdtm_tree** out) {
 
 int crdtm_tree_reset(crdtm_tree* t, int64_t replica_id) {
   if (!t) return CRDTM_E_ARG;
+  if (t->store && t->store.use_count() > 1) {  // other versions keep the shared arrays
+    int r = unshare_tree(t, false);
+    if (r || (r = init_root(t))) return r;
+  }
   // slot 0 / dict 0 / l_off[0] keep their init values: only the root
   // sentinel's `next` can change, and only to a slot we now drop.
   // (stream-ordered, no host wait: every later read of the state synchronises)
@@ -295,38 +303,24 @@ int crdtm_tree_reset(crdtm_tree* t, int64_t replica_id) {
 int crdtm_tree_destroy(crdtm_tree* t) {
   if (!t) return CRDTM_OK;
   hipStreamSynchronize(t->ctx->stream);
-  void* ps[] = {t->d.s_key, t->d.s_next, t->d.s_src, t->d.s_child, t->d.s_dict, t->d.s_flags, t->d.d_sent,
-                t->d.d_owner, t->d.l_kind, t->d.l_ts, t->d.l_val, t->d.l_off, t->d.l_path, t->d.doc};
-  for (void* p : ps)
-    if (p) hipFree(p);
+  t->store.reset();  // frees the arrays unless another version still shares them
   delete t;
   return CRDTM_OK;
 }
 
+// A new version handle sharing the state's device arrays (O(1)); the first
+// write to either handle gives it a private copy (Elm persistence,
+// src/CRDTree.elm:228-232: the old value stays valid after apply).
 int crdtm_tree_clone(const crdtm_tree* t, crdtm_tree** out) {
   if (!t || !out) return CRDTM_E_ARG;
-  HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
   auto* u = new crdtm_tree;
   u->ctx = t->ctx;
-  int r = grow_tree(u, t->cap);
-  if (r) return r;
-  auto cp = [&](void* dst, const void* src, uint64_t bytes) -> int {
-    if (bytes) HIP_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice));
-    return CRDTM_OK;
-  };
-  const uint64_t S = t->n_slots, D = t->n_dicts, Ln = t->log_n;
-  if ((r = cp(u->d.s_key, t->d.s_key, S * 8)) || (r = cp(u->d.s_next, t->d.s_next, S * 4)) ||
-      (r = cp(u->d.s_src, t->d.s_src, S * 4)) || (r = cp(u->d.s_child, t->d.s_child, S * 4)) ||
-      (r = cp(u->d.s_dict, t->d.s_dict, S * 4)) || (r = cp(u->d.s_flags, t->d.s_flags, S)) ||
-      (r = cp(u->d.d_sent, t->d.d_sent, D * 4)) || (r = cp(u->d.d_owner, t->d.d_owner, D * 4)) ||
-      (r = cp(u->d.l_kind, t->d.l_kind, Ln)) || (r = cp(u->d.l_ts, t->d.l_ts, Ln * 8)) ||
-      (r = cp(u->d.l_val, t->d.l_val, Ln * 4)) || (r = cp(u->d.l_off, t->d.l_off, (Ln + 1) * 4)) ||
-      (r = cp(u->d.l_path, t->d.l_path, t->log_npath * 8)) ||
-      (r = cp(u->d.doc, t->d.doc, (t->doc_valid ? t->doc_n : 0) * 4)))
-    return r;
-  u->n_slots = S;
-  u->n_dicts = D;
-  u->log_n = Ln;
+  u->d = t->d;
+  u->cap = t->cap;
+  u->store = t->store;
+  u->n_slots = t->n_slots;
+  u->n_dicts = t->n_dicts;
+  u->log_n = t->log_n;
   u->log_npath = t->log_npath;
   u->doc_n = t->doc_n;
   u->doc_valid = t->doc_valid;
@@ -350,6 +344,7 @@ int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_b
   if (ops->n_ops >= 0x7FFFFFF0ULL) return CRDTM_E_ARG;
   crdtm_ctx* c = t->ctx;
   HIP_CHECK(hipSetDevice(c->device));
+  if (int ru = unshare_tree(t, true)) return ru;  // this version is about to be written
   c->clear_marks();
   const uint64_t n = ops->n_ops;
   uint64_t np = ops->n_path;

@@ -76,6 +76,14 @@ struct TreeCaps {
   uint64_t slots = 0, dicts = 0, log = 0, lpath = 0, doc = 0;
 };
 
+// Owner of a tree state's device arrays. Versions (crdtm_tree_clone) share
+// one store until one of them is mutated (copy on write, api.hip unshare):
+// a kept version costs nothing until the next apply to either handle.
+struct DevStore {
+  TreeDev d;
+  ~DevStore();
+};
+
 }  // namespace crdtm
 
 struct crdtm_ctx {
@@ -126,6 +134,7 @@ struct crdtm_tree {
   std::map<int64_t, int64_t> replicas;
   uint64_t last_begin = 0, last_end = 0;
   int last_is_batch = 1;
+  std::shared_ptr<crdtm::DevStore> store;  // owns d's arrays; shared by versions until written
   uint64_t version = 0;              // bumped by every state change (apply, reset)
   // incremental re-merge (merge.hip apply_batch): while set, the engine runs
   // the fresh-tree paths over log ++ batch; own-replica Adds of the log are
@@ -197,6 +206,8 @@ int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& ws);
 int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdtm_result* res, bool* handled);
 // merge.hip
 int grow_tree(crdtm_tree* t, const TreeCaps& need);
+// copy on write (DevStore): a private copy of the state before it is written
+int unshare_tree(crdtm_tree* t, bool keep_contents);
 int apply_batch(crdtm_tree* t, const OpsDev& ops, uint8_t* status_dev, crdtm_result* res);
 int linearize(crdtm_tree* t);  // fills t->d.doc / t->doc_n from the tree state
 int forest_apply(crdtm_ctx* c, int64_t replica_id, const OpsDev& o, const uint32_t* doc_off_host, uint64_t n_docs,

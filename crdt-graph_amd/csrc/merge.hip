@@ -2593,7 +2593,25 @@ static int grow_array(T*& p, uint64_t old_n, uint64_t new_n) {
   return CRDTM_OK;
 }
 
+DevStore::~DevStore() {
+  void* ps[] = {d.s_key, d.s_next, d.s_src, d.s_child, d.s_dict, d.s_flags, d.d_sent,
+                d.d_owner, d.l_kind, d.l_ts, d.l_val, d.l_off, d.l_path, d.doc};
+  for (void* p : ps)
+    if (p) hipFree(p);
+}
+
+static int grow_tree_arrays(crdtm_tree* t, const TreeCaps& need);
+
+// Grows the state's arrays (keeping their contents); never called on a
+// store other versions share (api.hip unshares before every write).
 int grow_tree(crdtm_tree* t, const TreeCaps& need) {
+  if (!t->store) t->store = std::make_shared<DevStore>();
+  const int r = grow_tree_arrays(t, need);
+  t->store->d = t->d;  // the store owns whatever grow_array left in place
+  return r;
+}
+
+static int grow_tree_arrays(crdtm_tree* t, const TreeCaps& need) {
   HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
   TreeCaps& c = t->cap;
   auto bump = [](uint64_t have, uint64_t want) { return want <= have ? have : (want + want / 4 + 1024); };
@@ -2632,6 +2650,38 @@ int grow_tree(crdtm_tree* t, const TreeCaps& need) {
     if (r) return r;
     c.doc = n;
   }
+  return CRDTM_OK;
+}
+
+// Copy on write: before a version that shares its arrays with another is
+// written, it takes a private copy of the live portions (one device copy of
+// the state, the same order of bytes as one merge writes).
+int unshare_tree(crdtm_tree* t, bool keep_contents) {
+  if (!t->store || t->store.use_count() == 1) return CRDTM_OK;
+  HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+  const TreeDev old = t->d;
+  const TreeCaps cap = t->cap;
+  t->d = TreeDev{};
+  t->cap = TreeCaps{};
+  t->store.reset();
+  int r = grow_tree(t, cap);  // fresh private arrays of the same capacity
+  if (r) return r;
+  if (!keep_contents) return CRDTM_OK;
+  auto cp = [&](void* dst, const void* src, uint64_t bytes) -> int {
+    if (bytes) HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, t->ctx->stream));
+    return CRDTM_OK;
+  };
+  const uint64_t S = t->n_slots, D = t->n_dicts, Ln = t->log_n;
+  if ((r = cp(t->d.s_key, old.s_key, S * 8)) || (r = cp(t->d.s_next, old.s_next, S * 4)) ||
+      (r = cp(t->d.s_src, old.s_src, S * 4)) || (r = cp(t->d.s_child, old.s_child, S * 4)) ||
+      (r = cp(t->d.s_dict, old.s_dict, S * 4)) || (r = cp(t->d.s_flags, old.s_flags, S)) ||
+      (r = cp(t->d.d_sent, old.d_sent, D * 4)) || (r = cp(t->d.d_owner, old.d_owner, D * 4)) ||
+      (r = cp(t->d.l_kind, old.l_kind, Ln)) || (r = cp(t->d.l_ts, old.l_ts, Ln * 8)) ||
+      (r = cp(t->d.l_val, old.l_val, Ln * 4)) || (r = cp(t->d.l_off, old.l_off, (Ln + 1) * 4)) ||
+      (r = cp(t->d.l_path, old.l_path, t->log_npath * 8)) ||
+      (r = cp(t->d.doc, old.doc, (t->doc_valid ? t->doc_n : 0) * 4)))
+    return r;
+  HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
   return CRDTM_OK;
 }
 
@@ -3530,7 +3580,7 @@ int linearize(crdtm_tree* t) {
   if (r) return r;
   TreeCaps need = t->cap;
   need.doc = std::max<uint64_t>(need.doc, S + 1);
-  if (need.doc > t->cap.doc && (r = grow_tree(t, need))) return r;
+  if (need.doc > t->cap.doc && ((r = unshare_tree(t, true)) || (r = grow_tree(t, need)))) return r;
   LAUNCH(k_lin_doc, dim3(grid_for(S)), dim3(BLOCK), 0, s, t->d, S, excl, t->d.doc, t->cap.doc);
   // number of visible entries = weight sum up to the end: excl at exit(0)
   unsigned long long tot = 0;

@@ -90,3 +90,43 @@ def test_incremental_chain(name, mode, monkeypatch):
     if mode == "remerge" and name != "nested_interleaved":
         assert remerged == len(cuts) - 2  # every incremental step took the parallel paths
     olib().orc_free(ot)
+
+
+def test_versions_copy_on_write():
+    """Persistent versions (src/CRDTree.elm:228-232: `apply` returns a new
+    tree and the old one stays valid): crdtm_tree_clone shares the device
+    state, the first write to either handle copies it."""
+    import gc
+    from oracle.oracle import lib as olib
+    s = N.synth(n_ops=20000, replicas=8, window=16, p_delete=0.2, p_branch=0.1, max_depth=3, seed=77)
+
+    def oracle_upto(m):
+        ot, rc, _ = oracle_apply_arrays(sub(s, 0, 10000), 10000)
+        if m > 10000:
+            _, rc2, _ = oracle_apply_arrays(sub(s, 10000, m), m - 10000, tree=ot)
+            assert rc2 == 0
+        return ot
+
+    v0 = CRDTree.init(0)
+    assert v0.apply_arrays(sub(s, 0, 10000), 10000).code == 0
+    sum0, log0, doc0 = engine_summary(v0), engine_log(v0, 0), v0.document_handles()
+    v1 = v0.clone()
+    assert v1.apply_arrays(sub(s, 10000, 20000), 10000).code == 0
+    v2 = v0.clone()
+    assert v2.apply_arrays(sub(s, 10000, 15000), 5000).code == 0
+    assert engine_summary(v0) == sum0 and engine_log(v0, 0) == log0
+    assert np.array_equal(v0.document_handles(), doc0)
+    o20, o15 = oracle_upto(20000), oracle_upto(15000)
+    assert engine_summary(v1) == oracle_summary(o20)
+    assert engine_summary(v2) == oracle_summary(o15)
+    del v0
+    gc.collect()
+    assert engine_summary(v1) == oracle_summary(o20) and engine_log(v1, 0) == oracle_log(o20, 0)
+    v3 = v1.clone()
+    N.check(N.lib().crdtm_tree_reset(v3._h, 0))
+    assert engine_summary(v1) == oracle_summary(o20)
+    assert np.array_equal(v1.document_handles(), oracle_visible_vals(o20))
+    assert v3.apply_arrays(sub(s, 0, 10000), 10000).code == 0
+    assert engine_summary(v3) == oracle_summary(oracle_upto(10000))
+    for t in (o20, o15):
+        olib().orc_free(t)
