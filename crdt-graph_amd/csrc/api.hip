@@ -192,6 +192,9 @@ int crdtm_ctx_create(int device, void* stream, crdtm_ctx** out) {
     HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->own_stream = true;
   }
+  HIP_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+  HIP_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
   HIP_CHECK(hipMalloc(&c->dres, sizeof(DevResult)));
   HIP_CHECK(hipHostMalloc(&c->hres, sizeof(DevResult), hipHostMallocDefault));
   HIP_CHECK(hipMalloc(&c->crange, RID_SLOTS * sizeof(uint2)));
@@ -223,6 +226,10 @@ int crdtm_ctx_destroy(crdtm_ctx* c) {
   hipFree(c->ws.scan_status);
   hipFree(c->rtab);
   if (c->own_stream) hipStreamDestroy(c->stream);
+  hipStreamSynchronize(c->side);
+  hipStreamDestroy(c->side);
+  hipEventDestroy(c->ev_fork);
+  hipEventDestroy(c->ev_join);
   delete c;
   return CRDTM_OK;
 }
@@ -631,20 +638,308 @@ void crdtm_free(void* p) { std::free(p); }
 }  // extern "C"
 
 // ---------------------------------------------------------------------------
-// Traversal API (src/CRDTree.elm:421-625, src/CRDTree/Node.elm:96-174), served
-// from a host copy of the device state fetched once per tree version. Node
-// references: a slot index of the current state, CRDTM_REF_ROOT, or the
-// implicit sentinel of a live node's still-empty children dict
-// (CRDTM_REF_VSENT | slot). References stay valid until the next apply.
-// Semantics follow the reference literally: a node's parent is found from its
-// *path* (a dict sentinel's path is [] so its parent is the root), `next`
-// follows next *keys* in that parent's children skipping Tombstones, `prev`
-// scans the parent's chain from its sentinel (Tombstones included), `walk`
-// starts after its start node and after the head of every node it descends
-// into.
+// Traversal API (src/CRDTree.elm:421-625, src/CRDTree/Node.elm:96-174).
+// Point queries (get, node info, parent / next / prev / head, children) run
+// on the device, over the state's own arrays plus a (dict, key) -> slot hash
+// built in parallel once per tree version: one single-lane kernel per query
+// follows the reference's lookups, and only the answer crosses PCIe. `walk`,
+// whose output is the size of the document, reads a host copy of the state
+// (fetched once per version). Both run the same rules, written once over a
+// view of the state (TvDev / TvHost). Node references: a slot index of the
+// current state, CRDTM_REF_ROOT, or the implicit sentinel of a live node's
+// still-empty children dict (CRDTM_REF_VSENT | slot); valid until the next
+// apply. Semantics follow the reference literally: a node's parent is found
+// from its *path* (a dict sentinel's path is [] so its parent is the root),
+// `next` follows next *keys* in that parent's children skipping Tombstones,
+// `prev` scans the parent's chain from its sentinel (Tombstones included),
+// `walk` starts after its start node and after the head of every node it
+// descends into.
 // ---------------------------------------------------------------------------
 namespace {
 
+constexpr uint64_t REF_NONE = CRDTM_REF_NONE, REF_ROOT = CRDTM_REF_ROOT, REF_VSENT = CRDTM_REF_VSENT;
+
+// children dict of a node: kind 0 = empty (Tombstone), 1 = dict id, 2 = implicit {0: sentinel} of owner slot
+struct DictRef {
+  int kind;
+  uint64_t v;
+};
+
+template <class V>
+__host__ __device__ bool tv_ref_ok(const V& c, uint64_t r) {
+  if (r == REF_ROOT) return true;
+  if (r & REF_VSENT) {
+    const uint64_t s = r & ~REF_VSENT;
+    return s < c.S && !(c.flags(s) & F_TOMB) && c.child(s) == NONE;
+  }
+  return r < c.S;
+}
+
+template <class V>
+__host__ __device__ bool tv_is_tomb(const V& c, uint64_t r) {
+  return r != REF_ROOT && ((r & REF_VSENT) || (c.flags(r) & F_TOMB));
+}
+
+template <class V>
+__host__ __device__ DictRef tv_children(const V& c, uint64_t r) {
+  if (r == REF_ROOT) return {1, 0};
+  if (tv_is_tomb(c, r)) return {0, 0};
+  const uint32_t ch = c.child(r);
+  return ch == NONE ? DictRef{2, r} : DictRef{1, ch};
+}
+
+template <class V>
+__host__ __device__ uint64_t tv_lookup(const V& c, const DictRef& d, long long key) {
+  if (d.kind == 0) return REF_NONE;
+  if (d.kind == 2) return key == 0 ? (REF_VSENT | d.v) : REF_NONE;
+  const uint32_t s = c.find(static_cast<uint32_t>(d.v), key);
+  return s == NONE ? REF_NONE : s;
+}
+
+template <class V>
+__host__ __device__ bool tv_next_key(const V& c, uint64_t r, long long* k) {
+  if (r == REF_ROOT || (r & REF_VSENT)) return false;
+  const uint32_t nx = c.next(r);
+  if (nx == NONE) return false;
+  *k = c.key(nx);
+  return true;
+}
+
+// nextNode (src/Internal/Node.elm:257-268) in dict d
+template <class V>
+__host__ __device__ uint64_t tv_next_node(const V& c, uint64_t r, const DictRef& d) {
+  long long k;
+  for (uint64_t x = r;;) {
+    if (!tv_next_key(c, x, &k)) return REF_NONE;
+    x = tv_lookup(c, d, k);
+    if (x == REF_NONE) return REF_NONE;
+    if (!tv_is_tomb(c, x)) return x;
+  }
+}
+
+// Node.descendant from the root (src/Internal/Node.elm:289-299) along keys p(0..n-1)
+template <class V, class P>
+__host__ __device__ uint64_t tv_descend(const V& c, const P& p, uint64_t n) {
+  if (n == 0) return REF_NONE;
+  uint64_t r = REF_ROOT;
+  for (uint64_t j = 0; j < n && r != REF_NONE; ++j) r = tv_lookup(c, tv_children(c, r), p(j));
+  return r;
+}
+
+// Node.path: the Add's path without its last element, then the node's ts
+// (empty for the root and sentinels); the parent is `get` of all but the last
+template <class V>
+__host__ __device__ uint64_t tv_path_len(const V& c, uint64_t r) {
+  if (r == REF_ROOT || (r & REF_VSENT)) return 0;
+  const uint32_t src = c.src(r);
+  return src == NONE ? 0 : c.loff(src + 1) - c.loff(src);
+}
+template <class V>
+__host__ __device__ long long tv_path_at(const V& c, uint64_t r, uint64_t j) {
+  const uint32_t src = c.src(r);
+  const uint32_t b = c.loff(src), e = c.loff(src + 1);
+  return b + j + 1 < e ? c.lpath(b + j) : c.lts(src);
+}
+
+template <class V>
+__host__ __device__ uint64_t tv_parent(const V& c, uint64_t r) {  // src/CRDTree.elm:425-441
+  const uint64_t L = tv_path_len(c, r);
+  if (L <= 1) return REF_ROOT;
+  return tv_descend(c, [&](uint64_t j) { return tv_path_at(c, r, j); }, L - 1);
+}
+
+template <class V>
+__host__ __device__ uint64_t tv_next_of(const V& c, uint64_t r) {  // src/CRDTree.elm:560-566
+  const uint64_t par = tv_parent(c, r);
+  if (par == REF_NONE) return REF_NONE;
+  return tv_next_node(c, r, tv_children(c, par));
+}
+
+template <class V>
+__host__ __device__ uint64_t tv_prev_of(const V& c, uint64_t r) {  // src/CRDTree.elm:569-575 (Node.find)
+  const uint64_t par = tv_parent(c, r);
+  if (par == REF_NONE) return REF_NONE;
+  const DictRef d = tv_children(c, par);
+  uint64_t left = tv_lookup(c, d, 0);
+  long long k;
+  while (left != REF_NONE && tv_next_key(c, left, &k)) {
+    const uint64_t x = tv_lookup(c, d, k);
+    if (x == REF_NONE) return REF_NONE;
+    if (tv_next_of(c, x) == r) return x;
+    left = x;
+  }
+  return REF_NONE;
+}
+
+template <class V>
+__host__ __device__ uint64_t tv_head_of(const V& c, uint64_t r) {  // src/CRDTree/Node.elm:165-167
+  const DictRef d = tv_children(c, r);
+  const uint64_t s0 = tv_lookup(c, d, 0);
+  return s0 == REF_NONE ? REF_NONE : tv_next_node(c, s0, d);
+}
+
+// ---- the device view: the state's arrays + the per-version slot hash ----
+struct TvDev {
+  TreeDev T;
+  SlotHash H;
+  uint64_t S;
+  __device__ uint8_t flags(uint64_t s) const { return T.s_flags[s]; }
+  __device__ uint32_t child(uint64_t s) const { return T.s_child[s]; }
+  __device__ uint32_t next(uint64_t s) const { return T.s_next[s]; }
+  __device__ long long key(uint64_t s) const { return T.s_key[s]; }
+  __device__ uint32_t src(uint64_t s) const { return T.s_src[s]; }
+  __device__ uint32_t loff(uint32_t i) const { return T.l_off[i]; }
+  __device__ long long lpath(uint32_t j) const { return T.l_path[j]; }
+  __device__ long long lts(uint32_t i) const { return T.l_ts[i]; }
+  __device__ uint32_t lval(uint32_t i) const { return T.l_val[i]; }
+  __device__ uint32_t find(uint32_t d, long long k) const { return slothash_find(H, d, k); }
+};
+
+struct TravOut {
+  uint64_t ref;
+  uint64_t n;
+  int64_t next;
+  int32_t ok, kind, has_next;
+  uint32_t val;
+};
+
+enum : int { TQ_GET = 0, TQ_INFO = 1, TQ_REL = 2, TQ_CHILDREN = 3 };
+
+__global__ void __launch_bounds__(BLOCK) k_trav_index(TreeDev T, uint32_t S, SlotHash H) {
+  GRID_STRIDE(s, S) slothash_put_par(H, T.s_dict[s], T.s_key[s], s);
+}
+
+// One query on one lane (the reference's lookups are a dependent chain).
+__global__ void k_trav(TvDev v, int q, uint64_t ref, int which, const long long* path, uint64_t len, TravOut* out,
+                       uint64_t* list, uint64_t list_cap, long long* pbuf, uint64_t pcap) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  TravOut o{};
+  o.ok = 1;
+  if (q == TQ_GET) {
+    o.ref = tv_descend(v, [&](uint64_t j) { return path[j]; }, len);
+    *out = o;
+    return;
+  }
+  if (!tv_ref_ok(v, ref)) {
+    o.ok = 0;
+    *out = o;
+    return;
+  }
+  if (q == TQ_INFO) {
+    const bool tomb = tv_is_tomb(v, ref);
+    o.kind = ref == REF_ROOT ? 3 : (tomb ? 2 : 1);
+    o.val = (ref == REF_ROOT || tomb) ? 0u : v.lval(v.src(ref));
+    long long k = 0;
+    o.has_next = tv_next_key(v, ref, &k) ? 1 : 0;
+    o.next = o.has_next ? k : 0;
+    o.n = tv_path_len(v, ref);
+    for (uint64_t j = 0; j < o.n && j < pcap; ++j) pbuf[j] = tv_path_at(v, ref, j);
+  } else if (q == TQ_REL) {
+    switch (which) {
+      case CRDTM_REL_PARENT: o.ref = tv_parent(v, ref); break;
+      case CRDTM_REL_NEXT: o.ref = tv_next_of(v, ref); break;
+      case CRDTM_REL_PREV: o.ref = tv_prev_of(v, ref); break;
+      case CRDTM_REL_HEAD: o.ref = tv_head_of(v, ref); break;
+      default: o.ok = 0;
+    }
+  } else {  // CRDTree.Node.children: the live children in chain order
+    const DictRef d = tv_children(v, ref);
+    const uint64_t s0 = tv_lookup(v, d, 0);
+    uint64_t n = 0;
+    for (uint64_t x = s0 == REF_NONE ? REF_NONE : tv_next_node(v, s0, d); x != REF_NONE; x = tv_next_node(v, x, d)) {
+      if (n < list_cap) list[n] = x;
+      ++n;
+    }
+    o.n = n;
+  }
+  *out = o;
+}
+
+// Per-tree device traversal state: the slot hash of one version, query
+// scratch, a pinned result block.
+struct DevTrav {
+  uint64_t version = ~0ULL;
+  SlotHash H{nullptr, nullptr, nullptr, 0};
+  uint64_t hcap = 0;
+  TravOut* out = nullptr;
+  TravOut* hout = nullptr;
+  uint64_t* list = nullptr;
+  uint64_t list_cap = 0;
+  long long* buf = nullptr;  // query path in / node path out
+  uint64_t buf_cap = 0;
+  ~DevTrav() {
+    void* ps[] = {H.dict, H.key, H.slot, out, list, buf};
+    for (void* p : ps)
+      if (p) hipFree(p);
+    if (hout) hipHostFree(hout);
+  }
+};
+
+int dev_trav(const crdtm_tree* tc, DevTrav*& out) {
+  auto* t = const_cast<crdtm_tree*>(tc);
+  hipStream_t s = t->ctx->stream;
+  HIP_CHECK(hipSetDevice(t->ctx->device));
+  auto* c = static_cast<DevTrav*>(t->dtrav.get());
+  if (!c) {
+    auto p = std::make_shared<DevTrav>();
+    HIP_CHECK(hipMalloc(&p->out, sizeof(TravOut)));
+    HIP_CHECK(hipHostMalloc(&p->hout, sizeof(TravOut), hipHostMallocDefault));
+    t->dtrav = p;
+    c = p.get();
+  }
+  if (c->version != t->version) {
+    const uint64_t S = t->n_slots;
+    uint64_t H = 1024;
+    while (H < 2 * S) H <<= 1;
+    if (H > c->hcap) {
+      void* ps[] = {c->H.dict, c->H.key, c->H.slot};
+      for (void* p : ps)
+        if (p) HIP_CHECK(hipFree(p));
+      HIP_CHECK(hipMalloc(&c->H.dict, H * sizeof(uint32_t)));
+      HIP_CHECK(hipMalloc(&c->H.key, H * sizeof(long long)));
+      HIP_CHECK(hipMalloc(&c->H.slot, H * sizeof(uint32_t)));
+      c->hcap = H;
+    }
+    c->H.mask = static_cast<uint32_t>(H - 1);
+    HIP_CHECK(hipMemsetAsync(c->H.slot, 0xFF, H * sizeof(uint32_t), s));
+    hipLaunchKernelGGL(k_trav_index, dim3(grid_for(S)), dim3(BLOCK), 0, s, t->d, static_cast<uint32_t>(S), c->H);
+    HIP_CHECK(hipGetLastError());
+    c->version = t->version;
+  }
+  out = c;
+  return CRDTM_OK;
+}
+
+template <class T>
+int dev_room(T*& p, uint64_t& cap, uint64_t need) {
+  if (need <= cap) return CRDTM_OK;
+  if (p) HIP_CHECK(hipFree(p));
+  p = nullptr;
+  const uint64_t n = need + need / 2 + 64;
+  HIP_CHECK(hipMalloc(&p, n * sizeof(T)));
+  cap = n;
+  return CRDTM_OK;
+}
+
+// Runs one query; the answer lands in c->hout (and c->list / c->buf on the device).
+int dev_query(const crdtm_tree* t, int q, uint64_t ref, int which, const int64_t* path, uint64_t len, uint64_t lcap,
+              uint64_t pcap, DevTrav*& c) {
+  int r = dev_trav(t, c);
+  if (r) return r;
+  hipStream_t s = t->ctx->stream;
+  if ((r = dev_room(c->buf, c->buf_cap, std::max(len, pcap) + 1))) return r;
+  if ((r = dev_room(c->list, c->list_cap, lcap + 1))) return r;
+  if (len) HIP_CHECK(hipMemcpyAsync(c->buf, path, len * 8, hipMemcpyHostToDevice, s));
+  TvDev v{t->d, c->H, t->n_slots};
+  hipLaunchKernelGGL(k_trav, dim3(1), dim3(64), 0, s, v, q, ref, which, c->buf, len, c->out, c->list, lcap, c->buf,
+                     pcap);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipMemcpyAsync(c->hout, c->out, sizeof(TravOut), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return CRDTM_OK;
+}
+
+// ---- the host view (walk): a copy of the state fetched once per version ----
 struct PairHash {
   size_t operator()(const std::pair<uint32_t, long long>& p) const {
     return std::hash<long long>()(p.second * 0x9E3779B97F4A7C15LL ^ static_cast<long long>(p.first));
@@ -657,7 +952,23 @@ struct TravCache {
   std::unordered_map<std::pair<uint32_t, long long>, uint32_t, PairHash> index;  // (dict, key) -> slot
 };
 
-constexpr uint64_t REF_NONE = CRDTM_REF_NONE, REF_ROOT = CRDTM_REF_ROOT, REF_VSENT = CRDTM_REF_VSENT;
+struct TvHost {
+  const TravCache* c;
+  uint64_t S;
+  uint8_t flags(uint64_t s) const { return c->h.flags[s]; }
+  uint32_t child(uint64_t s) const { return c->h.child[s]; }
+  uint32_t next(uint64_t s) const { return c->h.next[s]; }
+  long long key(uint64_t s) const { return c->h.key[s]; }
+  uint32_t src(uint64_t s) const { return c->h.src[s]; }
+  uint32_t loff(uint32_t i) const { return c->h.l_off[i]; }
+  long long lpath(uint32_t j) const { return c->h.l_path[j]; }
+  long long lts(uint32_t i) const { return c->h.l_ts[i]; }
+  uint32_t lval(uint32_t i) const { return c->h.l_val[i]; }
+  uint32_t find(uint32_t d, long long k) const {
+    auto it = c->index.find({d, k});
+    return it == c->index.end() ? NONE : it->second;
+  }
+};
 
 int trav_cache(const crdtm_tree* tc, TravCache*& out) {
   auto* t = const_cast<crdtm_tree*>(tc);
@@ -679,121 +990,19 @@ int trav_cache(const crdtm_tree* tc, TravCache*& out) {
   return CRDTM_OK;
 }
 
-bool ref_ok(const TravCache& c, uint64_t r) {
-  if (r == REF_ROOT) return true;
-  if (r & REF_VSENT) {
-    const uint64_t s = r & ~REF_VSENT;
-    return s < c.h.key.size() && !(c.h.flags[s] & F_TOMB) && c.h.child[s] == NONE;
-  }
-  return r < c.h.key.size();
-}
-
-bool is_tomb(const TravCache& c, uint64_t r) { return r != REF_ROOT && ((r & REF_VSENT) || (c.h.flags[r] & F_TOMB)); }
-
-// children dict of a node: kind 0 = empty (Tombstone), 1 = dict id, 2 = implicit {0: sentinel} of owner slot
-struct DictRef {
-  int kind;
-  uint64_t v;
-};
-
-DictRef children_of(const TravCache& c, uint64_t r) {
-  if (r == REF_ROOT) return {1, 0};
-  if (is_tomb(c, r)) return {0, 0};
-  const uint32_t ch = c.h.child[r];
-  return ch == NONE ? DictRef{2, r} : DictRef{1, ch};
-}
-
-uint64_t lookup(const TravCache& c, const DictRef& d, long long key) {
-  if (d.kind == 0) return REF_NONE;
-  if (d.kind == 2) return key == 0 ? (REF_VSENT | d.v) : REF_NONE;
-  auto it = c.index.find({static_cast<uint32_t>(d.v), key});
-  return it == c.index.end() ? REF_NONE : it->second;
-}
-
-bool next_key(const TravCache& c, uint64_t r, long long* k) {
-  if (r == REF_ROOT || (r & REF_VSENT)) return false;
-  const uint32_t nx = c.h.next[r];
-  if (nx == NONE) return false;
-  *k = c.h.key[nx];
-  return true;
-}
-
-void node_path(const TravCache& c, uint64_t r, std::vector<long long>& p) {
-  p.clear();
-  if (r == REF_ROOT || (r & REF_VSENT)) return;
-  const uint32_t src = c.h.src[r];
-  if (src == NONE) return;  // a sentinel: Tombstone [] _
-  const uint32_t b = c.h.l_off[src], e = c.h.l_off[src + 1];
-  for (uint32_t j = b; j + 1 < e; ++j) p.push_back(c.h.l_path[j]);
-  p.push_back(c.h.l_ts[src]);
-}
-
-// nextNode (src/Internal/Node.elm:257-268) in dict d
-uint64_t next_node(const TravCache& c, uint64_t r, const DictRef& d) {
-  long long k;
-  for (uint64_t x = r;;) {
-    if (!next_key(c, x, &k)) return REF_NONE;
-    x = lookup(c, d, k);
-    if (x == REF_NONE) return REF_NONE;
-    if (!is_tomb(c, x)) return x;
-  }
-}
-
-uint64_t descend(const TravCache& c, const int64_t* p, uint64_t n) {  // Node.descendant (src/Internal/Node.elm:289-299)
-  if (n == 0) return REF_NONE;
-  uint64_t r = REF_ROOT;
-  for (uint64_t j = 0; j < n && r != REF_NONE; ++j) r = lookup(c, children_of(c, r), p[j]);
-  return r;
-}
-
-uint64_t parent_of(const TravCache& c, uint64_t r) {  // src/CRDTree.elm:425-441
-  std::vector<long long> p;
-  node_path(c, r, p);
-  if (!p.empty()) p.pop_back();
-  if (p.empty()) return REF_ROOT;
-  return descend(c, reinterpret_cast<const int64_t*>(p.data()), p.size());
-}
-
-uint64_t next_of(const TravCache& c, uint64_t r) {  // src/CRDTree.elm:560-566
-  const uint64_t par = parent_of(c, r);
-  if (par == REF_NONE) return REF_NONE;
-  return next_node(c, r, children_of(c, par));
-}
-
-uint64_t prev_of(const TravCache& c, uint64_t r) {  // src/CRDTree.elm:569-575 (Node.find, identity for ==)
-  const uint64_t par = parent_of(c, r);
-  if (par == REF_NONE) return REF_NONE;
-  const DictRef d = children_of(c, par);
-  uint64_t left = lookup(c, d, 0);
-  long long k;
-  while (left != REF_NONE && next_key(c, left, &k)) {
-    const uint64_t x = lookup(c, d, k);
-    if (x == REF_NONE) return REF_NONE;
-    if (next_of(c, x) == r) return x;
-    left = x;
-  }
-  return REF_NONE;
-}
-
-uint64_t head_of(const TravCache& c, uint64_t r) {  // src/CRDTree/Node.elm:165-167
-  const DictRef d = children_of(c, r);
-  const uint64_t s0 = lookup(c, d, 0);
-  return s0 == REF_NONE ? REF_NONE : next_node(c, s0, d);
-}
-
 // walkHelp (src/CRDTree.elm:602-625) with a function that always Takes; an
 // explicit stack instead of recursion (documents nest arbitrarily deep)
-void walk_from(const TravCache& c, uint64_t left, const DictRef& sib, std::vector<uint64_t>& out) {
+void walk_from(const TvHost& c, uint64_t left, const DictRef& sib, std::vector<uint64_t>& out) {
   std::vector<std::pair<uint64_t, DictRef>> st{{left, sib}};
   while (!st.empty()) {
     auto [l, d] = st.back();
     st.pop_back();
-    const uint64_t node = next_node(c, l, d);
+    const uint64_t node = tv_next_node(c, l, d);
     if (node == REF_NONE) continue;
     out.push_back(node);
     st.push_back({node, d});  // then the siblings after node
-    const uint64_t h = head_of(c, node);
-    if (h != REF_NONE) st.push_back({h, children_of(c, node)});  // first: node's children after its head
+    const uint64_t h = tv_head_of(c, node);
+    if (h != REF_NONE) st.push_back({h, tv_children(c, node)});  // first: node's children after its head
   }
 }
 
@@ -809,76 +1018,68 @@ extern "C" {
 
 int crdtm_tree_get(const crdtm_tree* t, const int64_t* path, uint64_t len, uint64_t* ref) {
   if (!t || !ref || (len && !path)) return CRDTM_E_ARG;
-  TravCache* c;
-  int r = trav_cache(t, c);
+  DevTrav* c;
+  int r = dev_query(t, TQ_GET, 0, 0, path, len, 0, 0, c);
   if (r) return r;
-  *ref = descend(*c, path, len);
+  *ref = c->hout->ref;
   return CRDTM_OK;
 }
 
 int crdtm_node_info(const crdtm_tree* t, uint64_t ref, int32_t* kind, uint32_t* val, int32_t* has_next,
                     int64_t* next, int64_t* path, uint64_t cap, uint64_t* path_len) {
   if (!t) return CRDTM_E_ARG;
-  TravCache* c;
-  int r = trav_cache(t, c);
+  DevTrav* c;
+  const uint64_t pcap = path ? cap : 0;
+  int r = dev_query(t, TQ_INFO, ref, 0, nullptr, 0, 0, pcap, c);
   if (r) return r;
-  if (!ref_ok(*c, ref)) return CRDTM_E_ARG;
-  const bool tomb = is_tomb(*c, ref);
-  if (kind) *kind = ref == REF_ROOT ? 3 : (tomb ? 2 : 1);
-  if (val) *val = (ref == REF_ROOT || tomb) ? 0u : c->h.l_val[c->h.src[ref]];
-  long long k = 0;
-  const bool hn = next_key(*c, ref, &k);
-  if (has_next) *has_next = hn ? 1 : 0;
-  if (next) *next = hn ? k : 0;
-  std::vector<long long> p;
-  node_path(*c, ref, p);
-  for (uint64_t j = 0; path && j < p.size() && j < cap; ++j) path[j] = p[j];
-  if (path_len) *path_len = p.size();
+  const TravOut o = *c->hout;
+  if (!o.ok) return CRDTM_E_ARG;
+  if (kind) *kind = o.kind;
+  if (val) *val = o.val;
+  if (has_next) *has_next = o.has_next;
+  if (next) *next = o.next;
+  if (path && o.n && cap) HIP_CHECK(hipMemcpy(path, c->buf, std::min(o.n, cap) * 8, hipMemcpyDeviceToHost));
+  if (path_len) *path_len = o.n;
   return CRDTM_OK;
 }
 
 int crdtm_tree_relative(const crdtm_tree* t, uint64_t ref, int which, uint64_t* out) {
   if (!t || !out) return CRDTM_E_ARG;
-  TravCache* c;
-  int r = trav_cache(t, c);
+  DevTrav* c;
+  int r = dev_query(t, TQ_REL, ref, which, nullptr, 0, 0, 0, c);
   if (r) return r;
-  if (!ref_ok(*c, ref)) return CRDTM_E_ARG;
-  switch (which) {
-    case CRDTM_REL_PARENT: *out = parent_of(*c, ref); break;
-    case CRDTM_REL_NEXT: *out = next_of(*c, ref); break;
-    case CRDTM_REL_PREV: *out = prev_of(*c, ref); break;
-    case CRDTM_REL_HEAD: *out = head_of(*c, ref); break;
-    default: return CRDTM_E_ARG;
-  }
+  if (!c->hout->ok) return CRDTM_E_ARG;
+  *out = c->hout->ref;
   return CRDTM_OK;
 }
 
 int crdtm_node_children(const crdtm_tree* t, uint64_t ref, uint64_t* out, uint64_t cap, uint64_t* n) {
   if (!t) return CRDTM_E_ARG;
-  TravCache* c;
-  int r = trav_cache(t, c);
+  DevTrav* c;
+  const uint64_t lcap = out ? cap : 0;
+  int r = dev_query(t, TQ_CHILDREN, ref, 0, nullptr, 0, lcap, 0, c);
   if (r) return r;
-  if (!ref_ok(*c, ref)) return CRDTM_E_ARG;
-  std::vector<uint64_t> v;
-  const DictRef d = children_of(*c, ref);
-  const uint64_t s0 = lookup(*c, d, 0);
-  for (uint64_t x = s0 == REF_NONE ? REF_NONE : next_node(*c, s0, d); x != REF_NONE; x = next_node(*c, x, d))
-    v.push_back(x);
-  return put_refs(v, out, cap, n);
+  const TravOut o = *c->hout;
+  if (!o.ok) return CRDTM_E_ARG;
+  if (out && o.n && lcap)
+    HIP_CHECK(hipMemcpy(out, c->list, std::min(o.n, lcap) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (n) *n = o.n;
+  return CRDTM_OK;
 }
 
 int crdtm_tree_walk(const crdtm_tree* t, uint64_t start, uint64_t* out, uint64_t cap, uint64_t* n) {
   if (!t) return CRDTM_E_ARG;
-  TravCache* c;
-  int r = trav_cache(t, c);
+  TravCache* tc;
+  int r = trav_cache(t, tc);
   if (r) return r;
+  const TvHost c{tc, tc->h.key.size()};
   std::vector<uint64_t> v;
   uint64_t s = start;
-  if (s == REF_NONE) s = head_of(*c, REF_ROOT);  // walk ... Nothing: from the root's head
-  else if (!ref_ok(*c, s)) return CRDTM_E_ARG;
+  if (s == REF_NONE) s = tv_head_of(c, REF_ROOT);  // walk ... Nothing: from the root's head
+  else if (!tv_ref_ok(c, s)) return CRDTM_E_ARG;
   if (s != REF_NONE) {
-    const uint64_t par = parent_of(*c, s);
-    if (par != REF_NONE) walk_from(*c, s, children_of(*c, par), v);
+    const uint64_t par = tv_parent(c, s);
+    if (par != REF_NONE) walk_from(c, s, tv_children(c, par), v);
   }
   return put_refs(v, out, cap, n);
 }

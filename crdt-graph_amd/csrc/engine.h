@@ -90,6 +90,10 @@ struct crdtm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
+  // a second stream for work off the critical path (the flat merge's log
+  // copy), forked from and joined back into `stream` with these events
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   crdtm::Arena ws;
   crdtm::DevResult* dres = nullptr;  // device
   crdtm::DevResult* hres = nullptr;  // pinned host
@@ -143,6 +147,7 @@ struct crdtm_tree {
   bool remerge = false;
   int64_t own_bias = 0;
   std::shared_ptr<void> trav;        // traversal cache (api.hip), valid for `version`
+  std::shared_ptr<void> dtrav;       // device traversal index (api.hip), valid for `version`
 };
 
 namespace crdtm {

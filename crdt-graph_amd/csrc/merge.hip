@@ -995,13 +995,16 @@ __global__ void __launch_bounds__(BLOCK) k_rep_max(OpsDev o, const uint8_t* st, 
     if (rk[j] != NONE) atomicMax(&rtab[rk[j]], rv[j]);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_rep_out(OpsDev o, const uint8_t* st, const uint32_t* rtab,
+__global__ void __launch_bounds__(BLOCK) k_rep_out(OpsDev o, const uint8_t* st, uint32_t* rtab,
                                                    long long* out, uint32_t* n_out, long long* inl) {
   GRID_STRIDE(i, o.n) {
     if (st[i] != ST_APPLIED) continue;
     const long long t = op_t(o, i);
     const uint32_t r = static_cast<uint32_t>(replica_of(t) + (1LL << (REPLICA_BITS - 1)));
     if (rtab[r] == i + 1) {
+      // the one winner of replica r also clears its entry (the table stays
+      // clean between calls): ops read after the clear see 0, never their own i + 1
+      rtab[r] = 0;
       const uint32_t k = atomicAdd(n_out, 1u);
       out[2 * k] = replica_of(t);
       out[2 * k + 1] = t;
@@ -1010,13 +1013,6 @@ __global__ void __launch_bounds__(BLOCK) k_rep_out(OpsDev o, const uint8_t* st, 
         inl[2 * k + 1] = t;
       }
     }
-  }
-}
-
-__global__ void __launch_bounds__(BLOCK) k_rep_reset(OpsDev o, const uint8_t* st, uint32_t* rtab) {
-  GRID_STRIDE(i, o.n) {
-    if (st[i] != ST_APPLIED) continue;
-    rtab[static_cast<uint32_t>(replica_of(op_t(o, i)) + (1LL << (REPLICA_BITS - 1)))] = 0;
   }
 }
 
@@ -2748,7 +2744,6 @@ int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& ws) {
   HIP_CHECK(hipMemsetAsync(&dr->n_replica_out, 0, sizeof(uint32_t), s));
   LAUNCH(k_rep_max, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, s, o, st, c->rtab);
   LAUNCH(k_rep_out, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab, rep, &dr->n_replica_out, dr->rep_inline);
-  LAUNCH(k_rep_reset, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab);
   if ((r = sync_read(c))) return r;
   if ((r = take_replicas(t, rep))) return r;
   t->last_begin = t->log_n;
@@ -3054,6 +3049,9 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   // so never inside an incremental re-merge) ----
   if (Q >= n && !t->remerge) {
     if ((r = grow_for(n, n))) return r;
+    // (the log copy stays on this stream: run beside the order kernels on a
+    // second stream it only slowed them by as much as it saved, the order
+    // phase being bandwidth-bound where it is not latency-bound)
     if ((r = flat_order_commit(t, o, ix, Q, maxr, st, n, true, fb))) return r;
     if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, nullptr, n, NONE, st_out);
     if ((r = sync_read(c))) return r;
@@ -3288,6 +3286,49 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   res->n_applied = h1.n_applied;
   res->n_already = h1.n_already;
 
+  // ---- the op log and the replicas table: they depend on the statuses only,
+  // so they run on the side stream while K2/K4 run here ----
+  // every op applied: the log is the batch (identity log index, the batch's
+  // path offsets), so the two log scans are skipped
+  const bool every = h1.n_applied == n;
+  uint32_t* appl = nullptr;
+  uint32_t* plen = nullptr;
+  if (every) {
+    LAUNCH(k_log_totals, dim3(1), dim3(1), 0, s, dr, n, static_cast<uint32_t>(o.n_path));
+  } else {
+    appl = ws.alloc<uint32_t>(n + 1);
+    plen = ws.alloc<uint32_t>(n + 1);
+    LAUNCH(k_post_flags, dim3(g), dim3(BLOCK), 0, s, o, w.st, appl, plen);
+    if ((r = scan_excl_u32(appl, appl, n, &dr->log_n, ws, s))) return r;
+    if ((r = scan_excl_u32(plen, plen, n, &dr->log_npath, ws, s))) return r;
+  }
+  TreeCaps need = t->cap;
+  need.slots = std::max<uint64_t>(need.slots, 1 + 2ULL * h1.n_adds_applied + 1);
+  need.dicts = std::max<uint64_t>(need.dicts, 1 + h1.n_adds_applied + 1);
+  need.log = std::max<uint64_t>(need.log, t->log_n + h1.n_applied + 1);
+  need.lpath = std::max<uint64_t>(need.lpath, t->log_npath + o.n_path + 1);
+  need.doc = std::max<uint64_t>(need.doc, h1.n_adds_applied + 1);
+  // capacity changes synchronise; they only happen on the first calls
+  if (need.slots > t->cap.slots || need.dicts > t->cap.dicts || need.log > t->cap.log ||
+      need.lpath > t->cap.lpath || need.doc > t->cap.doc) {
+    if ((r = grow_tree(t, need))) return r;
+  }
+  long long* rep = ws.alloc<long long>(2 * static_cast<uint64_t>(n) + 2);
+  HIP_CHECK(hipEventRecord(c->ev_fork, s));
+  HIP_CHECK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+  // (full grids: a small background grid starves k_log's chunk loop)
+  LAUNCH(k_log, dim3(g), dim3(BLOCK), 0, c->side, o, w.st, t->d, static_cast<uint32_t>(t->log_n),
+         static_cast<uint32_t>(t->log_npath), appl, plen);
+  LAUNCH(k_log_tail, dim3(1), dim3(1), 0, c->side, t->d, static_cast<uint32_t>(t->log_n), &dr->log_n,
+         static_cast<uint32_t>(t->log_npath), &dr->log_npath);
+  LAUNCH(k_rep_max, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, c->side, o, w.st, c->rtab);
+  LAUNCH(k_rep_out, dim3(g), dim3(BLOCK), 0, c->side, o, w.st, c->rtab, rep, &dr->n_replica_out, dr->rep_inline);
+  HIP_CHECK(hipEventRecord(c->ev_join, c->side));
+  struct Join {  // every exit waits for the side stream (the arena is reused by the next call)
+    crdtm_ctx* c;
+    ~Join() { hipStreamWaitEvent(c->stream, c->ev_join, 0); }
+  } join{c};
+
   // ---- K2: effective parents, document tree, sibling sort ----
   const uint32_t U = n + 2;
   uint8_t* sp = ws.alloc<uint8_t>(n + 1);
@@ -3326,37 +3367,11 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   LAUNCH(k_next, dim3(g), dim3(BLOCK), 0, s, o, w, excl, order, f1, nextn);
 
   // ---- K3 + commit ----
-  uint32_t* appl = ws.alloc<uint32_t>(n + 1);
-  uint32_t* plen = ws.alloc<uint32_t>(n + 1);
   uint32_t* kept = ws.alloc<uint32_t>(n + 1);
   uint32_t* live = ws.alloc<uint32_t>(n + 1);
-  // every op applied: the log is the batch (identity log index, the batch's
-  // path offsets), so the two log scans are skipped
-  const bool every = h1.n_applied == n;
-  if (every) {
-    appl = nullptr;
-    plen = nullptr;
-    LAUNCH(k_log_totals, dim3(1), dim3(1), 0, s, dr, n, static_cast<uint32_t>(o.n_path));
-  }
-  LAUNCH(k_commit_flags, dim3(g), dim3(BLOCK), 0, s, o, w, appl, plen, kept, live);
+  LAUNCH(k_commit_flags, dim3(g), dim3(BLOCK), 0, s, o, w, nullptr, nullptr, kept, live);
   if ((r = scan_excl_u32(kept, kept, n, &dr->n_nodes_kept, ws, s))) return r;
   if ((r = scan_excl_u32(live, live, n, &dr->n_live_kept, ws, s))) return r;
-  if (!every) {
-    if ((r = scan_excl_u32(appl, appl, n, &dr->log_n, ws, s))) return r;
-    if ((r = scan_excl_u32(plen, plen, n, &dr->log_npath, ws, s))) return r;
-  }
-  TreeCaps need = t->cap;
-  need.slots = std::max<uint64_t>(need.slots, 1 + 2ULL * h1.n_adds_applied + 1);
-  need.dicts = std::max<uint64_t>(need.dicts, 1 + h1.n_adds_applied + 1);
-  need.log = std::max<uint64_t>(need.log, t->log_n + h1.n_applied + 1);
-  need.lpath = std::max<uint64_t>(need.lpath, t->log_npath + o.n_path + 1);
-  need.doc = std::max<uint64_t>(need.doc, h1.n_adds_applied + 1);
-  // capacity changes synchronise; they only happen on the first calls
-  if (need.slots > t->cap.slots || need.dicts > t->cap.dicts || need.log > t->cap.log ||
-      need.lpath > t->cap.lpath || need.doc > t->cap.doc) {
-    if ((r = grow_tree(t, need))) return r;
-  }
-  long long* rep = ws.alloc<long long>(2 * static_cast<uint64_t>(n) + 2);
   if ((r = sync_read(c))) return r;
   const uint32_t K = c->hres->n_nodes_kept;
   CommitArgs ca;
@@ -3367,14 +3382,8 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   LAUNCH(k_commit_nodes, dim3(g), dim3(BLOCK), 0, s, o, w, t->d, ca, kept, live, appl, nextn, fc, excl,
                      t->d.doc);
   LAUNCH(k_commit_root, dim3(1), dim3(1), 0, s, o, t->d, kept, fc, 1u);
-  LAUNCH(k_log, dim3(g), dim3(BLOCK), 0, s, o, w.st, t->d, static_cast<uint32_t>(t->log_n),
-                     static_cast<uint32_t>(t->log_npath), appl, plen);
-  LAUNCH(k_log_tail, dim3(1), dim3(1), 0, s, t->d, static_cast<uint32_t>(t->log_n), &dr->log_n,
-                     static_cast<uint32_t>(t->log_npath), &dr->log_npath);
-  LAUNCH(k_rep_max, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, s, o, w.st, c->rtab);
-  LAUNCH(k_rep_out, dim3(g), dim3(BLOCK), 0, s, o, w.st, c->rtab, rep, &dr->n_replica_out, dr->rep_inline);
-  LAUNCH(k_rep_reset, dim3(g), dim3(BLOCK), 0, s, o, w.st, c->rtab);
   if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n, NONE, st_out);
+  HIP_CHECK(hipStreamWaitEvent(s, c->ev_join, 0));
   if ((r = sync_read(c))) return r;
   const DevResult& h2 = *c->hres;
   if ((r = take_replicas(t, rep))) return r;

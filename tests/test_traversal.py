@@ -89,3 +89,37 @@ def test_traversal_adversarial(seed):
         return
     paths = query_paths(ops, np.random.default_rng(seed))
     check_tree(et, _oracle(ot), paths[:400])
+
+
+def test_traversal_device_queries_large_tree():
+    """Point queries (get / parent / next / prev / children, all served by the
+    device kernels over the per-version slot hash) on a 60k-op config-2-shaped
+    tree (copy quirks, nested dicts), sampled nodes against the oracle."""
+    import crdtm._native as N
+    import crdtm.tree as T
+    s = N.synth(n_ops=60000, replicas=16, window=64, p_delete=0.2, p_branch=0.1, max_depth=4, seed=0xC0FFEE02)
+    n = len(s["kind"])
+    ot, rc, _ = oracle_apply_arrays(s, n)
+    et = CRDTree.init(0)
+    assert et.apply_arrays(s, n).code == rc == 0
+    o = _oracle(ot)
+    rng = np.random.default_rng(5)
+    off = s["path_off"]
+    orig = T.VALUES.value
+    T.VALUES.value = lambda h: h
+    try:
+        for i in rng.choice(n, 150, replace=False):
+            p = [int(x) for x in s["path"][off[i]:off[i + 1]]]
+            if s["kind"][i] == 0:
+                p = p[:-1] + [int(s["ts"][i])]
+            v = et.get(p)
+            assert _key(v) == o.node(p), p
+            if v is None:
+                continue
+            assert _key(et.parent(v)) == o.node_query("parent", p), p
+            assert _key(et.next(v)) == o.node_query("next", p), p
+            assert _key(et.prev(v)) == o.node_query("prev", p), p
+            assert [_key(c) for c in et.children(v)] == o.node_query("children", p), p
+        assert [_key(c) for c in et.children(et.root())] == o.node_query("children", [])
+    finally:
+        T.VALUES.value = orig
