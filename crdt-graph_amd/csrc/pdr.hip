@@ -43,6 +43,14 @@
 
 namespace crdtm {
 
+#ifdef PDR_STATS  // walk statistics of the replay (debug builds only)
+__device__ unsigned long long g_pdr_stats[8];
+__device__ bool pdr_stat_on;  // (unused)
+#define PDR_STAT(k) do { ++g_stc[k]; } while (0)
+#else
+#define PDR_STAT(k) do { } while (0)
+#endif
+
 constexpr uint32_t PM = 0xFFFFFFu;  // slot index mask; PM = end of chain
 enum : uint32_t { SF_TOMB = 1u << 24, SF_ORPHAN = 2u << 24, SF_COPY = 4u << 24, SF_MADE = 8u << 24 };
 constexpr uint32_t OW_NF = PM;           // op word code: the target/anchor is missing (NotFound)
@@ -77,6 +85,8 @@ struct PdrCtx {
   uint32_t* logn;          // per dict: entries logged, NONE = no log (small dict or room exhausted)
   uint32_t* ilog;          // per instance: snapshots rebuilt from the log -> prefix length, else NONE
   uint32_t log_min;        // slots a dict needs to keep a change log
+  uint32_t* where;         // per slot position: the chain block of the rank (pdr_blocked), NONE off the chain
+  uint32_t* blk_fail;      // DevResult::pdr_blk_fail
   PdrInst I;
 };
 
@@ -188,9 +198,17 @@ __device__ __forceinline__ uint32_t ld_uniform(const uint32_t* S, uint32_t k) {
 // p (slot word wp): the first live entry from p on, or PM; *wp becomes its
 // word. Tombstone runs through consecutive ranks are crossed 64 ranks at a
 // time (wave-uniform: every lane runs it with the same p).
+#ifdef PDR_STATS
+#define STC_PARAM , unsigned long long* g_stc
+#define STC_ARG , g_stc
+#else
+#define STC_PARAM
+#define STC_ARG
+#endif
 __device__ __forceinline__ uint32_t pdr_next_live(const uint32_t* S, uint32_t K, uint32_t lane, uint32_t p,
-                                                  uint32_t& wp) {
+                                                  uint32_t& wp STC_PARAM) {
   while (p != PM && (wp & SF_TOMB)) {
+    PDR_STAT(2);
     const uint32_t q = wp & PM;
     if (q == p + 1) {
       const uint32_t e = p + lane;
@@ -227,6 +245,10 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
   const uint32_t base = p.I.base[I];
   const uint32_t K = pdr_kcount(p, D);
   const uint32_t rb = p.rbase[D];
+#ifdef PDR_STATS
+  unsigned long long g_stc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const long long t_start = clock64();
+#endif
   for (uint32_t r = lane; r <= K; r += 64) S[r] = r == 0 ? (PM | SF_TOMB | SF_MADE) : PM;
   __syncthreads();
   const uint32_t ob = rb, oe = p.rbase[D + 1] - 1;
@@ -286,12 +308,15 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
         } else if (an == OW_NF || !(ld_uniform(S, an) & SF_MADE)) {
           s = ST_NOTFOUND;
         } else {
+          PDR_STAT(4);
           uint32_t node = an, nk = an;  // findInsertion
           uint32_t wn = ld_uniform(S, node);
           for (;;) {
             const uint32_t rn = wn & PM;
             if (rn == PM) break;
+            PDR_STAT(0);
             if (rn == node + 1 && x < rn) {
+              PDR_STAT(1);
               // Window step. The chain runs through consecutive ranks from
               // node (node -> node+1 -> ...), so every key ahead is larger
               // than x: the walk visits each live entry of the run and goes
@@ -317,7 +342,7 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
               // ranks node+1..node+M are tombstones: the next live entry lies past them
               uint32_t p = __builtin_amdgcn_readlane(a, M) & PM;
               uint32_t wl = p == PM ? 0u : ld_uniform(S, p);
-              p = pdr_next_live(S, K, lane, p, wl);
+              p = pdr_next_live(S, K, lane, p, wl STC_ARG);
               if (p == PM) break;  // only tombstones follow: stop here
               nk = node + 1u;      // (x < node + 1: the walk goes on)
               node = p;
@@ -325,7 +350,7 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
               continue;
             }
             uint32_t wl = ld_uniform(S, rn);
-            const uint32_t live = pdr_next_live(S, K, lane, rn, wl);
+            const uint32_t live = pdr_next_live(S, K, lane, rn, wl STC_ARG);
             if (live == PM) break;
             if (x > rn) break;  // ts > key(rn)
             nk = rn;
@@ -339,6 +364,7 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
             S[node] = (wn & ~PM) | x;
             logw(i, node, 0, (wn & ~PM) | x, 0);
           } else {
+            PDR_STAT(3);
             // copy quirk: slot nk := copy of node, next = x; the entries after
             // nk up to node drop off the chain when nk was on it
             if (!(wk & SF_ORPHAN)) {
@@ -375,6 +401,11 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
       if (ORIG) st[i] = s;  // uniform store
     }
   }
+#ifdef PDR_STATS
+  if (ORIG && lane == 0 && K > 28000)
+    printf("pdr big dict K=%u ops=%u adds %llu steps %llu windows %llu tomb %llu quirks %llu cycles %lld\n", K,
+           p.rbase[D + 1] - p.rbase[D], g_stc[4], g_stc[0], g_stc[1], g_stc[2], g_stc[3], clock64() - t_start);
+#endif
   if (ORIG && lane == 0) p.logn[D] = (logging && ln <= lcap) ? ln : NONE;
   __syncthreads();
   if (S != p.S + base) {
@@ -401,11 +432,461 @@ __global__ void __launch_bounds__(64) k_pdr_huge(PdrCtx p, const uint32_t* list,
   pdr_serial<ORIG>(p, st, I, p.S + p.I.base[I]);
 }
 
+// ---- P2b: the same replay over a blocked chain order (big dicts) ----
+// pdr_serial follows the chain one `next` at a time: ~13 dependent steps per
+// Add in config 2's two 39k-op dicts (walks cross other replicas' typing
+// runs), ~470 cycles each. Here the dict's chain (from its sentinel) is also
+// kept in order as a list of 64-entry blocks in LDS, one entry per lane
+// {rank:15, tombstone:1}, so findInsertion's walk (src/Internal/Node.elm:
+// 93-104) is decided 64 positions at a time with ballots: the compare
+// positions are the entries right after the anchor or after a live entry
+// (the walk compares `ts` with the raw next key of every node it visits and
+// moves to the next live node), the walk stops at the first compare position
+// whose rank is below x's, or where nothing live follows (Nothing from
+// nextNode), and the copy quirk's key n is the entry at the compare position
+// that led to the stop node. The slot words S (global) stay exact, as in
+// pdr_serial (assembly and the change log read them); W[rank] = the block
+// holding the rank, NONE off the chain. Adds anchored at an orphan (off the
+// chain) walk the slot words like pdr_serial and then edit the blocks.
+constexpr uint32_t BLK_E = 64;          // entries per block (one per lane)
+constexpr uint32_t BLK_KMAX = 32766;    // ranks fit 15 bits; bit 15 = tombstone
+constexpr uint32_t BE_T = 0x8000u;
+constexpr uint32_t BE_NONE = 0xFFFFu;   // no block / an empty lane
+constexpr uint32_t BLK_MIN = PDR_SMALL;  // smaller dicts keep pdr_serial (env CRDTM_PDR_BLK_MIN)
+
+__host__ __device__ constexpr uint32_t blk_nbmax(uint32_t K) { return K / 32 + 8; }  // splits <= Adds / 32
+__host__ __device__ constexpr uint32_t blk_lds_words(uint32_t K) {  // 32-bit words of LDS
+  return blk_nbmax(K) * (BLK_E / 2) + (blk_nbmax(K) + 1) / 2 + (blk_nbmax(K) + 3) / 4 + K / 32 + 1;
+}
+
+template <bool ORIG>
+__device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* lds) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t D = ORIG ? I : p.I.src[I];
+  const uint32_t bound = ORIG ? NONE : p.I.bound[I];
+  const uint32_t base = p.I.base[I];
+  const uint32_t K = pdr_kcount(p, D);
+  const uint32_t rb = p.rbase[D];
+  const uint32_t nbmax = blk_nbmax(K);
+  uint16_t* const ent = reinterpret_cast<uint16_t*>(lds);
+  uint16_t* const bnx = ent + nbmax * BLK_E;
+  uint8_t* const bcn = reinterpret_cast<uint8_t*>(lds + nbmax * (BLK_E / 2) + (nbmax + 1) / 2);
+  uint32_t* const cpy = lds + nbmax * (BLK_E / 2) + (nbmax + 1) / 2 + (nbmax + 3) / 4;  // COPY bit per rank
+  uint32_t* const S = p.S + base;
+  uint32_t* const W = p.where + base;
+  for (uint32_t r = lane; r <= K; r += 64) {
+    S[r] = r == 0 ? (PM | SF_TOMB | SF_MADE) : PM;
+    W[r] = r == 0 ? 0u : NONE;
+  }
+  for (uint32_t j = lane; j <= K / 32; j += 64) cpy[j] = 0;
+  if (lane == 0) {
+    ent[0] = static_cast<uint16_t>(BE_T);  // the sentinel (rank 0, a Tombstone)
+    bnx[0] = static_cast<uint16_t>(BE_NONE);
+    bcn[0] = 1;
+  }
+  uint32_t nb = 1;
+#ifdef PDR_STATS
+  unsigned long long g_stc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long tw = 0, tk = 0, ti = 0, tt0 = clock64(), nwin = 0, nscan = 0;
+#define BT_MARK(acc) do { const long long t1_ = clock64(); acc += t1_ - tt0; tt0 = t1_; } while (0)
+#else
+#define BT_MARK(acc) do { } while (0)
+#endif
+  __syncthreads();
+  const uint32_t ob = rb, oe = p.rbase[D + 1] - 1;
+  bool done = false;
+  const bool logging = ORIG && p.log != nullptr && K + 1 >= p.log_min;
+  const uint32_t lcap = 4 * (oe + 1 - rb);
+  uint4* const lg = logging ? p.log + 4ULL * rb : nullptr;
+  uint32_t ln = 0;
+  auto logw = [&](uint32_t i, uint32_t k, uint32_t kind, uint32_t a, uint32_t b) {
+    if (logging) {
+      if (ln < lcap) lg[ln] = make_uint4(i, k | (kind << 30), a, b);
+      ++ln;
+    }
+  };
+  auto isc = [&](uint32_t r) -> uint32_t {  // COPY flag of rank r (uniform LDS read)
+    return (__builtin_amdgcn_readfirstlane(cpy[r >> 5]) >> (r & 31)) & 1u;
+  };
+  auto setc = [&](uint32_t r) {
+    if (lane == 0) cpy[r >> 5] |= 1u << (r & 31);
+  };
+  auto load_blk = [&](uint32_t b, uint32_t& cnt) -> uint32_t {  // this lane's entry, BE_NONE past the end
+    // (both reads issue together: the entry read does not wait for the count)
+    const uint32_t v = ent[b * BLK_E + lane];
+    cnt = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(bcn[b]));
+    return lane < cnt ? v : BE_NONE;
+  };
+  auto idx_of = [&](uint32_t e, uint32_t r) -> uint32_t {
+    const unsigned long long m = __ballot(e != BE_NONE && (e & 0x7FFFu) == r);
+    return m ? static_cast<uint32_t>(__builtin_ctzll(m)) : BLK_E;
+  };
+  auto rk = [&](uint32_t e, uint32_t j) -> uint32_t { return __builtin_amdgcn_readlane(e, j) & 0x7FFFu; };
+  // the entry v becomes index i + 1 of block b (a full block splits first)
+  auto blk_insert_e = [&](uint32_t b, uint32_t i, uint32_t v, uint32_t e, uint32_t cnt) {  // e, cnt: block b loaded
+    if (cnt == BLK_E) {
+      const uint32_t b2 = nb++;
+      if (lane >= 32) {
+        ent[b2 * BLK_E + lane - 32] = static_cast<uint16_t>(e);
+        W[e & 0x7FFFu] = b2;
+      }
+      if (lane == 0) {
+        bcn[b] = 32;
+        bcn[b2] = 32;
+        bnx[b2] = bnx[b];
+        bnx[b] = static_cast<uint16_t>(b2);
+      }
+      if (i >= 32) {
+        b = b2;
+        i -= 32;
+      }
+      e = load_blk(b, cnt);
+    }
+    if (lane > i && lane < cnt) ent[b * BLK_E + lane + 1] = static_cast<uint16_t>(e);
+    if (lane == i + 1) ent[b * BLK_E + lane] = static_cast<uint16_t>(v);
+    if (lane == 0) {
+      bcn[b] = static_cast<uint8_t>(cnt + 1);
+      W[v & 0x7FFFu] = b;
+    }
+  };
+  auto blk_insert = [&](uint32_t b, uint32_t i, uint32_t v) {
+    uint32_t cnt;
+    const uint32_t e = load_blk(b, cnt);
+    blk_insert_e(b, i, v, e, cnt);
+  };
+  // copy quirk: the chain entries after (b, i) up to and including rank
+  // `last` drop off the chain (orphans): off the blocks, ORPHAN in S (+ log)
+  auto blk_orphan_after = [&](uint32_t b, uint32_t i, uint32_t last, uint32_t op) {
+    uint32_t s0 = i + 1;
+    for (;;) {
+      uint32_t cnt;
+      const uint32_t e = load_blk(b, cnt);
+      const unsigned long long mr = __ballot(lane >= s0 && lane < cnt && (e & 0x7FFFu) == last);
+      const uint32_t end = mr ? static_cast<uint32_t>(__builtin_ctzll(mr)) + 1u : cnt;
+      const uint32_t k = end > s0 ? end - s0 : 0u;
+      if (lane >= s0 && lane < end) {
+        const uint32_t q = e & 0x7FFFu;
+        const uint32_t wq = S[q] | SF_ORPHAN;
+        S[q] = wq;
+        W[q] = NONE;
+        if (logging && ln + (lane - s0) < lcap) lg[ln + (lane - s0)] = make_uint4(op, q, wq, 0u);
+      }
+      ln += logging ? k : 0u;
+      if (k) {
+        if (lane >= end && lane < cnt) ent[b * BLK_E + lane - k] = static_cast<uint16_t>(e);
+        if (lane == 0) bcn[b] = static_cast<uint8_t>(cnt - k);
+      }
+      if (mr) break;
+      b = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(bnx[b]));
+      s0 = 0;
+      if (b == BE_NONE) break;
+    }
+  };
+  auto set_tomb = [&](uint32_t r) {  // the chain entry of rank r becomes a Tombstone
+    const uint32_t b = __builtin_amdgcn_readfirstlane(W[r]);
+    if (b == NONE) return;  // an orphan
+    uint32_t cnt;
+    const uint32_t e = load_blk(b, cnt);
+    const uint32_t j = idx_of(e, r);
+    if (lane == j) ent[b * BLK_E + lane] = static_cast<uint16_t>(e | BE_T);
+  };
+  auto clear_tomb = [&](uint32_t b, uint32_t j) {
+    if (lane == j) ent[b * BLK_E + lane] = static_cast<uint16_t>(ent[b * BLK_E + lane] & 0x7FFFu);
+  };
+  bool fail = false;  // no room (cannot happen: blk_nbmax bounds the splits); the batch is replayed sequentially
+  uint32_t nx_i = ob + lane < oe ? p.olist[ob + lane] : NONE;
+  unsigned long long nx_w = ob + lane < oe ? p.opw[ob + lane] : 0ULL;
+  for (uint32_t k0 = ob; k0 < oe && !done; k0 += 64) {
+    const uint32_t my_i = nx_i;
+    const unsigned long long my_w = nx_w;
+    const uint32_t kn = k0 + 64 + lane;
+    nx_i = kn < oe ? p.olist[kn] : NONE;
+    nx_w = kn < oe ? p.opw[kn] : 0ULL;
+    const uint32_t cntop = min(64u, oe - k0);
+    for (uint32_t jo = 0; jo < cntop; ++jo) {
+      const uint32_t i = __builtin_amdgcn_readlane(my_i, jo);
+      const uint32_t wlo = __builtin_amdgcn_readlane(static_cast<uint32_t>(my_w), jo);
+      const uint32_t whi = __builtin_amdgcn_readlane(static_cast<uint32_t>(my_w >> 32), jo);
+      if (i >= bound) {
+        done = true;
+        break;
+      }
+      if (nb + 2 >= nbmax) {  // (a split could not find a block)
+        fail = true;
+        done = true;
+        break;
+      }
+      uint8_t s;
+      if (whi >> 31) {  // deleteHelp
+        const uint32_t t = wlo & PM;
+        if (t == 0) {
+          s = ST_ALREADY;
+        } else {
+          const uint32_t wt = t == OW_NF ? 0u : ld_uniform(S, t);
+          if (!(wt & SF_MADE)) {
+            s = ST_NOTFOUND;
+          } else if (wt & SF_TOMB) {
+            s = ST_ALREADY;
+          } else {
+            S[t] = wt | SF_TOMB;
+            logw(i, t, 0, wt | SF_TOMB, 0);
+            set_tomb(t);
+            s = ST_APPLIED;
+          }
+        }
+      } else {  // addAfterHelp
+        const uint32_t x = wlo & PM;
+        const uint32_t an = ((wlo >> 24) | (whi << 8)) & PM;
+        BT_MARK(ti);
+        const uint32_t ba = (x == 0 || an == OW_NF) ? NONE : __builtin_amdgcn_readfirstlane(W[an]);
+        BT_MARK(tw);
+        if (x == 0) {
+          s = ST_ALREADY;
+        } else if (an == OW_NF || (ba == NONE && !(ld_uniform(S, an) & SF_MADE))) {
+          s = ST_NOTFOUND;
+        } else if (ba != NONE) {
+          // ---- findInsertion over the blocks ----
+          uint32_t b = ba, cnt;
+          uint32_t e = load_blk(b, cnt);
+          const uint32_t i0 = idx_of(e, an);
+          const bool an_tomb = (__builtin_amdgcn_readlane(e, i0) & BE_T) != 0;
+          uint32_t s0 = i0 + 1;
+          bool carry = true;                                  // the entry before the window: live or the anchor
+          uint32_t prev_r = an, prev_b = b, prev_i = i0;      // that entry
+          uint32_t nkc = an, nkc_b = b, nkc_i = i0;           // the compare entry that led to the latest node
+          uint32_t node, node_b, node_i, nk, nk_b, nk_i, nxt;  // result (nxt: the rank after node, PM = none)
+          uint32_t cur_b, cur_e, cur_cnt;                      // the block loaded last (saves a reload)
+          bool node_tomb = false;
+          for (;;) {
+#ifdef PDR_STATS
+            ++nwin;
+#endif
+            const bool valid = lane >= s0 && lane < cnt;
+            const unsigned long long ml = __ballot(valid && !(e & BE_T));
+            const unsigned long long mkey = __ballot(valid && (e & 0x7FFFu) < x);
+            const unsigned long long mval = __ballot(valid);
+            unsigned long long mc = (ml << 1) & mval;
+            if (carry && s0 < cnt) mc |= 1ULL << s0;
+            const unsigned long long m1 = mc & mkey;
+            const int j1 = m1 ? __builtin_ctzll(m1) : -1;
+            int j2 = -1;
+            if (ml) {
+              const int ll = 63 - __builtin_clzll(ml);
+              if (static_cast<uint32_t>(ll) + 1 < cnt) j2 = ll + 1;
+            } else if (carry && s0 < cnt) {
+              j2 = static_cast<int>(s0);
+            }
+            int j = -1;
+            if (j1 >= 0 && (j2 < 0 || j1 <= j2)) {
+              j = j1;
+            } else if (j2 >= 0) {  // nothing live after j2 in this block: anything live further on?
+              bool any = false;
+              for (uint32_t bb = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(bnx[b])); bb != BE_NONE && !any;
+                   bb = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(bnx[bb]))) {
+                uint32_t c2;
+                const uint32_t e2 = load_blk(bb, c2);
+                any = __ballot(lane < c2 && !(e2 & BE_T)) != 0;
+#ifdef PDR_STATS
+                ++nscan;
+#endif
+              }
+              if (!any) j = j2;  // nextNode is Nothing: stop
+            }
+            if (j >= 0) {
+              const uint32_t uj = static_cast<uint32_t>(j);
+              nxt = rk(e, uj);
+              cur_b = b;
+              cur_e = e;
+              cur_cnt = cnt;
+              if (uj == s0) {
+                node = prev_r;
+                node_b = prev_b;
+                node_i = prev_i;
+                node_tomb = node == an && an_tomb;
+                const bool first = node == an && prev_b == ba && prev_i == i0;
+                nk = first ? an : nkc;
+                nk_b = first ? ba : nkc_b;
+                nk_i = first ? i0 : nkc_i;
+              } else {
+                node = rk(e, uj - 1);
+                node_b = b;
+                node_i = uj - 1;
+                const unsigned long long mcl = mc & ((2ULL << (uj - 1)) - 1ULL);
+                if (mcl) {
+                  const uint32_t c = 63u - static_cast<uint32_t>(__builtin_clzll(mcl));
+                  nk = rk(e, c);
+                  nk_b = b;
+                  nk_i = c;
+                } else {
+                  nk = nkc;
+                  nk_b = nkc_b;
+                  nk_i = nkc_i;
+                }
+              }
+              break;
+            }
+            if (mc) {
+              const uint32_t c = 63u - static_cast<uint32_t>(__builtin_clzll(mc));
+              nkc = rk(e, c);
+              nkc_b = b;
+              nkc_i = c;
+            }
+            if (cnt > s0) {
+              carry = (ml >> (cnt - 1)) & 1ULL;
+              prev_r = rk(e, cnt - 1);
+              prev_b = b;
+              prev_i = cnt - 1;
+            }
+            const uint32_t bn = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(bnx[b]));
+            if (bn == BE_NONE) {  // the chain ends: `next node` is Nothing
+              node = prev_r;
+              node_b = prev_b;
+              node_i = prev_i;
+              node_tomb = node == an && an_tomb;
+              const bool first = node == an && prev_b == ba && prev_i == i0;
+              nk = first ? an : nkc;
+              nk_b = first ? ba : nkc_b;
+              nk_i = first ? i0 : nkc_i;
+              nxt = PM;
+              cur_b = b;
+              cur_e = e;
+              cur_cnt = cnt;
+              break;
+            }
+            b = bn;
+            s0 = 0;
+            e = load_blk(b, cnt);
+          }
+          BT_MARK(tk);
+          // ---- the two inserts (src/Internal/Node.elm:87-89) ----
+          const uint32_t wx = nxt | SF_MADE;
+          S[x] = wx;
+          logw(i, x, 0, wx, 0);
+          if (nk == node) {
+            const uint32_t wn = (node_tomb ? SF_TOMB : 0u) | SF_MADE | (isc(node) ? SF_COPY : 0u) | x;
+            S[node] = wn;
+            logw(i, node, 0, wn, 0);
+            if (node_b == cur_b) blk_insert_e(node_b, node_i, x, cur_e, cur_cnt);
+            else blk_insert(node_b, node_i, x);
+          } else {
+            // copy quirk: slot nk := copy of node with next = x;
+            // the entries after nk up to node drop off the chain
+            const bool ncopy = isc(node);
+            blk_orphan_after(nk_b, nk_i, node, i);
+            const uint32_t wk = x | SF_MADE | SF_COPY;
+            S[nk] = wk;
+            logw(i, nk, 0, wk, 0);
+            uint32_t cs, cd, cb;
+            if (ncopy) {
+              cs = p.qsrc[base + node];
+              cd = p.qcd[base + node];
+              cb = p.qcb[base + node];
+            } else {
+              cs = cd = p.rop[rb + node];
+              cb = bound;
+            }
+            p.qsrc[base + nk] = cs;
+            p.qcd[base + nk] = cd;
+            p.qcb[base + nk] = min(cb, i);
+            logw(i, nk, 1, cs, cd);
+            logw(i, nk, 2, min(cb, i), 0);
+            if (ORIG && lane == 0) atomicMin(&p.tcopy[p.rop[rb + nk]], i);
+            setc(nk);
+            clear_tomb(nk_b, nk_i);
+            blk_insert(nk_b, nk_i, x);
+          }
+          s = ST_APPLIED;
+        } else {
+          // ---- an orphan anchor: pdr_serial's walk over the slot words ----
+          uint32_t node = an, nk = an;
+          uint32_t wn = ld_uniform(S, node);
+          for (;;) {
+            const uint32_t rn = wn & PM;
+            if (rn == PM) break;
+            uint32_t wl = ld_uniform(S, rn);
+            const uint32_t live = pdr_next_live(S, K, lane, rn, wl STC_ARG);
+            if (live == PM) break;
+            if (x > rn) break;
+            nk = rn;
+            node = live;
+            wn = wl;
+          }
+          const uint32_t wk = nk == node ? wn : ld_uniform(S, nk);
+          const uint32_t wx = (wn & PM) | (wk & SF_ORPHAN) | SF_MADE;
+          S[x] = wx;
+          logw(i, x, 0, wx, 0);
+          const bool on_chain = !(wk & SF_ORPHAN);
+          if (nk == node) {
+            S[node] = (wn & ~PM) | x;
+            logw(i, node, 0, (wn & ~PM) | x, 0);
+            if (on_chain) {
+              const uint32_t b = __builtin_amdgcn_readfirstlane(W[node]);
+              uint32_t cnt;
+              const uint32_t e = load_blk(b, cnt);
+              blk_insert(b, idx_of(e, node), x);
+            }
+          } else {
+            uint32_t bk = NONE, ik = 0;
+            if (on_chain) {
+              bk = __builtin_amdgcn_readfirstlane(W[nk]);
+              uint32_t cnt;
+              const uint32_t e = load_blk(bk, cnt);
+              ik = idx_of(e, nk);
+              blk_orphan_after(bk, ik, node, i);
+              wn |= SF_ORPHAN;
+            }
+            const uint32_t wkn = x | (wn & ~PM & ~SF_ORPHAN) | (wk & SF_ORPHAN) | SF_COPY;
+            S[nk] = wkn;
+            logw(i, nk, 0, wkn, 0);
+            uint32_t cs, cd, cb;
+            if (wn & SF_COPY) {
+              cs = p.qsrc[base + node];
+              cd = p.qcd[base + node];
+              cb = p.qcb[base + node];
+            } else {
+              cs = cd = p.rop[rb + node];
+              cb = bound;
+            }
+            p.qsrc[base + nk] = cs;
+            p.qcd[base + nk] = cd;
+            p.qcb[base + nk] = min(cb, i);
+            logw(i, nk, 1, cs, cd);
+            logw(i, nk, 2, min(cb, i), 0);
+            if (ORIG && lane == 0) atomicMin(&p.tcopy[p.rop[rb + nk]], i);
+            setc(nk);
+            if (on_chain) {
+              clear_tomb(bk, ik);
+              blk_insert(bk, ik, x);
+            }
+          }
+          s = ST_APPLIED;
+        }
+      }
+      if (ORIG) st[i] = s;
+    }
+  }
+#ifdef PDR_STATS
+  if (ORIG && lane == 0 && K > 28000)
+    printf("pdr blk K=%u ops=%u windows %lld scans %lld cyc: W-load %lld walk %lld insert+rest %lld nb %u\n", K,
+           oe + 1 - rb, nwin, nscan, tw, tk, ti, nb);
+#endif
+  if (ORIG && lane == 0) p.logn[D] = (logging && ln <= lcap) ? ln : NONE;
+  if (fail && lane == 0) atomicOr(p.blk_fail, 1u);
+  for (uint32_t r = lane; r <= K; r += 64) p.inst[base + r] = I;
+}
+
+template <bool ORIG>
+__global__ void __launch_bounds__(64) k_pdr_blk(PdrCtx p, const uint32_t* list, uint8_t* st) {
+  extern __shared__ uint32_t blk_lds[];
+  pdr_blocked<ORIG>(p, st, list[blockIdx.x], blk_lds);
+}
+
 // Sort instances [i0, i1) into three size tiers: static LDS, dynamic LDS,
 // global memory. count = {tier sizes, largest slot count of tier 1}.
 struct PdrTiers {
-  uint32_t* list[3];
-  uint32_t* count;
+  uint32_t* list[4];
+  uint32_t* count;  // [0..3] tier sizes, [4] largest slot count of tier 1, [5] most ops of a dict, [6] tier 3's
+  uint32_t blk_min;  // dicts of more slots than this (and at most BLK_KMAX + 1) take pdr_blocked (tier 3)
 };
 
 __global__ void __launch_bounds__(BLOCK) k_pdr_tier(PdrCtx p, uint32_t i0, uint32_t i1, uint32_t big_cap,
@@ -422,10 +903,12 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_tier(PdrCtx p, uint32_t i0, uint3
     }
     if (I <= n) p.I.base[I] = p.rbase[I];
     const uint32_t slots = pdr_kcount(p, D) + 1;
-    const uint32_t t = slots <= PDR_SMALL ? 0u : (slots <= big_cap ? 1u : 2u);
+    uint32_t t = slots <= PDR_SMALL ? 0u : (slots <= big_cap ? 1u : 2u);
+    if (slots > tt.blk_min && slots <= BLK_KMAX + 1) t = 3;
     tt.list[t][atomicAdd(&tt.count[t], 1u)] = I;
-    if (t == 1) atomicMax(&tt.count[3], slots);
-    if (I <= n) atomicMax(&tt.count[4], p.rbase[I + 1] - p.rbase[I]);  // ops replayed by this dict's wave
+    if (t == 1) atomicMax(&tt.count[4], slots);
+    if (t == 3) atomicMax(&tt.count[6], slots);
+    if (I <= n) atomicMax(&tt.count[5], p.rbase[I + 1] - p.rbase[I]);  // ops replayed by this dict's wave
   }
 }
 
@@ -741,17 +1224,22 @@ static int pdr_run_tiers(crdtm_ctx* c, const PdrCtx& p, uint32_t i0, uint32_t i1
                          const PdrTiers& tt, uint32_t big_cap, uint32_t* hcount) {
   hipStream_t s = c->stream;
   if (i1 <= i0) return CRDTM_OK;
-  HIP_CHECK(hipMemsetAsync(tt.count, 0, 5 * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(tt.count, 0, 8 * sizeof(uint32_t), s));
   LAUNCH(k_pdr_tier, dim3(grid_for(i1 - i0)), dim3(BLOCK), 0, s, p, i0, i1, big_cap, tt);
-  HIP_CHECK(hipMemcpyAsync(hcount, tt.count, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(hcount, tt.count, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
   const uint32_t* h = hcount;
   if (h[0]) {
     if (orig) LAUNCH(k_pdr_small<true>, dim3(h[0]), dim3(64), 0, s, p, tt.list[0], st);
     else LAUNCH(k_pdr_small<false>, dim3(h[0]), dim3(64), 0, s, p, tt.list[0], st);
   }
+  if (h[3]) {
+    const size_t lds = static_cast<size_t>(blk_lds_words(h[6] - 1)) * sizeof(uint32_t);
+    if (orig) LAUNCH(k_pdr_blk<true>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st);
+    else LAUNCH(k_pdr_blk<false>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st);
+  }
   if (h[1]) {
-    const size_t lds = static_cast<size_t>(h[3]) * sizeof(uint32_t);
+    const size_t lds = static_cast<size_t>(h[4]) * sizeof(uint32_t);
     if (orig) LAUNCH(k_pdr_big<true>, dim3(h[1]), dim3(64), lds, s, p, tt.list[1], st);
     else LAUNCH(k_pdr_big<false>, dim3(h[1]), dim3(64), lds, s, p, tt.list[1], st);
   }
@@ -772,6 +1260,10 @@ static uint32_t pdr_big_cap(int device) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pdr_big<true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, v) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pdr_big<false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, v) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pdr_blk<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, v) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pdr_blk<false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, v) != hipSuccess)
       v = 64 * 1024;
     cached = v;
@@ -792,7 +1284,7 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   const size_t arena_mark = ws.used;
   int r;
   const uint32_t big_cap = pdr_big_cap(c->device);
-  uint32_t hcount[5];
+  uint32_t hcount[8];
 
   PdrCtx p;
   p.o = o;
@@ -852,16 +1344,41 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   HIP_CHECK(hipMemsetAsync(last, 0, 3ULL * SCAP * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(p.ilog, 0xFF, ICAP * sizeof(uint32_t), s));
   PdrTiers tt;
-  for (int k = 0; k < 3; ++k) tt.list[k] = ws.alloc<uint32_t>(ICAP);
-  tt.count = ws.alloc<uint32_t>(5);
+  for (int k = 0; k < 4; ++k) tt.list[k] = ws.alloc<uint32_t>(ICAP);
+  tt.count = ws.alloc<uint32_t>(8);
+  tt.blk_min = BLK_MIN;
+  if (const char* e = getenv("CRDTM_PDR_BLK_MIN")) tt.blk_min = static_cast<uint32_t>(strtoul(e, nullptr, 10));
+  // the blocked order needs LDS for its largest dict: else the older tiers
+  if (static_cast<uint64_t>(blk_lds_words(BLK_KMAX)) * sizeof(uint32_t) > static_cast<uint64_t>(big_cap) * 4)
+    tt.blk_min = BLK_KMAX + 1;
+  p.where = ws.alloc<uint32_t>(SCAP);
+  p.blk_fail = &dr->pdr_blk_fail;
+  HIP_CHECK(hipMemsetAsync(&dr->pdr_blk_fail, 0, sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(p.inst, 0xFF, static_cast<size_t>(SCAP) * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(p.ch, 0xFF, static_cast<size_t>(SCAP) * sizeof(uint32_t), s));
 
   // ---- P2 + P3 ----
+#ifdef PDR_STATS
+  {
+    unsigned long long z[8] = {};
+    bool f = false;
+    HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_pdr_stats), z, sizeof(z)));
+    HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(pdr_stat_on), &f, sizeof(f)));
+  }
+#endif
   if ((r = pdr_run_tiers(c, p, 0, n + 1, true, st, tt, big_cap, hcount))) return r;
-  res->serial_dicts = static_cast<uint64_t>(hcount[0]) + hcount[1] + hcount[2];
+#ifdef PDR_STATS
+  {
+    unsigned long long z[8];
+    HIP_CHECK(hipStreamSynchronize(s));
+    HIP_CHECK(hipMemcpyFromSymbol(z, HIP_SYMBOL(g_pdr_stats), sizeof(z)));
+    std::fprintf(stderr, "pdr stats: adds %llu walk-steps %llu window-steps %llu tomb-skips %llu quirks %llu\n",
+                 z[4], z[0], z[1], z[2], z[3]);
+  }
+#endif
+  res->serial_dicts = static_cast<uint64_t>(hcount[0]) + hcount[1] + hcount[2] + hcount[3];
   res->serial_ops = n;  // every op, in order within its dict
-  res->serial_max = hcount[4];
+  res->serial_max = hcount[5];
   LAUNCH(k_pdr_stats_reset, dim3(1), dim3(1), 0, s, dr);
   LAUNCH(k_pdr_conflict, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, n, in.tag, in.cur, in.addpar, in.dtime,
          p.tcopy, dr);
@@ -869,7 +1386,7 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   if ((r = sync_read(c))) return r;
   const DevResult h1 = *c->hres;
   const long long new_ts = t->timestamp + h1.own_ok_adds - t->own_bias;
-  if (h1.pdr_conflict || replica_of(new_ts) != replica_of(t->timestamp)) {
+  if (h1.pdr_conflict || h1.pdr_blk_fail || replica_of(new_ts) != replica_of(t->timestamp)) {
     ws.used = arena_mark;
     return CRDTM_OK;
   }
@@ -897,7 +1414,7 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   for (uint32_t level = 0;; ++level) {
     LAUNCH(k_pdr_jobs, dim3(grid_for(s1 - s0)), dim3(BLOCK), 0, s, p, ok, s0, s1, JCAP, dr);
     if ((r = sync_read(c))) return r;
-    if (c->hres->pdr_overflow || level > in.maxlen + 1) {  // no room: sequential replay
+    if (c->hres->pdr_overflow || c->hres->pdr_blk_fail || level > in.maxlen + 1) {  // no room: sequential replay
       *handled = false;
       ws.used = arena_mark;
       return CRDTM_OK;

@@ -334,3 +334,39 @@ def test_flat_run_tree_depth(depth):
     assert res.code == 0 and res.path_taken == N.PATH_CLOSED_FORM
     assert engine_summary(et) == oracle_summary(ot)
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+
+
+@pytest.mark.parametrize("log_min", ["512", "1"])
+def test_blocked_chain_order_forced(monkeypatch, log_min):
+    """Every dict through the blocked chain-order replay (pdr.hip pdr_blocked,
+    normally only dicts of more than 4096 slots): the adversarial quirk streams
+    (copies, orphans, orphan anchors re-entering the chain, trailing
+    tombstones), config 1 and config 2 shapes, with and without change-log
+    snapshots, against the oracle."""
+    from adversarial import adversarial
+    monkeypatch.setenv("CRDTM_PDR_BLK_MIN", "1")
+    monkeypatch.setenv("CRDTM_PDR_LOG_MIN", log_min)
+    paths = {}
+    for seed in range(0, 128):
+        n = [40, 120, 400, 1500][seed % 4]
+        ops = adversarial(seed, n, replicas=2 + seed % 3, max_depth=1 + seed % 4)
+        arrs = pack(ops)
+        ot, rc, oerr = oracle_apply_arrays(arrs, n)
+        et = CRDTree.init(0)
+        res = et.apply_arrays(arrs, n)
+        paths[res.path_taken] = paths.get(res.path_taken, 0) + 1
+        assert res.code == rc, seed
+        if rc != 0:
+            assert res.err_index == oerr, seed
+            continue
+        assert engine_summary(et) == oracle_summary(ot), seed
+        assert engine_log(et, 0) == oracle_log(ot, 0), seed
+    assert paths.get(N.PATH_DICT_REPLAY, 0) > 32, paths
+    for name in ("cfg1", "cfg2_small"):
+        s, n = synth_case(**CASES[name])
+        ot, rc, _ = oracle_apply_arrays(s, n)
+        et = CRDTree.init(0)
+        res = et.apply_arrays(s, n)
+        assert res.code == rc == 0 and res.path_taken == N.PATH_DICT_REPLAY, name
+        assert engine_summary(et) == oracle_summary(ot), name
+        assert np.array_equal(et.document_handles(), oracle_visible_vals(ot)), name
