@@ -300,7 +300,7 @@ def main():
     value = world * n * args.steps / elapsed
     # SURVEY.md 8d (config 2): how much of the merge ran as in-order replay, and its device-time share
     serial_ms = sum(v for nm, v in per_step.items() if nm.startswith(("k_pdr_small", "k_pdr_big", "k_pdr_huge",
-                                                                        "k_replay<", "k_replay")))
+                                                                        "k_pdr_blk", "k_replay")))
     serial_ms -= per_step.get("k_replay_index", 0.0)
     serial["time_share"] = serial_ms / max(1e-9, sum(per_step.values()))
     serial["fraction_of_ops"] = serial["ops"] / n

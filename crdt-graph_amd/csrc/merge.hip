@@ -3286,8 +3286,8 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   res->n_applied = h1.n_applied;
   res->n_already = h1.n_already;
 
-  // ---- the op log and the replicas table: they depend on the statuses only,
-  // so they run on the side stream while K2/K4 run here ----
+  // ---- the op log depends on the statuses only, so it is written on the
+  // side stream while K2/K4 run here ----
   // every op applied: the log is the batch (identity log index, the batch's
   // path offsets), so the two log scans are skipped
   const bool every = h1.n_applied == n;
@@ -3321,8 +3321,6 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
          static_cast<uint32_t>(t->log_npath), appl, plen);
   LAUNCH(k_log_tail, dim3(1), dim3(1), 0, c->side, t->d, static_cast<uint32_t>(t->log_n), &dr->log_n,
          static_cast<uint32_t>(t->log_npath), &dr->log_npath);
-  LAUNCH(k_rep_max, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, c->side, o, w.st, c->rtab);
-  LAUNCH(k_rep_out, dim3(g), dim3(BLOCK), 0, c->side, o, w.st, c->rtab, rep, &dr->n_replica_out, dr->rep_inline);
   HIP_CHECK(hipEventRecord(c->ev_join, c->side));
   struct Join {  // every exit waits for the side stream (the arena is reused by the next call)
     crdtm_ctx* c;
@@ -3382,6 +3380,10 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   LAUNCH(k_commit_nodes, dim3(g), dim3(BLOCK), 0, s, o, w, t->d, ca, kept, live, appl, nextn, fc, excl,
                      t->d.doc);
   LAUNCH(k_commit_root, dim3(1), dim3(1), 0, s, o, t->d, kept, fc, 1u);
+  // (the replica fold stays here: beside the order kernels its hot table
+  // lines slowed both streams)
+  LAUNCH(k_rep_max, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, s, o, w.st, c->rtab);
+  LAUNCH(k_rep_out, dim3(g), dim3(BLOCK), 0, s, o, w.st, c->rtab, rep, &dr->n_replica_out, dr->rep_inline);
   if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n, NONE, st_out);
   HIP_CHECK(hipStreamWaitEvent(s, c->ev_join, 0));
   if ((r = sync_read(c))) return r;

@@ -501,7 +501,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
   uint32_t ln = 0;
   auto logw = [&](uint32_t i, uint32_t k, uint32_t kind, uint32_t a, uint32_t b) {
     if (logging) {
-      if (ln < lcap) lg[ln] = make_uint4(i, k | (kind << 30), a, b);
+      if (ln < lcap && lane == 0) lg[ln] = make_uint4(i, k | (kind << 30), a, b);
       ++ln;
     }
   };
@@ -582,8 +582,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
       if (b == BE_NONE) break;
     }
   };
-  auto set_tomb = [&](uint32_t r) {  // the chain entry of rank r becomes a Tombstone
-    const uint32_t b = __builtin_amdgcn_readfirstlane(W[r]);
+  auto set_tomb = [&](uint32_t r, uint32_t b) {  // the chain entry of rank r (in block b) becomes a Tombstone
     if (b == NONE) return;  // an orphan
     uint32_t cnt;
     const uint32_t e = load_blk(b, cnt);
@@ -623,14 +622,15 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
           s = ST_ALREADY;
         } else {
           const uint32_t wt = t == OW_NF ? 0u : ld_uniform(S, t);
+          const uint32_t bt = t == OW_NF ? NONE : __builtin_amdgcn_readfirstlane(W[t]);  // (issued with S[t])
           if (!(wt & SF_MADE)) {
             s = ST_NOTFOUND;
           } else if (wt & SF_TOMB) {
             s = ST_ALREADY;
           } else {
-            S[t] = wt | SF_TOMB;
+            if (lane == 0) S[t] = wt | SF_TOMB;
             logw(i, t, 0, wt | SF_TOMB, 0);
-            set_tomb(t);
+            set_tomb(t, bt);
             s = ST_APPLIED;
           }
         }
@@ -760,11 +760,11 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
           BT_MARK(tk);
           // ---- the two inserts (src/Internal/Node.elm:87-89) ----
           const uint32_t wx = nxt | SF_MADE;
-          S[x] = wx;
+          if (lane == 0) S[x] = wx;
           logw(i, x, 0, wx, 0);
           if (nk == node) {
             const uint32_t wn = (node_tomb ? SF_TOMB : 0u) | SF_MADE | (isc(node) ? SF_COPY : 0u) | x;
-            S[node] = wn;
+            if (lane == 0) S[node] = wn;
             logw(i, node, 0, wn, 0);
             if (node_b == cur_b) blk_insert_e(node_b, node_i, x, cur_e, cur_cnt);
             else blk_insert(node_b, node_i, x);
@@ -774,7 +774,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
             const bool ncopy = isc(node);
             blk_orphan_after(nk_b, nk_i, node, i);
             const uint32_t wk = x | SF_MADE | SF_COPY;
-            S[nk] = wk;
+            if (lane == 0) S[nk] = wk;
             logw(i, nk, 0, wk, 0);
             uint32_t cs, cd, cb;
             if (ncopy) {
@@ -785,9 +785,11 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
               cs = cd = p.rop[rb + node];
               cb = bound;
             }
-            p.qsrc[base + nk] = cs;
-            p.qcd[base + nk] = cd;
-            p.qcb[base + nk] = min(cb, i);
+            if (lane == 0) {
+              p.qsrc[base + nk] = cs;
+              p.qcd[base + nk] = cd;
+              p.qcb[base + nk] = min(cb, i);
+            }
             logw(i, nk, 1, cs, cd);
             logw(i, nk, 2, min(cb, i), 0);
             if (ORIG && lane == 0) atomicMin(&p.tcopy[p.rop[rb + nk]], i);
@@ -813,11 +815,11 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
           }
           const uint32_t wk = nk == node ? wn : ld_uniform(S, nk);
           const uint32_t wx = (wn & PM) | (wk & SF_ORPHAN) | SF_MADE;
-          S[x] = wx;
+          if (lane == 0) S[x] = wx;
           logw(i, x, 0, wx, 0);
           const bool on_chain = !(wk & SF_ORPHAN);
           if (nk == node) {
-            S[node] = (wn & ~PM) | x;
+            if (lane == 0) S[node] = (wn & ~PM) | x;
             logw(i, node, 0, (wn & ~PM) | x, 0);
             if (on_chain) {
               const uint32_t b = __builtin_amdgcn_readfirstlane(W[node]);
@@ -836,7 +838,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
               wn |= SF_ORPHAN;
             }
             const uint32_t wkn = x | (wn & ~PM & ~SF_ORPHAN) | (wk & SF_ORPHAN) | SF_COPY;
-            S[nk] = wkn;
+            if (lane == 0) S[nk] = wkn;
             logw(i, nk, 0, wkn, 0);
             uint32_t cs, cd, cb;
             if (wn & SF_COPY) {
@@ -847,9 +849,11 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
               cs = cd = p.rop[rb + node];
               cb = bound;
             }
-            p.qsrc[base + nk] = cs;
-            p.qcd[base + nk] = cd;
-            p.qcb[base + nk] = min(cb, i);
+            if (lane == 0) {
+              p.qsrc[base + nk] = cs;
+              p.qcd[base + nk] = cd;
+              p.qcb[base + nk] = min(cb, i);
+            }
             logw(i, nk, 1, cs, cd);
             logw(i, nk, 2, min(cb, i), 0);
             if (ORIG && lane == 0) atomicMin(&p.tcopy[p.rop[rb + nk]], i);
@@ -862,7 +866,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
           s = ST_APPLIED;
         }
       }
-      if (ORIG) st[i] = s;
+      if (ORIG && lane == 0) st[i] = s;
     }
   }
 #ifdef PDR_STATS
