@@ -107,12 +107,18 @@ int crdtm_tree_create(crdtm_ctx *ctx, int64_t replica_id, crdtm_tree **out);
 int crdtm_tree_destroy(crdtm_tree *t);
 /* Reset to `init replica_id` keeping the device allocations (benchmarks, pooling). */
 int crdtm_tree_reset(crdtm_tree *t, int64_t replica_id);
-/* Elm values are persistent: clone before apply to keep the old version. */
+/* Elm values are persistent (src/CRDTree.elm:228-232): clone before apply to keep
+ * the old version. O(1): the versions share the device state until one of them
+ * is written (apply / reset), which then takes a private copy (copy on write).
+ * Handles of one context are not used concurrently (see Threading). */
 int crdtm_tree_clone(const crdtm_tree *t, crdtm_tree **out);
 
 /* CRDTree.apply (src/CRDTree.elm:265-269): apply (Batch ops) when is_batch,
  * else the single op ops[0]. Sequential-apply semantics in array order; the
  * first failing op aborts and leaves the tree unchanged (transactional).
+ * Any tree, fresh or not: a tree that holds state merges log ++ ops on the
+ * parallel paths (res->flags & CRDTM_FLAG_REMERGE) or, when a sequential path
+ * is needed, replays ops on the existing state.
  * ops_on_device: 1 if every array of `ops` is device memory (inputs already
  * resident in HBM), 0 for host memory (copied in on the context stream).
  * status_out: optional device (ops_on_device) or host array [n_ops] of CRDTM_ST_*.
