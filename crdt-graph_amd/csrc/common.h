@@ -81,7 +81,6 @@ struct DevResult {
   uint32_t pdr_conflict;    // per-dict replay: a path crossed a key the copy quirk refilled
   uint32_t pdr_jobs;        // per-dict replay: snapshot dicts created so far
   uint32_t pdr_overflow;    // per-dict replay: snapshot room exhausted
-  uint32_t pdr_blk_fail;    // per-dict replay: a blocked chain order ran out of blocks (cannot happen)
   uint32_t pdr_dicts;       // per-dict replay: dicts of the new state
   uint32_t pdr_slots;       // per-dict replay: slots of the new state
   uint32_t since_end;       // operationsSince: 1 + log index of the newest Add with the asked ts

@@ -85,8 +85,8 @@ struct PdrCtx {
   uint32_t* logn;          // per dict: entries logged, NONE = no log (small dict or room exhausted)
   uint32_t* ilog;          // per instance: snapshots rebuilt from the log -> prefix length, else NONE
   uint32_t log_min;        // slots a dict needs to keep a change log
-  uint32_t* where;         // per slot position: the chain block of the rank (pdr_blocked), NONE off the chain
-  uint32_t* blk_fail;      // DevResult::pdr_blk_fail
+  uint32_t* where;         // per slot position: pdr_blocked's compaction scratch
+  uint32_t blk_spare;      // 0, or (tests) blocks beyond a repacked chain before pdr_blocked compacts
   PdrInst I;
 };
 
@@ -444,53 +444,55 @@ __global__ void __launch_bounds__(64) k_pdr_huge(PdrCtx p, const uint32_t* list,
 // moves to the next live node), the walk stops at the first compare position
 // whose rank is below x's, or where nothing live follows (Nothing from
 // nextNode), and the copy quirk's key n is the entry at the compare position
-// that led to the stop node. The slot words S (global) stay exact, as in
-// pdr_serial (assembly and the change log read them); W[rank] = the block
-// holding the rank, NONE off the chain. Adds anchored at an orphan (off the
-// chain) walk the slot words like pdr_serial and then edit the blocks.
+// that led to the stop node. Every rank's flags and block live in LDS too
+// (wf), so an op touches global memory only with stores: the slot words S
+// (exact, as in pdr_serial: the assembly and the change log read them) and
+// the log. (A global load would wait for every store before it: gfx9's vmcnt
+// counts both.) Adds anchored at an orphan (off the chain, rare) walk the
+// slot words like pdr_serial and then edit the blocks.
 constexpr uint32_t BLK_E = 64;          // entries per block (one per lane)
 constexpr uint32_t BLK_KMAX = 32766;    // ranks fit 15 bits; bit 15 = tombstone
 constexpr uint32_t BE_T = 0x8000u;
-constexpr uint32_t BE_NONE = 0xFFFFu;   // no block / an empty lane
+constexpr uint32_t BE_NONE = 0xFFFFu;   // an empty lane
 constexpr uint32_t BLK_MIN = PDR_SMALL;  // smaller dicts keep pdr_serial (env CRDTM_PDR_BLK_MIN)
+constexpr uint32_t BLK_FILL = 56;        // entries per block after a compaction
+// wf[rank]: block (11 bits, WB_NONE = off the chain) | MADE | TOMB | ORPHAN | COPY
+constexpr uint32_t WB_NONE = 0x7FFu, WF_MADE = 1u << 11, WF_TOMB = 1u << 12, WF_ORPH = 1u << 13, WF_COPY = 1u << 14;
+// block meta word: entries (8 bits) | next block << 8 (WB_NONE = the last block)
 
-__host__ __device__ constexpr uint32_t blk_nbmax(uint32_t K) { return K / 32 + 8; }  // splits <= Adds / 32
-__host__ __device__ constexpr uint32_t blk_lds_words(uint32_t K) {  // 32-bit words of LDS
-  return blk_nbmax(K) * (BLK_E / 2) + (blk_nbmax(K) + 1) / 2 + (blk_nbmax(K) + 3) / 4 + K / 32 + 1;
+__device__ __forceinline__ uint32_t wf_sflags(uint32_t w) {  // the slot-word flags of a wf entry
+  return ((w & WF_MADE) ? SF_MADE : 0u) | ((w & WF_TOMB) ? SF_TOMB : 0u) | ((w & WF_ORPH) ? SF_ORPHAN : 0u) |
+         ((w & WF_COPY) ? SF_COPY : 0u);
 }
 
 template <bool ORIG>
-__device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* lds) {
+__device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* lds, uint32_t lds_words) {
   const uint32_t lane = threadIdx.x;
   const uint32_t D = ORIG ? I : p.I.src[I];
   const uint32_t bound = ORIG ? NONE : p.I.bound[I];
   const uint32_t base = p.I.base[I];
   const uint32_t K = pdr_kcount(p, D);
   const uint32_t rb = p.rbase[D];
-  const uint32_t nbmax = blk_nbmax(K);
-  uint16_t* const ent = reinterpret_cast<uint16_t*>(lds);
-  uint16_t* const bnx = ent + nbmax * BLK_E;
-  uint8_t* const bcn = reinterpret_cast<uint8_t*>(lds + nbmax * (BLK_E / 2) + (nbmax + 1) / 2);
-  uint32_t* const cpy = lds + nbmax * (BLK_E / 2) + (nbmax + 1) / 2 + (nbmax + 3) / 4;  // COPY bit per rank
+  uint16_t* const wf = reinterpret_cast<uint16_t*>(lds);
+  const uint32_t wf_words = (K + 2) / 2;
+  uint32_t* const meta = lds + wf_words;
+  uint32_t nbmax = min(WB_NONE, (lds_words - wf_words) / (1 + BLK_E / 2));
+  if (p.blk_spare)  // (tests: few spare blocks, so compactions happen)
+    nbmax = min(nbmax, (K + 1 + BLK_FILL - 1) / BLK_FILL + p.blk_spare);
+  uint16_t* const ent = reinterpret_cast<uint16_t*>(meta + nbmax);
   uint32_t* const S = p.S + base;
-  uint32_t* const W = p.where + base;
+  uint32_t* const tmp = p.where + base;  // compaction scratch
   for (uint32_t r = lane; r <= K; r += 64) {
     S[r] = r == 0 ? (PM | SF_TOMB | SF_MADE) : PM;
-    W[r] = r == 0 ? 0u : NONE;
+    wf[r] = static_cast<uint16_t>(r == 0 ? (0u | WF_MADE | WF_TOMB) : WB_NONE);
   }
-  for (uint32_t j = lane; j <= K / 32; j += 64) cpy[j] = 0;
   if (lane == 0) {
     ent[0] = static_cast<uint16_t>(BE_T);  // the sentinel (rank 0, a Tombstone)
-    bnx[0] = static_cast<uint16_t>(BE_NONE);
-    bcn[0] = 1;
+    meta[0] = 1u | (WB_NONE << 8);
   }
   uint32_t nb = 1;
 #ifdef PDR_STATS
   unsigned long long g_stc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  long long tw = 0, tk = 0, ti = 0, tt0 = clock64(), nwin = 0, nscan = 0;
-#define BT_MARK(acc) do { const long long t1_ = clock64(); acc += t1_ - tt0; tt0 = t1_; } while (0)
-#else
-#define BT_MARK(acc) do { } while (0)
 #endif
   __syncthreads();
   const uint32_t ob = rb, oe = p.rbase[D + 1] - 1;
@@ -505,16 +507,15 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
       ++ln;
     }
   };
-  auto isc = [&](uint32_t r) -> uint32_t {  // COPY flag of rank r (uniform LDS read)
-    return (__builtin_amdgcn_readfirstlane(cpy[r >> 5]) >> (r & 31)) & 1u;
+  auto wfu = [&](uint32_t r) -> uint32_t { return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wf[r])); };
+  auto setwf = [&](uint32_t r, uint32_t v) {
+    if (lane == 0) wf[r] = static_cast<uint16_t>(v);
   };
-  auto setc = [&](uint32_t r) {
-    if (lane == 0) cpy[r >> 5] |= 1u << (r & 31);
-  };
-  auto load_blk = [&](uint32_t b, uint32_t& cnt) -> uint32_t {  // this lane's entry, BE_NONE past the end
-    // (both reads issue together: the entry read does not wait for the count)
-    const uint32_t v = ent[b * BLK_E + lane];
-    cnt = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(bcn[b]));
+  auto load_blk = [&](uint32_t b, uint32_t& cnt, uint32_t& nxb) -> uint32_t {  // this lane's entry, BE_NONE past the end
+    const uint32_t v = ent[b * BLK_E + lane];  // (issued with the meta read)
+    const uint32_t m = __builtin_amdgcn_readfirstlane(meta[b]);
+    cnt = m & 0xFFu;
+    nxb = m >> 8;
     return lane < cnt ? v : BE_NONE;
   };
   auto idx_of = [&](uint32_t e, uint32_t r) -> uint32_t {
@@ -522,77 +523,120 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
     return m ? static_cast<uint32_t>(__builtin_ctzll(m)) : BLK_E;
   };
   auto rk = [&](uint32_t e, uint32_t j) -> uint32_t { return __builtin_amdgcn_readlane(e, j) & 0x7FFFu; };
-  // the entry v becomes index i + 1 of block b (a full block splits first)
-  auto blk_insert_e = [&](uint32_t b, uint32_t i, uint32_t v, uint32_t e, uint32_t cnt) {  // e, cnt: block b loaded
+  // the first entry after block b's end, along the chain (PM: none)
+  auto first_after = [&](uint32_t nxb) -> uint32_t {
+    for (uint32_t bb = nxb; bb != WB_NONE;) {
+      const uint32_t m = __builtin_amdgcn_readfirstlane(meta[bb]);
+      if (m & 0xFFu) return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(ent[bb * BLK_E])) & 0x7FFFu;
+      bb = m >> 8;
+    }
+    return PM;
+  };
+  // repack the whole chain BLK_FILL entries per block (when a split finds no free block)
+  auto compact = [&]() {
+    uint32_t pos = 0;
+    for (uint32_t b = 0; b != WB_NONE;) {
+      uint32_t cnt, nxb;
+      const uint32_t e = load_blk(b, cnt, nxb);
+      if (lane < cnt) tmp[pos + lane] = e;
+      pos += cnt;
+      b = nxb;
+    }
+    __threadfence();  // the scratch writes land before they are read back (and no stale L1 lines)
+    const uint32_t nbn = (pos + BLK_FILL - 1) / BLK_FILL;
+    for (uint32_t k = 0; k < nbn; ++k) {
+      const uint32_t len = min(BLK_FILL, pos - k * BLK_FILL);
+      const uint32_t e = lane < len ? tmp[k * BLK_FILL + lane] : BE_NONE;
+      if (lane < len) {
+        ent[k * BLK_E + lane] = static_cast<uint16_t>(e);
+        const uint32_t r = e & 0x7FFFu;
+        wf[r] = static_cast<uint16_t>((wf[r] & ~WB_NONE) | k);
+      }
+      if (lane == 0) meta[k] = len | ((k + 1 < nbn ? k + 1 : WB_NONE) << 8);
+    }
+    nb = nbn;
+  };
+  // v becomes the entry after rank `prev`, which sits at index i of block b (e, cnt, nxb: block b loaded)
+  auto blk_insert_e = [&](uint32_t prev, uint32_t b, uint32_t i, uint32_t v, uint32_t e, uint32_t cnt,
+                          uint32_t nxb) {
     if (cnt == BLK_E) {
+      if (nb >= nbmax) {  // no free block: repack, then find prev again
+        compact();
+        b = wfu(prev) & WB_NONE;
+        e = load_blk(b, cnt, nxb);
+        i = idx_of(e, prev);
+      }
+    }
+    if (cnt == BLK_E) {  // split: the upper half moves to a fresh block
       const uint32_t b2 = nb++;
       if (lane >= 32) {
         ent[b2 * BLK_E + lane - 32] = static_cast<uint16_t>(e);
-        W[e & 0x7FFFu] = b2;
+        const uint32_t r = e & 0x7FFFu;
+        wf[r] = static_cast<uint16_t>((wf[r] & ~WB_NONE) | b2);
       }
       if (lane == 0) {
-        bcn[b] = 32;
-        bcn[b2] = 32;
-        bnx[b2] = bnx[b];
-        bnx[b] = static_cast<uint16_t>(b2);
+        meta[b2] = 32u | (nxb << 8);
+        meta[b] = 32u | (b2 << 8);
       }
-      if (i >= 32) {
+      const bool hi = i >= 32;  // the insert goes to the new upper block
+      if (hi) {
         b = b2;
         i -= 32;
+        e = __shfl_down(e, 32, 64);
+      } else {
+        nxb = b2;
       }
-      e = load_blk(b, cnt);
+      if (lane >= 32) e = BE_NONE;
+      cnt = 32;
     }
     if (lane > i && lane < cnt) ent[b * BLK_E + lane + 1] = static_cast<uint16_t>(e);
     if (lane == i + 1) ent[b * BLK_E + lane] = static_cast<uint16_t>(v);
     if (lane == 0) {
-      bcn[b] = static_cast<uint8_t>(cnt + 1);
-      W[v & 0x7FFFu] = b;
+      meta[b] = (cnt + 1) | (nxb << 8);
+      const uint32_t r = v & 0x7FFFu;
+      wf[r] = static_cast<uint16_t>((wf[r] & ~WB_NONE) | b);
     }
   };
-  auto blk_insert = [&](uint32_t b, uint32_t i, uint32_t v) {
-    uint32_t cnt;
-    const uint32_t e = load_blk(b, cnt);
-    blk_insert_e(b, i, v, e, cnt);
+  auto blk_insert = [&](uint32_t prev, uint32_t v) {
+    const uint32_t b = wfu(prev) & WB_NONE;
+    uint32_t cnt, nxb;
+    const uint32_t e = load_blk(b, cnt, nxb);
+    blk_insert_e(prev, b, idx_of(e, prev), v, e, cnt, nxb);
   };
-  // copy quirk: the chain entries after (b, i) up to and including rank
-  // `last` drop off the chain (orphans): off the blocks, ORPHAN in S (+ log)
-  auto blk_orphan_after = [&](uint32_t b, uint32_t i, uint32_t last, uint32_t op) {
-    uint32_t s0 = i + 1;
+  // copy quirk: the chain entries after rank `after` up to and including
+  // rank `last` drop off the chain (orphans): off the blocks, ORPHAN in wf
+  // and in their slot words (+ log)
+  auto blk_orphan_after = [&](uint32_t after, uint32_t last, uint32_t op) {
+    uint32_t b = wfu(after) & WB_NONE;
+    uint32_t cnt, nxb;
+    uint32_t e = load_blk(b, cnt, nxb);
+    uint32_t s0 = idx_of(e, after) + 1;
     for (;;) {
-      uint32_t cnt;
-      const uint32_t e = load_blk(b, cnt);
       const unsigned long long mr = __ballot(lane >= s0 && lane < cnt && (e & 0x7FFFu) == last);
       const uint32_t end = mr ? static_cast<uint32_t>(__builtin_ctzll(mr)) + 1u : cnt;
       const uint32_t k = end > s0 ? end - s0 : 0u;
+      const uint32_t succ_last = end < cnt ? rk(e, end) : first_after(nxb);
+      const uint32_t en = __shfl_down(e, 1, 64);
       if (lane >= s0 && lane < end) {
         const uint32_t q = e & 0x7FFFu;
-        const uint32_t wq = S[q] | SF_ORPHAN;
+        const uint32_t nq = lane + 1 < end ? (en & 0x7FFFu) : succ_last;
+        const uint32_t w = (wf[q] | WF_ORPH) | WB_NONE;
+        wf[q] = static_cast<uint16_t>(w);
+        const uint32_t wq = nq | wf_sflags(w);
         S[q] = wq;
-        W[q] = NONE;
         if (logging && ln + (lane - s0) < lcap) lg[ln + (lane - s0)] = make_uint4(op, q, wq, 0u);
       }
       ln += logging ? k : 0u;
       if (k) {
         if (lane >= end && lane < cnt) ent[b * BLK_E + lane - k] = static_cast<uint16_t>(e);
-        if (lane == 0) bcn[b] = static_cast<uint8_t>(cnt - k);
+        if (lane == 0) meta[b] = (cnt - k) | (nxb << 8);
       }
-      if (mr) break;
-      b = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(bnx[b]));
+      if (mr || nxb == WB_NONE) break;
+      b = nxb;
       s0 = 0;
-      if (b == BE_NONE) break;
+      e = load_blk(b, cnt, nxb);
     }
   };
-  auto set_tomb = [&](uint32_t r, uint32_t b) {  // the chain entry of rank r (in block b) becomes a Tombstone
-    if (b == NONE) return;  // an orphan
-    uint32_t cnt;
-    const uint32_t e = load_blk(b, cnt);
-    const uint32_t j = idx_of(e, r);
-    if (lane == j) ent[b * BLK_E + lane] = static_cast<uint16_t>(e | BE_T);
-  };
-  auto clear_tomb = [&](uint32_t b, uint32_t j) {
-    if (lane == j) ent[b * BLK_E + lane] = static_cast<uint16_t>(ent[b * BLK_E + lane] & 0x7FFFu);
-  };
-  bool fail = false;  // no room (cannot happen: blk_nbmax bounds the splits); the batch is replayed sequentially
   uint32_t nx_i = ob + lane < oe ? p.olist[ob + lane] : NONE;
   unsigned long long nx_w = ob + lane < oe ? p.opw[ob + lane] : 0ULL;
   for (uint32_t k0 = ob; k0 < oe && !done; k0 += 64) {
@@ -610,57 +654,56 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
         done = true;
         break;
       }
-      if (nb + 2 >= nbmax) {  // (a split could not find a block)
-        fail = true;
-        done = true;
-        break;
-      }
       uint8_t s;
       if (whi >> 31) {  // deleteHelp
         const uint32_t t = wlo & PM;
+        const uint32_t w = (t == 0 || t == OW_NF) ? 0u : wfu(t);
         if (t == 0) {
           s = ST_ALREADY;
+        } else if (!(w & WF_MADE)) {
+          s = ST_NOTFOUND;
+        } else if (w & WF_TOMB) {
+          s = ST_ALREADY;
         } else {
-          const uint32_t wt = t == OW_NF ? 0u : ld_uniform(S, t);
-          const uint32_t bt = t == OW_NF ? NONE : __builtin_amdgcn_readfirstlane(W[t]);  // (issued with S[t])
-          if (!(wt & SF_MADE)) {
-            s = ST_NOTFOUND;
-          } else if (wt & SF_TOMB) {
-            s = ST_ALREADY;
-          } else {
-            if (lane == 0) S[t] = wt | SF_TOMB;
-            logw(i, t, 0, wt | SF_TOMB, 0);
-            set_tomb(t, bt);
-            s = ST_APPLIED;
+          const uint32_t b = w & WB_NONE;
+          uint32_t nxt;
+          if (b != WB_NONE) {  // on the chain: the entry becomes a Tombstone
+            uint32_t cnt, nxb;
+            const uint32_t e = load_blk(b, cnt, nxb);
+            const uint32_t j = idx_of(e, t);
+            if (lane == j) ent[b * BLK_E + lane] = static_cast<uint16_t>(e | BE_T);
+            nxt = j + 1 < cnt ? rk(e, j + 1) : first_after(nxb);
+          } else {  // an orphan: its next key lives in its slot word only
+            nxt = ld_uniform(S, t) & PM;
           }
+          setwf(t, w | WF_TOMB);
+          const uint32_t wt = nxt | wf_sflags(w | WF_TOMB);
+          if (lane == 0) S[t] = wt;
+          logw(i, t, 0, wt, 0);
+          s = ST_APPLIED;
         }
       } else {  // addAfterHelp
         const uint32_t x = wlo & PM;
         const uint32_t an = ((wlo >> 24) | (whi << 8)) & PM;
-        BT_MARK(ti);
-        const uint32_t ba = (x == 0 || an == OW_NF) ? NONE : __builtin_amdgcn_readfirstlane(W[an]);
-        BT_MARK(tw);
+        const uint32_t wa = (x == 0 || an == OW_NF) ? 0u : wfu(an);
         if (x == 0) {
           s = ST_ALREADY;
-        } else if (an == OW_NF || (ba == NONE && !(ld_uniform(S, an) & SF_MADE))) {
+        } else if (!(wa & WF_MADE)) {
           s = ST_NOTFOUND;
-        } else if (ba != NONE) {
+        } else if ((wa & WB_NONE) != WB_NONE) {
           // ---- findInsertion over the blocks ----
-          uint32_t b = ba, cnt;
-          uint32_t e = load_blk(b, cnt);
+          const uint32_t ba = wa & WB_NONE;
+          uint32_t b = ba, cnt, nxb;
+          uint32_t e = load_blk(b, cnt, nxb);
           const uint32_t i0 = idx_of(e, an);
-          const bool an_tomb = (__builtin_amdgcn_readlane(e, i0) & BE_T) != 0;
           uint32_t s0 = i0 + 1;
-          bool carry = true;                                  // the entry before the window: live or the anchor
-          uint32_t prev_r = an, prev_b = b, prev_i = i0;      // that entry
-          uint32_t nkc = an, nkc_b = b, nkc_i = i0;           // the compare entry that led to the latest node
-          uint32_t node, node_b, node_i, nk, nk_b, nk_i, nxt;  // result (nxt: the rank after node, PM = none)
-          uint32_t cur_b, cur_e, cur_cnt;                      // the block loaded last (saves a reload)
-          bool node_tomb = false;
+          bool carry = true;        // the entry before the window: live or the anchor
+          uint32_t prev_r = an;     // that entry
+          uint32_t nkc = an;        // the compare entry that led to the latest node
+          bool at_anchor = true;    // no node visited yet
+          uint32_t node, nk, nxt;   // result (nxt: the rank after node, PM = none)
+          uint32_t cur_b = b, cur_e = e, cur_cnt = cnt, cur_nxb = nxb, node_i = i0;  // node's block (when loaded)
           for (;;) {
-#ifdef PDR_STATS
-            ++nwin;
-#endif
             const bool valid = lane >= s0 && lane < cnt;
             const unsigned long long ml = __ballot(valid && !(e & BE_T));
             const unsigned long long mkey = __ballot(valid && (e & 0x7FFFu) < x);
@@ -681,103 +724,88 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
               j = j1;
             } else if (j2 >= 0) {  // nothing live after j2 in this block: anything live further on?
               bool any = false;
-              for (uint32_t bb = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(bnx[b])); bb != BE_NONE && !any;
-                   bb = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(bnx[bb]))) {
-                uint32_t c2;
-                const uint32_t e2 = load_blk(bb, c2);
+              for (uint32_t bb = nxb; bb != WB_NONE && !any;) {
+                uint32_t c2, n2;
+                const uint32_t e2 = load_blk(bb, c2, n2);
                 any = __ballot(lane < c2 && !(e2 & BE_T)) != 0;
-#ifdef PDR_STATS
-                ++nscan;
-#endif
+                bb = n2;
               }
               if (!any) j = j2;  // nextNode is Nothing: stop
             }
             if (j >= 0) {
               const uint32_t uj = static_cast<uint32_t>(j);
               nxt = rk(e, uj);
-              cur_b = b;
-              cur_e = e;
-              cur_cnt = cnt;
-              if (uj == s0) {
+              if (uj == s0) {  // node = the entry before the window
                 node = prev_r;
-                node_b = prev_b;
-                node_i = prev_i;
-                node_tomb = node == an && an_tomb;
-                const bool first = node == an && prev_b == ba && prev_i == i0;
-                nk = first ? an : nkc;
-                nk_b = first ? ba : nkc_b;
-                nk_i = first ? i0 : nkc_i;
+                nk = at_anchor ? an : nkc;
+                if (b != ba || !at_anchor) {  // node sits in an earlier block: reload at insert
+                  cur_b = WB_NONE;
+                } else {
+                  cur_b = b;
+                  cur_e = e;
+                  cur_cnt = cnt;
+                  cur_nxb = nxb;
+                  node_i = i0;
+                }
               } else {
                 node = rk(e, uj - 1);
-                node_b = b;
-                node_i = uj - 1;
                 const unsigned long long mcl = mc & ((2ULL << (uj - 1)) - 1ULL);
-                if (mcl) {
-                  const uint32_t c = 63u - static_cast<uint32_t>(__builtin_clzll(mcl));
-                  nk = rk(e, c);
-                  nk_b = b;
-                  nk_i = c;
-                } else {
-                  nk = nkc;
-                  nk_b = nkc_b;
-                  nk_i = nkc_i;
-                }
+                nk = mcl ? rk(e, 63u - static_cast<uint32_t>(__builtin_clzll(mcl))) : nkc;
+                cur_b = b;
+                cur_e = e;
+                cur_cnt = cnt;
+                cur_nxb = nxb;
+                node_i = uj - 1;
               }
               break;
             }
-            if (mc) {
-              const uint32_t c = 63u - static_cast<uint32_t>(__builtin_clzll(mc));
-              nkc = rk(e, c);
-              nkc_b = b;
-              nkc_i = c;
-            }
+            if (mc) nkc = rk(e, 63u - static_cast<uint32_t>(__builtin_clzll(mc)));
             if (cnt > s0) {
               carry = (ml >> (cnt - 1)) & 1ULL;
               prev_r = rk(e, cnt - 1);
-              prev_b = b;
-              prev_i = cnt - 1;
+              at_anchor = false;
             }
-            const uint32_t bn = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(bnx[b]));
-            if (bn == BE_NONE) {  // the chain ends: `next node` is Nothing
+            if (nxb == WB_NONE) {  // the chain ends: `next node` is Nothing
               node = prev_r;
-              node_b = prev_b;
-              node_i = prev_i;
-              node_tomb = node == an && an_tomb;
-              const bool first = node == an && prev_b == ba && prev_i == i0;
-              nk = first ? an : nkc;
-              nk_b = first ? ba : nkc_b;
-              nk_i = first ? i0 : nkc_i;
+              nk = at_anchor ? an : nkc;
               nxt = PM;
-              cur_b = b;
-              cur_e = e;
-              cur_cnt = cnt;
+              if (cnt > s0 || (at_anchor && b == ba)) {
+                cur_b = b;
+                cur_e = e;
+                cur_cnt = cnt;
+                cur_nxb = nxb;
+                node_i = cnt > s0 ? cnt - 1 : i0;
+              } else {
+                cur_b = WB_NONE;
+              }
               break;
             }
-            b = bn;
+            b = nxb;
             s0 = 0;
-            e = load_blk(b, cnt);
+            e = load_blk(b, cnt, nxb);
           }
-          BT_MARK(tk);
           // ---- the two inserts (src/Internal/Node.elm:87-89) ----
           const uint32_t wx = nxt | SF_MADE;
           if (lane == 0) S[x] = wx;
+          setwf(x, WF_MADE | WB_NONE);
           logw(i, x, 0, wx, 0);
+          const uint32_t wnode = wfu(node);
           if (nk == node) {
-            const uint32_t wn = (node_tomb ? SF_TOMB : 0u) | SF_MADE | (isc(node) ? SF_COPY : 0u) | x;
+            const uint32_t wn = wf_sflags(wnode) | x;
             if (lane == 0) S[node] = wn;
             logw(i, node, 0, wn, 0);
-            if (node_b == cur_b) blk_insert_e(node_b, node_i, x, cur_e, cur_cnt);
-            else blk_insert(node_b, node_i, x);
+            if (cur_b != WB_NONE) blk_insert_e(node, cur_b, node_i, x, cur_e, cur_cnt, cur_nxb);
+            else blk_insert(node, x);
           } else {
             // copy quirk: slot nk := copy of node with next = x;
             // the entries after nk up to node drop off the chain
-            const bool ncopy = isc(node);
-            blk_orphan_after(nk_b, nk_i, node, i);
+            blk_orphan_after(nk, node, i);
             const uint32_t wk = x | SF_MADE | SF_COPY;
             if (lane == 0) S[nk] = wk;
+            setwf(nk, (wfu(nk) & WB_NONE) | WF_MADE | WF_COPY);
             logw(i, nk, 0, wk, 0);
             uint32_t cs, cd, cb;
-            if (ncopy) {
+            if (wnode & WF_COPY) {
               cs = p.qsrc[base + node];
               cd = p.qcd[base + node];
               cb = p.qcb[base + node];
@@ -793,9 +821,14 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
             logw(i, nk, 1, cs, cd);
             logw(i, nk, 2, min(cb, i), 0);
             if (ORIG && lane == 0) atomicMin(&p.tcopy[p.rop[rb + nk]], i);
-            setc(nk);
-            clear_tomb(nk_b, nk_i);
-            blk_insert(nk_b, nk_i, x);
+            {  // nk's entry is live again (a copy of node)
+              const uint32_t bk = wfu(nk) & WB_NONE;
+              uint32_t c3, n3;
+              const uint32_t e3 = load_blk(bk, c3, n3);
+              const uint32_t jk = idx_of(e3, nk);
+              if (lane == jk) ent[bk * BLK_E + lane] = static_cast<uint16_t>(e3 & 0x7FFFu);
+              blk_insert_e(nk, bk, jk, x, e3 & (lane == jk ? 0x7FFFu : 0xFFFFFFFFu), c3, n3);
+            }
           }
           s = ST_APPLIED;
         } else {
@@ -814,31 +847,23 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
             wn = wl;
           }
           const uint32_t wk = nk == node ? wn : ld_uniform(S, nk);
+          const bool on_chain = !(wk & SF_ORPHAN);
           const uint32_t wx = (wn & PM) | (wk & SF_ORPHAN) | SF_MADE;
           if (lane == 0) S[x] = wx;
+          setwf(x, WF_MADE | (on_chain ? 0u : WF_ORPH) | WB_NONE);
           logw(i, x, 0, wx, 0);
-          const bool on_chain = !(wk & SF_ORPHAN);
           if (nk == node) {
             if (lane == 0) S[node] = (wn & ~PM) | x;
             logw(i, node, 0, (wn & ~PM) | x, 0);
-            if (on_chain) {
-              const uint32_t b = __builtin_amdgcn_readfirstlane(W[node]);
-              uint32_t cnt;
-              const uint32_t e = load_blk(b, cnt);
-              blk_insert(b, idx_of(e, node), x);
-            }
+            if (on_chain) blk_insert(node, x);
           } else {
-            uint32_t bk = NONE, ik = 0;
             if (on_chain) {
-              bk = __builtin_amdgcn_readfirstlane(W[nk]);
-              uint32_t cnt;
-              const uint32_t e = load_blk(bk, cnt);
-              ik = idx_of(e, nk);
-              blk_orphan_after(bk, ik, node, i);
+              blk_orphan_after(nk, node, i);
               wn |= SF_ORPHAN;
             }
             const uint32_t wkn = x | (wn & ~PM & ~SF_ORPHAN) | (wk & SF_ORPHAN) | SF_COPY;
             if (lane == 0) S[nk] = wkn;
+            setwf(nk, (wfu(nk) & WB_NONE) | WF_MADE | WF_COPY | ((wk & SF_ORPHAN) ? WF_ORPH : 0u));
             logw(i, nk, 0, wkn, 0);
             uint32_t cs, cd, cb;
             if (wn & SF_COPY) {
@@ -857,10 +882,13 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
             logw(i, nk, 1, cs, cd);
             logw(i, nk, 2, min(cb, i), 0);
             if (ORIG && lane == 0) atomicMin(&p.tcopy[p.rop[rb + nk]], i);
-            setc(nk);
             if (on_chain) {
-              clear_tomb(bk, ik);
-              blk_insert(bk, ik, x);
+              const uint32_t bk = wfu(nk) & WB_NONE;
+              uint32_t c3, n3;
+              const uint32_t e3 = load_blk(bk, c3, n3);
+              const uint32_t jk = idx_of(e3, nk);
+              if (lane == jk) ent[bk * BLK_E + lane] = static_cast<uint16_t>(e3 & 0x7FFFu);
+              blk_insert_e(nk, bk, jk, x, e3 & (lane == jk ? 0x7FFFu : 0xFFFFFFFFu), c3, n3);
             }
           }
           s = ST_APPLIED;
@@ -869,20 +897,14 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
       if (ORIG && lane == 0) st[i] = s;
     }
   }
-#ifdef PDR_STATS
-  if (ORIG && lane == 0 && K > 28000)
-    printf("pdr blk K=%u ops=%u windows %lld scans %lld cyc: W-load %lld walk %lld insert+rest %lld nb %u\n", K,
-           oe + 1 - rb, nwin, nscan, tw, tk, ti, nb);
-#endif
   if (ORIG && lane == 0) p.logn[D] = (logging && ln <= lcap) ? ln : NONE;
-  if (fail && lane == 0) atomicOr(p.blk_fail, 1u);
   for (uint32_t r = lane; r <= K; r += 64) p.inst[base + r] = I;
 }
 
 template <bool ORIG>
-__global__ void __launch_bounds__(64) k_pdr_blk(PdrCtx p, const uint32_t* list, uint8_t* st) {
+__global__ void __launch_bounds__(64) k_pdr_blk(PdrCtx p, const uint32_t* list, uint8_t* st, uint32_t lds_words) {
   extern __shared__ uint32_t blk_lds[];
-  pdr_blocked<ORIG>(p, st, list[blockIdx.x], blk_lds);
+  pdr_blocked<ORIG>(p, st, list[blockIdx.x], blk_lds, lds_words);
 }
 
 // Sort instances [i0, i1) into three size tiers: static LDS, dynamic LDS,
@@ -890,7 +912,8 @@ __global__ void __launch_bounds__(64) k_pdr_blk(PdrCtx p, const uint32_t* list, 
 struct PdrTiers {
   uint32_t* list[4];
   uint32_t* count;  // [0..3] tier sizes, [4] largest slot count of tier 1, [5] most ops of a dict, [6] tier 3's
-  uint32_t blk_min;  // dicts of more slots than this (and at most BLK_KMAX + 1) take pdr_blocked (tier 3)
+  uint32_t blk_min;  // dicts of more slots than this (and at most blk_max) take pdr_blocked (tier 3)
+  uint32_t blk_max;
 };
 
 __global__ void __launch_bounds__(BLOCK) k_pdr_tier(PdrCtx p, uint32_t i0, uint32_t i1, uint32_t big_cap,
@@ -908,7 +931,7 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_tier(PdrCtx p, uint32_t i0, uint3
     if (I <= n) p.I.base[I] = p.rbase[I];
     const uint32_t slots = pdr_kcount(p, D) + 1;
     uint32_t t = slots <= PDR_SMALL ? 0u : (slots <= big_cap ? 1u : 2u);
-    if (slots > tt.blk_min && slots <= BLK_KMAX + 1) t = 3;
+    if (slots > tt.blk_min && slots <= tt.blk_max) t = 3;
     tt.list[t][atomicAdd(&tt.count[t], 1u)] = I;
     if (t == 1) atomicMax(&tt.count[4], slots);
     if (t == 3) atomicMax(&tt.count[6], slots);
@@ -1238,9 +1261,9 @@ static int pdr_run_tiers(crdtm_ctx* c, const PdrCtx& p, uint32_t i0, uint32_t i1
     else LAUNCH(k_pdr_small<false>, dim3(h[0]), dim3(64), 0, s, p, tt.list[0], st);
   }
   if (h[3]) {
-    const size_t lds = static_cast<size_t>(blk_lds_words(h[6] - 1)) * sizeof(uint32_t);
-    if (orig) LAUNCH(k_pdr_blk<true>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st);
-    else LAUNCH(k_pdr_blk<false>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st);
+    const size_t lds = static_cast<size_t>(big_cap) * sizeof(uint32_t);  // the whole LDS: one wave per CU
+    if (orig) LAUNCH(k_pdr_blk<true>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st, big_cap);
+    else LAUNCH(k_pdr_blk<false>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st, big_cap);
   }
   if (h[1]) {
     const size_t lds = static_cast<size_t>(h[4]) * sizeof(uint32_t);
@@ -1352,12 +1375,22 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   tt.count = ws.alloc<uint32_t>(8);
   tt.blk_min = BLK_MIN;
   if (const char* e = getenv("CRDTM_PDR_BLK_MIN")) tt.blk_min = static_cast<uint32_t>(strtoul(e, nullptr, 10));
-  // the blocked order needs LDS for its largest dict: else the older tiers
-  if (static_cast<uint64_t>(blk_lds_words(BLK_KMAX)) * sizeof(uint32_t) > static_cast<uint64_t>(big_cap) * 4)
-    tt.blk_min = BLK_KMAX + 1;
+  // the blocked order holds a dict's flags (2 B per slot) and its chain
+  // repacked BLK_FILL per block (+ room to split) in the LDS; larger dicts keep
+  // the older tiers
+  tt.blk_max = 0;
+  for (int kk = static_cast<int>(BLK_KMAX); kk > 0; kk -= 256) {
+    const uint32_t k = static_cast<uint32_t>(kk);
+    const uint32_t wfw = (k + 2) / 2;
+    if (wfw < big_cap && (big_cap - wfw) / (1 + BLK_E / 2) >= (k + 1) / BLK_FILL + 16) {
+      tt.blk_max = k + 1;
+      break;
+    }
+  }
   p.where = ws.alloc<uint32_t>(SCAP);
-  p.blk_fail = &dr->pdr_blk_fail;
-  HIP_CHECK(hipMemsetAsync(&dr->pdr_blk_fail, 0, sizeof(uint32_t), s));
+  p.blk_spare = 0;
+  if (const char* e = getenv("CRDTM_PDR_BLK_SPARE")) p.blk_spare = static_cast<uint32_t>(strtoul(e, nullptr, 10));
+
   HIP_CHECK(hipMemsetAsync(p.inst, 0xFF, static_cast<size_t>(SCAP) * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(p.ch, 0xFF, static_cast<size_t>(SCAP) * sizeof(uint32_t), s));
 
@@ -1390,7 +1423,7 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   if ((r = sync_read(c))) return r;
   const DevResult h1 = *c->hres;
   const long long new_ts = t->timestamp + h1.own_ok_adds - t->own_bias;
-  if (h1.pdr_conflict || h1.pdr_blk_fail || replica_of(new_ts) != replica_of(t->timestamp)) {
+  if (h1.pdr_conflict || replica_of(new_ts) != replica_of(t->timestamp)) {
     ws.used = arena_mark;
     return CRDTM_OK;
   }
@@ -1418,7 +1451,7 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   for (uint32_t level = 0;; ++level) {
     LAUNCH(k_pdr_jobs, dim3(grid_for(s1 - s0)), dim3(BLOCK), 0, s, p, ok, s0, s1, JCAP, dr);
     if ((r = sync_read(c))) return r;
-    if (c->hres->pdr_overflow || c->hres->pdr_blk_fail || level > in.maxlen + 1) {  // no room: sequential replay
+    if (c->hres->pdr_overflow || level > in.maxlen + 1) {  // no room: sequential replay
       *handled = false;
       ws.used = arena_mark;
       return CRDTM_OK;

@@ -336,8 +336,8 @@ def test_flat_run_tree_depth(depth):
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
 
 
-@pytest.mark.parametrize("log_min", ["512", "1"])
-def test_blocked_chain_order_forced(monkeypatch, log_min):
+@pytest.mark.parametrize("log_min,spare", [("512", "0"), ("1", "0"), ("512", "2")])
+def test_blocked_chain_order_forced(monkeypatch, log_min, spare):
     """Every dict through the blocked chain-order replay (pdr.hip pdr_blocked,
     normally only dicts of more than 4096 slots): the adversarial quirk streams
     (copies, orphans, orphan anchors re-entering the chain, trailing
@@ -346,6 +346,7 @@ def test_blocked_chain_order_forced(monkeypatch, log_min):
     from adversarial import adversarial
     monkeypatch.setenv("CRDTM_PDR_BLK_MIN", "1")
     monkeypatch.setenv("CRDTM_PDR_LOG_MIN", log_min)
+    monkeypatch.setenv("CRDTM_PDR_BLK_SPARE", spare)  # 2: compactions (repacking the chain) all the time
     paths = {}
     for seed in range(0, 128):
         n = [40, 120, 400, 1500][seed % 4]
