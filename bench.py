@@ -162,6 +162,8 @@ def cpu_baseline(s, m, doc_off=None, workers=1, batch_cut=20_000):
         out["js"] = js
         if doc_off is None and batch_cut:
             out["js_batch"] = jsoracle.run(f, mode="batch", limit=min(batch_cut, m), timeout=900)
+        if doc_off is None:  # SURVEY.md 8d mode (ii): apply over 10k-op Batch chunks
+            out["js_chunk"] = jsoracle.run(f, mode="chunk", chunk=10_000, timeout=900)
     if doc_off is None:
         L = olib()
         t = L.orc_init(0)
@@ -186,6 +188,11 @@ def cpu_line(cb, what):
         d["reference_batch_mode"] = {"value": b["ops_per_s"], "ops": b["ops"],
                                      "note": "apply (Batch ops) in one call: O(N^2) lastOperation accumulator "
                                              "(src/CRDTree.elm:224-232), cut off at this size"}
+    if "js_chunk" in cb:
+        c = cb["js_chunk"]
+        d["chunked_batch_mode"] = {"value": c["ops_per_s"], "ops": c.get("ops"),
+                                   "note": "apply (Batch chunk) over 10k-op chunks (same final tree; lastOperation "
+                                           "= the last chunk), SURVEY.md 8d mode (ii)"}
     if "cpp" in cb:
         d["cpp_restatement"] = {"value": cb["cpp"], "note": "oracle/crdtree_oracle.cpp (mutable maps), same sample"}
     return d
