@@ -136,9 +136,7 @@ __global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint2* rng, DevResult* 
   }
   __syncthreads();
   uint32_t mx = 0, bad = 0, neg = 0, ndel = 0, maxr = 0;
-  QUAD_LOOP(i0, o.n) {
-    Quad q;
-    load_quad(o, i0, q);
+  auto fold = [&](const Quad& q) {
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
       if (k >= q.cnt) break;
@@ -168,17 +166,46 @@ __global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint2* rng, DevResult* 
         }
       }
     }
+  };
+  // (512 workgroups keep the range flush short, so each thread keeps two
+  // quads and four path pairs in flight to cover the memory latency)
+  {
+    const uint32_t qs = 4 * gridDim.x * blockDim.x;
+    uint32_t i0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
+    for (; i0 + qs < o.n; i0 += 2 * qs) {
+      Quad qa, qb;
+      load_quad(o, i0, qa);
+      load_quad(o, i0 + qs, qb);
+      fold(qa);
+      fold(qb);
+    }
+    if (i0 < o.n) {
+      Quad qa;
+      load_quad(o, i0, qa);
+      fold(qa);
+    }
   }
   // path elements: 16-byte loads over an even-aligned range
   const uint64_t np = o.n_path, npair = np / 2;
-  for (uint64_t p = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; p < npair;
-       p += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    const longlong2 v = *reinterpret_cast<const longlong2*>(o.path + 2 * p);
-    if (v.x >= TWO53 || v.x <= -TWO53 || v.y >= TWO53 || v.y <= -TWO53) bad = 1;
+  auto out = [](long long v) { return v >= TWO53 || v <= -TWO53; };
+  {
+    const uint64_t ps = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    uint64_t p = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+    for (; p + 3 * ps < npair; p += 4 * ps) {
+      longlong2 v[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const longlong2*>(o.path + 2 * (p + u * ps));
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u)
+        if (out(v[u].x) || out(v[u].y)) bad = 1;
+    }
+    for (; p < npair; p += ps) {
+      const longlong2 v = *reinterpret_cast<const longlong2*>(o.path + 2 * p);
+      if (out(v.x) || out(v.y)) bad = 1;
+    }
   }
   if ((np & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-    const long long v = o.path[np - 1];
-    if (v >= TWO53 || v <= -TWO53) bad = 1;
+    if (out(o.path[np - 1])) bad = 1;
   }
   maxr = block_max(maxr);  // (synchronises the block) only ids <= maxr were touched
   for (uint32_t j = threadIdx.x; j <= maxr && j < REP_DIRECT; j += blockDim.x) {
@@ -382,14 +409,15 @@ struct LevelStart {
   uint32_t v[MAXLV_BUCKET + 1];
 };
 
-// A level-list entry carries what the level kernels would otherwise fetch
-// through dependent loads: the op, its path offset and its parent key
-// (path[L-2], 0 for |path| < 2), written by the streaming k_len_scatter.
+// A level-list entry: the op and its path offset (o.off[i]), so a level
+// kernel loads the op's keys without a dependent offset load. The parent key
+// path[L-2] is left to k_lv_dict: it shares lines with the prefix keys that
+// kernel loads anyway (carried here it made k_len_scatter touch every line of
+// the path array).
 struct LvEnt {
   uint32_t i, b;
-  long long kp;
 };
-static_assert(sizeof(LvEnt) == 16, "one 16-byte load per entry");
+static_assert(sizeof(LvEnt) == 8, "one 8-byte load per entry");
 
 __global__ void __launch_bounds__(BLOCK) k_len_scatter(OpsDev o, uint32_t maxlen, LevelStart start,
                                                        uint32_t* fill, LvEnt* lists) {
@@ -415,13 +443,7 @@ __global__ void __launch_bounds__(BLOCK) k_len_scatter(OpsDev o, uint32_t maxlen
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const uint32_t i = c0 + u * BLOCK + threadIdx.x;
-      if (L[u] != NONE) {
-        LvEnt e;
-        e.i = i;
-        e.b = b[u];
-        e.kp = L[u] >= 2 ? o.path[b[u] + L[u] - 2] : 0;
-        *reinterpret_cast<uint4*>(&lists[base[L[u]] + r[u]]) = *reinterpret_cast<const uint4*>(&e);
-      }
+      if (L[u] != NONE) *reinterpret_cast<uint2*>(&lists[base[L[u]] + r[u]]) = make_uint2(i, b[u]);
     }
     __syncthreads();
   }
@@ -436,12 +458,12 @@ __global__ void __launch_bounds__(BLOCK) k_lv_dict(OpsDev o, Work w, TsIndex h, 
                                                    uint32_t j) {
   const uint32_t n = o.n;
   GRID_STRIDE(q, cnt) {
-    const uint4 ev = *reinterpret_cast<const uint4*>(&list[q]);
+    const uint2 ev = *reinterpret_cast<const uint2*>(&list[q]);
     const uint32_t i = ev.x, b = ev.y;
     uint32_t cur = n;
     uint8_t s = ST_PENDING;
     if (j > 1) {
-      const long long kp = static_cast<long long>((static_cast<unsigned long long>(ev.w) << 32) | ev.z);
+      const long long kp = o.path[b + j - 2];  // the parent's key
       long long own[LV_UNROLL];
       if (j - 2 <= LV_UNROLL) {
 #pragma unroll
@@ -962,57 +984,82 @@ __device__ __forceinline__ long long op_t(const OpsDev& o, uint32_t i) {
   return o.kind[i] == CRDTM_ADD ? o.ts[i] : o.path[o.off[i + 1] - 1];
 }
 
-// Each block folds a contiguous chunk of ops into an LDS table (replica ->
-// last applied op), then publishes one atomicMax per distinct replica.
-constexpr uint32_t REP_LDS = 512;
-__global__ void __launch_bounds__(BLOCK) k_rep_max(OpsDev o, const uint8_t* st, uint32_t* rtab) {
-  __shared__ uint32_t rk[REP_LDS];
-  __shared__ uint32_t rv[REP_LDS];
-  for (uint32_t j = threadIdx.x; j < REP_LDS; j += blockDim.x) {
-    rk[j] = NONE;
-    rv[j] = 0;
-  }
+// Each block folds REP_PER * BLOCK consecutive ops into a direct-mapped LDS
+// table (replica id < REP_DIRECT -> 1 + its last applied op; other ids go
+// straight to the global table), loading four ops per thread at a time so the
+// dependent loads of op_t overlap. Same-address LDS atomics serialise, and a
+// batch has few replicas, so each wave first reduces per replica: the lanes
+// of one replica hold consecutive op indices, the highest of them publishes.
+// The block then publishes one atomicMax per replica it saw; the first
+// publisher of a replica (the table entry was 0) appends it to `rlist`, so the
+// output pass visits the touched replicas only.
+constexpr uint32_t REP_PER = 16;  // ops per thread
+__global__ void __launch_bounds__(BLOCK) k_rep_max(OpsDev o, const uint8_t* st, uint32_t* rtab, uint32_t* rlist,
+                                                   uint32_t* rcount) {
+  __shared__ uint32_t rv[REP_DIRECT];
+  for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) rv[j] = 0;
   __syncthreads();
   const uint32_t n = o.n;
-  const uint32_t chunk = (n + gridDim.x - 1) / gridDim.x;
-  const uint32_t b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
-  for (uint32_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
-    if (st[i] != ST_APPLIED) continue;
-    const uint32_t r = static_cast<uint32_t>(replica_of(op_t(o, i)) + (1LL << (REPLICA_BITS - 1)));
-    uint32_t p = (r * 0x9E3779B1u) >> 23;  // 9 bits
-    bool done = false;
-    for (uint32_t probe = 0; probe < 16 && !done; ++probe, p = (p + 1) & (REP_LDS - 1)) {
-      const uint32_t prev = atomicCAS(&rk[p], NONE, r);
-      if (prev == NONE || prev == r) {
-        atomicMax(&rv[p], i + 1);
-        done = true;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t b0 = blockIdx.x * (BLOCK * REP_PER) + threadIdx.x;
+  constexpr uint32_t OFF = 1u << (REPLICA_BITS - 1);
+  uint32_t mr = 0;
+  for (uint32_t k0 = 0; k0 < REP_PER; k0 += 4) {
+    uint32_t ii[4];
+    bool ok[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      ii[u] = b0 + (k0 + u) * BLOCK;
+      ok[u] = ii[u] < n && st[ii[u]] == ST_APPLIED;
+    }
+    long long t[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) t[u] = ok[u] ? op_t(o, ii[u]) : 0;
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t r = static_cast<uint32_t>(replica_of(t[u]) + OFF);
+      bool pend = ok[u];
+      for (unsigned long long m = __ballot(pend); m; m = __ballot(pend)) {
+        const uint32_t rl = __builtin_amdgcn_readlane(r, static_cast<uint32_t>(__builtin_ctzll(m)));
+        const unsigned long long mm = __ballot(pend && r == rl);
+        if (lane == 63u - static_cast<uint32_t>(__builtin_clzll(mm))) {
+          const uint32_t d = rl - OFF;  // (ids below 0 wrap high: global table)
+          if (d < REP_DIRECT) {
+            atomicMax(&rv[d], ii[u] + 1);
+            mr = max(mr, d);
+          } else if (atomicMax(&rtab[rl], ii[u] + 1) == 0) {
+            rlist[atomicAdd(rcount, 1u)] = rl;
+          }
+        }
+        if (r == rl) pend = false;
       }
     }
-    if (!done) atomicMax(&rtab[r], i + 1);  // LDS table crowded: publish directly
   }
-  __syncthreads();
-  for (uint32_t j = threadIdx.x; j < REP_LDS; j += blockDim.x)
-    if (rk[j] != NONE) atomicMax(&rtab[rk[j]], rv[j]);
+  mr = block_max(mr);  // (synchronises the block) only ids <= mr were touched
+  for (uint32_t j = threadIdx.x; j <= mr; j += blockDim.x)
+    if (rv[j] && atomicMax(&rtab[j + OFF], rv[j]) == 0) rlist[atomicAdd(rcount, 1u)] = j + OFF;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_rep_out(OpsDev o, const uint8_t* st, uint32_t* rtab,
-                                                   long long* out, uint32_t* n_out, long long* inl) {
-  GRID_STRIDE(i, o.n) {
-    if (st[i] != ST_APPLIED) continue;
+inline uint32_t rep_grid(uint32_t n) { return grid_for(n, BLOCK * REP_PER); }
+
+// One thread per touched replica: the winner is op rtab[r] - 1; the entry is
+// cleared (the table stays clean between calls).
+__global__ void __launch_bounds__(BLOCK) k_rep_out(OpsDev o, uint32_t* rtab, const uint32_t* rlist,
+                                                   const uint32_t* rcount, long long* out, uint32_t* n_out,
+                                                   long long* inl) {
+  const uint32_t nr = *rcount;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nr; k += gridDim.x * blockDim.x) {
+    const uint32_t r = rlist[k];
+    const uint32_t i = rtab[r] - 1;
+    rtab[r] = 0;
     const long long t = op_t(o, i);
-    const uint32_t r = static_cast<uint32_t>(replica_of(t) + (1LL << (REPLICA_BITS - 1)));
-    if (rtab[r] == i + 1) {
-      // the one winner of replica r also clears its entry (the table stays
-      // clean between calls): ops read after the clear see 0, never their own i + 1
-      rtab[r] = 0;
-      const uint32_t k = atomicAdd(n_out, 1u);
-      out[2 * k] = replica_of(t);
-      out[2 * k + 1] = t;
-      if (k < REP_INLINE) {
-        inl[2 * k] = replica_of(t);
-        inl[2 * k + 1] = t;
-      }
+    out[2 * k] = replica_of(t);
+    out[2 * k + 1] = t;
+    if (k < REP_INLINE) {
+      inl[2 * k] = replica_of(t);
+      inl[2 * k + 1] = t;
     }
+    if (k == 0) *n_out = nr;
   }
 }
 
@@ -1796,9 +1843,13 @@ constexpr unsigned long long REC_EMPTY = ~0ULL;
 // track_rep = 0: k_fl_check folds the replicas table from the records instead
 // (slot order: a thread's slots stay inside one replica's range, no per-op
 // LDS atomics).
+// log_to_tree: the flat speculation (fresh tree, every op applies) also
+// appends the batch to the log here (it IS the log: same CSR layout, path
+// elements [0, n_path)), so the ops stream from HBM once for both.
 __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_t Q, unsigned long long* rec,
                                                     long long ts0, uint32_t* rtab, DevResult* dres,
-                                                    uint32_t track_rep, uint32_t nrep) {
+                                                    uint32_t track_rep, uint32_t nrep, TreeDev T,
+                                                    uint32_t log_to_tree) {
   // dynamic LDS: the replica range table (nrep ids: base, min, max counter)
   // when it fits, else lookups go to the global table; rv when track_rep
   extern __shared__ __attribute__((aligned(16))) uint32_t scl[];
@@ -1829,6 +1880,32 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
   QUAD_LOOP_XCD(i0, o.n) {
     Quad qd;
     load_quad(o, i0, qd);
+    long long pk[4];  // the path element of each op (flat: |path| <= 1)
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) pk[k] = (k < qd.cnt && qd.off[k + 1] != qd.off[k]) ? o.path[qd.off[k]] : 0;
+    if (log_to_tree) {
+      if (qd.cnt == 4) {
+        *reinterpret_cast<uchar4*>(T.l_kind + i0) = make_uchar4(qd.kind[0], qd.kind[1], qd.kind[2], qd.kind[3]);
+        *reinterpret_cast<longlong2*>(T.l_ts + i0) = make_longlong2(qd.ts[0], qd.ts[1]);
+        *reinterpret_cast<longlong2*>(T.l_ts + i0 + 2) = make_longlong2(qd.ts[2], qd.ts[3]);
+        *reinterpret_cast<uint4*>(T.l_off + i0) = make_uint4(qd.off[0], qd.off[1], qd.off[2], qd.off[3]);
+        *reinterpret_cast<uint4*>(T.l_val + i0) = *reinterpret_cast<const uint4*>(o.val + i0);
+      } else {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {  // (static indices: no scratch)
+          if (k < qd.cnt) {
+            T.l_kind[i0 + k] = qd.kind[k];
+            T.l_ts[i0 + k] = qd.ts[k];
+            T.l_off[i0 + k] = qd.off[k];
+            T.l_val[i0 + k] = o.val[i0 + k];
+          }
+        }
+      }
+      if (i0 + qd.cnt == o.n) T.l_off[o.n] = o.off[o.n];
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k)
+        if (k < qd.cnt && qd.off[k + 1] != qd.off[k]) T.l_path[qd.off[k]] = pk[k];
+    }
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
       if (k >= qd.cnt) continue;
@@ -1846,7 +1923,7 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
         continue;
       }
       ++keys;
-      const long long kk = o.path[qd.off[k]];
+      const long long kk = pk[k];
       const uint32_t qa = kk == 0 ? Q : slot(kk);
       rec[q] = (static_cast<unsigned long long>(i) << 32) | qa;
       if (track_rep) {
@@ -2724,6 +2801,22 @@ __global__ void __launch_bounds__(BLOCK) k_post_flags(OpsDev o, const uint8_t* s
   }
 }
 
+// replicas[replicaId t] := t, last writer wins, over the applied ops: fold
+// into c->rtab, collect the touched replicas into `rep` (+ the inline copy).
+static_assert(offsetof(DevResult, n_rep_list) == offsetof(DevResult, n_replica_out) + sizeof(uint32_t),
+              "one memset clears both counters");
+static int replica_fold(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, Arena& ws,
+                        hipStream_t s) {
+  DevResult* dr = c->dres;
+  const uint32_t n = o.n;
+  uint32_t* rlist = ws.alloc<uint32_t>(std::min<uint64_t>(n, REPLICA_SLOTS) + 1);
+  HIP_CHECK(hipMemsetAsync(&dr->n_replica_out, 0, 2 * sizeof(uint32_t), s));  // n_replica_out, n_rep_list
+  LAUNCH(k_rep_max, dim3(rep_grid(n)), dim3(BLOCK), 0, s, o, st, c->rtab, rlist, &dr->n_rep_list);
+  LAUNCH(k_rep_out, dim3(64), dim3(BLOCK), 0, s, o, c->rtab, rlist, &dr->n_rep_list, rep, &dr->n_replica_out,
+         dr->rep_inline);
+  return CRDTM_OK;
+}
+
 // Append the applied ops to the log and fold replicas; shared by both paths.
 int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& ws) {
   crdtm_ctx* c = t->ctx;
@@ -2741,9 +2834,7 @@ int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& ws) {
                      static_cast<uint32_t>(t->log_npath), appl, plen);
   LAUNCH(k_log_tail, dim3(1), dim3(1), 0, s, t->d, static_cast<uint32_t>(t->log_n), &dr->log_n,
                      static_cast<uint32_t>(t->log_npath), &dr->log_npath);
-  HIP_CHECK(hipMemsetAsync(&dr->n_replica_out, 0, sizeof(uint32_t), s));
-  LAUNCH(k_rep_max, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, s, o, st, c->rtab);
-  LAUNCH(k_rep_out, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, c->rtab, rep, &dr->n_replica_out, dr->rep_inline);
+  if ((r = replica_fold(c, o, st, rep, ws, s))) return r;
   if ((r = sync_read(c))) return r;
   if ((r = take_replicas(t, rep))) return r;
   t->last_begin = t->log_n;
@@ -2863,7 +2954,7 @@ struct FlatBufs {
 };
 
 static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_t Q, uint32_t maxr,
-                             const uint8_t* st, uint32_t K, bool all_applied, FlatBufs& fb) {
+                             const uint8_t* st, uint32_t K, bool all_applied, bool log_done, FlatBufs& fb) {
   crdtm_ctx* c = t->ctx;
   hipStream_t s = c->stream;
   Arena& ws = c->ws;
@@ -2938,8 +3029,8 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     LAUNCH(k_fl_commit, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK),
            maxr + 1 <= HOST_RANGES ? 2 * (maxr + 1) * sizeof(uint32_t) : 0, s, o, ix, Q, maxr + 1, anc, rec, qc,
            logidx, t->d);
-    if (all_applied) LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
-  } else if (all_applied) {
+    if (all_applied && !log_done) LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
+  } else if (all_applied && !log_done) {
     LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
   }
   fb.rep = ws.alloc<long long>(2 * static_cast<uint64_t>(maxr) + 2);
@@ -3008,13 +3099,6 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   fb.anc = ws.alloc<uint32_t>(U);
   fb.cnt = ws.alloc<uint32_t>(U + 1);
   fb.fill = ws.alloc<uint32_t>(U + 1);
-  LAUNCH(k_fl_init, dim3(grid_for(Q, BLOCK, 4096)), dim3(BLOCK), 0, s, Q, fb.rec);
-  // replicas table: folded by the check over slot order when the range table fits in LDS
-  const uint32_t nrep = maxr + 1 <= HOST_RANGES ? maxr + 1 : 0u;
-  LAUNCH(k_fl_claim, dim3(quad_grid(n)), dim3(BLOCK), (3 * nrep + (nrep ? 0 : REP_DIRECT)) * sizeof(uint32_t), s,
-         o, ix, Q, fb.rec, t->timestamp, c->rtab, dr, nrep ? 0u : 1u, nrep);
-  LAUNCH(k_fl_check, dim3(grid_for(Q / 2 + 1, BLOCK, 2048)), dim3(BLOCK), 2 * nrep * sizeof(uint32_t), s, Q,
-         fb.rec, dr, ix.base, nrep, c->rtab);
   int r;
   auto grow_for = [&](uint32_t K, uint32_t applied) -> int {
     TreeCaps need = t->cap;
@@ -3028,6 +3112,16 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
       return grow_tree(t, need);
     return CRDTM_OK;
   };
+  // speculation (below): every op applies, so the claim also writes the log
+  const bool spec = Q >= n && !t->remerge;
+  if (spec && (r = grow_for(n, n))) return r;
+  LAUNCH(k_fl_init, dim3(grid_for(Q, BLOCK, 4096)), dim3(BLOCK), 0, s, Q, fb.rec);
+  // replicas table: folded by the check over slot order when the range table fits in LDS
+  const uint32_t nrep = maxr + 1 <= HOST_RANGES ? maxr + 1 : 0u;
+  LAUNCH(k_fl_claim, dim3(quad_grid(n)), dim3(BLOCK), (3 * nrep + (nrep ? 0 : REP_DIRECT)) * sizeof(uint32_t), s,
+         o, ix, Q, fb.rec, t->timestamp, c->rtab, dr, nrep ? 0u : 1u, nrep, t->d, spec ? 1u : 0u);
+  LAUNCH(k_fl_check, dim3(grid_for(Q / 2 + 1, BLOCK, 2048)), dim3(BLOCK), 2 * nrep * sizeof(uint32_t), s, Q,
+         fb.rec, dr, ix.base, nrep, c->rtab);
   auto finish = [&](uint32_t K, uint32_t applied, uint32_t already, uint64_t npath, long long new_ts) -> int {
     int rr = take_replicas(t, fb.rep);
     if (rr) return rr;
@@ -3047,12 +3141,8 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   };
   // ---- speculation: every op applies (writes the state before the check,
   // so never inside an incremental re-merge) ----
-  if (Q >= n && !t->remerge) {
-    if ((r = grow_for(n, n))) return r;
-    // (the log copy stays on this stream: run beside the order kernels on a
-    // second stream it only slowed them by as much as it saved, the order
-    // phase being bandwidth-bound where it is not latency-bound)
-    if ((r = flat_order_commit(t, o, ix, Q, maxr, st, n, true, fb))) return r;
+  if (spec) {
+    if ((r = flat_order_commit(t, o, ix, Q, maxr, st, n, true, true, fb))) return r;
     if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, nullptr, n, NONE, st_out);
     if ((r = sync_read(c))) return r;
     const DevResult& h = *c->hres;
@@ -3114,7 +3204,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   const bool all_applied = h1.n_applied == n;
   if ((r = grow_for(K, h1.n_applied))) return r;
   LAUNCH(k_fl_commit_reset, dim3(1), dim3(1), 0, s, dr);
-  if ((r = flat_order_commit(t, o, ix, Q, maxr, st, K, all_applied, fb))) return r;
+  if ((r = flat_order_commit(t, o, ix, Q, maxr, st, K, all_applied, spec, fb))) return r;
   if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, st, n, NONE, st_out);
   if ((r = sync_read(c))) return r;
   if (c->hres->run_fail && (r = flat_order_fallback(t, Q, K, fb))) return r;
@@ -3382,8 +3472,7 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   LAUNCH(k_commit_root, dim3(1), dim3(1), 0, s, o, t->d, kept, fc, 1u);
   // (the replica fold stays here: beside the order kernels its hot table
   // lines slowed both streams)
-  LAUNCH(k_rep_max, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, s, o, w.st, c->rtab);
-  LAUNCH(k_rep_out, dim3(g), dim3(BLOCK), 0, s, o, w.st, c->rtab, rep, &dr->n_replica_out, dr->rep_inline);
+  if ((r = replica_fold(c, o, w.st, rep, ws, s))) return r;
   if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n, NONE, st_out);
   HIP_CHECK(hipStreamWaitEvent(s, c->ev_join, 0));
   if ((r = sync_read(c))) return r;

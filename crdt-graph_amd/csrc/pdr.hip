@@ -1256,23 +1256,35 @@ static int pdr_run_tiers(crdtm_ctx* c, const PdrCtx& p, uint32_t i0, uint32_t i1
   HIP_CHECK(hipMemcpyAsync(hcount, tt.count, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
   const uint32_t* h = hcount;
-  if (h[0]) {
-    if (orig) LAUNCH(k_pdr_small<true>, dim3(h[0]), dim3(64), 0, s, p, tt.list[0], st);
-    else LAUNCH(k_pdr_small<false>, dim3(h[0]), dim3(64), 0, s, p, tt.list[0], st);
+  // the blocked tier (a few big dicts, one CU each, the longest replays) goes
+  // first on the main stream; the other tiers run beside it on the side stream
+  const bool fork = h[3] && (h[0] || h[1] || h[2]);
+  hipStream_t s2 = fork ? c->side : s;
+  if (fork) {
+    HIP_CHECK(hipEventRecord(c->ev_fork, s));
+    HIP_CHECK(hipStreamWaitEvent(s2, c->ev_fork, 0));
   }
   if (h[3]) {
     const size_t lds = static_cast<size_t>(big_cap) * sizeof(uint32_t);  // the whole LDS: one wave per CU
     if (orig) LAUNCH(k_pdr_blk<true>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st, big_cap);
     else LAUNCH(k_pdr_blk<false>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st, big_cap);
   }
+  if (h[0]) {
+    if (orig) LAUNCH(k_pdr_small<true>, dim3(h[0]), dim3(64), 0, s2, p, tt.list[0], st);
+    else LAUNCH(k_pdr_small<false>, dim3(h[0]), dim3(64), 0, s2, p, tt.list[0], st);
+  }
   if (h[1]) {
     const size_t lds = static_cast<size_t>(h[4]) * sizeof(uint32_t);
-    if (orig) LAUNCH(k_pdr_big<true>, dim3(h[1]), dim3(64), lds, s, p, tt.list[1], st);
-    else LAUNCH(k_pdr_big<false>, dim3(h[1]), dim3(64), lds, s, p, tt.list[1], st);
+    if (orig) LAUNCH(k_pdr_big<true>, dim3(h[1]), dim3(64), lds, s2, p, tt.list[1], st);
+    else LAUNCH(k_pdr_big<false>, dim3(h[1]), dim3(64), lds, s2, p, tt.list[1], st);
   }
   if (h[2]) {
-    if (orig) LAUNCH(k_pdr_huge<true>, dim3(h[2]), dim3(64), 0, s, p, tt.list[2], st);
-    else LAUNCH(k_pdr_huge<false>, dim3(h[2]), dim3(64), 0, s, p, tt.list[2], st);
+    if (orig) LAUNCH(k_pdr_huge<true>, dim3(h[2]), dim3(64), 0, s2, p, tt.list[2], st);
+    else LAUNCH(k_pdr_huge<false>, dim3(h[2]), dim3(64), 0, s2, p, tt.list[2], st);
+  }
+  if (fork) {
+    HIP_CHECK(hipEventRecord(c->ev_join, s2));
+    HIP_CHECK(hipStreamWaitEvent(s, c->ev_join, 0));
   }
   return CRDTM_OK;
 }
