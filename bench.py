@@ -35,6 +35,10 @@ WORKLOADS = {
     # depth <= 12, <= 8 children, 6.67M adds then deletes of half the nodes
     "deep10m": dict(n_ops=10_000_000, replicas=16, p_delete=1 / 3, max_depth=12, max_children=8, deletes_last=1,
                     seed=0xC0FFEE04),
+    # config 4's second variant: the same tree with its Deletes interleaved among
+    # the Adds, so dicts see tombstones before later inserts: the exact per-dict replay
+    "deep10m_il": dict(n_ops=10_000_000, replicas=16, p_delete=1 / 3, max_depth=12, max_children=8, deletes_last=0,
+                       seed=0xC0FFEE04),
     # one tree, 1M ops (80/20 interleaved), 16 replicas, branches, depth <= 4
     # (Deletes interleaved before later inserts: the exact sequential replay)
     "cfg2": dict(n_ops=1_000_000, replicas=16, window=64, p_delete=0.2, p_branch=0.1, max_depth=4,
@@ -42,7 +46,7 @@ WORKLOADS = {
     # SURVEY.md §8d config 1 shape: 2 replicas, 10k ops, 70/30 interleaved, depth <= 3
     "cfg1": dict(n_ops=10_000, replicas=2, window=8, p_delete=0.3, p_branch=0.05, max_depth=3, seed=0xC0FFEE01),
 }
-CPU_SAMPLE = {"flat10m": 100_000, "deep10m": 500_000, "trees": 2_000_000, "cfg2": 100_000, "cfg1": 10_000}
+CPU_SAMPLE = {"flat10m": 100_000, "deep10m": 500_000, "deep10m_il": 500_000, "trees": 2_000_000, "cfg2": 100_000, "cfg1": 10_000}
 # 100k documents x 1k ops (80/20), 8 replicas, sharded by
 # document id; 12.5k documents per GPU (100k at 8 GPUs), weak scaling.
 # Incremental merges: a 10M-node document, then successive 10k-op batches of the same stream
@@ -212,7 +216,12 @@ def main():
     ap.add_argument("--exchange", choices=("auto", "on", "off"), default="auto",
                     help="also run config 5 (op-log all-gather + sharded merge) after a single-document "
                          "workload and attach its line as 'exchange' (auto: when N > 1)")
+    ap.add_argument("--force-replay", action="store_true",
+                    help="every merge takes the one-lane sequential replay (env CRDTM_FORCE_REPLAY=1): "
+                         "measures the fallback cliff on the same batch")
     args = ap.parse_args()
+    if args.force_replay:
+        os.environ["CRDTM_FORCE_REPLAY"] = "1"  # (read by every merge)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

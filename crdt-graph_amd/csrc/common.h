@@ -41,6 +41,7 @@ enum : uint32_t {
   G_REPLICA_DRIFT = 4u, // own replica id changes during the batch (timestamp crosses 2^32)
   G_NOT_FRESH = 8u,     // tree already holds state (incremental merge)
   G_DEEP_PATH = 16u,    // a path longer than the length buckets of K1
+  G_FORCED = 32u,       // CRDTM_FORCE_REPLAY=1: the sequential replay on purpose (measures the fallback)
 };
 
 // Small device-side result block (one copy back per phase).

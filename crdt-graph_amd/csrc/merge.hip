@@ -3239,9 +3239,13 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   const uint32_t maxlen = c->hres->max_len;
   if (t->max_depth < maxlen) t->max_depth = maxlen;
   const uint32_t g = grid_for(n);
-  if (t->n_slots != 1 || t->log_n != 0) {
+  // (env CRDTM_FORCE_REPLAY=1: every batch takes the one-lane sequential
+  // replay, so the cost of that fallback is measurable on any workload)
+  const char* fe = getenv("CRDTM_FORCE_REPLAY");
+  const bool force_replay = fe && fe[0] == '1';
+  if (force_replay || t->n_slots != 1 || t->log_n != 0) {
     // incremental merge into existing state: exact replay
-    r = run_replay(t, o, w.st, res, G_NOT_FRESH);
+    r = run_replay(t, o, w.st, res, force_replay ? G_FORCED : G_NOT_FRESH);
     if (r == CRDTM_OK && st_out)
       LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n,
              res->err_index >= 0 ? static_cast<uint32_t>(res->err_index) : NONE, st_out);

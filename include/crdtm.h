@@ -73,7 +73,8 @@ typedef struct crdtm_result {
   uint64_t n_already;
   int64_t timestamp;  /* tree timestamp after the call */
   uint64_t n_slots;   /* slots held by the device state (empty children dicts are implicit) */
-  uint32_t guard;     /* bit0 ts collision, bit1 delete-before-add in a dict, bit2 replica-id drift, bit3 non-fresh tree */
+  uint32_t guard;     /* bit0 ts collision, bit1 delete-before-add in a dict, bit2 replica-id drift, bit3 non-fresh tree,
+                         bit4 path deeper than 64, bit5 sequential replay forced (env CRDTM_FORCE_REPLAY=1) */
   uint32_t flags;     /* CRDTM_FLAG_* */
   /* serial-work accounting: ops and dicts that went through an
    * exact in-order replay (one wave per dict, or one lane for the whole batch),

@@ -108,6 +108,28 @@ def test_deep10m():
     olib().orc_free(ot)
 
 
+def test_deep10m_interleaved():
+    """Config 4's second variant at 10M ops: the same deep
+    tree with its Deletes interleaved among the Adds (tombstones before later
+    inserts in the same dicts: the exact per-dict replay, bench workload
+    deep10m_il)."""
+    spec = dict(CFG4, deletes_last=0)
+    _, et, ot, res = full_parity(spec)
+    assert res.path_taken != N.PATH_CLOSED_FORM
+    olib().orc_free(ot)
+
+
+def test_forced_sequential_replay(monkeypatch):
+    """CRDTM_FORCE_REPLAY=1 sends a batch the parallel paths serve to the
+    one-lane sequential replay (how bench.py --force-replay measures that
+    fallback); its result must be the same."""
+    monkeypatch.setenv("CRDTM_FORCE_REPLAY", "1")
+    spec = dict(CFG2, n_ops=200_000)
+    _, et, ot, res = full_parity(spec, want_path=(N.PATH_REPLAY,))
+    assert res.guard & 32
+    olib().orc_free(ot)
+
+
 def test_nested_adds_every_applied_2m():
     """A nested adds-only batch (every op applies: the log is the batch, no
     log scans) over many scan tiles; log, lastOperation and operationsSince
