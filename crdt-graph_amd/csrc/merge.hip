@@ -3230,6 +3230,7 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   LAUNCH(k_dres_init, dim3(1), dim3(64), 0, s, dr);
   // (512 workgroups: each flushes its replica ranges and counters with
   // device-scope atomics that serialise per word, ~12 ns each)
+  // (measured: 512 beats 1024 and 2048 workgroups on flat10m and deep10m)
   LAUNCH(k_pre, dim3(std::min<uint32_t>(quad_grid(n), 512)), dim3(BLOCK), 0, s, o, c->crange, dr);
   LAUNCH(k_range_base, dim3(1), dim3(BLOCK), 0, s, c->crange, rbase, dr);
   RangeReset keep_clean{c};  // resets the context's replica ranges on every exit

@@ -61,16 +61,26 @@ def main(args):
               f"{(2 * f + w) / 1024:9.1f}")
     if out_json:
         import json
-        res = {}
+        # template instances share the base name bench.py's HIP-event marks
+        # use (k_dscan has five): merge them into per-dispatch averages
+        # weighted by dispatches, so average x dispatches = their total
+        tot = defaultdict(lambda: defaultdict(float))
         for k, cs in agg.items():
             b = base_name(k)
-            e = {c: v[0] for c, v in cs.items()}
-            e["dispatches"] = max(v[1] for v in cs.values())
+            nd = max(v[1] for v in cs.values())
+            tot[b]["dispatches"] += nd
+            for c, v in cs.items():
+                tot[b][c] += v[0] * nd
+        res = {}
+        for b, t in tot.items():
+            nd = t.pop("dispatches")
+            e = {c: v / nd for c, v in t.items()}
+            e["dispatches"] = int(nd)
             if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
                 # bytes per dispatch: [raw, corrected] = [F + W, 2F + W] (see the module docstring)
                 e["hbm_bytes"] = (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
                 e["hbm_bytes_raw"] = (e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
-            res.setdefault(b, e)
+            res[b] = e
         json.dump(res, open(out_json, "w"), indent=1, sort_keys=True)
 
 
