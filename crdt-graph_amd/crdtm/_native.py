@@ -18,6 +18,7 @@ PATH_CLOSED_FORM = 1
 PATH_REPLAY = 2
 PATH_DICT_REPLAY = 3
 FLAG_REMERGE = 1  # non-fresh tree merged as init ++ log ++ batch on the parallel paths
+FLAG_INCREMENTAL = 2  # adds-only batch merged into a clean flat document in place (incr.hip)
 REF_NONE = 2 ** 64 - 1
 REF_ROOT = 2 ** 64 - 2
 REL_PARENT, REL_NEXT, REL_PREV, REL_HEAD = 0, 1, 2, 3

@@ -303,6 +303,8 @@ int crdtm_tree_reset(crdtm_tree* t, int64_t replica_id) {
   t->replicas.clear();
   t->last_begin = t->last_end = 0;
   t->last_is_batch = 1;
+  t->flat_clean = true;
+  t->kidx_valid = false;
   ++t->version;
   return CRDTM_OK;
 }
@@ -337,6 +339,7 @@ int crdtm_tree_clone(const crdtm_tree* t, crdtm_tree** out) {
   u->last_begin = t->last_begin;
   u->last_end = t->last_end;
   u->last_is_batch = t->last_is_batch;
+  u->flat_clean = t->flat_clean;  // (the key index stays with `t`: each handle builds its own)
   *out = u;
   return CRDTM_OK;
 }

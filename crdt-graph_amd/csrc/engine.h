@@ -127,6 +127,23 @@ struct crdtm_ctx {
   }
 };
 
+namespace crdtm {
+// Index of a clean flat tree for the incremental closed form (incr.hip), owned
+// by one tree handle: key -> slot (hash), the keys in document order (two
+// buffers: each merge writes the other) and slot -> document rank.
+struct KeyIndex {
+  unsigned long long* keys = nullptr;  // ts ^ INT64_MIN, 0 = empty (TsHash layout)
+  uint32_t* vals = nullptr;
+  uint32_t mask = 0;
+  long long* dk[2] = {nullptr, nullptr};
+  uint32_t* rank = nullptr;
+  uint64_t ocap = 0;  // entries of dk[*] and rank
+  int cur = 0;
+  bool ord_ready = false;
+  ~KeyIndex();
+};
+}  // namespace crdtm
+
 struct crdtm_tree {
   crdtm_ctx* ctx = nullptr;
   crdtm::TreeDev d;
@@ -146,6 +163,12 @@ struct crdtm_tree {
   // last check (no speculation, no sequential replay: R_INCR instead)
   bool remerge = false;
   int64_t own_bias = 0;
+  // a single root dict of live nodes only (no tombstone, orphan or copy) with
+  // `doc` covering every node: the incremental flat closed form (incr.hip) may
+  // merge an adds-only batch into it; kidx = its key index while kidx_valid
+  bool flat_clean = true;
+  std::unique_ptr<crdtm::KeyIndex> kidx;
+  bool kidx_valid = false;
   std::shared_ptr<void> trav;        // traversal cache (api.hip), valid for `version`
   std::shared_ptr<void> dtrav;       // device traversal index (api.hip), valid for `version`
 };
@@ -205,6 +228,11 @@ constexpr int R_INCR = 1 << 20;
 
 // merge.hip
 int sync_read(crdtm_ctx* c);
+// replicas[replicaId t] := t over the applied ops (st) into `rep`; collected by take_replicas after a sync
+int replica_fold(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, Arena& ws, hipStream_t s);
+int take_replicas(crdtm_tree* t, const long long* rep_dev);
+// incr.hip: adds-only flat batch into a clean flat tree; *handled = false leaves it to apply_batch
+int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res, bool* handled);
 __global__ void k_reset_root(uint32_t* s_next);
 int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& ws);
 // pdr.hip

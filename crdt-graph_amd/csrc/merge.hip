@@ -984,7 +984,7 @@ __device__ __forceinline__ long long op_t(const OpsDev& o, uint32_t i) {
   return o.kind[i] == CRDTM_ADD ? o.ts[i] : o.path[o.off[i + 1] - 1];
 }
 
-// Each block folds REP_PER * BLOCK consecutive ops into a direct-mapped LDS
+// Each block folds rep_per * BLOCK consecutive ops into a direct-mapped LDS
 // table (replica id < REP_DIRECT -> 1 + its last applied op; other ids go
 // straight to the global table), loading four ops per thread at a time so the
 // dependent loads of op_t overlap. Same-address LDS atomics serialise, and a
@@ -993,18 +993,19 @@ __device__ __forceinline__ long long op_t(const OpsDev& o, uint32_t i) {
 // The block then publishes one atomicMax per replica it saw; the first
 // publisher of a replica (the table entry was 0) appends it to `rlist`, so the
 // output pass visits the touched replicas only.
-constexpr uint32_t REP_PER = 16;  // ops per thread
+// ops per thread: 16 on large batches (fewer table flushes), 4 on small ones (more workgroups in flight)
+inline uint32_t rep_per(uint32_t n) { return n >= (1u << 22) ? 16u : 4u; }
 __global__ void __launch_bounds__(BLOCK) k_rep_max(OpsDev o, const uint8_t* st, uint32_t* rtab, uint32_t* rlist,
-                                                   uint32_t* rcount) {
+                                                   uint32_t* rcount, uint32_t per) {
   __shared__ uint32_t rv[REP_DIRECT];
   for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) rv[j] = 0;
   __syncthreads();
   const uint32_t n = o.n;
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t b0 = blockIdx.x * (BLOCK * REP_PER) + threadIdx.x;
+  const uint32_t b0 = blockIdx.x * (BLOCK * per) + threadIdx.x;
   constexpr uint32_t OFF = 1u << (REPLICA_BITS - 1);
   uint32_t mr = 0;
-  for (uint32_t k0 = 0; k0 < REP_PER; k0 += 4) {
+  for (uint32_t k0 = 0; k0 < per; k0 += 4) {
     uint32_t ii[4];
     bool ok[4];
 #pragma unroll
@@ -1040,7 +1041,7 @@ __global__ void __launch_bounds__(BLOCK) k_rep_max(OpsDev o, const uint8_t* st, 
     if (rv[j] && atomicMax(&rtab[j + OFF], rv[j]) == 0) rlist[atomicAdd(rcount, 1u)] = j + OFF;
 }
 
-inline uint32_t rep_grid(uint32_t n) { return grid_for(n, BLOCK * REP_PER); }
+inline uint32_t rep_grid(uint32_t n) { return grid_for(n, BLOCK * rep_per(n)); }
 
 // One thread per touched replica: the winner is op rtab[r] - 1; the entry is
 // cleared (the table stays clean between calls).
@@ -2719,7 +2720,7 @@ static int grow_tree_arrays(crdtm_tree* t, const TreeCaps& need) {
   }
   if (need.doc > c.doc) {
     uint64_t n = bump(c.doc, need.doc);
-    int r = grow_array(t->d.doc, 0, n);
+    int r = grow_array(t->d.doc, t->doc_valid ? t->doc_n : 0, n);  // (the incremental merge reads it)
     if (r) return r;
     c.doc = n;
   }
@@ -2778,7 +2779,7 @@ int sync_read(crdtm_ctx* c) {
 
 // Replicas table entries collected by the commit (inline in the result
 // block when they fit, else one copy).
-static int take_replicas(crdtm_tree* t, const long long* rep_dev) {
+int take_replicas(crdtm_tree* t, const long long* rep_dev) {
   const DevResult& h = *t->ctx->hres;
   const uint32_t nrep = h.n_replica_out;
   if (!nrep) return CRDTM_OK;
@@ -2805,13 +2806,12 @@ __global__ void __launch_bounds__(BLOCK) k_post_flags(OpsDev o, const uint8_t* s
 // into c->rtab, collect the touched replicas into `rep` (+ the inline copy).
 static_assert(offsetof(DevResult, n_rep_list) == offsetof(DevResult, n_replica_out) + sizeof(uint32_t),
               "one memset clears both counters");
-static int replica_fold(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, Arena& ws,
-                        hipStream_t s) {
+int replica_fold(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, Arena& ws, hipStream_t s) {
   DevResult* dr = c->dres;
   const uint32_t n = o.n;
   uint32_t* rlist = ws.alloc<uint32_t>(std::min<uint64_t>(n, REPLICA_SLOTS) + 1);
   HIP_CHECK(hipMemsetAsync(&dr->n_replica_out, 0, 2 * sizeof(uint32_t), s));  // n_replica_out, n_rep_list
-  LAUNCH(k_rep_max, dim3(rep_grid(n)), dim3(BLOCK), 0, s, o, st, c->rtab, rlist, &dr->n_rep_list);
+  LAUNCH(k_rep_max, dim3(rep_grid(n)), dim3(BLOCK), 0, s, o, st, c->rtab, rlist, &dr->n_rep_list, rep_per(n));
   LAUNCH(k_rep_out, dim3(64), dim3(BLOCK), 0, s, o, c->rtab, rlist, &dr->n_rep_list, rep, &dr->n_replica_out,
          dr->rep_inline);
   return CRDTM_OK;
@@ -3128,6 +3128,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     res->path_taken = CRDTM_PATH_CLOSED_FORM;
     res->n_applied = applied;
     res->n_already = already;
+    t->flat_clean = true;  // one dict of live nodes (no Deletes on this path), doc covers them
     t->n_slots = 1ULL + K;
     t->n_dicts = 1;
     t->last_begin = t->log_n;
@@ -3552,7 +3553,7 @@ static bool remerge_wanted(const crdtm_tree* t, uint32_t n) {
   return t->log_n <= 4096ULL * n;
 }
 
-int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res) {
+static int apply_batch_paths(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res) {
   const bool fresh = t->n_slots == 1 && t->log_n == 0;
   if (fresh || o.n == 0 || !remerge_wanted(t, o.n)) return apply_core(t, o, st_out, res);
   crdtm_ctx* c = t->ctx;
@@ -3654,6 +3655,35 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   }
   if (st_out) HIP_CHECK(hipMemcpyAsync(st_out, st2 + L, o.n, hipMemcpyDeviceToDevice, s));
   return CRDTM_OK;
+}
+
+// Every apply: an adds-only batch into a clean flat document takes the
+// incremental closed form (incr.hip); the rest the paths above. The flat-clean
+// mark and the key index describe the state, so they follow it: any other
+// commit clears them (the flat closed form sets flat_clean again), a failing
+// batch leaves both as they were.
+int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res) {
+  const bool fresh = t->n_slots == 1 && t->log_n == 0;
+  const bool was_clean = t->flat_clean, was_kidx = t->kidx_valid;
+  if (!fresh && o.n) {
+    bool handled = false;
+    int r = finc_apply(t, o, st_out, res, &handled);
+    if (r != CRDTM_OK || handled) {
+      if (r != CRDTM_OK) {
+        t->flat_clean = was_clean;
+        t->kidx_valid = false;
+      }
+      return r;
+    }
+  }
+  t->flat_clean = false;
+  t->kidx_valid = false;
+  const int r = apply_batch_paths(t, o, st_out, res);
+  if (r != CRDTM_OK || res->code != CRDTM_OK) {  // the state is unchanged
+    t->flat_clean = was_clean;
+    t->kidx_valid = was_kidx && r == CRDTM_OK;
+  }
+  return r;
 }
 
 int linearize(crdtm_tree* t) {

@@ -86,6 +86,8 @@ typedef struct crdtm_result {
 
 /* crdtm_result.flags */
 #define CRDTM_FLAG_REMERGE 1 /* non-fresh tree: merged as init ++ log ++ batch on the parallel paths */
+#define CRDTM_FLAG_INCREMENTAL 2 /* non-fresh flat tree, adds-only batch: merged into the document in place
+                                    (incremental closed form, gaps of the base order; incr.hip) */
 
 typedef struct crdtm_ctx crdtm_ctx;   /* device + stream + workspace */
 typedef struct crdtm_tree crdtm_tree; /* one replica's CRDTree state, resident in HBM */

@@ -108,17 +108,6 @@ def test_deep10m():
     olib().orc_free(ot)
 
 
-def test_deep10m_interleaved():
-    """Config 4's second variant at 10M ops: the same deep
-    tree with its Deletes interleaved among the Adds (tombstones before later
-    inserts in the same dicts: the exact per-dict replay, bench workload
-    deep10m_il)."""
-    spec = dict(CFG4, deletes_last=0)
-    _, et, ot, res = full_parity(spec)
-    assert res.path_taken != N.PATH_CLOSED_FORM
-    olib().orc_free(ot)
-
-
 def test_forced_sequential_replay(monkeypatch):
     """CRDTM_FORCE_REPLAY=1 sends a batch the parallel paths serve to the
     one-lane sequential replay (how bench.py --force-replay measures that

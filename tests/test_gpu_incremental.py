@@ -47,10 +47,13 @@ def failing_batch(s, a):
                 path=np.concatenate([one["path"], bad["path"]]))
 
 
-@pytest.mark.parametrize("mode", ["remerge", "replay"])
+@pytest.mark.parametrize("mode", ["auto", "remerge", "replay"])
 @pytest.mark.parametrize("name", sorted(STREAMS))
 def test_incremental_chain(name, mode, monkeypatch):
-    monkeypatch.setenv("CRDTM_INCREMENTAL", mode)
+    if mode == "auto":  # the default: the incremental flat closed form where it applies
+        monkeypatch.delenv("CRDTM_INCREMENTAL", raising=False)
+    else:
+        monkeypatch.setenv("CRDTM_INCREMENTAL", mode)
     s = N.synth(**STREAMS[name])
     n = len(s["kind"])
     rng = np.random.default_rng(len(name))
@@ -61,7 +64,7 @@ def test_incremental_chain(name, mode, monkeypatch):
     from oracle.oracle import lib as olib
     ot = olib().orc_init(0)
     et = CRDTree.init(0)
-    remerged = 0
+    remerged = incr = 0
     for k, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
         if k == 3:  # a failing batch in the middle: Err, nothing changes
             before = engine_summary(et)
@@ -82,6 +85,10 @@ def test_incremental_chain(name, mode, monkeypatch):
             remerged += 1
         if k and mode == "replay":
             assert res.path_taken == N.PATH_REPLAY and not res.flags & N.FLAG_REMERGE
+        if mode != "auto":
+            assert not res.flags & N.FLAG_INCREMENTAL
+        elif res.flags & N.FLAG_INCREMENTAL:
+            incr += 1
         assert res.n_applied == len(oracle_log(ot, 0)[0]) - n_log0 == int(np.sum(st == 0)), k
         assert engine_summary(et) == oracle_summary(ot), (k, a, b)
         assert engine_log(et, 1) == oracle_log(ot, 1), k
@@ -89,6 +96,67 @@ def test_incremental_chain(name, mode, monkeypatch):
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
     if mode == "remerge" and name != "nested_interleaved":
         assert remerged == len(cuts) - 2  # every incremental step took the parallel paths
+    if mode == "auto":
+        # adds-only flat batches into a flat document: the incremental closed form
+        assert (incr == len(cuts) - 2) if name == "flat_adds" else incr == 0
+    olib().orc_free(ot)
+
+
+# flat typing streams for the incremental closed form (incr.hip): many
+# replicas typing at once (new runs landing in the same gaps, new anchors in
+# other gaps, non-Lamport anchors), few replicas with long lags, and the
+# sentinel as anchor
+FINC_STREAMS = {
+    "r64_w256": dict(n_ops=120000, replicas=64, window=256, seed=41),
+    "r4_w2000": dict(n_ops=60000, replicas=4, window=2000, seed=42),
+    "r16_w16": dict(n_ops=60000, replicas=16, window=16, seed=43),
+    "r2_w1": dict(n_ops=30000, replicas=2, window=1, seed=44),
+}
+
+
+@pytest.mark.parametrize("name", sorted(FINC_STREAMS))
+def test_incremental_flat_closed_form(name, monkeypatch):
+    """Adds-only flat batches merged into a flat document in place
+    (CRDTM_FLAG_INCREMENTAL): batches of 1 .. 20,000 ops chained against the
+    oracle tree (structure, visible order, log, lastOperation, replicas,
+    timestamp); then one Delete, after which the document is no longer clean
+    and later batches take the general paths."""
+    monkeypatch.delenv("CRDTM_INCREMENTAL", raising=False)
+    from oracle.oracle import lib as olib
+    s = N.synth(**FINC_STREAMS[name])
+    n = len(s["kind"])
+    rng = np.random.default_rng(7)
+    cuts = [0, n // 5]
+    while cuts[-1] < n:
+        cuts.append(min(n, cuts[-1] + int(rng.choice([1, 2, 64, 1000, 5000, 20000]))))
+    ot = olib().orc_init(0)
+    et = CRDTree.init(0)
+    used = 0
+    for k, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        chunk = sub(s, a, b)
+        _, rc, _ = oracle_apply_arrays(chunk, b - a, tree=ot)
+        res = et.apply_arrays(chunk, b - a)
+        assert res.code == rc == 0, (k, res.code, rc)
+        used += bool(res.flags & N.FLAG_INCREMENTAL)
+        if k % 7 == 0 or b == n:
+            assert engine_summary(et) == oracle_summary(ot), (k, a, b)
+            assert engine_log(et, 1) == oracle_log(ot, 1), k
+    assert used == len(cuts) - 2
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+    # a Delete makes the document unclean: no incremental closed form afterwards
+    key = int(s["ts"][n // 3])
+    dl = dict(kind=np.ones(1, np.uint8), ts=np.zeros(1, np.int64), val=np.zeros(1, np.uint32),
+              path_off=np.array([0, 1], np.uint32), path=np.array([key], np.int64))
+    _, rc, _ = oracle_apply_arrays(dl, 1, tree=ot)
+    res = et.apply_arrays(dl, 1)
+    assert res.code == rc == 0 and not res.flags & N.FLAG_INCREMENTAL
+    more = N.synth(**dict(FINC_STREAMS[name], n_ops=n + 3000))
+    chunk = sub(more, n, n + 3000)
+    _, rc, _ = oracle_apply_arrays(chunk, 3000, tree=ot)
+    res = et.apply_arrays(chunk, 3000)
+    assert res.code == rc and not res.flags & N.FLAG_INCREMENTAL
+    assert engine_summary(et) == oracle_summary(ot)
     olib().orc_free(ot)
 
 
