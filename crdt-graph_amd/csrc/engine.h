@@ -137,6 +137,8 @@ struct KeyIndex {
   uint32_t mask = 0;
   long long* dk[2] = {nullptr, nullptr};
   uint32_t* rank = nullptr;
+  uint32_t* doc2 = nullptr;  // the next document order (swapped with the tree's `doc` by each merge)
+  uint64_t doc2_cap = 0;
   uint64_t ocap = 0;  // entries of dk[*] and rank
   int cur = 0;
   bool ord_ready = false;

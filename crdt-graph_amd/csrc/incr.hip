@@ -33,7 +33,7 @@ namespace crdtm {
 
 constexpr uint32_t FI_BLK = 64;             // ranks per block minimum (one wave)
 constexpr uint32_t FI_SUP = 64;             // blocks per superblock
-constexpr uint32_t FI_MAX_BATCH = 1u << 16; // larger batches re-merge
+constexpr uint32_t FI_MAX_BATCH = 1u << 14; // larger batches re-merge (k_fi_jump holds 16 per thread)
 constexpr uint32_t FI_GAP_STEPS = 1u << 22; // walk budget per gap (else re-merge)
 constexpr long long FI_INF = 0x7fffffffffffffffLL;
 
@@ -42,7 +42,7 @@ enum : uint32_t { FI_FAIL = 1u, FI_BUDGET = 2u };
 
 KeyIndex::~KeyIndex() {
   for (void* q : {static_cast<void*>(keys), static_cast<void*>(vals), static_cast<void*>(dk[0]),
-                  static_cast<void*>(dk[1]), static_cast<void*>(rank)})
+                  static_cast<void*>(dk[1]), static_cast<void*>(rank), static_cast<void*>(doc2)})
     if (q) hipFree(q);
 }
 
@@ -68,21 +68,31 @@ __global__ void __launch_bounds__(BLOCK) k_fi_prep(uint32_t K, const uint32_t* d
   }
 }
 
-// bmin[b] = the smallest of keys [64 b, 64 b + 64), one wave per block
+// bmin[b] = the smallest of keys [64 b, 64 b + 64): a wave covers four
+// blocks, four keys per lane (two 16-byte loads), 16 lanes per block
 __global__ void __launch_bounds__(BLOCK) k_fi_bmin(uint32_t K, const long long* dk, long long* bmin) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t nb = (K + FI_BLK - 1) / FI_BLK;
-  for (uint32_t b0 = (blockIdx.x * blockDim.x + threadIdx.x) / 64; b0 < nb; b0 += gridDim.x * blockDim.x / 64) {
-    const uint32_t r = b0 * FI_BLK + lane;
-    long long k = r < K ? dk[r] : FI_INF;
+  const uint32_t nw = (nb + 3) / 4;
+  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64; w < nw; w += gridDim.x * blockDim.x / 64) {
+    const uint32_t r = w * 256 + 4 * lane;
+    long long k = FI_INF;
+    if (r + 4 <= K) {
+      const longlong2 a = *reinterpret_cast<const longlong2*>(dk + r);
+      const longlong2 c = *reinterpret_cast<const longlong2*>(dk + r + 2);
+      k = min(min(a.x, a.y), min(c.x, c.y));
+    } else {
+      for (uint32_t j = r; j < K && j < r + 4; ++j) k = min(k, dk[j]);
+    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
+    for (int o = 8; o > 0; o >>= 1) {
       const uint32_t lo = __shfl_xor(static_cast<uint32_t>(k), o, 64);
       const uint32_t hi = __shfl_xor(static_cast<uint32_t>(static_cast<unsigned long long>(k) >> 32), o, 64);
       const long long v = static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo);
       k = v < k ? v : k;
     }
-    if (lane == 0) bmin[b0] = k;
+    const uint32_t b = w * 4 + lane / 16;
+    if ((lane & 15) == 0 && b < nb) bmin[b] = k;
   }
 }
 
@@ -158,52 +168,49 @@ __global__ void __launch_bounds__(BLOCK) k_fi_resolve(OpsDev o, TsHash kx, TsHas
 }
 
 // Pointer jumping, all rounds in one workgroup: (start, min threshold)
-// composed along the new anchors; buffers 0 / 1 alternate, and after the
-// barrier of a round its writes are visible to the whole workgroup. Chains
-// are short (typing runs), so the rounds stop once no anchor is left; the
-// result is copied to buffer 0 if it ended in buffer 1.
-constexpr uint32_t FI_JUMP_THREADS = 1024;
-__global__ void __launch_bounds__(FI_JUMP_THREADS) k_fi_jump(uint32_t m, uint32_t rounds, uint32_t* pa,
-                                                             uint32_t* pb, uint32_t* sa, uint32_t* sb, long long* ta,
-                                                             long long* tb) {
+// composed along the new anchors. Each round reads every element's jumped
+// values into registers, then (after a barrier) writes them back in place:
+// no second buffer, and chains are short (typing runs), so the rounds stop
+// once no anchor is left. Up to FI_JUMP_PER elements per thread.
+constexpr uint32_t FI_JUMP_THREADS = 1024, FI_JUMP_PER = 16;
+__global__ void __launch_bounds__(FI_JUMP_THREADS) k_fi_jump(uint32_t m, uint32_t rounds, uint32_t* P, uint32_t* S,
+                                                             long long* T) {
   __shared__ uint32_t live[32];  // one flag per round (rounds <= 16: m <= 2^16)
   if (threadIdx.x < 32) live[threadIdx.x] = 0;
   __syncthreads();
-  uint32_t k = 0;
-  for (; k < rounds; ++k) {
-    const uint32_t* p0 = (k & 1) ? pb : pa;
-    const uint32_t* s0 = (k & 1) ? sb : sa;
-    const long long* t0 = (k & 1) ? tb : ta;
-    uint32_t* p1 = (k & 1) ? pa : pb;
-    uint32_t* s1 = (k & 1) ? sa : sb;
-    long long* t1 = (k & 1) ? ta : tb;
+  for (uint32_t k = 0; k < rounds; ++k) {
+    uint32_t np[FI_JUMP_PER], ns[FI_JUMP_PER];
+    long long nt[FI_JUMP_PER];
     uint32_t any = 0;
-    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-      const uint32_t p = p0[i];
-      if (p == NONE) {
-        p1[i] = NONE;
-        s1[i] = s0[i];
-        t1[i] = t0[i];
-      } else {
-        const uint32_t pp = p0[p];
-        p1[i] = pp;
-        s1[i] = s0[p];
-        t1[i] = min(t0[i], t0[p]);
-        any |= pp != NONE;
+#pragma unroll
+    for (uint32_t u = 0; u < FI_JUMP_PER; ++u) {
+      const uint32_t i = threadIdx.x + u * FI_JUMP_THREADS;
+      np[u] = NONE;
+      if (i < m) {
+        const uint32_t p = P[i];
+        ns[u] = S[i];
+        nt[u] = T[i];
+        if (p != NONE) {
+          np[u] = P[p];
+          ns[u] = S[p];
+          nt[u] = min(nt[u], T[p]);
+          any |= np[u] != NONE;
+        }
+      }
+    }
+    __syncthreads();  // every read of this round before any write
+#pragma unroll
+    for (uint32_t u = 0; u < FI_JUMP_PER; ++u) {
+      const uint32_t i = threadIdx.x + u * FI_JUMP_THREADS;
+      if (i < m) {
+        P[i] = np[u];
+        S[i] = ns[u];
+        T[i] = nt[u];
       }
     }
     if (any) live[k] = 1;
-    __syncthreads();
-    if (!live[k]) {
-      ++k;
-      break;
-    }
-  }
-  if (k & 1) {  // the result is in buffer 1
-    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-      sa[i] = sb[i];
-      ta[i] = tb[i];
-    }
+    __syncthreads();  // writes visible to the workgroup, live[k] final
+    if (!live[k]) break;
   }
 }
 
@@ -501,9 +508,9 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   const uint32_t bcap = pow2_ge(2ULL * m);
   TsHash bh{ws.alloc<unsigned long long>(bcap), ws.alloc<uint32_t>(bcap), bcap - 1};
   uint32_t* fi = ws.alloc<uint32_t>(4);
-  uint32_t* par[2] = {ws.alloc<uint32_t>(m), ws.alloc<uint32_t>(m)};
-  uint32_t* sta[2] = {ws.alloc<uint32_t>(m), ws.alloc<uint32_t>(m)};
-  long long* thr[2] = {ws.alloc<long long>(m), ws.alloc<long long>(m)};
+  uint32_t* par[1] = {ws.alloc<uint32_t>(m)};
+  uint32_t* sta[1] = {ws.alloc<uint32_t>(m)};
+  long long* thr[1] = {ws.alloc<long long>(m)};
   uint32_t* par0 = ws.alloc<uint32_t>(m);
   uint32_t* gk[2] = {ws.alloc<uint32_t>(m), ws.alloc<uint32_t>(m)};
   uint32_t* gv[2] = {ws.alloc<uint32_t>(m), ws.alloc<uint32_t>(m)};
@@ -513,7 +520,6 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   uint32_t* glist = ws.alloc<uint32_t>(m);
   uint32_t* ord = ws.alloc<uint32_t>(m);
   uint32_t* first = ws.alloc<uint32_t>(m);
-  uint32_t* newdoc = ws.alloc<uint32_t>(static_cast<uint64_t>(K) + m);
   uint32_t* newrank = ws.alloc<uint32_t>(m);
   uint8_t* st = ws.alloc<uint8_t>(m);
   long long* rep = ws.alloc<long long>(2ULL * m + 2);
@@ -530,7 +536,7 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
     LAUNCH(k_fi_prep, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d.s_key, dk, rank_of);
     X.ord_ready = true;
   }
-  LAUNCH(k_fi_bmin, dim3(grid_for(static_cast<uint64_t>(nb) * 64)), dim3(BLOCK), 0, s, K, dk, bmin);
+  LAUNCH(k_fi_bmin, dim3(grid_for(static_cast<uint64_t>(nb + 3) / 4 * 64)), dim3(BLOCK), 0, s, K, dk, bmin);
   LAUNCH(k_fi_sup, dim3(grid_for(ns)), dim3(BLOCK), 0, s, nb, bmin, smin);
   LAUNCH(k_fi_bidx, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, bh, fi);
   LAUNCH(k_fi_resolve, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, kx, bh, rank_of, replica_of(t->timestamp), par[0],
@@ -538,9 +544,7 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   // ---- phase B: gaps (pointer jumping over new anchors, one NSR query each) ----
   uint32_t rounds = 0;
   for (uint32_t span = 1; span < m; span <<= 1) ++rounds;
-  if (rounds)
-    LAUNCH(k_fi_jump, dim3(1), dim3(FI_JUMP_THREADS), 0, s, m, rounds, par[0], par[1], sta[0], sta[1], thr[0],
-           thr[1]);
+  if (rounds) LAUNCH(k_fi_jump, dim3(1), dim3(FI_JUMP_THREADS), 0, s, m, rounds, par[0], sta[0], thr[0]);
   const int cur = 0;
   LAUNCH(k_fi_gap, dim3(grid_for(64ULL * m)), dim3(BLOCK), 0, s, m, K, dk, bmin, smin, sta[cur], thr[cur], gk[0],
          gv[0]);
@@ -568,12 +572,22 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   need.doc = std::max<uint64_t>(need.doc, K64 + m + 1);
   if (need.slots > t->cap.slots || need.log > t->cap.log || need.lpath > t->cap.lpath || need.doc > t->cap.doc)
     if ((r = grow_tree(t, need))) return r;
+  if (X.doc2_cap < t->cap.doc) {  // the next order's buffer matches the tree's doc capacity
+    if (X.doc2) hipFree(X.doc2);
+    X.doc2 = nullptr;
+    HIP_CHECK(hipMalloc(&X.doc2, t->cap.doc * sizeof(uint32_t)));
+    X.doc2_cap = t->cap.doc;
+  }
+  uint32_t* newdoc = X.doc2;
   const uint32_t slot0 = static_cast<uint32_t>(t->n_slots);
   LAUNCH(k_fi_doc, dim3(grid_for(K64 + m)), dim3(BLOCK), 0, s, K, m, t->d.doc, sk, sv, ord, first, slot0, o.ts,
          dk, newdoc, newrank, X.dk[X.cur ^ 1], rank_of);
   X.cur ^= 1;
   LAUNCH(k_fi_next, dim3(grid_for(m)), dim3(BLOCK), 0, s, K, m, sv, ord, newrank, newdoc, slot0, t->d.s_next);
-  HIP_CHECK(hipMemcpyAsync(t->d.doc, newdoc, (K64 + m) * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  // the new order becomes the tree's (the store owns whichever buffer `doc` holds)
+  std::swap(t->d.doc, X.doc2);
+  std::swap(t->cap.doc, X.doc2_cap);
+  t->store->d.doc = t->d.doc;
   LAUNCH(k_fi_commit, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, slot0, static_cast<uint32_t>(t->log_n),
          static_cast<uint32_t>(t->log_npath), t->d);
   LAUNCH(k_kx_insert, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, slot0, kx);

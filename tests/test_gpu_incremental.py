@@ -117,7 +117,7 @@ FINC_STREAMS = {
 @pytest.mark.parametrize("name", sorted(FINC_STREAMS))
 def test_incremental_flat_closed_form(name, monkeypatch):
     """Adds-only flat batches merged into a flat document in place
-    (CRDTM_FLAG_INCREMENTAL): batches of 1 .. 20,000 ops chained against the
+    (CRDTM_FLAG_INCREMENTAL): batches of 1 .. 16,000 ops chained against the
     oracle tree (structure, visible order, log, lastOperation, replicas,
     timestamp); then one Delete, after which the document is no longer clean
     and later batches take the general paths."""
@@ -128,7 +128,7 @@ def test_incremental_flat_closed_form(name, monkeypatch):
     rng = np.random.default_rng(7)
     cuts = [0, n // 5]
     while cuts[-1] < n:
-        cuts.append(min(n, cuts[-1] + int(rng.choice([1, 2, 64, 1000, 5000, 20000]))))
+        cuts.append(min(n, cuts[-1] + int(rng.choice([1, 2, 64, 1000, 5000, 16000]))))
     ot = olib().orc_init(0)
     et = CRDTree.init(0)
     used = 0
