@@ -611,24 +611,39 @@ __global__ void __launch_bounds__(BLOCK) k_lv_fin(OpsDev o, Work w, TsIndex h, c
 __global__ void __launch_bounds__(BLOCK) k_stats(OpsDev o, Work w, long long ts0, DevResult* dres) {
   uint32_t app = 0, alr = 0, err = NONE, own = 0, addapp = 0, last_add = 0, first_del = NONE;
   const long long id0 = replica_of(ts0);
-  const uint32_t n = o.n;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  const uint32_t trips = (n + stride - 1) / stride;
-  for (uint32_t t = 0; t < trips; ++t) {
-    const uint32_t i = t * stride + blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) continue;
-    const uint8_t s = w.st[i];
-    if (s == ST_APPLIED) ++app;
-    else if (s == ST_ALREADY) ++alr;
-    else err = min(err, i);
-    if (o.kind[i] == CRDTM_ADD) {
-      if ((s == ST_APPLIED || s == ST_ALREADY) && replica_of(o.ts[i]) == id0) ++own;
-      if (s == ST_APPLIED) {
-        ++addapp;
-        last_add = max(last_add, i + 1);
+  // four ops per lane: statuses and kinds as one 4-byte load each, the
+  // timestamps as two 16-byte loads (independent of the statuses)
+  QUAD_LOOP(i0, o.n) {
+    Quad q;
+    load_quad(o, i0, q);
+    uint8_t sv[4];
+    if (q.cnt == 4) {
+      const uchar4 s4 = *reinterpret_cast<const uchar4*>(w.st + i0);
+      sv[0] = s4.x;
+      sv[1] = s4.y;
+      sv[2] = s4.z;
+      sv[3] = s4.w;
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) sv[k] = k < q.cnt ? w.st[i0 + k] : ST_ALREADY;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      if (k >= q.cnt) break;
+      const uint32_t i = i0 + k;
+      const uint8_t s = sv[k];
+      if (s == ST_APPLIED) ++app;
+      else if (s == ST_ALREADY) ++alr;
+      else err = min(err, i);
+      if (q.kind[k] == CRDTM_ADD) {
+        if ((s == ST_APPLIED || s == ST_ALREADY) && replica_of(q.ts[k]) == id0) ++own;
+        if (s == ST_APPLIED) {
+          ++addapp;
+          last_add = max(last_add, i + 1);
+        }
+      } else if (s == ST_APPLIED) {
+        first_del = min(first_del, i);
       }
-    } else if (s == ST_APPLIED) {
-      first_del = min(first_del, i);
     }
   }
   app = block_sum(app);
@@ -3328,7 +3343,7 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
     }
   }
   HIP_CHECK(hipMemsetAsync(&dr->first_del, 0xFF, sizeof(uint32_t), s));
-  LAUNCH(k_stats, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, o, w, t->timestamp, dr);
+  LAUNCH(k_stats, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, w, t->timestamp, dr);
   if ((r = sync_read(c))) return r;
   if (c->hres->first_del != NONE && c->hres->last_add > c->hres->first_del + 1) {
     LAUNCH(k_guard_maxadd, dim3(g), dim3(BLOCK), 0, s, o, w);

@@ -108,6 +108,47 @@ def test_deep10m():
     olib().orc_free(ot)
 
 
+def test_incremental_flat_1m(monkeypatch):
+    """The bench's incremental workload shape at scale: a 1M-node flat
+    document (config 3's stream, closed form), then successive 10k-op batches
+    of the same stream merged in place (CRDTM_FLAG_INCREMENTAL); the final
+    structure and visible digests against the fast flat restatement
+    (`orc_flat_replay`, pinned against the general one) over the whole
+    stream, and the device document order against the host walk."""
+    import ctypes as C
+    monkeypatch.delenv("CRDTM_INCREMENTAL", raising=False)
+    base, bsz, nb = 1_000_000, 10_000, 4
+    n = base + bsz * nb
+    s = N.synth(n_ops=n, replicas=64, window=256, seed=0xC0FFEE03)
+    off = s["path_off"]
+
+    def sub(a, b):
+        return dict(kind=s["kind"][a:b], ts=s["ts"][a:b], val=s["val"][a:b],
+                    path_off=(off[a:b + 1] - off[a]).astype(np.uint32), path=s["path"][off[a]:off[b]])
+
+    et = CRDTree.init(0)
+    assert et.apply_arrays(sub(0, base), base).code == 0
+    for k in range(nb):
+        a = base + k * bsz
+        res = et.apply_arrays(sub(a, a + bsz), bsz)
+        assert res.code == 0 and res.flags & N.FLAG_INCREMENTAL, (k, res.code, res.flags)
+        assert res.n_applied == bsz
+    h = np.zeros(2, np.uint64)
+    w = np.zeros(2, np.uint64)
+    err = C.c_int64(-1)
+    na = C.c_uint64()
+    rc = olib().orc_flat_replay(n, _ptr(s["kind"]), _ptr(s["ts"]), _ptr(s["path_off"]), _ptr(s["path"]),
+                                _ptr(s["val"]), C.byref(err), _ptr(h), _ptr(w), C.byref(na))
+    assert rc == 0 and na.value == n
+    for which in (0, 1):
+        _, enw, eh = et.canonical(which, full=False)
+        assert (enw, eh) == (int(w[which]), int(h[which])), which
+    words, nw, _ = et.canonical(1, full=True)
+    assert np.array_equal(et.document_handles().astype(np.int64), words[1::4])
+    en, ea, _ = engine_log_np(et, 0)  # the log: every op, in order
+    assert en == n and np.array_equal(ea["ts"][:n], s["ts"]) and np.array_equal(ea["path"][:n], s["path"])
+
+
 def test_forced_sequential_replay(monkeypatch):
     """CRDTM_FORCE_REPLAY=1 sends a batch the parallel paths serve to the
     one-lane sequential replay (how bench.py --force-replay measures that
