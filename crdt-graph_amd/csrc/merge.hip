@@ -1446,13 +1446,13 @@ struct Fnv {
 // ---------------------------------------------------------------------------
 // Forest fast path for flat documents (every op's path has length <= 1) of
 // at most FL_MAXOPS ops, in two kernels.
-// k_forest_prep (one 256-thread workgroup per document): the document's Add
-// keys and the sentinel key 0
-// are sorted in LDS (bitonic); a key's slot = the index of its first
-// occurrence, so slot order is key order (findInsertion's `ts > key` becomes
-// a slot comparison) and every op's target / anchor slot is one binary
-// search. Result: one packed word per op in HBM.
-// k_forest_lanes (one lane per document): the literal sequential replay of
+// k_forest_prep (one 256-thread workgroup per document): every Add key and
+// the sentinel key 0 get a slot such that slot order is key order
+// (findInsertion's `ts > key` becomes a slot comparison): the replicas'
+// counter ranges laid end to end when they fit (one scan), else the keys
+// sorted in LDS (bitonic) with a key's slot = its first sorted position.
+// Result: one packed word per op in HBM.
+// k_forest_wave (one wave per document): the literal sequential replay of
 // addAfterHelp / findInsertion / deleteHelp (src/Internal/Node.elm:56-122) on
 // one packed word per slot {next, present, tombstone, orphan}, including the
 // copy quirk (a flat node's children are always the initial empty dict, so a
@@ -1477,11 +1477,21 @@ __device__ __forceinline__ uint32_t fl_lower(const long long* k, long long x) {
 }
 
 constexpr uint32_t FPREP_THREADS = 256;  // one workgroup (4 waves) per document
+constexpr uint32_t FPREP_PER = FL_SLOTS / FPREP_THREADS;  // ops (sort keys) per thread
+constexpr uint32_t FPREP_REPS = 64;  // replica ids the dense slot map covers
 
+// A document's slot map. Dense form: slot(key) = base[replica] + counter, the
+// replicas' counter ranges laid end to end after the sentinel's slot 0 --
+// order preserving and injective, so findInsertion's `ts > key` stays a slot
+// comparison; unused counters just leave unused slots. It needs every Add key
+// >= 0 with replica id < FPREP_REPS and the ranges to fit FL_SLOTS; otherwise
+// the keys are sorted (bitonic) and a slot is a key's first sorted position.
 __global__ void __launch_bounds__(FPREP_THREADS) k_forest_prep(OpsDev o, const uint32_t* doc_off, uint32_t n_docs, long long ts0,
                                                     uint32_t* opw, uint16_t* sent, uint8_t* fb, longlong2* vt) {
   __shared__ long long skey[FL_SLOTS];
   __shared__ uint32_t cre[FL_SLOTS];  // slot -> its first Add (the one that can create it)
+  __shared__ uint32_t rlo[FPREP_REPS], rhi[FPREP_REPS], rbase[FPREP_REPS];
+  __shared__ uint32_t pflags;  // bit0: a path longer than 1 (not flat); bit1: no dense map
   const uint32_t d = blockIdx.x;
   if (d >= n_docs) return;
   const uint32_t lane = threadIdx.x;
@@ -1492,62 +1502,127 @@ __global__ void __launch_bounds__(FPREP_THREADS) k_forest_prep(OpsDev o, const u
   }
   constexpr long long INF = 0x7fffffffffffffffLL;
   const long long own = replica_of(ts0);
-  uint32_t bad = 0;
-  for (uint32_t j = lane; j < FL_SLOTS; j += FPREP_THREADS) {
-    long long key = INF;
+  for (uint32_t j = lane; j < FL_SLOTS; j += FPREP_THREADS) cre[j] = NONE;
+  if (lane < FPREP_REPS) {
+    rlo[lane] = 0xffffffffu;
+    rhi[lane] = 0;
+  }
+  if (lane == 0) pflags = 0;
+  __syncthreads();
+  // op j = lane + u * FPREP_THREADS stays in registers: ts, first path key,
+  // and {1: empty path, 2: Add, 4: Add with a one-key path (owns a sort key)}
+  long long kt[FPREP_PER], ka[FPREP_PER];
+  uint32_t ks[FPREP_PER];
+  uint32_t flags = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < FPREP_PER; ++u) {
+    const uint32_t j = lane + u * FPREP_THREADS;
+    kt[u] = ka[u] = 0;
+    ks[u] = 0;
     if (j < nops) {
       const uint32_t i = ob + j;
-      const uint32_t L = o.off[i + 1] - o.off[i];
-      if (L > 1) bad = 1;
-      if (o.kind[i] == CRDTM_ADD && L == 1) key = o.ts[i];
-    } else if (j == nops) {
-      key = 0;  // the root dict's sentinel
+      const uint32_t p0 = o.off[i], L = o.off[i + 1] - p0;
+      const bool add = o.kind[i] == CRDTM_ADD;
+      kt[u] = o.ts[i];
+      if (L > 1) flags |= 1u;
+      if (L >= 1) ka[u] = o.path[p0];
+      ks[u] = (L == 0 ? 1u : 0u) | (add ? 2u : 0u) | (add && L == 1 ? 4u : 0u);
+      if (add && L == 1) {
+        const long long t = kt[u];
+        const unsigned long long r = static_cast<unsigned long long>(t) >> 32;
+        if (t < 0 || r >= FPREP_REPS) {
+          flags |= 2u;
+        } else if (t > 0) {
+          atomicMin(&rlo[r], static_cast<uint32_t>(t));
+          atomicMax(&rhi[r], static_cast<uint32_t>(t));
+        }
+      }
     }
-    skey[j] = key;
-    cre[j] = NONE;
   }
-  if (__syncthreads_or(bad)) {
+  if (flags) atomicOr(&pflags, flags);
+  __syncthreads();
+  const uint32_t pf = pflags;
+  if (pf & 1u) {
     if (lane == 0) fb[d] = 1;
     return;
   }
-  for (uint32_t k = 2; k <= FL_SLOTS; k <<= 1) {
-    for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-      for (uint32_t i = lane; i < FL_SLOTS; i += FPREP_THREADS) {
-        const uint32_t ixj = i ^ jj;
-        if (ixj > i) {
-          const long long a = skey[i], b = skey[ixj];
-          if ((a > b) == ((i & k) == 0)) {
-            skey[i] = b;
-            skey[ixj] = a;
+  if (!(pf & 2u) && lane < FPREP_REPS) {  // wave 0: the replicas' slot bases (one scan)
+    const uint32_t lo = rlo[lane], hi = rhi[lane];
+    const uint32_t range = hi < lo ? 0u : (hi - lo < FL_SLOTS ? hi - lo + 1u : FL_SLOTS);
+    uint32_t inc = range;
+#pragma unroll
+    for (uint32_t k = 1; k < FPREP_REPS; k <<= 1) {
+      const uint32_t y = __shfl_up(inc, k, FPREP_REPS);
+      if (lane >= k) inc += y;
+    }
+    rbase[lane] = 1u + (inc - range) - lo;
+    if (lane == FPREP_REPS - 1 && inc >= FL_SLOTS) atomicOr(&pflags, 2u);
+  }
+  __syncthreads();
+  const bool dense = !(pflags & 2u);
+  uint32_t tsl[FPREP_PER];
+  if (dense) {
+#pragma unroll
+    for (uint32_t u = 0; u < FPREP_PER; ++u) {
+      const long long t = kt[u];  // (an owned key is in the map; other ops' ts are not looked up)
+      tsl[u] = (ks[u] & 4u) && t != 0 ? rbase[static_cast<unsigned long long>(t) >> 32] + static_cast<uint32_t>(t) : 0u;
+      if (ks[u] & 4u) atomicMin(&cre[tsl[u]], lane + u * FPREP_THREADS);
+    }
+  } else {
+#pragma unroll
+    for (uint32_t u = 0; u < FPREP_PER; ++u) {
+      const uint32_t j = lane + u * FPREP_THREADS;
+      skey[j] = j < nops ? ((ks[u] & 4u) ? kt[u] : INF) : (j == nops ? 0 : INF);  // 0: the root dict's sentinel
+    }
+    for (uint32_t k = 2; k <= FL_SLOTS; k <<= 1) {
+      for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+        __syncthreads();
+        for (uint32_t i = lane; i < FL_SLOTS; i += FPREP_THREADS) {
+          const uint32_t ixj = i ^ jj;
+          if (ixj > i) {
+            const long long a = skey[i], b = skey[ixj];
+            if ((a > b) == ((i & k) == 0)) {
+              skey[i] = b;
+              skey[ixj] = a;
+            }
           }
         }
       }
-      __syncthreads();
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < FPREP_PER; ++u) {
+      tsl[u] = (ks[u] & 2u) ? fl_lower(skey, kt[u]) : 0u;
+      if (ks[u] & 4u) atomicMin(&cre[tsl[u]], lane + u * FPREP_THREADS);
     }
   }
-  for (uint32_t j = lane; j < nops; j += FPREP_THREADS) {
-    const uint32_t i = ob + j;
-    const uint32_t L = o.off[i + 1] - o.off[i];
+  __syncthreads();  // cre complete: a slot is present iff some Add owns its key
+#pragma unroll
+  for (uint32_t u = 0; u < FPREP_PER; ++u) {
+    const uint32_t j = lane + u * FPREP_THREADS;
+    if (j >= nops) continue;
     uint32_t w;
-    if (L == 0) {
+    if (ks[u] & 1u) {
       w = FO_INV | FL_N | (FL_N << 11);
     } else {
-      const long long k0 = o.path[o.off[i]];
-      const uint32_t p = fl_lower(skey, k0);
-      const uint32_t ps = (p < FL_SLOTS && skey[p] == k0) ? p : FL_N;
-      if (o.kind[i] != CRDTM_ADD) {
-        w = FO_DEL | ps | (FL_N << 11);
+      const long long k0 = ka[u];
+      uint32_t ps = FL_N;
+      if (dense) {
+        const unsigned long long r = static_cast<unsigned long long>(k0) >> 32;
+        const uint32_t c = static_cast<uint32_t>(k0);
+        if (k0 == 0) ps = 0;
+        else if (k0 > 0 && r < FPREP_REPS && c >= rlo[r] && c <= rhi[r] && cre[rbase[r] + c] != NONE) ps = rbase[r] + c;
       } else {
-        const long long t = o.ts[i];
-        w = fl_lower(skey, t) | (ps << 11) | (replica_of(t) == own ? FO_OWN : 0u);
+        const uint32_t p = fl_lower(skey, k0);
+        if (p < FL_SLOTS && skey[p] == k0) ps = p;
       }
+      if (!(ks[u] & 2u)) w = FO_DEL | ps | (FL_N << 11);
+      else w = tsl[u] | (ps << 11) | (replica_of(kt[u]) == own ? FO_OWN : 0u);
     }
-    opw[i] = w;
-    if (o.kind[i] == CRDTM_ADD && L == 1) atomicMin(&cre[w & FL_N], j);
+    opw[ob + j] = w;
   }
-  if (lane == 0) sent[d] = static_cast<uint16_t>(fl_lower(skey, 0));
+  if (lane == 0) sent[d] = static_cast<uint16_t>(dense ? 0u : fl_lower(skey, 0));
   if (!vt) return;
-  __syncthreads();
   // hash inputs per slot: value and timestamp of the Add that creates it
   longlong2* v = vt + static_cast<uint64_t>(d) * FL_SLOTS;
   for (uint32_t j = lane; j < FL_SLOTS; j += FPREP_THREADS) {
@@ -1557,162 +1632,141 @@ __global__ void __launch_bounds__(FPREP_THREADS) k_forest_prep(OpsDev o, const u
 }
 
 // ---------------------------------------------------------------------------
-// Lane-per-document replay (the literal addAfterHelp / findInsertion /
-// deleteHelp, src/Internal/Node.elm:56-122, copy quirk included): lane m < D
-// of a workgroup replays document blockIdx.x * D + m on a 16-bit word per slot {next:11, present, tombstone, orphan} in LDS. A
-// wave-uniform replay puts every step on the CU's scalar unit (~123k scalar
-// instructions per 1,000-op document); here each step is a handful of vector
-// instructions, and small D leaves many waves per SIMD to hide the dependent
-// LDS latency of the walks. The op words reach LDS 64 per document at a time,
-// loaded coalesced by the whole wave. What a slot carries for the hash (value,
-// timestamp of its Add; a copy takes the copied node's) lives in `vt`, written
-// by k_forest_prep and updated on the (rare) copy quirk.
+// Wave-per-document replay (the literal addAfterHelp / findInsertion /
+// deleteHelp, src/Internal/Node.elm:56-122, copy quirk included) on a 16-bit
+// word per slot {next:11, present, tombstone, orphan} in LDS. What a slot
+// carries for the hash (value, timestamp of its Add; a copy takes the copied
+// node's) lives in `vt`, written by k_forest_prep and updated on the (rare)
+// copy quirk.
 // ---------------------------------------------------------------------------
 constexpr uint16_t FW_PRESENT = 1u << 11, FW_TOMB = 1u << 12, FW_ORPHAN = 1u << 13;
 // slot words cover indices [0, FL_N]: slot FL_N ("none") stays 0 (absent, not
 // a tombstone), so lookups of "none" need no test and tombstone runs end there
 constexpr uint32_t FLANE_REGION = FL_N + 1;
 
-// slot j of lane m at j * D + m: each lane keeps to its own banks
-template <uint32_t D>
-struct LaneSlots {
-  uint16_t* base;
-  __device__ __forceinline__ uint32_t operator[](uint32_t j) const { return base[j * D]; }
-  __device__ __forceinline__ void set(uint32_t j, uint32_t w) const { base[j * D] = static_cast<uint16_t>(w); }
-};
+// One wave per document, every lane computing the same replay: the op word
+// comes from a register holding 64 op words (readlane) and every slot word is
+// read by all lanes at one address, so the data stays in vector registers
+// (the 4 SIMDs' ALUs) while each decision takes its condition to a scalar
+// register and branches on it -- no exec-mask bookkeeping around divergent
+// code on the CU's one scalar unit.
+__device__ __forceinline__ uint32_t wuni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
-template <uint32_t D>
-__global__ void __launch_bounds__(64) k_forest_lanes(const uint32_t* doc_off, uint32_t n_docs, long long ts0,
-                                                     const uint32_t* opw, const uint16_t* sent, const uint8_t* fb,
-                                                     longlong2* vt, int32_t* code_out, uint32_t* err_out,
-                                                     uint32_t* applied_out, unsigned long long* vhash,
-                                                     unsigned long long* vwords, long long* tstamp,
-                                                     uint32_t* overflow) {
-  extern __shared__ uint16_t slw[];  // [FLANE_REGION][D] slot words, then [64][D] op words
-  uint32_t* lops = reinterpret_cast<uint32_t*>(slw + FLANE_REGION * D);
+__global__ void __launch_bounds__(64) k_forest_wave(const uint32_t* doc_off, uint32_t n_docs, long long ts0,
+                                                    const uint32_t* opw, const uint16_t* sent, const uint8_t* fb,
+                                                    longlong2* vt, int32_t* code_out, uint32_t* err_out,
+                                                    uint32_t* applied_out, unsigned long long* vhash,
+                                                    unsigned long long* vwords, long long* tstamp, uint32_t* overflow) {
+  __shared__ uint16_t sl[FLANE_REGION];
+  const uint32_t d = blockIdx.x;
   const uint32_t lane = threadIdx.x;
-  for (uint32_t j = lane; j < FLANE_REGION * D / 8; j += 64) reinterpret_cast<uint4*>(slw)[j] = make_uint4(0, 0, 0, 0);
-  const uint32_t d0 = blockIdx.x * D;
-  uint32_t obm[D], nm[D], cmax = 0;
-#pragma unroll
-  for (uint32_t m = 0; m < D; ++m) {
-    const uint32_t dm = d0 + m;
-    obm[m] = nm[m] = 0;
-    if (dm < n_docs && !fb[dm]) {
-      obm[m] = doc_off[dm];
-      nm[m] = doc_off[dm + 1] - obm[m];
-    }
-    cmax = max(cmax, nm[m]);
-  }
-  const uint32_t d = d0 + lane;
-  const bool act = lane < D && d < n_docs && !fb[d];
-  const uint32_t nops = act ? doc_off[d + 1] - doc_off[d] : 0u;
-  const LaneSlots<D> sl{slw + (lane < D ? lane : 0u)};
+  if (d >= n_docs || fb[d]) return;
+  for (uint32_t j = lane; j < FLANE_REGION / 8; j += 64) reinterpret_cast<uint4*>(sl)[j] = make_uint4(0, 0, 0, 0);
+  const uint32_t ob = wuni(doc_off[d]), nops = wuni(doc_off[d + 1]) - ob;
+  const uint32_t s0 = wuni(sent[d]);
   __syncthreads();
-  const uint32_t s0 = act ? sent[d] : 0u;
-  if (act) sl.set(s0, FL_N | FW_PRESENT | FW_TOMB);
-  // (fresh documents start at counter 0 of their replica: no run of at most
-  // FL_MAXOPS own Adds crosses into the next replica id, so the OWN bit of each
-  // op is the reference's per-op comparison)
+  auto rd = [&](uint32_t j) { return static_cast<uint32_t>(sl[j]); };
+  auto wr = [&](uint32_t j, uint32_t w) { sl[j] = static_cast<uint16_t>(w); };
+  wr(s0, FL_N | FW_PRESENT | FW_TOMB);
   uint32_t own = 0, applied = 0, err = NONE;
   int32_t code = CRDTM_OK;
-  bool run = act;
-  for (uint32_t c0 = 0; c0 < cmax; c0 += 64) {
-#pragma unroll
-    for (uint32_t m = 0; m < D; ++m) lops[lane * D + m] = c0 + lane < nm[m] ? opw[obm[m] + c0 + lane] : 0u;
-    __syncthreads();
-    if (run) {
-      const uint32_t kend = min(64u, nops - min(nops, c0));
-      for (uint32_t k = 0; k < kend; ++k) {
-        const uint32_t w = lops[k * D + lane];
-        const uint32_t t = w & FL_N;
-        const uint32_t st = sl[t];
-        if (w & (FO_DEL | FO_INV)) {
-          if ((w & FO_INV) || !(st & FW_PRESENT)) {  // InvalidPath / deleteHelp NotFound (:112-122)
-            err = c0 + k;
-            code = (w & FO_INV) ? CRDTM_INVALID_PATH : CRDTM_OPERATION_FAILED;
-            run = false;
-            break;
-          }
-          if (!(st & FW_TOMB)) {
-            sl.set(t, st | FW_TOMB);
-            ++applied;
-          }
-          continue;
-        }
-        const uint32_t ownb = (w >> 24) & 1u;
-        if (st & FW_PRESENT) {  // `child ts parent` exists: AlreadyApplied
-          own += ownb;
-          continue;
-        }
-        const uint32_t a = (w >> 11) & FL_N;
-        const uint32_t sa = sl[a];
-        if (!(sa & FW_PRESENT)) {  // anchor missing: NotFound
+  uint32_t vw = lane < nops ? opw[ob + lane] : 0u;
+  for (uint32_t c0 = 0; c0 < nops; c0 += 64) {
+    const uint32_t nxt = c0 + 64 + lane < nops ? opw[ob + c0 + 64 + lane] : 0u;  // next 64 op words, in flight
+    const uint32_t kend = min(64u, nops - c0);
+    for (uint32_t k = 0; k < kend; ++k) {
+      const uint32_t w = __builtin_amdgcn_readlane(vw, k);
+      const uint32_t t = w & FL_N;
+      const uint32_t st = rd(t);
+      if (wuni(w & (FO_DEL | FO_INV))) {
+        if (wuni((w & FO_INV) | ((st & FW_PRESENT) ^ FW_PRESENT))) {  // InvalidPath / deleteHelp NotFound (:112-122)
           err = c0 + k;
-          code = CRDTM_OPERATION_FAILED;
-          run = false;
+          code = (w & FO_INV) ? CRDTM_INVALID_PATH : CRDTM_OPERATION_FAILED;
           break;
         }
-        const uint32_t x = t;
-        uint32_t nk = a, node = a, sn = sa;  // findInsertion (:93-104)
-        for (;;) {
-          const uint32_t rn = sn & FL_N;
-          uint32_t live = rn, wl = sl[rn];
-          while (wl & FW_TOMB) {  // nextNode: the first live node after next
-            live = wl & FL_N;
-            wl = sl[live];
-          }
-          if (live == FL_N || x > rn) break;
-          nk = rn;
-          node = live;
-          sn = wl;
+        if (!wuni(st & FW_TOMB)) {
+          wr(t, st | FW_TOMB);
+          ++applied;
         }
-        const uint32_t snk = nk == node ? sn : sl[nk];
-        sl.set(x, (sn & FL_N) | FW_PRESENT | (snk & FW_ORPHAN));
-        if (nk == node) {
-          sl.set(node, (sn & ~FL_N) | x);
-        } else {  // copy quirk: slot nk := copy of node with next = x
-          if (!(snk & FW_ORPHAN)) {
-            for (uint32_t q = snk & FL_N; q != FL_N;) {
-              const uint32_t sq = sl[q];
-              sl.set(q, sq | FW_ORPHAN);
-              if (q == node) break;
-              q = sq & FL_N;
-            }
+        continue;
+      }
+      const uint32_t ownb = (w >> 24) & 1u;
+      if (wuni(st & FW_PRESENT)) {  // `child ts parent` exists: AlreadyApplied
+        own += ownb;
+        continue;
+      }
+      const uint32_t a = (w >> 11) & FL_N;
+      const uint32_t sa = rd(a);
+      if (!wuni(sa & FW_PRESENT)) {  // anchor missing: NotFound
+        err = c0 + k;
+        code = CRDTM_OPERATION_FAILED;
+        break;
+      }
+      const uint32_t x = t;
+      uint32_t nk = a, node = a, sn = sa;  // findInsertion (:93-104)
+      for (;;) {
+        const uint32_t rn = sn & FL_N;
+        uint32_t live = rn, wl = rd(rn);
+        while (wuni(wl & FW_TOMB)) {  // nextNode: the first live node after next
+          live = wl & FL_N;
+          wl = rd(live);
+        }
+        if (wuni(live == FL_N || x > rn)) break;
+        nk = rn;
+        node = live;
+        sn = wl;
+      }
+      const bool same = wuni(nk == node);
+      const uint32_t snk = same ? sn : rd(nk);
+      wr(x, (sn & FL_N) | FW_PRESENT | (snk & FW_ORPHAN));
+      if (same) {
+        wr(node, (sn & ~FL_N) | x);
+      } else {  // copy quirk: slot nk := copy of node with next = x
+        if (!wuni(snk & FW_ORPHAN)) {
+          for (uint32_t q = snk & FL_N; wuni(q != FL_N);) {
+            const uint32_t sq = rd(q);
+            wr(q, sq | FW_ORPHAN);
+            if (wuni(q == node)) break;
+            q = sq & FL_N;
           }
-          sl.set(nk, x | FW_PRESENT | (snk & FW_ORPHAN));
+        }
+        wr(nk, x | FW_PRESENT | (snk & FW_ORPHAN));
+        if (lane == 0) {
           longlong2* v = vt + static_cast<uint64_t>(d) * FL_SLOTS;
           v[nk] = v[node];
         }
-        ++applied;
-        own += ownb;  // incrementTimestamp (src/CRDTree.elm:337-343)
       }
+      ++applied;
+      own += ownb;  // incrementTimestamp (src/CRDTree.elm:337-343)
     }
-    __syncthreads();
+    if (code != CRDTM_OK) break;
+    vw = nxt;
   }
-  if (!act) return;
-  code_out[d] = code;
-  err_out[d] = err;
-  applied_out[d] = applied;
-  tstamp[d] = ts0 + own;
-  overflow[d] = 0;
+  if (lane == 0) {
+    code_out[d] = code;
+    err_out[d] = err;
+    applied_out[d] = applied;
+    tstamp[d] = ts0 + own;
+    overflow[d] = 0;
+  }
   // the visible document's hash (the oracle's dumpVisible words), its
   // (value, timestamp) loads issued 8 entries ahead of the hash chain
   Fnv h;
   if (code == CRDTM_OK) {
+    __threadfence_block();  // the copy quirk's vt writes (lane 0) before every lane's reads
     const longlong2* v = vt + static_cast<uint64_t>(d) * FL_SLOTS;
-    uint32_t wc = sl[s0];
+    uint32_t wc = rd(s0);
     bool more = true;
     while (more) {
       uint32_t sv[8];
       uint32_t c = 0;
       for (; c < 8; ++c) {
-        uint32_t nx = wc & FL_N, wn = sl[nx];
-        while (wn & FW_TOMB) {
+        uint32_t nx = wc & FL_N, wn = rd(nx);
+        while (wuni(wn & FW_TOMB)) {
           nx = wn & FL_N;
-          wn = sl[nx];
+          wn = rd(nx);
         }
-        if (nx == FL_N) {
+        if (wuni(nx == FL_N)) {
           more = false;
           break;
         }
@@ -1734,14 +1788,16 @@ __global__ void __launch_bounds__(64) k_forest_lanes(const uint32_t* doc_off, ui
       }
     }
   }
-  vhash[d] = h.h;
-  vwords[d] = h.n;
+  if (lane == 0) {
+    vhash[d] = h.h;
+    vwords[d] = h.n;
+  }
 }
 
 __global__ void __launch_bounds__(64) k_forest(OpsDev o, ForestArgs f, const uint64_t* sbase, const uint64_t* dbase,
                                                const uint64_t* hbase, const uint8_t* fb) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= f.n_docs || !fb[d]) return;  // served by k_forest_prep / k_forest_lanes
+  if (d >= f.n_docs || !fb[d]) return;  // served by k_forest_prep / k_forest_wave
   {
     uint32_t* hs = f.hslot + hbase[d];  // this document's hash region starts empty
     for (uint32_t p = 0, H = forest_hash_cap(f.doc_off[d + 1] - f.doc_off[d]); p < H; ++p) hs[p] = NONE;
@@ -3799,12 +3855,12 @@ int forest_apply(crdtm_ctx* c, int64_t replica_id, const OpsDev& o, const uint32
   longlong2* vt = ws.alloc<longlong2>(n_docs * FL_SLOTS);
   LAUNCH(k_forest_prep, dim3(static_cast<uint32_t>(n_docs)), dim3(FPREP_THREADS), 0, s, o, doff, f.n_docs, f.ts0, opw,
          sent, fb, vt);
-  // one document per wave measured fastest (1, 2, 4, 8 per wave: 2.70, 2.95,
-  // 3.80, 5.70 ms on 12.5k config-5 documents): lanes of one wave diverge on
-  // every walk, and one document per wave gives the most waves to hide latency
-  constexpr uint32_t DPW = 1;
-  LAUNCH(k_forest_lanes<DPW>, dim3(static_cast<uint32_t>((n_docs + DPW - 1) / DPW)), dim3(64),
-         DPW * (FLANE_REGION * sizeof(uint16_t) + 64 * sizeof(uint32_t)), s, doff, f.n_docs, f.ts0, opw, sent, fb, vt,
+  // one wave per document, its replay's branches scalar and its data vector
+  // (measured on 12.5k config-5 documents: 2.36 ms; one lane per document with
+  // divergent vector control 2.65 ms at one document per wave and 2.95 / 3.80 /
+  // 5.70 ms at 2 / 4 / 8; the replay wholly scalar 2.79 ms; a flattened step
+  // machine at 4-16 documents per wave 6-8.6 ms)
+  LAUNCH(k_forest_wave, dim3(static_cast<uint32_t>(n_docs)), dim3(64), 0, s, doff, f.n_docs, f.ts0, opw, sent, fb, vt,
          f.code, f.err, f.applied, f.vhash, f.vwords, f.tstamp, f.overflow);
   LAUNCH(k_forest, dim3(static_cast<uint32_t>((n_docs + 63) / 64)), dim3(64), 0, s, o, f, dsb, ddb, dhb, fb);
   std::vector<uint32_t> e(n_docs), ov(n_docs);

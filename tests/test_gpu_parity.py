@@ -219,6 +219,78 @@ def test_forest_matches_oracle_per_document():
     assert (nw, hh) == (int(out["words"][d]), int(out["hash"][d]))
 
 
+def _forest_doc(seed, n_ops, fmap=None, edits=()):
+    """One flat synthetic document as rows (kind, ts, path, val); `fmap` remaps
+    every key (timestamps and path keys alike, 0 stays the sentinel)."""
+    s = N.synth(n_ops=n_ops, n_docs=1, replicas=8, window=16, p_delete=0.2, seed=seed)
+    f = (lambda k: k if k == 0 else fmap(k)) if fmap else (lambda k: k)
+    off = s["path_off"]
+    rows = [(int(s["kind"][i]), f(int(s["ts"][i])), [f(int(x)) for x in s["path"][off[i]:off[i + 1]]], int(s["val"][i]))
+            for i in range(len(s["kind"]))]
+    for at, row in sorted(edits, key=lambda e: -e[0]):
+        rows.insert(at, row)
+    return rows
+
+
+@pytest.mark.parametrize("layout", ["dense", "holes", "big_replica", "wide_range", "negative", "mixed"])
+def test_forest_slot_map_edges(layout):
+    """k_forest_prep's two slot maps (dense per-replica ranges; bitonic sort when
+    a key is negative, a replica id >= 64 or the ranges exceed 1,024 slots) and
+    the ops they must agree on -- duplicate keys, ts 0, anchors and deletes of
+    in-range keys no Add owns, empty paths -- against the oracle per document."""
+    import ctypes as C
+    from crdtm.tree import forest_apply
+    from oracle.oracle import lib as olib
+    R = lambda r, c: (r << 32) | c
+    maps = {"dense": None, "holes": lambda k: R(k >> 32, (k & 0xFFFFFFFF) * 3 + 7),
+            "big_replica": lambda k: k + (100 << 32), "wide_range": lambda k: k + (5000 if (k >> 32) == 3 else 0),
+            "negative": None, "mixed": None}
+    docs = []
+    for j in range(12):
+        fm = maps[layout]
+        if layout == "mixed":
+            fm = [None, maps["holes"], maps["big_replica"], maps["wide_range"]][j % 4]
+        base = _forest_doc(0xF0 + j, 300, fm)
+        add0 = [r for r in base if r[0] == 0]
+        k = j % 6
+        if k == 1:  # duplicate of an earlier Add, later in the stream
+            base.insert(250, add0[40])
+        elif k == 2:  # ts 0 Add (collides with the sentinel: AlreadyApplied)
+            base.insert(100, (0, 0, [0], 9))
+        elif k == 3 and layout in ("holes", "mixed"):  # anchor on a hole key (NotFound)
+            a = add0[10][1]
+            base.insert(200, (0, R(7, 999999), [a + 1], 9))
+        elif k == 4:  # empty path (InvalidPath)
+            base.insert(150, (0, R(7, 999998), [], 9))
+        elif k == 5:  # delete of a never-added in-range key
+            base.insert(120, (1, 0, [add0[5][1] + 1], 0))
+        if layout == "negative" and j % 2 == 0:
+            base.insert(50, (0, -5, [0], 3))
+        docs.append(base)
+    rows = [r for d in docs for r in d]
+    doc_off = np.zeros(len(docs) + 1, np.uint32)
+    doc_off[1:] = np.cumsum([len(d) for d in docs])
+    poff = np.zeros(len(rows) + 1, np.uint32)
+    poff[1:] = np.cumsum([len(r[2]) for r in rows])
+    s = dict(kind=np.array([r[0] for r in rows], np.uint8), ts=np.array([r[1] for r in rows], np.int64),
+             path_off=poff, path=np.array([x for r in rows for x in r[2]] + [0], np.int64),
+             val=np.array([r[3] for r in rows], np.uint32))
+    out = forest_apply(s, doc_off)
+    L = olib()
+    for d in range(len(docs)):
+        a, b = int(doc_off[d]), int(doc_off[d + 1])
+        sub = dict(kind=s["kind"][a:b].copy(), ts=s["ts"][a:b].copy(), val=s["val"][a:b].copy(),
+                   path_off=(poff[a:b + 1] - poff[a]).astype(np.uint32), path=s["path"][poff[a]:poff[b]].copy())
+        t, rc, err = oracle_apply_arrays(sub, b - a)
+        assert out["code"][d] == rc, f"document {d}"
+        if rc == 0:
+            h = C.c_uint64()
+            nw = L.orc_canonical(t, 1, None, 0, C.byref(h))
+            assert (int(out["words"][d]), int(out["hash"][d])) == (nw, h.value), f"document {d}"
+            assert int(out["timestamp"][d]) == L.orc_timestamp(t)
+        L.orc_free(t)
+
+
 def _flat_variant(s, edits):
     """Rebuild a flat stream (path length 1) with edits: ('ins', k, ts, anchor)
     inserts an Add at position k; ('empty', k) inserts an Add with path []."""
