@@ -454,9 +454,28 @@ __global__ void __launch_bounds__(BLOCK) k_len_scatter(OpsDev o, uint32_t maxlen
 // level-uniform predicates, so the op's own keys load before the parent
 // lookup resolves and the parent's keys load together.
 constexpr uint32_t LV_UNROLL = 14;
+constexpr uint32_t LV_PAIRS = (LV_UNROLL + 2) / 2;
+// k[l] = path[base + l] for l + 2 < j, as 16-byte loads from the even index
+// at or below base (half the load instructions and L2 line requests of
+// 8-byte loads; the path array is 16-byte aligned, checked by the caller)
+__device__ __forceinline__ void lv_keys(const long long* path, uint32_t base, uint32_t j, long long* k) {
+  const uint32_t sh = base & 1u;
+  const longlong2* p2 = reinterpret_cast<const longlong2*>(path + (base - sh));
+  long long e[2 * LV_PAIRS];
+#pragma unroll
+  for (uint32_t m = 0; m < LV_PAIRS; ++m) {
+    const longlong2 v = 2 * m < sh + j - 2 ? p2[m] : make_longlong2(0, 0);
+    e[2 * m] = v.x;
+    e[2 * m + 1] = v.y;
+  }
+#pragma unroll
+  for (uint32_t l = 0; l < LV_UNROLL; ++l) k[l] = l + 2 < j ? (sh ? e[l + 1] : e[l]) : 0;
+}
+
 __global__ void __launch_bounds__(BLOCK) k_lv_dict(OpsDev o, Work w, TsIndex h, const LvEnt* list, uint32_t cnt,
                                                    uint32_t j) {
   const uint32_t n = o.n;
+  const bool wide = (reinterpret_cast<uintptr_t>(o.path) & 15u) == 0 && j - 2 <= LV_UNROLL;
   GRID_STRIDE(q, cnt) {
     const uint2 ev = *reinterpret_cast<const uint2*>(&list[q]);
     const uint32_t i = ev.x, b = ev.y;
@@ -465,7 +484,9 @@ __global__ void __launch_bounds__(BLOCK) k_lv_dict(OpsDev o, Work w, TsIndex h, 
     if (j > 1) {
       const long long kp = o.path[b + j - 2];  // the parent's key
       long long own[LV_UNROLL];
-      if (j - 2 <= LV_UNROLL) {
+      if (wide) {
+        lv_keys(o.path, b, j, own);
+      } else if (j - 2 <= LV_UNROLL) {
 #pragma unroll
         for (uint32_t l = 0; l < LV_UNROLL; ++l) own[l] = l + 2 < j ? o.path[b + l] : 0;
       }
@@ -478,7 +499,12 @@ __global__ void __launch_bounds__(BLOCK) k_lv_dict(OpsDev o, Work w, TsIndex h, 
         dg = r.w;
         // independent loads (no early exit) so they issue together
         unsigned long long diff = 0;
-        if (j - 2 <= LV_UNROLL) {
+        if (wide) {
+          long long par[LV_UNROLL];
+          lv_keys(o.path, bg, j, par);
+#pragma unroll
+          for (uint32_t l = 0; l < LV_UNROLL; ++l) diff |= static_cast<unsigned long long>(par[l] ^ own[l]);
+        } else if (j - 2 <= LV_UNROLL) {
 #pragma unroll
           for (uint32_t l = 0; l < LV_UNROLL; ++l)
             if (l + 2 < j) diff |= static_cast<unsigned long long>(o.path[bg + l] ^ own[l]);
