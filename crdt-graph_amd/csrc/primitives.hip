@@ -590,8 +590,7 @@ template <bool PACKED>
 __global__ void __launch_bounds__(BLOCK) k_lr_walk(const uint2* __restrict__ ent, const uint32_t* __restrict__ succ,
                                                    const unsigned long long* __restrict__ w, uint64_t n,
                                                    uint32_t kbits, uint32_t head, uint64_t head_id, uint64_t nb,
-                                                   uint32_t* __restrict__ owner, unsigned long long* __restrict__ local,
-                                                   uint32_t* __restrict__ red_succ,
+                                                   uint4* __restrict__ ol, uint32_t* __restrict__ red_succ,
                                                    unsigned long long* __restrict__ red_w) {
   for (uint64_t id = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; id <= nb;
        id += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
@@ -617,8 +616,9 @@ __global__ void __launch_bounds__(BLOCK) k_lr_walk(const uint2* __restrict__ ent
         nxt = succ[cur];
         wc = w[cur];
       }
-      owner[cur] = static_cast<uint32_t>(id);
-      local[cur] = acc;
+      // owner and local prefix as one 16-byte record: one line per visited
+      // entry instead of one in each of two arrays
+      ol[cur] = make_uint4(static_cast<uint32_t>(id), static_cast<uint32_t>(acc), static_cast<uint32_t>(acc >> 32), 0u);
       acc += wc;
       if (nxt >= n || steps > n) { nxt = NONE; break; }  // end (cycle guard never taken on a valid list)
       if (nxt == lr_cand(nxt >> kbits, kbits)) break;      // next splitter
@@ -642,14 +642,22 @@ __global__ void k_lr_serial(const uint32_t* __restrict__ succ, const unsigned lo
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_lr_apply(uint64_t n, const uint32_t* __restrict__ owner,
-                                                    const unsigned long long* __restrict__ local,
-                                                    const unsigned long long* __restrict__ red_excl,
+// An entry marked ABSENT is on no list (~0); every other entry lies on the
+// one list from the head (an Euler tour of a tree; a reduced list of its
+// sublists), so its walk record was written.
+__global__ void __launch_bounds__(BLOCK) k_lr_apply(uint64_t n, const uint2* __restrict__ ent,
+                                                    const uint32_t* __restrict__ succ, const uint4* __restrict__ ol,
+                                                    uint64_t nb, const unsigned long long* __restrict__ red_excl,
                                                     unsigned long long* __restrict__ excl) {
   for (uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; e < n;
        e += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    const uint32_t o = owner[e];
-    excl[e] = (o == NONE) ? ~0ULL : red_excl[o] + local[e];
+    const uint32_t s = ent ? ent[e].x : succ[e];
+    if (s == ABSENT) {
+      excl[e] = ~0ULL;
+      continue;
+    }
+    const uint4 r = ol[e];
+    excl[e] = r.x <= nb ? red_excl[r.x] + (static_cast<unsigned long long>(r.z) << 32 | r.y) : ~0ULL;
   }
 }
 
@@ -658,18 +666,16 @@ static int list_rank_level(const uint2* ent, const uint32_t* succ, const unsigne
   const uint32_t kbits = level == 0 ? 4u : 3u;
   const uint64_t nb = (n + (1ULL << kbits) - 1) >> kbits;
   const uint64_t head_id = (lr_cand(head >> kbits, kbits) == head) ? (head >> kbits) : nb;
-  uint32_t* owner = ws.alloc<uint32_t>(n);
-  unsigned long long* local = ws.alloc<unsigned long long>(n);
+  uint4* ol = ws.alloc<uint4>(n);
   uint32_t* red_succ = ws.alloc<uint32_t>(nb + 1);
   unsigned long long* red_w = ws.alloc<unsigned long long>(nb + 1);
   unsigned long long* red_excl = ws.alloc<unsigned long long>(nb + 1);
-  HIP_CHECK(hipMemsetAsync(owner, 0xFF, n * sizeof(uint32_t), st));
   if (ent) {
     LAUNCH(k_lr_walk<true>, dim3(grid_for(nb + 1)), dim3(BLOCK), 0, st, ent, nullptr, nullptr, n, kbits, head,
-           head_id, nb, owner, local, red_succ, red_w);
+           head_id, nb, ol, red_succ, red_w);
   } else {
     LAUNCH(k_lr_walk<false>, dim3(grid_for(nb + 1)), dim3(BLOCK), 0, st, nullptr, succ, w, n, kbits, head, head_id,
-           nb, owner, local, red_succ, red_w);
+           nb, ol, red_succ, red_w);
   }
   if (nb + 1 <= LR_SERIAL || level >= 7) {
     LAUNCH(k_lr_serial, dim3(1), dim3(64), 0, st, red_succ, red_w, head_id, red_excl, nb + 1);
@@ -678,7 +684,7 @@ static int list_rank_level(const uint2* ent, const uint32_t* succ, const unsigne
                             level + 1);
     if (r) return r;
   }
-  LAUNCH(k_lr_apply, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, owner, local, red_excl, excl);
+  LAUNCH(k_lr_apply, dim3(grid_for(n)), dim3(BLOCK), 0, st, n, ent, succ, ol, nb, red_excl, excl);
   return CRDTM_OK;
 }
 
