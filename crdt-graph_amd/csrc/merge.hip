@@ -1036,6 +1036,20 @@ __device__ __forceinline__ long long op_t(const OpsDev& o, uint32_t i) {
 // output pass visits the touched replicas only.
 // ops per thread: 16 on large batches (fewer table flushes), 4 on small ones (more workgroups in flight)
 inline uint32_t rep_per(uint32_t n) { return n >= (1u << 22) ? 16u : 4u; }
+constexpr uint32_t REP_ROUNDS = 4;
+// replica rl (offset id) saw op v - 1: the LDS table for small ids, else the
+// global table (its first publisher appends it to the touched list)
+__device__ __forceinline__ void rep_publish(uint32_t* rv, uint32_t* rtab, uint32_t* rlist, uint32_t* rcount,
+                                            uint32_t rl, uint32_t v, uint32_t& mr) {
+  constexpr uint32_t OFF = 1u << (REPLICA_BITS - 1);
+  const uint32_t d = rl - OFF;  // (ids below 0 wrap high: global table)
+  if (d < REP_DIRECT) {
+    atomicMax(&rv[d], v);
+    mr = max(mr, d);
+  } else if (atomicMax(&rtab[rl], v) == 0) {
+    rlist[atomicAdd(rcount, 1u)] = rl;
+  }
+}
 __global__ void __launch_bounds__(BLOCK) k_rep_max(OpsDev o, const uint8_t* st, uint32_t* rtab, uint32_t* rlist,
                                                    uint32_t* rcount, uint32_t per) {
   __shared__ uint32_t rv[REP_DIRECT];
@@ -1061,20 +1075,17 @@ __global__ void __launch_bounds__(BLOCK) k_rep_max(OpsDev o, const uint8_t* st, 
     for (uint32_t u = 0; u < 4; ++u) {
       const uint32_t r = static_cast<uint32_t>(replica_of(t[u]) + OFF);
       bool pend = ok[u];
-      for (unsigned long long m = __ballot(pend); m; m = __ballot(pend)) {
+      // up to REP_ROUNDS replicas per wave reduce first (one atomic each); a
+      // wave holding more (many replicas interleaved) sends the rest to the
+      // table lane by lane -- different words, so those atomics run in parallel
+      uint32_t round = 0;
+      for (unsigned long long m = __ballot(pend); m && round < REP_ROUNDS; m = __ballot(pend), ++round) {
         const uint32_t rl = __builtin_amdgcn_readlane(r, static_cast<uint32_t>(__builtin_ctzll(m)));
         const unsigned long long mm = __ballot(pend && r == rl);
-        if (lane == 63u - static_cast<uint32_t>(__builtin_clzll(mm))) {
-          const uint32_t d = rl - OFF;  // (ids below 0 wrap high: global table)
-          if (d < REP_DIRECT) {
-            atomicMax(&rv[d], ii[u] + 1);
-            mr = max(mr, d);
-          } else if (atomicMax(&rtab[rl], ii[u] + 1) == 0) {
-            rlist[atomicAdd(rcount, 1u)] = rl;
-          }
-        }
+        if (lane == 63u - static_cast<uint32_t>(__builtin_clzll(mm))) rep_publish(rv, rtab, rlist, rcount, rl, ii[u] + 1, mr);
         if (r == rl) pend = false;
       }
+      if (pend) rep_publish(rv, rtab, rlist, rcount, r, ii[u] + 1, mr);
     }
   }
   mr = block_max(mr);  // (synchronises the block) only ids <= mr were touched
