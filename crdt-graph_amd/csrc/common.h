@@ -16,6 +16,7 @@ namespace crdtm {
 constexpr uint32_t NONE = 0xFFFFFFFFu;     // absent index / list end
 constexpr uint32_t ABSENT = 0xFFFFFFFEu;   // entry not part of a list
 constexpr uint32_t PDR_REACHED = 0xFFFFFFFDu;  // K1 tag: the op's path resolved to its leaf dict
+constexpr uint32_t TAG_DUP = 0xFFFFFFFAu;      // K1 tag, k_lv_leaf -> k_lv_fin only: an Add whose key is taken (ts 0 or an earlier Add)
 constexpr uint32_t TAG_LAZY = 0xFFFFFFFBu;     // K1 tag: stopped at a Tombstone of the chain ending at cur
 constexpr uint32_t SENT_T = 0xFFFFFFFDu;       // K1 leaf target: the dict's sentinel (key 0)
 constexpr uint32_t MISS_T = 0xFFFFFFFCu;       // K1 leaf target: key not in the dict

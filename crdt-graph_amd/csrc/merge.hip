@@ -576,7 +576,10 @@ __global__ void __launch_bounds__(BLOCK) k_lv_leaf(OpsDev o, Work w, TsIndex h, 
         if (f != i) {
           const uint4 r = w.nrec[f];
           if (nrec_len(r) != j || r.z != cur) atomicOr(&dres->guard, G_COLLISION);
+          w.tag[i] = TAG_DUP;
         }
+      } else {
+        w.tag[i] = TAG_DUP;
       }
     } else if (tgt == SENT_T) {
       w.st[i] = ST_ALREADY;
@@ -596,15 +599,14 @@ __global__ void __launch_bounds__(BLOCK) k_lv_fin(OpsDev o, Work w, TsIndex h, c
   GRID_STRIDE(q, cnt) {
     const uint32_t i = list[q].i;
     if (w.st[i] != ST_PENDING) continue;
+    const uint32_t tg = w.tag[i];
     w.tag[i] = PDR_REACHED;
     if (o.kind[i] == CRDTM_DELETE) {
       w.st[i] = (w.dtime[w.leaf[i]] == i) ? ST_APPLIED : ST_ALREADY;
       continue;
     }
-    const long long ts = o.ts[i];
     uint8_t s;
-    if (ts == 0) s = ST_ALREADY;                         // key 0 = the sentinel
-    else if (tsindex_find(h, ts) != i) s = ST_ALREADY;    // child ts parent exists
+    if (tg == TAG_DUP) s = ST_ALREADY;  // key 0 = the sentinel, or `child ts parent` exists (k_lv_leaf)
     else {
       const uint32_t a = w.leaf[i];
       s = (a == SENT_T || (a != MISS_T && a < i)) ? ST_APPLIED : ST_NOTFOUND;
