@@ -788,29 +788,40 @@ __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* total) 
 }
 
 // sort key: group 0 before group 1, then descending ts (|ts| < 2^53)
+// (also clears k_scatter's cursors and k_links' outputs, in the same pass)
 __global__ void __launch_bounds__(BLOCK) k_up_count(OpsDev o, Work w, const uint32_t* anc, const uint8_t* sp,
-                                                    uint32_t* cnt, long long* skey) {
+                                                    uint32_t* cnt, long long* skey, uint32_t* thot, uint32_t* fill,
+                                                    uint32_t* fc, uint32_t* ns, uint32_t* f1) {
   const uint32_t n = o.n, U = n + 1, H = n;  // super root excluded (no parent)
   uint32_t hot = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the super root's entries (uid n + 1)
+    fill[U] = fill[U + 1] = 0;
+    fc[U] = ns[U] = f1[U] = NONE;
+  }
   GRID_STRIDE(v, U) {
+    fill[v] = 0;
+    fc[v] = NONE;
+    ns[v] = NONE;
+    f1[v] = NONE;
     if (!doc_present(o, w, sp, v)) continue;
     const uint32_t u = doc_up(o, anc, v);
     if (u == H) ++hot;
     else atomicAdd(&cnt[u], 1u);
     skey[v] = v < n ? (doc_group1(o, anc, v) ? (1LL << 60) : 0LL) + (TWO53 - o.ts[v]) : 0LL;
   }
+  thot[blockIdx.x * blockDim.x + threadIdx.x] = hot;  // k_scatter's per-thread share (same grid)
   hot = block_sum(hot);
   if (threadIdx.x == 0 && hot) atomicAdd(&cnt[H], hot);
 }
 
+// (launched on k_up_count's grid: thread t's children of the root sentinel
+// were counted there, in the same order)
 __global__ void __launch_bounds__(BLOCK) k_scatter(OpsDev o, Work w, const uint32_t* anc, const uint8_t* sp,
-                                                   const uint32_t* start, uint32_t* fill, uint32_t* carr) {
+                                                   const uint32_t* start, uint32_t* fill, uint32_t* carr,
+                                                   const uint32_t* thot) {
   __shared__ uint32_t blk_base;
   const uint32_t n = o.n, U = n + 1, H = n;
-  uint32_t hot = 0;
-  GRID_STRIDE(v, U) {
-    if (doc_present(o, w, sp, v) && doc_up(o, anc, v) == H) ++hot;
-  }
+  const uint32_t hot = thot[blockIdx.x * blockDim.x + threadIdx.x];
   uint32_t tot;
   uint32_t mine = block_excl_sum(hot, &tot);
   if (threadIdx.x == 0) blk_base = tot ? atomicAdd(&fill[H], tot) : 0u;
@@ -3545,17 +3556,15 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   uint32_t* f1 = ws.alloc<uint32_t>(U);
   HIP_CHECK(hipMemsetAsync(sp, 0, n + 1, s));
   HIP_CHECK(hipMemsetAsync(cnt, 0, (U + 1) * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(fill, 0, (U + 1) * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(fc, 0xFF, U * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(ns, 0xFF, U * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(f1, 0xFF, U * sizeof(uint32_t), s));
   if (!flat) LAUNCH(k_ep_init, dim3(g), dim3(BLOCK), 0, s, o, w, anc);
   LAUNCH(k_ep_jump, dim3(g), dim3(BLOCK), 0, s, o, w, anc, sp);
   const uint32_t gU = grid_for(U);
-  LAUNCH(k_up_count, dim3(grid_for(U, BLOCK, 2048)), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, skey);
+  const uint32_t gUc = grid_for(U, BLOCK, 2048);  // k_up_count and k_scatter share it
+  uint32_t* thot = ws.alloc<uint32_t>(static_cast<uint64_t>(gUc) * BLOCK);
+  LAUNCH(k_up_count, dim3(gUc), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, skey, thot, fill, fc, ns, f1);
   uint32_t* n_child_total = &dr->n_sentinels;  // scratch word for the scan total
   if ((r = scan_excl_u32(cnt, cnt, U + 1, n_child_total, ws, s))) return r;
-  LAUNCH(k_scatter, dim3(grid_for(U, BLOCK, 2048)), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, fill, carr);
+  LAUNCH(k_scatter, dim3(gUc), dim3(BLOCK), 0, s, o, w, anc, sp, cnt, fill, carr, thot);
   if ((r = segmented_sort(cnt, U, carr, U, skey, ws, s, dr))) return r;
   LAUNCH(k_links, dim3(gU), dim3(BLOCK), 0, s, o, anc, cnt, n_child_total, carr, fc, ns, f1);
 
