@@ -3531,18 +3531,6 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
     if ((r = grow_tree(t, need))) return r;
   }
   long long* rep = ws.alloc<long long>(2 * static_cast<uint64_t>(n) + 2);
-  HIP_CHECK(hipEventRecord(c->ev_fork, s));
-  HIP_CHECK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-  // (full grids: a small background grid starves k_log's chunk loop)
-  LAUNCH(k_log, dim3(g), dim3(BLOCK), 0, c->side, o, w.st, t->d, static_cast<uint32_t>(t->log_n),
-         static_cast<uint32_t>(t->log_npath), appl, plen);
-  LAUNCH(k_log_tail, dim3(1), dim3(1), 0, c->side, t->d, static_cast<uint32_t>(t->log_n), &dr->log_n,
-         static_cast<uint32_t>(t->log_npath), &dr->log_npath);
-  HIP_CHECK(hipEventRecord(c->ev_join, c->side));
-  struct Join {  // every exit waits for the side stream (the arena is reused by the next call)
-    crdtm_ctx* c;
-    ~Join() { hipStreamWaitEvent(c->stream, c->ev_join, 0); }
-  } join{c};
 
   // ---- K2: effective parents, document tree, sibling sort ----
   const uint32_t U = n + 2;
@@ -3557,6 +3545,20 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   HIP_CHECK(hipMemsetAsync(sp, 0, n + 1, s));
   HIP_CHECK(hipMemsetAsync(cnt, 0, (U + 1) * sizeof(uint32_t), s));
   if (!flat) LAUNCH(k_ep_init, dim3(g), dim3(BLOCK), 0, s, o, w, anc);
+  HIP_CHECK(hipEventRecord(c->ev_fork, s));
+  HIP_CHECK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+  // (forked after k_ep_init, so the log copy overlaps the latency-bound
+  // pointer jumping instead of the streaming passes; full grids: a small
+  // background grid starves k_log's chunk loop)
+  LAUNCH(k_log, dim3(g), dim3(BLOCK), 0, c->side, o, w.st, t->d, static_cast<uint32_t>(t->log_n),
+         static_cast<uint32_t>(t->log_npath), appl, plen);
+  LAUNCH(k_log_tail, dim3(1), dim3(1), 0, c->side, t->d, static_cast<uint32_t>(t->log_n), &dr->log_n,
+         static_cast<uint32_t>(t->log_npath), &dr->log_npath);
+  HIP_CHECK(hipEventRecord(c->ev_join, c->side));
+  struct Join {  // every exit waits for the side stream (the arena is reused by the next call)
+    crdtm_ctx* c;
+    ~Join() { hipStreamWaitEvent(c->stream, c->ev_join, 0); }
+  } join{c};
   LAUNCH(k_ep_jump, dim3(g), dim3(BLOCK), 0, s, o, w, anc, sp);
   const uint32_t gU = grid_for(U);
   const uint32_t gUc = grid_for(U, BLOCK, 2048);  // k_up_count and k_scatter share it
