@@ -8,11 +8,14 @@ C ABI), inputs already resident in HBM.
 
 Default workload = SURVEY.md config 3: one flat RGA text document, 10M char
 inserts from 64 replicas (window 256, seed 0xC0FFEE03). With N ranks (one
-process per GPU, torchrun), every rank merges its own independent document
+process per GPU: an external torchrun, or bench.py starts the N ranks itself
+when launched without one), every rank merges its own independent document
 (seed + rank): documents shard by id with no data-path collective, so the
-scaling is weak; the only collectives are the timing barrier and max.
+scaling is weak; the only collectives are the timing barrier and max. With
+N > 1 the config-5 line (RCCL all-gather of op logs + sharded merge) rides
+along under "exchange".
 
-    python bench.py --gpus N --steps K --warmup W [--workload flat10m|deep10m]
+    python bench.py --gpus N --steps K --warmup W [--workload flat10m|deep10m|deep10m_il|cfg2|trees|incr]
 """
 import argparse
 import ctypes as C
@@ -35,6 +38,11 @@ WORKLOADS = {
     # depth <= 12, <= 8 children, 6.67M adds then deletes of half the nodes
     "deep10m": dict(n_ops=10_000_000, replicas=16, p_delete=1 / 3, max_depth=12, max_children=8, deletes_last=1,
                     seed=0xC0FFEE04),
+    # config 4's second variant: the same deep tree shape with its Deletes interleaved
+    # among the Adds (live leaves; synth.cpp genDeep), so dicts hold tombstones before later inserts:
+    # measures the exact per-dict replay
+    "deep10m_il": dict(n_ops=10_000_000, replicas=16, p_delete=1 / 3, max_depth=12, max_children=8, deletes_last=0,
+                       seed=0xC0FFEE04),
     # one tree, 1M ops (80/20 interleaved), 16 replicas, branches, depth <= 4
     # (Deletes interleaved before later inserts: the exact sequential replay)
     "cfg2": dict(n_ops=1_000_000, replicas=16, window=64, p_delete=0.2, p_branch=0.1, max_depth=4,
@@ -42,7 +50,7 @@ WORKLOADS = {
     # SURVEY.md §8d config 1 shape: 2 replicas, 10k ops, 70/30 interleaved, depth <= 3
     "cfg1": dict(n_ops=10_000, replicas=2, window=8, p_delete=0.3, p_branch=0.05, max_depth=3, seed=0xC0FFEE01),
 }
-CPU_SAMPLE = {"flat10m": 100_000, "deep10m": 500_000, "trees": 2_000_000, "cfg2": 100_000, "cfg1": 10_000}
+CPU_SAMPLE = {"flat10m": 100_000, "deep10m": 500_000, "deep10m_il": 500_000, "trees": 2_000_000, "cfg2": 100_000, "cfg1": 10_000}
 # 100k documents x 1k ops (80/20), 8 replicas, sharded by
 # document id; 12.5k documents per GPU (100k at 8 GPUs), weak scaling.
 # Incremental merges: a 10M-node document, then successive 10k-op batches of the same stream
@@ -198,6 +206,74 @@ def cpu_line(cb, what):
     return d
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N ranks of this same
+    command line under torch.distributed.run (one process per GPU, rendezvous
+    on 127.0.0.1) as a child process and return its exit code. Runs before
+    this process touches the GPU (no exec from a GPU-initialised process)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, rank, world):
+    """--dry-run: the multi-rank plumbing of a real run on the CPU (gloo): the
+    ranks the launcher started, the timing barrier and max over ranks, and the
+    config-5 exchange (shard.Exchange all-gather of the simulated replicas' op
+    logs, then each rank's assembly of the documents it owns). No merge runs,
+    so no throughput is claimed (`value` null)."""
+    import torch
+    import torch.distributed as dist
+    from crdtm import _native as N
+    from crdtm import shard
+    if world > 1:
+        dist.init_process_group("gloo")
+    per, dpg = 100, 8
+    n_docs = dpg * world
+    s = N.synth(n_ops=per, n_docs=n_docs, replicas=TREES["replicas"], window=TREES["window"],
+                p_delete=TREES["p_delete"], seed=TREES["seed"])
+    doc_off = np.arange(n_docs + 1, dtype=np.uint32) * per
+    ex = shard.Exchange(torch.from_numpy(shard.local_log(s, doc_off, rank, world, TREES["replicas"])))
+    kept = 0
+    for _ in range(args.warmup):
+        ex.gather()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        _, my_off, keep = shard.assemble(ex.gather(), rank, world, n_docs, per)
+        kept = int(keep.sum())
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    n_mine = (n_docs - rank + world - 1) // world
+    ok = kept == n_mine * per and int(my_off[-1]) == kept
+    t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        line = {"metric": "merged ops/sec (whole node) on 10M-op batch", "value": None, "unit": "ops/s",
+                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": float(t[0]) / max(1, args.steps) * 1e3, "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "int64", "data": "synthetic", "dry_run": True,
+                "config": {"workload": "dry run (launcher and exchange plumbing, no merge)",
+                           "parallelism": f"documents sharded by id over {world} rank(s) (gloo)"},
+                "exchange": {"documents": n_docs, "records_per_rank_block": int(getattr(ex, "block", kept)),
+                             "assembled_ok": bool(t[1] == 0)}}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if t[1] != 0:
+        sys.exit(1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -215,15 +291,26 @@ def main():
     ap.add_argument("--force-replay", action="store_true",
                     help="every merge takes the one-lane sequential replay (env CRDTM_FORCE_REPLAY=1): "
                          "measures the fallback cliff on the same batch")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher plumbing only, no GPU: ranks (gloo), timing barrier, max over ranks and the "
+                         "config-5 op-log exchange + assembly run; no merge is timed and `value` is null")
     args = ap.parse_args()
     if args.force_replay:
         os.environ["CRDTM_FORCE_REPLAY"] = "1"  # (read by every merge)
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # self-launch: one child rank per GPU (before anything touches the GPU)
+        sys.exit(launch_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but {world} rank(s) were launched", file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
+    if args.dry_run:
+        return dry_run(args, rank, world)
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))

@@ -395,21 +395,6 @@ class CRDTree:
             i += 3 + pl
         return out
 
-    def get_value(self, path):
-        """CRDTree.getValue (src/CRDTree.elm:486-488) over the canonical structure."""
-        words, n, _ = self.canonical(0)
-        want = [int(x) for x in path]
-        i = 0
-        stack = []
-        while i < n:
-            d, k, kind, hn, nx, v, pl = (int(x) for x in words[i:i + 7])
-            del stack[d:]
-            stack.append(k)
-            if stack == want:
-                return VALUES.value(v) if kind == 1 else None
-            i += 7 + pl
-        return None
-
 
 def init(replica_id_: int, device: int = 0) -> CRDTree:
     return CRDTree.init(replica_id_, device)

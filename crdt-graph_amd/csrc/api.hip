@@ -426,6 +426,21 @@ int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_b
     // lastOperation: the op itself, or Batch of the applied ops; an
     // AlreadyApplied single op leaves Batch [] (src/CRDTree.elm:318-319)
     t->last_is_batch = (is_batch || res->n_applied == 0) ? 1 : 0;
+    // Every path leaves the document order (north-star kernel 4) current:
+    // the closed forms compute it as they merge; the replays' states are
+    // linearised here, inside the call (and inside a timed bench step).
+    if (!t->doc_valid && n) {
+      r = ensure_arena(c, arena_need(0, 0, t) + 64 * (t->n_slots + t->n_dicts));
+      if (r) return r;
+      g_prof = c->profile ? c : nullptr;
+      try {
+        r = linearize(t);
+      } catch (const ArenaOverflow&) {
+        r = CRDTM_E_NOMEM;
+      }
+      g_prof = nullptr;
+      if (r) return r;
+    }
   }
   res->timestamp = t->timestamp;
   res->n_slots = t->n_slots;

@@ -185,7 +185,51 @@ void genDeep(const crdtm_synth_params& p, uint64_t seed, uint32_t doc, Out& o) {
   std::vector<uint32_t> counter(R + 1, 1);
   std::vector<int64_t> tmp;
   auto nchild = [&](int32_t pn) -> uint16_t { return pn == 0 ? rootKidsN[0] : nodes[pn - 1].nchild; };
-  for (uint64_t s = 0; s < nAdd; ++s) {
+  // Interleaved variant (deletes_last = 0, SURVEY.md 8d config 4's second
+  // stream): each step is a Delete with probability (deletes left) / (ops
+  // left), so the batch holds exactly nAdd Adds and nDel Deletes, spread
+  // uniformly. A Delete targets a uniformly chosen live leaf (like a replica
+  // deleting a visible node without children, the typing model's rule), which
+  // then stops being a parent candidate: every op of the stream applies, and
+  // later Adds keep landing in dicts that already hold tombstones — with
+  // anchors that may be those deleted siblings (findInsertion's tombstone skip
+  // and copy quirk, src/Internal/Node.elm:93-104).
+  const bool inter = !p.deletes_last && nDel > 0;
+  std::vector<int32_t> leaves;    // live nodes without children
+  std::vector<uint32_t> leafPos;  // node -> position in `leaves`, UINT32_MAX = not a leaf
+  std::vector<uint8_t> inElig;    // node + 1 -> listed in `eligible`
+  if (inter) {
+    leaves.reserve(nAdd);
+    leafPos.assign(nAdd, UINT32_MAX);
+    inElig.assign(nAdd + 1, 0);
+    inElig[0] = 1;
+  }
+  auto dropLeaf = [&](int32_t v) {
+    const uint32_t pos = leafPos[v];
+    leaves[pos] = leaves.back();
+    leafPos[leaves[pos]] = pos;
+    leaves.pop_back();
+    leafPos[v] = UINT32_MAX;
+  };
+  uint64_t delLeft = inter ? nDel : 0;
+  for (uint64_t s = 0, addsDone = 0; addsDone < nAdd; ++s) {
+    if (inter && delLeft > 0 && !leaves.empty() && rng.below(delLeft + (nAdd - addsDone)) < delLeft) {
+      const int32_t v = leaves[rng.below(leaves.size())];
+      emitDel(o, nodes, v, doc, tmp);
+      dropLeaf(v);
+      const int32_t x = v + 1;
+      if (inElig[x]) {  // no longer a parent candidate
+        const uint32_t pos = eligPos[x];
+        eligible[pos] = eligible.back();
+        eligPos[eligible[pos]] = pos;
+        eligible.pop_back();
+        inElig[x] = 0;
+      }
+      --delLeft;
+      continue;
+    }
+    ++addsDone;
+    if (eligible.empty()) break;
     const uint64_t ei = rng.below(eligible.size());
     const int32_t pn = eligible[ei];  // parent node + 1
     const uint16_t k = nchild(pn);
@@ -210,12 +254,20 @@ void genDeep(const crdtm_synth_params& p, uint64_t seed, uint32_t doc, Out& o) {
       eligible[pos] = eligible.back();
       eligPos[eligible[pos]] = pos;
       eligible.pop_back();
+      if (inter) inElig[pn] = 0;
     }
     if (g.depth < p.max_depth) {
       eligPos[x] = static_cast<uint32_t>(eligible.size());
       eligible.push_back(x);
+      if (inter) inElig[x] = 1;
+    }
+    if (inter) {
+      if (pn > 0 && leafPos[pn - 1] != UINT32_MAX) dropLeaf(pn - 1);
+      leafPos[x - 1] = static_cast<uint32_t>(leaves.size());
+      leaves.push_back(x - 1);
     }
   }
+  if (inter) return;
   std::vector<uint32_t> idx(nodes.size());
   for (size_t i = 0; i < idx.size(); ++i) idx[i] = static_cast<uint32_t>(i);
   for (uint64_t k = 0; k < nDel && k < idx.size(); ++k) {

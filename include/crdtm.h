@@ -146,9 +146,13 @@ int crdtm_tree_ops(const crdtm_tree *t, int which, crdtm_ops *out, int *is_batch
 int crdtm_tree_ops_since(const crdtm_tree *t, int64_t ts, crdtm_ops *out);
 
 /* ---- traversal (CRDTree.get/parent/next/prev/walk, src/CRDTree.elm:421-625;
- *      CRDTree.Node.children/head, src/CRDTree/Node.elm:96-174). Host-side
- *      reads of the device state (copied once per tree version). A node
- *      reference is valid until the next apply/reset of the tree. */
+ *      CRDTree.Node.children/head, src/CRDTree/Node.elm:96-174). get,
+ *      node_info, relative and node_children run on the device (one small
+ *      kernel per query over the state's own arrays and a (dict, key) -> slot
+ *      index built once per tree version); only the answer is copied back.
+ *      walk, whose output is document-sized, reads a host copy of the state
+ *      taken once per version. A node reference is valid until the next
+ *      apply/reset of the tree. */
 #define CRDTM_REF_NONE UINT64_MAX                 /* Nothing */
 #define CRDTM_REF_ROOT (UINT64_MAX - 1)           /* the Root node */
 #define CRDTM_REF_VSENT (1ULL << 62)              /* | slot: sentinel of a live node's empty children */
