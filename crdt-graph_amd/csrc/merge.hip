@@ -122,8 +122,10 @@ inline uint32_t quad_grid(uint64_t n) {
 // ---------------------------------------------------------------------------
 
 // Batch pre-pass: per-replica counter ranges of the Add timestamps (dense
-// index layout), longest path, |x| < 2^53 range checks over ts and path
-// elements, negative timestamps, Delete count and the largest replica id.
+// index layout), longest path, |x| < 2^53 range checks over ts, negative
+// timestamps, Delete count and the largest replica id. The path elements'
+// range check rides on the flat claim (k_fl_claim reads them anyway) and is a
+// pass of its own (k_path_range) on the other paths.
 // Replica ids below REP_DIRECT fold into a direct-mapped LDS table with
 // no-return LDS atomics; larger ids go straight to the global table.
 constexpr uint32_t REP_DIRECT = 4096;
@@ -185,28 +187,6 @@ __global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint2* rng, DevResult* 
       fold(qa);
     }
   }
-  // path elements: 16-byte loads over an even-aligned range
-  const uint64_t np = o.n_path, npair = np / 2;
-  auto out = [](long long v) { return v >= TWO53 || v <= -TWO53; };
-  {
-    const uint64_t ps = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-    uint64_t p = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-    for (; p + 3 * ps < npair; p += 4 * ps) {
-      longlong2 v[4];
-#pragma unroll
-      for (uint32_t u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const longlong2*>(o.path + 2 * (p + u * ps));
-#pragma unroll
-      for (uint32_t u = 0; u < 4; ++u)
-        if (out(v[u].x) || out(v[u].y)) bad = 1;
-    }
-    for (; p < npair; p += ps) {
-      const longlong2 v = *reinterpret_cast<const longlong2*>(o.path + 2 * p);
-      if (out(v.x) || out(v.y)) bad = 1;
-    }
-  }
-  if ((np & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-    if (out(o.path[np - 1])) bad = 1;
-  }
   maxr = block_max(maxr);  // (synchronises the block) only ids <= maxr were touched
   for (uint32_t j = threadIdx.x; j <= maxr && j < REP_DIRECT; j += blockDim.x) {
     if (rlo[j] != NONE) {
@@ -225,6 +205,30 @@ __global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint2* rng, DevResult* 
     if (ndel) atomicAdd(&dres->n_del, ndel);
     if (maxr) atomicMax(&dres->max_replica, maxr);
   }
+}
+
+// |x| < 2^53 over every path element (16-byte loads over an even-aligned range)
+__global__ void __launch_bounds__(BLOCK) k_path_range(OpsDev o, DevResult* dres) {
+  const uint64_t np = o.n_path, npair = np / 2;
+  auto out = [](long long v) { return v >= TWO53 || v <= -TWO53; };
+  uint32_t bad = 0;
+  const uint64_t ps = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  uint64_t p = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+  for (; p + 3 * ps < npair; p += 4 * ps) {
+    longlong2 v[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const longlong2*>(o.path + 2 * (p + u * ps));
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u)
+      if (out(v[u].x) || out(v[u].y)) bad = 1;
+  }
+  for (; p < npair; p += ps) {
+    const longlong2 v = *reinterpret_cast<const longlong2*>(o.path + 2 * p);
+    if (out(v.x) || out(v.y)) bad = 1;
+  }
+  if ((np & 1) && blockIdx.x == 0 && threadIdx.x == 0 && out(o.path[np - 1])) bad = 1;
+  bad = block_max(bad);
+  if (threadIdx.x == 0 && bad) atomicOr(&dres->bad_range, 1u);
 }
 
 // Per-op state of the level-synchronous (nested / hash-indexed) path.
@@ -2000,13 +2004,15 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
     return sbase[r] + (c - lo);
   };
   const long long id0 = replica_of(ts0);
-  uint32_t keys = 0, own = 0, slow = 0, err = NONE, mr = 0;
+  uint32_t keys = 0, own = 0, slow = 0, err = NONE, mr = 0, bad = 0;
   QUAD_LOOP_XCD(i0, o.n) {
     Quad qd;
     load_quad(o, i0, qd);
     long long pk[4];  // the path element of each op (flat: |path| <= 1)
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) pk[k] = (k < qd.cnt && qd.off[k + 1] != qd.off[k]) ? o.path[qd.off[k]] : 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) bad |= (pk[k] >= TWO53 || pk[k] <= -TWO53) ? 1u : 0u;  // (|x| < 2^53)
     if (log_to_tree) {
       if (qd.cnt == 4) {
         *reinterpret_cast<uchar4*>(T.l_kind + i0) = make_uchar4(qd.kind[0], qd.kind[1], qd.kind[2], qd.kind[3]);
@@ -2069,7 +2075,9 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
   own = block_sum(own);
   slow = block_sum(slow);
   err = block_min(err);
+  bad = block_max(bad);
   if (threadIdx.x == 0) {  // 16 shards a line apart: ~12 ns per atomic on one word
+    if (bad) atomicOr(&dres->bad_range, 1u);
     uint32_t* sh = dres->fl_part + 32 * (blockIdx.x & 15);
     if (keys) atomicAdd(&sh[1], keys);
     if (own) atomicAdd(&sh[2], own);
@@ -3092,10 +3100,12 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     // ---- K2a: effective parents (run-skipping walk over the anchor runs) ----
     const uint32_t gq = grid_for(Q);
     uint32_t* rh = ws.alloc<uint32_t>(Q);
-    if ((r = dscan<MaxOp, true>(RunHeadGen{rec, Q, anc}, rh, Q, nullptr, ws, s, nullptr))) return r;
+    if ((r = dscan<MaxOp, true>(RunHeadGen{rec, Q, anc}, rh, Q, nullptr, ws, s, nullptr, nullptr,
+                                "k_dscan_runhead")))
+      return r;
     uint32_t* rid = ws.alloc<uint32_t>(Q);  // ep-run head flags, then inclusive head counts
     LAUNCH(k_fl_ep_runs, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, rh, rid);
-    if ((r = dscan<SumOp, true>(ArrGen{rid}, rid, Q, &dr->run_count, ws, s, nullptr))) return r;
+    if ((r = dscan<SumOp, true>(ArrGen{rid}, rid, Q, &dr->run_count, ws, s, nullptr, nullptr, "k_dscan_rid"))) return r;
     uint32_t* qc = nullptr;
     if (Q != K) {  // slots with no node: compact
       qc = fb.qc = ws.alloc<uint32_t>(Q);
@@ -3131,9 +3141,9 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     // ---- subtree sizes (one launch), slot ranks inside runs, head ranks ----
     LAUNCH(k_run_tree_up, dim3(gr), dim3(BLOCK), 0, s, ra, sarr);
     LAUNCH(k_run_gather, dim3(gr), dim3(BLOCK), 0, s, ra, sarr, tk);
-    if ((r = dscan<SumOp, false>(ArrGen{tk}, xs, K, nullptr, ws, s, nullptr, ra.nR))) return r;
+    if ((r = dscan<SumOp, false>(ArrGen{tk}, xs, K, nullptr, ws, s, nullptr, ra.nR, "k_dscan_xs"))) return r;
     LAUNCH(k_run_side, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, tk, xs, gstart, side);
-    if ((r = dscan<SumOp, false>(SideGen{anc, side}, side, Q, nullptr, ws, s, nullptr))) return r;
+    if ((r = dscan<SumOp, false>(SideGen{anc, side}, side, Q, nullptr, ws, s, nullptr, nullptr, "k_dscan_side"))) return r;
     LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, gstart, side);
     LAUNCH(k_run_pos, dim3(gr), dim3(BLOCK), 0, s, ra, dr);
     LAUNCH(k_run_expand, dim3(gq), dim3(BLOCK), 0, s, ra, Q, anc, rid, side, qc, t->d.doc);
@@ -3277,6 +3287,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
       own += h.fl_part[32 * k + 2];
       slow += h.fl_part[32 * k + 3];
     }
+    if (h.bad_range) return CRDTM_E_RANGE;  // (k_fl_claim's path check; the caller restores the fresh tree)
     const long long new_ts = t->timestamp + own - t->own_bias;
     const bool every = h.err_index == NONE && slow == 0 && present == keys && keys == n;
     if (every && replica_of(new_ts) == replica_of(t->timestamp)) {
@@ -3301,6 +3312,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     if ((r = sync_read(c))) return r;
   }
   const DevResult h1 = *c->hres;
+  if (h1.bad_range) return CRDTM_E_RANGE;
   uint32_t guard = 0;
   const long long new_ts = t->timestamp + h1.own_ok_adds - t->own_bias;
   if (replica_of(new_ts) != replica_of(t->timestamp)) guard |= G_REPLICA_DRIFT;
@@ -3370,6 +3382,11 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   const bool force_replay = fe && fe[0] == '1';
   if (force_replay || t->n_slots != 1 || t->log_n != 0) {
     // incremental merge into existing state: exact replay
+    if (o.n_path) {
+      LAUNCH(k_path_range, dim3(std::min<uint32_t>(grid_for(o.n_path / 2 + 1), 1024)), dim3(BLOCK), 0, s, o, dr);
+      if ((r = sync_read(c))) return r;
+      if (c->hres->bad_range) return CRDTM_E_RANGE;
+    }
     r = run_replay(t, o, w.st, res, force_replay ? G_FORCED : G_NOT_FRESH);
     if (r == CRDTM_OK && st_out)
       LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n,
@@ -3384,6 +3401,11 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   ix.base = rbase;
   ix.dense = (!c->hres->has_negative && range_total <= 4ULL * n + 65536) ? 1u : 0u;
   const bool flat = maxlen == 1 && c->hres->n_del == 0;
+  if (!(ix.dense && flat) && o.n_path) {  // (the flat claim checks its own path elements)
+    LAUNCH(k_path_range, dim3(std::min<uint32_t>(grid_for(o.n_path / 2 + 1), 1024)), dim3(BLOCK), 0, s, o, dr);
+    if ((r = sync_read(c))) return r;
+    if (c->hres->bad_range) return CRDTM_E_RANGE;
+  }
   if (ix.dense) {
     ix.h = TsHash{nullptr, nullptr, 0};
     ix.first = nullptr;

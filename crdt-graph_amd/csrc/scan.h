@@ -201,7 +201,7 @@ struct ArrGen {
 // n_dev (optional): the item count on the device, at most n (the grid covers n).
 template <class OP, bool INCL, class GEN>
 int dscan(GEN gen, uint32_t* out, uint64_t n, uint32_t* total, Arena& ws, hipStream_t st, uint32_t* err,
-          const uint32_t* n_dev = nullptr) {
+          const uint32_t* n_dev = nullptr, const char* label = "k_dscan") {
   if (n == 0) {
     if (total) HIP_CHECK(hipMemsetAsync(total, 0, sizeof(uint32_t), st));
     return CRDTM_OK;
@@ -220,7 +220,7 @@ int dscan(GEN gen, uint32_t* out, uint64_t n, uint32_t* total, Arena& ws, hipStr
   prof_begin(st);
   hipLaunchKernelGGL(kfn, dim3(static_cast<uint32_t>(tiles)), dim3(BLOCK), 0, st, gen, out, n, status, ticket,
                      static_cast<uint32_t>(tiles), ws.scan_epoch, total, err, n_dev);
-  prof_mark("k_dscan", st);
+  prof_mark(label, st);
   return CRDTM_OK;
 }
 

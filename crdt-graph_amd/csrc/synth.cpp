@@ -212,8 +212,9 @@ void genDeep(const crdtm_synth_params& p, uint64_t seed, uint32_t doc, Out& o) {
     leafPos[v] = UINT32_MAX;
   };
   uint64_t delLeft = inter ? nDel : 0;
-  for (uint64_t s = 0, addsDone = 0; addsDone < nAdd; ++s) {
-    if (inter && delLeft > 0 && !leaves.empty() && rng.below(delLeft + (nAdd - addsDone)) < delLeft) {
+  for (uint64_t s = 0, addsDone = 0; addsDone < nAdd || (delLeft > 0 && !leaves.empty()); ++s) {
+    if (inter && delLeft > 0 && !leaves.empty() &&
+        (addsDone == nAdd || rng.below(delLeft + (nAdd - addsDone)) < delLeft)) {
       const int32_t v = leaves[rng.below(leaves.size())];
       emitDel(o, nodes, v, doc, tmp);
       dropLeaf(v);

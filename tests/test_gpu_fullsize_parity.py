@@ -108,6 +108,18 @@ def test_deep10m():
     olib().orc_free(ot)
 
 
+def test_deep10m_interleaved():
+    """Config 4's second variant at its full 10M ops: the same
+    deep tree shape with its Deletes interleaved among the Adds (live leaves,
+    synth.cpp genDeep), so dicts hold tombstones before later inserts — the
+    regime of src/Internal/Node.elm:93-122 — through the exact per-dict replay
+    (bench workload deep10m_il)."""
+    spec = dict(CFG4, deletes_last=0)
+    _, et, ot, res = full_parity(spec)
+    assert res.path_taken != N.PATH_CLOSED_FORM and res.guard & 2, (res.path_taken, res.guard)
+    olib().orc_free(ot)
+
+
 def test_incremental_flat_1m(monkeypatch):
     """The bench's incremental workload shape at scale: a 1M-node flat
     document (config 3's stream, closed form), then successive 10k-op batches

@@ -165,3 +165,30 @@ def test_forest_nested_and_long_documents():
         assert int(out["timestamp"][d]) == L.orc_timestamp(t), d
         assert int(out["applied"][d]) == len(oracle_log(t, 0)[0]), d
         L.orc_free(t)
+
+
+@pytest.mark.parametrize("where", ["flat_path", "flat_ts", "nested_path", "flat_negative_path"])
+def test_out_of_range_keys_rejected(where):
+    """Elm Int runs on JS doubles: keys at or beyond 2^53 are outside the
+    reference's exact range, so crdtm_apply refuses them with
+    CRDTM_E_RANGE (the flat claim checks its own path elements; the other
+    paths a pass of their own) and the tree stays the fresh tree it was."""
+    big = 1 << 53
+    s, n = long_path_stream(3, seed=5, interleaved=False) if where == "nested_path" else \
+        (lambda v: (v, len(v["kind"])))(N.synth(n_ops=5000, replicas=8, window=16, seed=9))
+    s = {k: v.copy() for k, v in s.items() if v is not None}
+    j = n // 2
+    if where == "flat_ts":
+        s["ts"][j] = big + 5
+    elif where == "flat_negative_path":
+        s["path"][s["path_off"][j]] = -big
+    else:
+        s["path"][s["path_off"][j]] = big
+    et = CRDTree.init(0)
+    with pytest.raises(N.CrdtmError):
+        et.apply_arrays(s, n)
+    assert engine_summary(et) == engine_summary(CRDTree.init(0))
+    ok, m = long_path_stream(3, seed=6, interleaved=False)  # the tree still merges
+    ot, rc, _ = oracle_apply_arrays(ok, m)
+    assert et.apply_arrays(ok, m).code == rc == 0
+    assert engine_summary(et) == oracle_summary(ot)
