@@ -390,6 +390,24 @@ def main():
             nm = labels[j].decode()
             acc.setdefault(nm, []).append(ms[j])
     L.crdtm_ctx_profile(ctx, 0)
+    # guard G, measured by the per-dict
+    # replay in one more untimed step: Adds whose walk met a Tombstone above
+    # their timestamp, and the ops before each dict's first such Add (what a
+    # closed-form prefix per dict could serve)
+    guard_g = None
+    if path_taken == 3:
+        os.environ["CRDTM_GUARD_STATS"] = "1"
+        step()
+        del os.environ["CRDTM_GUARD_STATS"]
+        gs = np.zeros(4, np.uint64)
+        if L.crdtm_ctx_guard_stats(ctx, gs.ctypes.data_as(C.c_void_p)) == 1:
+            walked, fail, prefix, nrep = (int(x) for x in gs)
+            guard_g = {"adds_walked": walked, "adds_failing": fail, "failure_rate": fail / max(1, walked),
+                       "ops_replayed": nrep, "closed_form_prefix_ops": prefix,
+                       "closed_form_prefix_fraction": prefix / max(1, nrep),
+                       "note": "an Add fails guard G when its findInsertion walk meets a Tombstone above its "
+                               "timestamp; a dict's ops before its first failing Add are what a closed-form "
+                               "prefix could serve (the rest needs the in-order replay)"}
     # a kernel launched several times per step is summed within the step
     ps = max(1, args.profile_steps)
     per_step = {nm: sum(v) / ps for nm, v in acc.items()}
@@ -419,7 +437,7 @@ def main():
         "config": {"workload": f"{args.workload}: {n} ops per GPU, one document per GPU",
                    "replicas": spec.get("replicas"), "window": spec.get("window", 0),
                    "path": {1: "closed-form", 2: "replay", 3: "per-dict replay"}.get(path_taken, "?"),
-                   "guard": guard, "serial_replay": serial,
+                   "guard": guard, "serial_replay": serial, "guard_g": guard_g,
                    "parallelism": f"documents sharded by id over {world} GPU(s)"},
         "roofline": roofline(args.workload, per_step, launches, B_alg, ms_step, ps),
     }

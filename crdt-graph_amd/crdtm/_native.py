@@ -81,6 +81,7 @@ SIGNATURES = [
                                     C.POINTER(C.c_size_t)]),
     ("crdtm_json_canonical", C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     ("crdtm_free", None, [P]),
+    ("crdtm_ctx_guard_stats", C.c_int, [P, P]),
     ("crdtm_ctx_profile", C.c_int, [P, C.c_int]),
     ("crdtm_ctx_phase_times", C.c_int, [P, C.c_char_p, C.c_size_t, P, C.c_int]),
 ]

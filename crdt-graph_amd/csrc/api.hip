@@ -154,6 +154,7 @@ uint64_t arena_need(uint64_t n, uint64_t np, const crdtm_tree* t) {
 int ensure_arena(crdtm_ctx* c, uint64_t bytes) {
   if (c->ws.cap >= bytes) return CRDTM_OK;
   HIP_CHECK(hipStreamSynchronize(c->stream));
+  HIP_CHECK(hipStreamSynchronize(c->side));
   if (c->ws.base) HIP_CHECK(hipFree(c->ws.base));
   c->ws.base = nullptr;
   c->ws.cap = 0;
@@ -225,6 +226,7 @@ int crdtm_ctx_destroy(crdtm_ctx* c) {
   hipFree(c->crange);
   hipFree(c->ws.scan_status);
   hipFree(c->rtab);
+  if (c->gstat_dev) hipFree(c->gstat_dev);
   if (c->own_stream) hipStreamDestroy(c->stream);
   hipStreamSynchronize(c->side);
   hipStreamDestroy(c->side);
@@ -356,6 +358,7 @@ int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_b
   HIP_CHECK(hipSetDevice(c->device));
   if (int ru = unshare_tree(t, true)) return ru;  // this version is about to be written
   c->clear_marks();
+  c->gstat_valid = 0;
   const uint64_t n = ops->n_ops;
   uint64_t np = ops->n_path;
   if (!ops_on_device && n) np = ops->path_off[n];
@@ -414,6 +417,7 @@ int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_b
       break;
     } catch (const ArenaOverflow&) {
       HIP_CHECK(hipStreamSynchronize(c->stream));
+      HIP_CHECK(hipStreamSynchronize(c->side));  // (side-stream work may read the old arena)
       r = CRDTM_E_NOMEM;
     }
   }
@@ -568,6 +572,12 @@ int crdtm_tree_document(const crdtm_tree* tc, uint32_t* vals, uint64_t cap, uint
     return CRDTM_E_NOMEM;
   }
   return CRDTM_OK;
+}
+
+int crdtm_ctx_guard_stats(crdtm_ctx* c, uint64_t* out) {
+  if (!c || !out) return CRDTM_E_ARG;
+  for (int k = 0; k < 4; ++k) out[k] = c->gstat_valid ? c->gstat[k] : 0;
+  return c->gstat_valid;
 }
 
 int crdtm_ctx_profile(crdtm_ctx* c, int enable) {

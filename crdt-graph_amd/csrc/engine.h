@@ -95,6 +95,10 @@ struct crdtm_ctx {
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   crdtm::Arena ws;
+  // guard-G statistics of the last apply's per-dict replay (CRDTM_GUARD_STATS=1, pdr.hip)
+  unsigned long long* gstat_dev = nullptr;
+  uint64_t gstat[4] = {0, 0, 0, 0};
+  int gstat_valid = 0;
   crdtm::DevResult* dres = nullptr;  // device
   crdtm::DevResult* hres = nullptr;  // pinned host
   uint32_t* rtab = nullptr;          // replica table [REPLICA_SLOTS], 0 = empty (kept clean between calls)

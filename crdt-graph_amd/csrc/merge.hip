@@ -2210,25 +2210,23 @@ __global__ void __launch_bounds__(BLOCK) k_fl_rep_collect(OpsDev o, uint32_t nr,
   }
 }
 
-// K2a: effective parent. A typing run is a maximal slot interval [h, c]
-// with anc[q] = q - 1 for q in (h, c]; rh[q] = h (inclusive max-scan, see
-// k_rh_*). Walking x's anchor chain from c down a run visits c, c-1, ..., h
-// in slot order, so the first node below x is x - 1 when h < x, and the
-// whole run is skipped otherwise: one step per run instead of per node
-// (flat10m: max walk 312 nodes -> 23 runs). anc[] is overwritten with ep as
-// walks finish; a concurrent reader then sees ep(h) instead of anchor(h),
-// which skips only nodes > h > x, so every walk stays exact.
-// (k_fl_ep_runs, with the K4 run decomposition below.)
-
-// Run heads: rh[q] = max{q' <= q : anc[q'] != q' - 1}, an inclusive
-// max-scan over head flags (scan.h).
-struct RunHeadGen {
+// Runs and their ids in one scan. A run is a maximal slot interval [h, e)
+// whose every slot but h is anchored at the slot before it (a replica's
+// typing run: consecutive counters are consecutive slots); an absent slot is
+// a run of its own with no node (a "hole" run). Head flags are summed into
+// rid[q] = 1 + the index of q's run; the generator writes anc[q] (anchor slot
+// per slot, ABSENT = no node) as a side output and, from the scanned values,
+// every run's head slot and the anchor of its head (epilogue).
+struct RunIdGen {
   static constexpr bool kStriped = false;  // loads through load() (it writes anc as a side output)
+  static constexpr bool kEpilogue = true;
   __device__ __forceinline__ bool aligned(uint64_t) const { return false; }
   __device__ __forceinline__ uint4 load4(uint64_t) const { return make_uint4(0u, 0u, 0u, 0u); }
   const unsigned long long* rec;
   uint32_t Q;
-  uint32_t* anc;  // side output: anchor slot per slot (ABSENT = no node)
+  uint32_t* anc;    // side output: anchor slot per slot (ABSENT = no node)
+  uint32_t* heads;  // run -> head slot
+  uint32_t* hanc;   // run -> anchor slot of its head (ABSENT: a hole run)
   // A missing anchor (NONE) only occurs in a batch that fails (NotFound),
   // which the flat speculation discards: it reads as the sentinel so that
   // the speculative walks stay in bounds.
@@ -2237,7 +2235,13 @@ struct RunHeadGen {
     const uint32_t a = static_cast<uint32_t>(r);
     return a == NONE ? Q : a;
   }
+  // q continues the run of q - 1 iff both hold a node and q is anchored at q - 1
+  __device__ __forceinline__ uint32_t flag(uint32_t q, uint32_t a, uint32_t aprev) const {
+    return (q == 0 || a == ABSENT || aprev == ABSENT || a != q - 1) ? 1u : 0u;
+  }
   __device__ __forceinline__ void load(uint64_t b, uint64_t n, uint32_t* v) const {
+    const uint32_t q0 = static_cast<uint32_t>(b);
+    uint32_t aprev = q0 > 0 && q0 - 1 < n ? anchor(rec[q0 - 1]) : ABSENT;
     if (b + DS_ITEMS <= n) {
       uint32_t a[DS_ITEMS];
 #pragma unroll
@@ -2251,8 +2255,8 @@ struct RunHeadGen {
         *reinterpret_cast<uint4*>(anc + b + j) = make_uint4(a[j], a[j + 1], a[j + 2], a[j + 3]);
 #pragma unroll
       for (int j = 0; j < DS_ITEMS; ++j) {
-        const uint32_t q = static_cast<uint32_t>(b) + j;
-        v[j] = (q == 0 || a[j] != q - 1) ? q : 0u;
+        v[j] = flag(q0 + j, a[j], aprev);
+        aprev = a[j];
       }
     } else {
 #pragma unroll
@@ -2263,8 +2267,21 @@ struct RunHeadGen {
           a = anchor(rec[q]);
           anc[q] = a;
         }
-        v[j] = (q < n && (q == 0 || a != q - 1)) ? static_cast<uint32_t>(q) : 0u;
+        v[j] = q < n ? flag(static_cast<uint32_t>(q), a, aprev) : 0u;
+        aprev = a;
       }
+    }
+  }
+  __device__ __forceinline__ void epilogue(uint64_t b, uint64_t n, const uint32_t* v, uint32_t start) const {
+    uint32_t prev = start;
+#pragma unroll
+    for (int j = 0; j < DS_ITEMS; ++j) {
+      const uint64_t q = b + j;
+      if (q < n && v[j] != prev) {  // a head: its run's index is v[j] - 1
+        heads[v[j] - 1] = static_cast<uint32_t>(q);
+        hanc[v[j] - 1] = anc[q];  // (this thread's own store above)
+      }
+      prev = v[j];
     }
   }
 };
@@ -2500,77 +2517,34 @@ __global__ void __launch_bounds__(BLOCK) k_fl_log_copy(OpsDev o, TreeDev T) {
 }
 
 // ---------------------------------------------------------------------------
-// K4 (flat): the document order by ep-run decomposition. An ep-run is a
-// maximal interval of present slots [h, h + len) with ep(q) = q - 1 inside.
-// A node's children all have larger slots (an effective parent has the
-// smaller timestamp), so q + 1 is the smallest, i.e. the LAST child of q in
-// the descending order (src/Internal/Node.elm:93-104 via the closed form,
+// K4 (flat): the document order by run decomposition. A run is a maximal
+// interval of present slots [h, h + len) each anchored at the slot before it
+// (RunIdGen), so ep(q) = q - 1 inside (the first node below q on its anchor
+// chain). A node's children all have larger slots (an effective parent has
+// the smaller timestamp), so q + 1 is the smallest, i.e. the LAST child of q
+// in the descending order (src/Internal/Node.elm:93-104 via the closed form,
 // DESIGN.md): the pre-order visits q, then q's other ("side") children's
-// subtrees, then q + 1. With side(q) = the sizes of q's side children's
-// subtrees and P(q) = sum over the run's slots before q of (1 + side), a
-// slot's document rank is pos(head) + P(q), the subtree of run r has
-// T(r) = P(end) and a side child run r of slot j starts at
-// pos(j) + 1 + (the subtrees of j's side children with a larger slot).
-// Runs form a shallow tree (flat10m: 1.0M runs, depth <= 11): T comes
-// bottom-up level by level, pos(head) top-down as a sum along the run's
-// ancestor chain. Every per-slot pass streams through slot order; only the
-// 1M-run passes gather. A run tree deeper than RUN_MAXD takes the generic
-// Euler-tour list ranking instead (run_fail).
+// subtrees, then q + 1. Every side child heads a run ("child run" of q's run,
+// attached at q), so a slot's document rank is pos(head) + the run's slots
+// before it + the subtrees of the run's child runs attached below it; the
+// subtree of run r has T(r) = len(r) + the subtrees of its child runs; and a
+// child run r of slot j starts at pos(j) + 1 + (the subtrees of j's other
+// child runs with a larger slot). Runs form a shallow tree (flat10m: 1.0M
+// runs, depth <= 11): T comes bottom-up, pos(head) top-down as a sum along
+// the run's ancestor chain. Everything between the run scan and the final
+// expansion works on the 1M runs, not the 10M slots. A run tree deeper than
+// RUN_MAXD takes the generic Euler-tour list ranking instead (run_fail).
 // ---------------------------------------------------------------------------
 constexpr uint32_t RUN_MAXD = 64;
 
-// K2a (see above); hflag[q] = q heads an ep-run.
-__global__ void __launch_bounds__(BLOCK) k_fl_ep_runs(uint32_t Q, uint32_t* anc, const uint32_t* rh, uint32_t* hflag) {
-  GRID_STRIDE(x, Q) {
-    uint32_t d = anc[x];
-    if (d == ABSENT) {
-      hflag[x] = 0;
-      continue;
-    }
-    if (d < Q && d > x) {
-      // (a valid batch's anchors form a forest of present slots; a failing
-      // batch run by the flat speculation may anchor at a slot without a node
-      // or hold a cycle: those walks end at the sentinel, which keeps every
-      // walk finite and in bounds, and the speculation is discarded)
-      for (uint32_t steps = 0; d < Q && d > x; ++steps) {
-        const uint32_t h = rh[d];
-        if (h < x) {
-          d = x - 1;
-          break;
-        }
-        if (steps > Q) {
-          d = Q;
-          break;
-        }
-        d = __hip_atomic_load(&anc[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (d >= Q || (d != x - 1 && __hip_atomic_load(&anc[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ABSENT))
-        d = Q;
-      __hip_atomic_store(&anc[x], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (d != Q && (d >= x || anc[d] == ABSENT)) {  // (self-anchored / nodeless anchor: a failing batch)
-      d = Q;
-      anc[x] = d;
-    }
-    hflag[x] = (x == 0 || d != x - 1) ? 1u : 0u;
-  }
-}
-
-// heads[run] = its first slot (rid = inclusive count of heads); side[] := 0
-__global__ void __launch_bounds__(BLOCK) k_run_heads(uint32_t Q, const uint32_t* ep, const uint32_t* rid,
-                                                     uint32_t* heads, uint32_t* side) {
-  GRID_STRIDE(q, Q) {
-    const uint32_t e = ep[q];
-    side[q] = 0;
-    if (e != ABSENT && (q == 0 || e != q - 1)) heads[rid[q] - 1] = q;
-  }
-}
-
 struct RunArr {
   const uint32_t* nR;        // device: number of runs
-  uint32_t* heads;
-  uint32_t* par;             // parent run (NONE: a child of the root sentinel)
+  uint32_t* heads;           // head slot
+  uint32_t* hanc;            // anchor of the head (ABSENT: a hole run), then its effective parent
+  uint32_t* par;             // parent run (NONE: a child of the root sentinel, or a hole run)
   uint32_t* len;
   uint32_t* nch;             // child runs
+  uint32_t* estart;          // sorted position of the run's first child run (valid when nch > 0)
   unsigned long long* ca;    // children arrived << 32 | their subtree sizes
   uint32_t* T;               // subtree size
   uint32_t* w;               // top-down increment along the chain
@@ -2579,24 +2553,70 @@ struct RunArr {
 
 #define RUN_LOOP(r) for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x, nr_ = *a.nR; r < nr_; r += gridDim.x * blockDim.x)
 
-// parent run and length of every run; the sibling sort's input (key =
-// attach slot, the root sentinel = Q) listed in descending run order, so the
-// stable sort leaves siblings at one slot in descending slot order
-__global__ void __launch_bounds__(BLOCK) k_run_par(RunArr a, uint32_t Q, uint32_t K, const uint32_t* ep,
-                                                   const uint32_t* rid, const uint32_t* qc, uint32_t* skey,
-                                                   uint32_t* sval) {
+// K2a at run granularity. Inside a run ep(q) = q - 1; only a head needs its
+// effective parent (the first node on its anchor chain below it), and only a
+// head anchored at a larger slot walks: the chain runs down through whole
+// runs (a run's slots are all larger than x when its head is), so each step
+// jumps from the run holding d to its head's anchor (flat10m: 0.49M walks of
+// at most 23 steps). hanc[] is overwritten with ep as walks finish; a
+// concurrent reader then sees ep(h) instead of anchor(h), which skips only
+// nodes > h > x, so every walk stays exact. Then the run's parent run (the
+// run holding ep), its length, and the sibling sort's input (key = attach
+// slot, the root sentinel = Q, hole runs Q + 1) listed in descending run
+// order, so the stable sort leaves siblings at one slot in descending slot
+// order.
+__global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, const uint32_t* rid, const uint32_t* anc,
+                                                  uint32_t* skey, uint32_t* sval) {
   const uint32_t R = *a.nR;
   RUN_LOOP(r) {
-    const uint32_t h = a.heads[r];
+    const uint32_t x = a.heads[r];
+    uint32_t d = a.hanc[r];
     const uint32_t hn = r + 1 < R ? a.heads[r + 1] : Q;
-    const uint32_t ln = qc ? (r + 1 < R ? qc[hn] : K) - qc[h] : hn - h;
-    const uint32_t p = ep[h];
-    a.par[r] = p == Q ? NONE : rid[p] - 1;
-    a.len[r] = ln;
+    if (d == ABSENT) {  // a hole run
+      a.par[r] = NONE;
+      a.len[r] = 0;
+      a.nch[r] = 0;
+      a.ca[r] = 0;
+      skey[R - 1 - r] = Q + 1;
+      sval[R - 1 - r] = r;
+      continue;
+    }
+    if (d < Q && d > x) {
+      // (a valid batch's anchors form a forest of present slots; a failing
+      // batch run by the flat speculation may anchor at a slot without a node
+      // or hold a cycle: those walks end at the sentinel, which keeps every
+      // walk finite and in bounds, and the speculation is discarded)
+      for (uint32_t steps = 0; d < Q && d > x; ++steps) {
+        const uint32_t j = rid[d] - 1;
+        const uint32_t h = a.heads[j];
+        if (h <= x || steps > R) {
+          d = Q;
+          break;
+        }
+        d = __hip_atomic_load(&a.hanc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (d >= Q || anc[d] == ABSENT) d = Q;
+      __hip_atomic_store(&a.hanc[r], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (d != Q && (d >= x || anc[d] == ABSENT)) {  // (self-anchored / nodeless anchor: a failing batch)
+      d = Q;
+      a.hanc[r] = d;
+    }
+    a.par[r] = d == Q ? NONE : rid[d] - 1;
+    a.len[r] = hn - x;  // (a hole after the run is a run of its own)
     a.nch[r] = 0;
     a.ca[r] = 0;
-    skey[R - 1 - r] = p;
+    skey[R - 1 - r] = d;
     sval[R - 1 - r] = r;
+  }
+}
+
+// The generic order's input (a run tree deeper than RUN_MAXD): ep per slot
+// (q - 1 inside a run, the walked effective parent at a head), into anc.
+__global__ void __launch_bounds__(BLOCK) k_run_ep_slots(RunArr a, uint32_t Q, const uint32_t* rid, uint32_t* anc) {
+  GRID_STRIDE(q, Q) {
+    if (anc[q] == ABSENT) continue;
+    const uint32_t r = rid[q] - 1;
+    anc[q] = a.heads[r] == q ? a.hanc[r] : q - 1;
   }
 }
 
@@ -2607,7 +2627,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_nch(RunArr a, uint32_t Q, const u
   const uint32_t R = *a.nR;
   RUN_LOOP(k) {
     const uint32_t p = pk[k];
-    if (p != Q && (k + 1 == R || pk[k + 1] != p)) atomicAdd(&a.nch[a.par[sarr[k]]], k - gstart[p] + 1);
+    if (p < Q && (k + 1 == R || pk[k + 1] != p)) atomicAdd(&a.nch[a.par[sarr[k]]], k - gstart[p] + 1);
   }
 }
 
@@ -2668,59 +2688,39 @@ __global__ void __launch_bounds__(BLOCK) k_run_gather(RunArr a, const uint32_t* 
   RUN_LOOP(k) tk[k] = a.T[sarr[k]];
 }
 
-// gstart[p] = the first position of slot p's sibling group in the sorted list
-__global__ void __launch_bounds__(BLOCK) k_run_gstart(RunArr a, const uint32_t* pk, uint32_t* gstart) {
+// gstart[p] = the first position of slot p's sibling group in the sorted
+// list; estart[P] = the first position of run P's child runs (they are
+// contiguous: P owns a contiguous slot range and the list is by slot)
+__global__ void __launch_bounds__(BLOCK) k_run_gstart(RunArr a, uint32_t Q, const uint32_t* pk, const uint32_t* sarr,
+                                                      uint32_t* gstart) {
   RUN_LOOP(k) {
     const uint32_t p = pk[k];
-    if (k == 0 || pk[k - 1] != p) gstart[p] = k;
-  }
-}
-
-// side(p) = the subtree sizes of the runs hanging from slot p: the last
-// sibling of each slot's group stores the group's sum (no atomics)
-__global__ void __launch_bounds__(BLOCK) k_run_side(RunArr a, uint32_t Q, const uint32_t* pk, const uint32_t* tk,
-                                                    const uint32_t* xs, const uint32_t* gstart, uint32_t* side) {
-  const uint32_t R = *a.nR;
-  RUN_LOOP(k) {
-    const uint32_t p = pk[k];
-    if (p != Q && (k + 1 == R || pk[k + 1] != p)) side[p] = xs[k] + tk[k] - xs[gstart[p]];
-  }
-}
-
-// G(q) = exclusive prefix of (1 + side(q)) over present slots: a slot's rank
-// inside its run is G(q) - G(head)
-struct SideGen {
-  static constexpr bool kStriped = false;
-  const uint32_t* ep;
-  const uint32_t* side;
-  __device__ __forceinline__ bool aligned(uint64_t) const { return false; }
-  __device__ __forceinline__ uint4 load4(uint64_t) const { return make_uint4(0u, 0u, 0u, 0u); }
-  __device__ __forceinline__ void load(uint64_t b, uint64_t n, uint32_t* v) const {
-    if (b + DS_ITEMS <= n) {
-#pragma unroll
-      for (int j = 0; j < DS_ITEMS; j += 4) {
-        const uint4 e = *reinterpret_cast<const uint4*>(ep + b + j);
-        const uint4 s = *reinterpret_cast<const uint4*>(side + b + j);
-        v[j] = e.x != ABSENT ? 1u + s.x : 0u;
-        v[j + 1] = e.y != ABSENT ? 1u + s.y : 0u;
-        v[j + 2] = e.z != ABSENT ? 1u + s.z : 0u;
-        v[j + 3] = e.w != ABSENT ? 1u + s.w : 0u;
+    if (k == 0 || pk[k - 1] != p) {
+      if (p <= Q) gstart[p] = k;
+      if (p < Q) {
+        const uint32_t P = a.par[sarr[k]];
+        if (k == 0 || pk[k - 1] >= Q || a.par[sarr[k - 1]] != P) a.estart[P] = k;
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < DS_ITEMS; ++j) v[j] = (b + j < n && ep[b + j] != ABSENT) ? 1u + side[b + j] : 0u;
     }
   }
-};
+}
 
 // w(r): the head's rank minus its parent run head's rank (root children:
-// the rank itself)
+// the rank itself). Inside the parent run P, slot p is preceded by p - head(P)
+// slots of P and by the subtrees of P's child runs attached before p; run r
+// itself comes after p and after its siblings at p with a larger slot (the
+// ones sorted before it): together, the child runs of P sorted before r.
 __global__ void __launch_bounds__(BLOCK) k_run_w(RunArr a, uint32_t Q, const uint32_t* sarr, const uint32_t* pk,
-                                                 const uint32_t* xs, const uint32_t* gstart, const uint32_t* G) {
+                                                 const uint32_t* xs, const uint32_t* gstart) {
   RUN_LOOP(k) {
     const uint32_t r = sarr[k], p = pk[k];
-    const uint32_t off = xs[k] - xs[gstart[p]];  // siblings hanging from p with a larger slot
-    a.w[r] = p == Q ? off : G[p] - G[a.heads[a.par[r]]] + 1u + off;
+    if (p > Q) continue;  // (hole runs)
+    if (p == Q) {
+      a.w[r] = xs[k] - xs[gstart[Q]];
+    } else {
+      const uint32_t P = a.par[r];
+      a.w[r] = xs[k] - xs[a.estart[P]] + (p - a.heads[P]) + 1u;
+    }
   }
 }
 
@@ -2740,12 +2740,30 @@ __global__ void __launch_bounds__(BLOCK) k_run_pos(RunArr a, DevResult* dres) {
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, const uint32_t* ep, const uint32_t* rid,
-                                                      const uint32_t* G, const uint32_t* qc, uint32_t* doc) {
+// doc[rank] = tree slot, per slot: rank = the head's rank + the slots of the
+// run before q + the subtrees of the run's child runs attached at slots below
+// q (child runs at q itself follow q). The child runs of the run are
+// contiguous in the sorted list with ascending attach slots: a binary search
+// finds the first one at or above q (most runs have none).
+__global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint32_t K, const uint32_t* anc,
+                                                      const uint32_t* rid, const uint32_t* pk, const uint32_t* xs,
+                                                      const uint32_t* tk, const uint32_t* qc, uint32_t* doc) {
   GRID_STRIDE(q, Q) {
-    if (ep[q] == ABSENT) continue;
+    if (anc[q] == ABSENT) continue;
     const uint32_t r = rid[q] - 1;
-    doc[a.posh[r] + G[q] - G[a.heads[r]]] = 1 + (qc ? qc[q] : q);
+    uint32_t p = a.posh[r] + (q - a.heads[r]);
+    const uint32_t ne = a.nch[r];
+    if (ne) {
+      const uint32_t e0 = a.estart[r];
+      uint32_t lo = e0, hi = e0 + ne;  // first k with pk[k] >= q
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pk[mid] < q) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo > e0) p += xs[lo - 1] + tk[lo - 1] - xs[e0];
+    }
+    if (p < K) doc[p] = 1 + (qc ? qc[q] : q);  // (a rank past K: a speculation that fails)
   }
 }
 
@@ -3081,6 +3099,9 @@ struct FlatBufs {
   uint32_t* cnt;
   uint32_t* fill;
   uint32_t* qc;
+  uint32_t* rid;    // slot -> 1 + its run
+  uint32_t* heads;  // run -> head slot
+  uint32_t* hanc;   // run -> effective parent of its head
   long long* rep;
 };
 
@@ -3097,56 +3118,52 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
   int r;
   fb.qc = nullptr;
   if (K > 0) {
-    // ---- K2a: effective parents (run-skipping walk over the anchor runs) ----
+    // ---- runs: one scan (run ids, heads, anchors) ----
     const uint32_t gq = grid_for(Q);
-    uint32_t* rh = ws.alloc<uint32_t>(Q);
-    if ((r = dscan<MaxOp, true>(RunHeadGen{rec, Q, anc}, rh, Q, nullptr, ws, s, nullptr, nullptr,
-                                "k_dscan_runhead")))
+    RunArr ra;
+    ra.nR = &dr->run_count;
+    // (a run per present slot at most, plus a hole run per absent slot)
+    ra.heads = fb.heads = ws.alloc<uint32_t>(Q + 1);
+    ra.hanc = fb.hanc = ws.alloc<uint32_t>(Q + 1);
+    uint32_t* rid = fb.rid = ws.alloc<uint32_t>(Q);
+    if ((r = dscan<SumOp, true>(RunIdGen{rec, Q, anc, ra.heads, ra.hanc}, rid, Q, &dr->run_count, ws, s, nullptr,
+                                nullptr, "k_dscan_runs")))
       return r;
-    uint32_t* rid = ws.alloc<uint32_t>(Q);  // ep-run head flags, then inclusive head counts
-    LAUNCH(k_fl_ep_runs, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK), 0, s, Q, anc, rh, rid);
-    if ((r = dscan<SumOp, true>(ArrGen{rid}, rid, Q, &dr->run_count, ws, s, nullptr, nullptr, "k_dscan_rid"))) return r;
     uint32_t* qc = nullptr;
     if (Q != K) {  // slots with no node: compact
       qc = fb.qc = ws.alloc<uint32_t>(Q);
       LAUNCH(k_fl_present, dim3(gq), dim3(BLOCK), 0, s, Q, anc, qc);
       if ((r = scan_excl_u32(qc, qc, Q, nullptr, ws, s))) return r;
     }
-    // ---- K4: ep-runs, parent runs, sibling order (stable radix sort by attach slot) ----
-    RunArr ra;
-    ra.nR = &dr->run_count;
-    ra.heads = ws.alloc<uint32_t>(K + 1);
-    ra.par = ws.alloc<uint32_t>(K + 1);
-    ra.len = ws.alloc<uint32_t>(K + 1);
-    ra.nch = ws.alloc<uint32_t>(K + 1);
-    ra.ca = ws.alloc<unsigned long long>(K + 1);
-    ra.T = ws.alloc<uint32_t>(K + 1);
-    ra.w = ws.alloc<uint32_t>(K + 1);
-    ra.posh = ws.alloc<uint32_t>(K + 1);
-    uint32_t* side = ws.alloc<uint32_t>(Q + 1);  // side(q), then G(q)
-    uint32_t* sk[2] = {ws.alloc<uint32_t>(K + 1), ws.alloc<uint32_t>(K + 1)};
-    uint32_t* sv[2] = {ws.alloc<uint32_t>(K + 1), ws.alloc<uint32_t>(K + 1)};
-    uint32_t* xs = ws.alloc<uint32_t>(K + 1);
+    // ---- K2a (heads' effective parents), parent runs, sibling order (stable radix sort by attach slot) ----
+    ra.par = ws.alloc<uint32_t>(Q + 1);
+    ra.len = ws.alloc<uint32_t>(Q + 1);
+    ra.nch = ws.alloc<uint32_t>(Q + 1);
+    ra.estart = ws.alloc<uint32_t>(Q + 1);
+    ra.ca = ws.alloc<unsigned long long>(Q + 1);
+    ra.T = ws.alloc<uint32_t>(Q + 1);
+    ra.w = ws.alloc<uint32_t>(Q + 1);
+    ra.posh = ws.alloc<uint32_t>(Q + 1);
+    uint32_t* sk[2] = {ws.alloc<uint32_t>(Q + 1), ws.alloc<uint32_t>(Q + 1)};
+    uint32_t* sv[2] = {ws.alloc<uint32_t>(Q + 1), ws.alloc<uint32_t>(Q + 1)};
+    uint32_t* xs = ws.alloc<uint32_t>(Q + 1);
     uint32_t* gstart = fb.cnt;  // [Q + 1] (the generic order's child counts; unused here)
-    const uint32_t gr = grid_for(K, BLOCK, 2048);
-    LAUNCH(k_run_heads, dim3(gq), dim3(BLOCK), 0, s, Q, anc, rid, ra.heads, side);
-    LAUNCH(k_run_par, dim3(gr), dim3(BLOCK), 0, s, ra, Q, K, anc, rid, qc, sk[0], sv[0]);
+    const uint32_t gr = grid_for(Q, BLOCK, 2048);
+    LAUNCH(k_run_ep, dim3(gr), dim3(BLOCK), 0, s, ra, Q, rid, anc, sk[0], sv[0]);
     uint32_t sbits = 8;
-    while (sbits < 32 && (static_cast<uint64_t>(Q) >> sbits) != 0) sbits += 8;
+    while (sbits < 32 && ((static_cast<uint64_t>(Q) + 1) >> sbits) != 0) sbits += 8;
     uint32_t *pk = nullptr, *sarr = nullptr;  // attach slot, run: siblings grouped by slot, slots ascending
-    if ((r = radix_sort_pairs(sk[0], sv[0], sk[1], sv[1], ra.nR, K, sbits, ws, s, &pk, &sarr))) return r;
+    if ((r = radix_sort_pairs(sk[0], sv[0], sk[1], sv[1], ra.nR, Q, sbits, ws, s, &pk, &sarr))) return r;
     uint32_t* tk = pk == sk[0] ? sk[1] : sk[0];  // (free after the sort)
-    LAUNCH(k_run_gstart, dim3(gr), dim3(BLOCK), 0, s, ra, pk, gstart);
+    LAUNCH(k_run_gstart, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, sarr, gstart);
     LAUNCH(k_run_nch, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, sarr, gstart);
-    // ---- subtree sizes (one launch), slot ranks inside runs, head ranks ----
+    // ---- subtree sizes (one launch), head ranks, the document order ----
     LAUNCH(k_run_tree_up, dim3(gr), dim3(BLOCK), 0, s, ra, sarr);
     LAUNCH(k_run_gather, dim3(gr), dim3(BLOCK), 0, s, ra, sarr, tk);
-    if ((r = dscan<SumOp, false>(ArrGen{tk}, xs, K, nullptr, ws, s, nullptr, ra.nR, "k_dscan_xs"))) return r;
-    LAUNCH(k_run_side, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, tk, xs, gstart, side);
-    if ((r = dscan<SumOp, false>(SideGen{anc, side}, side, Q, nullptr, ws, s, nullptr, nullptr, "k_dscan_side"))) return r;
-    LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, gstart, side);
+    if ((r = dscan<SumOp, false>(ArrGen{tk}, xs, Q, nullptr, ws, s, nullptr, ra.nR, "k_dscan_xs"))) return r;
+    LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, gstart);
     LAUNCH(k_run_pos, dim3(gr), dim3(BLOCK), 0, s, ra, dr);
-    LAUNCH(k_run_expand, dim3(gq), dim3(BLOCK), 0, s, ra, Q, anc, rid, side, qc, t->d.doc);
+    LAUNCH(k_run_expand, dim3(gq), dim3(BLOCK), 0, s, ra, Q, K, anc, rid, pk, xs, tk, qc, t->d.doc);
     LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d, t->cap.slots);
     uint32_t* logidx = nullptr;
     if (!all_applied) {  // compacted log (its scans share the ctx scan pool: main stream)
@@ -3186,6 +3203,12 @@ static int flat_order_fallback(crdtm_tree* t, uint32_t Q, uint32_t K, FlatBufs& 
   uint32_t* fill = fb.fill;
   uint32_t* qc = fb.qc;
   int r;
+  {  // ep per slot (the run path keeps it per run)
+    RunArr ra{};
+    ra.heads = fb.heads;
+    ra.hanc = fb.hanc;
+    LAUNCH(k_run_ep_slots, dim3(gq), dim3(BLOCK), 0, s, ra, Q, fb.rid, anc);
+  }
   // ---- a run tree deeper than RUN_MAXD: children of every node, Euler tour + list ranking ----
   uint32_t* carr = ws.alloc<uint32_t>(U);
   uint32_t* ns = ws.alloc<uint32_t>(U);
@@ -3401,11 +3424,20 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   ix.base = rbase;
   ix.dense = (!c->hres->has_negative && range_total <= 4ULL * n + 65536) ? 1u : 0u;
   const bool flat = maxlen == 1 && c->hres->n_del == 0;
-  if (!(ix.dense && flat) && o.n_path) {  // (the flat claim checks its own path elements)
-    LAUNCH(k_path_range, dim3(std::min<uint32_t>(grid_for(o.n_path / 2 + 1), 1024)), dim3(BLOCK), 0, s, o, dr);
-    if ((r = sync_read(c))) return r;
-    if (c->hres->bad_range) return CRDTM_E_RANGE;
+  // path elements' range check (the flat claim checks its own): one streaming
+  // pass on the side stream beside K1's latency-bound levels, joined before
+  // the next result read, which checks it before anything is written
+  const bool side_range = !(ix.dense && flat) && o.n_path;
+  if (side_range) {
+    HIP_CHECK(hipEventRecord(c->ev_fork, s));
+    HIP_CHECK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+    LAUNCH(k_path_range, dim3(std::min<uint32_t>(grid_for(o.n_path / 2 + 1), 1024)), dim3(BLOCK), 0, c->side, o,
+           dr);
+    HIP_CHECK(hipEventRecord(c->ev_join, c->side));
   }
+  auto range_ok = [&]() -> int {  // (after a sync_read that followed the join)
+    return c->hres->bad_range ? CRDTM_E_RANGE : CRDTM_OK;
+  };
   if (ix.dense) {
     ix.h = TsHash{nullptr, nullptr, 0};
     ix.first = nullptr;
@@ -3438,6 +3470,8 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   } else {
     HIP_CHECK(hipMemsetAsync(w.maxadd, 0, (n + 1) * sizeof(uint32_t), s));
     if (maxlen > MAXLV_BUCKET) {  // paths this deep are not bucketed: exact replay
+      HIP_CHECK(hipStreamWaitEvent(s, c->ev_join, 0));
+      if ((r = sync_read(c)) || (r = range_ok())) return r;
       r = run_replay(t, o, w.st, res, G_DEEP_PATH);
       if (r == CRDTM_OK && st_out)
         LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, w.st, n,
@@ -3474,7 +3508,8 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   }
   HIP_CHECK(hipMemsetAsync(&dr->first_del, 0xFF, sizeof(uint32_t), s));
   LAUNCH(k_stats, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, w, t->timestamp, dr);
-  if ((r = sync_read(c))) return r;
+  if (side_range) HIP_CHECK(hipStreamWaitEvent(s, c->ev_join, 0));
+  if ((r = sync_read(c)) || (r = range_ok())) return r;
   if (c->hres->first_del != NONE && c->hres->last_add > c->hres->first_del + 1) {
     LAUNCH(k_guard_maxadd, dim3(g), dim3(BLOCK), 0, s, o, w);
     LAUNCH(k_guard_del, dim3(g), dim3(BLOCK), 0, s, o, w, dr);

@@ -87,6 +87,12 @@ struct PdrCtx {
   uint32_t log_min;        // slots a dict needs to keep a change log
   uint32_t* where;         // per slot position: pdr_blocked's compaction scratch
   uint32_t blk_spare;      // 0, or (tests) blocks beyond a repacked chain before pdr_blocked compacts
+  // guard-G statistics (env CRDTM_GUARD_STATS=1; nullptr: off). An Add fails
+  // guard G when its findInsertion walk meets a Tombstone whose key is above
+  // its own timestamp — a node that canonical RGA would pass and that was
+  // deleted before the Add: the first such Add of a
+  // dict ends the prefix the closed form could serve exactly.
+  unsigned long long* gcount;  // [0] Adds that walked, [1] G-failing ones, [2] ops before each dict's first failure
   PdrInst I;
 };
 
@@ -234,11 +240,21 @@ __device__ __forceinline__ uint32_t pdr_next_live(const uint32_t* S, uint32_t K,
   return p;
 }
 
+__device__ __forceinline__ void pdr_gstat_flush(const PdrCtx& p, uint32_t adds, uint32_t fails, uint32_t prefix) {
+  if (adds) atomicAdd(&p.gcount[0], static_cast<unsigned long long>(adds));
+  if (fails) atomicAdd(&p.gcount[1], static_cast<unsigned long long>(fails));
+  if (prefix) atomicAdd(&p.gcount[2], static_cast<unsigned long long>(prefix));
+}
+
 // ---- P2: the serial replay of one dict (instance) on one wave ----
 // All lanes run the loop with identical values (wave-uniform control flow,
 // broadcast LDS reads); S points to LDS (or to the region for huge dicts).
-template <bool ORIG>
+// MODE: 0 a snapshot instance, 1 an original dict, 2 an original dict with
+// the guard-G statistics (CRDTM_GUARD_STATS=1: separate code, so the timed
+// replay carries no trace of them)
+template <int MODE>
 __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S) {
+  constexpr bool ORIG = MODE >= 1, GST = MODE == 2;
   const uint32_t lane = threadIdx.x;
   const uint32_t D = ORIG ? I : p.I.src[I];
   const uint32_t bound = ORIG ? NONE : p.I.bound[I];
@@ -268,6 +284,8 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
   // while this one replays (the loads do not depend on the slot state)
   uint32_t nx_i = ob + lane < oe ? p.olist[ob + lane] : NONE;
   unsigned long long nx_w = ob + lane < oe ? p.opw[ob + lane] : 0ULL;
+  constexpr bool gst = GST;
+  uint32_t g_adds = 0, g_fail = 0, g_first = NONE;  // (guard-G statistics)
   for (uint32_t k0 = ob; k0 < oe && !done; k0 += 64) {
     const uint32_t my_i = nx_i;
     const unsigned long long my_w = nx_w;
@@ -311,6 +329,7 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
           PDR_STAT(4);
           uint32_t node = an, nk = an;  // findInsertion
           uint32_t wn = ld_uniform(S, node);
+          bool gfail = false;  // a Tombstone above x met by the walk (guard G)
           for (;;) {
             const uint32_t rn = wn & PM;
             if (rn == PM) break;
@@ -330,9 +349,12 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
               const unsigned long long vb = __ballot(in && (a & SF_MADE) && !(a & SF_TOMB));
               const uint32_t m = lb == ~0ULL ? 64u : static_cast<uint32_t>(__builtin_ctzll(~lb));  // >= 1
               const uint32_t M = m < 63u ? m : 63u;  // ranks node..node+M are chained
-              const unsigned long long vis = vb & ((M == 63u ? ~0ULL : ((2ULL << M) - 1ULL)) & ~1ULL);
+              const unsigned long long chained = (M == 63u ? ~0ULL : ((2ULL << M) - 1ULL)) & ~1ULL;
+              const unsigned long long vis = vb & chained;
               if (vis) {
                 const uint32_t vs = 63u - static_cast<uint32_t>(__builtin_clzll(vis));
+                if constexpr (GST)
+                  if (chained & ~vb & ((2ULL << vs) - 1ULL)) gfail = true;  // crossed a Tombstone (above x)
                 const unsigned long long rest = (vis & ~(1ULL << vs)) | 1ULL;
                 nk = node + (63u - static_cast<uint32_t>(__builtin_clzll(rest))) + 1u;
                 wn = __builtin_amdgcn_readlane(a, vs);
@@ -340,6 +362,7 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
                 continue;
               }
               // ranks node+1..node+M are tombstones: the next live entry lies past them
+              if constexpr (GST) gfail = true;  // (all above x: crossed, or passed over by the stop)
               uint32_t p = __builtin_amdgcn_readlane(a, M) & PM;
               uint32_t wl = p == PM ? 0u : ld_uniform(S, p);
               p = pdr_next_live(S, K, lane, p, wl STC_ARG);
@@ -350,12 +373,21 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
               continue;
             }
             uint32_t wl = ld_uniform(S, rn);
+            if constexpr (GST)
+              if ((wl & SF_TOMB) && x < rn) gfail = true;  // a Tombstone above x: crossed or stopped before
             const uint32_t live = pdr_next_live(S, K, lane, rn, wl STC_ARG);
             if (live == PM) break;
             if (x > rn) break;  // ts > key(rn)
             nk = rn;
             node = live;
             wn = wl;
+          }
+          if (gst) {
+            ++g_adds;
+            if (gfail) {
+              ++g_fail;
+              g_first = min(g_first, k0 + j);
+            }
           }
           const uint32_t wk = nk == node ? wn : ld_uniform(S, nk);
           S[x] = (wn & PM) | (wk & SF_ORPHAN) | SF_MADE;
@@ -407,6 +439,7 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
            p.rbase[D + 1] - p.rbase[D], g_stc[4], g_stc[0], g_stc[1], g_stc[2], g_stc[3], clock64() - t_start);
 #endif
   if (ORIG && lane == 0) p.logn[D] = (logging && ln <= lcap) ? ln : NONE;
+  if (gst && lane == 0) pdr_gstat_flush(p, g_adds, g_fail, (g_first == NONE ? oe : g_first) - ob);
   __syncthreads();
   if (S != p.S + base) {
     for (uint32_t r = lane; r <= K; r += 64) p.S[base + r] = S[r];
@@ -414,22 +447,22 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
   for (uint32_t r = lane; r <= K; r += 64) p.inst[base + r] = I;
 }
 
-template <bool ORIG>
+template <int MODE>
 __global__ void __launch_bounds__(64) k_pdr_small(PdrCtx p, const uint32_t* list, uint8_t* st) {
   __shared__ uint32_t S[PDR_SMALL];
-  pdr_serial<ORIG>(p, st, list[blockIdx.x], S);
+  pdr_serial<MODE>(p, st, list[blockIdx.x], S);
 }
 
-template <bool ORIG>
+template <int MODE>
 __global__ void __launch_bounds__(64) k_pdr_big(PdrCtx p, const uint32_t* list, uint8_t* st) {
   extern __shared__ uint32_t S_dyn[];
-  pdr_serial<ORIG>(p, st, list[blockIdx.x], S_dyn);
+  pdr_serial<MODE>(p, st, list[blockIdx.x], S_dyn);
 }
 
-template <bool ORIG>
+template <int MODE>
 __global__ void __launch_bounds__(64) k_pdr_huge(PdrCtx p, const uint32_t* list, uint8_t* st) {
   const uint32_t I = list[blockIdx.x];
-  pdr_serial<ORIG>(p, st, I, p.S + p.I.base[I]);
+  pdr_serial<MODE>(p, st, I, p.S + p.I.base[I]);
 }
 
 // ---- P2b: the same replay over a blocked chain order (big dicts) ----
@@ -465,8 +498,9 @@ __device__ __forceinline__ uint32_t wf_sflags(uint32_t w) {  // the slot-word fl
          ((w & WF_COPY) ? SF_COPY : 0u);
 }
 
-template <bool ORIG>
+template <int MODE>
 __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* lds, uint32_t lds_words) {
+  constexpr bool ORIG = MODE >= 1, GST = MODE == 2;
   const uint32_t lane = threadIdx.x;
   const uint32_t D = ORIG ? I : p.I.src[I];
   const uint32_t bound = ORIG ? NONE : p.I.bound[I];
@@ -639,6 +673,8 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
   };
   uint32_t nx_i = ob + lane < oe ? p.olist[ob + lane] : NONE;
   unsigned long long nx_w = ob + lane < oe ? p.opw[ob + lane] : 0ULL;
+  constexpr bool gst = GST;
+  uint32_t g_adds = 0, g_fail = 0, g_first = NONE;  // (guard-G statistics, as in pdr_serial)
   for (uint32_t k0 = ob; k0 < oe && !done; k0 += 64) {
     const uint32_t my_i = nx_i;
     const unsigned long long my_w = nx_w;
@@ -703,6 +739,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
           bool at_anchor = true;    // no node visited yet
           uint32_t node, nk, nxt;   // result (nxt: the rank after node, PM = none)
           uint32_t cur_b = b, cur_e = e, cur_cnt = cnt, cur_nxb = nxb, node_i = i0;  // node's block (when loaded)
+          bool gfail = false;  // a Tombstone above x met by the walk (guard G)
           for (;;) {
             const bool valid = lane >= s0 && lane < cnt;
             const unsigned long long ml = __ballot(valid && !(e & BE_T));
@@ -734,6 +771,12 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
             }
             if (j >= 0) {
               const uint32_t uj = static_cast<uint32_t>(j);
+              // compare entries passed before the stop are above x; the stop
+              // entry is above x only when nothing live follows it
+              if constexpr (GST) {
+                const unsigned long long mtomb = mval & ~ml;
+                if ((mc & mtomb & ((1ULL << uj) - 1ULL)) || (((mtomb & ~mkey) >> uj) & 1ULL)) gfail = true;
+              }
               nxt = rk(e, uj);
               if (uj == s0) {  // node = the entry before the window
                 node = prev_r;
@@ -759,6 +802,8 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
               }
               break;
             }
+            if constexpr (GST)
+              if (mc & mval & ~ml) gfail = true;  // (no stop in this block: every compare entry passed)
             if (mc) nkc = rk(e, 63u - static_cast<uint32_t>(__builtin_clzll(mc)));
             if (cnt > s0) {
               carry = (ml >> (cnt - 1)) & 1ULL;
@@ -783,6 +828,13 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
             b = nxb;
             s0 = 0;
             e = load_blk(b, cnt, nxb);
+          }
+          if (gst) {
+            ++g_adds;
+            if (gfail) {
+              ++g_fail;
+              g_first = min(g_first, k0 + jo);
+            }
           }
           // ---- the two inserts (src/Internal/Node.elm:87-89) ----
           const uint32_t wx = nxt | SF_MADE;
@@ -835,16 +887,26 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
           // ---- an orphan anchor: pdr_serial's walk over the slot words ----
           uint32_t node = an, nk = an;
           uint32_t wn = ld_uniform(S, node);
+          bool gfail = false;
           for (;;) {
             const uint32_t rn = wn & PM;
             if (rn == PM) break;
             uint32_t wl = ld_uniform(S, rn);
+            if constexpr (GST)
+              if ((wl & SF_TOMB) && x < rn) gfail = true;
             const uint32_t live = pdr_next_live(S, K, lane, rn, wl STC_ARG);
             if (live == PM) break;
             if (x > rn) break;
             nk = rn;
             node = live;
             wn = wl;
+          }
+          if (gst) {
+            ++g_adds;
+            if (gfail) {
+              ++g_fail;
+              g_first = min(g_first, k0 + jo);
+            }
           }
           const uint32_t wk = nk == node ? wn : ld_uniform(S, nk);
           const bool on_chain = !(wk & SF_ORPHAN);
@@ -898,13 +960,14 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
     }
   }
   if (ORIG && lane == 0) p.logn[D] = (logging && ln <= lcap) ? ln : NONE;
+  if (gst && lane == 0) pdr_gstat_flush(p, g_adds, g_fail, (g_first == NONE ? oe : g_first) - ob);
   for (uint32_t r = lane; r <= K; r += 64) p.inst[base + r] = I;
 }
 
-template <bool ORIG>
+template <int MODE>
 __global__ void __launch_bounds__(64) k_pdr_blk(PdrCtx p, const uint32_t* list, uint8_t* st, uint32_t lds_words) {
   extern __shared__ uint32_t blk_lds[];
-  pdr_blocked<ORIG>(p, st, list[blockIdx.x], blk_lds, lds_words);
+  pdr_blocked<MODE>(p, st, list[blockIdx.x], blk_lds, lds_words);
 }
 
 // Sort instances [i0, i1) into three size tiers: static LDS, dynamic LDS,
@@ -1266,21 +1329,25 @@ static int pdr_run_tiers(crdtm_ctx* c, const PdrCtx& p, uint32_t i0, uint32_t i1
   }
   if (h[3]) {
     const size_t lds = static_cast<size_t>(big_cap) * sizeof(uint32_t);  // the whole LDS: one wave per CU
-    if (orig) LAUNCH(k_pdr_blk<true>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st, big_cap);
-    else LAUNCH(k_pdr_blk<false>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st, big_cap);
+    if (orig && p.gcount) LAUNCH(k_pdr_blk<2>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st, big_cap);
+    else if (orig) LAUNCH(k_pdr_blk<1>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st, big_cap);
+    else LAUNCH(k_pdr_blk<0>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st, big_cap);
   }
   if (h[0]) {
-    if (orig) LAUNCH(k_pdr_small<true>, dim3(h[0]), dim3(64), 0, s2, p, tt.list[0], st);
-    else LAUNCH(k_pdr_small<false>, dim3(h[0]), dim3(64), 0, s2, p, tt.list[0], st);
+    if (orig && p.gcount) LAUNCH(k_pdr_small<2>, dim3(h[0]), dim3(64), 0, s2, p, tt.list[0], st);
+    else if (orig) LAUNCH(k_pdr_small<1>, dim3(h[0]), dim3(64), 0, s2, p, tt.list[0], st);
+    else LAUNCH(k_pdr_small<0>, dim3(h[0]), dim3(64), 0, s2, p, tt.list[0], st);
   }
   if (h[1]) {
     const size_t lds = static_cast<size_t>(h[4]) * sizeof(uint32_t);
-    if (orig) LAUNCH(k_pdr_big<true>, dim3(h[1]), dim3(64), lds, s2, p, tt.list[1], st);
-    else LAUNCH(k_pdr_big<false>, dim3(h[1]), dim3(64), lds, s2, p, tt.list[1], st);
+    if (orig && p.gcount) LAUNCH(k_pdr_big<2>, dim3(h[1]), dim3(64), lds, s2, p, tt.list[1], st);
+    else if (orig) LAUNCH(k_pdr_big<1>, dim3(h[1]), dim3(64), lds, s2, p, tt.list[1], st);
+    else LAUNCH(k_pdr_big<0>, dim3(h[1]), dim3(64), lds, s2, p, tt.list[1], st);
   }
   if (h[2]) {
-    if (orig) LAUNCH(k_pdr_huge<true>, dim3(h[2]), dim3(64), 0, s2, p, tt.list[2], st);
-    else LAUNCH(k_pdr_huge<false>, dim3(h[2]), dim3(64), 0, s2, p, tt.list[2], st);
+    if (orig && p.gcount) LAUNCH(k_pdr_huge<2>, dim3(h[2]), dim3(64), 0, s2, p, tt.list[2], st);
+    else if (orig) LAUNCH(k_pdr_huge<1>, dim3(h[2]), dim3(64), 0, s2, p, tt.list[2], st);
+    else LAUNCH(k_pdr_huge<0>, dim3(h[2]), dim3(64), 0, s2, p, tt.list[2], st);
   }
   if (fork) {
     HIP_CHECK(hipEventRecord(c->ev_join, s2));
@@ -1296,14 +1363,12 @@ static uint32_t pdr_big_cap(int device) {
     int v = 0;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess || v <= 0)
       v = 64 * 1024;
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pdr_big<true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, v) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pdr_big<false>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, v) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pdr_blk<true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, v) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pdr_blk<false>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, v) != hipSuccess)
+    const void* fns[] = {reinterpret_cast<const void*>(&k_pdr_big<0>), reinterpret_cast<const void*>(&k_pdr_big<1>),
+                         reinterpret_cast<const void*>(&k_pdr_big<2>), reinterpret_cast<const void*>(&k_pdr_blk<0>),
+                         reinterpret_cast<const void*>(&k_pdr_blk<1>), reinterpret_cast<const void*>(&k_pdr_blk<2>)};
+    bool ok = true;
+    for (const void* f : fns) ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, v) == hipSuccess;
+    if (!ok)
       v = 64 * 1024;
     cached = v;
   }
@@ -1415,6 +1480,12 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
     HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(pdr_stat_on), &f, sizeof(f)));
   }
 #endif
+  p.gcount = nullptr;  // guard-G statistics (untimed measurement runs only)
+  if (const char* e = getenv("CRDTM_GUARD_STATS"); e && e[0] == '1') {
+    if (!c->gstat_dev) HIP_CHECK(hipMalloc(&c->gstat_dev, 4 * sizeof(unsigned long long)));
+    HIP_CHECK(hipMemsetAsync(c->gstat_dev, 0, 4 * sizeof(unsigned long long), s));
+    p.gcount = c->gstat_dev;
+  }
   if ((r = pdr_run_tiers(c, p, 0, n + 1, true, st, tt, big_cap, hcount))) return r;
 #ifdef PDR_STATS
   {
@@ -1438,6 +1509,13 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   if (h1.pdr_conflict || replica_of(new_ts) != replica_of(t->timestamp)) {
     ws.used = arena_mark;
     return CRDTM_OK;
+  }
+  if (p.gcount) {  // (only a replay that serves the batch reports)
+    unsigned long long gh[4];
+    HIP_CHECK(hipMemcpy(gh, c->gstat_dev, sizeof(gh), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 3; ++k) c->gstat[k] = gh[k];
+    c->gstat[3] = n;
+    c->gstat_valid = 1;
   }
   *handled = true;
   res->path_taken = CRDTM_PATH_DICT_REPLAY;

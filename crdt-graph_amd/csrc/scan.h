@@ -139,6 +139,7 @@ __global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* out, uint64_
   }
   __syncthreads();
   uint32_t run = OP::op(s_prefix, texcl);
+  const uint32_t start = run;
 #pragma unroll
   for (int j = 0; j < DS_ITEMS; ++j) {
     const uint32_t x = v[j];
@@ -150,6 +151,9 @@ __global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* out, uint64_
       run = OP::op(run, x);
     }
   }
+  // a generator may consume the scanned values of its own items (items b ..
+  // b + DS_ITEMS, `start` = the prefix before them) before they are stored
+  if constexpr (GEN::kEpilogue) gen.epilogue(b, n, v, start);
   if (full && (reinterpret_cast<uintptr_t>(out + tb) & 15) == 0) {
     // (every lane finished reading sx: the look-back's __syncthreads lie between)
 #pragma unroll
@@ -178,6 +182,7 @@ struct SumOp {
 
 struct ArrGen {
   static constexpr bool kStriped = true;  // k_dscan may load full tiles lane-contiguously
+  static constexpr bool kEpilogue = false;
   const uint32_t* in;
   __device__ __forceinline__ bool aligned(uint64_t b) const { return (reinterpret_cast<uintptr_t>(in + b) & 15) == 0; }
   __device__ __forceinline__ uint4 load4(uint64_t b) const { return *reinterpret_cast<const uint4*>(in + b); }

@@ -241,6 +241,18 @@ int crdtm_json_encode(const crdtm_ops *ops, int is_batch, const char *val_bytes,
 int crdtm_json_canonical(const char *text, size_t len, char **out, size_t *out_len);
 void crdtm_free(void *p);
 
+/* ---- guard G on the per-dict replay: measured when the
+ * environment variable CRDTM_GUARD_STATS=1 is set during crdtm_apply (an
+ * untimed measurement run; it adds a few instructions per replayed Add).
+ * An Add fails guard G when its findInsertion walk (src/Internal/Node.elm:
+ * 93-104) meets a Tombstone whose key is above the Add's timestamp: a node
+ * canonical RGA would pass, deleted before the Add; a dict's first such Add
+ * ends the prefix a closed form could serve exactly. out[0] Adds that walked,
+ * out[1] G-failing Adds, out[2] ops of the replayed dicts before each dict's
+ * first G-failing Add, out[3] ops replayed. Returns 1 when the last apply of
+ * this context collected them, else 0 (out zeroed). */
+int crdtm_ctx_guard_stats(crdtm_ctx *ctx, uint64_t *out);
+
 /* ---- profiling: per-kernel device time of the last apply (HIP events) ---- */
 /* Returns the number of named phases; fills names (NUL-separated) and ms. */
 int crdtm_ctx_profile(crdtm_ctx *ctx, int enable);

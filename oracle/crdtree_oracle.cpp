@@ -78,15 +78,32 @@ Node* nextNode(Node* node, Dict& c) {
   }
 }
 
+// Guard G statistics of the last orc_apply (test infrastructure; the
+// definition the engine's per-dict replay measures, include/crdtm.h
+// crdtm_ctx_guard_stats): Adds whose findInsertion walk ran, and those whose
+// walk met a Tombstone above their timestamp as a raw `next` key.
+struct GStats {
+  uint64_t walked = 0, fail = 0;
+};
+thread_local GStats g_gstats;
+
 // findInsertion (src/Internal/Node.elm:93-104). Returns (leftKey, leftNode);
 // after a tombstone skip leftKey != key(leftNode) (Appendix A.5).
 std::pair<int64_t, Node*> findInsertion(int64_t ts, int64_t n, Node* node, Dict& c) {
+  ++g_gstats.walked;
+  bool gfail = false;
+  auto done = [&](std::pair<int64_t, Node*> r) {
+    if (gfail) ++g_gstats.fail;
+    return r;
+  };
   for (;;) {
-    if (node->kind == ROOT || !node->has_next) return {n, node};
-    Node* live = nextNode(node, c);
-    if (!live) return {n, node};
+    if (node->kind == ROOT || !node->has_next) return done({n, node});
     const int64_t k = node->next;
-    if (ts > k) return {n, node};
+    auto it = c.find(k);
+    if (it != c.end() && it->second.kind == TOMB && ts < k) gfail = true;  // (statistics only)
+    Node* live = nextNode(node, c);
+    if (!live) return done({n, node});
+    if (ts > k) return done({n, node});
     n = k;
     node = live;
   }
@@ -391,10 +408,18 @@ int orc_apply(orc_tree* o, int is_batch, int local, uint64_t n_ops, const uint8_
   }
   Tree work = o->t;  // Elm: the caller still holds the old tree on Err
   work.err_index = -1;
+  g_gstats = GStats{};
   int r = local ? applyLocal(top, work) : apply(top, work);
   if (err_index) *err_index = work.err_index;
   if (r == T_OK) o->t = std::move(work);
   return r;
+}
+
+// guard G statistics of the last orc_apply: out[0] Adds whose findInsertion
+// walk ran, out[1] those that met a Tombstone above their timestamp
+void orc_guard_stats(uint64_t* out) {
+  out[0] = g_gstats.walked;
+  out[1] = g_gstats.fail;
 }
 
 int64_t orc_timestamp(const orc_tree* o) { return o->t.timestamp; }

@@ -45,6 +45,8 @@ def lib():
         L.orc_apply.argtypes = [P, C.c_int, C.c_int, C.c_uint64, P, P, P, P, P, C.POINTER(C.c_int64)]
         L.orc_timestamp.restype = C.c_int64
         L.orc_timestamp.argtypes = [P]
+        L.orc_guard_stats.restype = None
+        L.orc_guard_stats.argtypes = [P]
         L.orc_cursor.restype = C.c_uint64
         L.orc_cursor.argtypes = [P, P, C.c_uint64]
         L.orc_set_cursor.argtypes = [P, P, C.c_uint64]

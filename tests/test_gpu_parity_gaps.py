@@ -192,3 +192,41 @@ def test_out_of_range_keys_rejected(where):
     ot, rc, _ = oracle_apply_arrays(ok, m)
     assert et.apply_arrays(ok, m).code == rc == 0
     assert engine_summary(et) == oracle_summary(ot)
+
+
+@pytest.mark.parametrize("blocked", [False, True])
+def test_guard_g_statistics_match_oracle(monkeypatch, blocked):
+    """Guard G per Add, measured inside the per-dict
+    replay (CRDTM_GUARD_STATS=1, crdtm_ctx_guard_stats): the Adds whose
+    findInsertion walk ran and those whose walk met a Tombstone above their
+    timestamp, against the oracle's count over the same sequential apply
+    (orc_guard_stats) — both replay tiers (one-lane walk, blocked chain order)."""
+    from adversarial import adversarial
+    from crdtm.tree import pack
+    from oracle.oracle import lib as olib
+    monkeypatch.setenv("CRDTM_GUARD_STATS", "1")
+    if blocked:
+        monkeypatch.setenv("CRDTM_PDR_BLK_MIN", "1")
+    streams = [N.synth(n_ops=20000, replicas=16, window=64, p_delete=0.2, p_branch=0.1, max_depth=4, seed=0xC0FFEE02),
+               N.synth(n_ops=10000, replicas=2, window=8, p_delete=0.3, p_branch=0.05, max_depth=3, seed=0xC0FFEE01)]
+    streams += [pack(adversarial(seed, [400, 1500][seed % 2], replicas=2 + seed % 3, max_depth=1 + seed % 4))
+                for seed in range(8)]
+    checked = 0
+    for s in streams:
+        n = len(s["path_off"]) - 1  # (pack() pads its per-op arrays by one)
+        ot, rc, _ = oracle_apply_arrays(s, n)
+        want = np.zeros(2, np.uint64)
+        olib().orc_guard_stats(want.ctypes.data_as(C.c_void_p))
+        et = CRDTree.init(0)
+        res = et.apply_arrays(s, n)
+        got = np.zeros(4, np.uint64)
+        ok = N.lib().crdtm_ctx_guard_stats(N.context(0), got.ctypes.data_as(C.c_void_p))
+        assert res.code == rc
+        if rc != 0 or res.path_taken != N.PATH_DICT_REPLAY:
+            assert ok == 0  # (only a per-dict replay that serves the batch reports)
+            continue
+        assert ok == 1
+        assert (int(got[0]), int(got[1])) == (int(want[0]), int(want[1]))
+        assert int(got[2]) <= int(got[3]) == n
+        checked += 1
+    assert checked >= 4

@@ -322,3 +322,27 @@ def test_flat_fast_restatement_matches_general(seed):
     assert L.orc_flat_check(len(keys), _ptr(keys), m, *chk) == 0
     keys[100], keys[101] = keys[101], keys[100]
     assert L.orc_flat_check(len(keys), _ptr(keys), m, *chk) > 0
+
+
+def test_guard_g_statistics_hand_traced():
+    """Guard G as the oracle counts it: an Add fails when
+    its findInsertion walk meets a Tombstone above its timestamp as a raw
+    `next` key. Appendix C.1: Add 15 after 10 meets Tombstone 20 > 15 (the
+    copy quirk fires); C.2 (the Deletes last): no Add fails; a Tombstone below
+    the Add's timestamp stops the walk without failing it."""
+    import ctypes as C
+    import numpy as np
+    from oracle.oracle import lib
+
+    def stats(ops):
+        t = OTree(0)
+        assert t.apply(Batch(ops))[0] == "Ok"
+        out = np.zeros(2, np.uint64)
+        lib().orc_guard_stats(out.ctypes.data_as(C.c_void_p))
+        return tuple(int(x) for x in out)
+
+    adds = [Add(10, [0], "a"), Add(20, [10], "b"), Add(30, [20], "c")]
+    assert stats(adds + [Delete([20]), Add(15, [10], "d")]) == (4, 1)
+    assert stats(adds + [Add(15, [10], "d"), Delete([20]), Delete([30])]) == (4, 0)
+    # a Tombstone below the Add: 40 after 10 stops at Tombstone 20 < 40
+    assert stats(adds + [Delete([20]), Add(40, [10], "d")]) == (4, 0)
