@@ -2459,47 +2459,6 @@ __global__ void __launch_bounds__(BLOCK) k_fl_present(uint32_t Q, const uint32_t
   GRID_STRIDE(q, Q) f[q] = anc[q] != ABSENT ? 1u : 0u;
 }
 
-// Node records in slot order. The key is recomputed from the slot: the
-// replica r with base[r] <= q (largest such r) and counter min[r] + q -
-// base[r] (tables in LDS when the replica ids fit, else the op's ts).
-__global__ void __launch_bounds__(BLOCK) k_fl_commit(OpsDev o, TsIndex x, uint32_t Q, uint32_t nrep,
-                                                     const uint32_t* anc, const unsigned long long* rec,
-                                                     const uint32_t* qc, const uint32_t* logidx, TreeDev T) {
-  extern __shared__ uint32_t sbc[];  // dynamic: 2 * nrep words when the tables fit (HOST_RANGES)
-  uint32_t* sb = sbc;
-  uint32_t* sc = sbc + nrep;
-  const bool lds = nrep <= HOST_RANGES;
-  if (lds) {
-    for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x) {
-      sb[j] = x.base[j];
-      sc[j] = x.rng[j].x;
-    }
-  }
-  __syncthreads();
-  GRID_STRIDE(q, Q) {
-    if (anc[q] == ABSENT) continue;
-    const uint32_t slot = 1 + (qc ? qc[q] : q);
-    const uint32_t i = static_cast<uint32_t>(rec[q] >> 32);
-    long long key;
-    if (lds) {
-      uint32_t lo = 0, hi = nrep;  // largest r with sb[r] <= q
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (sb[mid] <= q) lo = mid;
-        else hi = mid;
-      }
-      key = (static_cast<long long>(lo) << 32) | static_cast<long long>(sc[lo] + (q - sb[lo]));
-    } else {
-      key = o.ts[i];
-    }
-    T.s_key[slot] = key;
-    T.s_dict[slot] = 0;
-    T.s_src[slot] = logidx ? logidx[i] : i;
-    T.s_flags[slot] = 0;
-    T.s_child[slot] = NONE;
-  }
-}
-
 // Log append into a fresh tree when every op applied: the log is the batch
 // itself (same CSR layout, path elements [0, n_path)).
 __global__ void __launch_bounds__(BLOCK) k_fl_log_copy(OpsDev o, TreeDev T) {
@@ -2740,16 +2699,35 @@ __global__ void __launch_bounds__(BLOCK) k_run_pos(RunArr a, DevResult* dres) {
   }
 }
 
-// doc[rank] = tree slot, per slot: rank = the head's rank + the slots of the
-// run before q + the subtrees of the run's child runs attached at slots below
-// q (child runs at q itself follow q). The child runs of the run are
-// contiguous in the sorted list with ascending attach slots: a binary search
-// finds the first one at or above q (most runs have none).
+// Per slot, the document order and the commit in one pass over slot order:
+// doc[rank] = tree slot, where rank = the head's rank + the slots of the run
+// before q + the subtrees of the run's child runs attached at slots below q
+// (child runs at q itself follow q; the run's child runs are contiguous in
+// the sorted list with ascending attach slots: a binary search finds the
+// first one at or above q, most runs have none); and the node record of tree
+// slot 1 + q (compacted: slot order = timestamp order), the key recomputed
+// from the slot (the replica r with base[r] <= q, largest such r, and
+// counter min[r] + q - base[r]; tables in LDS when the replica ids fit, else
+// the op's ts), its children dict implicit.
 __global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint32_t K, const uint32_t* anc,
                                                       const uint32_t* rid, const uint32_t* pk, const uint32_t* xs,
-                                                      const uint32_t* tk, const uint32_t* qc, uint32_t* doc) {
+                                                      const uint32_t* tk, const uint32_t* qc, uint32_t* doc, OpsDev o,
+                                                      TsIndex x, uint32_t nrep, const unsigned long long* rec,
+                                                      const uint32_t* logidx, TreeDev T) {
+  extern __shared__ uint32_t sbc[];  // dynamic: 2 * nrep words when the tables fit (HOST_RANGES)
+  uint32_t* sb = sbc;
+  uint32_t* sc = sbc + nrep;
+  const bool lds = nrep <= HOST_RANGES;
+  if (lds) {
+    for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x) {
+      sb[j] = x.base[j];
+      sc[j] = x.rng[j].x;
+    }
+  }
+  __syncthreads();
   GRID_STRIDE(q, Q) {
     if (anc[q] == ABSENT) continue;
+    const uint32_t slot = 1 + (qc ? qc[q] : q);
     const uint32_t r = rid[q] - 1;
     uint32_t p = a.posh[r] + (q - a.heads[r]);
     const uint32_t ne = a.nch[r];
@@ -2763,7 +2741,25 @@ __global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint
       }
       if (lo > e0) p += xs[lo - 1] + tk[lo - 1] - xs[e0];
     }
-    if (p < K) doc[p] = 1 + (qc ? qc[q] : q);  // (a rank past K: a speculation that fails)
+    if (p < K) doc[p] = slot;  // (a rank past K: a speculation that fails)
+    const uint32_t i = static_cast<uint32_t>(rec[q] >> 32);
+    long long key;
+    if (lds) {
+      uint32_t lo = 0, hi = nrep;  // largest r with sb[r] <= q
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sb[mid] <= q) lo = mid;
+        else hi = mid;
+      }
+      key = (static_cast<long long>(lo) << 32) | static_cast<long long>(sc[lo] + (q - sb[lo]));
+    } else {
+      key = o.ts[i];
+    }
+    T.s_key[slot] = key;
+    T.s_dict[slot] = 0;
+    T.s_src[slot] = logidx ? logidx[i] : i;
+    T.s_flags[slot] = 0;
+    T.s_child[slot] = NONE;
   }
 }
 
@@ -3163,8 +3159,6 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     if ((r = dscan<SumOp, false>(ArrGen{tk}, xs, Q, nullptr, ws, s, nullptr, ra.nR, "k_dscan_xs"))) return r;
     LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, gstart);
     LAUNCH(k_run_pos, dim3(gr), dim3(BLOCK), 0, s, ra, dr);
-    LAUNCH(k_run_expand, dim3(gq), dim3(BLOCK), 0, s, ra, Q, K, anc, rid, pk, xs, tk, qc, t->d.doc);
-    LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d, t->cap.slots);
     uint32_t* logidx = nullptr;
     if (!all_applied) {  // compacted log (its scans share the ctx scan pool: main stream)
       logidx = ws.alloc<uint32_t>(n + 1);
@@ -3175,10 +3169,11 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
       LAUNCH(k_log, dim3(g), dim3(BLOCK), 0, s, o, st, t->d, 0u, 0u, logidx, plen);
       LAUNCH(k_log_tail, dim3(1), dim3(1), 0, s, t->d, 0u, &dr->log_n, 0u, &dr->log_npath);
     }
-    // ---- commit ----
-    LAUNCH(k_fl_commit, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK),
-           maxr + 1 <= HOST_RANGES ? 2 * (maxr + 1) * sizeof(uint32_t) : 0, s, o, ix, Q, maxr + 1, anc, rec, qc,
-           logidx, t->d);
+    // ---- the document order and the commit (one pass), the chain ----
+    LAUNCH(k_run_expand, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK),
+           maxr + 1 <= HOST_RANGES ? 2 * (maxr + 1) * sizeof(uint32_t) : 0, s, ra, Q, K, anc, rid, pk, xs, tk, qc,
+           t->d.doc, o, ix, maxr + 1, rec, logidx, t->d);
+    LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d, t->cap.slots);
     if (all_applied && !log_done) LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
   } else if (all_applied && !log_done) {
     LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
