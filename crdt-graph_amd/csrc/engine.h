@@ -197,8 +197,7 @@ int segmented_sort_asc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* c
                           hipStream_t st, DevResult* dres);
 // stable LSD radix sort of (key, value) pairs by the low `bits` key bits (primitives.hip)
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, const uint32_t* n_dev, uint32_t n_max,
-                     uint32_t bits, Arena& ws, hipStream_t st, uint32_t** out_k, uint32_t** out_v,
-                     uint32_t** hist_out = nullptr, uint32_t* ntiles_out = nullptr);
+                     uint32_t bits, Arena& ws, hipStream_t st, uint32_t** out_k, uint32_t** out_v);
 // ent[e] = {succ, wbits}: see primitives.hip / listrank.h (list_rank_fused)
 int list_rank(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws, hipStream_t st);
 int list_rank_packed(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws,

@@ -1964,16 +1964,22 @@ constexpr unsigned long long REC_EMPTY = ~0ULL;
 // index per replica (replicas table), the own-replica Add count
 // (incrementTimestamp), the Adds with a slot, and the ops that would not
 // apply on their own (empty path: InvalidPath, its smallest index to
-// err_index; ts 0: the sentinel's key, AlreadyApplied). k_fl_check then
-// checks every slot's Add against its anchor and counts the slots: as many
-// slots as keyed Adds means no duplicate timestamps. Only a batch where some
-// op does not apply runs the per-op k_fl_status.
-// track_rep = 0: k_fl_check folds the replicas table from the records instead
-// (slot order: a thread's slots stay inside one replica's range, no per-op
-// LDS atomics).
+// err_index; ts 0: the sentinel's key, AlreadyApplied). The order's slot
+// pass (k_run_expand with `chk`) then checks every slot's Add against its
+// anchor and counts the slots: as many slots as keyed Adds means no duplicate
+// timestamps. Only a batch where some op does not apply runs the per-op
+// k_fl_status.
+// track_rep = 0: k_run_expand folds the replicas table from the records
+// instead (slot order: a wave's slots stay inside one replica's range, no
+// per-op LDS atomics).
 // log_to_tree: the flat speculation (fresh tree, every op applies) also
 // appends the batch to the log here (it IS the log: same CSR layout, path
 // elements [0, n_path)), so the ops stream from HBM once for both.
+// SIMPLE: every op is an Add with a one-element path (k_pre: no Delete, the
+// longest path 1 and as many path elements as ops), so op i's anchor is
+// path[i]: the pass reads the timestamps, anchors (and values for the log) as
+// 16-byte vectors and writes the log's kinds and offsets without reading them.
+template <bool SIMPLE>
 __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_t Q, unsigned long long* rec,
                                                     long long ts0, uint32_t* rtab, DevResult* dres,
                                                     uint32_t track_rep, uint32_t nrep, TreeDev T,
@@ -2007,15 +2013,42 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
   uint32_t keys = 0, own = 0, slow = 0, err = NONE, mr = 0, bad = 0;
   QUAD_LOOP_XCD(i0, o.n) {
     Quad qd;
-    load_quad(o, i0, qd);
     long long pk[4];  // the path element of each op (flat: |path| <= 1)
+    if (SIMPLE) {
+      if (i0 + 4 <= o.n) {
+        qd.cnt = 4;
+        const longlong2 a = *reinterpret_cast<const longlong2*>(o.ts + i0);
+        const longlong2 b = *reinterpret_cast<const longlong2*>(o.ts + i0 + 2);
+        const longlong2 c = *reinterpret_cast<const longlong2*>(o.path + i0);
+        const longlong2 d = *reinterpret_cast<const longlong2*>(o.path + i0 + 2);
+        qd.ts[0] = a.x; qd.ts[1] = a.y; qd.ts[2] = b.x; qd.ts[3] = b.y;
+        pk[0] = c.x; pk[1] = c.y; pk[2] = d.x; pk[3] = d.y;
+      } else {
+        qd.cnt = o.n - i0;
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) pk[k] = (k < qd.cnt && qd.off[k + 1] != qd.off[k]) ? o.path[qd.off[k]] : 0;
+        for (uint32_t k = 0; k < 4; ++k) {
+          qd.ts[k] = k < qd.cnt ? o.ts[i0 + k] : 0;
+          pk[k] = k < qd.cnt ? o.path[i0 + k] : 0;
+        }
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < 5; ++k) qd.off[k] = i0 + k;
+    } else {
+      load_quad(o, i0, qd);
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) pk[k] = (k < qd.cnt && qd.off[k + 1] != qd.off[k]) ? o.path[qd.off[k]] : 0;
+    }
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) bad |= (pk[k] >= TWO53 || pk[k] <= -TWO53) ? 1u : 0u;  // (|x| < 2^53)
     if (log_to_tree) {
       if (qd.cnt == 4) {
-        *reinterpret_cast<uchar4*>(T.l_kind + i0) = make_uchar4(qd.kind[0], qd.kind[1], qd.kind[2], qd.kind[3]);
+        if (SIMPLE) {
+          *reinterpret_cast<uchar4*>(T.l_kind + i0) = make_uchar4(CRDTM_ADD, CRDTM_ADD, CRDTM_ADD, CRDTM_ADD);
+          *reinterpret_cast<longlong2*>(T.l_path + i0) = make_longlong2(pk[0], pk[1]);
+          *reinterpret_cast<longlong2*>(T.l_path + i0 + 2) = make_longlong2(pk[2], pk[3]);
+        } else {
+          *reinterpret_cast<uchar4*>(T.l_kind + i0) = make_uchar4(qd.kind[0], qd.kind[1], qd.kind[2], qd.kind[3]);
+        }
         *reinterpret_cast<longlong2*>(T.l_ts + i0) = make_longlong2(qd.ts[0], qd.ts[1]);
         *reinterpret_cast<longlong2*>(T.l_ts + i0 + 2) = make_longlong2(qd.ts[2], qd.ts[3]);
         *reinterpret_cast<uint4*>(T.l_off + i0) = make_uint4(qd.off[0], qd.off[1], qd.off[2], qd.off[3]);
@@ -2024,23 +2057,26 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {  // (static indices: no scratch)
           if (k < qd.cnt) {
-            T.l_kind[i0 + k] = qd.kind[k];
+            T.l_kind[i0 + k] = SIMPLE ? static_cast<uint8_t>(CRDTM_ADD) : qd.kind[k];
             T.l_ts[i0 + k] = qd.ts[k];
             T.l_off[i0 + k] = qd.off[k];
             T.l_val[i0 + k] = o.val[i0 + k];
+            if (SIMPLE) T.l_path[i0 + k] = pk[k];
           }
         }
       }
-      if (i0 + qd.cnt == o.n) T.l_off[o.n] = o.off[o.n];
+      if (i0 + qd.cnt == o.n) T.l_off[o.n] = SIMPLE ? o.n : o.off[o.n];
+      if (!SIMPLE) {
 #pragma unroll
-      for (uint32_t k = 0; k < 4; ++k)
-        if (k < qd.cnt && qd.off[k + 1] != qd.off[k]) T.l_path[qd.off[k]] = pk[k];
+        for (uint32_t k = 0; k < 4; ++k)
+          if (k < qd.cnt && qd.off[k + 1] != qd.off[k]) T.l_path[qd.off[k]] = pk[k];
+      }
     }
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
       if (k >= qd.cnt) continue;
       const uint32_t i = i0 + k;
-      if (qd.off[k + 1] == qd.off[k]) {  // update [] = InvalidPath (src/Internal/Node.elm:147-148)
+      if (!SIMPLE && qd.off[k + 1] == qd.off[k]) {  // update [] = InvalidPath (src/Internal/Node.elm:147-148)
         ++slow;
         err = min(err, i);
         continue;
@@ -2214,17 +2250,16 @@ __global__ void __launch_bounds__(BLOCK) k_fl_rep_collect(OpsDev o, uint32_t nr,
 // whose every slot but h is anchored at the slot before it (a replica's
 // typing run: consecutive counters are consecutive slots); an absent slot is
 // a run of its own with no node (a "hole" run). Head flags are summed into
-// rid[q] = 1 + the index of q's run; the generator writes anc[q] (anchor slot
-// per slot, ABSENT = no node) as a side output and, from the scanned values,
-// every run's head slot and the anchor of its head (epilogue).
+// rid[q] = 1 + the index of q's run; from the scanned values the generator
+// writes every run's head slot and the anchor of its head (epilogue). (The
+// later kernels read a slot's presence and anchor from its record.)
 struct RunIdGen {
-  static constexpr bool kStriped = false;  // loads through load() (it writes anc as a side output)
+  static constexpr bool kStriped = false;  // loads through load() (8-byte records -> flags)
   static constexpr bool kEpilogue = true;
   __device__ __forceinline__ bool aligned(uint64_t) const { return false; }
   __device__ __forceinline__ uint4 load4(uint64_t) const { return make_uint4(0u, 0u, 0u, 0u); }
   const unsigned long long* rec;
   uint32_t Q;
-  uint32_t* anc;    // side output: anchor slot per slot (ABSENT = no node)
   uint32_t* heads;  // run -> head slot
   uint32_t* hanc;   // run -> anchor slot of its head (ABSENT: a hole run)
   // A missing anchor (NONE) only occurs in a batch that fails (NotFound),
@@ -2251,9 +2286,6 @@ struct RunIdGen {
         a[j + 1] = anchor(x.y);
       }
 #pragma unroll
-      for (int j = 0; j < DS_ITEMS; j += 4)
-        *reinterpret_cast<uint4*>(anc + b + j) = make_uint4(a[j], a[j + 1], a[j + 2], a[j + 3]);
-#pragma unroll
       for (int j = 0; j < DS_ITEMS; ++j) {
         v[j] = flag(q0 + j, a[j], aprev);
         aprev = a[j];
@@ -2262,11 +2294,7 @@ struct RunIdGen {
 #pragma unroll
       for (int j = 0; j < DS_ITEMS; ++j) {
         const uint64_t q = b + j;
-        uint32_t a = ABSENT;
-        if (q < n) {
-          a = anchor(rec[q]);
-          anc[q] = a;
-        }
+        const uint32_t a = q < n ? anchor(rec[q]) : ABSENT;
         v[j] = q < n ? flag(static_cast<uint32_t>(q), a, aprev) : 0u;
         aprev = a;
       }
@@ -2279,78 +2307,12 @@ struct RunIdGen {
       const uint64_t q = b + j;
       if (q < n && v[j] != prev) {  // a head: its run's index is v[j] - 1
         heads[v[j] - 1] = static_cast<uint32_t>(q);
-        hanc[v[j] - 1] = anc[q];  // (this thread's own store above)
+        hanc[v[j] - 1] = anchor(rec[q]);  // (a line this thread has just read)
       }
       prev = v[j];
     }
   }
 };
-
-// Per-slot check of k_fl_claim's records (addAfterHelp,
-// src/Internal/Node.elm:68-70): the Add of slot q applies iff its anchor is
-// the sentinel or a slot whose Add comes earlier in the batch, else it fails
-// (NotFound -> OperationFailed); the smallest failing index goes to
-// err_index. Counts the slots holding an Add (fl_part[0]).
-// With nrep > 0 (replica ids < nrep, base table in LDS) it also folds the
-// replicas table: every workgroup checks one contiguous slot chunk, so a
-// thread's slots run through few replica ranges; it keeps the largest op
-// index of the current replica in a register and touches LDS only when the
-// range changes (replicas[r] = the last applied Add of r, src/CRDTree.elm:313).
-__global__ void __launch_bounds__(BLOCK) k_fl_check(uint32_t Q, const unsigned long long* rec, DevResult* dres,
-                                                    const uint32_t* base, uint32_t nrep, uint32_t* rtab) {
-  extern __shared__ uint32_t sck[];  // [nrep] range bases, [nrep] largest index + 1
-  uint32_t* sb = sck;
-  uint32_t* rv = sck + nrep;
-  for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x) {
-    sb[j] = base[j];
-    rv[j] = 0;
-  }
-  __syncthreads();
-  uint32_t present = 0, err = NONE;
-  const uint32_t npair = (Q + 1) / 2;
-  const uint32_t chunk = (npair + gridDim.x - 1) / gridDim.x;
-  const uint32_t k0 = blockIdx.x * chunk, k1 = min(npair, k0 + chunk);
-  uint32_t cr = NONE, cmax = 0, rlo = 0, rhi = 0;  // current replica, its [lo, hi) slot range
-  for (uint32_t k = k0 + threadIdx.x; k < k1; k += blockDim.x) {
-    const bool pair = 2 * k + 1 < Q;
-    const ulonglong2 x = pair ? *reinterpret_cast<const ulonglong2*>(rec + 2 * k) : make_ulonglong2(rec[Q - 1], REC_EMPTY);
-    const unsigned long long r2[2] = {x.x, x.y};
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const unsigned long long r = r2[j];
-      if (r == REC_EMPTY) continue;
-      ++present;
-      const uint32_t fi = static_cast<uint32_t>(r >> 32), qa = static_cast<uint32_t>(r);
-      if (qa != Q && (qa == NONE || static_cast<uint32_t>(rec[qa] >> 32) >= fi)) err = min(err, fi);
-      if (nrep) {
-        const uint32_t q = 2 * k + j;
-        if (q < rlo || q >= rhi) {
-          if (cmax) atomicMax(&rv[cr], cmax);
-          uint32_t lo = 0, hi = nrep;  // largest replica whose range starts at or below q
-          while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (sb[mid] <= q) lo = mid;
-            else hi = mid;
-          }
-          cr = lo;
-          rlo = sb[lo];
-          rhi = lo + 1 < nrep ? sb[lo + 1] : NONE;
-          cmax = 0;
-        }
-        cmax = max(cmax, fi + 1);
-      }
-    }
-  }
-  if (cmax) atomicMax(&rv[cr], cmax);
-  present = block_sum(present);  // (synchronises the block)
-  err = block_min(err);
-  for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x)
-    if (rv[j]) atomicMax(&rtab[j + (1u << (REPLICA_BITS - 1))], rv[j]);
-  if (threadIdx.x == 0) {
-    if (present) atomicAdd(&dres->fl_part[32 * (blockIdx.x & 15)], present);
-    if (err != NONE) atomicMin(&dres->err_index, err);
-  }
-}
 
 // Counting-sort scatter; single-child parents (the common case in a typing
 // stream) take a plain store. The root sentinel's children are placed by
@@ -2455,13 +2417,39 @@ __global__ void __launch_bounds__(BLOCK) k_fl_next(uint32_t K, const uint32_t* d
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_fl_present(uint32_t Q, const uint32_t* anc, uint32_t* f) {
-  GRID_STRIDE(q, Q) f[q] = anc[q] != ABSENT ? 1u : 0u;
+__global__ void __launch_bounds__(BLOCK) k_fl_present(uint32_t Q, const unsigned long long* rec, uint32_t* f) {
+  GRID_STRIDE(q, Q) f[q] = rec[q] != REC_EMPTY ? 1u : 0u;
 }
 
 // Log append into a fresh tree when every op applied: the log is the batch
-// itself (same CSR layout, path elements [0, n_path)).
+// itself (same CSR layout, path elements [0, n_path)). SIMPLE (k_fl_claim):
+// op i is an Add whose one path element is path[i], so the kinds and offsets
+// are written without reading them; four ops per lane, 16-byte accesses.
+template <bool SIMPLE>
 __global__ void __launch_bounds__(BLOCK) k_fl_log_copy(OpsDev o, TreeDev T) {
+  if (SIMPLE) {
+    QUAD_LOOP(i0, o.n) {
+      if (i0 + 4 <= o.n) {
+        *reinterpret_cast<uchar4*>(T.l_kind + i0) = make_uchar4(CRDTM_ADD, CRDTM_ADD, CRDTM_ADD, CRDTM_ADD);
+        *reinterpret_cast<longlong2*>(T.l_ts + i0) = *reinterpret_cast<const longlong2*>(o.ts + i0);
+        *reinterpret_cast<longlong2*>(T.l_ts + i0 + 2) = *reinterpret_cast<const longlong2*>(o.ts + i0 + 2);
+        *reinterpret_cast<uint4*>(T.l_off + i0) = make_uint4(i0, i0 + 1, i0 + 2, i0 + 3);
+        *reinterpret_cast<uint4*>(T.l_val + i0) = *reinterpret_cast<const uint4*>(o.val + i0);
+        *reinterpret_cast<longlong2*>(T.l_path + i0) = *reinterpret_cast<const longlong2*>(o.path + i0);
+        *reinterpret_cast<longlong2*>(T.l_path + i0 + 2) = *reinterpret_cast<const longlong2*>(o.path + i0 + 2);
+      } else {
+        for (uint32_t i = i0; i < o.n; ++i) {
+          T.l_kind[i] = CRDTM_ADD;
+          T.l_ts[i] = o.ts[i];
+          T.l_off[i] = i;
+          T.l_val[i] = o.val[i];
+          T.l_path[i] = o.path[i];
+        }
+      }
+      if (i0 + 4 >= o.n) T.l_off[o.n] = o.n;
+    }
+    return;
+  }
   GRID_STRIDE(i, o.n + 1) {
     T.l_off[i] = o.off[i];
     if (i == o.n) continue;
@@ -2502,8 +2490,7 @@ struct RunArr {
   uint32_t* hanc;            // anchor of the head (ABSENT: a hole run), then its effective parent
   uint32_t* par;             // parent run (NONE: a child of the root sentinel, or a hole run)
   uint32_t* len;
-  uint32_t* nch;             // child runs
-  uint32_t* estart;          // sorted position of the run's first child run (valid when nch > 0)
+  uint2* er;                 // sorted positions [er.x, er.y) of the run's child runs ({0, 0}: none)
   unsigned long long* ca;    // children arrived << 32 | their subtree sizes
   uint32_t* T;               // subtree size
   uint32_t* w;               // top-down increment along the chain
@@ -2524,8 +2511,8 @@ struct RunArr {
 // slot, the root sentinel = Q, hole runs Q + 1) listed in descending run
 // order, so the stable sort leaves siblings at one slot in descending slot
 // order.
-__global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, const uint32_t* rid, const uint32_t* anc,
-                                                  uint32_t* skey, uint32_t* sval) {
+__global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, const uint32_t* rid,
+                                                  const unsigned long long* rec, uint32_t* skey, uint32_t* sval) {
   const uint32_t R = *a.nR;
   RUN_LOOP(r) {
     const uint32_t x = a.heads[r];
@@ -2534,7 +2521,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, const ui
     if (d == ABSENT) {  // a hole run
       a.par[r] = NONE;
       a.len[r] = 0;
-      a.nch[r] = 0;
+      a.er[r] = make_uint2(0u, 0u);
       a.ca[r] = 0;
       skey[R - 1 - r] = Q + 1;
       sval[R - 1 - r] = r;
@@ -2554,15 +2541,15 @@ __global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, const ui
         }
         d = __hip_atomic_load(&a.hanc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (d >= Q || anc[d] == ABSENT) d = Q;
+      if (d >= Q || rec[d] == REC_EMPTY) d = Q;
       __hip_atomic_store(&a.hanc[r], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (d != Q && (d >= x || anc[d] == ABSENT)) {  // (self-anchored / nodeless anchor: a failing batch)
+    } else if (d != Q && (d >= x || rec[d] == REC_EMPTY)) {  // (self-anchored / nodeless anchor: a failing batch)
       d = Q;
       a.hanc[r] = d;
     }
     a.par[r] = d == Q ? NONE : rid[d] - 1;
     a.len[r] = hn - x;  // (a hole after the run is a run of its own)
-    a.nch[r] = 0;
+    a.er[r] = make_uint2(0u, 0u);
     a.ca[r] = 0;
     skey[R - 1 - r] = d;
     sval[R - 1 - r] = r;
@@ -2570,23 +2557,17 @@ __global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, const ui
 }
 
 // The generic order's input (a run tree deeper than RUN_MAXD): ep per slot
-// (q - 1 inside a run, the walked effective parent at a head), into anc.
-__global__ void __launch_bounds__(BLOCK) k_run_ep_slots(RunArr a, uint32_t Q, const uint32_t* rid, uint32_t* anc) {
+// (q - 1 inside a run, the walked effective parent at a head, ABSENT = no
+// node), into anc.
+__global__ void __launch_bounds__(BLOCK) k_run_ep_slots(RunArr a, uint32_t Q, const uint32_t* rid,
+                                                        const unsigned long long* rec, uint32_t* anc) {
   GRID_STRIDE(q, Q) {
-    if (anc[q] == ABSENT) continue;
+    if (rec[q] == REC_EMPTY) {
+      anc[q] = ABSENT;
+      continue;
+    }
     const uint32_t r = rid[q] - 1;
     anc[q] = a.heads[r] == q ? a.hanc[r] : q - 1;
-  }
-}
-
-// children per parent run: the last sibling of every attach slot's group adds
-// the group's size (one atomic per group, not per child)
-__global__ void __launch_bounds__(BLOCK) k_run_nch(RunArr a, uint32_t Q, const uint32_t* pk, const uint32_t* sarr,
-                                                   const uint32_t* gstart) {
-  const uint32_t R = *a.nR;
-  RUN_LOOP(k) {
-    const uint32_t p = pk[k];
-    if (p < Q && (k + 1 == R || pk[k + 1] != p)) atomicAdd(&a.nch[a.par[sarr[k]]], k - gstart[p] + 1);
   }
 }
 
@@ -2605,7 +2586,8 @@ __device__ __forceinline__ void run_climb(RunArr& a, uint32_t x, uint32_t t) {
     const uint32_t p = a.par[x];
     if (p == NONE) return;
     const unsigned long long old = atomicAdd(&a.ca[p], (1ULL << 32) | t);
-    if (static_cast<uint32_t>(old >> 32) + 1u != a.nch[p]) return;
+    const uint2 e = a.er[p];
+    if (static_cast<uint32_t>(old >> 32) + 1u != e.y - e.x) return;
     t = a.len[p] + static_cast<uint32_t>(old) + t;
     x = p;
   }
@@ -2621,7 +2603,8 @@ __global__ void __launch_bounds__(BLOCK) k_run_tree_up(RunArr a, const uint32_t*
     if (k < R) {
       const uint32_t r = sarr[k];
       key = a.par[r];
-      if (a.nch[r] == 0) {
+      const uint2 e = a.er[r];
+      if (e.y == e.x) {
         const uint32_t t = a.len[r];
         a.T[r] = t;
         v = (1ULL << 32) | t;
@@ -2637,30 +2620,41 @@ __global__ void __launch_bounds__(BLOCK) k_run_tree_up(RunArr a, const uint32_t*
     const uint32_t nk = __shfl_down(key, 1, 64);
     if ((lane == 63 || nk != key) && key < NONE - 64 && (v >> 32)) {
       const unsigned long long old = atomicAdd(&a.ca[key], v);
-      if (static_cast<uint32_t>(old >> 32) + static_cast<uint32_t>(v >> 32) == a.nch[key])
+      const uint2 e = a.er[key];
+      if (static_cast<uint32_t>(old >> 32) + static_cast<uint32_t>(v >> 32) == e.y - e.x)
         run_climb(a, key, a.len[key] + static_cast<uint32_t>(old) + static_cast<uint32_t>(v));
     }
   }
 }
 
+// The subtree sizes in sorted order (tk), summed inclusively by the xs scan:
+// S(k) = the sizes of the first k entries = k ? xs[k - 1] : 0. (A gather
+// inside the scan's load would hold up its look-back chain.)
 __global__ void __launch_bounds__(BLOCK) k_run_gather(RunArr a, const uint32_t* sarr, uint32_t* tk) {
   RUN_LOOP(k) tk[k] = a.T[sarr[k]];
 }
+__device__ __forceinline__ uint32_t run_S(const uint32_t* xs, uint32_t k) { return k ? xs[k - 1] : 0u; }
 
-// gstart[p] = the first position of slot p's sibling group in the sorted
-// list; estart[P] = the first position of run P's child runs (they are
-// contiguous: P owns a contiguous slot range and the list is by slot)
+// Per parent run P the sorted positions er = [x, y) of its child runs
+// (contiguous: P owns a contiguous slot range and the list is by slot); the
+// first position of the root sentinel's children to *groot. Neighbours'
+// parents come from the adjacent lanes (a wave holds consecutive positions).
 __global__ void __launch_bounds__(BLOCK) k_run_gstart(RunArr a, uint32_t Q, const uint32_t* pk, const uint32_t* sarr,
-                                                      uint32_t* gstart) {
-  RUN_LOOP(k) {
-    const uint32_t p = pk[k];
-    if (k == 0 || pk[k - 1] != p) {
-      if (p <= Q) gstart[p] = k;
-      if (p < Q) {
-        const uint32_t P = a.par[sarr[k]];
-        if (k == 0 || pk[k - 1] >= Q || a.par[sarr[k - 1]] != P) a.estart[P] = k;
-      }
-    }
+                                                      uint32_t* groot) {
+  const uint32_t R = *a.nR;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t k0 = blockIdx.x * blockDim.x; k0 < R; k0 += gridDim.x * blockDim.x) {
+    const uint32_t k = k0 + threadIdx.x;
+    const uint32_t p = k < R ? pk[k] : Q + 1;
+    const uint32_t P = p < Q ? a.par[sarr[k]] : NONE;
+    uint32_t Pp = __shfl_up(P, 1, 64), Pn = __shfl_down(P, 1, 64);
+    if (k >= R) continue;
+    if (p == Q && (k == 0 || pk[k - 1] != Q)) *groot = k;
+    if (p >= Q) continue;
+    if (lane == 0) Pp = k ? (pk[k - 1] < Q ? a.par[sarr[k - 1]] : NONE) : NONE;
+    if (lane == 63 || k + 1 == R) Pn = k + 1 < R && pk[k + 1] < Q ? a.par[sarr[k + 1]] : NONE;
+    if (Pp != P) a.er[P].x = k;
+    if (Pn != P) a.er[P].y = k + 1;
   }
 }
 
@@ -2670,15 +2664,15 @@ __global__ void __launch_bounds__(BLOCK) k_run_gstart(RunArr a, uint32_t Q, cons
 // itself comes after p and after its siblings at p with a larger slot (the
 // ones sorted before it): together, the child runs of P sorted before r.
 __global__ void __launch_bounds__(BLOCK) k_run_w(RunArr a, uint32_t Q, const uint32_t* sarr, const uint32_t* pk,
-                                                 const uint32_t* xs, const uint32_t* gstart) {
+                                                 const uint32_t* xs, const uint32_t* groot) {
   RUN_LOOP(k) {
     const uint32_t r = sarr[k], p = pk[k];
     if (p > Q) continue;  // (hole runs)
     if (p == Q) {
-      a.w[r] = xs[k] - xs[gstart[Q]];
+      a.w[r] = run_S(xs, k) - run_S(xs, *groot);
     } else {
       const uint32_t P = a.par[r];
-      a.w[r] = xs[k] - xs[a.estart[P]] + (p - a.heads[P]) + 1u;
+      a.w[r] = run_S(xs, k) - run_S(xs, a.er[P].x) + (p - a.heads[P]) + 1u;
     }
   }
 }
@@ -2709,57 +2703,104 @@ __global__ void __launch_bounds__(BLOCK) k_run_pos(RunArr a, DevResult* dres) {
 // from the slot (the replica r with base[r] <= q, largest such r, and
 // counter min[r] + q - base[r]; tables in LDS when the replica ids fit, else
 // the op's ts), its children dict implicit.
-__global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint32_t K, const uint32_t* anc,
-                                                      const uint32_t* rid, const uint32_t* pk, const uint32_t* xs,
-                                                      const uint32_t* tk, const uint32_t* qc, uint32_t* doc, OpsDev o,
-                                                      TsIndex x, uint32_t nrep, const unsigned long long* rec,
-                                                      const uint32_t* logidx, TreeDev T) {
-  extern __shared__ uint32_t sbc[];  // dynamic: 2 * nrep words when the tables fit (HOST_RANGES)
+//
+// With `chk` (the flat speculation) it also does the claim's check from the
+// records it reads anyway: every present slot's Add must come after its
+// anchor's (addAfterHelp, src/Internal/Node.elm:68-70; inside a run the
+// anchor is the slot before, whose record the neighbouring lane has just
+// read), the present slots are counted (as many as keyed Adds: no duplicate
+// timestamps) and, with the replica tables in LDS, the replicas table is
+// folded in slot order (a wave's 64 slots usually lie in one replica's
+// range: one LDS atomic per wave). The loop trip count is wave-uniform so
+// every lane takes part in the wave reductions.
+__global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint32_t K, const uint32_t* rid,
+                                                      const uint32_t* pk, const uint32_t* xs, const uint32_t* qc,
+                                                      uint32_t* doc, OpsDev o, TsIndex x, uint32_t nrep,
+                                                      const unsigned long long* rec, const uint32_t* logidx, TreeDev T,
+                                                      DevResult* chk, uint32_t* rtab) {
+  extern __shared__ uint32_t sbc[];  // dynamic: 3 * nrep words when the tables fit (HOST_RANGES)
   uint32_t* sb = sbc;
   uint32_t* sc = sbc + nrep;
+  uint32_t* srv = sbc + 2 * nrep;  // (chk) largest op index + 1 per replica
   const bool lds = nrep <= HOST_RANGES;
   if (lds) {
     for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x) {
       sb[j] = x.base[j];
       sc[j] = x.rng[j].x;
+      srv[j] = 0;
     }
   }
   __syncthreads();
-  GRID_STRIDE(q, Q) {
-    if (anc[q] == ABSENT) continue;
-    const uint32_t slot = 1 + (qc ? qc[q] : q);
-    const uint32_t r = rid[q] - 1;
-    uint32_t p = a.posh[r] + (q - a.heads[r]);
-    const uint32_t ne = a.nch[r];
-    if (ne) {
-      const uint32_t e0 = a.estart[r];
-      uint32_t lo = e0, hi = e0 + ne;  // first k with pk[k] >= q
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (pk[mid] < q) lo = mid + 1;
-        else hi = mid;
+  uint32_t present = 0, err = NONE;
+  for (uint32_t q0 = blockIdx.x * blockDim.x; q0 < Q; q0 += gridDim.x * blockDim.x) {
+    const uint32_t q = q0 + threadIdx.x;
+    const unsigned long long rq = q < Q ? rec[q] : REC_EMPTY;
+    uint32_t rep = NONE, fi = 0;
+    if (rq != REC_EMPTY) {
+      fi = static_cast<uint32_t>(rq >> 32);
+      const uint32_t slot = 1 + (qc ? qc[q] : q);
+      const uint32_t r = rid[q] - 1;
+      uint32_t p = a.posh[r] + (q - a.heads[r]);
+      const uint2 er = a.er[r];
+      const uint32_t e0 = er.x, e1 = er.y;
+      if (e1 > e0) {
+        uint32_t lo = e0, hi = e1;  // first k with pk[k] >= q
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (pk[mid] < q) lo = mid + 1;
+          else hi = mid;
+        }
+        if (lo > e0) p += xs[lo - 1] - run_S(xs, e0);
       }
-      if (lo > e0) p += xs[lo - 1] + tk[lo - 1] - xs[e0];
-    }
-    if (p < K) doc[p] = slot;  // (a rank past K: a speculation that fails)
-    const uint32_t i = static_cast<uint32_t>(rec[q] >> 32);
-    long long key;
-    if (lds) {
-      uint32_t lo = 0, hi = nrep;  // largest r with sb[r] <= q
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (sb[mid] <= q) lo = mid;
-        else hi = mid;
+      if (p < K) doc[p] = slot;  // (a rank past K: a speculation that fails)
+      long long key;
+      if (lds) {
+        uint32_t lo = 0, hi = nrep;  // largest r with sb[r] <= q
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (sb[mid] <= q) lo = mid;
+          else hi = mid;
+        }
+        key = (static_cast<long long>(lo) << 32) | static_cast<long long>(sc[lo] + (q - sb[lo]));
+        rep = lo;
+      } else {
+        key = o.ts[fi];
       }
-      key = (static_cast<long long>(lo) << 32) | static_cast<long long>(sc[lo] + (q - sb[lo]));
-    } else {
-      key = o.ts[i];
+      T.s_key[slot] = key;
+      T.s_dict[slot] = 0;
+      T.s_src[slot] = logidx ? logidx[fi] : fi;
+      T.s_flags[slot] = 0;
+      T.s_child[slot] = NONE;
+      if (chk) {
+        ++present;
+        const uint32_t qa = static_cast<uint32_t>(rq);
+        if (qa != Q && (qa == NONE || static_cast<uint32_t>(rec[qa] >> 32) >= fi)) err = min(err, fi);
+      }
     }
-    T.s_key[slot] = key;
-    T.s_dict[slot] = 0;
-    T.s_src[slot] = logidx ? logidx[i] : i;
-    T.s_flags[slot] = 0;
-    T.s_child[slot] = NONE;
+    if (chk && lds) {  // (wave-uniform) replicas[r] := its last Add, one LDS atomic per wave and replica
+      const unsigned long long m = __ballot(rep != NONE);
+      if (m) {
+        const uint32_t r0 = __shfl(rep, __ffsll(static_cast<long long>(m)) - 1, 64);
+        if (__ballot(rep != NONE && rep != r0) == 0) {
+          uint32_t v = rep != NONE ? fi + 1 : 0u;
+#pragma unroll
+          for (int o2 = 32; o2 > 0; o2 >>= 1) v = max(v, __shfl_xor(v, o2, 64));
+          if ((threadIdx.x & 63) == 0) atomicMax(&srv[r0], v);
+        } else if (rep != NONE) {
+          atomicMax(&srv[rep], fi + 1);
+        }
+      }
+    }
+  }
+  if (!chk) return;  // (grid-uniform)
+  present = block_sum(present);  // (synchronises the block: srv complete)
+  err = block_min(err);
+  if (lds)
+    for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x)
+      if (srv[j]) atomicMax(&rtab[j + (1u << (REPLICA_BITS - 1))], srv[j]);
+  if (threadIdx.x == 0) {
+    if (present) atomicAdd(&chk->fl_part[32 * (blockIdx.x & 15)], present);
+    if (err != NONE) atomicMin(&chk->err_index, err);
   }
 }
 
@@ -3101,8 +3142,16 @@ struct FlatBufs {
   long long* rep;
 };
 
+static void fl_log_copy(crdtm_ctx* c, const OpsDev& o, const TreeDev& T, bool simple) {
+  if (simple)
+    LAUNCH(k_fl_log_copy<true>, dim3(quad_grid(o.n)), dim3(BLOCK), 0, c->stream, o, T);
+  else
+    LAUNCH(k_fl_log_copy<false>, dim3(grid_for(o.n + 1)), dim3(BLOCK), 0, c->stream, o, T);
+}
+
 static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_t Q, uint32_t maxr,
-                             const uint8_t* st, uint32_t K, bool all_applied, bool log_done, FlatBufs& fb) {
+                             const uint8_t* st, uint32_t K, bool all_applied, bool log_done, bool simple,
+                             bool check, FlatBufs& fb) {
   crdtm_ctx* c = t->ctx;
   hipStream_t s = c->stream;
   Arena& ws = c->ws;
@@ -3122,20 +3171,19 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     ra.heads = fb.heads = ws.alloc<uint32_t>(Q + 1);
     ra.hanc = fb.hanc = ws.alloc<uint32_t>(Q + 1);
     uint32_t* rid = fb.rid = ws.alloc<uint32_t>(Q);
-    if ((r = dscan<SumOp, true>(RunIdGen{rec, Q, anc, ra.heads, ra.hanc}, rid, Q, &dr->run_count, ws, s, nullptr,
+    if ((r = dscan<SumOp, true>(RunIdGen{rec, Q, ra.heads, ra.hanc}, rid, Q, &dr->run_count, ws, s, nullptr,
                                 nullptr, "k_dscan_runs")))
       return r;
     uint32_t* qc = nullptr;
     if (Q != K) {  // slots with no node: compact
       qc = fb.qc = ws.alloc<uint32_t>(Q);
-      LAUNCH(k_fl_present, dim3(gq), dim3(BLOCK), 0, s, Q, anc, qc);
+      LAUNCH(k_fl_present, dim3(gq), dim3(BLOCK), 0, s, Q, rec, qc);
       if ((r = scan_excl_u32(qc, qc, Q, nullptr, ws, s))) return r;
     }
     // ---- K2a (heads' effective parents), parent runs, sibling order (stable radix sort by attach slot) ----
     ra.par = ws.alloc<uint32_t>(Q + 1);
     ra.len = ws.alloc<uint32_t>(Q + 1);
-    ra.nch = ws.alloc<uint32_t>(Q + 1);
-    ra.estart = ws.alloc<uint32_t>(Q + 1);
+    ra.er = ws.alloc<uint2>(Q + 1);
     ra.ca = ws.alloc<unsigned long long>(Q + 1);
     ra.T = ws.alloc<uint32_t>(Q + 1);
     ra.w = ws.alloc<uint32_t>(Q + 1);
@@ -3143,21 +3191,20 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     uint32_t* sk[2] = {ws.alloc<uint32_t>(Q + 1), ws.alloc<uint32_t>(Q + 1)};
     uint32_t* sv[2] = {ws.alloc<uint32_t>(Q + 1), ws.alloc<uint32_t>(Q + 1)};
     uint32_t* xs = ws.alloc<uint32_t>(Q + 1);
-    uint32_t* gstart = fb.cnt;  // [Q + 1] (the generic order's child counts; unused here)
+    uint32_t* groot = fb.cnt;  // one word: the root sentinel's first child in the sorted list
     const uint32_t gr = grid_for(Q, BLOCK, 2048);
-    LAUNCH(k_run_ep, dim3(gr), dim3(BLOCK), 0, s, ra, Q, rid, anc, sk[0], sv[0]);
+    LAUNCH(k_run_ep, dim3(gr), dim3(BLOCK), 0, s, ra, Q, rid, rec, sk[0], sv[0]);
     uint32_t sbits = 8;
     while (sbits < 32 && ((static_cast<uint64_t>(Q) + 1) >> sbits) != 0) sbits += 8;
     uint32_t *pk = nullptr, *sarr = nullptr;  // attach slot, run: siblings grouped by slot, slots ascending
     if ((r = radix_sort_pairs(sk[0], sv[0], sk[1], sv[1], ra.nR, Q, sbits, ws, s, &pk, &sarr))) return r;
-    uint32_t* tk = pk == sk[0] ? sk[1] : sk[0];  // (free after the sort)
-    LAUNCH(k_run_gstart, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, sarr, gstart);
-    LAUNCH(k_run_nch, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, sarr, gstart);
+    LAUNCH(k_run_gstart, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, sarr, groot);
     // ---- subtree sizes (one launch), head ranks, the document order ----
     LAUNCH(k_run_tree_up, dim3(gr), dim3(BLOCK), 0, s, ra, sarr);
+    uint32_t* tk = pk == sk[0] ? sk[1] : sk[0];  // (free after the sort)
     LAUNCH(k_run_gather, dim3(gr), dim3(BLOCK), 0, s, ra, sarr, tk);
-    if ((r = dscan<SumOp, false>(ArrGen{tk}, xs, Q, nullptr, ws, s, nullptr, ra.nR, "k_dscan_xs"))) return r;
-    LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, gstart);
+    if ((r = dscan<SumOp, true>(ArrGen{tk}, xs, Q, nullptr, ws, s, nullptr, ra.nR, "k_dscan_xs"))) return r;
+    LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, groot);
     LAUNCH(k_run_pos, dim3(gr), dim3(BLOCK), 0, s, ra, dr);
     uint32_t* logidx = nullptr;
     if (!all_applied) {  // compacted log (its scans share the ctx scan pool: main stream)
@@ -3171,12 +3218,12 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     }
     // ---- the document order and the commit (one pass), the chain ----
     LAUNCH(k_run_expand, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK),
-           maxr + 1 <= HOST_RANGES ? 2 * (maxr + 1) * sizeof(uint32_t) : 0, s, ra, Q, K, anc, rid, pk, xs, tk, qc,
-           t->d.doc, o, ix, maxr + 1, rec, logidx, t->d);
+           maxr + 1 <= HOST_RANGES ? 3 * (maxr + 1) * sizeof(uint32_t) : 0, s, ra, Q, K, rid, pk, xs, qc, t->d.doc,
+           o, ix, maxr + 1, rec, logidx, t->d, check ? dr : nullptr, c->rtab);
     LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d, t->cap.slots);
-    if (all_applied && !log_done) LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
+    if (all_applied && !log_done) fl_log_copy(c, o, t->d, simple);
   } else if (all_applied && !log_done) {
-    LAUNCH(k_fl_log_copy, dim3(g), dim3(BLOCK), 0, s, o, t->d);
+    fl_log_copy(c, o, t->d, simple);
   }
   fb.rep = ws.alloc<long long>(2 * static_cast<uint64_t>(maxr) + 2);
   LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, fb.rep,
@@ -3202,7 +3249,7 @@ static int flat_order_fallback(crdtm_tree* t, uint32_t Q, uint32_t K, FlatBufs& 
     RunArr ra{};
     ra.heads = fb.heads;
     ra.hanc = fb.hanc;
-    LAUNCH(k_run_ep_slots, dim3(gq), dim3(BLOCK), 0, s, ra, Q, fb.rid, anc);
+    LAUNCH(k_run_ep_slots, dim3(gq), dim3(BLOCK), 0, s, ra, Q, fb.rid, fb.rec, anc);
   }
   // ---- a run tree deeper than RUN_MAXD: children of every node, Euler tour + list ranking ----
   uint32_t* carr = ws.alloc<uint32_t>(U);
@@ -3237,7 +3284,7 @@ static int flat_order_fallback(crdtm_tree* t, uint32_t Q, uint32_t K, FlatBufs& 
 // batch where some op does not apply is then decided op by op and committed
 // again (the tree is fresh: its root sentinel is restored in between).
 static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_t Q, uint32_t maxr, uint8_t* st,
-                      uint8_t* st_out, crdtm_result* res) {
+                      uint8_t* st_out, crdtm_result* res, bool simple) {
   crdtm_ctx* c = t->ctx;
   hipStream_t s = c->stream;
   Arena& ws = c->ws;
@@ -3269,10 +3316,13 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   LAUNCH(k_fl_init, dim3(grid_for(Q, BLOCK, 4096)), dim3(BLOCK), 0, s, Q, fb.rec);
   // replicas table: folded by the check over slot order when the range table fits in LDS
   const uint32_t nrep = maxr + 1 <= HOST_RANGES ? maxr + 1 : 0u;
-  LAUNCH(k_fl_claim, dim3(quad_grid(n)), dim3(BLOCK), (3 * nrep + (nrep ? 0 : REP_DIRECT)) * sizeof(uint32_t), s,
-         o, ix, Q, fb.rec, t->timestamp, c->rtab, dr, nrep ? 0u : 1u, nrep, t->d, spec ? 1u : 0u);
-  LAUNCH(k_fl_check, dim3(grid_for(Q / 2 + 1, BLOCK, 2048)), dim3(BLOCK), 2 * nrep * sizeof(uint32_t), s, Q,
-         fb.rec, dr, ix.base, nrep, c->rtab);
+  const uint32_t shm = (3 * nrep + (nrep ? 0 : REP_DIRECT)) * sizeof(uint32_t);
+  if (simple)
+    LAUNCH(k_fl_claim<true>, dim3(quad_grid(n)), dim3(BLOCK), shm, s, o, ix, Q, fb.rec, t->timestamp, c->rtab, dr,
+           nrep ? 0u : 1u, nrep, t->d, spec ? 1u : 0u);
+  else
+    LAUNCH(k_fl_claim<false>, dim3(quad_grid(n)), dim3(BLOCK), shm, s, o, ix, Q, fb.rec, t->timestamp, c->rtab, dr,
+           nrep ? 0u : 1u, nrep, t->d, spec ? 1u : 0u);
   auto finish = [&](uint32_t K, uint32_t applied, uint32_t already, uint64_t npath, long long new_ts) -> int {
     int rr = take_replicas(t, fb.rep);
     if (rr) return rr;
@@ -3294,11 +3344,11 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   // ---- speculation: every op applies (writes the state before the check,
   // so never inside an incremental re-merge) ----
   if (spec) {
-    if ((r = flat_order_commit(t, o, ix, Q, maxr, st, n, true, true, fb))) return r;
+    if ((r = flat_order_commit(t, o, ix, Q, maxr, st, n, true, true, simple, true, fb))) return r;
     if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, nullptr, n, NONE, st_out);
     if ((r = sync_read(c))) return r;
     const DevResult& h = *c->hres;
-    uint32_t present = 0, keys = 0, own = 0, slow = 0;  // (k_fl_check / k_fl_claim shards)
+    uint32_t present = 0, keys = 0, own = 0, slow = 0;  // (k_run_expand / k_fl_claim shards)
     for (int k = 0; k < 16; ++k) {
       present += h.fl_part[32 * k];
       keys += h.fl_part[32 * k + 1];
@@ -3358,7 +3408,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   const bool all_applied = h1.n_applied == n;
   if ((r = grow_for(K, h1.n_applied))) return r;
   LAUNCH(k_fl_commit_reset, dim3(1), dim3(1), 0, s, dr);
-  if ((r = flat_order_commit(t, o, ix, Q, maxr, st, K, all_applied, spec, fb))) return r;
+  if ((r = flat_order_commit(t, o, ix, Q, maxr, st, K, all_applied, spec, simple, false, fb))) return r;
   if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, st, n, NONE, st_out);
   if ((r = sync_read(c))) return r;
   if (c->hres->run_fail && (r = flat_order_fallback(t, Q, K, fb))) return r;
@@ -3436,7 +3486,9 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   if (ix.dense) {
     ix.h = TsHash{nullptr, nullptr, 0};
     ix.first = nullptr;
-    if (flat) return apply_flat(t, o, ix, static_cast<uint32_t>(range_total), maxr, w.st, st_out, res);
+    // (simple: every op an Add whose path is its anchor alone, op i's at path[i])
+    if (flat)
+      return apply_flat(t, o, ix, static_cast<uint32_t>(range_total), maxr, w.st, st_out, res, o.n_path == n);
     ix.first = ws.alloc<uint32_t>(range_total + 1);
     HIP_CHECK(hipMemsetAsync(ix.first, 0xFF, (range_total + 1) * sizeof(uint32_t), s));
     LAUNCH(k_index_store, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix);

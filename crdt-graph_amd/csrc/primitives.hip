@@ -476,42 +476,64 @@ int segmented_sort_asc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* c
 constexpr uint32_t RS_ITEMS = 8;
 constexpr uint32_t RS_TILE = BLOCK * RS_ITEMS;
 
+// The tiles that hold items: the host launches for n_max, the device count
+// decides (the histogram is digit-major over these tiles only, so its scan
+// and the launches past the items cost nothing when n is far below n_max).
+__device__ __forceinline__ uint32_t rs_tiles(uint32_t n) { return n ? (n + RS_TILE - 1) / RS_TILE : 1u; }
+
 __global__ void __launch_bounds__(BLOCK) k_rs_hist(const uint32_t* __restrict__ keys, const uint32_t* n_dev,
-                                                   uint32_t shift, uint32_t ntiles, uint32_t* __restrict__ hist) {
+                                                   uint32_t shift, uint32_t* __restrict__ hist,
+                                                   uint32_t* __restrict__ hn) {
   __shared__ uint32_t h[256];
   const uint32_t n = *n_dev;
+  const uint32_t nt = rs_tiles(n);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *hn = 256 * nt;  // (the scan's device-side length)
+  if (blockIdx.x >= nt) return;
   for (uint32_t j = threadIdx.x; j < 256; j += BLOCK) h[j] = 0;
   __syncthreads();
   const uint32_t base = blockIdx.x * RS_TILE;
+  uint32_t k[RS_ITEMS];  // every load in flight before the first LDS atomic
 #pragma unroll
   for (uint32_t j = 0; j < RS_ITEMS; ++j) {
     const uint32_t i = base + j * BLOCK + threadIdx.x;
-    if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+    k[j] = i < n ? keys[i] : 0u;
   }
+#pragma unroll
+  for (uint32_t j = 0; j < RS_ITEMS; ++j)
+    if (base + j * BLOCK + threadIdx.x < n) atomicAdd(&h[(k[j] >> shift) & 255u], 1u);
   __syncthreads();
-  for (uint32_t d = threadIdx.x; d < 256; d += BLOCK) hist[d * ntiles + blockIdx.x] = h[d];
+  for (uint32_t d = threadIdx.x; d < 256; d += BLOCK) hist[d * nt + blockIdx.x] = h[d];
 }
 
 __global__ void __launch_bounds__(BLOCK) k_rs_scatter(const uint32_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ vals, const uint32_t* n_dev,
-                                                      uint32_t shift, uint32_t ntiles, const uint32_t* __restrict__ off,
+                                                      uint32_t shift, const uint32_t* __restrict__ off,
                                                       uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
   constexpr uint32_t NW = BLOCK / 64;
   __shared__ uint32_t run[256];
   __shared__ uint32_t wc[NW][256];
   const uint32_t n = *n_dev;
+  const uint32_t nt = rs_tiles(n);
   const uint32_t base = blockIdx.x * RS_TILE;
   if (base >= n) return;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (uint32_t d = threadIdx.x; d < 256; d += BLOCK) run[d] = off[d * ntiles + blockIdx.x];
+  for (uint32_t d = threadIdx.x; d < 256; d += BLOCK) run[d] = off[d * nt + blockIdx.x];
   for (uint32_t d = lane; d < 256; d += 64) wc[wv][d] = 0;  // kept all-zero between rounds
   const unsigned long long lt = (1ULL << lane) - 1ULL;
+  uint32_t ka[RS_ITEMS], va[RS_ITEMS];  // the tile's items, all loads in flight before the ranking rounds
+#pragma unroll
+  for (uint32_t j = 0; j < RS_ITEMS; ++j) {
+    const uint32_t i = base + j * BLOCK + threadIdx.x;
+    ka[j] = i < n ? keys[i] : 0u;
+    va[j] = i < n ? vals[i] : 0u;
+  }
   __syncthreads();
+#pragma unroll
   for (uint32_t j = 0; j < RS_ITEMS; ++j) {
     const uint32_t i = base + j * BLOCK + threadIdx.x;
     const bool valid = i < n;
-    const uint32_t k = valid ? keys[i] : 0u;
-    const uint32_t v = valid ? vals[i] : 0u;
+    const uint32_t k = ka[j];
+    const uint32_t v = va[j];
     const uint32_t d = (k >> shift) & 255u;
     unsigned long long m = __ballot(valid);
 #pragma unroll
@@ -544,21 +566,17 @@ __global__ void __launch_bounds__(BLOCK) k_rs_scatter(const uint32_t* __restrict
 // Sorts n_dev (<= n_max) pairs by the low `bits` bits of the keys, stably.
 // The result lands in (k0, v0) when the pass count is even, else in (k1, v1):
 // *out_k / *out_v point to it.
-// *hist_out (optional): the last pass's scanned histogram, digit d's first
-// output position at [d * *ntiles_out].
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, const uint32_t* n_dev, uint32_t n_max,
-                     uint32_t bits, Arena& ws, hipStream_t st, uint32_t** out_k, uint32_t** out_v, uint32_t** hist_out,
-                     uint32_t* ntiles_out) {
+                     uint32_t bits, Arena& ws, hipStream_t st, uint32_t** out_k, uint32_t** out_v) {
   const uint32_t ntiles = std::max<uint32_t>(1, (n_max + RS_TILE - 1) / RS_TILE);
-  uint32_t* hist = ws.alloc<uint32_t>(256ULL * ntiles + 1);
-  if (hist_out) *hist_out = hist;
-  if (ntiles_out) *ntiles_out = ntiles;
+  uint32_t* hist = ws.alloc<uint32_t>(256ULL * ntiles + 2);
+  uint32_t* hn = hist + 256ULL * ntiles + 1;  // 256 x the tiles that hold items (device)
   uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
   for (uint32_t shift = 0; shift < bits; shift += 8) {
-    LAUNCH(k_rs_hist, dim3(ntiles), dim3(BLOCK), 0, st, ki, n_dev, shift, ntiles, hist);
-    int r = scan_excl_u32(hist, hist, 256ULL * ntiles, nullptr, ws, st);
+    LAUNCH(k_rs_hist, dim3(ntiles), dim3(BLOCK), 0, st, ki, n_dev, shift, hist, hn);
+    int r = dscan<SumOp, false>(ArrGen{hist}, hist, 256ULL * ntiles, nullptr, ws, st, nullptr, hn);
     if (r) return r;
-    LAUNCH(k_rs_scatter, dim3(ntiles), dim3(BLOCK), 0, st, ki, vi, n_dev, shift, ntiles, hist, ko, vo);
+    LAUNCH(k_rs_scatter, dim3(ntiles), dim3(BLOCK), 0, st, ki, vi, n_dev, shift, hist, ko, vo);
     std::swap(ki, ko);
     std::swap(vi, vo);
   }
