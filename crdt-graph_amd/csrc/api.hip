@@ -196,6 +196,7 @@ int crdtm_ctx_create(int device, void* stream, crdtm_ctx** out) {
   HIP_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
   HIP_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
   HIP_CHECK(hipMalloc(&c->dres, sizeof(DevResult)));
   HIP_CHECK(hipHostMalloc(&c->hres, sizeof(DevResult), hipHostMallocDefault));
   HIP_CHECK(hipMalloc(&c->crange, RID_SLOTS * sizeof(uint2)));
@@ -232,6 +233,7 @@ int crdtm_ctx_destroy(crdtm_ctx* c) {
   hipStreamDestroy(c->side);
   hipEventDestroy(c->ev_fork);
   hipEventDestroy(c->ev_join);
+  hipEventDestroy(c->ev_sync);
   delete c;
   return CRDTM_OK;
 }

@@ -94,6 +94,7 @@ struct crdtm_ctx {
   // copy), forked from and joined back into `stream` with these events
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_sync = nullptr;  // recorded after each result read; the host spins on it (sync_read)
   crdtm::Arena ws;
   // guard-G statistics of the last apply's per-dict replay (CRDTM_GUARD_STATS=1, pdr.hip)
   unsigned long long* gstat_dev = nullptr;

@@ -2732,9 +2732,13 @@ __global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint
   }
   __syncthreads();
   uint32_t present = 0, err = NONE;
+  const uint32_t lane = threadIdx.x & 63;
   for (uint32_t q0 = blockIdx.x * blockDim.x; q0 < Q; q0 += gridDim.x * blockDim.x) {
     const uint32_t q = q0 + threadIdx.x;
     const unsigned long long rq = q < Q ? rec[q] : REC_EMPTY;
+    // the previous slot's record from the neighbouring lane (a wave holds consecutive slots)
+    unsigned long long rp = __shfl_up(rq, 1, 64);
+    if (chk && lane == 0 && q > 0 && q < Q) rp = rec[q - 1];
     uint32_t rep = NONE, fi = 0;
     if (rq != REC_EMPTY) {
       fi = static_cast<uint32_t>(rq >> 32);
@@ -2774,7 +2778,10 @@ __global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint
       if (chk) {
         ++present;
         const uint32_t qa = static_cast<uint32_t>(rq);
-        if (qa != Q && (qa == NONE || static_cast<uint32_t>(rec[qa] >> 32) >= fi)) err = min(err, fi);
+        if (qa != Q) {
+          const unsigned long long ra = qa == NONE ? REC_EMPTY : (qa + 1 == q ? rp : rec[qa]);
+          if (static_cast<uint32_t>(ra >> 32) >= fi) err = min(err, fi);  // (REC_EMPTY: no Add at the anchor)
+        }
       }
     }
     if (chk && lds) {  // (wave-uniform) replicas[r] := its last Add, one LDS atomic per wave and replica
@@ -2953,9 +2960,17 @@ static uint32_t pow2_at_least(uint64_t x) {
 
 // Reads the device result block. A scan whose look-back gave up has written
 // partial prefixes: report it as an engine error before anything is used.
+// The host waits for the result block by polling an event recorded after the
+// copy: a blocking stream synchronisation sleeps and wakes ~15 us after the
+// copy ends, idling the device between the merge's phases and calls.
 int sync_read(crdtm_ctx* c) {
   HIP_CHECK(hipMemcpyAsync(c->hres, c->dres, sizeof(DevResult), hipMemcpyDeviceToHost, c->stream));
-  HIP_CHECK(hipStreamSynchronize(c->stream));
+  HIP_CHECK(hipEventRecord(c->ev_sync, c->stream));
+  for (;;) {
+    const hipError_t e = hipEventQuery(c->ev_sync);
+    if (e == hipSuccess) break;
+    if (e != hipErrorNotReady) HIP_CHECK(e);
+  }
   if (c->hres->scan_err) {
     std::fprintf(stderr, "crdtm: a device scan's look-back did not resolve\n");
     return CRDTM_E_HIP;
