@@ -115,7 +115,11 @@ def roofline(workload, per_step, launches, B_alg, ms_step, steps_profiled):
     pmc, src = pmc_table(workload)
 
     def kbytes(nm, key="hbm_bytes"):
-        e = pmc.get(nm.split("<")[0])
+        base = nm.split("<")[0]
+        # labelled scan phases (k_dscan_runs, k_dscan_xs, ...) are instances of
+        # k_dscan, whose PMC entry is the dispatch-weighted mean over all of
+        # them: summed over the step's dispatches it gives their exact total
+        e = pmc.get(base) or (pmc.get("k_dscan") if base.startswith("k_dscan") else None)
         if e and key not in e and key == "hbm_bytes" and "hbm_bytes_corrected" in e:
             key = "hbm_bytes_corrected"  # (round-1 summaries)
         return None if not e or key not in e else e[key]
