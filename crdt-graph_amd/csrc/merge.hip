@@ -313,20 +313,52 @@ __global__ void __launch_bounds__(BLOCK) k_index_insert(OpsDev o, TsIndex x) {
 // (one arbitrary writer wins among duplicates), then every Add that did not
 // win takes an atomicMin, so the slot ends as the first Add of that
 // timestamp. Batches without duplicate timestamps pay no atomic at all.
-__global__ void __launch_bounds__(BLOCK) k_index_store(OpsDev o, TsIndex x) {
+// The replica range table (base, min, max counter) is read from LDS when its
+// nrep ids fit (as in k_fl_claim), else from the global table.
+struct RangeLds {
+  uint32_t* sbase;
+  uint32_t* smin;
+  uint32_t* smax;
+  uint32_t nrep;
+  __device__ __forceinline__ void load(const TsIndex& x) {
+    for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x) {
+      sbase[j] = x.base[j];
+      const uint2 g = x.rng[j];
+      smin[j] = g.x;
+      smax[j] = g.y;
+    }
+    __syncthreads();
+  }
+  __device__ __forceinline__ uint32_t slot(const TsIndex& x, long long ts) const {
+    if (!nrep) return tsindex_slot(x, ts);
+    if (ts <= 0) return NONE;
+    const uint64_t r = static_cast<uint64_t>(ts) >> 32;
+    if (r >= nrep) return NONE;
+    const uint32_t c = static_cast<uint32_t>(ts), lo = smin[r];
+    if (lo == NONE || c < lo || c > smax[r]) return NONE;
+    return sbase[r] + (c - lo);
+  }
+};
+
+__global__ void __launch_bounds__(BLOCK) k_index_store(OpsDev o, TsIndex x, uint32_t nrep) {
+  extern __shared__ uint32_t srt[];  // [3 * nrep]
+  RangeLds t{srt, srt + nrep, srt + 2 * nrep, nrep};
+  t.load(x);
   QUAD_LOOP_XCD(i0, o.n) {
     Quad q;
     load_quad(o, i0, q);
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
       if (k >= q.cnt) break;
-      if (q.kind[k] == CRDTM_ADD && q.off[k + 1] != q.off[k] && q.ts[k] > 0)
-        x.first[tsindex_slot(x, q.ts[k])] = i0 + k;
+      if (q.kind[k] == CRDTM_ADD && q.off[k + 1] != q.off[k] && q.ts[k] > 0) x.first[t.slot(x, q.ts[k])] = i0 + k;
     }
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_index_fix(OpsDev o, TsIndex x) {
+__global__ void __launch_bounds__(BLOCK) k_index_fix(OpsDev o, TsIndex x, uint32_t nrep) {
+  extern __shared__ uint32_t srt[];  // [3 * nrep]
+  RangeLds t{srt, srt + nrep, srt + 2 * nrep, nrep};
+  t.load(x);
   QUAD_LOOP_XCD(i0, o.n) {
     Quad q;
     load_quad(o, i0, q);
@@ -334,7 +366,7 @@ __global__ void __launch_bounds__(BLOCK) k_index_fix(OpsDev o, TsIndex x) {
     for (uint32_t k = 0; k < 4; ++k) {
       if (k >= q.cnt) break;
       if (q.kind[k] != CRDTM_ADD || q.off[k + 1] == q.off[k] || q.ts[k] <= 0) continue;
-      uint32_t* f = &x.first[tsindex_slot(x, q.ts[k])];
+      uint32_t* f = &x.first[t.slot(x, q.ts[k])];
       if (*f != i0 + k) atomicMin(f, i0 + k);
     }
   }
@@ -794,7 +826,7 @@ __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* total) 
 // group, then its size at its last position) and one scan makes them the
 // children CSR. (The counting sort it replaces paid one random device
 // atomic per node twice, counting and placing: deep10m 0.67 ms.)
-// Also the sibling sort key (k_up_count's) and k_links' cleared outputs.
+// Also the sibling sort key and k_links' cleared outputs.
 __global__ void __launch_bounds__(BLOCK) k_doc_keys(OpsDev o, Work w, const uint32_t* anc, const uint8_t* sp,
                                                     uint32_t* key, uint32_t* val, long long* skey, uint32_t* fc,
                                                     uint32_t* ns, uint32_t* f1, uint32_t* nitems) {
@@ -833,17 +865,33 @@ __global__ void __launch_bounds__(BLOCK) k_doc_gcount(const uint32_t* sk, uint32
 }
 
 // fc = first child, ns = next sibling, f1 = first ep-child (group 1)
-__global__ void __launch_bounds__(BLOCK) k_links(OpsDev o, const uint32_t* anc, const uint32_t* start,
+// pu[p] = the parent uid of carr[p] (the grouping sort's keys: sorting
+// within a group keeps them); the neighbours' come from the adjacent lanes.
+__global__ void __launch_bounds__(BLOCK) k_links(OpsDev o, const uint32_t* anc, const uint32_t* pu,
                                                  const uint32_t* total, const uint32_t* carr, uint32_t* fc,
                                                  uint32_t* ns, uint32_t* f1) {
   const uint32_t tot = *total;
-  GRID_STRIDE(p, tot) {
-    const uint32_t v = carr[p];
-    const uint32_t u = doc_up(o, anc, v);
-    const bool first = p == start[u];
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t p0 = blockIdx.x * blockDim.x; p0 < tot; p0 += gridDim.x * blockDim.x) {
+    const uint32_t p = p0 + threadIdx.x;
+    const bool valid = p < tot;
+    const uint32_t v = valid ? carr[p] : NONE, u = valid ? pu[p] : NONE;
+    const bool g1 = valid && doc_group1(o, anc, v);
+    uint32_t up = __shfl_up(u, 1, 64), un = __shfl_down(u, 1, 64), vn = __shfl_down(v, 1, 64);
+    bool g1p = __shfl_up(g1 ? 1u : 0u, 1, 64) != 0;
+    if (!valid) continue;
+    if (lane == 0 && p > 0) {
+      up = pu[p - 1];
+      g1p = doc_group1(o, anc, carr[p - 1]);
+    }
+    if (lane == 63 && p + 1 < tot) {
+      un = pu[p + 1];
+      vn = carr[p + 1];
+    }
+    const bool first = p == 0 || up != u;
     if (first) fc[u] = v;
-    if (doc_group1(o, anc, v) && (first || !doc_group1(o, anc, carr[p - 1]))) f1[u] = v;
-    ns[v] = (p + 1 < start[u + 1]) ? carr[p + 1] : NONE;
+    if (g1 && (first || !g1p)) f1[u] = v;
+    ns[v] = (p + 1 < tot && un == u) ? vn : NONE;
   }
 }
 
@@ -3498,8 +3546,9 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
       return apply_flat(t, o, ix, static_cast<uint32_t>(range_total), maxr, w.st, st_out, res, o.n_path == n);
     ix.first = ws.alloc<uint32_t>(range_total + 1);
     HIP_CHECK(hipMemsetAsync(ix.first, 0xFF, (range_total + 1) * sizeof(uint32_t), s));
-    LAUNCH(k_index_store, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix);
-    LAUNCH(k_index_fix, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, ix);
+    const uint32_t nrep = maxr + 1 <= HOST_RANGES ? maxr + 1 : 0u;
+    LAUNCH(k_index_store, dim3(quad_grid(n)), dim3(BLOCK), 3 * nrep * sizeof(uint32_t), s, o, ix, nrep);
+    LAUNCH(k_index_fix, dim3(quad_grid(n)), dim3(BLOCK), 3 * nrep * sizeof(uint32_t), s, o, ix, nrep);
   } else {
     const uint32_t H = pow2_at_least(2 * static_cast<uint64_t>(n));
     ix.first = nullptr;
@@ -3677,6 +3726,7 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   } join{c};
   LAUNCH(k_ep_jump, dim3(g), dim3(BLOCK), 0, s, o, w, anc, sp);
   const uint32_t gU = grid_for(U);
+  uint32_t* sk = nullptr;  // the parent uid of every carr position
   {  // children of every document node, grouped by a radix sort on the parent uid (CSR in cnt, items in carr)
     const uint32_t m = n + 1;  // uids that may have a parent
     uint32_t* ka = ws.alloc<uint32_t>(m);
@@ -3687,7 +3737,7 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
     LAUNCH(k_doc_keys, dim3(gm), dim3(BLOCK), 0, s, o, w, anc, sp, ka, carr, skey, fc, ns, f1, nitems);
     uint32_t kbits = 8;  // NONE (no parent) must sort after every uid <= n + 1
     while (kbits < 32 && ((static_cast<uint64_t>(n) + 2) >> kbits) != 0) kbits += 8;
-    uint32_t *sk = nullptr, *sv = nullptr;
+    uint32_t* sv = nullptr;
     if ((r = radix_sort_pairs(ka, carr, kb, vb, nitems, m, kbits, ws, s, &sk, &sv))) return r;
     carr = sv;  // (the children in parent order: the CSR's items)
     LAUNCH(k_doc_gstart, dim3(gm), dim3(BLOCK), 0, s, sk, m, fill);
@@ -3696,7 +3746,7 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   uint32_t* n_child_total = &dr->n_sentinels;  // scratch word for the scan total
   if ((r = scan_excl_u32(cnt, cnt, U + 1, n_child_total, ws, s))) return r;
   if ((r = segmented_sort(cnt, U, carr, U, skey, ws, s, dr))) return r;
-  LAUNCH(k_links, dim3(gU), dim3(BLOCK), 0, s, o, anc, cnt, n_child_total, carr, fc, ns, f1);
+  LAUNCH(k_links, dim3(grid_for(U, BLOCK, 4096)), dim3(BLOCK), 0, s, o, anc, sk, n_child_total, carr, fc, ns, f1);
 
   // ---- K4: Euler tour + list ranking ----
   const uint64_t E = 2ULL * U;
