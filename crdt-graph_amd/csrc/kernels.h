@@ -150,6 +150,49 @@ __device__ __forceinline__ uint32_t wave_ticket(uint32_t* ctr, bool pred) {
   return base + static_cast<uint32_t>(__popcll(m & ((1ULL << lane) - 1ULL)));
 }
 
+// Workgroup-aggregated tickets into NT counters: thread t takes the next
+// index of counter `which` (NT or more: none). One device atomic per counter
+// and workgroup call (a counter bumped by every wave still serialises ~12 ns
+// per atomic on one word). Every thread of the workgroup must call it.
+// GLOBAL = false: the counters live in LDS (s_ctr, this workgroup's running
+// offsets into ranges it reserved before), no device atomic at all.
+template <uint32_t NT, bool GLOBAL = true>
+__device__ __forceinline__ uint32_t block_ticket(uint32_t* ctr, uint32_t which) {
+  constexpr uint32_t NW = BLOCK / 64;
+  __shared__ uint32_t s_cnt[NT][NW];
+  __shared__ uint32_t s_base[NT];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const unsigned long long lt = (1ULL << lane) - 1ULL;
+  uint32_t rank = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < NT; ++k) {
+    const unsigned long long m = __ballot(which == k);
+    if (which == k) rank = static_cast<uint32_t>(__popcll(m & lt));
+    if (lane == 0) s_cnt[k][wv] = static_cast<uint32_t>(__popcll(m));
+  }
+  __syncthreads();
+  if (threadIdx.x < NT) {
+    const uint32_t k = threadIdx.x;
+    uint32_t tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w) {
+      const uint32_t c = s_cnt[k][w];
+      s_cnt[k][w] = tot;  // -> the waves' exclusive prefix
+      tot += c;
+    }
+    if (GLOBAL) {
+      s_base[k] = tot ? atomicAdd(&ctr[k], tot) : 0u;
+    } else {
+      s_base[k] = ctr[k];
+      ctr[k] += tot;
+    }
+  }
+  __syncthreads();
+  const uint32_t r = which < NT ? s_base[which] + s_cnt[which][wv] + rank : NONE;
+  __syncthreads();  // (the next call reuses the LDS)
+  return r;
+}
+
 // wave64 inclusive scan of u32 (CDNA: 64 lanes, __shfl_up over width 64)
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const int lane = threadIdx.x & 63;

@@ -735,11 +735,16 @@ __global__ void __launch_bounds__(BLOCK) k_guard_maxadd(OpsDev o, Work w) {
   }
 }
 
+// (one atomic per wave that finds a violation: a same-word atomic per Delete
+// serialised 1.8 ms on deep10m_il's 3.3M interleaved Deletes)
 __global__ void __launch_bounds__(BLOCK) k_guard_del(OpsDev o, Work w, DevResult* dres) {
-  GRID_STRIDE(i, o.n) {
-    if (o.kind[i] != CRDTM_DELETE || w.st[i] != ST_APPLIED) continue;
-    const uint32_t p = w.addpar[w.leaf[i]];
-    if (w.maxadd[p] > i + 1) atomicOr(&dres->guard, G_DEL_BEFORE_ADD);
+  for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < o.n; i0 += gridDim.x * blockDim.x) {
+    const uint32_t i = i0 + threadIdx.x;
+    bool v = false;
+    if (i < o.n && o.kind[i] == CRDTM_DELETE && w.st[i] == ST_APPLIED) v = w.maxadd[w.addpar[w.leaf[i]]] > i + 1;
+    if (__ballot(v) && (threadIdx.x & 63) == 0 &&
+        !(__hip_atomic_load(&dres->guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & G_DEL_BEFORE_ADD))
+      atomicOr(&dres->guard, G_DEL_BEFORE_ADD);  // (once set, the plain read skips the atomic)
   }
 }
 

@@ -979,26 +979,70 @@ struct PdrTiers {
   uint32_t blk_max;
 };
 
+// (Two passes over the instances: each workgroup counts its share per tier,
+// reserves it with one device atomic per tier, then writes its entries at
+// offsets kept in LDS. A counter bumped per dict, or per wave, serialises
+// ~12 ns per atomic on one word: 20 ms, then 1.5 ms, over deep10m_il's 1.6M
+// dicts. The grid is capped, so there are few workgroups; loops are
+// block-uniform.)
+__device__ __forceinline__ uint32_t pdr_tier_of(const PdrCtx& p, uint32_t I, uint32_t big_cap, const PdrTiers& tt,
+                                                uint32_t& slots, uint32_t& ops) {
+  const uint32_t n = p.o.n;
+  uint32_t D = I;
+  ops = 0;
+  if (I > n) {
+    if (p.ilog[I] != NONE) return NONE;  // rebuilt from the source dict's change log
+    D = p.I.src[I];
+  } else if (p.rbase[I + 1] == p.rbase[I]) {
+    return NONE;  // a dict no op reached
+  } else {
+    ops = p.rbase[I + 1] - p.rbase[I];  // ops replayed by this dict's wave
+  }
+  slots = pdr_kcount(p, D) + 1;
+  uint32_t t = slots <= PDR_SMALL ? 0u : (slots <= big_cap ? 1u : 2u);
+  if (slots > tt.blk_min && slots <= tt.blk_max) t = 3;
+  return t;
+}
+
 __global__ void __launch_bounds__(BLOCK) k_pdr_tier(PdrCtx p, uint32_t i0, uint32_t i1, uint32_t big_cap,
                                                     PdrTiers tt) {
-  const uint32_t n = p.o.n;
-  GRID_STRIDE(k, i1 - i0) {
+  __shared__ uint32_t s_off[4];
+  const uint32_t n = p.o.n, m = i1 - i0, stride = gridDim.x * blockDim.x;
+  uint32_t c[4] = {0u, 0u, 0u, 0u};
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < m; k += stride) {
+    uint32_t slots, ops;
+    const uint32_t t = pdr_tier_of(p, i0 + k, big_cap, tt, slots, ops);
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) c[q] += t == q ? 1u : 0u;
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < 4; ++q) {
+    const uint32_t tot = block_sum(c[q]);
+    if (threadIdx.x == 0) s_off[q] = tot ? atomicAdd(&tt.count[q], tot) : 0u;
+  }
+  __syncthreads();
+  uint32_t m4 = 0, m5 = 0, m6 = 0;
+  for (uint32_t k0 = blockIdx.x * blockDim.x; k0 < m; k0 += stride) {
+    const uint32_t k = k0 + threadIdx.x;
     const uint32_t I = i0 + k;
-    uint32_t D = I;
-    if (I > n) {
-      if (p.ilog[I] != NONE) continue;  // rebuilt from the source dict's change log
-      D = p.I.src[I];
-    } else if (p.rbase[I + 1] == p.rbase[I]) {
-      continue;  // a dict no op reached
+    uint32_t slots = 0, ops = 0, t = NONE;
+    if (k < m) {
+      t = pdr_tier_of(p, I, big_cap, tt, slots, ops);
+      if (t != NONE && I <= n) p.I.base[I] = p.rbase[I];
     }
-    if (I <= n) p.I.base[I] = p.rbase[I];
-    const uint32_t slots = pdr_kcount(p, D) + 1;
-    uint32_t t = slots <= PDR_SMALL ? 0u : (slots <= big_cap ? 1u : 2u);
-    if (slots > tt.blk_min && slots <= tt.blk_max) t = 3;
-    tt.list[t][atomicAdd(&tt.count[t], 1u)] = I;
-    if (t == 1) atomicMax(&tt.count[4], slots);
-    if (t == 3) atomicMax(&tt.count[6], slots);
-    if (I <= n) atomicMax(&tt.count[5], p.rbase[I + 1] - p.rbase[I]);  // ops replayed by this dict's wave
+    const uint32_t j = block_ticket<4, false>(s_off, t);
+    if (t < 4) tt.list[t][j] = I;
+    if (t == 1) m4 = max(m4, slots);
+    if (t == 3) m6 = max(m6, slots);
+    m5 = max(m5, ops);
+  }
+  m4 = block_max(m4);
+  m5 = block_max(m5);
+  m6 = block_max(m6);
+  if (threadIdx.x == 0) {
+    if (m4) atomicMax(&tt.count[4], m4);
+    if (m5) atomicMax(&tt.count[5], m5);
+    if (m6) atomicMax(&tt.count[6], m6);
   }
 }
 
@@ -1095,29 +1139,47 @@ __device__ __forceinline__ uint32_t pdr_src_dict(const PdrCtx& p, uint32_t I) { 
 
 // A live slot whose children are a frozen (dict, bound) view gets a snapshot
 // job when that view is non-empty. Slot positions [s0, s1).
+__device__ __forceinline__ bool pdr_job_of(const PdrCtx& p, const uint8_t* ok, uint32_t g, uint32_t& I, uint32_t& cd,
+                                           uint32_t& cb, uint32_t& r) {
+  const uint32_t n = p.o.n;
+  I = p.inst[g];
+  if (I == NONE) return false;
+  if (I <= n && !ok[I]) return false;  // an unreachable original dict
+  const uint32_t w = p.S[g];
+  if (!(w & SF_MADE) || (w & SF_TOMB)) return false;  // (sentinels too)
+  if (I <= n && !(w & SF_COPY)) return false;         // children = the live original dict
+  r = g - p.I.base[I];
+  if (w & SF_COPY) {
+    cd = p.qcd[g];
+    cb = p.qcb[g];
+  } else {
+    cd = p.rop[p.rbase[pdr_src_dict(p, I)] + r];
+    cb = p.I.bound[I];
+  }
+  const uint32_t f0 = pdr_first_op(p, cd);
+  return !(f0 == NONE || f0 >= cb);  // (else the copy is an empty dict: implicit)
+}
+
+// (two passes, as k_pdr_tier: one device atomic per workgroup for the job numbers)
 __global__ void __launch_bounds__(BLOCK) k_pdr_jobs(PdrCtx p, const uint8_t* ok, uint32_t s0, uint32_t s1,
                                                     uint32_t jcap, DevResult* dres) {
-  const uint32_t n = p.o.n;
-  GRID_STRIDE(k, s1 - s0) {
+  __shared__ uint32_t s_off[1];
+  const uint32_t n = p.o.n, m = s1 - s0, stride = gridDim.x * blockDim.x;
+  uint32_t c = 0;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < m; k += stride) {
+    uint32_t I, cd, cb, r;
+    c += pdr_job_of(p, ok, s0 + k, I, cd, cb, r) ? 1u : 0u;
+  }
+  const uint32_t tot = block_sum(c);
+  if (threadIdx.x == 0) s_off[0] = tot ? atomicAdd(&dres->pdr_jobs, tot) : 0u;
+  __syncthreads();
+  for (uint32_t k0 = blockIdx.x * blockDim.x; k0 < m; k0 += stride) {
+    const uint32_t k = k0 + threadIdx.x;
     const uint32_t g = s0 + k;
-    const uint32_t I = p.inst[g];
-    if (I == NONE) continue;
-    if (I <= n && !ok[I]) continue;  // an unreachable original dict
-    const uint32_t w = p.S[g];
-    if (!(w & SF_MADE) || (w & SF_TOMB)) continue;  // (sentinels too)
-    if (I <= n && !(w & SF_COPY)) continue;         // children = the live original dict
-    uint32_t cd, cb;
-    const uint32_t r = g - p.I.base[I];
-    if (w & SF_COPY) {
-      cd = p.qcd[g];
-      cb = p.qcb[g];
-    } else {
-      cd = p.rop[p.rbase[pdr_src_dict(p, I)] + r];
-      cb = p.I.bound[I];
-    }
-    const uint32_t f0 = pdr_first_op(p, cd);
-    if (f0 == NONE || f0 >= cb) continue;  // the copy is an empty dict (implicit)
-    const uint32_t j = atomicAdd(&dres->pdr_jobs, 1u);
+    uint32_t I = NONE, cd = 0, cb = 0, r = 0;
+    const bool job = k < m && pdr_job_of(p, ok, g, I, cd, cb, r);
+    const uint32_t j = block_ticket<1, false>(s_off, job ? 0u : NONE);
+    if (!job) continue;
     if (j >= jcap) {
       atomicOr(&dres->pdr_overflow, 1u);
       continue;
@@ -1315,7 +1377,7 @@ static int pdr_run_tiers(crdtm_ctx* c, const PdrCtx& p, uint32_t i0, uint32_t i1
   hipStream_t s = c->stream;
   if (i1 <= i0) return CRDTM_OK;
   HIP_CHECK(hipMemsetAsync(tt.count, 0, 8 * sizeof(uint32_t), s));
-  LAUNCH(k_pdr_tier, dim3(grid_for(i1 - i0)), dim3(BLOCK), 0, s, p, i0, i1, big_cap, tt);
+  LAUNCH(k_pdr_tier, dim3(grid_for(i1 - i0, BLOCK, 512)), dim3(BLOCK), 0, s, p, i0, i1, big_cap, tt);
   HIP_CHECK(hipMemcpyAsync(hcount, tt.count, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
   const uint32_t* h = hcount;
@@ -1539,7 +1601,7 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   uint32_t* joff = ws.alloc<uint32_t>(JCAP + 1);
   uint32_t* epre = ws.alloc<uint32_t>(JCAP + 1);
   for (uint32_t level = 0;; ++level) {
-    LAUNCH(k_pdr_jobs, dim3(grid_for(s1 - s0)), dim3(BLOCK), 0, s, p, ok, s0, s1, JCAP, dr);
+    LAUNCH(k_pdr_jobs, dim3(grid_for(s1 - s0, BLOCK, 512)), dim3(BLOCK), 0, s, p, ok, s0, s1, JCAP, dr);
     if ((r = sync_read(c))) return r;
     if (c->hres->pdr_overflow || level > in.maxlen + 1) {  // no room: sequential replay
       *handled = false;
