@@ -264,6 +264,20 @@ inline void prof_begin(hipStream_t st) {
 inline void prof_mark(const char* name, hipStream_t st) {
   if (g_prof) mark(g_prof, name, st);
 }
+// Host wait for everything queued on stream s by polling an event (a
+// blocking stream synchronisation sleeps and wakes ~15 us late, idling the
+// device between the phases of a merge). One event per host thread.
+inline int stream_wait(hipStream_t s) {
+  static thread_local hipEvent_t ev = nullptr;
+  if (!ev) HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HIP_CHECK(hipEventRecord(ev, s));
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return CRDTM_OK;
+    if (e != hipErrorNotReady) HIP_CHECK(e);
+  }
+}
+
 #define LAUNCH(k, grid, block, shm, st, ...)                    \
   do {                                                          \
     ::crdtm::prof_begin(st);                                    \

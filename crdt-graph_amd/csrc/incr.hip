@@ -558,7 +558,7 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   LAUNCH(k_fi_gaps, dim3(m), dim3(64), 0, s, m, glist, fi + 2, sk, sv, par0, pos, o.ts, nxt, ord, first, fi);
   uint32_t hf[4];
   HIP_CHECK(hipMemcpyAsync(hf, fi, sizeof(hf), hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
+  if (int rw = stream_wait(s)) return rw;
   const long long new_ts = t->timestamp + hf[1];
   if (hf[0] || replica_of(new_ts) != replica_of(t->timestamp)) {
     ws.used = mark0;  // the general paths decide (the key index stays valid: the state is untouched)

@@ -3596,7 +3596,7 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
     LAUNCH(k_len_count, dim3(grid_for(n, BLOCK, 1024)), dim3(BLOCK), 0, s, o, maxlen, lcnt);
     uint32_t hc[MAXLV_BUCKET + 1];
     HIP_CHECK(hipMemcpyAsync(hc, lcnt, (maxlen + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    if (int rw = stream_wait(s)) return rw;
     LevelStart hs{};
     uint32_t acc = 0;
     for (uint32_t j = 0; j <= maxlen; ++j) {

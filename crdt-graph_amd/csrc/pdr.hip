@@ -100,7 +100,8 @@ struct PdrCtx {
 // kind 0: slot word := a; kind 1: copy payload (node carried a, children dict
 // b); kind 2: children as-of op a. A snapshot as of op b is the last write per
 // slot among the entries with op < b, found in parallel (k_pdr_snap_*).
-constexpr uint32_t PDR_LOG_MIN = 512;  // smaller dicts re-replay their snapshots (env CRDTM_PDR_LOG_MIN)
+constexpr uint32_t PDR_LOG_MIN = 512;
+constexpr uint32_t PDR_LANE = 32;  // dicts of at most this many slots replay on one lane (k_pdr_lane)  // smaller dicts re-replay their snapshots (env CRDTM_PDR_LOG_MIN)
 
 __device__ __forceinline__ uint32_t pdr_kcount(const PdrCtx& p, uint32_t D) { return p.cbase[D + 1] - p.cbase[D]; }
 
@@ -972,11 +973,121 @@ __global__ void __launch_bounds__(64) k_pdr_blk(PdrCtx p, const uint32_t* list, 
 
 // Sort instances [i0, i1) into three size tiers: static LDS, dynamic LDS,
 // global memory. count = {tier sizes, largest slot count of tier 1}.
+// ---- P2c: tiny dicts, one lane each ----
+// The same replay as pdr_serial (its plain walk: src/Internal/Node.elm:93-104
+// findInsertion, nextNode skipping Tombstones, the copy quirk and its
+// orphans, deleteHelp) by one lane per dict over the dict's slot words in
+// global memory: a dict of a few ops wastes 63 lanes and a workgroup launch
+// in pdr_serial (deep10m_il: 1.6M dicts of <= 17 ops). Only dicts without a
+// change log take it (snapshots are rebuilt by re-replaying small dicts).
+template <int MODE>
+__global__ void __launch_bounds__(BLOCK) k_pdr_lane(PdrCtx p, const uint32_t* list, uint32_t cnt, uint8_t* st) {
+  constexpr bool ORIG = MODE >= 1;
+  GRID_STRIDE(k, cnt) {
+    const uint32_t I = list[k];
+    const uint32_t D = ORIG ? I : p.I.src[I];
+    const uint32_t bound = ORIG ? NONE : p.I.bound[I];
+    const uint32_t base = p.I.base[I];
+    const uint32_t K = pdr_kcount(p, D);
+    const uint32_t rb = p.rbase[D];
+    uint32_t* const S = p.S + base;
+    for (uint32_t r = 0; r <= K; ++r) {
+      S[r] = r == 0 ? (PM | SF_TOMB | SF_MADE) : PM;
+      p.inst[base + r] = I;
+    }
+    const uint32_t oe = p.rbase[D + 1] - 1;
+    for (uint32_t q = rb; q < oe; ++q) {
+      const uint32_t i = p.olist[q];
+      if (i >= bound) break;
+      const unsigned long long w = p.opw[q];
+      const uint32_t wlo = static_cast<uint32_t>(w), whi = static_cast<uint32_t>(w >> 32);
+      uint8_t s;
+      if (whi >> 31) {  // deleteHelp
+        const uint32_t t = wlo & PM;
+        if (t == 0) {
+          s = ST_ALREADY;
+        } else {
+          const uint32_t wt = t == OW_NF ? 0u : S[t];
+          if (!(wt & SF_MADE)) {
+            s = ST_NOTFOUND;
+          } else if (wt & SF_TOMB) {
+            s = ST_ALREADY;
+          } else {
+            S[t] = wt | SF_TOMB;
+            s = ST_APPLIED;
+          }
+        }
+      } else {  // addAfterHelp
+        const uint32_t x = wlo & PM;
+        const uint32_t an = ((wlo >> 24) | (whi << 8)) & PM;
+        if (x == 0) {
+          s = ST_ALREADY;
+        } else if (an == OW_NF || !(S[an] & SF_MADE)) {
+          s = ST_NOTFOUND;
+        } else {
+          uint32_t node = an, nk = an;  // findInsertion
+          uint32_t wn = S[node];
+          for (;;) {
+            const uint32_t rn = wn & PM;
+            if (rn == PM) break;
+            uint32_t live = rn, wl = S[rn];  // nextNode: the first live node from rn on
+            while (live != PM && (wl & SF_TOMB)) {
+              live = wl & PM;
+              if (live != PM) wl = S[live];
+            }
+            if (live == PM) break;
+            if (x > rn) break;  // ts > key(rn)
+            nk = rn;
+            node = live;
+            wn = wl;
+          }
+          const uint32_t wk = nk == node ? wn : S[nk];
+          S[x] = (wn & PM) | (wk & SF_ORPHAN) | SF_MADE;
+          if (nk == node) {
+            S[node] = (wn & ~PM) | x;
+          } else {
+            // copy quirk: slot nk := copy of node, next = x; the entries after
+            // nk up to node drop off the chain when nk was on it
+            if (!(wk & SF_ORPHAN)) {
+              for (uint32_t q2 = wk & PM; q2 != PM;) {
+                const uint32_t wq = S[q2];
+                S[q2] = wq | SF_ORPHAN;
+                if (q2 == node) break;
+                q2 = wq & PM;
+              }
+              wn |= SF_ORPHAN;
+            }
+            S[nk] = x | (wn & ~PM & ~SF_ORPHAN) | (wk & SF_ORPHAN) | SF_COPY;
+            uint32_t cs, cd, cb;
+            if (wn & SF_COPY) {
+              cs = p.qsrc[base + node];
+              cd = p.qcd[base + node];
+              cb = p.qcb[base + node];
+            } else {
+              cs = cd = p.rop[rb + node];
+              cb = bound;
+            }
+            p.qsrc[base + nk] = cs;
+            p.qcd[base + nk] = cd;
+            p.qcb[base + nk] = min(cb, i);
+            if (ORIG) atomicMin(&p.tcopy[p.rop[rb + nk]], i);
+          }
+          s = ST_APPLIED;
+        }
+      }
+      if (ORIG) st[i] = s;
+    }
+    if (ORIG) p.logn[D] = NONE;  // (no change log)
+  }
+}
+
 struct PdrTiers {
-  uint32_t* list[4];
-  uint32_t* count;  // [0..3] tier sizes, [4] largest slot count of tier 1, [5] most ops of a dict, [6] tier 3's
+  uint32_t* list[5];
+  uint32_t* count;  // [0..3] tier sizes, [4] largest slot count of tier 1, [5] most ops of a dict, [6] tier 3's,
+                    // [7] tier 4's size
   uint32_t blk_min;  // dicts of more slots than this (and at most blk_max) take pdr_blocked (tier 3)
   uint32_t blk_max;
+  uint32_t lane_max;  // dicts of at most this many slots and no change log: one lane each (tier 4; 0 = off)
 };
 
 // (Two passes over the instances: each workgroup counts its share per tier,
@@ -1001,24 +1112,25 @@ __device__ __forceinline__ uint32_t pdr_tier_of(const PdrCtx& p, uint32_t I, uin
   slots = pdr_kcount(p, D) + 1;
   uint32_t t = slots <= PDR_SMALL ? 0u : (slots <= big_cap ? 1u : 2u);
   if (slots > tt.blk_min && slots <= tt.blk_max) t = 3;
+  if (t == 0 && slots <= tt.lane_max && (I > n || p.log == nullptr || slots < p.log_min)) t = 4;
   return t;
 }
 
 __global__ void __launch_bounds__(BLOCK) k_pdr_tier(PdrCtx p, uint32_t i0, uint32_t i1, uint32_t big_cap,
                                                     PdrTiers tt) {
-  __shared__ uint32_t s_off[4];
+  __shared__ uint32_t s_off[5];
   const uint32_t n = p.o.n, m = i1 - i0, stride = gridDim.x * blockDim.x;
-  uint32_t c[4] = {0u, 0u, 0u, 0u};
+  uint32_t c[5] = {0u, 0u, 0u, 0u, 0u};
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < m; k += stride) {
     uint32_t slots, ops;
     const uint32_t t = pdr_tier_of(p, i0 + k, big_cap, tt, slots, ops);
 #pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) c[q] += t == q ? 1u : 0u;
+    for (uint32_t q = 0; q < 5; ++q) c[q] += t == q ? 1u : 0u;
   }
 #pragma unroll
-  for (uint32_t q = 0; q < 4; ++q) {
+  for (uint32_t q = 0; q < 5; ++q) {
     const uint32_t tot = block_sum(c[q]);
-    if (threadIdx.x == 0) s_off[q] = tot ? atomicAdd(&tt.count[q], tot) : 0u;
+    if (threadIdx.x == 0) s_off[q] = tot ? atomicAdd(&tt.count[q < 4 ? q : 7], tot) : 0u;
   }
   __syncthreads();
   uint32_t m4 = 0, m5 = 0, m6 = 0;
@@ -1030,8 +1142,8 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_tier(PdrCtx p, uint32_t i0, uint3
       t = pdr_tier_of(p, I, big_cap, tt, slots, ops);
       if (t != NONE && I <= n) p.I.base[I] = p.rbase[I];
     }
-    const uint32_t j = block_ticket<4, false>(s_off, t);
-    if (t < 4) tt.list[t][j] = I;
+    const uint32_t j = block_ticket<5, false>(s_off, t);
+    if (t < 5) tt.list[t][j] = I;
     if (t == 1) m4 = max(m4, slots);
     if (t == 3) m6 = max(m6, slots);
     m5 = max(m5, ops);
@@ -1379,11 +1491,11 @@ static int pdr_run_tiers(crdtm_ctx* c, const PdrCtx& p, uint32_t i0, uint32_t i1
   HIP_CHECK(hipMemsetAsync(tt.count, 0, 8 * sizeof(uint32_t), s));
   LAUNCH(k_pdr_tier, dim3(grid_for(i1 - i0, BLOCK, 512)), dim3(BLOCK), 0, s, p, i0, i1, big_cap, tt);
   HIP_CHECK(hipMemcpyAsync(hcount, tt.count, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
+  if (int rw = stream_wait(s)) return rw;
   const uint32_t* h = hcount;
   // the blocked tier (a few big dicts, one CU each, the longest replays) goes
   // first on the main stream; the other tiers run beside it on the side stream
-  const bool fork = h[3] && (h[0] || h[1] || h[2]);
+  const bool fork = h[3] && (h[0] || h[1] || h[2] || h[7]);
   hipStream_t s2 = fork ? c->side : s;
   if (fork) {
     HIP_CHECK(hipEventRecord(c->ev_fork, s));
@@ -1394,6 +1506,10 @@ static int pdr_run_tiers(crdtm_ctx* c, const PdrCtx& p, uint32_t i0, uint32_t i1
     if (orig && p.gcount) LAUNCH(k_pdr_blk<2>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st, big_cap);
     else if (orig) LAUNCH(k_pdr_blk<1>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st, big_cap);
     else LAUNCH(k_pdr_blk<0>, dim3(h[3]), dim3(64), lds, s, p, tt.list[3], st, big_cap);
+  }
+  if (h[7]) {  // (no tier 4 with the guard-G statistics: lane_max = 0)
+    if (orig) LAUNCH(k_pdr_lane<1>, dim3(grid_for(h[7])), dim3(BLOCK), 0, s2, p, tt.list[4], h[7], st);
+    else LAUNCH(k_pdr_lane<0>, dim3(grid_for(h[7])), dim3(BLOCK), 0, s2, p, tt.list[4], h[7], st);
   }
   if (h[0]) {
     if (orig && p.gcount) LAUNCH(k_pdr_small<2>, dim3(h[0]), dim3(64), 0, s2, p, tt.list[0], st);
@@ -1510,8 +1626,11 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   HIP_CHECK(hipMemsetAsync(last, 0, 3ULL * SCAP * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(p.ilog, 0xFF, ICAP * sizeof(uint32_t), s));
   PdrTiers tt;
-  for (int k = 0; k < 4; ++k) tt.list[k] = ws.alloc<uint32_t>(ICAP);
+  for (int k = 0; k < 5; ++k) tt.list[k] = ws.alloc<uint32_t>(ICAP);
   tt.count = ws.alloc<uint32_t>(8);
+  // tiny dicts replay one per lane (env CRDTM_PDR_LANE: the slot bound, 0 = off); not with the guard statistics
+  tt.lane_max = PDR_LANE;
+  if (const char* e = getenv("CRDTM_PDR_LANE")) tt.lane_max = static_cast<uint32_t>(strtoul(e, nullptr, 10));
   tt.blk_min = BLK_MIN;
   if (const char* e = getenv("CRDTM_PDR_BLK_MIN")) tt.blk_min = static_cast<uint32_t>(strtoul(e, nullptr, 10));
   // the blocked order holds a dict's flags (2 B per slot) and its chain
@@ -1547,18 +1666,19 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
     if (!c->gstat_dev) HIP_CHECK(hipMalloc(&c->gstat_dev, 4 * sizeof(unsigned long long)));
     HIP_CHECK(hipMemsetAsync(c->gstat_dev, 0, 4 * sizeof(unsigned long long), s));
     p.gcount = c->gstat_dev;
+    tt.lane_max = 0;  // (the statistics come from the wave replays)
   }
   if ((r = pdr_run_tiers(c, p, 0, n + 1, true, st, tt, big_cap, hcount))) return r;
 #ifdef PDR_STATS
   {
     unsigned long long z[8];
-    HIP_CHECK(hipStreamSynchronize(s));
+    if (int rw = stream_wait(s)) return rw;
     HIP_CHECK(hipMemcpyFromSymbol(z, HIP_SYMBOL(g_pdr_stats), sizeof(z)));
     std::fprintf(stderr, "pdr stats: adds %llu walk-steps %llu window-steps %llu tomb-skips %llu quirks %llu\n",
                  z[4], z[0], z[1], z[2], z[3]);
   }
 #endif
-  res->serial_dicts = static_cast<uint64_t>(hcount[0]) + hcount[1] + hcount[2] + hcount[3];
+  res->serial_dicts = static_cast<uint64_t>(hcount[0]) + hcount[1] + hcount[2] + hcount[3] + hcount[7];
   res->serial_ops = n;  // every op, in order within its dict
   res->serial_max = hcount[5];
   LAUNCH(k_pdr_stats_reset, dim3(1), dim3(1), 0, s, dr);

@@ -408,7 +408,7 @@ static int segmented_sort_t(const uint32_t* seg_start, uint32_t n_seg, uint32_t*
   LAUNCH(k_sort_big_filter, dim3(16), dim3(BLOCK), 0, st, seg_start, big, nbig, huge, nhuge);
   uint32_t cn[3] = {0, 0, 0};  // big, huge, mid
   HIP_CHECK(hipMemcpyAsync(cn, nbig, sizeof(cn), hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipStreamSynchronize(st));
+  if (int rw = stream_wait(st)) return rw;
   const uint32_t nh = cn[1];
   static const bool stats = getenv("CRDTM_SORT_STATS") != nullptr;
   if (stats)
@@ -430,7 +430,7 @@ static int segmented_sort_t(const uint32_t* seg_start, uint32_t n_seg, uint32_t*
   LAUNCH(k_huge_meta, dim3(1), dim3(BLOCK), 0, st, seg_start, huge, ht, meta);
   uint32_t hm[3];
   HIP_CHECK(hipMemcpyAsync(hm, meta, sizeof(hm), hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipStreamSynchronize(st));
+  if (int rw = stream_wait(st)) return rw;
   LAUNCH(k_sort_chunks<KEY>, dim3(hm[0]), dim3(1024), 0, st, carr, ht, sort_key);
   uint32_t* src = carr;
   uint32_t* dst = scratch;

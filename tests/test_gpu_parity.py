@@ -86,12 +86,15 @@ def test_synthetic_streams(name):
         assert res.path_taken == N.PATH_CLOSED_FORM, f"expected the closed form, guard={res.guard}"
 
 
+@pytest.mark.parametrize("lane", ["32", "0"])
 @pytest.mark.parametrize("chunk", range(8))
-def test_adversarial_streams(chunk):
+def test_adversarial_streams(monkeypatch, chunk, lane):
     """Interleaved Deletes and tombstone walks (copy quirks, nested dicts):
     the per-dict replay, its conflict fallback and the sequential replay all
-    match the oracle."""
+    match the oracle. lane: dicts of at most that many slots replay one per
+    lane (k_pdr_lane, the default), or (0) every dict on a wave (pdr_serial)."""
     from adversarial import adversarial
+    monkeypatch.setenv("CRDTM_PDR_LANE", lane)
     paths = {}
     for seed in range(16 * chunk, 16 * chunk + 16):
         n = [40, 120, 400, 1500][seed % 4]
