@@ -240,6 +240,8 @@ int take_replicas(crdtm_tree* t, const long long* rep_dev);
 // incr.hip: adds-only flat batch into a clean flat tree; *handled = false leaves it to apply_batch
 int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res, bool* handled);
 __global__ void k_reset_root(uint32_t* s_next);
+// each group's first position in sorted keys (NONE: no group) (merge.hip)
+__global__ void k_doc_gstart(const uint32_t* sk, uint32_t m, uint32_t* gs);
 int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& ws);
 // pdr.hip
 int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdtm_result* res, bool* handled);

@@ -131,16 +131,6 @@ __device__ __forceinline__ bool pdr_is_key(const OpsDev& o, const TsIndex& ix, u
   return ts != 0 && tsindex_find(ix, ts) == i;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_pdr_count(OpsDev o, TsIndex ix, const uint32_t* tag, const uint32_t* cur,
-                                                     uint32_t* cnt, uint32_t* ccnt) {
-  GRID_STRIDE(i, o.n) {
-    if (tag[i] != PDR_REACHED) continue;
-    const uint32_t d = cur[i];
-    atomicAdd(&cnt[d], 1u);
-    if (pdr_is_key(o, ix, i)) atomicAdd(&ccnt[d], 1u);
-  }
-}
-
 // region size: one position per reached op + 1 (sentinel slot / list pad);
 // the root dict always exists
 __global__ void __launch_bounds__(BLOCK) k_pdr_size(uint32_t n, uint32_t* cnt) {
@@ -150,14 +140,46 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_size(uint32_t n, uint32_t* cnt) {
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_pdr_scatter(OpsDev o, TsIndex ix, const uint32_t* tag, const uint32_t* cur,
-                                                       const uint32_t* rbase, uint32_t* fill, uint32_t* olist,
-                                                       const uint32_t* cbase, uint32_t* cfill, uint32_t* carr) {
-  GRID_STRIDE(i, o.n) {
-    if (tag[i] != PDR_REACHED) continue;
-    const uint32_t d = cur[i];
-    olist[rbase[d] + atomicAdd(&fill[d], 1u)] = i;  // the pad (NONE) stays last
-    if (pdr_is_key(o, ix, i)) carr[cbase[d] + atomicAdd(&cfill[d], 1u)] = i;
+// Grouping without atomics (replaces k_pdr_count / k_pdr_scatter, which
+// took two random device atomics per op): a stable radix sort of the ops by
+// dict (key NONE: not reached) keeps each dict's ops in batch order; the
+// group sizes come from the sorted keys, and a scan over the sorted positions
+// of "this op is a key" (the first Add of its timestamp) numbers the keys
+// inside each dict.
+__global__ void __launch_bounds__(BLOCK) k_pdr_keys(uint32_t n, const uint32_t* tag, const uint32_t* cur,
+                                                    uint32_t* key, uint32_t* val, uint32_t* nitems) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *nitems = n;
+  GRID_STRIDE(i, n) {
+    key[i] = tag[i] == PDR_REACHED ? cur[i] : NONE;
+    val[i] = i;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_pdr_kflag(OpsDev o, TsIndex ix, const uint32_t* sk, const uint32_t* sv,
+                                                     uint32_t* kf) {
+  GRID_STRIDE(k, o.n + 1) kf[k] = k < o.n && sk[k] != NONE && pdr_is_key(o, ix, sv[k]) ? 1u : 0u;
+}
+
+// per dict (at its last sorted position): ops (into rbase) and keys (into cbase)
+__global__ void __launch_bounds__(BLOCK) k_pdr_gcount(uint32_t m, const uint32_t* sk, const uint32_t* gs,
+                                                      const uint32_t* X, uint32_t* cnt, uint32_t* ccnt) {
+  GRID_STRIDE(k, m) {
+    const uint32_t d = sk[k];
+    if (d == NONE || (k + 1 < m && sk[k + 1] == d)) continue;
+    cnt[d] = k + 1 - gs[d];
+    ccnt[d] = X[k + 1] - X[gs[d]];
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_pdr_place(uint32_t m, const uint32_t* sk, const uint32_t* sv,
+                                                     const uint32_t* gs, const uint32_t* X, const uint32_t* rbase,
+                                                     const uint32_t* cbase, uint32_t* olist, uint32_t* carr) {
+  GRID_STRIDE(k, m) {
+    const uint32_t d = sk[k];
+    if (d == NONE) continue;
+    const uint32_t g = gs[d], i = sv[k];
+    olist[rbase[d] + (k - g)] = i;  // the pad (NONE) stays last
+    if (X[k + 1] != X[k]) carr[cbase[d] + (X[k] - X[g])] = i;
   }
 }
 
@@ -1579,7 +1601,25 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   p.rankof = ws.alloc<uint32_t>(n);
   p.tcopy = ws.alloc<uint32_t>(n);
   LAUNCH(k_pdr_init, dim3(grid_for(n + 2)), dim3(BLOCK), 0, s, n, rbase, fill, cbase, cfill, p.rankof, p.tcopy);
-  LAUNCH(k_pdr_count, dim3(g), dim3(BLOCK), 0, s, o, in.ix, in.tag, in.cur, rbase, cbase);
+  // ops grouped by dict (stable radix sort: batch order inside each dict), per-dict op and key counts
+  uint32_t* gs = fill;  // [n + 2] each dict's first sorted position
+  uint32_t* X = cfill;  // [n + 2] exclusive scan over the sorted positions of "is a key"
+  uint32_t *sk = nullptr, *sv = nullptr;
+  {
+    uint32_t* ka = ws.alloc<uint32_t>(n);
+    uint32_t* va = ws.alloc<uint32_t>(n);
+    uint32_t* kb = ws.alloc<uint32_t>(n);
+    uint32_t* vb = ws.alloc<uint32_t>(n);
+    uint32_t* nitems = ws.alloc<uint32_t>(1);
+    LAUNCH(k_pdr_keys, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, n, in.tag, in.cur, ka, va, nitems);
+    uint32_t kbits = 8;  // NONE (not reached) sorts after every dict id <= n
+    while (kbits < 32 && ((static_cast<uint64_t>(n) + 1) >> kbits) != 0) kbits += 8;
+    if ((r = radix_sort_pairs(ka, va, kb, vb, nitems, n, kbits, ws, s, &sk, &sv))) return r;
+    LAUNCH(k_doc_gstart, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, sk, n, gs);
+    LAUNCH(k_pdr_kflag, dim3(grid_for(n + 1, BLOCK, 2048)), dim3(BLOCK), 0, s, o, in.ix, sk, sv, X);
+    if ((r = scan_excl_u32(X, X, n + 1, nullptr, ws, s))) return r;
+    LAUNCH(k_pdr_gcount, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, n, sk, gs, X, rbase, cbase);
+  }
   LAUNCH(k_pdr_size, dim3(grid_for(n + 1)), dim3(BLOCK), 0, s, n, rbase);
   if ((r = scan_excl_u32(rbase, rbase, n + 2, &dr->pdr_slots, ws, s))) return r;
   if ((r = scan_excl_u32(cbase, cbase, n + 2, &dr->pdr_dicts, ws, s))) return r;
@@ -1593,8 +1633,7 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   uint32_t* carr = ws.alloc<uint32_t>(KT + 1);
   p.olist = olist;
   HIP_CHECK(hipMemsetAsync(olist, 0xFF, static_cast<size_t>(R0) * sizeof(uint32_t), s));
-  LAUNCH(k_pdr_scatter, dim3(g), dim3(BLOCK), 0, s, o, in.ix, in.tag, in.cur, rbase, fill, olist, cbase, cfill, carr);
-  if ((r = segmented_sort_asc_id(rbase, n + 1, olist, R0, ws, s, dr))) return r;
+  LAUNCH(k_pdr_place, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, n, sk, sv, gs, X, rbase, cbase, olist, carr);
   if ((r = segmented_sort(cbase, n + 1, carr, KT, o.ts, ws, s, dr))) return r;
   p.rop = ws.alloc<uint32_t>(R0);
   LAUNCH(k_pdr_rank, dim3(grid_for(KT)), dim3(BLOCK), 0, s, KT, carr, in.cur, cbase, rbase, p.rankof, p.rop);
