@@ -146,18 +146,21 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_size(uint32_t n, uint32_t* cnt) {
 // group sizes come from the sorted keys, and a scan over the sorted positions
 // of "this op is a key" (the first Add of its timestamp) numbers the keys
 // inside each dict.
-__global__ void __launch_bounds__(BLOCK) k_pdr_keys(uint32_t n, const uint32_t* tag, const uint32_t* cur,
+// (val = the op | is-a-key << 31, decided here in op order: coalesced kinds
+// and timestamps; op indices stay below 2^31)
+__global__ void __launch_bounds__(BLOCK) k_pdr_keys(OpsDev o, TsIndex ix, const uint32_t* tag, const uint32_t* cur,
                                                     uint32_t* key, uint32_t* val, uint32_t* nitems) {
+  const uint32_t n = o.n;
   if (blockIdx.x == 0 && threadIdx.x == 0) *nitems = n;
   GRID_STRIDE(i, n) {
-    key[i] = tag[i] == PDR_REACHED ? cur[i] : NONE;
-    val[i] = i;
+    const bool reached = tag[i] == PDR_REACHED;
+    key[i] = reached ? cur[i] : NONE;
+    val[i] = i | ((reached && pdr_is_key(o, ix, i)) ? 0x80000000u : 0u);
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_pdr_kflag(OpsDev o, TsIndex ix, const uint32_t* sk, const uint32_t* sv,
-                                                     uint32_t* kf) {
-  GRID_STRIDE(k, o.n + 1) kf[k] = k < o.n && sk[k] != NONE && pdr_is_key(o, ix, sv[k]) ? 1u : 0u;
+__global__ void __launch_bounds__(BLOCK) k_pdr_kflag(uint32_t n, const uint32_t* sv, uint32_t* kf) {
+  GRID_STRIDE(k, n + 1) kf[k] = k < n ? sv[k] >> 31 : 0u;
 }
 
 // per dict (at its last sorted position): ops (into rbase) and keys (into cbase)
@@ -177,7 +180,7 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_place(uint32_t m, const uint32_t*
   GRID_STRIDE(k, m) {
     const uint32_t d = sk[k];
     if (d == NONE) continue;
-    const uint32_t g = gs[d], i = sv[k];
+    const uint32_t g = gs[d], i = sv[k] & 0x7FFFFFFFu;
     olist[rbase[d] + (k - g)] = i;  // the pad (NONE) stays last
     if (X[k + 1] != X[k]) carr[cbase[d] + (X[k] - X[g])] = i;
   }
@@ -1611,12 +1614,12 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
     uint32_t* kb = ws.alloc<uint32_t>(n);
     uint32_t* vb = ws.alloc<uint32_t>(n);
     uint32_t* nitems = ws.alloc<uint32_t>(1);
-    LAUNCH(k_pdr_keys, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, n, in.tag, in.cur, ka, va, nitems);
+    LAUNCH(k_pdr_keys, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, o, in.ix, in.tag, in.cur, ka, va, nitems);
     uint32_t kbits = 8;  // NONE (not reached) sorts after every dict id <= n
     while (kbits < 32 && ((static_cast<uint64_t>(n) + 1) >> kbits) != 0) kbits += 8;
     if ((r = radix_sort_pairs(ka, va, kb, vb, nitems, n, kbits, ws, s, &sk, &sv))) return r;
     LAUNCH(k_doc_gstart, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, sk, n, gs);
-    LAUNCH(k_pdr_kflag, dim3(grid_for(n + 1, BLOCK, 2048)), dim3(BLOCK), 0, s, o, in.ix, sk, sv, X);
+    LAUNCH(k_pdr_kflag, dim3(grid_for(n + 1, BLOCK, 2048)), dim3(BLOCK), 0, s, n, sv, X);
     if ((r = scan_excl_u32(X, X, n + 1, nullptr, ws, s))) return r;
     LAUNCH(k_pdr_gcount, dim3(grid_for(n, BLOCK, 2048)), dim3(BLOCK), 0, s, n, sk, gs, X, rbase, cbase);
   }
