@@ -302,6 +302,7 @@ int crdtm_tree_reset(crdtm_tree* t, int64_t replica_id) {
   t->log_npath = 0;
   t->doc_n = 0;
   t->doc_valid = true;
+  t->doc_gapped = false;
   t->max_depth = 0;
   t->timestamp = replica_id * TWO32;
   t->replicas.clear();
@@ -326,6 +327,18 @@ int crdtm_tree_destroy(crdtm_tree* t) {
 // src/CRDTree.elm:228-232: the old value stays valid after apply).
 int crdtm_tree_clone(const crdtm_tree* t, crdtm_tree** out) {
   if (!t || !out) return CRDTM_E_ARG;
+  if (t->doc_gapped) {  // the order lives in t's own index: write the shared `doc` from it first
+    auto* tw = const_cast<crdtm_tree*>(t);
+    crdtm_ctx* c = t->ctx;
+    HIP_CHECK(hipSetDevice(c->device));
+    int r = ensure_arena(c, arena_need(0, 0, tw) + 64 * (t->n_slots + t->n_dicts));
+    if (r) return r;
+    try {
+      if ((r = linearize(tw))) return r;
+    } catch (const ArenaOverflow&) {
+      return CRDTM_E_NOMEM;
+    }
+  }
   auto* u = new crdtm_tree;
   u->ctx = t->ctx;
   u->d = t->d;

@@ -134,19 +134,33 @@ struct crdtm_ctx {
 
 namespace crdtm {
 // Index of a clean flat tree for the incremental closed form (incr.hip), owned
-// by one tree handle: key -> slot (hash), the keys in document order (two
-// buffers: each merge writes the other) and slot -> document rank.
+// by one tree handle: key -> slot (hash), and the document order as a gapped
+// array of blocks (FI_CAP positions each, a quarter full when built):
+// slot ids and keys per position (padding positions hold the key +inf),
+// entries per block, the smallest key per 64 positions and per 4096, and
+// slot -> position. An adds-only batch shifts entries inside the blocks it
+// lands in only; a block that would overflow spreads an aligned window of
+// up to 64 blocks evenly (a packed-memory array), and only a window that
+// cannot take it rebuilds the layout.
 struct KeyIndex {
   unsigned long long* keys = nullptr;  // ts ^ INT64_MIN, 0 = empty (TsHash layout)
   uint32_t* vals = nullptr;
   uint32_t mask = 0;
-  long long* dk[2] = {nullptr, nullptr};
-  uint32_t* rank = nullptr;
-  uint32_t* doc2 = nullptr;  // the next document order (swapped with the tree's `doc` by each merge)
+  uint32_t* bent = nullptr;  // [nbk * FI_CAP] slot per position
+  long long* bdk = nullptr;  // [nbk * FI_CAP] key per position, +inf = padding
+  uint32_t* bcnt = nullptr;  // [nbk] entries per block (>= 1)
+  uint32_t* bfirst = nullptr;  // [nbk] a batch's new nodes of the block: sorted range
+  uint32_t* bend = nullptr;    //   [bfirst, bend) (both 0 between batches)
+  uint32_t* bwin = nullptr;  // [nbk] level + 1 of the rebalance window over the block (0 between batches)
+  long long* bmin = nullptr; // [nbk FI_CAP / 64] smallest key per 64 positions
+  long long* smin = nullptr; // smallest key per 4096 positions
+  uint64_t bcap = 0;         // blocks the arrays hold
+  uint32_t nbk = 0;          // blocks in use
+  uint32_t* rank = nullptr;  // slot -> position
+  uint64_t rcap = 0;
+  uint32_t* doc2 = nullptr;  // the next dense order (a rebuild's merge)
   uint64_t doc2_cap = 0;
-  uint64_t ocap = 0;  // entries of dk[*] and rank
-  int cur = 0;
-  bool ord_ready = false;
+  bool ord_ready = false;  // the blocks describe the tree's document
   ~KeyIndex();
 };
 }  // namespace crdtm
@@ -157,6 +171,9 @@ struct crdtm_tree {
   crdtm::TreeCaps cap;
   uint64_t n_slots = 0, n_dicts = 0, log_n = 0, log_npath = 0, doc_n = 0;
   bool doc_valid = false;
+  // the document order is current in kidx's blocks, `doc` is not (incr.hip);
+  // linearize() writes `doc` from them
+  bool doc_gapped = false;
   uint32_t max_depth = 0;
   int64_t timestamp = 0;
   std::map<int64_t, int64_t> replicas;
@@ -199,6 +216,10 @@ int segmented_sort_asc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* c
 // stable LSD radix sort of (key, value) pairs by the low `bits` key bits (primitives.hip)
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, const uint32_t* n_dev, uint32_t n_max,
                      uint32_t bits, Arena& ws, hipStream_t st, uint32_t** out_k, uint32_t** out_v);
+// the same for n <= RS_SMALL_MAX pairs in one workgroup (primitives.hip), into (kout, vout)
+constexpr uint32_t RS_SMALL_MAX = 16384;
+int radix_sort_small(const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t bits, uint32_t* kout,
+                     uint32_t* vout, hipStream_t st);
 // ent[e] = {succ, wbits}: see primitives.hip / listrank.h (list_rank_fused)
 int list_rank(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws, hipStream_t st);
 int list_rank_packed(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws,
@@ -251,6 +272,7 @@ int grow_tree(crdtm_tree* t, const TreeCaps& need);
 int unshare_tree(crdtm_tree* t, bool keep_contents);
 int apply_batch(crdtm_tree* t, const OpsDev& ops, uint8_t* status_dev, crdtm_result* res);
 int linearize(crdtm_tree* t);  // fills t->d.doc / t->doc_n from the tree state
+int fi_materialize(crdtm_tree* t);  // incr.hip: `doc` from the gapped order (doc_gapped)
 int forest_apply(crdtm_ctx* c, int64_t replica_id, const OpsDev& o, const uint32_t* doc_off_host, uint64_t n_docs,
                  int32_t* code, int64_t* err, uint32_t* applied, uint64_t* vhash, uint64_t* vwords, int64_t* tstamp);
 uint64_t forest_ws_bytes(const uint32_t* doc_off_host, uint64_t n_docs, uint64_t n_ops, uint64_t n_path);

@@ -23,7 +23,16 @@
 // Every other case — a Delete, a nested path, a duplicate or existing key, an
 // anchor that is missing or later in the batch, replica-id drift, a tree that
 // is not a clean flat document — is left to the general paths (merge.hip).
+//
+// The base order lives in a gapped array (KeyIndex, engine.h): blocks of
+// FI_CAP positions, built a quarter full, padding keyed +inf so the NSR searches
+// run over it unchanged. A batch rewrites only the blocks its gaps fall in
+// (O(batch) positions, not O(document)); a block that would overflow makes
+// that batch merge densely (O(document)) and rebuild the blocks with fresh
+// slack. The tree's dense `doc` is written from the blocks when read
+// (linearize -> fi_materialize).
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 
 #include "engine.h"
@@ -31,18 +40,31 @@
 
 namespace crdtm {
 
-constexpr uint32_t FI_BLK = 64;             // ranks per block minimum (one wave)
-constexpr uint32_t FI_SUP = 64;             // blocks per superblock
+constexpr uint32_t FI_BLK = 64;             // positions per minimum (one wave)
+constexpr uint32_t FI_SUP = 64;             // minima per superblock minimum
+constexpr uint32_t FI_CAP = 256;            // positions per block of the gapped order
+constexpr uint32_t FI_FILL = 64;            // entries per block when (re)built
 constexpr uint32_t FI_MAX_BATCH = 1u << 14; // larger batches re-merge (k_fi_jump holds 16 per thread)
 constexpr uint32_t FI_GAP_STEPS = 1u << 22; // walk budget per gap (else re-merge)
 constexpr long long FI_INF = 0x7fffffffffffffffLL;
+constexpr uint32_t FI_BPB = FI_CAP / FI_BLK;  // minima per block (one per wave of k_fi_rewrite)
+static_assert(FI_CAP % FI_BLK == 0 && FI_CAP <= 1024, "whole waves per block");
 
-// flags word bits (fi[0])
-enum : uint32_t { FI_FAIL = 1u, FI_BUDGET = 2u };
+constexpr uint32_t FI_WIN_MAX = 6;          // rebalance windows of up to 2^6 blocks
+constexpr uint32_t FI_WIN_ENT = (FI_CAP << FI_WIN_MAX) / 2;  // entries of the largest window (half full)
+constexpr uint32_t FI_WIN_THREADS = 1024;
+
+// flags word bits (fi[0]); FI_OVER alone: no window takes a block's batch,
+// merge densely. fi[1] own-replica Adds, fi[2] gaps, fi[3] blocks landed in,
+// fi[4] overflowing blocks, fi[5] rebalance windows
+enum : uint32_t { FI_FAIL = 1u, FI_BUDGET = 2u, FI_OVER = 4u };
+constexpr uint32_t FI_WORDS = 8;
 
 KeyIndex::~KeyIndex() {
-  for (void* q : {static_cast<void*>(keys), static_cast<void*>(vals), static_cast<void*>(dk[0]),
-                  static_cast<void*>(dk[1]), static_cast<void*>(rank), static_cast<void*>(doc2)})
+  for (void* q : {static_cast<void*>(keys), static_cast<void*>(vals), static_cast<void*>(bent),
+                  static_cast<void*>(bdk), static_cast<void*>(bcnt), static_cast<void*>(bend),
+                  static_cast<void*>(bfirst), static_cast<void*>(bwin), static_cast<void*>(bmin),
+                  static_cast<void*>(smin), static_cast<void*>(rank), static_cast<void*>(doc2)})
     if (q) hipFree(q);
 }
 
@@ -58,13 +80,28 @@ __global__ void __launch_bounds__(BLOCK) k_kx_insert(OpsDev o, uint32_t slot0, T
   GRID_STRIDE(i, o.n) tshash_insert(h, o.ts[i], slot0 + i);
 }
 
-// dk[r] = key of doc[r], rank_of[slot] = r (when the index has no document order yet)
-__global__ void __launch_bounds__(BLOCK) k_fi_prep(uint32_t K, const uint32_t* doc, const long long* s_key,
-                                                   long long* dk, uint32_t* rank_of) {
-  GRID_STRIDE(r, K) {
-    const uint32_t sl = doc[r];
-    dk[r] = s_key[sl];
-    rank_of[sl] = r;
+// the gapped order from a dense one: block b holds ranks [FI_FILL b, FI_FILL b + FI_FILL)
+__global__ void __launch_bounds__(BLOCK) k_fi_build(uint32_t K, uint32_t nbk, const uint32_t* doc,
+                                                    const long long* s_key, uint32_t* bent, long long* bdk,
+                                                    uint32_t* bcnt, uint32_t* bfirst, uint32_t* bend,
+                                                    uint32_t* bwin, uint32_t* rank_of) {
+  GRID_STRIDE(p, nbk * FI_CAP) {
+    const uint32_t b = p / FI_CAP, j = p % FI_CAP, r = b * FI_FILL + j;
+    if (j < FI_FILL && r < K) {
+      const uint32_t sl = doc[r];
+      bent[p] = sl;
+      bdk[p] = s_key[sl];
+      rank_of[sl] = p;
+    } else {
+      bent[p] = NONE;
+      bdk[p] = FI_INF;
+    }
+    if (j == 0) {
+      bcnt[b] = min(FI_FILL, K - b * FI_FILL);
+      bfirst[b] = 0;
+      bend[b] = 0;
+      bwin[b] = 0;
+    }
   }
 }
 
@@ -104,6 +141,17 @@ __global__ void __launch_bounds__(BLOCK) k_fi_sup(uint32_t nb, const long long* 
     for (uint32_t b = s * FI_SUP; b < e; ++b) m = min(m, bmin[b]);
     smin[s] = m;
   }
+}
+
+__device__ __forceinline__ long long wave_min64(long long k) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = __shfl_xor(static_cast<uint32_t>(k), o, 64);
+    const uint32_t hi = __shfl_xor(static_cast<uint32_t>(static_cast<unsigned long long>(k) >> 32), o, 64);
+    const long long v = static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo);
+    k = v < k ? v : k;
+  }
+  return k;
 }
 
 // batch keys -> op index; a key seen twice fails the batch
@@ -167,34 +215,47 @@ __global__ void __launch_bounds__(BLOCK) k_fi_resolve(OpsDev o, TsHash kx, TsHas
   }
 }
 
-// Pointer jumping, all rounds in one workgroup: (start, min threshold)
-// composed along the new anchors. Each round reads every element's jumped
-// values into registers, then (after a barrier) writes them back in place:
-// no second buffer, and chains are short (typing runs), so the rounds stop
-// once no anchor is left. Up to FI_JUMP_PER elements per thread.
+// Pointer jumping, all rounds in one workgroup, in LDS: each op's pointer
+// to its farthest known new ancestor (u16) and the op of the smallest
+// timestamp on the chain up to it (u16, the timestamp itself kept in
+// registers for the thread's own ops). A pointer stops at the chain's root
+// (the op whose anchor is a base node); the rounds stop once none moved.
+// Then (start, threshold) = (the root's start, min(chain min, root's ts)).
 constexpr uint32_t FI_JUMP_THREADS = 1024, FI_JUMP_PER = 16;
-__global__ void __launch_bounds__(FI_JUMP_THREADS) k_fi_jump(uint32_t m, uint32_t rounds, uint32_t* P, uint32_t* S,
-                                                             long long* T) {
-  __shared__ uint32_t live[32];  // one flag per round (rounds <= 16: m <= 2^16)
-  if (threadIdx.x < 32) live[threadIdx.x] = 0;
+constexpr uint16_t FI_J_NONE = 0xFFFFu;
+static_assert(FI_JUMP_THREADS * FI_JUMP_PER >= FI_MAX_BATCH && FI_MAX_BATCH <= FI_J_NONE, "u16 op indices");
+__global__ void __launch_bounds__(FI_JUMP_THREADS) k_fi_jump(uint32_t m, uint32_t rounds, const uint32_t* P,
+                                                             uint32_t* S, long long* T, const long long* ts) {
+  __shared__ uint16_t lp[FI_JUMP_THREADS * FI_JUMP_PER], lt[FI_JUMP_THREADS * FI_JUMP_PER];
+  uint16_t mp[FI_JUMP_PER], mt[FI_JUMP_PER];
+  long long mv[FI_JUMP_PER];
+#pragma unroll
+  for (uint32_t u = 0; u < FI_JUMP_PER; ++u) {
+    const uint32_t i = threadIdx.x + u * FI_JUMP_THREADS;
+    const uint32_t p = i < m ? P[i] : NONE;
+    mp[u] = p == NONE ? FI_J_NONE : static_cast<uint16_t>(p);
+    mt[u] = static_cast<uint16_t>(i);
+    mv[u] = i < m ? T[i] : 0;
+    lp[i] = mp[u];
+    lt[i] = mt[u];
+  }
   __syncthreads();
   for (uint32_t k = 0; k < rounds; ++k) {
-    uint32_t np[FI_JUMP_PER], ns[FI_JUMP_PER];
-    long long nt[FI_JUMP_PER];
-    uint32_t any = 0;
+    int moved = 0;
 #pragma unroll
     for (uint32_t u = 0; u < FI_JUMP_PER; ++u) {
-      const uint32_t i = threadIdx.x + u * FI_JUMP_THREADS;
-      np[u] = NONE;
-      if (i < m) {
-        const uint32_t p = P[i];
-        ns[u] = S[i];
-        nt[u] = T[i];
-        if (p != NONE) {
-          np[u] = P[p];
-          ns[u] = S[p];
-          nt[u] = min(nt[u], T[p]);
-          any |= np[u] != NONE;
+      const uint16_t p = mp[u];
+      if (p != FI_J_NONE) {
+        const uint16_t pp = lp[p];
+        if (pp != FI_J_NONE) {  // T over [i, p) composed with T over [p, pp)
+          const uint16_t tq = lt[p];
+          const long long tv = ts[tq];
+          if (tv < mv[u]) {
+            mv[u] = tv;
+            mt[u] = tq;
+          }
+          mp[u] = pp;
+          moved = 1;
         }
       }
     }
@@ -202,15 +263,19 @@ __global__ void __launch_bounds__(FI_JUMP_THREADS) k_fi_jump(uint32_t m, uint32_
 #pragma unroll
     for (uint32_t u = 0; u < FI_JUMP_PER; ++u) {
       const uint32_t i = threadIdx.x + u * FI_JUMP_THREADS;
-      if (i < m) {
-        P[i] = np[u];
-        S[i] = ns[u];
-        T[i] = nt[u];
-      }
+      lp[i] = mp[u];
+      lt[i] = mt[u];
     }
-    if (any) live[k] = 1;
-    __syncthreads();  // writes visible to the workgroup, live[k] final
-    if (!live[k]) break;
+    if (!__syncthreads_or(moved)) break;
+  }
+#pragma unroll
+  for (uint32_t u = 0; u < FI_JUMP_PER; ++u) {
+    const uint32_t i = threadIdx.x + u * FI_JUMP_THREADS;
+    const uint16_t r = mp[u];
+    if (i < m && r != FI_J_NONE) {
+      S[i] = S[r];  // (a root's own start: roots are not written)
+      T[i] = min(mv[u], ts[r]);
+    }
   }
 }
 
@@ -252,16 +317,291 @@ __global__ void __launch_bounds__(BLOCK) k_fi_gap(uint32_t m, uint32_t K, const 
   }
 }
 
-__global__ void k_fi_setn(uint32_t* p, uint32_t v) { *p = v; }
-
 __global__ void __launch_bounds__(BLOCK) k_fi_pos(uint32_t m, const uint32_t* gv, uint32_t* pos) {
   GRID_STRIDE(k, m) pos[gv[k]] = k;
 }
 
-// gap heads: the first sorted position of every gap, listed (any order)
+// gap heads: the first sorted position of every gap, listed (any order);
+// one item per thread (wave-aggregated tickets: ~10k heads on one counter)
 __global__ void __launch_bounds__(BLOCK) k_fi_gstart(uint32_t m, const uint32_t* gk, uint32_t* list, uint32_t* cnt) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool head = k < m && (k == 0 || gk[k - 1] != gk[k]);
+  const uint32_t t = wave_ticket(cnt, head);
+  if (head) list[t] = k;
+}
+
+// block of a gap position (Kp = past the end: the last block)
+__device__ __forceinline__ uint32_t fi_blk(uint32_t g, uint32_t Kp) { return (g < Kp ? g : Kp - 1) / FI_CAP; }
+
+// blocks the batch lands in: the first sorted position of each, listed (any
+// order) in tl / fi[3], with their sorted range [bfirst, bend) per block; and
+// the entry before each gap's first new node, from the layout before the
+// batch (gpred: a base entry, since gaps are separated by their base nodes)
+__global__ void __launch_bounds__(BLOCK) k_fi_tblk(uint32_t m, uint32_t nbk, const uint32_t* sk, const uint32_t* ord,
+                                                   const uint32_t* bent, const uint32_t* bcnt, uint32_t* bfirst,
+                                                   uint32_t* bend, uint32_t* tl, uint32_t* gpred, uint32_t* fi) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x, Kp = nbk * FI_CAP;
+  uint32_t b = 0;
+  bool head = false;
+  if (k < m) {
+    const uint32_t g = sk[k];
+    b = fi_blk(g, Kp);
+    head = k == 0 || fi_blk(sk[k - 1], Kp) != b;
+    if (head) bfirst[b] = k;
+    if (k + 1 == m || fi_blk(sk[k + 1], Kp) != b) bend[b] = k + 1;
+    if (ord[k] == 0) {
+      uint32_t pr;
+      if (g >= Kp) pr = bent[(nbk - 1) * FI_CAP + bcnt[nbk - 1] - 1];
+      else if (g % FI_CAP) pr = bent[g - 1];
+      else pr = b ? bent[(b - 1) * FI_CAP + bcnt[b - 1] - 1] : 0u;
+      gpred[k] = pr;
+    }
+  }
+  const uint32_t t = wave_ticket(&fi[3], head);
+  if (head) tl[t] = k;
+}
+
+// Rebalance windows (packed-memory array): for each block the batch would
+// overflow (one wave per block it lands in), the smallest aligned window of
+// 2^l blocks (l = 1..FI_WIN_MAX, clipped at the end) whose entries + new nodes
+// fill at most half of it; every block of the window takes level l + 1 (the
+// largest over windows: aligned windows nest), the block goes to ovl / fi[4].
+// None: FI_OVER (the batch merges densely).
+__global__ void __launch_bounds__(BLOCK) k_fi_win_pick(uint32_t nbk, const uint32_t* sk, const uint32_t* tl,
+                                                       const uint32_t* bcnt, const uint32_t* bfirst,
+                                                       const uint32_t* bend, uint32_t* bwin, uint32_t* ovl,
+                                                       uint32_t* fi) {
+  const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
+  if (w >= fi[3]) return;  // (wave-uniform)
+  const uint32_t b = fi_blk(sk[tl[w]], nbk * FI_CAP);
+  if (bcnt[b] + bend[b] - bfirst[b] <= FI_CAP) return;
+  if (lane == 0) ovl[atomicAdd(&fi[4], 1u)] = b;
+  for (uint32_t l = 1; l <= FI_WIN_MAX; ++l) {
+    const uint32_t n = 1u << l, w0 = b & ~(n - 1), ne = min(n, nbk - w0);
+    uint32_t v = lane < ne ? bcnt[w0 + lane] + bend[w0 + lane] - bfirst[w0 + lane] : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (2 * v <= ne * FI_CAP) {
+      if (lane < ne) atomicMax(&bwin[w0 + lane], l + 1);
+      return;
+    }
+  }
+  if (lane == 0) atomicOr(&fi[0], FI_OVER);
+}
+
+// the windows that act (one per maximal window: the first overflowing block
+// of it to flag its leader lists it) in wl / fi[5]
+constexpr uint32_t FI_WIN_LISTED = 0x80u;
+__global__ void __launch_bounds__(BLOCK) k_fi_win_list(const uint32_t* ovl, uint32_t* fi, uint32_t* bwin,
+                                                       uint32_t* wl, uint32_t* wlev) {
+  GRID_STRIDE(w, fi[4]) {
+    const uint32_t b = ovl[w], L = bwin[b] & ~FI_WIN_LISTED;
+    const uint32_t w0 = b & ~((1u << (L - 1)) - 1u);
+    if (atomicCAS(&bwin[w0], L, L | FI_WIN_LISTED) == L) {
+      const uint32_t u = atomicAdd(&fi[5], 1u);
+      wl[u] = w0;
+      wlev[u] = L;
+    }
+  }
+}
+
+// One workgroup per block the batch lands in, outside every window: the
+// block's entries and its new nodes merged in LDS, then written back in
+// place. A base entry moves right by the new nodes whose gap is at or before
+// it; a new node sits at its gap + the new nodes of earlier gaps in the block
+// + its order in its gap. Moved and new entries get their position in
+// rank_of, the new nodes their next links (and the entry before each gap
+// its new first); the block's minima are recomputed.
+__global__ void __launch_bounds__(FI_CAP) k_fi_rewrite(uint32_t nbk, const uint32_t* tl, const uint32_t* fi,
+                                                       const uint32_t* sk, const uint32_t* sv, const uint32_t* ord,
+                                                       const uint32_t* first, const uint32_t* gpred, uint32_t slot0,
+                                                       const long long* ts, uint32_t* bent, long long* bdk,
+                                                       uint32_t* bcnt, uint32_t* bfirst, uint32_t* bend,
+                                                       const uint32_t* bwin, long long* bmin, uint32_t* rank_of,
+                                                       uint32_t* s_next) {
+  __shared__ uint32_t se[FI_CAP];
+  __shared__ long long sd[FI_CAP];
+  if (blockIdx.x >= fi[3]) return;  // (workgroup-uniform)
+  const uint32_t Kp = nbk * FI_CAP, k = tl[blockIdx.x], j = threadIdx.x;
+  const uint32_t b = fi_blk(sk[k], Kp), base = b * FI_CAP;
+  if (bwin[b]) return;  // a window rebalances it
+  const uint32_t e = bend[b], cnt = bcnt[b];
+  if (j < cnt) {
+    const uint32_t pos = base + j;
+    uint32_t lo = k, hi = e;  // new nodes with gap <= pos
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (sk[mid] <= pos) lo = mid + 1;
+      else hi = mid;
+    }
+    const uint32_t nj = j + (lo - k), sl = bent[pos];
+    se[nj] = sl;
+    sd[nj] = bdk[pos];
+    if (nj != j) rank_of[sl] = base + nj;
+  }
+  for (uint32_t q = k + j; q < e; q += FI_CAP) {
+    const uint32_t g = sk[q];
+    const uint32_t nj = (g >= Kp ? cnt : g - base) + (first[q] - k) + ord[q];
+    const uint32_t op = sv[q];
+    se[nj] = slot0 + op;
+    sd[nj] = ts[op];
+    rank_of[slot0 + op] = base + nj;
+  }
+  __syncthreads();
+  const uint32_t c2 = cnt + (e - k);
+  // next links: a new node's successor is the next entry of its block (its
+  // gap's base node follows it; past the end only at the document's end)
+  for (uint32_t q = k + j; q < e; q += FI_CAP) {
+    const uint32_t g = sk[q];
+    const uint32_t nj = (g >= Kp ? cnt : g - base) + (first[q] - k) + ord[q], sl = slot0 + sv[q];
+    s_next[sl] = nj + 1 < c2 ? se[nj + 1] : NONE;
+    if (ord[q] == 0) s_next[gpred[q]] = sl;
+  }
+  long long v = FI_INF;
+  if (j < c2) {
+    bent[base + j] = se[j];
+    v = sd[j];
+    bdk[base + j] = v;
+  }
+  v = wave_min64(v);
+  if ((j & 63) == 0) bmin[FI_BPB * b + (j >> 6)] = v;
+  if (j == 0) {
+    bcnt[b] = c2;
+    bfirst[b] = 0;
+    bend[b] = 0;
+  }
+}
+
+// One workgroup per rebalance window [w0, w0 + ne): every block's merged
+// content (as in k_fi_rewrite) staged in LDS in window order, then spread
+// evenly over the window's blocks (each keeps >= 1 entry: every block had
+// one), padding cleared, minima recomputed, next links of the new nodes set,
+// the window's marks cleared.
+__global__ void __launch_bounds__(FI_WIN_THREADS) k_fi_win(uint32_t nbk, const uint32_t* wl, const uint32_t* wlev,
+                                                           const uint32_t* fi, const uint32_t* sk, const uint32_t* sv,
+                                                           const uint32_t* ord, const uint32_t* first,
+                                                           const uint32_t* gpred, uint32_t slot0, const long long* ts,
+                                                           uint32_t* bent, long long* bdk, uint32_t* bcnt,
+                                                           uint32_t* bfirst, uint32_t* bend, uint32_t* bwin,
+                                                           long long* bmin, uint32_t* rank_of, uint32_t* s_next) {
+  extern __shared__ unsigned long long fi_win_lds[];
+  long long* sd = reinterpret_cast<long long*>(fi_win_lds);     // [FI_WIN_ENT]
+  uint32_t* se = reinterpret_cast<uint32_t*>(sd + FI_WIN_ENT);  // [FI_WIN_ENT]
+  __shared__ uint32_t vp[(1u << FI_WIN_MAX) + 1];  // window-order start of each block's content
+  if (blockIdx.x >= fi[5]) return;  // (workgroup-uniform)
+  const uint32_t Kp = nbk * FI_CAP, w0 = wl[blockIdx.x], L = wlev[blockIdx.x];
+  const uint32_t ne = min(1u << (L - 1), nbk - w0);
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = FI_WIN_THREADS / 64;
+  if (tid < 64) {
+    const uint32_t v = tid < ne ? bcnt[w0 + tid] + bend[w0 + tid] - bfirst[w0 + tid] : 0u;
+    const uint32_t inc = wave_incl_scan(v);
+    vp[tid] = inc - v;
+    if (tid == 63) vp[64] = inc;
+  }
+  __syncthreads();
+  const uint32_t T = vp[64];
+  // stage: one wave per block of the window
+  for (uint32_t i = wv; i < ne; i += nw) {
+    const uint32_t b = w0 + i, base = b * FI_CAP, cnt = bcnt[b], k = bfirst[b], e = bend[b], v0 = vp[i];
+    for (uint32_t j = lane; j < cnt; j += 64) {
+      const uint32_t p = base + j;
+      uint32_t lo = k, hi = e;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sk[mid] <= p) lo = mid + 1;
+        else hi = mid;
+      }
+      se[v0 + j + (lo - k)] = bent[p];
+      sd[v0 + j + (lo - k)] = bdk[p];
+    }
+    for (uint32_t q = k + lane; q < e; q += 64) {
+      const uint32_t g = sk[q];
+      const uint32_t nj = (g >= Kp ? cnt : g - base) + (first[q] - k) + ord[q];
+      const uint32_t op = sv[q];
+      se[v0 + nj] = slot0 + op;
+      sd[v0 + nj] = ts[op];
+    }
+  }
+  __syncthreads();
+  // next links of the new nodes (their successor is in the window: see k_fi_rewrite)
+  for (uint32_t i = wv; i < ne; i += nw) {
+    const uint32_t b = w0 + i, base = b * FI_CAP, cnt = bcnt[b], k = bfirst[b], e = bend[b], v0 = vp[i];
+    for (uint32_t q = k + lane; q < e; q += 64) {
+      const uint32_t g = sk[q];
+      const uint32_t v = v0 + (g >= Kp ? cnt : g - base) + (first[q] - k) + ord[q], sl = slot0 + sv[q];
+      s_next[sl] = v + 1 < T ? se[v + 1] : NONE;
+      if (ord[q] == 0) s_next[gpred[q]] = sl;
+    }
+  }
+  // spread: block i of the window takes qn (+1 for the first rm) entries
+  const uint32_t qn = T / ne, rm = T % ne;
+  auto vstart = [&](uint32_t i) -> uint32_t { return i * qn + min(i, rm); };
+  for (uint32_t x = tid; x < ne * FI_CAP; x += FI_WIN_THREADS) {
+    const uint32_t i = x / FI_CAP, j = x % FI_CAP, c = qn + (i < rm ? 1u : 0u), p = (w0 + i) * FI_CAP + j;
+    if (j < c) {
+      const uint32_t v = vstart(i) + j, sl = se[v];
+      bent[p] = sl;
+      bdk[p] = sd[v];
+      rank_of[sl] = p;
+    } else {
+      bent[p] = NONE;
+      bdk[p] = FI_INF;
+    }
+  }
+  // minima per 64 positions (one wave each, from the stage)
+  for (uint32_t gq = wv; gq < ne * FI_BPB; gq += nw) {
+    const uint32_t i = gq / FI_BPB, c = qn + (i < rm ? 1u : 0u), j = (gq % FI_BPB) * 64 + lane;
+    const long long v = wave_min64(j < c ? sd[vstart(i) + j] : FI_INF);
+    if (lane == 0) bmin[FI_BPB * w0 + gq] = v;
+  }
+  __syncthreads();  // (every wave has read bfirst / bend)
+  for (uint32_t i = tid; i < ne; i += FI_WIN_THREADS) {
+    bcnt[w0 + i] = qn + (i < rm ? 1u : 0u);
+    bfirst[w0 + i] = 0;
+    bend[w0 + i] = 0;
+    bwin[w0 + i] = 0;
+  }
+}
+
+// superblock minima over the rewritten blocks' superblocks (one wave each;
+// blocks of one superblock write the same value)
+__device__ __forceinline__ void fi_sup_one(uint32_t sp, uint32_t nb, const long long* bmin, long long* smin) {
+  const uint32_t lane = threadIdx.x & 63, q = sp * FI_SUP + lane;
+  const long long v = wave_min64(q < nb ? bmin[q] : FI_INF);
+  if (lane == 0) smin[sp] = v;
+}
+__global__ void __launch_bounds__(BLOCK) k_fi_sup_fix(uint32_t Kp, const uint32_t* tl, const uint32_t* fi,
+                                                      const uint32_t* sk, const long long* bmin, long long* smin) {
+  const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64;
+  if (w >= fi[3]) return;  // (wave-uniform)
+  fi_sup_one(FI_BPB * fi_blk(sk[tl[w]], Kp) / FI_SUP, Kp / FI_BLK, bmin, smin);
+}
+// ... and over every superblock a window's blocks touch (one wave per window)
+__global__ void __launch_bounds__(BLOCK) k_fi_sup_win(uint32_t nbk, const uint32_t* wl, const uint32_t* fi,
+                                                      const uint32_t* wlev, const long long* bmin, long long* smin) {
+  const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64;
+  if (w >= fi[5]) return;  // (wave-uniform)
+  const uint32_t w0 = wl[w], ne = min(1u << (wlev[w] - 1), nbk - w0);
+  for (uint32_t sp = FI_BPB * w0 / FI_SUP; sp <= (FI_BPB * (w0 + ne) - 1) / FI_SUP; ++sp)
+    fi_sup_one(sp, FI_BPB * nbk, bmin, smin);
+}
+
+// the dense order from the gapped one (off = exclusive scan of bcnt)
+__global__ void __launch_bounds__(BLOCK) k_fi_compact(uint32_t nbk, const uint32_t* off, const uint32_t* bent,
+                                                      const uint32_t* bcnt, uint32_t* doc) {
+  GRID_STRIDE(p, nbk * FI_CAP) {
+    const uint32_t b = p / FI_CAP, j = p % FI_CAP;
+    if (j < bcnt[b]) doc[off[b] + j] = bent[p];
+  }
+}
+
+// gap positions (sorted) -> dense ranks, for a dense merge (monotone: the
+// order stays sorted)
+__global__ void __launch_bounds__(BLOCK) k_fi_dense_gaps(uint32_t m, uint32_t Kp, uint32_t K, const uint32_t* off,
+                                                         uint32_t* sk) {
   GRID_STRIDE(k, m) {
-    if (k == 0 || gk[k - 1] != gk[k]) list[atomicAdd(cnt, 1u)] = k;
+    const uint32_t g = sk[k];
+    sk[k] = g >= Kp ? K : off[g / FI_CAP] + g % FI_CAP;
   }
 }
 
@@ -379,9 +719,7 @@ __device__ __forceinline__ uint32_t fi_count_le(const uint32_t* gk, uint32_t lo,
 
 __global__ void __launch_bounds__(BLOCK) k_fi_doc(uint32_t K, uint32_t m, const uint32_t* doc, const uint32_t* gk,
                                                   const uint32_t* gv, const uint32_t* ord, const uint32_t* first,
-                                                  uint32_t slot0, const long long* ts, const long long* dk,
-                                                  uint32_t* newdoc, uint32_t* newrank, long long* newdk,
-                                                  uint32_t* rank_of) {
+                                                  uint32_t slot0, uint32_t* newdoc, uint32_t* newrank) {
   __shared__ uint32_t bnd[2];
   const uint32_t r0 = blockIdx.x * blockDim.x, r = r0 + threadIdx.x;
   if (r0 < K && threadIdx.x < 2) {
@@ -390,17 +728,12 @@ __global__ void __launch_bounds__(BLOCK) k_fi_doc(uint32_t K, uint32_t m, const 
   }
   __syncthreads();
   if (r < K) {
-    const uint32_t p = r + fi_count_le(gk, bnd[0], bnd[1], r), sl = doc[r];
-    newdoc[p] = sl;
-    newdk[p] = dk[r];
-    rank_of[sl] = p;
+    newdoc[r + fi_count_le(gk, bnd[0], bnd[1], r)] = doc[r];
   } else if (r < K + m) {
     const uint32_t k = r - K;
-    const uint32_t p = gk[k] + first[k] + ord[k], op = gv[k];
+    const uint32_t p = gk[k] + first[k] + ord[k];
     newrank[k] = p;
-    newdoc[p] = slot0 + op;
-    newdk[p] = ts[op];
-    rank_of[slot0 + op] = p;
+    newdoc[p] = slot0 + gv[k];
   }
 }
 
@@ -446,29 +779,83 @@ static bool finc_allowed() {
   return !(e && (!strcmp(e, "replay") || !strcmp(e, "remerge")));
 }
 
-// (Re)builds the tree's key index when it does not describe the state; the
-// document-order arrays get room for the batch and are rebuilt (ord_ready)
-// when they are new or the index was stale.
-static int kx_ensure(crdtm_tree* t, uint64_t extra) {
+// The dense order from the gapped one, into the tree's `doc`.
+static int fi_compact_doc(crdtm_tree* t, Arena& ws, hipStream_t s) {
+  KeyIndex& X = *t->kidx;
+  uint32_t* off = ws.alloc<uint32_t>(X.nbk + 1);
+  int r = scan_excl_u32(X.bcnt, off, X.nbk, nullptr, ws, s);
+  if (r) return r;
+  LAUNCH(k_fi_compact, dim3(grid_for(static_cast<uint64_t>(X.nbk) * FI_CAP)), dim3(BLOCK), 0, s, X.nbk, off, X.bent,
+         X.bcnt, t->d.doc);
+  t->doc_gapped = false;
+  return CRDTM_OK;
+}
+
+int fi_materialize(crdtm_tree* t) {
+  if (!t->doc_gapped) return CRDTM_OK;
+  if (!t->kidx || !t->kidx->ord_ready || !t->kidx_valid) {  // (cannot happen after a good merge)
+    t->doc_gapped = false;
+    t->doc_valid = false;
+    return CRDTM_OK;
+  }
+  return fi_compact_doc(t, t->ctx->ws, t->ctx->stream);
+}
+
+// The gapped order from the tree's dense `doc` (K entries), a quarter full.
+static int fi_build(crdtm_tree* t, uint32_t K, hipStream_t s) {
+  KeyIndex& X = *t->kidx;
+  const uint32_t nbk = (K + FI_FILL - 1) / FI_FILL;
+  if (X.bcap < nbk) {
+    for (void* q : {static_cast<void*>(X.bent), static_cast<void*>(X.bdk), static_cast<void*>(X.bcnt),
+                    static_cast<void*>(X.bend), static_cast<void*>(X.bfirst), static_cast<void*>(X.bwin),
+                    static_cast<void*>(X.bmin), static_cast<void*>(X.smin)})
+      if (q) hipFree(q);
+    const uint64_t bc = 2ULL * nbk + 64;
+    HIP_CHECK(hipMalloc(&X.bent, bc * FI_CAP * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&X.bdk, bc * FI_CAP * sizeof(long long)));
+    HIP_CHECK(hipMalloc(&X.bcnt, bc * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&X.bend, bc * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&X.bfirst, bc * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&X.bwin, bc * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&X.bmin, FI_BPB * bc * sizeof(long long)));
+    HIP_CHECK(hipMalloc(&X.smin, (FI_BPB * bc / FI_SUP + 1) * sizeof(long long)));
+    X.bcap = bc;
+  }
+  X.nbk = nbk;
+  const uint32_t Kp = nbk * FI_CAP;
+  LAUNCH(k_fi_build, dim3(grid_for(Kp)), dim3(BLOCK), 0, s, K, nbk, t->d.doc, t->d.s_key, X.bent, X.bdk, X.bcnt,
+         X.bfirst, X.bend, X.bwin, X.rank);
+  LAUNCH(k_fi_bmin, dim3(grid_for(static_cast<uint64_t>(Kp / FI_BLK + 3) / 4 * 64)), dim3(BLOCK), 0, s, Kp, X.bdk,
+         X.bmin);
+  LAUNCH(k_fi_sup, dim3(grid_for(FI_BPB * nbk / FI_SUP + 1)), dim3(BLOCK), 0, s, FI_BPB * nbk, X.bmin, X.smin);
+  X.ord_ready = true;
+  return CRDTM_OK;
+}
+
+// (Re)builds the tree's key index when it does not describe the state, with
+// room for `extra` more nodes; the gapped order is rebuilt (ord_ready) when
+// its arrays are new or the index was stale (a gapped document is written
+// back to `doc` first).
+static int kx_ensure(crdtm_tree* t, uint64_t extra, Arena& ws) {
   crdtm_ctx* c = t->ctx;
-  const uint64_t need_h = 2 * (t->n_slots + extra) + 1024, need_o = t->n_slots + extra + 1;
+  const uint64_t need_h = 2 * (t->n_slots + extra) + 1024, need_r = t->n_slots + extra + 1;
   if (!t->kidx) t->kidx = std::make_unique<KeyIndex>();
   KeyIndex& x = *t->kidx;
-  if (x.ocap < need_o) {
-    for (long long*& q : x.dk) {
-      if (q) hipFree(q);
-      q = nullptr;
-    }
+  const bool hash_ok = t->kidx_valid && static_cast<uint64_t>(x.mask) + 1 >= need_h;
+  if (hash_ok && x.rcap >= need_r) return CRDTM_OK;
+  if (t->doc_gapped) {
+    int r = fi_compact_doc(t, ws, c->stream);
+    if (r) return r;
+  }
+  x.ord_ready = false;
+  if (x.rcap < need_r) {
     if (x.rank) hipFree(x.rank);
     x.rank = nullptr;
-    const uint64_t oc = 2 * need_o + 4096;
-    HIP_CHECK(hipMalloc(&x.dk[0], oc * sizeof(long long)));
-    HIP_CHECK(hipMalloc(&x.dk[1], oc * sizeof(long long)));
-    HIP_CHECK(hipMalloc(&x.rank, oc * sizeof(uint32_t)));
-    x.ocap = oc;
-    x.ord_ready = false;
+    const uint64_t rc = 2 * need_r + 4096;
+    HIP_CHECK(hipMalloc(&x.rank, rc * sizeof(uint32_t)));
+    x.rcap = rc;
   }
-  if (t->kidx_valid && static_cast<uint64_t>(x.mask) + 1 >= need_h) return CRDTM_OK;
+  if (hash_ok) return CRDTM_OK;
   if (static_cast<uint64_t>(x.mask) + 1 < need_h) {
     if (x.keys) hipFree(x.keys);
     if (x.vals) hipFree(x.vals);
@@ -485,7 +872,6 @@ static int kx_ensure(crdtm_tree* t, uint64_t extra) {
   LAUNCH(k_kx_build, dim3(grid_for(t->n_slots)), dim3(BLOCK), 0, c->stream, t->d.s_key,
          static_cast<uint32_t>(t->n_slots), TsHash{x.keys, x.vals, x.mask});
   t->kidx_valid = true;
-  x.ord_ready = false;
   return CRDTM_OK;
 }
 
@@ -494,76 +880,84 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   const uint32_t m = o.n;
   const uint64_t K64 = t->n_slots - 1;
   if (!finc_allowed() || m == 0 || m > FI_MAX_BATCH || !t->flat_clean || !t->doc_valid || t->n_dicts != 1 ||
-      t->doc_n != K64 || K64 == 0 || o.n_path != m || K64 + m >= 0x7FFFFFF0ULL)
+      t->doc_n != K64 || K64 == 0 || o.n_path != m || K64 + m >= 0x7FFFFFF0ULL || 2 * (K64 + m) >= 0x7FFFFFF0ULL)
     return CRDTM_OK;
+  if (t->doc_gapped && !(t->kidx && t->kidx->ord_ready && t->kidx_valid)) return CRDTM_OK;
   crdtm_ctx* c = t->ctx;
   hipStream_t s = c->stream;
   Arena& ws = c->ws;
   const uint32_t K = static_cast<uint32_t>(K64);
   const size_t mark0 = ws.used;
+  int r;
+  if ((r = kx_ensure(t, m, ws))) return r;
+  KeyIndex& X = *t->kidx;
+  if (!X.ord_ready && (r = fi_build(t, K, s))) return r;
+  const uint32_t nbk = X.nbk, Kp = nbk * FI_CAP;
   // every workspace buffer first: nothing is written to the state before the last check
-  const uint32_t nb = (K + FI_BLK - 1) / FI_BLK, ns = (nb + FI_SUP - 1) / FI_SUP;
-  long long* bmin = ws.alloc<long long>(nb);
-  long long* smin = ws.alloc<long long>(ns);
   const uint32_t bcap = pow2_ge(2ULL * m);
   TsHash bh{ws.alloc<unsigned long long>(bcap), ws.alloc<uint32_t>(bcap), bcap - 1};
-  uint32_t* fi = ws.alloc<uint32_t>(4);
+  uint32_t* fi = ws.alloc<uint32_t>(FI_WORDS);
   uint32_t* par[1] = {ws.alloc<uint32_t>(m)};
   uint32_t* sta[1] = {ws.alloc<uint32_t>(m)};
   long long* thr[1] = {ws.alloc<long long>(m)};
   uint32_t* par0 = ws.alloc<uint32_t>(m);
   uint32_t* gk[2] = {ws.alloc<uint32_t>(m), ws.alloc<uint32_t>(m)};
   uint32_t* gv[2] = {ws.alloc<uint32_t>(m), ws.alloc<uint32_t>(m)};
-  uint32_t* nm = ws.alloc<uint32_t>(1);
   uint32_t* pos = ws.alloc<uint32_t>(m);
   uint32_t* nxt = ws.alloc<uint32_t>(m);
   uint32_t* glist = ws.alloc<uint32_t>(m);
+  uint32_t* tl = ws.alloc<uint32_t>(m);
+  uint32_t* ovl = ws.alloc<uint32_t>(m);
+  uint32_t* gpred = ws.alloc<uint32_t>(m);
+  uint32_t* wl = ws.alloc<uint32_t>(m);
+  uint32_t* wlev = ws.alloc<uint32_t>(m);
   uint32_t* ord = ws.alloc<uint32_t>(m);
   uint32_t* first = ws.alloc<uint32_t>(m);
   uint32_t* newrank = ws.alloc<uint32_t>(m);
   uint8_t* st = ws.alloc<uint8_t>(m);
   long long* rep = ws.alloc<long long>(2ULL * m + 2);
-  int r;
-  if ((r = kx_ensure(t, m))) return r;
-  KeyIndex& X = *t->kidx;
   const TsHash kx{X.keys, X.vals, X.mask};
-  long long* dk = X.dk[X.cur];
   uint32_t* rank_of = X.rank;
-  // ---- phase A: base order, anchors, validity ----
-  HIP_CHECK(hipMemsetAsync(fi, 0, 4 * sizeof(uint32_t), s));
+  // ---- phase A: anchors, validity ----
+  HIP_CHECK(hipMemsetAsync(fi, 0, FI_WORDS * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(bh.keys, 0, static_cast<size_t>(bcap) * sizeof(unsigned long long), s));
-  if (!X.ord_ready) {  // (kept up to date by every incremental merge after this one)
-    LAUNCH(k_fi_prep, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d.s_key, dk, rank_of);
-    X.ord_ready = true;
-  }
-  LAUNCH(k_fi_bmin, dim3(grid_for(static_cast<uint64_t>(nb + 3) / 4 * 64)), dim3(BLOCK), 0, s, K, dk, bmin);
-  LAUNCH(k_fi_sup, dim3(grid_for(ns)), dim3(BLOCK), 0, s, nb, bmin, smin);
   LAUNCH(k_fi_bidx, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, bh, fi);
   LAUNCH(k_fi_resolve, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, kx, bh, rank_of, replica_of(t->timestamp), par[0],
          par0, sta[0], thr[0], fi);
-  // ---- phase B: gaps (pointer jumping over new anchors, one NSR query each) ----
+  // ---- phase B: gaps (pointer jumping over new anchors, one NSR query each
+  // over the gapped order), the blocks they land in ----
   uint32_t rounds = 0;
   for (uint32_t span = 1; span < m; span <<= 1) ++rounds;
-  if (rounds) LAUNCH(k_fi_jump, dim3(1), dim3(FI_JUMP_THREADS), 0, s, m, rounds, par[0], sta[0], thr[0]);
-  const int cur = 0;
-  LAUNCH(k_fi_gap, dim3(grid_for(64ULL * m)), dim3(BLOCK), 0, s, m, K, dk, bmin, smin, sta[cur], thr[cur], gk[0],
+  if (rounds) LAUNCH(k_fi_jump, dim3(1), dim3(FI_JUMP_THREADS), 0, s, m, rounds, par[0], sta[0], thr[0], o.ts);
+  LAUNCH(k_fi_gap, dim3(grid_for(64ULL * m)), dim3(BLOCK), 0, s, m, Kp, X.bdk, X.bmin, X.smin, sta[0], thr[0], gk[0],
          gv[0]);
-  LAUNCH(k_fi_setn, dim3(1), dim3(1), 0, s, nm, m);
-  uint32_t bits = 8;
-  while (bits < 32 && (static_cast<uint64_t>(K) >> bits) != 0) bits += 8;
-  uint32_t *sk = nullptr, *sv = nullptr;
-  if ((r = radix_sort_pairs(gk[0], gv[0], gk[1], gv[1], nm, m, bits, ws, s, &sk, &sv))) return r;
+  uint32_t bits = 4;  // (gap positions run to Kp inclusive)
+  while (bits < 32 && (static_cast<uint64_t>(Kp) >> bits) != 0) bits += 4;
+  uint32_t *sk = gk[1], *sv = gv[1];
+  if ((r = radix_sort_small(gk[0], gv[0], m, bits, sk, sv, s))) return r;
+  const uint32_t gm = (m + BLOCK - 1) / BLOCK;  // one item per thread
   LAUNCH(k_fi_pos, dim3(grid_for(m)), dim3(BLOCK), 0, s, m, sv, pos);
-  LAUNCH(k_fi_gstart, dim3(grid_for(m)), dim3(BLOCK), 0, s, m, sk, glist, fi + 2);
+  LAUNCH(k_fi_gstart, dim3(gm), dim3(BLOCK), 0, s, m, sk, glist, fi + 2);
   LAUNCH(k_fi_gaps, dim3(m), dim3(64), 0, s, m, glist, fi + 2, sk, sv, par0, pos, o.ts, nxt, ord, first, fi);
-  uint32_t hf[4];
+  LAUNCH(k_fi_tblk, dim3(gm), dim3(BLOCK), 0, s, m, nbk, sk, ord, X.bent, X.bcnt, X.bfirst, X.bend, tl, gpred, fi);
+  LAUNCH(k_fi_win_pick, dim3(grid_for(64ULL * m)), dim3(BLOCK), 0, s, nbk, sk, tl, X.bcnt, X.bfirst, X.bend, X.bwin,
+         ovl, fi);
+  LAUNCH(k_fi_win_list, dim3(grid_for(m)), dim3(BLOCK), 0, s, ovl, fi, X.bwin, wl, wlev);
+  uint32_t hf[FI_WORDS];
   HIP_CHECK(hipMemcpyAsync(hf, fi, sizeof(hf), hipMemcpyDeviceToHost, s));
   if (int rw = stream_wait(s)) return rw;
   const long long new_ts = t->timestamp + hf[1];
-  if (hf[0] || replica_of(new_ts) != replica_of(t->timestamp)) {
-    ws.used = mark0;  // the general paths decide (the key index stays valid: the state is untouched)
+  if ((hf[0] & (FI_FAIL | FI_BUDGET)) || replica_of(new_ts) != replica_of(t->timestamp)) {
+    // the general paths decide: the state is untouched, the key index stays
+    // valid; the blocks' per-batch marks are not cleared, so they are rebuilt
+    // when next used
+    if (t->doc_gapped && (r = fi_compact_doc(t, ws, s))) return r;
+    X.ord_ready = false;
+    ws.used = mark0;
     return CRDTM_OK;
   }
+  const bool dense = hf[0] & FI_OVER;
+  if (getenv("CRDTM_FI_DEBUG")) fprintf(stderr, "finc m=%u K=%u nbk=%u flags=%u gaps=%u blocks=%u over=%u windows=%u\n", m, K, nbk, hf[0], hf[2], hf[3], hf[4], hf[5]);
   // ---- phase C: commit ----
   TreeCaps need = t->cap;
   need.slots = std::max<uint64_t>(need.slots, t->n_slots + m + 1);
@@ -572,24 +966,45 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   need.doc = std::max<uint64_t>(need.doc, K64 + m + 1);
   if (need.slots > t->cap.slots || need.log > t->cap.log || need.lpath > t->cap.lpath || need.doc > t->cap.doc)
     if ((r = grow_tree(t, need))) return r;
-  if (X.doc2_cap < t->cap.doc) {  // the next order's buffer matches the tree's doc capacity
-    if (X.doc2) hipFree(X.doc2);
-    X.doc2 = nullptr;
-    HIP_CHECK(hipMalloc(&X.doc2, t->cap.doc * sizeof(uint32_t)));
-    X.doc2_cap = t->cap.doc;
-  }
-  uint32_t* newdoc = X.doc2;
   const uint32_t slot0 = static_cast<uint32_t>(t->n_slots);
-  LAUNCH(k_fi_doc, dim3(grid_for(K64 + m)), dim3(BLOCK), 0, s, K, m, t->d.doc, sk, sv, ord, first, slot0, o.ts,
-         dk, newdoc, newrank, X.dk[X.cur ^ 1], rank_of);
-  X.cur ^= 1;
-  LAUNCH(k_fi_next, dim3(grid_for(m)), dim3(BLOCK), 0, s, K, m, sv, ord, newrank, newdoc, slot0, t->d.s_next);
-  // the new order becomes the tree's (the store owns whichever buffer `doc` holds)
-  std::swap(t->d.doc, X.doc2);
-  std::swap(t->cap.doc, X.doc2_cap);
-  t->store->d.doc = t->d.doc;
   LAUNCH(k_fi_commit, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, slot0, static_cast<uint32_t>(t->log_n),
          static_cast<uint32_t>(t->log_npath), t->d);
+  if (!dense) {  // O(batch): the blocks the batch lands in
+    LAUNCH(k_fi_rewrite, dim3(hf[3]), dim3(FI_CAP), 0, s, nbk, tl, fi, sk, sv, ord, first, gpred, slot0, o.ts, X.bent,
+           X.bdk, X.bcnt, X.bfirst, X.bend, X.bwin, X.bmin, rank_of, t->d.s_next);
+    static const bool win_lds = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fi_win),
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    FI_WIN_ENT * 12) == hipSuccess;
+    if (hf[5] && !win_lds) return CRDTM_E_HIP;
+    if (hf[5])
+      LAUNCH(k_fi_win, dim3(hf[5]), dim3(FI_WIN_THREADS), FI_WIN_ENT * 12, s, nbk, wl, wlev, fi, sk, sv, ord, first,
+             gpred, slot0, o.ts, X.bent, X.bdk, X.bcnt, X.bfirst, X.bend, X.bwin, X.bmin, rank_of, t->d.s_next);
+    LAUNCH(k_fi_sup_fix, dim3(grid_for(64ULL * hf[3])), dim3(BLOCK), 0, s, Kp, tl, fi, sk, X.bmin, X.smin);
+    if (hf[5])
+      LAUNCH(k_fi_sup_win, dim3(grid_for(64ULL * hf[5])), dim3(BLOCK), 0, s, nbk, wl, fi, wlev, X.bmin, X.smin);
+    t->doc_gapped = true;
+  } else {  // a block overflows: merge densely, then rebuild the blocks
+    if ((r = fi_compact_doc(t, ws, s))) return r;
+    uint32_t* off = ws.alloc<uint32_t>(nbk + 1);
+    if ((r = scan_excl_u32(X.bcnt, off, nbk, nullptr, ws, s))) return r;
+    LAUNCH(k_fi_dense_gaps, dim3(grid_for(m)), dim3(BLOCK), 0, s, m, Kp, K, off, sk);
+    if (X.doc2_cap < t->cap.doc) {  // the next order's buffer matches the tree's doc capacity
+      if (X.doc2) hipFree(X.doc2);
+      X.doc2 = nullptr;
+      HIP_CHECK(hipMalloc(&X.doc2, t->cap.doc * sizeof(uint32_t)));
+      X.doc2_cap = t->cap.doc;
+    }
+    uint32_t* newdoc = X.doc2;
+    LAUNCH(k_fi_doc, dim3(grid_for(K64 + m)), dim3(BLOCK), 0, s, K, m, t->d.doc, sk, sv, ord, first, slot0, newdoc,
+           newrank);
+    LAUNCH(k_fi_next, dim3(grid_for(m)), dim3(BLOCK), 0, s, K, m, sv, ord, newrank, newdoc, slot0, t->d.s_next);
+    // the new order becomes the tree's (the store owns whichever buffer `doc` holds)
+    std::swap(t->d.doc, X.doc2);
+    std::swap(t->cap.doc, X.doc2_cap);
+    t->store->d.doc = t->d.doc;
+    if ((r = fi_build(t, K + m, s))) return r;
+    t->doc_gapped = false;
+  }
   LAUNCH(k_kx_insert, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, slot0, kx);
   HIP_CHECK(hipMemsetAsync(st, ST_APPLIED, m, s));
   if ((r = replica_fold(c, o, st, rep, ws, s))) return r;

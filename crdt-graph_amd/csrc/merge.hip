@@ -3982,20 +3982,28 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   }
   t->flat_clean = false;
   t->kidx_valid = false;
+  const bool was_gapped = t->doc_gapped;  // (after finc_apply: it may have written `doc` back)
+  t->doc_gapped = false;  // (the general paths write `doc`, or leave it to linearize)
   const int r = apply_batch_paths(t, o, st_out, res);
   if (r != CRDTM_OK || res->code != CRDTM_OK) {  // the state is unchanged
     t->flat_clean = was_clean;
     t->kidx_valid = was_kidx && r == CRDTM_OK;
+    t->doc_gapped = was_gapped && t->kidx_valid;
+    if (was_gapped && !t->doc_gapped) t->doc_valid = false;  // (an engine error: linearize from the state)
   }
   return r;
 }
 
 int linearize(crdtm_tree* t) {
-  if (t->doc_valid) return CRDTM_OK;
   crdtm_ctx* c = t->ctx;
   hipStream_t s = c->stream;
   Arena& ws = c->ws;
   ws.reset();
+  if (t->doc_gapped) {  // current in the incremental merge's gapped order: compact it
+    int r = fi_materialize(t);
+    if (r) return r;
+  }
+  if (t->doc_valid) return CRDTM_OK;
   const uint32_t S = static_cast<uint32_t>(t->n_slots), D = static_cast<uint32_t>(t->n_dicts);
   uint8_t* ok = ws.alloc<uint8_t>(D);
   uint8_t* ok2 = ws.alloc<uint8_t>(D);

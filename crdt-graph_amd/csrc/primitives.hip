@@ -585,6 +585,103 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, con
   return CRDTM_OK;
 }
 
+// One-workgroup radix sort for small batches (n <= RS_SMALL_MAX): the pairs
+// stay in LDS for every pass (4-bit digits, 512 threads x 32 consecutive
+// items): per pass each thread counts its items' digits, one workgroup scan
+// over the digit-major [16][512] counts gives every thread its runs, and the
+// items scatter back into LDS, stably. One launch instead of three per 8-bit
+// pass (the multi-workgroup sort above is latency-bound at this size).
+constexpr uint32_t RS_SMALL_T = 512, RS_SMALL_IPT = RS_SMALL_MAX / RS_SMALL_T;
+static_assert(RS_SMALL_IPT == 32, "one pad word per thread's 32 items");
+// (item i at word i + i / 32: a thread's 32 consecutive items sit in 32 banks)
+__device__ __forceinline__ uint32_t rs_pad(uint32_t i) { return i + (i >> 5); }
+constexpr uint32_t RS_SMALL_WORDS = RS_SMALL_MAX + RS_SMALL_MAX / 32;
+constexpr size_t RS_SMALL_LDS = 2 * RS_SMALL_WORDS * sizeof(uint32_t) + 16 * RS_SMALL_T * sizeof(uint16_t);
+
+__global__ void __launch_bounds__(RS_SMALL_T) k_rs_small(const uint32_t* __restrict__ kin,
+                                                         const uint32_t* __restrict__ vin, uint32_t n, uint32_t bits,
+                                                         uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
+  extern __shared__ uint32_t rs_small_lds[];
+  uint32_t* sk = rs_small_lds;
+  uint32_t* sv = sk + RS_SMALL_WORDS;
+  uint16_t* cnt = reinterpret_cast<uint16_t*>(sv + RS_SMALL_WORDS);  // [digit][thread]
+  __shared__ uint32_t wsum[RS_SMALL_T / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (uint32_t i = t; i < RS_SMALL_MAX; i += RS_SMALL_T) {
+    sk[rs_pad(i)] = i < n ? kin[i] : 0xFFFFFFFFu;  // padding: digit 15 in every pass, after every item
+    sv[rs_pad(i)] = i < n ? vin[i] : 0u;
+  }
+  __syncthreads();
+  for (uint32_t shift = 0; shift < bits; shift += 4) {
+    uint32_t k[RS_SMALL_IPT], v[RS_SMALL_IPT];
+    unsigned long long c0 = 0, c1 = 0;  // 8-bit counters of digits 0-7 / 8-15
+#pragma unroll
+    for (uint32_t j = 0; j < RS_SMALL_IPT; ++j) {
+      k[j] = sk[t * (RS_SMALL_IPT + 1) + j];
+      v[j] = sv[t * (RS_SMALL_IPT + 1) + j];
+      const uint32_t d = (k[j] >> shift) & 15u;
+      if (d < 8) c0 += 1ULL << (8 * d);
+      else c1 += 1ULL << (8 * (d - 8));
+    }
+#pragma unroll
+    for (uint32_t d = 0; d < 16; ++d)
+      cnt[d * RS_SMALL_T + t] = static_cast<uint16_t>(((d < 8 ? c0 : c1) >> (8 * (d & 7))) & 0xFFu);
+    __syncthreads();
+    // exclusive scan of cnt in digit-major order: thread t owns entries [16 t, 16 t + 16)
+    uint32_t loc[16], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      loc[j] = sum;
+      sum += cnt[t * 16 + j];
+    }
+    const uint32_t inc = wave_incl_scan(sum);
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t pre = inc - sum;
+    for (uint32_t w = 0; w < wv; ++w) pre += wsum[w];
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) cnt[t * 16 + j] = static_cast<uint16_t>(pre + loc[j]);
+    __syncthreads();
+    // scatter (every thread holds its items: the arrays are free); an item's
+    // place = its digit's run start for this thread + the thread's earlier
+    // items of that digit (packed 8-bit running counts)
+    // (every run start read before the first store: the stores would order the loads)
+    uint32_t q[RS_SMALL_IPT];
+#pragma unroll
+    for (uint32_t j = 0; j < RS_SMALL_IPT; ++j) q[j] = cnt[((k[j] >> shift) & 15u) * RS_SMALL_T + t];
+    unsigned long long r0 = 0, r1 = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < RS_SMALL_IPT; ++j) {
+      const uint32_t d = (k[j] >> shift) & 15u;
+      const uint32_t sh = 8 * (d & 7);
+      const uint32_t before = static_cast<uint32_t>(((d < 8 ? r0 : r1) >> sh) & 0xFFu);
+      if (d < 8) r0 += 1ULL << sh;
+      else r1 += 1ULL << sh;
+      q[j] = rs_pad(q[j] + before);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < RS_SMALL_IPT; ++j) {
+      sk[q[j]] = k[j];
+      sv[q[j]] = v[j];
+    }
+    __syncthreads();
+  }
+  for (uint32_t i = t; i < n; i += RS_SMALL_T) {
+    kout[i] = sk[rs_pad(i)];
+    vout[i] = sv[rs_pad(i)];
+  }
+}
+
+int radix_sort_small(const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t bits, uint32_t* kout,
+                     uint32_t* vout, hipStream_t st) {
+  static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_small),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 static_cast<int>(RS_SMALL_LDS)) == hipSuccess;
+  if (!lds_ok || n > RS_SMALL_MAX) return CRDTM_E_HIP;
+  if (n) LAUNCH(k_rs_small, dim3(1), dim3(RS_SMALL_T), RS_SMALL_LDS, st, kin, vin, n, bits, kout, vout);
+  return CRDTM_OK;
+}
+
 // ---------------------------------------------------------------------------
 // List ranking (north-star kernel 4). Level 0 input: ent[e] = {succ, wbits}
 // (succ: NONE = end of list, ABSENT = not in any list; wbits bit1 -> high

@@ -141,6 +141,12 @@ def test_incremental_flat_closed_form(name, monkeypatch):
         if k % 7 == 0 or b == n:
             assert engine_summary(et) == oracle_summary(ot), (k, a, b)
             assert engine_log(et, 1) == oracle_log(ot, 1), k
+        if k % 5 == 2:  # the order is kept gapped between batches: read it back mid-chain
+            assert np.array_equal(et.document_handles(), oracle_visible_vals(ot)), k
+        if k == 3:  # a version taken from a gapped order sees the same document
+            v = et.clone()
+            assert np.array_equal(v.document_handles(), oracle_visible_vals(ot))
+            del v
     assert used == len(cuts) - 2
     assert engine_log(et, 0) == oracle_log(ot, 0)
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
