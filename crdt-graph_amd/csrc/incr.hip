@@ -957,7 +957,6 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
     return CRDTM_OK;
   }
   const bool dense = hf[0] & FI_OVER;
-  if (getenv("CRDTM_FI_DEBUG")) fprintf(stderr, "finc m=%u K=%u nbk=%u flags=%u gaps=%u blocks=%u over=%u windows=%u\n", m, K, nbk, hf[0], hf[2], hf[3], hf[4], hf[5]);
   // ---- phase C: commit ----
   TreeCaps need = t->cap;
   need.slots = std::max<uint64_t>(need.slots, t->n_slots + m + 1);

@@ -596,7 +596,11 @@ static_assert(RS_SMALL_IPT == 32, "one pad word per thread's 32 items");
 // (item i at word i + i / 32: a thread's 32 consecutive items sit in 32 banks)
 __device__ __forceinline__ uint32_t rs_pad(uint32_t i) { return i + (i >> 5); }
 constexpr uint32_t RS_SMALL_WORDS = RS_SMALL_MAX + RS_SMALL_MAX / 32;
-constexpr size_t RS_SMALL_LDS = 2 * RS_SMALL_WORDS * sizeof(uint32_t) + 16 * RS_SMALL_T * sizeof(uint16_t);
+// counts [digit][thread] as u16, one pad word per 64 (the scan reads 16
+// consecutive counts per thread: without the pad, 16 lanes share a bank)
+__device__ __forceinline__ uint32_t rs_cpad(uint32_t x) { return x + 2 * (x >> 6); }
+constexpr uint32_t RS_SMALL_CNT = 16 * RS_SMALL_T + 2 * (16 * RS_SMALL_T / 64);
+constexpr size_t RS_SMALL_LDS = 2 * RS_SMALL_WORDS * sizeof(uint32_t) + RS_SMALL_CNT * sizeof(uint16_t);
 
 __global__ void __launch_bounds__(RS_SMALL_T) k_rs_small(const uint32_t* __restrict__ kin,
                                                          const uint32_t* __restrict__ vin, uint32_t n, uint32_t bits,
@@ -607,9 +611,19 @@ __global__ void __launch_bounds__(RS_SMALL_T) k_rs_small(const uint32_t* __restr
   uint16_t* cnt = reinterpret_cast<uint16_t*>(sv + RS_SMALL_WORDS);  // [digit][thread]
   __shared__ uint32_t wsum[RS_SMALL_T / 64];
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  for (uint32_t i = t; i < RS_SMALL_MAX; i += RS_SMALL_T) {
-    sk[rs_pad(i)] = i < n ? kin[i] : 0xFFFFFFFFu;  // padding: digit 15 in every pass, after every item
-    sv[rs_pad(i)] = i < n ? vin[i] : 0u;
+  {  // every global load in flight before the first LDS store
+    uint32_t k0[RS_SMALL_IPT], v0[RS_SMALL_IPT];
+#pragma unroll
+    for (uint32_t j = 0; j < RS_SMALL_IPT; ++j) {
+      const uint32_t i = t + j * RS_SMALL_T;
+      k0[j] = i < n ? kin[i] : 0xFFFFFFFFu;  // padding: digit 15 in every pass, after every item
+      v0[j] = i < n ? vin[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < RS_SMALL_IPT; ++j) {
+      sk[rs_pad(t + j * RS_SMALL_T)] = k0[j];
+      sv[rs_pad(t + j * RS_SMALL_T)] = v0[j];
+    }
   }
   __syncthreads();
   for (uint32_t shift = 0; shift < bits; shift += 4) {
@@ -625,14 +639,14 @@ __global__ void __launch_bounds__(RS_SMALL_T) k_rs_small(const uint32_t* __restr
     }
 #pragma unroll
     for (uint32_t d = 0; d < 16; ++d)
-      cnt[d * RS_SMALL_T + t] = static_cast<uint16_t>(((d < 8 ? c0 : c1) >> (8 * (d & 7))) & 0xFFu);
+      cnt[rs_cpad(d * RS_SMALL_T + t)] = static_cast<uint16_t>(((d < 8 ? c0 : c1) >> (8 * (d & 7))) & 0xFFu);
     __syncthreads();
     // exclusive scan of cnt in digit-major order: thread t owns entries [16 t, 16 t + 16)
     uint32_t loc[16], sum = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 16; ++j) {
       loc[j] = sum;
-      sum += cnt[t * 16 + j];
+      sum += cnt[rs_cpad(t * 16 + j)];
     }
     const uint32_t inc = wave_incl_scan(sum);
     if (lane == 63) wsum[wv] = inc;
@@ -640,7 +654,7 @@ __global__ void __launch_bounds__(RS_SMALL_T) k_rs_small(const uint32_t* __restr
     uint32_t pre = inc - sum;
     for (uint32_t w = 0; w < wv; ++w) pre += wsum[w];
 #pragma unroll
-    for (uint32_t j = 0; j < 16; ++j) cnt[t * 16 + j] = static_cast<uint16_t>(pre + loc[j]);
+    for (uint32_t j = 0; j < 16; ++j) cnt[rs_cpad(t * 16 + j)] = static_cast<uint16_t>(pre + loc[j]);
     __syncthreads();
     // scatter (every thread holds its items: the arrays are free); an item's
     // place = its digit's run start for this thread + the thread's earlier
@@ -648,7 +662,7 @@ __global__ void __launch_bounds__(RS_SMALL_T) k_rs_small(const uint32_t* __restr
     // (every run start read before the first store: the stores would order the loads)
     uint32_t q[RS_SMALL_IPT];
 #pragma unroll
-    for (uint32_t j = 0; j < RS_SMALL_IPT; ++j) q[j] = cnt[((k[j] >> shift) & 15u) * RS_SMALL_T + t];
+    for (uint32_t j = 0; j < RS_SMALL_IPT; ++j) q[j] = cnt[rs_cpad(((k[j] >> shift) & 15u) * RS_SMALL_T + t)];
     unsigned long long r0 = 0, r1 = 0;
 #pragma unroll
     for (uint32_t j = 0; j < RS_SMALL_IPT; ++j) {
