@@ -154,6 +154,12 @@ __device__ __forceinline__ long long wave_min64(long long k) {
   return k;
 }
 
+// the batch key table and the flags words cleared (one launch)
+__global__ void __launch_bounds__(BLOCK) k_fi_clear(unsigned long long* keys, uint32_t cap, uint32_t* fi) {
+  GRID_STRIDE(q, cap) keys[q] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < FI_WORDS) fi[threadIdx.x] = 0;
+}
+
 // batch keys -> op index; a key seen twice fails the batch
 __global__ void __launch_bounds__(BLOCK) k_fi_bidx(OpsDev o, TsHash bh, uint32_t* fi) {
   GRID_STRIDE(i, o.n) {
@@ -317,14 +323,13 @@ __global__ void __launch_bounds__(BLOCK) k_fi_gap(uint32_t m, uint32_t K, const 
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_fi_pos(uint32_t m, const uint32_t* gv, uint32_t* pos) {
-  GRID_STRIDE(k, m) pos[gv[k]] = k;
-}
-
-// gap heads: the first sorted position of every gap, listed (any order);
-// one item per thread (wave-aggregated tickets: ~10k heads on one counter)
-__global__ void __launch_bounds__(BLOCK) k_fi_gstart(uint32_t m, const uint32_t* gk, uint32_t* list, uint32_t* cnt) {
+// sorted position of every op (pos) and the gap heads: the first sorted
+// position of every gap, listed (any order); one item per thread
+// (wave-aggregated tickets: ~10k heads on one counter)
+__global__ void __launch_bounds__(BLOCK) k_fi_gstart(uint32_t m, const uint32_t* gk, const uint32_t* gv,
+                                                     uint32_t* pos, uint32_t* list, uint32_t* cnt) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < m) pos[gv[k]] = k;
   const bool head = k < m && (k == 0 || gk[k - 1] != gk[k]);
   const uint32_t t = wave_ticket(cnt, head);
   if (head) list[t] = k;
@@ -612,14 +617,17 @@ __global__ void __launch_bounds__(BLOCK) k_fi_dense_gaps(uint32_t m, uint32_t Kp
 // the LDS stage walks global memory instead); then ord[] = the list order
 // and first[] = the gap's first sorted position.
 constexpr uint32_t FI_GAP_LDS = 1024;
-__global__ void __launch_bounds__(64) k_fi_gaps(uint32_t m, const uint32_t* list, const uint32_t* cnt,
-                                                const uint32_t* gk, const uint32_t* gv, const uint32_t* par0,
-                                                const uint32_t* pos, const long long* ts, uint32_t* nxt,
-                                                uint32_t* ord, uint32_t* first, uint32_t* fi) {
-  __shared__ long long lk[FI_GAP_LDS];
-  __shared__ uint32_t la[FI_GAP_LDS], ln[FI_GAP_LDS], lo[FI_GAP_LDS];
-  const uint32_t w = blockIdx.x, lane = threadIdx.x;
-  if (w >= *cnt) return;
+struct FiGapLds {
+  long long lk[FI_GAP_LDS];
+  uint32_t la[FI_GAP_LDS], ln[FI_GAP_LDS], lo[FI_GAP_LDS];
+};
+__device__ __forceinline__ void fi_gap_one(uint32_t w, uint32_t m, const uint32_t* list, const uint32_t* gk,
+                                           const uint32_t* gv, const uint32_t* par0, const uint32_t* pos,
+                                           const long long* ts, uint32_t* nxt, uint32_t* ord, uint32_t* first,
+                                           uint32_t* fi, FiGapLds& L) {
+  long long* lk = L.lk;
+  uint32_t *la = L.la, *ln = L.ln, *lo = L.lo;
+  const uint32_t lane = threadIdx.x;
   const uint32_t k = list[w], g = gk[k];
   uint32_t e = k + 1;  // the gap's end: 64 positions per step
   for (;;) {
@@ -633,16 +641,30 @@ __global__ void __launch_bounds__(64) k_fi_gaps(uint32_t m, const uint32_t* list
   }
   const uint32_t n = e - k;
   if (n <= FI_GAP_LDS) {
-    for (uint32_t j = lane; j < n; j += 64) {
-      const uint32_t op = gv[k + j];
-      lk[j] = ts[op];
-      const uint32_t a = par0[op];
-      uint32_t l = NONE;
-      if (a != NONE) {
-        const uint32_t pa = pos[a];
-        if (pa >= k && pa < e) l = pa - k;
+    // three dependent gathers (op, its key and anchor, the anchor's sorted
+    // position), each issued for all of the lane's entries at once
+    constexpr uint32_t PER = FI_GAP_LDS / 64;
+    uint32_t op[PER], av[PER];
+    long long kv[PER];
+#pragma unroll
+    for (uint32_t u = 0; u < PER; ++u) {
+      const uint32_t j = lane + 64 * u;
+      op[u] = j < n ? gv[k + j] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < PER; ++u) {
+      const bool in = lane + 64 * u < n;
+      kv[u] = in ? ts[op[u]] : 0;
+      av[u] = in ? par0[op[u]] : NONE;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < PER; ++u) {
+      const uint32_t j = lane + 64 * u;
+      if (j < n) {
+        const uint32_t pa = av[u] != NONE ? pos[av[u]] : NONE;
+        lk[j] = kv[u];
+        la[j] = (pa >= k && pa < e) ? pa - k : NONE;
       }
-      la[j] = l;
     }
     __syncthreads();
     if (lane == 0) {
@@ -705,6 +727,21 @@ __global__ void __launch_bounds__(64) k_fi_gaps(uint32_t m, const uint32_t* list
   }
 }
 
+// (a grid of at most FI_GAPS_GRID single-wave workgroups loops over the gaps:
+// one per op would schedule thousands of LDS-holding workgroups that exit)
+constexpr uint32_t FI_GAPS_GRID = 2048;
+__global__ void __launch_bounds__(64) k_fi_gaps(uint32_t m, const uint32_t* list, const uint32_t* cnt,
+                                                const uint32_t* gk, const uint32_t* gv, const uint32_t* par0,
+                                                const uint32_t* pos, const long long* ts, uint32_t* nxt,
+                                                uint32_t* ord, uint32_t* first, uint32_t* fi) {
+  __shared__ FiGapLds L;
+  const uint32_t ng = *cnt;
+  for (uint32_t w = blockIdx.x; w < ng; w += gridDim.x) {
+    fi_gap_one(w, m, list, gk, gv, par0, pos, ts, nxt, ord, first, fi, L);
+    __syncthreads();  // (the next gap reuses the LDS)
+  }
+}
+
 // new document ranks: base rank r -> r + (new nodes in gaps <= r); new node
 // at sorted position k -> its gap + the new nodes of earlier gaps + its order.
 // Each workgroup bounds its base ranks' searches by two searches of its own.
@@ -751,9 +788,11 @@ __global__ void __launch_bounds__(BLOCK) k_fi_next(uint32_t K, uint32_t m, const
 
 // node records of the new slots and the log append (every op applied, |path| = 1)
 __global__ void __launch_bounds__(BLOCK) k_fi_commit(OpsDev o, uint32_t slot0, uint32_t log0, uint32_t lpath0,
-                                                     TreeDev T) {
+                                                     TreeDev T, uint8_t* st, uint8_t* st_out) {
   GRID_STRIDE(i, o.n) {
     const uint32_t sl = slot0 + i;
+    st[i] = ST_APPLIED;
+    if (st_out) st_out[i] = CRDTM_ST_APPLIED;
     T.s_key[sl] = o.ts[i];
     T.s_src[sl] = log0 + i;
     T.s_flags[sl] = 0;
@@ -919,8 +958,7 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   const TsHash kx{X.keys, X.vals, X.mask};
   uint32_t* rank_of = X.rank;
   // ---- phase A: anchors, validity ----
-  HIP_CHECK(hipMemsetAsync(fi, 0, FI_WORDS * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(bh.keys, 0, static_cast<size_t>(bcap) * sizeof(unsigned long long), s));
+  LAUNCH(k_fi_clear, dim3(grid_for(bcap)), dim3(BLOCK), 0, s, bh.keys, bcap, fi);
   LAUNCH(k_fi_bidx, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, bh, fi);
   LAUNCH(k_fi_resolve, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, kx, bh, rank_of, replica_of(t->timestamp), par[0],
          par0, sta[0], thr[0], fi);
@@ -936,9 +974,8 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   uint32_t *sk = gk[1], *sv = gv[1];
   if ((r = radix_sort_small(gk[0], gv[0], m, bits, sk, sv, s))) return r;
   const uint32_t gm = (m + BLOCK - 1) / BLOCK;  // one item per thread
-  LAUNCH(k_fi_pos, dim3(grid_for(m)), dim3(BLOCK), 0, s, m, sv, pos);
-  LAUNCH(k_fi_gstart, dim3(gm), dim3(BLOCK), 0, s, m, sk, glist, fi + 2);
-  LAUNCH(k_fi_gaps, dim3(m), dim3(64), 0, s, m, glist, fi + 2, sk, sv, par0, pos, o.ts, nxt, ord, first, fi);
+  LAUNCH(k_fi_gstart, dim3(gm), dim3(BLOCK), 0, s, m, sk, sv, pos, glist, fi + 2);
+  LAUNCH(k_fi_gaps, dim3(std::min(m, FI_GAPS_GRID)), dim3(64), 0, s, m, glist, fi + 2, sk, sv, par0, pos, o.ts, nxt, ord, first, fi);
   LAUNCH(k_fi_tblk, dim3(gm), dim3(BLOCK), 0, s, m, nbk, sk, ord, X.bent, X.bcnt, X.bfirst, X.bend, tl, gpred, fi);
   LAUNCH(k_fi_win_pick, dim3(grid_for(64ULL * m)), dim3(BLOCK), 0, s, nbk, sk, tl, X.bcnt, X.bfirst, X.bend, X.bwin,
          ovl, fi);
@@ -967,7 +1004,7 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
     if ((r = grow_tree(t, need))) return r;
   const uint32_t slot0 = static_cast<uint32_t>(t->n_slots);
   LAUNCH(k_fi_commit, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, slot0, static_cast<uint32_t>(t->log_n),
-         static_cast<uint32_t>(t->log_npath), t->d);
+         static_cast<uint32_t>(t->log_npath), t->d, st, st_out);
   if (!dense) {  // O(batch): the blocks the batch lands in
     LAUNCH(k_fi_rewrite, dim3(hf[3]), dim3(FI_CAP), 0, s, nbk, tl, fi, sk, sv, ord, first, gpred, slot0, o.ts, X.bent,
            X.bdk, X.bcnt, X.bfirst, X.bend, X.bwin, X.bmin, rank_of, t->d.s_next);
@@ -1005,9 +1042,7 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
     t->doc_gapped = false;
   }
   LAUNCH(k_kx_insert, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, slot0, kx);
-  HIP_CHECK(hipMemsetAsync(st, ST_APPLIED, m, s));
   if ((r = replica_fold(c, o, st, rep, ws, s))) return r;
-  if (st_out) HIP_CHECK(hipMemsetAsync(st_out, CRDTM_ST_APPLIED, m, s));
   if ((r = sync_read(c))) return r;
   if ((r = take_replicas(t, rep))) return r;
   t->n_slots += m;
