@@ -19,6 +19,8 @@ PATH_REPLAY = 2
 PATH_DICT_REPLAY = 3
 FLAG_REMERGE = 1  # non-fresh tree merged as init ++ log ++ batch on the parallel paths
 FLAG_INCREMENTAL = 2  # adds-only batch merged into a clean flat document in place (incr.hip)
+FLAG_INCR_WINDOWS = 4  # ... and blocks of its gapped order were spread over rebalance windows
+FLAG_INCR_DENSE = 8  # ... and no window could take it: merged densely, the blocks rebuilt
 REF_NONE = 2 ** 64 - 1
 REF_ROOT = 2 ** 64 - 2
 REL_PARENT, REL_NEXT, REL_PREV, REL_HEAD = 0, 1, 2, 3

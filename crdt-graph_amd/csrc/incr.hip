@@ -1054,7 +1054,8 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   t->timestamp = new_ts;
   t->flat_clean = true;
   res->path_taken = CRDTM_PATH_CLOSED_FORM;
-  res->flags |= CRDTM_FLAG_INCREMENTAL;
+  res->flags |= CRDTM_FLAG_INCREMENTAL | (dense ? CRDTM_FLAG_INCR_DENSE : 0u) |
+                (!dense && hf[5] ? CRDTM_FLAG_INCR_WINDOWS : 0u);
   res->n_applied = m;
   res->n_already = 0;
   *handled = true;

@@ -88,6 +88,8 @@ typedef struct crdtm_result {
 #define CRDTM_FLAG_REMERGE 1 /* non-fresh tree: merged as init ++ log ++ batch on the parallel paths */
 #define CRDTM_FLAG_INCREMENTAL 2 /* non-fresh flat tree, adds-only batch: merged into the document in place
                                     (incremental closed form, gaps of the base order; incr.hip) */
+#define CRDTM_FLAG_INCR_WINDOWS 4 /* with INCREMENTAL: blocks of the gapped order were spread over windows */
+#define CRDTM_FLAG_INCR_DENSE 8   /* with INCREMENTAL: no window could take the batch: dense merge, rebuilt */
 
 typedef struct crdtm_ctx crdtm_ctx;   /* device + stream + workspace */
 typedef struct crdtm_tree crdtm_tree; /* one replica's CRDTree state, resident in HBM */

@@ -111,6 +111,12 @@ FINC_STREAMS = {
     "r4_w2000": dict(n_ops=60000, replicas=4, window=2000, seed=42),
     "r16_w16": dict(n_ops=60000, replicas=16, window=16, seed=43),
     "r2_w1": dict(n_ops=30000, replicas=2, window=1, seed=44),
+    # one cursor typing on: every batch lands in one gap at the document's
+    # end (rebalance windows over the last blocks, a gap too large for any
+    # window: the dense merge)
+    "r1_cursor": dict(n_ops=60000, replicas=1, window=1, p_continue=1.0, seed=45),
+    # three cursors that rarely jump: a few hot gaps per batch
+    "r3_hot": dict(n_ops=60000, replicas=3, window=4, p_continue=0.995, seed=46),
 }
 
 
@@ -131,13 +137,15 @@ def test_incremental_flat_closed_form(name, monkeypatch):
         cuts.append(min(n, cuts[-1] + int(rng.choice([1, 2, 64, 1000, 5000, 16000]))))
     ot = olib().orc_init(0)
     et = CRDTree.init(0)
-    used = 0
+    used = windows = dense = 0
     for k, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
         chunk = sub(s, a, b)
         _, rc, _ = oracle_apply_arrays(chunk, b - a, tree=ot)
         res = et.apply_arrays(chunk, b - a)
         assert res.code == rc == 0, (k, res.code, rc)
         used += bool(res.flags & N.FLAG_INCREMENTAL)
+        windows += bool(res.flags & N.FLAG_INCR_WINDOWS)
+        dense += bool(res.flags & N.FLAG_INCR_DENSE)
         if k % 7 == 0 or b == n:
             assert engine_summary(et) == oracle_summary(ot), (k, a, b)
             assert engine_log(et, 1) == oracle_log(ot, 1), k
@@ -148,6 +156,8 @@ def test_incremental_flat_closed_form(name, monkeypatch):
             assert np.array_equal(v.document_handles(), oracle_visible_vals(ot))
             del v
     assert used == len(cuts) - 2
+    if name == "r1_cursor":  # one hot gap: the windows and the dense merge both ran
+        assert windows and dense, (windows, dense)
     assert engine_log(et, 0) == oracle_log(ot, 0)
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
     # a Delete makes the document unclean: no incremental closed form afterwards
