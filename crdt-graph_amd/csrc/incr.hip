@@ -285,6 +285,64 @@ __global__ void __launch_bounds__(FI_JUMP_THREADS) k_fi_jump(uint32_t m, uint32_
   }
 }
 
+// The same with the thresholds themselves in LDS (8 + 2 bytes per op: m <=
+// FI_JUMP_LDS_MAX): no global gather in the rounds.
+constexpr uint32_t FI_JUMP_LDS_MAX = 16000;
+__global__ void __launch_bounds__(FI_JUMP_THREADS) k_fi_jump_lds(uint32_t m, uint32_t rounds, const uint32_t* P,
+                                                                 uint32_t* S, long long* T) {
+  extern __shared__ unsigned long long fi_jump_lds[];
+  long long* lt = reinterpret_cast<long long*>(fi_jump_lds);  // [m] threshold over [i, pointer)
+  uint16_t* lp = reinterpret_cast<uint16_t*>(lt + m);         // [m] pointer
+  uint16_t mp[FI_JUMP_PER];
+  long long mv[FI_JUMP_PER];
+#pragma unroll
+  for (uint32_t u = 0; u < FI_JUMP_PER; ++u) {
+    const uint32_t i = threadIdx.x + u * FI_JUMP_THREADS;
+    const uint32_t p = i < m ? P[i] : NONE;
+    mp[u] = p == NONE ? FI_J_NONE : static_cast<uint16_t>(p);
+    mv[u] = i < m ? T[i] : 0;
+    if (i < m) {
+      lp[i] = mp[u];
+      lt[i] = mv[u];
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = 0; k < rounds; ++k) {
+    int moved = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < FI_JUMP_PER; ++u) {
+      const uint16_t p = mp[u];
+      if (p != FI_J_NONE) {
+        const uint16_t pp = lp[p];
+        if (pp != FI_J_NONE) {
+          mv[u] = min(mv[u], lt[p]);
+          mp[u] = pp;
+          moved = 1;
+        }
+      }
+    }
+    __syncthreads();  // every read of this round before any write
+#pragma unroll
+    for (uint32_t u = 0; u < FI_JUMP_PER; ++u) {
+      const uint32_t i = threadIdx.x + u * FI_JUMP_THREADS;
+      if (i < m) {
+        lp[i] = mp[u];
+        lt[i] = mv[u];
+      }
+    }
+    if (!__syncthreads_or(moved)) break;
+  }
+#pragma unroll
+  for (uint32_t u = 0; u < FI_JUMP_PER; ++u) {
+    const uint32_t i = threadIdx.x + u * FI_JUMP_THREADS;
+    const uint16_t r = mp[u];
+    if (i < m && r != FI_J_NONE) {
+      S[i] = S[r];  // (a root's own start: roots are not written)
+      T[i] = min(mv[u], lt[r]);  // (a root's threshold is its own timestamp)
+    }
+  }
+}
+
 // g = NSR(start, thr) over the base keys, one wave per query: 64 keys, 64
 // block minima or 64 superblock minima per step (ballot), then down again
 __global__ void __launch_bounds__(BLOCK) k_fi_gap(uint32_t m, uint32_t K, const long long* dk, const long long* bmin,
@@ -966,7 +1024,14 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   // over the gapped order), the blocks they land in ----
   uint32_t rounds = 0;
   for (uint32_t span = 1; span < m; span <<= 1) ++rounds;
-  if (rounds) LAUNCH(k_fi_jump, dim3(1), dim3(FI_JUMP_THREADS), 0, s, m, rounds, par[0], sta[0], thr[0], o.ts);
+  static const bool jump_lds = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fi_jump_lds),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   FI_JUMP_LDS_MAX * 10) == hipSuccess;
+  if (rounds && jump_lds && m <= FI_JUMP_LDS_MAX)
+    LAUNCH(k_fi_jump_lds, dim3(1), dim3(FI_JUMP_THREADS), static_cast<size_t>(m) * 10, s, m, rounds, par[0], sta[0],
+           thr[0]);
+  else if (rounds)
+    LAUNCH(k_fi_jump, dim3(1), dim3(FI_JUMP_THREADS), 0, s, m, rounds, par[0], sta[0], thr[0], o.ts);
   LAUNCH(k_fi_gap, dim3(grid_for(64ULL * m)), dim3(BLOCK), 0, s, m, Kp, X.bdk, X.bmin, X.smin, sta[0], thr[0], gk[0],
          gv[0]);
   uint32_t bits = 4;  // (gap positions run to Kp inclusive)
