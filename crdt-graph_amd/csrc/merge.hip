@@ -2778,10 +2778,18 @@ __global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint
   }
   __syncthreads();
   uint32_t present = 0, err = NONE;
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t q0 = blockIdx.x * blockDim.x; q0 < Q; q0 += gridDim.x * blockDim.x) {
+  const uint32_t lane = threadIdx.x & 63, stride = gridDim.x * blockDim.x;
+  // (the next slot's record and run id load before this slot's stores)
+  uint32_t q0 = blockIdx.x * blockDim.x;
+  unsigned long long rq_n = q0 + threadIdx.x < Q ? rec[q0 + threadIdx.x] : REC_EMPTY;
+  uint32_t rid_n = q0 + threadIdx.x < Q ? rid[q0 + threadIdx.x] : 0u;
+  for (; q0 < Q; q0 += stride) {
     const uint32_t q = q0 + threadIdx.x;
-    const unsigned long long rq = q < Q ? rec[q] : REC_EMPTY;
+    const unsigned long long rq = rq_n;
+    const uint32_t rid_q = rid_n;
+    const uint32_t qn = q + stride;
+    rq_n = qn < Q ? rec[qn] : REC_EMPTY;
+    rid_n = qn < Q ? rid[qn] : 0u;
     // the previous slot's record from the neighbouring lane (a wave holds consecutive slots)
     unsigned long long rp = __shfl_up(rq, 1, 64);
     if (chk && lane == 0 && q > 0 && q < Q) rp = rec[q - 1];
@@ -2789,7 +2797,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint
     if (rq != REC_EMPTY) {
       fi = static_cast<uint32_t>(rq >> 32);
       const uint32_t slot = 1 + (qc ? qc[q] : q);
-      const uint32_t r = rid[q] - 1;
+      const uint32_t r = rid_q - 1;
       uint32_t p = a.posh[r] + (q - a.heads[r]);
       const uint2 er = a.er[r];
       const uint32_t e0 = er.x, e1 = er.y;
