@@ -361,6 +361,15 @@ int crdtm_tree_clone(const crdtm_tree* t, crdtm_tree** out) {
   return CRDTM_OK;
 }
 
+// Linearise inside apply when the batch is at least 1/16 of the document
+// (env CRDTM_LINEARIZE=eager|lazy overrides).
+static bool linearize_eagerly(const crdtm_tree* t, uint64_t n) {
+  const char* e = getenv("CRDTM_LINEARIZE");
+  if (e && !strcmp(e, "eager")) return true;
+  if (e && !strcmp(e, "lazy")) return false;
+  return 16 * n >= t->n_slots;
+}
+
 int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_batch, uint8_t* status_out,
                 crdtm_result* res) {
   if (!t || !ops || !res) return CRDTM_E_ARG;
@@ -445,20 +454,26 @@ int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_b
     // lastOperation: the op itself, or Batch of the applied ops; an
     // AlreadyApplied single op leaves Batch [] (src/CRDTree.elm:318-319)
     t->last_is_batch = (is_batch || res->n_applied == 0) ? 1 : 0;
-    // Every path leaves the document order (north-star kernel 4) current:
-    // the closed forms compute it as they merge; the replays' states are
-    // linearised here, inside the call (and inside a timed bench step).
-    if (!t->doc_valid && n) {
+    // The document order (north-star kernel 4): the closed forms compute it
+    // as they merge; a replay's state is linearised here, inside the call
+    // (and inside a timed bench step), when the batch is large against the
+    // document — linearising is O(document), so a small edit leaves it to
+    // the first read (crdtm_tree_document, clone), which linearises then.
+    // The batch is committed at this point: a failure here only leaves the
+    // order to that first read.
+    if (!t->doc_valid && n && linearize_eagerly(t, n)) {
       r = ensure_arena(c, arena_need(0, 0, t) + 64 * (t->n_slots + t->n_dicts));
-      if (r) return r;
       g_prof = c->profile ? c : nullptr;
       try {
-        r = linearize(t);
+        if (r == CRDTM_OK) r = linearize(t);
       } catch (const ArenaOverflow&) {
         r = CRDTM_E_NOMEM;
       }
       g_prof = nullptr;
-      if (r) return r;
+      if (r != CRDTM_OK) {
+        t->doc_valid = false;
+        r = CRDTM_OK;
+      }
     }
   }
   res->timestamp = t->timestamp;

@@ -290,15 +290,26 @@ inline void prof_mark(const char* name, hipStream_t st) {
 }
 // Host wait for everything queued on stream s by polling an event (a
 // blocking stream synchronisation sleeps and wakes ~15 us late, idling the
-// device between the phases of a merge). One event per host thread.
+// device between the phases of a merge). One event per host thread and
+// device (the caller has made the stream's device current); the poll loop
+// pauses between queries so a waiting thread does not hammer the runtime.
+inline void spin_pause() { __builtin_ia32_pause(); }
 inline int stream_wait(hipStream_t s) {
-  static thread_local hipEvent_t ev = nullptr;
-  if (!ev) HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-  HIP_CHECK(hipEventRecord(ev, s));
+  constexpr int MAXDEV = 64;
+  static thread_local hipEvent_t ev[MAXDEV] = {};
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= MAXDEV) {
+    HIP_CHECK(hipStreamSynchronize(s));
+    return CRDTM_OK;
+  }
+  if (!ev[dev]) HIP_CHECK(hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming));
+  HIP_CHECK(hipEventRecord(ev[dev], s));
   for (;;) {
-    const hipError_t e = hipEventQuery(ev);
+    const hipError_t e = hipEventQuery(ev[dev]);
     if (e == hipSuccess) return CRDTM_OK;
     if (e != hipErrorNotReady) HIP_CHECK(e);
+    spin_pause();
   }
 }
 

@@ -1049,6 +1049,11 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   HIP_CHECK(hipMemcpyAsync(hf, fi, sizeof(hf), hipMemcpyDeviceToHost, s));
   if (int rw = stream_wait(s)) return rw;
   const long long new_ts = t->timestamp + hf[1];
+  // (resolved before phase C: nothing may fail once the commit is queued)
+  static const bool win_lds = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fi_win),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                  FI_WIN_ENT * 12) == hipSuccess;
+  if (hf[5] && !win_lds) hf[0] |= FI_OVER;  // (no LDS for the windows: the dense merge takes the batch)
   if ((hf[0] & (FI_FAIL | FI_BUDGET)) || replica_of(new_ts) != replica_of(t->timestamp)) {
     // the general paths decide: the state is untouched, the key index stays
     // valid; the blocks' per-batch marks are not cleared, so they are rebuilt
@@ -1073,10 +1078,6 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   if (!dense) {  // O(batch): the blocks the batch lands in
     LAUNCH(k_fi_rewrite, dim3(hf[3]), dim3(FI_CAP), 0, s, nbk, tl, fi, sk, sv, ord, first, gpred, slot0, o.ts, X.bent,
            X.bdk, X.bcnt, X.bfirst, X.bend, X.bwin, X.bmin, rank_of, t->d.s_next);
-    static const bool win_lds = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fi_win),
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                    FI_WIN_ENT * 12) == hipSuccess;
-    if (hf[5] && !win_lds) return CRDTM_E_HIP;
     if (hf[5])
       LAUNCH(k_fi_win, dim3(hf[5]), dim3(FI_WIN_THREADS), FI_WIN_ENT * 12, s, nbk, wl, wlev, fi, sk, sv, ord, first,
              gpred, slot0, o.ts, X.bent, X.bdk, X.bcnt, X.bfirst, X.bend, X.bwin, X.bmin, rank_of, t->d.s_next);

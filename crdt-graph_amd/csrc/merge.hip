@@ -3024,6 +3024,7 @@ int sync_read(crdtm_ctx* c) {
     const hipError_t e = hipEventQuery(c->ev_sync);
     if (e == hipSuccess) break;
     if (e != hipErrorNotReady) HIP_CHECK(e);
+    spin_pause();
   }
   if (c->hres->scan_err) {
     std::fprintf(stderr, "crdtm: a device scan's look-back did not resolve\n");

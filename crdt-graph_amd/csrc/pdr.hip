@@ -92,7 +92,8 @@ struct PdrCtx {
   // its own timestamp — a node that canonical RGA would pass and that was
   // deleted before the Add: the first such Add of a
   // dict ends the prefix the closed form could serve exactly.
-  unsigned long long* gcount;  // [0] Adds that walked, [1] G-failing ones, [2] ops before each dict's first failure
+  unsigned long long* gcount;  // [0] Adds that walked, [1] G-failing ones, [2] ops before each dict's first failure,
+                               // [3] ops the dicts' replays reached
   PdrInst I;
 };
 
@@ -100,8 +101,8 @@ struct PdrCtx {
 // kind 0: slot word := a; kind 1: copy payload (node carried a, children dict
 // b); kind 2: children as-of op a. A snapshot as of op b is the last write per
 // slot among the entries with op < b, found in parallel (k_pdr_snap_*).
-constexpr uint32_t PDR_LOG_MIN = 512;
-constexpr uint32_t PDR_LANE = 32;  // dicts of at most this many slots replay on one lane (k_pdr_lane)  // smaller dicts re-replay their snapshots (env CRDTM_PDR_LOG_MIN)
+constexpr uint32_t PDR_LOG_MIN = 512;  // smaller dicts re-replay their snapshots (env CRDTM_PDR_LOG_MIN)
+constexpr uint32_t PDR_LANE = 32;      // dicts of at most this many slots replay on one lane (k_pdr_lane)
 
 __device__ __forceinline__ uint32_t pdr_kcount(const PdrCtx& p, uint32_t D) { return p.cbase[D + 1] - p.cbase[D]; }
 
@@ -266,7 +267,9 @@ __device__ __forceinline__ uint32_t pdr_next_live(const uint32_t* S, uint32_t K,
   return p;
 }
 
-__device__ __forceinline__ void pdr_gstat_flush(const PdrCtx& p, uint32_t adds, uint32_t fails, uint32_t prefix) {
+__device__ __forceinline__ void pdr_gstat_flush(const PdrCtx& p, uint32_t adds, uint32_t fails, uint32_t prefix,
+                                                uint32_t ops) {
+  if (ops) atomicAdd(&p.gcount[3], static_cast<unsigned long long>(ops));
   if (adds) atomicAdd(&p.gcount[0], static_cast<unsigned long long>(adds));
   if (fails) atomicAdd(&p.gcount[1], static_cast<unsigned long long>(fails));
   if (prefix) atomicAdd(&p.gcount[2], static_cast<unsigned long long>(prefix));
@@ -465,7 +468,7 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
            p.rbase[D + 1] - p.rbase[D], g_stc[4], g_stc[0], g_stc[1], g_stc[2], g_stc[3], clock64() - t_start);
 #endif
   if (ORIG && lane == 0) p.logn[D] = (logging && ln <= lcap) ? ln : NONE;
-  if (gst && lane == 0) pdr_gstat_flush(p, g_adds, g_fail, (g_first == NONE ? oe : g_first) - ob);
+  if (gst && lane == 0) pdr_gstat_flush(p, g_adds, g_fail, (g_first == NONE ? oe : g_first) - ob, oe - ob);
   __syncthreads();
   if (S != p.S + base) {
     for (uint32_t r = lane; r <= K; r += 64) p.S[base + r] = S[r];
@@ -986,7 +989,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
     }
   }
   if (ORIG && lane == 0) p.logn[D] = (logging && ln <= lcap) ? ln : NONE;
-  if (gst && lane == 0) pdr_gstat_flush(p, g_adds, g_fail, (g_first == NONE ? oe : g_first) - ob);
+  if (gst && lane == 0) pdr_gstat_flush(p, g_adds, g_fail, (g_first == NONE ? oe : g_first) - ob, oe - ob);
   for (uint32_t r = lane; r <= K; r += 64) p.inst[base + r] = I;
 }
 
@@ -1737,8 +1740,7 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   if (p.gcount) {  // (only a replay that serves the batch reports)
     unsigned long long gh[4];
     HIP_CHECK(hipMemcpy(gh, c->gstat_dev, sizeof(gh), hipMemcpyDeviceToHost));
-    for (int k = 0; k < 3; ++k) c->gstat[k] = gh[k];
-    c->gstat[3] = n;
+    for (int k = 0; k < 4; ++k) c->gstat[k] = gh[k];
     c->gstat_valid = 1;
   }
   *handled = true;

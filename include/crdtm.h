@@ -251,7 +251,8 @@ void crdtm_free(void *p);
  * canonical RGA would pass, deleted before the Add; a dict's first such Add
  * ends the prefix a closed form could serve exactly. out[0] Adds that walked,
  * out[1] G-failing Adds, out[2] ops of the replayed dicts before each dict's
- * first G-failing Add, out[3] ops replayed. Returns 1 when the last apply of
+ * first G-failing Add, out[3] ops the replayed dicts reached (ops that
+ * stopped at a Tombstone on their path, or no dict, are not counted). Returns 1 when the last apply of
  * this context collected them, else 0 (out zeroed). */
 int crdtm_ctx_guard_stats(crdtm_ctx *ctx, uint64_t *out);
 

@@ -654,15 +654,134 @@ void orc_merge_last(orc_tree* o, const orc_tree* prev) {
 // specialised to an Adds-only batch on a fresh tree whose paths all have
 // length 1 (one dict, no Tombstone besides the sentinel, so no copy quirk):
 // the dict is an array of keys in ascending order with a `next` link per
-// key, so a 10M-op batch replays in seconds instead of the general
-// restatement's minutes. Used for full-size parity of config 3; pinned
-// against orc_apply by tests/test_oracle_kat.py. Returns 0 (Ok), 3
-// (OperationFailed) with *err_index, or -1 when the batch is outside the
+// key. Pinned against orc_apply by tests/test_oracle_kat.py. Returns 0 (Ok),
+// 3 (OperationFailed) with *err_index, or -1 when the batch is outside the
 // specialisation (a Delete, a path of length != 1). hash[0..1] / words[0..1]
 // receive the canonical structure and visible-order digests (orc_canonical).
+//
+// Two ways to run findInsertion's walk (:93-104), same `next` links:
+//  * literal (orc_flat_replay_literal): follow `next` from the anchor while
+//    the inserted key is below the next key. A walk passes every larger key
+//    after its anchor, so a low replica id's Add in a long document walks
+//    ~10^4-10^5 nodes: config 3's 10M ops take hours;
+//  * searched (orc_flat_replay): the same stop node found in O(log n). The
+//    loop stops at the last node u after the anchor such that every node
+//    after the anchor up to u has a key above x (keys are distinct: `made`),
+//    i.e. u = the node before the first node after the anchor whose key is
+//    below x, or the list's last node when there is none. A treap over the
+//    list order with the smallest key per subtree finds that first node
+//    (climb from the anchor, descend into the first subtree whose minimum is
+//    below x). Used for full-size parity of config 3; pinned against the
+//    literal walk by tests/test_oracle_flat.py.
+namespace {
+struct ListTreap {  // in-order = the dict's `next` order; ids = key slots (slot order = key order)
+  static constexpr uint32_t NIL = 0xFFFFFFFFu;
+  std::vector<uint32_t> L, R, P, mn;
+  uint32_t root = NIL;
+  explicit ListTreap(size_t k) : L(k, NIL), R(k, NIL), P(k, NIL), mn(k, NIL) {}
+  static uint64_t pri(uint32_t v) {
+    uint64_t z = v + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+  }
+  uint32_t submin(uint32_t t) const { return t == NIL ? NIL : mn[t]; }
+  void pull(uint32_t t) { mn[t] = std::min(t, std::min(submin(L[t]), submin(R[t]))); }
+  // the first node at or after the in-order start of subtree t with id < x
+  uint32_t leftmost_less(uint32_t t, uint32_t x) const {
+    for (;;) {
+      if (L[t] != NIL && mn[L[t]] < x) t = L[t];
+      else if (t < x) return t;
+      else t = R[t];
+    }
+  }
+  // the first node after a (in-order) with id < x, NIL if none
+  uint32_t first_after_less(uint32_t a, uint32_t x) const {
+    if (R[a] != NIL && mn[R[a]] < x) return leftmost_less(R[a], x);
+    for (uint32_t c = a; P[c] != NIL; c = P[c]) {
+      const uint32_t p = P[c];
+      if (L[p] != c) continue;  // c was p's right child: p comes before
+      if (p < x) return p;
+      if (R[p] != NIL && mn[R[p]] < x) return leftmost_less(R[p], x);
+    }
+    return NIL;
+  }
+  uint32_t pred(uint32_t b) const {
+    if (L[b] != NIL) {
+      uint32_t t = L[b];
+      while (R[t] != NIL) t = R[t];
+      return t;
+    }
+    uint32_t c = b;
+    while (P[c] != NIL && L[P[c]] == c) c = P[c];
+    return P[c];
+  }
+  uint32_t last() const {
+    uint32_t t = root;
+    while (R[t] != NIL) t = R[t];
+    return t;
+  }
+  void rotate_up(uint32_t y) {  // y takes its parent's place
+    const uint32_t p = P[y], g = P[p];
+    if (L[p] == y) {
+      L[p] = R[y];
+      if (R[y] != NIL) P[R[y]] = p;
+      R[y] = p;
+    } else {
+      R[p] = L[y];
+      if (L[y] != NIL) P[L[y]] = p;
+      L[y] = p;
+    }
+    P[p] = y;
+    P[y] = g;
+    if (g == NIL) root = y;
+    else if (L[g] == p) L[g] = y;
+    else R[g] = y;
+    pull(p);
+    pull(y);
+  }
+  void insert_first(uint32_t y) {
+    root = y;
+    mn[y] = y;
+  }
+  // y right after u in the order
+  void insert_after(uint32_t u, uint32_t y) {
+    uint32_t at = u;
+    bool left = false;
+    if (R[u] != NIL) {
+      at = R[u];
+      while (L[at] != NIL) at = L[at];
+      left = true;
+    }
+    (left ? L[at] : R[at]) = y;
+    P[y] = at;
+    mn[y] = y;
+    for (uint32_t t = at; t != NIL && mn[t] > y; t = P[t]) mn[t] = y;
+    while (P[y] != NIL && pri(y) > pri(P[y])) rotate_up(y);
+  }
+};
+
+int flat_replay(bool searched, uint64_t n, const uint8_t* kind, const int64_t* ts, const uint32_t* path_off,
+                const int64_t* path, const uint32_t* val, int64_t* err_index, uint64_t* hash, uint64_t* words,
+                uint64_t* n_applied);
+}  // namespace
+
 extern "C" int orc_flat_replay(uint64_t n, const uint8_t* kind, const int64_t* ts, const uint32_t* path_off,
                                const int64_t* path, const uint32_t* val, int64_t* err_index, uint64_t* hash,
                                uint64_t* words, uint64_t* n_applied) {
+  return flat_replay(true, n, kind, ts, path_off, path, val, err_index, hash, words, n_applied);
+}
+
+extern "C" int orc_flat_replay_literal(uint64_t n, const uint8_t* kind, const int64_t* ts, const uint32_t* path_off,
+                                       const int64_t* path, const uint32_t* val, int64_t* err_index, uint64_t* hash,
+                                       uint64_t* words, uint64_t* n_applied) {
+  return flat_replay(false, n, kind, ts, path_off, path, val, err_index, hash, words, n_applied);
+}
+
+namespace {
+int flat_replay(bool searched, uint64_t n, const uint8_t* kind, const int64_t* ts, const uint32_t* path_off,
+                const int64_t* path, const uint32_t* val, int64_t* err_index, uint64_t* hash, uint64_t* words,
+                uint64_t* n_applied) {
   std::vector<int64_t> keys;
   keys.reserve(n + 1);
   keys.push_back(0);
@@ -682,6 +801,8 @@ extern "C" int orc_flat_replay(uint64_t n, const uint8_t* kind, const int64_t* t
   std::vector<uint8_t> made(K, 0);
   const int64_t z = slot(0);
   made[z] = 1;  // the sentinel 0 -> Tombstone [] Nothing
+  ListTreap tr(searched ? K : 0);
+  if (searched) tr.insert_first(static_cast<uint32_t>(z));
   uint64_t applied = 0;
   for (uint64_t i = 0; i < n; ++i) {
     const int64_t x = slot(ts[i]);  // always found
@@ -693,10 +814,16 @@ extern "C" int orc_flat_replay(uint64_t n, const uint8_t* kind, const int64_t* t
     }
     // findInsertion: slot order is key order, and no node but the sentinel is a Tombstone
     uint32_t node = static_cast<uint32_t>(a);
-    for (;;) {
-      const uint32_t rn = nxt[node];
-      if (rn == NIL || x > static_cast<int64_t>(rn)) break;
-      node = rn;
+    if (searched) {
+      const uint32_t b = tr.first_after_less(node, static_cast<uint32_t>(x));
+      node = b == NIL ? tr.last() : tr.pred(b);
+      tr.insert_after(node, static_cast<uint32_t>(x));
+    } else {
+      for (;;) {
+        const uint32_t rn = nxt[node];
+        if (rn == NIL || x > static_cast<int64_t>(rn)) break;
+        node = rn;
+      }
     }
     nxt[x] = nxt[node];
     nxt[node] = static_cast<uint32_t>(x);
@@ -737,6 +864,7 @@ extern "C" int orc_flat_replay(uint64_t n, const uint8_t* kind, const int64_t* t
   words[1] = s1.n;
   return 0;
 }
+}  // namespace
 
 // ---- full-size property check of a flat merge (test infrastructure) ----
 // For an Adds-only batch with paths of length 1 on a fresh tree, every

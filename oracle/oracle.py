@@ -66,6 +66,8 @@ def lib():
         L.orc_node_query.argtypes = [P, C.c_int, P, C.c_uint64, P, C.c_uint64]
         L.orc_flat_replay.restype = C.c_int
         L.orc_flat_replay.argtypes = [C.c_uint64, P, P, P, P, P, C.POINTER(C.c_int64), P, P, C.POINTER(C.c_uint64)]
+        L.orc_flat_replay_literal.restype = C.c_int
+        L.orc_flat_replay_literal.argtypes = L.orc_flat_replay.argtypes
         L.orc_flat_check.restype = C.c_uint64
         L.orc_flat_check.argtypes = [C.c_uint64, P, C.c_uint64, P, P, P]
         L.orc_reset_last.argtypes = [P]

@@ -9,9 +9,12 @@ document).
 * the RGA order properties of oracle/crdtree_oracle.cpp `orc_flat_check`:
   each key after its anchor, every key between them larger (what every
   findInsertion walk guarantees for an Adds-only flat batch);
-* the first 1M ops of the same stream: canonical structure and visible
-  digests equal the fast flat restatement's (`orc_flat_replay`, pinned
-  against the general restatement in tests/test_oracle_kat.py).
+* exact parity over all 10M ops: canonical structure and visible digests
+  and their word counts equal the searched flat restatement's
+  (`orc_flat_replay`: findInsertion's stop node through a treap, pinned
+  against the literal walk in tests/test_oracle_flat.py, which
+  tests/test_oracle_kat.py pins against the general restatement); the
+  reference behaviour is src/Internal/Node.elm:93-104 over 10M siblings.
 """
 import ctypes as C
 
@@ -42,6 +45,17 @@ def test_flat10m_order_properties():
     assert np.array_equal(t.document_handles().astype(np.int64), words[1::4])
     bad = olib().orc_flat_check(n, _ptr(keys), n, _ptr(s["ts"]), _ptr(s["path_off"]), _ptr(s["path"]))
     assert bad == 0, bad
+    # exact: the whole batch through the searched restatement (~15 s on one core)
+    h = np.zeros(2, np.uint64)
+    w = np.zeros(2, np.uint64)
+    err = C.c_int64(-1)
+    na = C.c_uint64()
+    rc = olib().orc_flat_replay(n, _ptr(s["kind"]), _ptr(s["ts"]), _ptr(s["path_off"]), _ptr(s["path"]),
+                                _ptr(s["val"]), C.byref(err), _ptr(h), _ptr(w), C.byref(na))
+    assert rc == 0 and na.value == n
+    for which in (0, 1):
+        _, enw, eh = t.canonical(which, full=False)
+        assert (enw, eh) == (int(w[which]), int(h[which])), which
 
 
 def test_flat1m_matches_fast_restatement():
