@@ -225,6 +225,7 @@ int crdtm_ctx_destroy(crdtm_ctx* c) {
   hipFree(c->dres);
   hipHostFree(c->hres);
   hipFree(c->crange);
+  if (c->fl_rec) hipFree(c->fl_rec);
   hipFree(c->ws.scan_status);
   hipFree(c->rtab);
   if (c->gstat_dev) hipFree(c->gstat_dev);

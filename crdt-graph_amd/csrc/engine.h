@@ -104,6 +104,11 @@ struct crdtm_ctx {
   crdtm::DevResult* hres = nullptr;  // pinned host
   uint32_t* rtab = nullptr;          // replica table [REPLICA_SLOTS], 0 = empty (kept clean between calls)
   uint2* crange = nullptr;           // replica counter ranges [RID_SLOTS] {min, max}, kept clean between calls
+  // flat merge: slot -> anchor code tagged with the merge's epoch (merge.hip
+  // FlatRec); a slot carrying another epoch holds no Add, so no clearing pass
+  uint2* fl_rec = nullptr;
+  uint64_t fl_cap = 0;
+  uint32_t fl_epoch = 0;
   bool profile = false;
   // profiling: one {name, begin, end} event pair per kernel launch
   struct Mark {
@@ -215,7 +220,8 @@ int segmented_sort_asc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* c
                           hipStream_t st, DevResult* dres);
 // stable LSD radix sort of (key, value) pairs by the low `bits` key bits (primitives.hip)
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, const uint32_t* n_dev, uint32_t n_max,
-                     uint32_t bits, Arena& ws, hipStream_t st, uint32_t** out_k, uint32_t** out_v);
+                     uint32_t bits, Arena& ws, hipStream_t st, uint32_t** out_k, uint32_t** out_v,
+                     uint32_t* inv = nullptr);
 // the same for n <= RS_SMALL_MAX pairs in one workgroup (primitives.hip), into (kout, vout)
 constexpr uint32_t RS_SMALL_MAX = 16384;
 int radix_sort_small(const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t bits, uint32_t* kout,

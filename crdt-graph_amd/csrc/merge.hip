@@ -1999,10 +1999,34 @@ __global__ void __launch_bounds__(64) k_forest(OpsDev o, ForestArgs f, const uin
 // Q. anc[q] = ABSENT marks a slot without an applied Add.
 // ---------------------------------------------------------------------------
 
-// K1 (flat). Slot records rec[q] = (index of the first Add of slot q) << 32
-// | (anchor slot of that Add: Q = the dict's sentinel, NONE = anchor key not
-// in the batch); REC_EMPTY = no Add.
-constexpr unsigned long long REC_EMPTY = ~0ULL;
+// K1 (flat). Slot records rec[q] = {x: the anchor code of slot q's Add (its
+// anchor slot, Q = the dict's sentinel, or `anone` = anchor key not in the
+// batch) tagged with the merge's epoch, y: that Add's op index} (y is valid
+// only where x is present; one 8-byte record, so the claim scatters one store
+// per op and a reader of both halves touches one line). rec is the context's
+// own buffer (engine.h crdtm_ctx::fl_rec): every flat merge takes the next
+// epoch (1..62), so a slot whose word carries another epoch holds no Add and
+// nothing clears the buffer between merges (a clearing pass wrote 80 MB per
+// 10M-slot merge); the buffer is zeroed when the epochs wrap. Narrow mode
+// packs the epoch into the top 6 bits of x and needs Q < 2^26 - 2; wide mode
+// (larger Q) keeps full 32-bit anchor codes and clears x to FR_EMPTY before
+// each merge (k_fl_init).
+constexpr uint32_t FR_EMPTY = 0xFFFFFFFFu;
+constexpr uint32_t FR_ABITS = 26;
+constexpr uint32_t FR_EPOCHS = 62;  // (epoch 63 with a missing anchor would read as FR_EMPTY)
+struct FlatRec {
+  uint2* rec;
+  uint32_t ep;     // epoch << FR_ABITS (narrow), 0 (wide)
+  uint32_t amask;  // anchor code field
+  uint32_t anone;  // code of a missing anchor
+  __device__ __forceinline__ bool present(uint32_t w) const { return w != FR_EMPTY && (w & ~amask) == ep; }
+  __device__ __forceinline__ uint32_t code(uint32_t qa) const { return (qa == NONE ? anone : qa) | ep; }
+  // slot, Q (the sentinel) or NONE
+  __device__ __forceinline__ uint32_t anchor(uint32_t w) const {
+    const uint32_t a = w & amask;
+    return a == anone ? NONE : a;
+  }
+};
 
 // K1 (flat), one pass over the ops: every Add writes its slot record with
 // one plain 8-byte store (an arbitrary duplicate wins), and the pass folds
@@ -2026,7 +2050,7 @@ constexpr unsigned long long REC_EMPTY = ~0ULL;
 // path[i]: the pass reads the timestamps, anchors (and values for the log) as
 // 16-byte vectors and writes the log's kinds and offsets without reading them.
 template <bool SIMPLE>
-__global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_t Q, unsigned long long* rec,
+__global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_t Q, FlatRec fr,
                                                     long long ts0, uint32_t* rtab, DevResult* dres,
                                                     uint32_t track_rep, uint32_t nrep, TreeDev T,
                                                     uint32_t log_to_tree) {
@@ -2137,7 +2161,7 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
       ++keys;
       const long long kk = pk[k];
       const uint32_t qa = kk == 0 ? Q : slot(kk);
-      rec[q] = (static_cast<unsigned long long>(i) << 32) | qa;
+      fr.rec[q] = make_uint2(fr.code(qa), i);
       if (track_rep) {
         const uint32_t rr = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32);
         if (rr < REP_DIRECT) {
@@ -2173,9 +2197,8 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
 // then), fused with the batch accounting and the replicas fold: every
 // applied Add's replica keeps its last op index in a direct-mapped LDS table
 // (ids < REP_DIRECT), flushed once per workgroup into the replica table.
-__global__ void __launch_bounds__(BLOCK) k_fl_status(OpsDev o, uint8_t* st, TsIndex x, uint32_t Q,
-                                                     unsigned long long* rec, long long ts0, uint32_t* rtab,
-                                                     DevResult* dres) {
+__global__ void __launch_bounds__(BLOCK) k_fl_status(OpsDev o, uint8_t* st, TsIndex x, uint32_t Q, FlatRec fr,
+                                                     long long ts0, uint32_t* rtab, DevResult* dres) {
   __shared__ uint32_t rv[REP_DIRECT];
   for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) rv[j] = 0;
   __syncthreads();
@@ -2198,20 +2221,22 @@ __global__ void __launch_bounds__(BLOCK) k_fl_status(OpsDev o, uint8_t* st, TsIn
         if (q == NONE) {
           s = ST_ALREADY;  // ts 0 is the sentinel's key (:63-65)
         } else {
-          const unsigned long long r = rec[q];
-          const uint32_t fi = static_cast<uint32_t>(r >> 32);
+          const uint32_t fi = fr.rec[q].y;
           if (fi != i) {
             s = ST_ALREADY;  // `child ts parent` exists (:63-65)
-            if (i < fi) {    // lost the store race to a later duplicate: take the slot
-              const long long kk = o.path[qd.off[k]];
-              const uint32_t qa = kk == 0 ? Q : tsindex_slot(x, kk);
-              atomicMin(&rec[q], (static_cast<unsigned long long>(i) << 32) | qa);
+            if (i < fi) {    // lost the store race to a later duplicate: take the slot (decided again)
+              atomicMin(&fr.rec[q].y, i);
               dup = 1;
             }
           } else {
-            const uint32_t qa = static_cast<uint32_t>(r);
-            bool ok = qa == Q;  // anchored at the sentinel
-            if (!ok && qa != NONE) ok = static_cast<uint32_t>(rec[qa] >> 32) < i;  // anchor Added before (:68-70)
+            const long long kk = o.path[qd.off[k]];
+            const uint32_t qa = kk == 0 ? Q : tsindex_slot(x, kk);
+            fr.rec[q].x = fr.code(qa);  // (the op index may have reached the slot after a duplicate's anchor)
+            bool ok = qa == Q;          // anchored at the sentinel
+            if (!ok && qa != NONE) {    // anchor Added before (:68-70)
+              const uint2 ra = fr.rec[qa];
+              ok = fr.present(ra.x) && ra.y < i;
+            }
             s = ok ? ST_APPLIED : ST_NOTFOUND;
           }
         }
@@ -2292,73 +2317,188 @@ __global__ void __launch_bounds__(BLOCK) k_fl_rep_collect(OpsDev o, uint32_t nr,
   }
 }
 
-// Runs and their ids in one scan. A run is a maximal slot interval [h, e)
-// whose every slot but h is anchored at the slot before it (a replica's
-// typing run: consecutive counters are consecutive slots); an absent slot is
-// a run of its own with no node (a "hole" run). Head flags are summed into
-// rid[q] = 1 + the index of q's run; from the scanned values the generator
-// writes every run's head slot and the anchor of its head (epilogue). (The
-// later kernels read a slot's presence and anchor from its record.)
-struct RunIdGen {
-  static constexpr bool kStriped = false;  // loads through load() (8-byte records -> flags)
-  static constexpr bool kEpilogue = true;
-  __device__ __forceinline__ bool aligned(uint64_t) const { return false; }
-  __device__ __forceinline__ uint4 load4(uint64_t) const { return make_uint4(0u, 0u, 0u, 0u); }
-  const unsigned long long* rec;
-  uint32_t Q;
-  uint32_t* heads;  // run -> head slot
-  uint32_t* hanc;   // run -> anchor slot of its head (ABSENT: a hole run)
-  // A missing anchor (NONE) only occurs in a batch that fails (NotFound),
-  // which the flat speculation discards: it reads as the sentinel so that
-  // the speculative walks stay in bounds.
-  __device__ __forceinline__ uint32_t anchor(unsigned long long r) const {
-    if (r == REC_EMPTY) return ABSENT;
-    const uint32_t a = static_cast<uint32_t>(r);
-    return a == NONE ? Q : a;
-  }
-  // q continues the run of q - 1 iff both hold a node and q is anchored at q - 1
-  __device__ __forceinline__ uint32_t flag(uint32_t q, uint32_t a, uint32_t aprev) const {
-    return (q == 0 || a == ABSENT || aprev == ABSENT || a != q - 1) ? 1u : 0u;
-  }
-  __device__ __forceinline__ void load(uint64_t b, uint64_t n, uint32_t* v) const {
-    const uint32_t q0 = static_cast<uint32_t>(b);
-    uint32_t aprev = q0 > 0 && q0 - 1 < n ? anchor(rec[q0 - 1]) : ABSENT;
-    if (b + DS_ITEMS <= n) {
-      uint32_t a[DS_ITEMS];
-#pragma unroll
-      for (int j = 0; j < DS_ITEMS; j += 2) {
-        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(rec + b + j);
-        a[j] = anchor(x.x);
-        a[j + 1] = anchor(x.y);
-      }
-#pragma unroll
-      for (int j = 0; j < DS_ITEMS; ++j) {
-        v[j] = flag(q0 + j, a[j], aprev);
-        aprev = a[j];
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < DS_ITEMS; ++j) {
-        const uint64_t q = b + j;
-        const uint32_t a = q < n ? anchor(rec[q]) : ABSENT;
-        v[j] = q < n ? flag(static_cast<uint32_t>(q), a, aprev) : 0u;
-        aprev = a;
-      }
-    }
-  }
-  __device__ __forceinline__ void epilogue(uint64_t b, uint64_t n, const uint32_t* v, uint32_t start) const {
-    uint32_t prev = start;
-#pragma unroll
-    for (int j = 0; j < DS_ITEMS; ++j) {
-      const uint64_t q = b + j;
-      if (q < n && v[j] != prev) {  // a head: its run's index is v[j] - 1
-        heads[v[j] - 1] = static_cast<uint32_t>(q);
-        hanc[v[j] - 1] = anchor(rec[q]);  // (a line this thread has just read)
-      }
-      prev = v[j];
-    }
-  }
+// Runs. A run is a maximal slot interval [h, e) whose every slot but h is
+// anchored at the slot before it (a replica's typing run: consecutive
+// counters are consecutive slots); an absent slot is a run of its own with
+// no node (a "hole" run). The run of a slot is not stored per slot: every
+// word of 64 slots keeps the bit mask of its run heads (hm) and the number
+// of heads before it (hb, an exclusive scan of the masks' popcounts), so
+// run(q) = hb[q / 64] + popcount(hm[q / 64] up to q) - 1 — 12 bytes per 64
+// slots, small enough to stay in L2 while the walks below look runs up (a
+// 4-byte run id per slot was a 40 MB array written by a look-back scan and
+// read back by every walk step and by the slot pass).
+struct RunMask {
+  const unsigned long long* hm;
+  const uint32_t* hb;
 };
+__device__ __forceinline__ uint32_t run_of(const RunMask& rm, uint32_t q) {
+  const uint32_t w = q >> 6;
+  const unsigned long long below = (2ULL << (q & 63)) - 1ULL;  // (q & 63 == 63: every bit)
+  return rm.hb[w] + static_cast<uint32_t>(__popcll(rm.hm[w] & below)) - 1u;
+}
+
+// The key of slot q from the replica range tables: the replica r with
+// base[r] <= q (the largest such r: an empty range shares its base with the
+// next replica) and counter min[r] + q - base[r] (slot order = timestamp
+// order, src/CRDTree.elm:137).
+__device__ __forceinline__ long long fl_key(uint32_t q, const uint32_t* sb, const uint32_t* sc, uint32_t nrep,
+                                            uint32_t& rep) {
+  uint32_t lo = 0, hi = nrep;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (sb[mid] <= q) lo = mid;
+    else hi = mid;
+  }
+  rep = lo;
+  return (static_cast<long long>(lo) << 32) | static_cast<long long>(sc[lo] + (q - sb[lo]));
+}
+
+// One pass over the slot records in slot order, one wave per word of 64
+// slots (lane = slot):
+//  * the run heads by ballot (a missing anchor only occurs in a batch that
+//    fails, which the flat speculation discards): hm, and the count per word;
+//  * the node record of every present slot (tree slot 1 + its compacted
+//    index; key recomputed from the slot, tables in LDS when the replica ids
+//    fit, else the op's ts; implicit empty children dict): coalesced stores
+//    of a streaming pass, instead of the per-slot stores of the rank pass;
+//  * with `chk` (the flat speculation) the claim's check: every present
+//    slot's Add must come after its anchor's (addAfterHelp,
+//    src/Internal/Node.elm:68-70; inside a run the anchor is the slot before,
+//    whose record the neighbouring lane holds), the present slots are counted
+//    (as many as keyed Adds: no duplicate timestamps), and the replicas table
+//    is folded (a wave's slots usually lie in one replica's range: one LDS
+//    atomic per wave and replica).
+// The trip count is wave-uniform, so every lane takes part in the ballots.
+constexpr uint32_t RM_UNROLL = 4;
+__global__ void __launch_bounds__(BLOCK) k_run_mask(FlatRec fr, uint32_t Q, unsigned long long* hm, uint32_t* hc,
+                                                   TreeDev T, const uint32_t* qc, const uint32_t* logidx, OpsDev o,
+                                                   TsIndex x, uint32_t nrep, DevResult* chk, uint32_t* rtab) {
+  extern __shared__ uint32_t smk[];  // dynamic: 3 * nrep words when the tables fit (HOST_RANGES)
+  const bool lds = nrep <= HOST_RANGES;
+  uint32_t* sb = smk;
+  uint32_t* sc = smk + nrep;
+  uint32_t* srv = smk + 2 * nrep;  // (chk) largest op index + 1 per replica
+  if (lds) {
+    for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x) {
+      sb[j] = x.base[j];
+      sc[j] = x.rng[j].x;
+      srv[j] = 0;
+    }
+  }
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nw = (Q + 63) >> 6;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwave = (gridDim.x * blockDim.x) >> 6;
+  uint32_t present = 0, err = NONE;
+  for (uint32_t w0 = wave * RM_UNROLL; w0 < nw; w0 += nwave * RM_UNROLL) {
+    uint2 rq[RM_UNROLL], rp[RM_UNROLL];
+#pragma unroll
+    for (uint32_t u = 0; u < RM_UNROLL; ++u) {  // every load in flight first
+      const uint32_t q = ((w0 + u) << 6) + lane;
+      rq[u] = q < Q ? fr.rec[q] : make_uint2(FR_EMPTY, 0u);
+      rp[u] = (lane == 0 && q > 0 && q - 1 < Q) ? fr.rec[q - 1] : make_uint2(FR_EMPTY, 0u);
+    }
+    // the anchors' records of run heads (the check) load before this
+    // iteration's stores: gfx9 waits on loads and stores in issue order
+    uint2 ra[RM_UNROLL];
+#pragma unroll
+    for (uint32_t u = 0; u < RM_UNROLL; ++u) {
+      const uint32_t q = ((w0 + u) << 6) + lane;
+      const uint32_t px = __shfl_up(rq[u].x, 1, 64), py = __shfl_up(rq[u].y, 1, 64);
+      if (lane != 0) rp[u] = make_uint2(px, py);
+      const uint32_t qa = fr.anchor(rq[u].x);
+      ra[u] = make_uint2(FR_EMPTY, 0u);
+      if (chk && q < Q && fr.present(rq[u].x) && qa != Q && qa != NONE && qa + 1 != q) ra[u] = fr.rec[qa];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < RM_UNROLL; ++u) {
+      const uint32_t q = ((w0 + u) << 6) + lane;
+      const bool pres = q < Q && fr.present(rq[u].x);
+      const uint32_t qa = fr.anchor(rq[u].x);
+      const bool cont = pres && q > 0 && fr.present(rp[u].x) && qa == q - 1;
+      const unsigned long long m = __ballot(q < Q && !cont);
+      if (lane == 0 && w0 + u < nw) {
+        hm[w0 + u] = m;
+        hc[w0 + u] = static_cast<uint32_t>(__popcll(m));
+      }
+      uint32_t rep = NONE;
+      const uint32_t fi = rq[u].y;
+      if (pres) {
+        const uint32_t slot = 1 + (qc ? qc[q] : q);
+        T.s_key[slot] = lds ? fl_key(q, sb, sc, nrep, rep) : o.ts[fi];
+        T.s_dict[slot] = 0;
+        T.s_src[slot] = logidx ? logidx[fi] : fi;
+        T.s_flags[slot] = 0;
+        T.s_child[slot] = NONE;
+        if (chk) {
+          ++present;
+          if (qa != Q) {
+            bool ok = false;  // an Add at the anchor, before this one
+            if (qa + 1 == q) ok = fr.present(rp[u].x) && rp[u].y < fi;
+            else if (qa != NONE) ok = fr.present(ra[u].x) && ra[u].y < fi;
+            if (!ok) err = min(err, fi);
+          }
+        }
+      }
+      if (chk && lds) {  // (wave-uniform) replicas[r] := its last Add
+        const unsigned long long mr = __ballot(rep != NONE);
+        if (mr) {
+          const uint32_t r0 = __shfl(rep, __ffsll(static_cast<long long>(mr)) - 1, 64);
+          if (__ballot(rep != NONE && rep != r0) == 0) {
+            uint32_t v = rep != NONE ? fi + 1 : 0u;
+#pragma unroll
+            for (int o2 = 32; o2 > 0; o2 >>= 1) v = max(v, __shfl_xor(v, o2, 64));
+            if (lane == 0) atomicMax(&srv[r0], v);
+          } else if (rep != NONE) {
+            atomicMax(&srv[rep], fi + 1);
+          }
+        }
+      }
+    }
+  }
+  if (!chk) return;  // (grid-uniform)
+  present = block_sum(present);  // (synchronises the block: srv complete)
+  err = block_min(err);
+  if (lds)
+    for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x)
+      if (srv[j]) atomicMax(&rtab[j + (1u << (REPLICA_BITS - 1))], srv[j]);
+  if (threadIdx.x == 0) {
+    if (present) atomicAdd(&chk->fl_part[32 * (blockIdx.x & 15)], present);
+    if (err != NONE) atomicMin(&chk->err_index, err);
+  }
+}
+
+// Per run: its head slot and the head's anchor (ABSENT: a hole run; a
+// missing anchor reads as the sentinel so that the speculative walks stay in
+// bounds), hh[r] = {head, anchor}; k_run_ep replaces the anchor by the
+// head's effective parent.
+__global__ void __launch_bounds__(BLOCK) k_run_heads(FlatRec fr, uint32_t Q, RunMask rm, uint2* hh) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nw = (Q + 63) >> 6;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwave = (gridDim.x * blockDim.x) >> 6;
+  const unsigned long long lt = (1ULL << lane) - 1ULL;
+  for (uint32_t w0 = wave * RM_UNROLL; w0 < nw; w0 += nwave * RM_UNROLL) {
+    unsigned long long m[RM_UNROLL];
+    uint32_t x[RM_UNROLL], b[RM_UNROLL];
+#pragma unroll
+    for (uint32_t u = 0; u < RM_UNROLL; ++u) {  // every load in flight first
+      const uint32_t w = w0 + u;
+      m[u] = w < nw ? rm.hm[w] : 0ULL;
+      b[u] = w < nw ? rm.hb[w] : 0u;
+      x[u] = ((m[u] >> lane) & 1ULL) ? fr.rec[(w << 6) + lane].x : FR_EMPTY;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < RM_UNROLL; ++u) {
+      if (!((m[u] >> lane) & 1ULL)) continue;
+      uint32_t a = ABSENT;
+      if (fr.present(x[u])) {
+        a = fr.anchor(x[u]);
+        if (a == NONE) a = Q;
+      }
+      hh[b[u] + static_cast<uint32_t>(__popcll(m[u] & lt))] = make_uint2(((w0 + u) << 6) + lane, a);
+    }
+  }
+}
 
 // Counting-sort scatter; single-child parents (the common case in a typing
 // stream) take a plain store. The root sentinel's children are placed by
@@ -2463,8 +2603,8 @@ __global__ void __launch_bounds__(BLOCK) k_fl_next(uint32_t K, const uint32_t* d
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_fl_present(uint32_t Q, const unsigned long long* rec, uint32_t* f) {
-  GRID_STRIDE(q, Q) f[q] = rec[q] != REC_EMPTY ? 1u : 0u;
+__global__ void __launch_bounds__(BLOCK) k_fl_present(uint32_t Q, FlatRec fr, uint32_t* f) {
+  GRID_STRIDE(q, Q) f[q] = fr.present(fr.rec[q].x) ? 1u : 0u;
 }
 
 // Log append into a fresh tree when every op applied: the log is the batch
@@ -2529,16 +2669,17 @@ __global__ void __launch_bounds__(BLOCK) k_fl_log_copy(OpsDev o, TreeDev T) {
 // RUN_MAXD takes the generic Euler-tour list ranking instead (run_fail).
 // ---------------------------------------------------------------------------
 constexpr uint32_t RUN_MAXD = 64;
+constexpr uint32_t EX_ITERS = 128;  // k_run_expand keeps its run-mask words in LDS up to this many iterations
 
 struct RunArr {
   const uint32_t* nR;        // device: number of runs
-  uint32_t* heads;           // head slot
-  uint32_t* hanc;            // anchor of the head (ABSENT: a hole run), then its effective parent
+  uint2* hh;                 // {head slot, anchor of the head (ABSENT: a hole run), then its effective parent}
   uint32_t* par;             // parent run (NONE: a child of the root sentinel, or a hole run)
   uint32_t* len;
   uint2* er;                 // sorted positions [er.x, er.y) of the run's child runs ({0, 0}: none)
   unsigned long long* ca;    // children arrived << 32 | their subtree sizes
-  uint32_t* T;               // subtree size
+  uint32_t* tk;              // subtree sizes in sorted order (k_run_tree_up writes T(r) at kinv[r])
+  const uint32_t* kinv;      // run -> its position in the sorted order
   uint32_t* w;               // top-down increment along the chain
   uint32_t* posh;            // document rank of the head
 };
@@ -2549,21 +2690,31 @@ struct RunArr {
 // effective parent (the first node on its anchor chain below it), and only a
 // head anchored at a larger slot walks: the chain runs down through whole
 // runs (a run's slots are all larger than x when its head is), so each step
-// jumps from the run holding d to its head's anchor (flat10m: 0.49M walks of
-// at most 23 steps). hanc[] is overwritten with ep as walks finish; a
-// concurrent reader then sees ep(h) instead of anchor(h), which skips only
-// nodes > h > x, so every walk stays exact. Then the run's parent run (the
-// run holding ep), its length, and the sibling sort's input (key = attach
-// slot, the root sentinel = Q, hole runs Q + 1) listed in descending run
-// order, so the stable sort leaves siblings at one slot in descending slot
-// order.
-__global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, const uint32_t* rid,
-                                                  const unsigned long long* rec, uint32_t* skey, uint32_t* sval) {
+// jumps from the run holding d to its head's anchor (flat10m: 0.49M walks,
+// mean 3.7 steps, at most 23). hh[].y is overwritten with ep as walks
+// finish; a concurrent reader then sees ep(h) instead of anchor(h), which
+// skips only nodes > h > x, so every walk stays exact. A walk only descends
+// to smaller heads, so the runs are taken from the last one down (the grid
+// starts with the largest slots): most steps then meet an effective parent
+// already resolved. Each step is one look-up of the run masks (L2) and one
+// 8-byte {head, anchor} load. Then the run's parent run (the run holding ep),
+// its length, and the sibling sort's input (key = attach slot, the root
+// sentinel = Q, hole runs Q + 1) listed in descending run order, so the
+// stable sort leaves siblings at one slot in descending slot order.
+__device__ __forceinline__ uint2 hh_load(const uint2* p) {
+  const unsigned long long v =
+      __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_uint2(static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32));
+}
+__global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, RunMask rm, FlatRec fr, uint32_t* skey,
+                                                  uint32_t* sval, uint32_t ab) {
   const uint32_t R = *a.nR;
-  RUN_LOOP(r) {
-    const uint32_t x = a.heads[r];
-    uint32_t d = a.hanc[r];
-    const uint32_t hn = r + 1 < R ? a.heads[r + 1] : Q;
+  RUN_LOOP(k) {
+    const uint32_t r = (ab & 1) ? k : R - 1 - k;
+    const uint2 me = a.hh[r];
+    const uint32_t x = me.x;
+    uint32_t d = me.y;
+    const uint32_t hn = r + 1 < R ? a.hh[r + 1].x : Q;
     if (d == ABSENT) {  // a hole run
       a.par[r] = NONE;
       a.len[r] = 0;
@@ -2579,21 +2730,21 @@ __global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, const ui
       // or hold a cycle: those walks end at the sentinel, which keeps every
       // walk finite and in bounds, and the speculation is discarded)
       for (uint32_t steps = 0; d < Q && d > x; ++steps) {
-        const uint32_t j = rid[d] - 1;
-        const uint32_t h = a.heads[j];
-        if (h <= x || steps > R) {
+        const uint2 hj = hh_load(a.hh + run_of(rm, d));
+        if (hj.x <= x || steps > R) {
           d = Q;
           break;
         }
-        d = __hip_atomic_load(&a.hanc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        d = hj.y;
       }
-      if (d >= Q || rec[d] == REC_EMPTY) d = Q;
-      __hip_atomic_store(&a.hanc[r], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (d != Q && (d >= x || rec[d] == REC_EMPTY)) {  // (self-anchored / nodeless anchor: a failing batch)
+      if (d >= Q || !fr.present(fr.rec[d].x)) d = Q;
+      if (ab & 2) a.hh[r].y = d;
+      else __hip_atomic_store(&a.hh[r].y, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (d != Q && (d >= x || !fr.present(fr.rec[d].x))) {  // (self-anchored / nodeless anchor: a failing batch)
       d = Q;
-      a.hanc[r] = d;
+      __hip_atomic_store(&a.hh[r].y, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    a.par[r] = d == Q ? NONE : rid[d] - 1;
+    a.par[r] = d == Q ? NONE : run_of(rm, d);
     a.len[r] = hn - x;  // (a hole after the run is a run of its own)
     a.er[r] = make_uint2(0u, 0u);
     a.ca[r] = 0;
@@ -2605,15 +2756,15 @@ __global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, const ui
 // The generic order's input (a run tree deeper than RUN_MAXD): ep per slot
 // (q - 1 inside a run, the walked effective parent at a head, ABSENT = no
 // node), into anc.
-__global__ void __launch_bounds__(BLOCK) k_run_ep_slots(RunArr a, uint32_t Q, const uint32_t* rid,
-                                                        const unsigned long long* rec, uint32_t* anc) {
+__global__ void __launch_bounds__(BLOCK) k_run_ep_slots(RunArr a, uint32_t Q, RunMask rm, FlatRec fr,
+                                                        uint32_t* anc) {
   GRID_STRIDE(q, Q) {
-    if (rec[q] == REC_EMPTY) {
+    if (!fr.present(fr.rec[q].x)) {
       anc[q] = ABSENT;
       continue;
     }
-    const uint32_t r = rid[q] - 1;
-    anc[q] = a.heads[r] == q ? a.hanc[r] : q - 1;
+    const uint2 h = a.hh[run_of(rm, q)];
+    anc[q] = h.x == q ? h.y : q - 1;
   }
 }
 
@@ -2628,7 +2779,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_ep_slots(RunArr a, uint32_t Q, co
 // thousands of atomics on one word, ~12 ns each).
 __device__ __forceinline__ void run_climb(RunArr& a, uint32_t x, uint32_t t) {
   for (;;) {
-    a.T[x] = t;
+    a.tk[a.kinv[x]] = t;
     const uint32_t p = a.par[x];
     if (p == NONE) return;
     const unsigned long long old = atomicAdd(&a.ca[p], (1ULL << 32) | t);
@@ -2652,7 +2803,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_tree_up(RunArr a, const uint32_t*
       const uint2 e = a.er[r];
       if (e.y == e.x) {
         const uint32_t t = a.len[r];
-        a.T[r] = t;
+        a.tk[k] = t;  // (kinv[r] == k)
         v = (1ULL << 32) | t;
       }
     }
@@ -2673,12 +2824,9 @@ __global__ void __launch_bounds__(BLOCK) k_run_tree_up(RunArr a, const uint32_t*
   }
 }
 
-// The subtree sizes in sorted order (tk), summed inclusively by the xs scan:
-// S(k) = the sizes of the first k entries = k ? xs[k - 1] : 0. (A gather
-// inside the scan's load would hold up its look-back chain.)
-__global__ void __launch_bounds__(BLOCK) k_run_gather(RunArr a, const uint32_t* sarr, uint32_t* tk) {
-  RUN_LOOP(k) tk[k] = a.T[sarr[k]];
-}
+// The subtree sizes in sorted order (tk, written by k_run_tree_up at each
+// run's sorted position), summed inclusively by the xs scan:
+// S(k) = the sizes of the first k entries = k ? xs[k - 1] : 0.
 __device__ __forceinline__ uint32_t run_S(const uint32_t* xs, uint32_t k) { return k ? xs[k - 1] : 0u; }
 
 // Per parent run P the sorted positions er = [x, y) of its child runs
@@ -2718,7 +2866,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_w(RunArr a, uint32_t Q, const uin
       a.w[r] = run_S(xs, k) - run_S(xs, *groot);
     } else {
       const uint32_t P = a.par[r];
-      a.w[r] = run_S(xs, k) - run_S(xs, a.er[P].x) + (p - a.heads[P]) + 1u;
+      a.w[r] = run_S(xs, k) - run_S(xs, a.er[P].x) + (p - a.hh[P].x) + 1u;
     }
   }
 }
@@ -2739,129 +2887,66 @@ __global__ void __launch_bounds__(BLOCK) k_run_pos(RunArr a, DevResult* dres) {
   }
 }
 
-// Per slot, the document order and the commit in one pass over slot order:
-// doc[rank] = tree slot, where rank = the head's rank + the slots of the run
-// before q + the subtrees of the run's child runs attached at slots below q
-// (child runs at q itself follow q; the run's child runs are contiguous in
-// the sorted list with ascending attach slots: a binary search finds the
-// first one at or above q, most runs have none); and the node record of tree
-// slot 1 + q (compacted: slot order = timestamp order), the key recomputed
-// from the slot (the replica r with base[r] <= q, largest such r, and
-// counter min[r] + q - base[r]; tables in LDS when the replica ids fit, else
-// the op's ts), its children dict implicit.
-//
-// With `chk` (the flat speculation) it also does the claim's check from the
-// records it reads anyway: every present slot's Add must come after its
-// anchor's (addAfterHelp, src/Internal/Node.elm:68-70; inside a run the
-// anchor is the slot before, whose record the neighbouring lane has just
-// read), the present slots are counted (as many as keyed Adds: no duplicate
-// timestamps) and, with the replica tables in LDS, the replicas table is
-// folded in slot order (a wave's 64 slots usually lie in one replica's
-// range: one LDS atomic per wave). The loop trip count is wave-uniform so
-// every lane takes part in the wave reductions.
-__global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint32_t K, const uint32_t* rid,
+// Per slot, the document order: doc[rank] = tree slot, where rank = the
+// head's rank + the slots of the run before q + the subtrees of the run's
+// child runs attached at slots below q (child runs at q itself follow q; the
+// run's child runs are contiguous in the sorted list with ascending attach
+// slots: a binary search finds the first one at or above q, most runs have
+// none). The run of q comes from the run masks of its word, which the
+// workgroup stages in LDS for all its iterations (gfx9 waits on its vector
+// memory counter in order, so a global prefetch of them would be waited for
+// before this slot's dependent loads).
+__global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint32_t K, RunMask rm,
                                                       const uint32_t* pk, const uint32_t* xs, const uint32_t* qc,
-                                                      uint32_t* doc, OpsDev o, TsIndex x, uint32_t nrep,
-                                                      const unsigned long long* rec, const uint32_t* logidx, TreeDev T,
-                                                      DevResult* chk, uint32_t* rtab) {
-  extern __shared__ uint32_t sbc[];  // dynamic: 3 * nrep words when the tables fit (HOST_RANGES)
-  uint32_t* sb = sbc;
-  uint32_t* sc = sbc + nrep;
-  uint32_t* srv = sbc + 2 * nrep;  // (chk) largest op index + 1 per replica
-  const bool lds = nrep <= HOST_RANGES;
-  if (lds) {
-    for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x) {
-      sb[j] = x.base[j];
-      sc[j] = x.rng[j].x;
-      srv[j] = 0;
+                                                      uint32_t* doc, FlatRec fr) {
+  extern __shared__ uint32_t smw[];  // [iters * waves] {mask lo, mask hi, base}
+  const uint32_t iters = (Q + gridDim.x * blockDim.x - 1) / (gridDim.x * blockDim.x);
+  const bool mlds = iters <= EX_ITERS;
+  const uint32_t wpb = blockDim.x >> 6;
+  if (mlds) {
+    const uint32_t nw = (Q + 63) >> 6;
+    for (uint32_t j = threadIdx.x; j < iters * wpb; j += blockDim.x) {
+      const uint32_t w = (blockIdx.x + (j / wpb) * gridDim.x) * wpb + j % wpb;
+      const unsigned long long m = w < nw ? rm.hm[w] : 0ULL;
+      smw[3 * j] = static_cast<uint32_t>(m);
+      smw[3 * j + 1] = static_cast<uint32_t>(m >> 32);
+      smw[3 * j + 2] = w < nw ? rm.hb[w] : 0u;
     }
   }
   __syncthreads();
-  uint32_t present = 0, err = NONE;
   const uint32_t lane = threadIdx.x & 63, stride = gridDim.x * blockDim.x;
-  // (the next slot's record and run id load before this slot's stores)
+  const unsigned long long below = (2ULL << lane) - 1ULL;
   uint32_t q0 = blockIdx.x * blockDim.x;
-  unsigned long long rq_n = q0 + threadIdx.x < Q ? rec[q0 + threadIdx.x] : REC_EMPTY;
-  uint32_t rid_n = q0 + threadIdx.x < Q ? rid[q0 + threadIdx.x] : 0u;
-  for (; q0 < Q; q0 += stride) {
+  uint32_t x_n = q0 + threadIdx.x < Q ? fr.rec[q0 + threadIdx.x].x : FR_EMPTY;  // (prefetch)
+  for (uint32_t it = 0; q0 < Q; q0 += stride, ++it) {
     const uint32_t q = q0 + threadIdx.x;
-    const unsigned long long rq = rq_n;
-    const uint32_t rid_q = rid_n;
-    const uint32_t qn = q + stride;
-    rq_n = qn < Q ? rec[qn] : REC_EMPTY;
-    rid_n = qn < Q ? rid[qn] : 0u;
-    // the previous slot's record from the neighbouring lane (a wave holds consecutive slots)
-    unsigned long long rp = __shfl_up(rq, 1, 64);
-    if (chk && lane == 0 && q > 0 && q < Q) rp = rec[q - 1];
-    uint32_t rep = NONE, fi = 0;
-    if (rq != REC_EMPTY) {
-      fi = static_cast<uint32_t>(rq >> 32);
-      const uint32_t slot = 1 + (qc ? qc[q] : q);
-      const uint32_t r = rid_q - 1;
-      uint32_t p = a.posh[r] + (q - a.heads[r]);
-      const uint2 er = a.er[r];
-      const uint32_t e0 = er.x, e1 = er.y;
-      if (e1 > e0) {
-        uint32_t lo = e0, hi = e1;  // first k with pk[k] >= q
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (pk[mid] < q) lo = mid + 1;
-          else hi = mid;
-        }
-        if (lo > e0) p += xs[lo - 1] - run_S(xs, e0);
-      }
-      if (p < K) doc[p] = slot;  // (a rank past K: a speculation that fails)
-      long long key;
-      if (lds) {
-        uint32_t lo = 0, hi = nrep;  // largest r with sb[r] <= q
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (sb[mid] <= q) lo = mid;
-          else hi = mid;
-        }
-        key = (static_cast<long long>(lo) << 32) | static_cast<long long>(sc[lo] + (q - sb[lo]));
-        rep = lo;
-      } else {
-        key = o.ts[fi];
-      }
-      T.s_key[slot] = key;
-      T.s_dict[slot] = 0;
-      T.s_src[slot] = logidx ? logidx[fi] : fi;
-      T.s_flags[slot] = 0;
-      T.s_child[slot] = NONE;
-      if (chk) {
-        ++present;
-        const uint32_t qa = static_cast<uint32_t>(rq);
-        if (qa != Q) {
-          const unsigned long long ra = qa == NONE ? REC_EMPTY : (qa + 1 == q ? rp : rec[qa]);
-          if (static_cast<uint32_t>(ra >> 32) >= fi) err = min(err, fi);  // (REC_EMPTY: no Add at the anchor)
-        }
-      }
+    const uint32_t xq = x_n;
+    x_n = q + stride < Q ? fr.rec[q + stride].x : FR_EMPTY;
+    if (!(q < Q && fr.present(xq))) continue;
+    unsigned long long mq;
+    uint32_t bq;
+    if (mlds) {
+      const uint32_t* e = smw + 3 * (it * wpb + (threadIdx.x >> 6));
+      mq = (static_cast<unsigned long long>(e[1]) << 32) | e[0];
+      bq = e[2];
+    } else {
+      mq = rm.hm[q >> 6];
+      bq = rm.hb[q >> 6];
     }
-    if (chk && lds) {  // (wave-uniform) replicas[r] := its last Add, one LDS atomic per wave and replica
-      const unsigned long long m = __ballot(rep != NONE);
-      if (m) {
-        const uint32_t r0 = __shfl(rep, __ffsll(static_cast<long long>(m)) - 1, 64);
-        if (__ballot(rep != NONE && rep != r0) == 0) {
-          uint32_t v = rep != NONE ? fi + 1 : 0u;
-#pragma unroll
-          for (int o2 = 32; o2 > 0; o2 >>= 1) v = max(v, __shfl_xor(v, o2, 64));
-          if ((threadIdx.x & 63) == 0) atomicMax(&srv[r0], v);
-        } else if (rep != NONE) {
-          atomicMax(&srv[rep], fi + 1);
-        }
+    const uint32_t r = bq + static_cast<uint32_t>(__popcll(mq & below)) - 1u;
+    uint32_t p = a.posh[r] + (q - a.hh[r].x);
+    const uint2 er = a.er[r];
+    const uint32_t e0 = er.x, e1 = er.y;
+    if (e1 > e0) {
+      uint32_t lo = e0, hi = e1;  // first k with pk[k] >= q
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pk[mid] < q) lo = mid + 1;
+        else hi = mid;
       }
+      if (lo > e0) p += xs[lo - 1] - run_S(xs, e0);
     }
-  }
-  if (!chk) return;  // (grid-uniform)
-  present = block_sum(present);  // (synchronises the block: srv complete)
-  err = block_min(err);
-  if (lds)
-    for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x)
-      if (srv[j]) atomicMax(&rtab[j + (1u << (REPLICA_BITS - 1))], srv[j]);
-  if (threadIdx.x == 0) {
-    if (present) atomicAdd(&chk->fl_part[32 * (blockIdx.x & 15)], present);
-    if (err != NONE) atomicMin(&chk->err_index, err);
+    if (p < K) doc[p] = 1 + (qc ? qc[q] : q);  // (a rank past K: a speculation that fails)
   }
 }
 
@@ -3186,14 +3271,59 @@ static int run_replay(crdtm_tree* t, const OpsDev& o, uint8_t* st, crdtm_result*
   return CRDTM_E_NOMEM;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_fl_init(uint32_t Q, unsigned long long* rec) {
-  GRID_STRIDE(q, Q) rec[q] = REC_EMPTY;
+__global__ void __launch_bounds__(BLOCK) k_fl_init(uint32_t Q, uint2* rec) {
+  GRID_STRIDE(q, Q) rec[q].x = FR_EMPTY;
+}
+
+// The slot records of one flat merge: a new epoch of the context's anchor
+// buffer (grown and zeroed when needed, zeroed when the epochs wrap; wide
+// mode clears it instead), the op indices from the arena.
+static int flat_rec(crdtm_ctx* c, uint32_t Q, FlatRec& fr) {
+  hipStream_t s = c->stream;
+  if (c->fl_cap < static_cast<uint64_t>(Q) + 1) {
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (c->fl_rec) HIP_CHECK(hipFree(c->fl_rec));
+    c->fl_rec = nullptr;
+    const uint64_t cap = std::max<uint64_t>(static_cast<uint64_t>(Q) + 1 + Q / 4, 1 << 16);
+    HIP_CHECK(hipMalloc(&c->fl_rec, cap * sizeof(uint2)));
+    c->fl_cap = cap;
+    c->fl_epoch = FR_EPOCHS;  // (forces the zeroing below)
+  }
+  fr.rec = c->fl_rec;
+  static const bool ab_arena = getenv("CRDTM_AB") && !strcmp(getenv("CRDTM_AB"), "arena");
+  if (ab_arena) fr.rec = c->ws.alloc<uint2>(Q + 1);
+  const bool narrow = !ab_arena && static_cast<uint64_t>(Q) + 2 < (1ULL << FR_ABITS) - 1;
+  if (narrow) {
+    if (++c->fl_epoch > FR_EPOCHS) {
+      HIP_CHECK(hipMemsetAsync(c->fl_rec, 0, c->fl_cap * sizeof(uint2), s));  // (epoch 0 is never current)
+      c->fl_epoch = 1;
+    }
+    fr.ep = c->fl_epoch << FR_ABITS;
+    fr.amask = (1u << FR_ABITS) - 1u;
+    fr.anone = fr.amask;
+  } else {
+    fr.ep = 0;
+    fr.amask = ~0u;
+    fr.anone = FR_EMPTY - 1u;
+    c->fl_epoch = FR_EPOCHS;  // (the next narrow merge zeroes the buffer first)
+    LAUNCH(k_fl_init, dim3(grid_for(Q, BLOCK, 4096)), dim3(BLOCK), 0, s, Q, fr.rec);
+  }
+  return CRDTM_OK;
 }
 
 // Launches k_range_reset when a merge leaves apply_batch by any path.
+// (`armed` is cleared when the merge reset the table itself, stream-ordered
+// before its final result read, and set again if it had to rebuild it)
 struct RangeReset {
   crdtm_ctx* c;
-  ~RangeReset() { LAUNCH(k_range_reset, dim3(64), dim3(BLOCK), 0, c->stream, c->crange, c->dres); }
+  bool armed = true;
+  void now() {
+    LAUNCH(k_range_reset, dim3(64), dim3(BLOCK), 0, c->stream, c->crange, c->dres);
+    armed = false;
+  }
+  ~RangeReset() {
+    if (armed) now();
+  }
 };
 
 // Flat closed form: launches K2/K4 (the order), the commit and the replica
@@ -3201,14 +3331,13 @@ struct RangeReset {
 // may be too deep (DevResult::run_fail, read with the final result): then
 // flat_order_fallback recomputes `doc` and the chain.
 struct FlatBufs {
-  unsigned long long* rec;
+  FlatRec fr;
   uint32_t* anc;
   uint32_t* cnt;
   uint32_t* fill;
   uint32_t* qc;
-  uint32_t* rid;    // slot -> 1 + its run
-  uint32_t* heads;  // run -> head slot
-  uint32_t* hanc;   // run -> effective parent of its head
+  RunMask rm;       // slot -> its run
+  uint2* hh;        // run -> {head slot, effective parent of its head}
   long long* rep;
 };
 
@@ -3228,53 +3357,21 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
   DevResult* dr = c->dres;
   const uint32_t n = o.n;
   const uint32_t g = grid_for(n);
-  unsigned long long* rec = fb.rec;
+  const FlatRec& fr = fb.fr;
   int r;
   fb.qc = nullptr;
   if (K > 0) {
-    // ---- runs: one scan (run ids, heads, anchors) ----
+    // ---- runs: head masks per word of 64 slots, their scan, {head, anchor} per run ----
     const uint32_t gq = grid_for(Q);
+    const uint32_t NW = (Q + 63) / 64;
     RunArr ra;
     ra.nR = &dr->run_count;
     // (a run per present slot at most, plus a hole run per absent slot)
-    ra.heads = fb.heads = ws.alloc<uint32_t>(Q + 1);
-    ra.hanc = fb.hanc = ws.alloc<uint32_t>(Q + 1);
-    uint32_t* rid = fb.rid = ws.alloc<uint32_t>(Q);
-    if ((r = dscan<SumOp, true>(RunIdGen{rec, Q, ra.heads, ra.hanc}, rid, Q, &dr->run_count, ws, s, nullptr,
-                                nullptr, "k_dscan_runs")))
-      return r;
-    uint32_t* qc = nullptr;
-    if (Q != K) {  // slots with no node: compact
-      qc = fb.qc = ws.alloc<uint32_t>(Q);
-      LAUNCH(k_fl_present, dim3(gq), dim3(BLOCK), 0, s, Q, rec, qc);
-      if ((r = scan_excl_u32(qc, qc, Q, nullptr, ws, s))) return r;
-    }
-    // ---- K2a (heads' effective parents), parent runs, sibling order (stable radix sort by attach slot) ----
-    ra.par = ws.alloc<uint32_t>(Q + 1);
-    ra.len = ws.alloc<uint32_t>(Q + 1);
-    ra.er = ws.alloc<uint2>(Q + 1);
-    ra.ca = ws.alloc<unsigned long long>(Q + 1);
-    ra.T = ws.alloc<uint32_t>(Q + 1);
-    ra.w = ws.alloc<uint32_t>(Q + 1);
-    ra.posh = ws.alloc<uint32_t>(Q + 1);
-    uint32_t* sk[2] = {ws.alloc<uint32_t>(Q + 1), ws.alloc<uint32_t>(Q + 1)};
-    uint32_t* sv[2] = {ws.alloc<uint32_t>(Q + 1), ws.alloc<uint32_t>(Q + 1)};
-    uint32_t* xs = ws.alloc<uint32_t>(Q + 1);
-    uint32_t* groot = fb.cnt;  // one word: the root sentinel's first child in the sorted list
-    const uint32_t gr = grid_for(Q, BLOCK, 2048);
-    LAUNCH(k_run_ep, dim3(gr), dim3(BLOCK), 0, s, ra, Q, rid, rec, sk[0], sv[0]);
-    uint32_t sbits = 8;
-    while (sbits < 32 && ((static_cast<uint64_t>(Q) + 1) >> sbits) != 0) sbits += 8;
-    uint32_t *pk = nullptr, *sarr = nullptr;  // attach slot, run: siblings grouped by slot, slots ascending
-    if ((r = radix_sort_pairs(sk[0], sv[0], sk[1], sv[1], ra.nR, Q, sbits, ws, s, &pk, &sarr))) return r;
-    LAUNCH(k_run_gstart, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, sarr, groot);
-    // ---- subtree sizes (one launch), head ranks, the document order ----
-    LAUNCH(k_run_tree_up, dim3(gr), dim3(BLOCK), 0, s, ra, sarr);
-    uint32_t* tk = pk == sk[0] ? sk[1] : sk[0];  // (free after the sort)
-    LAUNCH(k_run_gather, dim3(gr), dim3(BLOCK), 0, s, ra, sarr, tk);
-    if ((r = dscan<SumOp, true>(ArrGen{tk}, xs, Q, nullptr, ws, s, nullptr, ra.nR, "k_dscan_xs"))) return r;
-    LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, groot);
-    LAUNCH(k_run_pos, dim3(gr), dim3(BLOCK), 0, s, ra, dr);
+    ra.hh = fb.hh = ws.alloc<uint2>(Q + 1);
+    unsigned long long* hm = ws.alloc<unsigned long long>(NW + 1);
+    uint32_t* hc = ws.alloc<uint32_t>(NW + 1);
+    uint32_t* hb = ws.alloc<uint32_t>(NW + 1);
+    fb.rm = RunMask{hm, hb};
     uint32_t* logidx = nullptr;
     if (!all_applied) {  // compacted log (its scans share the ctx scan pool: main stream)
       logidx = ws.alloc<uint32_t>(n + 1);
@@ -3285,10 +3382,53 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
       LAUNCH(k_log, dim3(g), dim3(BLOCK), 0, s, o, st, t->d, 0u, 0u, logidx, plen);
       LAUNCH(k_log_tail, dim3(1), dim3(1), 0, s, t->d, 0u, &dr->log_n, 0u, &dr->log_npath);
     }
-    // ---- the document order and the commit (one pass), the chain ----
-    LAUNCH(k_run_expand, dim3(grid_for(Q, BLOCK, 2048)), dim3(BLOCK),
-           maxr + 1 <= HOST_RANGES ? 3 * (maxr + 1) * sizeof(uint32_t) : 0, s, ra, Q, K, rid, pk, xs, qc, t->d.doc,
-           o, ix, maxr + 1, rec, logidx, t->d, check ? dr : nullptr, c->rtab);
+    uint32_t* qc = nullptr;
+    if (Q != K) {  // slots with no node: compact
+      qc = fb.qc = ws.alloc<uint32_t>(Q);
+      LAUNCH(k_fl_present, dim3(gq), dim3(BLOCK), 0, s, Q, fr, qc);
+      if ((r = scan_excl_u32(qc, qc, Q, nullptr, ws, s))) return r;
+    }
+    const uint32_t gw = std::max<uint32_t>(1, std::min<uint32_t>(2048, (NW + RM_UNROLL * (BLOCK / 64) - 1) /
+                                                                           (RM_UNROLL * (BLOCK / 64))));
+    LAUNCH(k_run_mask, dim3(gw), dim3(BLOCK), maxr + 1 <= HOST_RANGES ? 3 * (maxr + 1) * sizeof(uint32_t) : 0, s,
+           fr, Q, hm, hc, t->d, qc, logidx, o, ix, maxr + 1, check ? dr : nullptr, c->rtab);
+    if ((r = dscan<SumOp, false>(ArrGen{hc}, hb, NW, &dr->run_count, ws, s, nullptr, nullptr, "k_dscan_runs")))
+      return r;
+    LAUNCH(k_run_heads, dim3(grid_for(64ULL * NW, BLOCK, 4096)), dim3(BLOCK), 0, s, fr, Q, fb.rm, ra.hh);
+    // ---- K2a (heads' effective parents), parent runs, sibling order (stable radix sort by attach slot) ----
+    ra.par = ws.alloc<uint32_t>(Q + 1);
+    ra.len = ws.alloc<uint32_t>(Q + 1);
+    ra.er = ws.alloc<uint2>(Q + 1);
+    ra.ca = ws.alloc<unsigned long long>(Q + 1);
+    uint32_t* kinv = ws.alloc<uint32_t>(Q + 1);
+    ra.kinv = kinv;
+    ra.w = ws.alloc<uint32_t>(Q + 1);
+    ra.posh = ws.alloc<uint32_t>(Q + 1);
+    uint32_t* sk[2] = {ws.alloc<uint32_t>(Q + 1), ws.alloc<uint32_t>(Q + 1)};
+    uint32_t* sv[2] = {ws.alloc<uint32_t>(Q + 1), ws.alloc<uint32_t>(Q + 1)};
+    uint32_t* xs = ws.alloc<uint32_t>(Q + 1);
+    uint32_t* groot = fb.cnt;  // one word: the root sentinel's first child in the sorted list
+    const uint32_t gr = grid_for(Q, BLOCK, 2048);
+    const char* abv = getenv("CRDTM_AB");
+    const uint32_t ab_ep = abv ? ((!strcmp(abv, "asc") ? 1u : 0u) | (!strcmp(abv, "plainst") ? 2u : 0u)) : 0u;
+    LAUNCH(k_run_ep, dim3(gr), dim3(BLOCK), 0, s, ra, Q, fb.rm, fr, sk[0], sv[0], ab_ep);
+    uint32_t sbits = 8;
+    while (sbits < 32 && ((static_cast<uint64_t>(Q) + 1) >> sbits) != 0) sbits += 8;
+    uint32_t *pk = nullptr, *sarr = nullptr;  // attach slot, run: siblings grouped by slot, slots ascending
+    if ((r = radix_sort_pairs(sk[0], sv[0], sk[1], sv[1], ra.nR, Q, sbits, ws, s, &pk, &sarr, kinv))) return r;
+    ra.tk = pk == sk[0] ? sk[1] : sk[0];  // (free after the sort)
+    LAUNCH(k_run_gstart, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, sarr, groot);
+    // ---- subtree sizes (one launch, in sorted order), head ranks, the document order ----
+    LAUNCH(k_run_tree_up, dim3(gr), dim3(BLOCK), 0, s, ra, sarr);
+    if ((r = dscan<SumOp, true>(ArrGen{ra.tk}, xs, Q, nullptr, ws, s, nullptr, ra.nR, "k_dscan_xs"))) return r;
+    LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, groot);
+    LAUNCH(k_run_pos, dim3(gr), dim3(BLOCK), 0, s, ra, dr);
+    // ---- the document order, the chain ----
+    const uint32_t gx = grid_for(Q, BLOCK, 2048);
+    const uint32_t ex_iters = (Q + gx * BLOCK - 1) / (gx * BLOCK);
+    LAUNCH(k_run_expand, dim3(gx), dim3(BLOCK),
+           ex_iters <= EX_ITERS ? 3 * ex_iters * (BLOCK / 64) * sizeof(uint32_t) : 0, s, ra, Q, K, fb.rm, pk, xs, qc,
+           t->d.doc, fr);
     LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d, t->cap.slots);
     if (all_applied && !log_done) fl_log_copy(c, o, t->d, simple);
   } else if (all_applied && !log_done) {
@@ -3316,9 +3456,8 @@ static int flat_order_fallback(crdtm_tree* t, uint32_t Q, uint32_t K, FlatBufs& 
   int r;
   {  // ep per slot (the run path keeps it per run)
     RunArr ra{};
-    ra.heads = fb.heads;
-    ra.hanc = fb.hanc;
-    LAUNCH(k_run_ep_slots, dim3(gq), dim3(BLOCK), 0, s, ra, Q, fb.rid, fb.rec, anc);
+    ra.hh = fb.hh;
+    LAUNCH(k_run_ep_slots, dim3(gq), dim3(BLOCK), 0, s, ra, Q, fb.rm, fb.fr, anc);
   }
   // ---- a run tree deeper than RUN_MAXD: children of every node, Euler tour + list ranking ----
   uint32_t* carr = ws.alloc<uint32_t>(U);
@@ -3353,7 +3492,7 @@ static int flat_order_fallback(crdtm_tree* t, uint32_t Q, uint32_t K, FlatBufs& 
 // batch where some op does not apply is then decided op by op and committed
 // again (the tree is fresh: its root sentinel is restored in between).
 static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_t Q, uint32_t maxr, uint8_t* st,
-                      uint8_t* st_out, crdtm_result* res, bool simple) {
+                      uint8_t* st_out, crdtm_result* res, bool simple, RangeReset& rr) {
   crdtm_ctx* c = t->ctx;
   hipStream_t s = c->stream;
   Arena& ws = c->ws;
@@ -3362,7 +3501,6 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   const uint32_t g = grid_for(n);
   const uint32_t U = Q + 1;  // nodes + the root sentinel
   FlatBufs fb{};
-  fb.rec = ws.alloc<unsigned long long>(Q + 1);
   fb.anc = ws.alloc<uint32_t>(U);
   fb.cnt = ws.alloc<uint32_t>(U + 1);
   fb.fill = ws.alloc<uint32_t>(U + 1);
@@ -3382,15 +3520,15 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   // speculation (below): every op applies, so the claim also writes the log
   const bool spec = Q >= n && !t->remerge;
   if (spec && (r = grow_for(n, n))) return r;
-  LAUNCH(k_fl_init, dim3(grid_for(Q, BLOCK, 4096)), dim3(BLOCK), 0, s, Q, fb.rec);
+  if ((r = flat_rec(c, Q, fb.fr))) return r;
   // replicas table: folded by the check over slot order when the range table fits in LDS
   const uint32_t nrep = maxr + 1 <= HOST_RANGES ? maxr + 1 : 0u;
   const uint32_t shm = (3 * nrep + (nrep ? 0 : REP_DIRECT)) * sizeof(uint32_t);
   if (simple)
-    LAUNCH(k_fl_claim<true>, dim3(quad_grid(n)), dim3(BLOCK), shm, s, o, ix, Q, fb.rec, t->timestamp, c->rtab, dr,
+    LAUNCH(k_fl_claim<true>, dim3(quad_grid(n)), dim3(BLOCK), shm, s, o, ix, Q, fb.fr, t->timestamp, c->rtab, dr,
            nrep ? 0u : 1u, nrep, t->d, spec ? 1u : 0u);
   else
-    LAUNCH(k_fl_claim<false>, dim3(quad_grid(n)), dim3(BLOCK), shm, s, o, ix, Q, fb.rec, t->timestamp, c->rtab, dr,
+    LAUNCH(k_fl_claim<false>, dim3(quad_grid(n)), dim3(BLOCK), shm, s, o, ix, Q, fb.fr, t->timestamp, c->rtab, dr,
            nrep ? 0u : 1u, nrep, t->d, spec ? 1u : 0u);
   auto finish = [&](uint32_t K, uint32_t applied, uint32_t already, uint64_t npath, long long new_ts) -> int {
     int rr = take_replicas(t, fb.rep);
@@ -3415,6 +3553,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   if (spec) {
     if ((r = flat_order_commit(t, o, ix, Q, maxr, st, n, true, true, simple, true, fb))) return r;
     if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, nullptr, n, NONE, st_out);
+    rr.now();  // (the order's last range read is behind: no launch after the result read)
     if ((r = sync_read(c))) return r;
     const DevResult& h = *c->hres;
     uint32_t present = 0, keys = 0, own = 0, slow = 0;  // (k_run_expand / k_fl_claim shards)
@@ -3434,18 +3573,22 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     }
     // not confirmed: the fresh tree's only reachable change is its root sentinel's `next`
     LAUNCH(k_reset_root, dim3(1), dim3(1), 0, s, t->d.s_next);
+    // the replica ranges again (reset above; k_pre's other results are idempotent, no Delete here)
+    LAUNCH(k_pre, dim3(std::min<uint32_t>(quad_grid(n), 512)), dim3(BLOCK), 0, s, o, c->crange, dr);
+    LAUNCH(k_range_base, dim3(1), dim3(BLOCK), 0, s, c->crange, const_cast<uint32_t*>(ix.base), dr);
+    rr.armed = true;
   }
   // ---- per-op statuses: duplicates, ts 0, errors ----
   LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr, nullptr,
          nullptr);
   LAUNCH(k_fl_stat_reset, dim3(1), dim3(1), 0, s, dr);
-  LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, fb.rec, t->timestamp, c->rtab, dr);
+  LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, fb.fr, t->timestamp, c->rtab, dr);
   if ((r = sync_read(c))) return r;
   if (c->hres->dup_fix) {  // a smaller duplicate took its slot: the records are final now, decide again
     LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr, nullptr,
            nullptr);
     LAUNCH(k_fl_stat_reset, dim3(1), dim3(1), 0, s, dr);
-    LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, fb.rec, t->timestamp, c->rtab, dr);
+    LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, fb.fr, t->timestamp, c->rtab, dr);
     if ((r = sync_read(c))) return r;
   }
   const DevResult h1 = *c->hres;
@@ -3557,7 +3700,8 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
     ix.first = nullptr;
     // (simple: every op an Add whose path is its anchor alone, op i's at path[i])
     if (flat)
-      return apply_flat(t, o, ix, static_cast<uint32_t>(range_total), maxr, w.st, st_out, res, o.n_path == n);
+      return apply_flat(t, o, ix, static_cast<uint32_t>(range_total), maxr, w.st, st_out, res, o.n_path == n,
+                        keep_clean);
     ix.first = ws.alloc<uint32_t>(range_total + 1);
     HIP_CHECK(hipMemsetAsync(ix.first, 0xFF, (range_total + 1) * sizeof(uint32_t), s));
     const uint32_t nrep = maxr + 1 <= HOST_RANGES ? maxr + 1 : 0u;

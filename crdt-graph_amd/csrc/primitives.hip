@@ -508,7 +508,8 @@ __global__ void __launch_bounds__(BLOCK) k_rs_hist(const uint32_t* __restrict__ 
 __global__ void __launch_bounds__(BLOCK) k_rs_scatter(const uint32_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ vals, const uint32_t* n_dev,
                                                       uint32_t shift, const uint32_t* __restrict__ off,
-                                                      uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
+                                                      uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                      uint32_t* __restrict__ inv) {
   constexpr uint32_t NW = BLOCK / 64;
   __shared__ uint32_t run[256];
   __shared__ uint32_t wc[NW][256];
@@ -559,15 +560,17 @@ __global__ void __launch_bounds__(BLOCK) k_rs_scatter(const uint32_t* __restrict
     if (valid) {
       kout[pos] = k;
       vout[pos] = v;
+      if (inv) inv[v] = pos;
     }
   }
 }
 
 // Sorts n_dev (<= n_max) pairs by the low `bits` bits of the keys, stably.
 // The result lands in (k0, v0) when the pass count is even, else in (k1, v1):
-// *out_k / *out_v point to it.
+// *out_k / *out_v point to it. inv (optional, values < n_max): inv[v] = the
+// sorted position of value v, written by the last pass.
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, const uint32_t* n_dev, uint32_t n_max,
-                     uint32_t bits, Arena& ws, hipStream_t st, uint32_t** out_k, uint32_t** out_v) {
+                     uint32_t bits, Arena& ws, hipStream_t st, uint32_t** out_k, uint32_t** out_v, uint32_t* inv) {
   const uint32_t ntiles = std::max<uint32_t>(1, (n_max + RS_TILE - 1) / RS_TILE);
   uint32_t* hist = ws.alloc<uint32_t>(256ULL * ntiles + 2);
   uint32_t* hn = hist + 256ULL * ntiles + 1;  // 256 x the tiles that hold items (device)
@@ -576,7 +579,8 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, con
     LAUNCH(k_rs_hist, dim3(ntiles), dim3(BLOCK), 0, st, ki, n_dev, shift, hist, hn);
     int r = dscan<SumOp, false>(ArrGen{hist}, hist, 256ULL * ntiles, nullptr, ws, st, nullptr, hn);
     if (r) return r;
-    LAUNCH(k_rs_scatter, dim3(ntiles), dim3(BLOCK), 0, st, ki, vi, n_dev, shift, hist, ko, vo);
+    LAUNCH(k_rs_scatter, dim3(ntiles), dim3(BLOCK), 0, st, ki, vi, n_dev, shift, hist, ko, vo,
+           shift + 8 >= bits ? inv : nullptr);
     std::swap(ki, ko);
     std::swap(vi, vo);
   }

@@ -227,6 +227,6 @@ def test_guard_g_statistics_match_oracle(monkeypatch, blocked):
             continue
         assert ok == 1
         assert (int(got[0]), int(got[1])) == (int(want[0]), int(want[1]))
-        assert int(got[2]) <= int(got[3]) == n
+        assert int(got[2]) <= int(got[3]) <= n  # (out[3]: the ops the replayed dicts reached)
         checked += 1
     assert checked >= 4
