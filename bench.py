@@ -109,7 +109,57 @@ def pmc_table(workload):
     return {}, None
 
 
-def roofline(workload, per_step, launches, B_alg, ms_step, steps_profiled):
+def pmc_live(args, counters=("FETCH_SIZE", "WRITE_SIZE")):
+    """HBM traffic per step measured on this box, now: one `rocprofv3 --pmc`
+    pass per counter (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE do not
+    fit one pass) over a child run of this bench (--pmc-child) that performs
+    exactly one step of the workload (incremental workloads: the base document
+    alone is a second child, subtracted). Counts the engine's own kernels
+    (crdtm::*) in KB per dispatch. Returns {kernel base name: [F, W] bytes per
+    step}, or None when rocprofv3 is missing or a pass fails."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    from collections import defaultdict
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    modes = ["step", "base"] if args.workload in ("incr", "incr_cfg2") else ["step"]
+    tot = {m: defaultdict(lambda: [0.0, 0.0]) for m in modes}
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    with tempfile.TemporaryDirectory() as td:
+        for m in modes:
+            for ci, ctr in enumerate(counters):
+                d = os.path.join(td, f"{m}_{ctr}")
+                cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", ctr, "-d", d, "-o", "run",
+                       "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--workload",
+                       args.workload, "--pmc-child", m]
+                if args.n_ops:
+                    cmd += ["--n-ops", str(args.n_ops)]
+                if args.docs_per_gpu:
+                    cmd += ["--docs-per-gpu", str(args.docs_per_gpu)]
+                r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env)
+                f = os.path.join(d, "run_counter_collection.csv")
+                if r.returncode != 0 or not os.path.exists(f):
+                    return None
+                for row in csv.DictReader(open(f)):
+                    k = row["Kernel_Name"]
+                    if "crdtm::" not in k:
+                        continue
+                    b = k.split("(")[0].replace("void ", "").split("<")[0].split("::")[-1]
+                    tot[m][b][ci] += float(row["Counter_Value"]) * 1024.0
+    out = dict(tot["step"])
+    if "base" in tot:
+        for b, v in tot["base"].items():
+            e = out.setdefault(b, [0.0, 0.0])
+            e[0] = max(0.0, e[0] - v[0])
+            e[1] = max(0.0, e[1] - v[1])
+        out = {b: v for b, v in out.items() if v[0] + v[1] > 0}
+    return out
+
+
+def roofline(workload, per_step, launches, B_alg, ms_step, steps_profiled, live=None):
     """SURVEY.md §8d roofline of the whole merge (one crdtm_apply / forest
     step): achieved = algorithmic bytes / merge time, against the 8 TB/s HBM
     peak; traffic = the merge's HBM bytes summed over its kernels' PMC counts
@@ -129,30 +179,52 @@ def roofline(workload, per_step, launches, B_alg, ms_step, steps_profiled):
 
     merge_s = ms_step / 1e3
     achieved = B_alg / merge_s / 1e9
-    traffic, traffic_raw, covered = 0.0, 0.0, True
-    for nm in per_step:
-        b, braw = kbytes(nm), kbytes(nm, "hbm_bytes_raw")
-        if b is None or braw is None:
-            covered = False
-            continue
-        traffic += b * launches[nm] / steps_profiled
-        traffic_raw += braw * launches[nm] / steps_profiled
+    if live:
+        # measured in this run: [raw F + W, corrected 2F + W] per step (MI355X_MICROARCH.md: FETCH_SIZE
+        # counts half the bytes of coalesced reads on gfx950; exact for streams, an upper bound for gathers)
+        def step_bytes(nm, corrected=True):
+            base = nm.split("<")[0]
+            if base.startswith("k_dscan"):
+                return None  # (labelled scan phases share k_dscan's entry: reported in the total only)
+            e = live.get(base)
+            return None if e is None else (2 * e[0] + e[1] if corrected else e[0] + e[1])
+        traffic = sum(2 * f + w for f, w in live.values())
+        traffic_raw = sum(f + w for f, w in live.values())
+        src = "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over one step of this workload (bench.py --pmc-child)"
+        covered = True
+        # the time share of the kernels whose counters the passes saw
+        seen = sum(t for nm, t in per_step.items() if nm.split("<")[0] in live or nm.startswith("k_dscan"))
+    else:
+        def step_bytes(nm, corrected=True):
+            b = kbytes(nm, "hbm_bytes" if corrected else "hbm_bytes_raw")
+            return None if b is None else b * launches[nm] / steps_profiled
+        traffic, traffic_raw, covered, seen = 0.0, 0.0, True, 0.0
+        for nm, t in per_step.items():
+            b, braw = step_bytes(nm), step_bytes(nm, False)
+            if b is None or braw is None:
+                covered = False
+                continue
+            traffic += b
+            traffic_raw += braw
+            seen += t
     kernels = []
     for nm, t in sorted(per_step.items(), key=lambda kv: -kv[1])[:8]:
-        b = kbytes(nm)
+        b = step_bytes(nm)
         per = launches[nm] / steps_profiled
         e = {"name": nm, "ms_per_step": t, "launches_per_step": per}
         if b is not None:
-            e["hbm_bytes_per_step"] = b * per
-            e["hbm_gbs"] = b * per / (t / 1e3) / 1e9
+            e["hbm_bytes_per_step"] = b
+            e["hbm_gbs"] = b / (t / 1e3) / 1e9
             e["hbm_frac"] = e["hbm_gbs"] / HBM_PEAK_GBS
         kernels.append(e)
+    tot_ms = sum(per_step.values())
+    have = bool(live) or bool(pmc)
     return {"bound": "hbm", "scope": "whole merge (every kernel of one step)", "achieved": achieved,
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": (traffic if covered and pmc else None),
-            "traffic_lower": (traffic_raw if covered and pmc else None), "traffic_source": src,
-            "traffic_over_alg": (traffic / B_alg if covered and pmc else None),
-            "alg_bytes": B_alg, "kernels_ms_per_step": sum(per_step.values()),
+            "traffic": (traffic if have else None), "traffic_lower": (traffic_raw if have else None),
+            "traffic_complete": covered, "traffic_time_share": (seen / tot_ms if tot_ms else None),
+            "traffic_source": src, "traffic_over_alg": (traffic / B_alg if have else None),
+            "alg_bytes": B_alg, "kernels_ms_per_step": tot_ms,
             "dominant_kernel": kernels[0] if kernels else None, "top_kernels": kernels}
 
 
@@ -230,6 +302,10 @@ def launch_ranks(n):
     return subprocess.call(cmd, env=env)
 
 
+def want_pmc(args, world):
+    return args.pmc == "on" or (args.pmc == "auto" and world == 1 and not args.pmc_child)
+
+
 def dry_run(args, rank, world):
     """--dry-run: the multi-rank plumbing of a real run on the CPU (gloo): the
     ranks the launcher started, the timing barrier and max over ranks, and the
@@ -298,10 +374,15 @@ def main():
     ap.add_argument("--force-replay", action="store_true",
                     help="every merge takes the one-lane sequential replay (env CRDTM_FORCE_REPLAY=1): "
                          "measures the fallback cliff on the same batch")
+    ap.add_argument("--pmc", choices=("auto", "on", "off"), default="auto",
+                    help="measure HBM traffic per step live with rocprofv3 --pmc child passes (auto: 1 GPU)")
+    ap.add_argument("--pmc-child", choices=("step", "base"), default=None, help=argparse.SUPPRESS)
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher plumbing only, no GPU: ranks (gloo), timing barrier, max over ranks and the "
                          "config-5 op-log exchange + assembly run; no merge is timed and `value` is null")
     args = ap.parse_args()
+    if args.pmc_child:  # (a profiled child: one GPU, no launcher, no PMC of its own)
+        args.gpus, args.pmc, args.exchange = 1, "off", "off"
     if args.force_replay:
         os.environ["CRDTM_FORCE_REPLAY"] = "1"  # (read by every merge)
 
@@ -330,7 +411,7 @@ def main():
     L = N.lib()
     if args.workload in ("trees", "incr", "incr_cfg2"):
         line = (run_trees if args.workload == "trees" else run_incr)(args, rank, world, local_rank)
-        if rank == 0:
+        if rank == 0 and line is not None:
             print(json.dumps(line), flush=True)
         if world > 1:
             dist.destroy_process_group()
@@ -360,6 +441,13 @@ def main():
         N.check(L.crdtm_apply(tree, C.byref(ops), 1, 1, None, C.byref(res)), "apply")
         if res.code != 0:
             raise RuntimeError(f"merge failed: code {res.code} at op {res.err_index}")
+
+    if args.pmc_child:  # exactly one step under rocprofv3 --pmc (pmc_live)
+        step()
+        torch.cuda.synchronize()
+        L.crdtm_tree_destroy(tree)
+        L.crdtm_ctx_destroy(ctx)
+        return
 
     for _ in range(args.warmup):
         step()
@@ -446,7 +534,8 @@ def main():
                    "path": {1: "closed-form", 2: "replay", 3: "per-dict replay"}.get(path_taken, "?"),
                    "guard": guard, "serial_replay": serial, "guard_g": guard_g,
                    "parallelism": f"documents sharded by id over {world} GPU(s)"},
-        "roofline": roofline(args.workload, per_step, launches, B_alg, ms_step, ps),
+        "roofline": roofline(args.workload, per_step, launches, B_alg, ms_step, ps,
+                             live=pmc_live(args) if (rank == 0 and want_pmc(args, world)) else None),
     }
     if rank == 0:
         sc = stream_copy_gbs(dev)
@@ -540,6 +629,14 @@ def run_incr(args, rank, world, local_rank):
             acct["incremental"] += bool(res.flags & N.FLAG_INCREMENTAL)
             acct["paths"][res.path_taken] = acct["paths"].get(res.path_taken, 0) + 1
 
+    if args.pmc_child:  # the base document alone, or the base and one step (pmc_live subtracts)
+        rebuild()
+        if args.pmc_child == "step":
+            step()
+        torch.cuda.synchronize()
+        L.crdtm_tree_destroy(tree)
+        L.crdtm_ctx_destroy(ctx)
+        return None
     for _ in range(args.warmup):
         rebuild()
         step()
@@ -568,7 +665,12 @@ def run_incr(args, rank, world, local_rank):
         per_k[nm] = per_k.get(nm, 0.0) + ms[j]
         launches[nm] = launches.get(nm, 0) + 1
     ms_step = elapsed / args.steps * 1e3
-    B_alg = 57 * bsz  # flat Add = 57 B; one batch (nested: the flat figure, a lower bound)
+    # SURVEY.md 8d algorithmic bytes of the step's nb batches (Add 49 + 8L, Delete 9 + 8L)
+    a0 = base
+    B_alg = alg_bytes({"kind": s["kind"][a0:], "path_off": s["path_off"][a0:]})
+    # the kernels of the profiled batch (the step's last), times the batches of a step
+    per_k = {k: v * nb for k, v in per_k.items()}
+    launches = {k: v * nb for k, v in launches.items()}
     line = {
         "metric": "merged ops/sec (whole node) on 10M-op batch",
         "value": world * bsz * nb * args.steps / elapsed, "unit": "ops/s", "n_gpus": world, "steps": args.steps,
@@ -585,13 +687,11 @@ def run_incr(args, rank, world, local_rank):
                              for p_, c_ in acct["paths"].items()},
                    "ms_per_batch": ms_step / nb,
                    "parallelism": f"one document per GPU ({world} GPU(s)), replicas only"},
-        "roofline": roofline("incr", per_k, launches, B_alg, ms_step / nb, 1),
+        "roofline": roofline("incr", per_k, launches, B_alg, ms_step, 1,
+                             live=pmc_live(args) if (rank == 0 and want_pmc(args, world)) else None),
     }
-    line["roofline"]["note"] = ("achieved = the batch's own algorithmic bytes / time per batch; a batch is ~20 "
-                                "latency-bound launches of small kernels" if not nested else
-                                "achieved = the flat per-Add bytes x batch / time per batch; these batches "
-                                "re-merge log ++ batch on the fresh-tree paths (no in-place path for nested "
-                                "or tombstoned trees yet)")
+    line["roofline"]["note"] = ("per step (all its batches): achieved = the batches' algorithmic bytes / step "
+                                "time; kernel times are the profiled last batch x batches per step")
     if rank == 0 and world == 1:
         m = args.cpu_sample if args.cpu_sample >= 0 else CPU_SAMPLE["cfg2" if nested else "flat10m"]
         if m > 0:
@@ -650,6 +750,11 @@ def run_trees(args, rank, world, local_rank, cpu=True):
         state["ops_t"] = ops_t
         state["n"] = n
 
+    if args.pmc_child:  # exactly one step under rocprofv3 --pmc (pmc_live)
+        step()
+        torch.cuda.synchronize()
+        L.crdtm_ctx_destroy(ctx)
+        return None
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -709,7 +814,8 @@ def run_trees(args, rank, world, local_rank, cpu=True):
         "config": {"workload": f"trees: {n_mine} documents x {per} ops per GPU ({n} ops), {n_docs} documents total",
                    "replicas": TREES["replicas"], "documents_ok": ok_docs,
                    "parallelism": f"documents sharded by id over {world} GPU(s); op logs all-gathered (RCCL)"},
-        "roofline": roofline("trees", per_k, launches, B_alg, ms_step, 1),
+        "roofline": roofline("trees", per_k, launches, B_alg, ms_step, 1,
+                             live=pmc_live(args) if (cpu and rank == 0 and want_pmc(args, world)) else None),
         "all_gather_ms": ag_ms,
     }
     if args.verbose and rank == 0:

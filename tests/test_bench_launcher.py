@@ -19,15 +19,19 @@ def _env():
     return env
 
 
-def test_self_launch_world2_dry_run():
-    p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "1"],
+import pytest
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_self_launch_dry_run(world):
+    p = subprocess.run([sys.executable, BENCH, "--gpus", str(world), "--dry-run", "--steps", "2", "--warmup", "1"],
                        capture_output=True, text=True, timeout=300, env=_env())
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout  # rank 0 prints one line
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 2 and line["dry_run"] is True and line["value"] is None
-    assert line["exchange"]["assembled_ok"] is True and line["exchange"]["documents"] == 16
+    assert line["n_gpus"] == world and line["dry_run"] is True and line["value"] is None
+    assert line["exchange"]["assembled_ok"] is True and line["exchange"]["documents"] == 8 * world
 
 
 def test_rank_count_mismatch_fails():

@@ -9,7 +9,7 @@ rc=$?
 tail -4 gpurun_out/${T}_tests.log
 [ $rc = 0 ] || exit $rc
 for w in "$@"; do
-  timeout -k 10 300 python -u bench.py --workload $w --cpu-sample 0 --verbose > gpurun_out/${T}_$w.log 2>&1 \
+  timeout -k 10 300 python -u bench.py --workload $w --cpu-sample 0 --pmc off --verbose > gpurun_out/${T}_$w.log 2>&1 \
     || { echo BENCH_FAIL $w; tail -20 gpurun_out/${T}_$w.log; exit 1; }
   echo "$w $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/${T}_$w.log | head -1)"
 done
