@@ -246,6 +246,19 @@ __device__ __forceinline__ uint32_t block_min(uint32_t v) {
   return r;
 }
 
+// the same for a workgroup of NT threads
+template <uint32_t NT, class F>
+__device__ __forceinline__ uint32_t block_reduce_t(uint32_t v, uint32_t id, F op) {
+  __shared__ uint32_t s[NT / 64];
+  for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t r = id;
+  for (uint32_t w = 0; w < NT / 64; ++w) r = op(r, s[w]);
+  __syncthreads();
+  return r;
+}
+
 #define GRID_STRIDE(i, n) \
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += gridDim.x * blockDim.x)
 

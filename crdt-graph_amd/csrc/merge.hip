@@ -129,7 +129,11 @@ inline uint32_t quad_grid(uint64_t n) {
 // Replica ids below REP_DIRECT fold into a direct-mapped LDS table with
 // no-return LDS atomics; larger ids go straight to the global table.
 constexpr uint32_t REP_DIRECT = 4096;
-__global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint2* rng, DevResult* dres) {
+// (PB = 1024 threads: 512 workgroups keep the range flush short, and the
+// larger workgroups give every CU 32 waves to cover the memory latency)
+constexpr uint32_t PRE_T = 1024;
+template <uint32_t PB>
+__global__ void __launch_bounds__(PB) __attribute__((amdgpu_waves_per_eu(PB == 1024 ? 8 : 4, 8))) k_pre(OpsDev o, uint2* rng, DevResult* dres) {
   __shared__ __attribute__((aligned(16))) uint32_t rlo[REP_DIRECT];
   __shared__ __attribute__((aligned(16))) uint32_t rhi[REP_DIRECT];
   for (uint32_t j = threadIdx.x; j < REP_DIRECT / 4; j += blockDim.x) {
@@ -187,17 +191,18 @@ __global__ void __launch_bounds__(BLOCK) k_pre(OpsDev o, uint2* rng, DevResult* 
       fold(qa);
     }
   }
-  maxr = block_max(maxr);  // (synchronises the block) only ids <= maxr were touched
+  auto mxf = [](uint32_t a, uint32_t b) { return a > b ? a : b; };
+  maxr = block_reduce_t<PB>(maxr, 0u, mxf);  // (synchronises the block) only ids <= maxr were touched
   for (uint32_t j = threadIdx.x; j <= maxr && j < REP_DIRECT; j += blockDim.x) {
     if (rlo[j] != NONE) {
       atomicMin(&rng[j].x, rlo[j]);
       atomicMax(&rng[j].y, rhi[j]);
     }
   }
-  mx = block_max(mx);
-  bad = block_max(bad);
-  neg = block_max(neg);
-  ndel = block_sum(ndel);
+  mx = block_reduce_t<PB>(mx, 0u, mxf);
+  bad = block_reduce_t<PB>(bad, 0u, mxf);
+  neg = block_reduce_t<PB>(neg, 0u, mxf);
+  ndel = block_reduce_t<PB>(ndel, 0u, [](uint32_t a, uint32_t b) { return a + b; });
   if (threadIdx.x == 0) {
     if (mx) atomicMax(&dres->max_len, mx);
     if (bad) atomicOr(&dres->bad_range, 1u);
@@ -288,6 +293,16 @@ __global__ void __launch_bounds__(BLOCK) k_range_base(const uint2* rng, uint32_t
 __global__ void __launch_bounds__(BLOCK) k_range_reset(uint2* rng, const DevResult* dres) {
   const uint32_t nr = dres->max_replica + 1;
   GRID_STRIDE(r, nr) rng[r] = make_uint2(NONE, 0u);
+}
+
+static void launch_pre(crdtm_ctx* c, const OpsDev& o, hipStream_t s) {
+  static const bool ab_small = getenv("CRDTM_AB") && !strcmp(getenv("CRDTM_AB"), "pre256");
+  if (ab_small) {
+    LAUNCH(k_pre<BLOCK>, dim3(std::min<uint32_t>(quad_grid(o.n), 512)), dim3(BLOCK), 0, s, o, c->crange, c->dres);
+    return;
+  }
+  const uint32_t g = static_cast<uint32_t>(std::min<uint64_t>((o.n / 4 + PRE_T - 1) / PRE_T + 1, 512));
+  LAUNCH(k_pre<PRE_T>, dim3(g), dim3(PRE_T), 0, s, o, c->crange, c->dres);
 }
 
 __global__ void k_dres_init(DevResult* d) {
@@ -2370,6 +2385,7 @@ __device__ __forceinline__ long long fl_key(uint32_t q, const uint32_t* sb, cons
 //    atomic per wave and replica).
 // The trip count is wave-uniform, so every lane takes part in the ballots.
 constexpr uint32_t RM_UNROLL = 4;
+template <uint32_t U>
 __global__ void __launch_bounds__(BLOCK) k_run_mask(FlatRec fr, uint32_t Q, unsigned long long* hm, uint32_t* hc,
                                                    TreeDev T, const uint32_t* qc, const uint32_t* logidx, OpsDev o,
                                                    TsIndex x, uint32_t nrep, DevResult* chk, uint32_t* rtab) {
@@ -2390,19 +2406,19 @@ __global__ void __launch_bounds__(BLOCK) k_run_mask(FlatRec fr, uint32_t Q, unsi
   const uint32_t nw = (Q + 63) >> 6;
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwave = (gridDim.x * blockDim.x) >> 6;
   uint32_t present = 0, err = NONE;
-  for (uint32_t w0 = wave * RM_UNROLL; w0 < nw; w0 += nwave * RM_UNROLL) {
-    uint2 rq[RM_UNROLL], rp[RM_UNROLL];
+  for (uint32_t w0 = wave * U; w0 < nw; w0 += nwave * U) {
+    uint2 rq[U], rp[U];
 #pragma unroll
-    for (uint32_t u = 0; u < RM_UNROLL; ++u) {  // every load in flight first
+    for (uint32_t u = 0; u < U; ++u) {  // every load in flight first
       const uint32_t q = ((w0 + u) << 6) + lane;
       rq[u] = q < Q ? fr.rec[q] : make_uint2(FR_EMPTY, 0u);
       rp[u] = (lane == 0 && q > 0 && q - 1 < Q) ? fr.rec[q - 1] : make_uint2(FR_EMPTY, 0u);
     }
     // the anchors' records of run heads (the check) load before this
     // iteration's stores: gfx9 waits on loads and stores in issue order
-    uint2 ra[RM_UNROLL];
+    uint2 ra[U];
 #pragma unroll
-    for (uint32_t u = 0; u < RM_UNROLL; ++u) {
+    for (uint32_t u = 0; u < U; ++u) {
       const uint32_t q = ((w0 + u) << 6) + lane;
       const uint32_t px = __shfl_up(rq[u].x, 1, 64), py = __shfl_up(rq[u].y, 1, 64);
       if (lane != 0) rp[u] = make_uint2(px, py);
@@ -2411,7 +2427,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_mask(FlatRec fr, uint32_t Q, unsi
       if (chk && q < Q && fr.present(rq[u].x) && qa != Q && qa != NONE && qa + 1 != q) ra[u] = fr.rec[qa];
     }
 #pragma unroll
-    for (uint32_t u = 0; u < RM_UNROLL; ++u) {
+    for (uint32_t u = 0; u < U; ++u) {
       const uint32_t q = ((w0 + u) << 6) + lane;
       const bool pres = q < Q && fr.present(rq[u].x);
       const uint32_t qa = fr.anchor(rq[u].x);
@@ -3388,10 +3404,12 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
       LAUNCH(k_fl_present, dim3(gq), dim3(BLOCK), 0, s, Q, fr, qc);
       if ((r = scan_excl_u32(qc, qc, Q, nullptr, ws, s))) return r;
     }
-    const uint32_t gw = std::max<uint32_t>(1, std::min<uint32_t>(2048, (NW + RM_UNROLL * (BLOCK / 64) - 1) /
-                                                                           (RM_UNROLL * (BLOCK / 64))));
-    LAUNCH(k_run_mask, dim3(gw), dim3(BLOCK), maxr + 1 <= HOST_RANGES ? 3 * (maxr + 1) * sizeof(uint32_t) : 0, s,
-           fr, Q, hm, hc, t->d, qc, logidx, o, ix, maxr + 1, check ? dr : nullptr, c->rtab);
+    const uint32_t gw = std::max<uint32_t>(1, std::min<uint32_t>(2048, (NW + RM_MASK_UNROLL * (BLOCK / 64) - 1) /
+                                                                           (RM_MASK_UNROLL * (BLOCK / 64))));
+    // (two words per wave and iteration: 48 VGPRs, full occupancy; four: 68, 110 -> 120 us at flat10m)
+    LAUNCH(k_run_mask<RM_MASK_UNROLL>, dim3(gw), dim3(BLOCK),
+           maxr + 1 <= HOST_RANGES ? 3 * (maxr + 1) * sizeof(uint32_t) : 0, s, fr, Q, hm, hc, t->d, qc, logidx, o, ix,
+           maxr + 1, check ? dr : nullptr, c->rtab);
     if ((r = dscan<SumOp, false>(ArrGen{hc}, hb, NW, &dr->run_count, ws, s, nullptr, nullptr, "k_dscan_runs")))
       return r;
     LAUNCH(k_run_heads, dim3(grid_for(64ULL * NW, BLOCK, 4096)), dim3(BLOCK), 0, s, fr, Q, fb.rm, ra.hh);
@@ -3574,7 +3592,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     // not confirmed: the fresh tree's only reachable change is its root sentinel's `next`
     LAUNCH(k_reset_root, dim3(1), dim3(1), 0, s, t->d.s_next);
     // the replica ranges again (reset above; k_pre's other results are idempotent, no Delete here)
-    LAUNCH(k_pre, dim3(std::min<uint32_t>(quad_grid(n), 512)), dim3(BLOCK), 0, s, o, c->crange, dr);
+    launch_pre(c, o, s);
     LAUNCH(k_range_base, dim3(1), dim3(BLOCK), 0, s, c->crange, const_cast<uint32_t*>(ix.base), dr);
     rr.armed = true;
   }
@@ -3647,7 +3665,7 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   // (512 workgroups: each flushes its replica ranges and counters with
   // device-scope atomics that serialise per word, ~12 ns each)
   // (measured: 512 beats 1024 and 2048 workgroups on flat10m and deep10m)
-  LAUNCH(k_pre, dim3(std::min<uint32_t>(quad_grid(n), 512)), dim3(BLOCK), 0, s, o, c->crange, dr);
+  launch_pre(c, o, s);
   LAUNCH(k_range_base, dim3(1), dim3(BLOCK), 0, s, c->crange, rbase, dr);
   RangeReset keep_clean{c};  // resets the context's replica ranges on every exit
   int r;
