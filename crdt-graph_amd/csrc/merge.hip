@@ -2384,7 +2384,8 @@ __device__ __forceinline__ long long fl_key(uint32_t q, const uint32_t* sb, cons
 //    is folded (a wave's slots usually lie in one replica's range: one LDS
 //    atomic per wave and replica).
 // The trip count is wave-uniform, so every lane takes part in the ballots.
-constexpr uint32_t RM_UNROLL = 4;
+constexpr uint32_t RM_UNROLL = 4;       // k_run_heads: words per wave and iteration
+constexpr uint32_t RM_MASK_UNROLL = 2;  // k_run_mask (48 VGPRs, full occupancy; 4 words: 68, 120 -> 110 us at flat10m)
 template <uint32_t U>
 __global__ void __launch_bounds__(BLOCK) k_run_mask(FlatRec fr, uint32_t Q, unsigned long long* hm, uint32_t* hc,
                                                    TreeDev T, const uint32_t* qc, const uint32_t* logidx, OpsDev o,
@@ -3406,7 +3407,6 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     }
     const uint32_t gw = std::max<uint32_t>(1, std::min<uint32_t>(2048, (NW + RM_MASK_UNROLL * (BLOCK / 64) - 1) /
                                                                            (RM_MASK_UNROLL * (BLOCK / 64))));
-    // (two words per wave and iteration: 48 VGPRs, full occupancy; four: 68, 110 -> 120 us at flat10m)
     LAUNCH(k_run_mask<RM_MASK_UNROLL>, dim3(gw), dim3(BLOCK),
            maxr + 1 <= HOST_RANGES ? 3 * (maxr + 1) * sizeof(uint32_t) : 0, s, fr, Q, hm, hc, t->d, qc, logidx, o, ix,
            maxr + 1, check ? dr : nullptr, c->rtab);
