@@ -296,11 +296,6 @@ __global__ void __launch_bounds__(BLOCK) k_range_reset(uint2* rng, const DevResu
 }
 
 static void launch_pre(crdtm_ctx* c, const OpsDev& o, hipStream_t s) {
-  static const bool ab_small = getenv("CRDTM_AB") && !strcmp(getenv("CRDTM_AB"), "pre256");
-  if (ab_small) {
-    LAUNCH(k_pre<BLOCK>, dim3(std::min<uint32_t>(quad_grid(o.n), 512)), dim3(BLOCK), 0, s, o, c->crange, c->dres);
-    return;
-  }
   const uint32_t g = static_cast<uint32_t>(std::min<uint64_t>((o.n / 4 + PRE_T - 1) / PRE_T + 1, 512));
   LAUNCH(k_pre<PRE_T>, dim3(g), dim3(PRE_T), 0, s, o, c->crange, c->dres);
 }
@@ -2724,10 +2719,10 @@ __device__ __forceinline__ uint2 hh_load(const uint2* p) {
   return make_uint2(static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32));
 }
 __global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, RunMask rm, FlatRec fr, uint32_t* skey,
-                                                  uint32_t* sval, uint32_t ab) {
+                                                  uint32_t* sval) {
   const uint32_t R = *a.nR;
   RUN_LOOP(k) {
-    const uint32_t r = (ab & 1) ? k : R - 1 - k;
+    const uint32_t r = R - 1 - k;
     const uint2 me = a.hh[r];
     const uint32_t x = me.x;
     uint32_t d = me.y;
@@ -2755,8 +2750,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, RunMask 
         d = hj.y;
       }
       if (d >= Q || !fr.present(fr.rec[d].x)) d = Q;
-      if (ab & 2) a.hh[r].y = d;
-      else __hip_atomic_store(&a.hh[r].y, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.hh[r].y, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (d != Q && (d >= x || !fr.present(fr.rec[d].x))) {  // (self-anchored / nodeless anchor: a failing batch)
       d = Q;
       __hip_atomic_store(&a.hh[r].y, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3307,9 +3301,7 @@ static int flat_rec(crdtm_ctx* c, uint32_t Q, FlatRec& fr) {
     c->fl_epoch = FR_EPOCHS;  // (forces the zeroing below)
   }
   fr.rec = c->fl_rec;
-  static const bool ab_arena = getenv("CRDTM_AB") && !strcmp(getenv("CRDTM_AB"), "arena");
-  if (ab_arena) fr.rec = c->ws.alloc<uint2>(Q + 1);
-  const bool narrow = !ab_arena && static_cast<uint64_t>(Q) + 2 < (1ULL << FR_ABITS) - 1;
+  const bool narrow = static_cast<uint64_t>(Q) + 2 < (1ULL << FR_ABITS) - 1;
   if (narrow) {
     if (++c->fl_epoch > FR_EPOCHS) {
       HIP_CHECK(hipMemsetAsync(c->fl_rec, 0, c->fl_cap * sizeof(uint2), s));  // (epoch 0 is never current)
@@ -3427,9 +3419,7 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     uint32_t* xs = ws.alloc<uint32_t>(Q + 1);
     uint32_t* groot = fb.cnt;  // one word: the root sentinel's first child in the sorted list
     const uint32_t gr = grid_for(Q, BLOCK, 2048);
-    const char* abv = getenv("CRDTM_AB");
-    const uint32_t ab_ep = abv ? ((!strcmp(abv, "asc") ? 1u : 0u) | (!strcmp(abv, "plainst") ? 2u : 0u)) : 0u;
-    LAUNCH(k_run_ep, dim3(gr), dim3(BLOCK), 0, s, ra, Q, fb.rm, fr, sk[0], sv[0], ab_ep);
+    LAUNCH(k_run_ep, dim3(gr), dim3(BLOCK), 0, s, ra, Q, fb.rm, fr, sk[0], sv[0]);
     uint32_t sbits = 8;
     while (sbits < 32 && ((static_cast<uint64_t>(Q) + 1) >> sbits) != 0) sbits += 8;
     uint32_t *pk = nullptr, *sarr = nullptr;  // attach slot, run: siblings grouped by slot, slots ascending
