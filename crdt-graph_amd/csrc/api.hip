@@ -311,6 +311,7 @@ int crdtm_tree_reset(crdtm_tree* t, int64_t replica_id) {
   t->last_is_batch = 1;
   t->flat_clean = true;
   t->kidx_valid = false;
+  t->ilr_valid = false;
   ++t->version;
   return CRDTM_OK;
 }

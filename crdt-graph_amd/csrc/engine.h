@@ -168,6 +168,21 @@ struct KeyIndex {
   bool ord_ready = false;  // the blocks describe the tree's document
   ~KeyIndex();
 };
+// Index of a tree state for the incremental per-dict replay (ilr.hip), owned
+// by one tree handle: (dict, key) -> slot hash and per-dict member lists of
+// the state, kept current by the replay's own commits (any other commit
+// drops it), plus per-slot event times of the batch in flight.
+struct IlrIndex {
+  SlotHash H{};
+  uint32_t hcap = 0;           // hash entries (power of two)
+  uint64_t hused = 0;          // entries in use
+  uint32_t* dhead = nullptr;   // [dcap] first member slot of each dict
+  uint32_t* mnext = nullptr;   // [scap] next member of the slot's dict
+  uint32_t* ev = nullptr;      // [3 * scap] per slot: created / deleted / refilled at op (NONE)
+  uint32_t* xmap = nullptr;    // [scap] source slot -> its copy, during one deep copy
+  uint64_t dcap = 0, scap = 0;
+  ~IlrIndex();
+};
 }  // namespace crdtm
 
 struct crdtm_tree {
@@ -198,6 +213,9 @@ struct crdtm_tree {
   bool flat_clean = true;
   std::unique_ptr<crdtm::KeyIndex> kidx;
   bool kidx_valid = false;
+  // incremental per-dict replay index (ilr.hip), valid while ilr_valid
+  std::unique_ptr<crdtm::IlrIndex> ilr;
+  bool ilr_valid = false;
   std::shared_ptr<void> trav;        // traversal cache (api.hip), valid for `version`
   std::shared_ptr<void> dtrav;       // device traversal index (api.hip), valid for `version`
 };
@@ -266,6 +284,40 @@ int replica_fold(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* re
 int take_replicas(crdtm_tree* t, const long long* rep_dev);
 // incr.hip: adds-only flat batch into a clean flat tree; *handled = false leaves it to apply_batch
 int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res, bool* handled);
+// ilr.hip: a batch into a tree that holds state, replayed per children dict on the
+// state itself; *handled = false leaves it to the re-merge (nothing written)
+int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res, bool* handled);
+bool ilr_wanted(const crdtm_tree* t, uint32_t n);
+// merge.hip helpers shared with ilr.hip
+void launch_pre(crdtm_ctx* c, const OpsDev& o, hipStream_t s);
+// Resets the context's replica range table entries 0..nr-1 (nr = 0: the
+// ones k_pre touched, read from the DevResult — valid only until the next
+// DevResult reset, so callers pass nr once they have read max_replica).
+void range_reset(crdtm_ctx* c, uint32_t nr);
+// Launches range_reset when a merge leaves by any path. (`armed` is cleared
+// when the merge reset the table itself, stream-ordered before its final
+// result read, and set again if it had to rebuild it)
+struct RangeReset {
+  crdtm_ctx* c;
+  bool armed = true;
+  uint32_t nr = 0;
+  void now() {
+    range_reset(c, nr);
+    armed = false;
+  }
+  ~RangeReset() {
+    if (armed) now();
+  }
+};
+__global__ void k_dres_init(DevResult* d);
+__global__ void k_path_range(OpsDev o, DevResult* dres);
+__global__ void k_post_flags(OpsDev o, const uint8_t* st, uint32_t* appl, uint32_t* plen);
+__global__ void k_log(OpsDev o, const uint8_t* st, TreeDev T, uint32_t log_base, uint32_t lpath_base,
+                      const uint32_t* appl, const uint32_t* plen);
+__global__ void k_log_tail(TreeDev T, uint32_t log_base, const uint32_t* n_app, uint32_t lpath_base,
+                           const uint32_t* np);
+__global__ void k_status_out(const uint8_t* st, uint32_t n, uint32_t err, uint8_t* out);
+__global__ void k_replay_index(TreeDev T, uint32_t n_slots, SlotHash H, uint32_t* dhead, uint32_t* mnext);
 __global__ void k_reset_root(uint32_t* s_next);
 // each group's first position in sorted keys (NONE: no group) (merge.hip)
 __global__ void k_doc_gstart(const uint32_t* sk, uint32_t m, uint32_t* gs);

@@ -1,0 +1,930 @@
+// ilr.hip — incremental merge into a tree that already holds state, replayed
+// per children dict on the state itself ("ILR": incremental level replay).
+//
+// `apply batch state` (src/CRDTree.elm:265-269) applies the batch's ops in
+// order with the literal addAfterHelp / findInsertion / deleteHelp semantics
+// (src/Internal/Node.elm:56-163). Ops that land in different children dicts
+// interact only through path resolution (update, :138-163): an op's path
+// crosses the nodes of shallower dicts. So the batch is grouped by the dict
+// it lands in — ops with path length L and the same owner key path[L-2] (the
+// root dict for L = 1) — and replayed level by level (L = 1, 2, ...), one
+// lane per group and the group's ops in batch order, on the tree state's own
+// slots. When level L runs, every shallower dict holds its whole batch, so an
+// op i resolves its path "as of op i" through per-slot event times recorded
+// by the shallower levels: a node created by op j exists for i only if j < i,
+// one deleted by op j is a Tombstone for i only if j < i (its children stay
+// in place until the commit, for the ops before the Delete), one the copy
+// quirk re-filled at op j is live (with the copied children) only if j < i.
+// Inside a group's dict only that group writes, so the dict is exactly at
+// op i when op i runs.
+//
+// What this order cannot decide sends the batch to the re-merge (merge.hip
+// apply_batch_paths; nothing is written): a path slot with two events (a
+// Delete and a re-fill), a group whose ops resolve to different dicts, and a
+// copy quirk whose copied node has batch activity below it (its deep copy
+// must be the children as of the quirk). Any error (the first failing op in
+// batch order is exact: each op only sees earlier ops) rolls the state back
+// through per-group undo logs. Each group takes its Adds' slots from a range
+// reserved for it (a prefix sum over the groups; an Add that does not apply
+// leaves a dead slot in a dict nothing reaches); materialised sentinels,
+// deep copies and dicts come from device counters. The slots' sources are op
+// indices (tagged) until the commit turns them into log indices. Per batch:
+// O(batch) work — grouping, the levels, and a commit that visits only the
+// new slots and the undo entries; the (dict, key) -> slot hash, the dict
+// member lists and the event times persist with the tree handle.
+//
+// Visibility: the groups of one level run as concurrent workgroups spread
+// over the XCDs, whose L2s are not coherent with each other inside a kernel.
+// So nothing one lane writes is read by another lane of the same launch: a
+// lane writes only the slots of its own dict (and of dicts it creates), and
+// the slots it creates go to a table of its own (per group, in the arena),
+// published into the shared (dict, key) hash by a separate kernel after the
+// level. During a level the shared hash is read-only.
+#include <cstdio>
+#include <cstring>
+
+#include "engine.h"
+#include "scan.h"
+
+namespace crdtm {
+
+IlrIndex::~IlrIndex() {
+  if (H.dict) hipFree(H.dict);
+  if (H.key) hipFree(H.key);
+  if (H.slot) hipFree(H.slot);
+  if (dhead) hipFree(dhead);
+  if (mnext) hipFree(mnext);
+  if (ev) hipFree(ev);
+  if (xmap) hipFree(xmap);
+}
+
+constexpr uint32_t ILR_TAG = 0x80000000u;  // s_src of this batch: ILR_TAG | op index
+constexpr uint32_t ILR_MAXL = 64;          // deeper paths: the re-merge
+constexpr uint32_t EV_CRE = 0, EV_DEL = 1, EV_CPY = 2;
+constexpr uint32_t IMPLICIT = 0xFFFFFFFEu;  // a live node's children still the implicit {0: Tombstone}
+constexpr uint32_t LV_PTOT = ILR_MAXL + 1, LV_QTOT = ILR_MAXL + 2, LV_N = ILR_MAXL + 4;
+// conflict reasons (DevResult::ilr_why) and overflow reasons (ilr_overflow)
+enum : uint32_t { IW_TWO_EVENTS = 1, IW_TWO_DICTS = 2, IW_COPY_BELOW = 4, IW_REFILL = 8, IW_SHAPE = 16, IW_DEPTH = 32 };
+enum : uint32_t { IO_SLOTS = 1, IO_DICTS = 2, IO_UNDO = 4, IO_PRIV = 8 };
+enum : uint32_t { IF_NEXT = 0, IF_SRC = 1, IF_CHILD = 2, IF_FLAGS = 3 };
+
+// per group of m ops with `adds` Adds: private table entries (at most half
+// used: its nodes and a materialised sentinel), undo triples and their offset
+__host__ __device__ inline uint32_t ilr_pcap(uint32_t adds) {
+  uint32_t p = 16;
+  while (p < 2 * (adds + 1)) p <<= 1;
+  return p;
+}
+__host__ __device__ inline uint32_t ilr_ucap(uint32_t m) { return 3 * m + 8; }
+__host__ __device__ inline uint64_t ilr_uoff(uint32_t gbeg, uint32_t g) { return 3ULL * gbeg + 8ULL * g; }
+
+struct IlrArgs {
+  TreeDev T;
+  SlotHash H;
+  uint32_t* dhead;
+  uint32_t* mnext;
+  uint32_t* ev;  // [3 * scap]
+  uint32_t* xmap;
+  uint32_t scap;
+  uint32_t committed;  // slots of the state before the batch
+  uint32_t cap_slots, cap_dicts;
+  uint32_t hash_limit;  // entries the shared hash may hold
+  // (depth, key) of every node some op's path crosses (deep-copy conflict check)
+  const unsigned long long* tk;
+  uint32_t tk_mask;
+  long long ts0;
+  DevResult* dr;
+  // per group: its private table (dict, key) -> slot over pk/pd/ps[poff[g], + pcap[g])
+  long long* pk;
+  uint32_t* pd;
+  uint32_t* ps;
+  const uint32_t* poff;
+  const uint32_t* pcap;
+  // per group: its reserved Add slots [committed + qoff[g], + qn[g])
+  const uint32_t* qoff;
+  const uint32_t* qn;
+  // per group: undo triples (slot, field, old) at ilr_uoff, ucnt[g] used
+  uint32_t* undo;
+  uint32_t* ucnt;
+  uint32_t grave;  // the dead dict of this batch's unused reserved slots
+};
+
+__device__ __forceinline__ unsigned long long ilr_tk_key(uint32_t depth, long long key) {
+  return ((static_cast<unsigned long long>(depth) << 54) | (static_cast<unsigned long long>(key + TWO53))) + 1ULL;
+}
+__device__ __forceinline__ uint32_t ilr_hash64(unsigned long long k, uint32_t mask) {
+  return static_cast<uint32_t>(mix64(k)) & mask;
+}
+__device__ void ilr_set_insert(unsigned long long* t, uint32_t mask, unsigned long long k) {
+  uint32_t p = ilr_hash64(k, mask);
+  for (;;) {
+    const unsigned long long prev = atomicCAS(&t[p], 0ULL, k);
+    if (prev == 0ULL || prev == k) return;
+    p = (p + 1) & mask;
+  }
+}
+__device__ bool ilr_set_has(const unsigned long long* t, uint32_t mask, unsigned long long k) {
+  uint32_t p = ilr_hash64(k, mask);
+  for (;;) {
+    const unsigned long long v = t[p];
+    if (v == k) return true;
+    if (v == 0ULL) return false;
+    p = (p + 1) & mask;
+  }
+}
+
+// One group's lane: the Replayer's literal semantics (merge.hip) on the
+// shared state, with event times, reserved slots, a private table and an
+// undo log of its own.
+struct IlrLane {
+  IlrArgs a;
+  bool bad;  // overflow or conflict: the batch goes to the re-merge
+  long long* pk;
+  uint32_t* pd;
+  uint32_t* ps;
+  uint32_t pmask, pused;
+  uint32_t qnext, qend;
+  uint32_t* un;
+  uint32_t ucap, ucnt;
+
+  __device__ uint32_t& ev(uint32_t s, uint32_t k) { return a.ev[3ULL * s + k]; }
+  __device__ void conflict(uint32_t why) {
+    atomicOr(&a.dr->ilr_why, why);
+    atomicOr(&a.dr->ilr_conflict, 1u);
+    bad = true;
+  }
+  __device__ void overflow(uint32_t why) {
+    atomicOr(&a.dr->ilr_overflow, why);
+    bad = true;
+  }
+  // (dict, key) -> slot: the slots this group created in this level, then
+  // the shared hash (complete for everything before this level)
+  __device__ uint32_t find(uint32_t d, long long k) const {
+    for (uint32_t p = slothash_pos(d, k, pmask);; p = (p + 1) & pmask) {
+      const uint32_t v = ps[p];
+      if (v == NONE) break;
+      if (pd[p] == d && pk[p] == k) return v;
+    }
+    return slothash_find(a.H, d, k);
+  }
+  __device__ void log_undo(uint32_t s, uint32_t field, uint32_t old) {
+    if (s >= a.committed) return;
+    if (ucnt >= ucap) {
+      overflow(IO_UNDO);
+      return;
+    }
+    un[3 * ucnt] = s;
+    un[3 * ucnt + 1] = field;
+    un[3 * ucnt + 2] = old;
+    ++ucnt;
+  }
+  __device__ void set_next(uint32_t s, uint32_t v) { log_undo(s, IF_NEXT, a.T.s_next[s]); a.T.s_next[s] = v; }
+  __device__ void set_src(uint32_t s, uint32_t v) { log_undo(s, IF_SRC, a.T.s_src[s]); a.T.s_src[s] = v; }
+  __device__ void set_child(uint32_t s, uint32_t v) { log_undo(s, IF_CHILD, a.T.s_child[s]); a.T.s_child[s] = v; }
+  __device__ void set_flags(uint32_t s, uint32_t v) {
+    log_undo(s, IF_FLAGS, a.T.s_flags[s]);
+    a.T.s_flags[s] = static_cast<uint8_t>(v);
+  }
+
+  // a new slot: an Add's from the group's reserved range, others from the counter
+  __device__ uint32_t take_slot(bool reserved) {
+    const uint32_t s = (reserved && qnext < qend) ? qnext++ : atomicAdd(&a.dr->ilr_slots, 1u);
+    if (s >= a.cap_slots || s >= a.scap || s + 1 > a.hash_limit) {
+      overflow(IO_SLOTS);
+      return NONE;
+    }
+    return s;
+  }
+  // slot s into dict d (a dict this lane owns); `priv`: this level's ops may
+  // look it up (its nodes and sentinels; deep copies are reached by later
+  // levels only, through the shared hash)
+  __device__ void put_slot(uint32_t s, uint32_t d, long long key, uint32_t next, uint32_t src, uint32_t child,
+                           uint8_t flags, uint32_t at, bool priv) {
+    a.T.s_key[s] = key;
+    a.T.s_dict[s] = d;
+    a.T.s_next[s] = next;
+    a.T.s_src[s] = src;
+    a.T.s_child[s] = child;
+    a.T.s_flags[s] = flags;
+    ev(s, EV_CRE) = at;
+    ev(s, EV_DEL) = NONE;
+    ev(s, EV_CPY) = NONE;
+    if (priv) {
+      if (2 * (pused + 1) > pmask + 1) {
+        overflow(IO_PRIV);
+        return;
+      }
+      uint32_t p = slothash_pos(d, key, pmask);
+      while (ps[p] != NONE) p = (p + 1) & pmask;
+      pd[p] = d;
+      pk[p] = key;
+      ps[p] = s;
+      ++pused;
+    }
+    a.mnext[s] = a.dhead[d];
+    a.dhead[d] = s;
+  }
+  __device__ uint32_t new_dict(uint32_t owner) {
+    const uint32_t d = atomicAdd(&a.dr->ilr_dicts, 1u);
+    if (d >= a.cap_dicts) {
+      overflow(IO_DICTS);
+      return NONE;
+    }
+    a.dhead[d] = NONE;
+    a.T.d_owner[d] = owner;
+    a.T.d_sent[d] = NONE;
+    return d;
+  }
+  // the children dict of live node s, created on first use: its sentinel only
+  // (emptyChildren, src/Internal/Node.elm:46-48); the sentinel has always
+  // been there for earlier ops (no creation time)
+  __device__ uint32_t materialise(uint32_t s) {
+    const uint32_t dd = new_dict(s);
+    if (dd == NONE) return NONE;
+    const uint32_t ss = take_slot(false);
+    if (ss == NONE) return NONE;
+    put_slot(ss, dd, 0, NONE, NONE, NONE, F_TOMB | F_SENT, NONE, true);
+    a.T.d_sent[dd] = ss;
+    set_child(s, dd);
+    return bad ? NONE : dd;
+  }
+  // Persistent copy of dict `src` and every dict below it into `dst`
+  // (depth-first over an explicit stack; the source subtree holds no slot of
+  // this batch: the conflict check before the quirk guarantees it). xmap
+  // maps each source slot to its copy for the `next` links.
+  __device__ void deep_copy(uint32_t src, uint32_t dst, uint32_t at) {
+    uint32_t stk_s[ILR_MAXL], stk_d[ILR_MAXL], stk_m[ILR_MAXL];
+    int sp = 0;
+    stk_s[0] = src;
+    stk_d[0] = dst;
+    stk_m[0] = a.dhead[src];
+    while (sp >= 0 && !bad) {
+      const uint32_t sd = stk_s[sp], dd = stk_d[sp], m = stk_m[sp];
+      if (m == NONE) {  // every member copied: the `next` links inside the copy
+        for (uint32_t q = a.dhead[sd]; q != NONE; q = a.mnext[q]) {
+          const uint32_t nx = a.T.s_next[q];
+          if (nx != NONE) a.T.s_next[a.xmap[q]] = a.xmap[nx];
+        }
+        --sp;
+        continue;
+      }
+      stk_m[sp] = a.mnext[m];
+      const uint8_t fl = a.T.s_flags[m];
+      const uint32_t nm = take_slot(false);
+      if (nm == NONE) return;
+      put_slot(nm, dd, a.T.s_key[m], NONE, a.T.s_src[m], NONE, fl, at, false);
+      a.xmap[m] = nm;
+      if (fl & F_SENT) a.T.d_sent[dd] = nm;
+      const uint32_t c = a.T.s_child[m];
+      if (c != NONE && !(fl & F_TOMB)) {  // (a Tombstone has no children, :237-238)
+        const uint32_t nc = new_dict(nm);
+        if (nc == NONE) return;
+        a.T.s_child[nm] = nc;
+        if (sp + 1 >= static_cast<int>(ILR_MAXL)) {  // (deeper than any path the engine accepts)
+          conflict(IW_DEPTH);
+          return;
+        }
+        ++sp;
+        stk_s[sp] = c;
+        stk_d[sp] = nc;
+        stk_m[sp] = a.dhead[c];
+      }
+    }
+  }
+
+  // The prefix path[b .. b+L-2] as of op i (update, src/Internal/Node.elm:
+  // 138-163): ST_APPLIED with the landing dict d (or IMPLICIT) and its owner
+  // slot, ST_ALREADY (a Tombstone on the way), ST_INVALID (a key not there
+  // yet), or 3 (undecidable: a conflict). hi = the first later op at which a
+  // crossed slot changes state: the answer holds for the ops in (i, hi).
+  __device__ uint32_t resolve(const OpsDev& o, uint32_t b, uint32_t L, uint32_t i, uint32_t& d, uint32_t& own,
+                              uint32_t& hi) {
+    d = 0;
+    own = NONE;
+    hi = NONE;
+    for (uint32_t l = 0; l + 1 < L; ++l) {
+      const long long key = o.path[b + l];
+      if (d == IMPLICIT) return key == 0 ? ST_ALREADY : ST_INVALID;
+      const uint32_t sl = slothash_find(a.H, d, key);  // (shallower dicts: all in the shared hash)
+      if (sl == NONE) return ST_INVALID;
+      const uint32_t cr = ev(sl, EV_CRE), de = ev(sl, EV_DEL), cp = ev(sl, EV_CPY);
+      if (cr != NONE && cr > i) hi = min(hi, cr);
+      if (de != NONE && de > i) hi = min(hi, de);
+      if (cp != NONE && cp > i) hi = min(hi, cp);
+      if (cr != NONE && cr > i) return ST_INVALID;
+      if (de != NONE && cp != NONE) {
+        conflict(IW_TWO_EVENTS);
+        return 3;
+      }
+      const bool live = de != NONE ? i < de : (cp != NONE ? i > cp : !(a.T.s_flags[sl] & F_TOMB));
+      if (!live) return ST_ALREADY;
+      own = sl;
+      const uint32_t c = a.T.s_child[sl];
+      d = c == NONE ? IMPLICIT : c;
+    }
+    return ST_APPLIED;
+  }
+};
+
+// ---- grouping ----
+// per op: its group key in the group hash (L, owner key), the sort key
+// (L << gbits | group slot), the crossed (depth, key) pairs; empty paths are
+// InvalidPath (update [], src/Internal/Node.elm:147-148) and sort first
+__global__ void __launch_bounds__(BLOCK) k_ilr_group(OpsDev o, unsigned long long* gk, uint32_t gmask, uint32_t gbits,
+                                                     unsigned long long* tk, uint32_t tk_mask, uint32_t* skey,
+                                                     uint32_t* sval, uint8_t* st, DevResult* dr) {
+  GRID_STRIDE(i, o.n) {
+    const uint32_t b = o.off[i], L = o.off[i + 1] - b;
+    sval[i] = i;
+    if (L == 0) {
+      st[i] = ST_INVALID;
+      atomicMin(&dr->err_index, i);
+      skey[i] = 0;
+      continue;
+    }
+    const long long owner = L >= 2 ? o.path[b + L - 2] : 0;
+    const unsigned long long k = ilr_tk_key(L, owner);
+    uint32_t p = ilr_hash64(k, gmask);
+    for (;;) {
+      const unsigned long long prev = atomicCAS(&gk[p], 0ULL, k);
+      if (prev == 0ULL || prev == k) break;
+      p = (p + 1) & gmask;
+    }
+    skey[i] = (L << gbits) | p;
+    for (uint32_t l = 0; l + 1 < L; ++l) ilr_set_insert(tk, tk_mask, ilr_tk_key(l + 1, o.path[b + l]));
+  }
+}
+
+// group boundaries over the sorted keys: flag[k] = 1 at a group's first op (levels >= 1)
+__global__ void __launch_bounds__(BLOCK) k_ilr_gflag(const uint32_t* sk, uint32_t n, uint32_t gbits, uint32_t* flag) {
+  GRID_STRIDE(k, n) flag[k] = ((sk[k] >> gbits) != 0 && (k == 0 || sk[k] != sk[k - 1])) ? 1u : 0u;
+}
+// group j = [gbeg[j], gend[j]) of the sorted ops; groups per level; per
+// group its Adds (reserved slots) and private table size
+__global__ void __launch_bounds__(BLOCK) k_ilr_glist(const uint32_t* sk, const uint32_t* sv, uint32_t n,
+                                                     uint32_t gbits, const uint32_t* flag, const uint32_t* gidx,
+                                                     OpsDev o, uint32_t* gbeg, uint32_t* gend, uint32_t* lvcnt,
+                                                     uint32_t* qn, uint32_t* pcap) {
+  GRID_STRIDE(k, n) {
+    if (!flag[k]) continue;
+    const uint32_t j = gidx[k];
+    gbeg[j] = k;
+    atomicAdd(&lvcnt[sk[k] >> gbits], 1u);
+    uint32_t e = k, adds = 0;
+    do {  // (groups are short; the walk stays inside the group)
+      adds += o.kind[sv[e]] == CRDTM_ADD;
+      ++e;
+    } while (e < n && sk[e] == sk[k]);
+    gend[j] = e;
+    qn[j] = adds;
+    pcap[j] = ilr_pcap(adds);
+  }
+}
+
+// ---- one level: one lane per group ----
+__global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const uint32_t* vs, const uint32_t* gbeg,
+                                                  const uint32_t* gend, uint32_t g0, uint8_t* st) {
+  if (threadIdx.x != 0) return;
+  const uint32_t g = g0 + blockIdx.x;
+  const uint32_t kb = gbeg[g], ke = gend[g];
+  IlrLane R;
+  R.a = args;
+  R.bad = false;
+  R.pk = args.pk + args.poff[g];
+  R.pd = args.pd + args.poff[g];
+  R.ps = args.ps + args.poff[g];
+  R.pmask = args.pcap[g] - 1;
+  R.pused = 0;
+  R.qnext = args.committed + args.qoff[g];
+  R.qend = R.qnext + args.qn[g];
+  R.un = args.undo + 3 * ilr_uoff(kb, g);
+  R.ucap = ilr_ucap(ke - kb);
+  R.ucnt = 0;
+  const long long id0 = replica_of(args.ts0);
+  uint32_t app = 0, alr = 0, own = 0, err = NONE;
+  // the resolved prefix, valid for ops before chi with the same path as op cpi
+  uint32_t cpi = NONE, chi = 0, cres = 0, cd = NONE, cown = NONE, gown = NONE;
+  bool owned = false;
+  // the last slots this group created or found in its dict (typing anchors at
+  // its own previous character): key -> slot
+  long long rk0 = 0, rk1 = 0, rk2 = 0, rk3 = 0;
+  uint32_t rs0 = NONE, rs1 = NONE, rs2 = NONE, rs3 = NONE;
+  auto recent = [&](long long k) -> uint32_t {
+    return (rs0 != NONE && rk0 == k) ? rs0 : (rs1 != NONE && rk1 == k) ? rs1 : (rs2 != NONE && rk2 == k) ? rs2
+           : (rs3 != NONE && rk3 == k) ? rs3 : NONE;
+  };
+  auto remember = [&](long long k, uint32_t v) {
+    rk3 = rk2; rs3 = rs2;
+    rk2 = rk1; rs2 = rs1;
+    rk1 = rk0; rs1 = rs0;
+    rk0 = k; rs0 = v;
+  };
+  for (uint32_t k = kb; k < ke && !R.bad; ++k) {
+    const uint32_t i = vs[k];
+    const uint32_t b = o.off[i], L = o.off[i + 1] - b;
+    const uint8_t kind = o.kind[i];
+    uint8_t s = ST_APPLIED;
+    // ---- the prefix as of op i (path[L-2] is the group's owner key) ----
+    bool hit = cpi != NONE && i < chi;
+    if (hit) {
+      const uint32_t cb = o.off[cpi];
+      for (uint32_t l = 0; hit && l + 2 < L; ++l) hit = o.path[b + l] == o.path[cb + l];
+    }
+    if (!hit) {
+      cres = R.resolve(o, b, L, i, cd, cown, chi);
+      cpi = i;
+      if (cres == 3) break;
+    }
+    if (cres != ST_APPLIED) {
+      s = static_cast<uint8_t>(cres);
+    } else {
+      if (owned && cown != gown) {  // (one owner key, two nodes: two dicts in one group)
+        R.conflict(IW_TWO_DICTS);
+        break;
+      }
+      owned = true;
+      gown = cown;
+      const long long kk = o.path[b + L - 1];
+      const long long ts = o.ts[i];
+      uint32_t d = cd;
+      if (d == IMPLICIT) {
+        // the empty children {0: Tombstone}: only an Add after the sentinel
+        // changes it (then the dict is created); ts 0 or Delete 0: AlreadyApplied
+        if (kind == CRDTM_ADD && ts != 0 && kk == 0) {
+          d = R.materialise(cown);
+          if (d == NONE) break;
+          cd = d;
+        } else {
+          s = (kk == 0 || (kind == CRDTM_ADD && ts == 0)) ? ST_ALREADY : ST_NOTFOUND;
+        }
+      }
+      if (s == ST_APPLIED) {
+        if (kind == CRDTM_DELETE) {  // deleteHelp (:112-122)
+          uint32_t t = recent(kk);
+          if (t == NONE) t = R.find(d, kk);
+          if (t == NONE) {
+            s = ST_NOTFOUND;
+          } else if (args.T.s_flags[t] & F_TOMB) {
+            s = ST_ALREADY;
+          } else {
+            R.set_flags(t, args.T.s_flags[t] | F_TOMB);
+            if (R.ev(t, EV_DEL) == NONE) R.ev(t, EV_DEL) = i;  // children drop at the commit
+          }
+        } else if (R.find(d, ts) != NONE) {  // addAfterHelp (:56-90)
+          s = ST_ALREADY;
+        } else {
+          uint32_t found = recent(kk);
+          if (found == NONE) found = R.find(d, kk);
+          if (found == NONE) {
+            s = ST_NOTFOUND;
+          } else {
+            // findInsertion (:93-104): ls = the slot of the key it returns
+            uint32_t node = found, ls = found, rn;
+            for (;;) {
+              rn = args.T.s_next[node];
+              if (rn == NONE) break;
+              uint32_t live = rn;
+              while (live != NONE && (args.T.s_flags[live] & F_TOMB)) live = args.T.s_next[live];
+              if (live == NONE) break;
+              if (ts > args.T.s_key[rn]) break;
+              ls = rn;
+              node = live;
+            }
+            const uint32_t x = R.take_slot(true);
+            if (x == NONE) break;
+            const uint8_t lsf = args.T.s_flags[ls];
+            // x is reachable from the dict's sentinel iff its predecessor is
+            R.put_slot(x, d, ts, rn, ILR_TAG | i, NONE, (lsf & F_ORPHAN) ? F_ORPHAN : 0, i, true);
+            if (R.bad) break;
+            if (ls == node) {
+              R.set_next(node, x);
+            } else {
+              // the copy quirk: slot ls := copy of node with
+              // next = ts; the entries after it up to node drop off the
+              // chain. Its children are node's as of op i: undecidable here
+              // when the batch reaches below node (a later level, which may
+              // also create node's children dict). A slot the batch deleted
+              // and now re-fills would have three states for later levels.
+              if (ilr_set_has(args.tk, args.tk_mask, ilr_tk_key(L, args.T.s_key[node]))) {
+                R.conflict(IW_COPY_BELOW);
+                break;
+              }
+              if (R.ev(ls, EV_CPY) != NONE || R.ev(ls, EV_DEL) != NONE) {
+                R.conflict(IW_REFILL);
+                break;
+              }
+              if (!(lsf & F_ORPHAN)) {
+                for (uint32_t q = args.T.s_next[ls]; q != NONE; q = args.T.s_next[q]) {
+                  R.set_flags(q, args.T.s_flags[q] | F_ORPHAN);
+                  if (q == node) break;
+                }
+              }
+              const uint32_t c = args.T.s_child[node];
+              R.set_src(ls, args.T.s_src[node]);
+              R.set_flags(ls, (args.T.s_flags[node] & ~F_ORPHAN) | (lsf & F_ORPHAN));
+              R.set_next(ls, x);
+              R.ev(ls, EV_CPY) = i;
+              uint32_t nc = NONE;
+              if (c != NONE) {
+                nc = R.new_dict(ls);
+                if (nc == NONE) break;
+                R.deep_copy(c, nc, i);
+                if (R.bad) break;
+              }
+              R.set_child(ls, nc);
+            }
+            remember(ts, x);
+          }
+        }
+      }
+    }
+    if (R.bad) break;
+    st[i] = s;
+    if (s == ST_APPLIED) ++app;
+    else if (s == ST_ALREADY) ++alr;
+    else err = min(err, i);
+    // incrementTimestamp (src/CRDTree.elm:337-343): Ok Adds of the own replica
+    if ((s == ST_APPLIED || s == ST_ALREADY) && kind == CRDTM_ADD && replica_of(o.ts[i]) == id0) ++own;
+  }
+  args.ucnt[g] = R.ucnt;
+  if (!R.bad) {
+    // reserved slots no Add took: dead entries of the batch's dead dict
+    for (uint32_t x = R.qnext; x < R.qend; ++x) {
+      args.T.s_key[x] = x;
+      args.T.s_dict[x] = args.grave;
+      args.T.s_next[x] = NONE;
+      args.T.s_src[x] = NONE;
+      args.T.s_child[x] = NONE;
+      args.T.s_flags[x] = F_TOMB | F_ORPHAN;
+      R.ev(x, EV_CRE) = NONE;
+      R.ev(x, EV_DEL) = NONE;
+      R.ev(x, EV_CPY) = NONE;
+      args.mnext[x] = NONE;
+    }
+  }
+  if (app) atomicAdd(&args.dr->n_applied, app);
+  if (alr) atomicAdd(&args.dr->n_already, alr);
+  if (own) atomicAdd(&args.dr->own_ok_adds, own);
+  if (err != NONE) atomicMin(&args.dr->err_index, err);
+}
+
+// the slot counter before a level
+__global__ void k_ilr_mark(const DevResult* d, uint32_t* mark) { *mark = d->ilr_slots; }
+// after a level: its slots into the shared hash — the groups' reserved
+// ranges and what the counter gave (skipped once the batch overflowed or
+// conflicted: it is rolled back and the index rebuilt)
+__global__ void __launch_bounds__(BLOCK) k_ilr_publish(TreeDev T, SlotHash H, const uint32_t* qoff, uint32_t g0,
+                                                       uint32_t g1, uint32_t committed, const uint32_t* mark,
+                                                       const DevResult* d, uint32_t cap) {
+  if (d->ilr_overflow || d->ilr_conflict) return;
+  const uint32_t a0 = committed + qoff[g0], a1 = committed + qoff[g1];
+  const uint32_t b0 = *mark, b1 = min(d->ilr_slots, cap);
+  const uint32_t na = a1 - a0, nb = b1 > b0 ? b1 - b0 : 0u;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < na + nb; j += gridDim.x * blockDim.x) {
+    const uint32_t s = j < na ? a0 + j : b0 + (j - na);
+    slothash_put_par(H, T.s_dict[s], T.s_key[s], s);
+  }
+}
+
+// undo of one level's groups, each newest first (launched deepest level first:
+// a field two levels wrote — an owner's children — gets its oldest value)
+__global__ void __launch_bounds__(BLOCK) k_ilr_rollback(TreeDev T, const uint32_t* undo, const uint32_t* ucnt,
+                                                        const uint32_t* gbeg, uint32_t g0, uint32_t cnt) {
+  GRID_STRIDE(j, cnt) {
+    const uint32_t g = g0 + j;
+    const uint32_t* u = undo + 3 * ilr_uoff(gbeg[g], g);
+    for (uint32_t e = ucnt[g]; e-- > 0;) {
+      const uint32_t s = u[3 * e], f = u[3 * e + 1], v = u[3 * e + 2];
+      if (f == IF_NEXT) T.s_next[s] = v;
+      else if (f == IF_SRC) T.s_src[s] = v;
+      else if (f == IF_CHILD) T.s_child[s] = v;
+      else T.s_flags[s] = static_cast<uint8_t>(v);
+    }
+  }
+}
+
+// commit, for the slots the batch touched — the new ones [lo, hi) and the
+// state's slots in the undo logs: sources tagged with an op index take its
+// log index; a node the batch deleted drops its children (children
+// Tombstone = Dict.empty, src/Internal/Node.elm:237-238)
+__device__ __forceinline__ void ilr_fix_slot(TreeDev& T, uint32_t s, const uint32_t* logidx, uint32_t log_base,
+                                             const uint32_t* ev) {
+  const uint32_t src = T.s_src[s];
+  if (src != NONE && (src & ILR_TAG)) T.s_src[s] = log_base + logidx[src & ~ILR_TAG];
+  if (ev[3ULL * s + EV_DEL] != NONE) T.s_child[s] = NONE;
+}
+__global__ void __launch_bounds__(BLOCK) k_ilr_fix(TreeDev T, uint32_t lo, uint32_t hi, const uint32_t* undo,
+                                                   uint32_t nu, const uint32_t* logidx, uint32_t log_base,
+                                                   const uint32_t* ev) {
+  const uint32_t nn = hi - lo;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nn + nu; j += gridDim.x * blockDim.x) {
+    if (j < nn) {
+      ilr_fix_slot(T, lo + j, logidx, log_base, ev);
+    } else {
+      const uint32_t s = undo[3ULL * (j - nn)];
+      if (s != NONE && (undo[3ULL * (j - nn) + 1] == IF_SRC || undo[3ULL * (j - nn) + 1] == IF_FLAGS))
+        ilr_fix_slot(T, s, logidx, log_base, ev);  // (the entries of one slot: same result, any order)
+    }
+  }
+}
+// then the event times back to NONE (a separate pass: the fix reads them)
+__global__ void __launch_bounds__(BLOCK) k_ilr_ev_reset(uint32_t lo, uint32_t hi, const uint32_t* undo, uint32_t nu,
+                                                        uint32_t* ev) {
+  const uint32_t nn = hi - lo;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nn + nu; j += gridDim.x * blockDim.x) {
+    const uint32_t s = j < nn ? lo + j : undo[3ULL * (j - nn)];
+    if (s == NONE) continue;
+    ev[3ULL * s] = NONE;
+    ev[3ULL * s + 1] = NONE;
+    ev[3ULL * s + 2] = NONE;
+  }
+}
+
+__global__ void k_ilr_counters(DevResult* d, TreeDev T, uint32_t* dhead, uint32_t committed, const uint32_t* qtot,
+                               uint32_t grave) {
+  d->ilr_slots = committed + *qtot;
+  d->ilr_dicts = grave + 1;
+  d->ilr_conflict = 0;
+  d->ilr_overflow = 0;
+  d->ilr_why = 0;
+  T.d_owner[grave] = NONE;  // (no owner: never alive, src/Internal/Node.elm has no such dict)
+  T.d_sent[grave] = NONE;
+  dhead[grave] = NONE;
+}
+
+static uint32_t pow2_ge(uint64_t x) {
+  uint32_t p = 1024;
+  while (p < x && p < (1u << 31)) p <<= 1;
+  return p;
+}
+
+bool ilr_wanted(const crdtm_tree* t, uint32_t n) {
+  const char* e = getenv("CRDTM_INCREMENTAL");
+  if (e && (!strcmp(e, "replay") || !strcmp(e, "remerge"))) return false;
+  if (e && !strcmp(e, "ilr")) return true;
+  // per-dict replay on the state: worth it when the state outweighs the batch
+  // (the re-merge's parallel work grows with log + batch)
+  return t->n_slots >= 4ULL * n && t->max_depth <= ILR_MAXL;
+}
+
+// (re)build the index of the state: hash sized for the slot capacity
+static int ilr_build(crdtm_tree* t) {
+  crdtm_ctx* c = t->ctx;
+  hipStream_t s = c->stream;
+  if (!t->ilr) t->ilr.reset(new IlrIndex);
+  IlrIndex& X = *t->ilr;
+  const uint32_t H = pow2_ge(2 * t->cap.slots);
+  if (X.hcap < H) {
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (X.H.dict) hipFree(X.H.dict);
+    if (X.H.key) hipFree(X.H.key);
+    if (X.H.slot) hipFree(X.H.slot);
+    X.H.dict = nullptr;
+    X.H.key = nullptr;
+    X.H.slot = nullptr;
+    HIP_CHECK(hipMalloc(&X.H.dict, H * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&X.H.key, H * sizeof(long long)));
+    HIP_CHECK(hipMalloc(&X.H.slot, H * sizeof(uint32_t)));
+    X.hcap = H;
+    X.H.mask = H - 1;
+  }
+  if (X.dcap < t->cap.dicts) {
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (X.dhead) hipFree(X.dhead);
+    X.dhead = nullptr;
+    HIP_CHECK(hipMalloc(&X.dhead, t->cap.dicts * sizeof(uint32_t)));
+    X.dcap = t->cap.dicts;
+  }
+  if (X.scap < t->cap.slots) {
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (X.mnext) hipFree(X.mnext);
+    if (X.ev) hipFree(X.ev);
+    if (X.xmap) hipFree(X.xmap);
+    X.mnext = nullptr;
+    X.ev = nullptr;
+    X.xmap = nullptr;
+    HIP_CHECK(hipMalloc(&X.mnext, t->cap.slots * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&X.ev, 3 * t->cap.slots * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&X.xmap, t->cap.slots * sizeof(uint32_t)));
+    X.scap = t->cap.slots;
+  }
+  HIP_CHECK(hipMemsetAsync(X.H.slot, 0xFF, X.hcap * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(X.dhead, 0xFF, X.dcap * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(X.ev, 0xFF, 3 * X.scap * sizeof(uint32_t), s));
+  LAUNCH(k_replay_index, dim3(grid_for(t->n_slots)), dim3(BLOCK), 0, s, t->d, static_cast<uint32_t>(t->n_slots), X.H,
+         X.dhead, X.mnext);
+  X.hused = t->n_slots;
+  t->ilr_valid = true;
+  return CRDTM_OK;
+}
+
+int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res, bool* handled) {
+  *handled = false;
+  crdtm_ctx* c = t->ctx;
+  hipStream_t s = c->stream;
+  Arena& ws = c->ws;
+  DevResult* dr = c->dres;
+  const uint32_t n = o.n;
+  const size_t mark0 = ws.used;
+  int r;
+  // ranges and the longest path (one host round trip)
+  LAUNCH(k_dres_init, dim3(1), dim3(64), 0, s, dr);
+  launch_pre(c, o, s);
+  RangeReset keep_clean{c};  // (k_pre fills the context's replica ranges; nothing here reads them)
+  if (o.n_path)
+    LAUNCH(k_path_range, dim3(std::min<uint32_t>(grid_for(o.n_path / 2 + 1), 1024)), dim3(BLOCK), 0, s, o, dr);
+  if ((r = sync_read(c))) return r;
+  keep_clean.nr = c->hres->max_replica + 1;
+  keep_clean.now();
+  if (c->hres->bad_range) return CRDTM_E_RANGE;  // (the state is untouched)
+  const uint32_t maxlen = c->hres->max_len;
+  if (maxlen > ILR_MAXL) return CRDTM_OK;
+  // capacity: new nodes and their dicts, the dead dict, room for deep copies
+  // (an overflow sends the batch to the re-merge)
+  TreeCaps need = t->cap;
+  const uint64_t extra = 1024 + n / 2;
+  need.slots = std::max<uint64_t>(need.slots, t->n_slots + 2ULL * n + extra);
+  need.dicts = std::max<uint64_t>(need.dicts, t->n_dicts + n + extra);
+  need.log = std::max<uint64_t>(need.log, t->log_n + n + 1);
+  need.lpath = std::max<uint64_t>(need.lpath, t->log_npath + o.n_path + 1);
+  if (need.slots > t->cap.slots || need.dicts > t->cap.dicts || need.log > t->cap.log || need.lpath > t->cap.lpath) {
+    if ((r = grow_tree(t, need))) return r;
+  }
+  IlrIndex* X = t->ilr.get();
+  if (!t->ilr_valid || !X || X->scap < t->cap.slots || X->dcap < t->cap.dicts || X->hcap < 2 * t->cap.slots) {
+    if ((r = ilr_build(t))) return r;
+    X = t->ilr.get();
+  }
+  // ---- groups: (L, owner key), sorted by level, batch order inside ----
+  const uint32_t gsz = pow2_ge(2ULL * n + 16);
+  uint32_t gbits = 0;
+  while ((1u << gbits) < gsz) ++gbits;
+  unsigned long long* gk = ws.alloc<unsigned long long>(gsz);
+  const uint32_t tsz = pow2_ge(2ULL * o.n_path + 16);
+  unsigned long long* tk = ws.alloc<unsigned long long>(tsz);
+  uint32_t* sk[2] = {ws.alloc<uint32_t>(n + 1), ws.alloc<uint32_t>(n + 1)};
+  uint32_t* sv[2] = {ws.alloc<uint32_t>(n + 1), ws.alloc<uint32_t>(n + 1)};
+  uint8_t* st = ws.alloc<uint8_t>(n + 1);
+  uint32_t* nd = ws.alloc<uint32_t>(2);
+  uint32_t* flag = ws.alloc<uint32_t>(n + 1);
+  uint32_t* gidx = ws.alloc<uint32_t>(n + 1);
+  uint32_t* gbeg = ws.alloc<uint32_t>(n + 1);
+  uint32_t* gend = ws.alloc<uint32_t>(n + 1);
+  uint32_t* qn = ws.alloc<uint32_t>(n + 2);
+  uint32_t* qoff = ws.alloc<uint32_t>(n + 2);
+  uint32_t* pcap = ws.alloc<uint32_t>(n + 2);
+  uint32_t* poff = ws.alloc<uint32_t>(n + 2);
+  uint32_t* ucnt = ws.alloc<uint32_t>(n + 1);
+  uint32_t* lvcnt = ws.alloc<uint32_t>(LV_N);
+  HIP_CHECK(hipMemsetAsync(gk, 0, gsz * sizeof(unsigned long long), s));
+  HIP_CHECK(hipMemsetAsync(tk, 0, tsz * sizeof(unsigned long long), s));
+  HIP_CHECK(hipMemsetAsync(lvcnt, 0, LV_N * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(qn, 0, (n + 2) * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(pcap, 0, (n + 2) * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(nd), n, 1, s));
+  LAUNCH(k_ilr_group, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, gk, gsz - 1, gbits, tk, tsz - 1, sk[0], sv[0], st, dr);
+  uint32_t *ks = nullptr, *vs = nullptr;
+  if ((r = radix_sort_pairs(sk[0], sv[0], sk[1], sv[1], nd, n, gbits + 7, ws, s, &ks, &vs))) return r;
+  LAUNCH(k_ilr_gflag, dim3(grid_for(n)), dim3(BLOCK), 0, s, ks, n, gbits, flag);
+  if ((r = scan_excl_u32(flag, gidx, n, &dr->ilr_groups, ws, s))) return r;
+  LAUNCH(k_ilr_glist, dim3(grid_for(n)), dim3(BLOCK), 0, s, ks, vs, n, gbits, flag, gidx, o, gbeg, gend, lvcnt, qn,
+         pcap);
+  // reserved slot ranges and private tables: offsets and totals (in lvcnt)
+  if ((r = scan_excl_u32(qn, qoff, n + 1, lvcnt + LV_QTOT, ws, s))) return r;
+  if ((r = scan_excl_u32(pcap, poff, n + 1, lvcnt + LV_PTOT, ws, s))) return r;
+  const uint32_t grave = static_cast<uint32_t>(t->n_dicts);
+  LAUNCH(k_ilr_counters, dim3(1), dim3(1), 0, s, dr, t->d, X->dhead, static_cast<uint32_t>(t->n_slots),
+         lvcnt + LV_QTOT, grave);
+  uint32_t* hl = c->hres->ilr_levels;  // (pinned)
+  HIP_CHECK(hipMemcpyAsync(hl, lvcnt, LV_N * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  if (int rw = stream_wait(s)) return rw;
+  uint32_t lv[LV_N];
+  memcpy(lv, hl, sizeof(lv));
+  uint32_t G = 0;
+  for (uint32_t L = 1; L <= ILR_MAXL; ++L) G += lv[L];
+  const uint32_t ptot = lv[LV_PTOT];
+  long long* pk = ws.alloc<long long>(ptot);
+  uint32_t* pd = ws.alloc<uint32_t>(ptot);
+  uint32_t* ps = ws.alloc<uint32_t>(ptot);
+  const uint64_t nu = 3ULL * n + 8ULL * G + 8;  // undo triples (ilr_uoff layout)
+  uint32_t* undo = ws.alloc<uint32_t>(3 * nu);
+  uint32_t* marks = ws.alloc<uint32_t>(ILR_MAXL + 2);
+  HIP_CHECK(hipMemsetAsync(ps, 0xFF, static_cast<size_t>(ptot) * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(undo, 0xFF, 3 * nu * sizeof(uint32_t), s));
+  // ---- the levels ----
+  IlrArgs a;
+  a.T = t->d;
+  a.H = X->H;
+  a.dhead = X->dhead;
+  a.mnext = X->mnext;
+  a.ev = X->ev;
+  a.xmap = X->xmap;
+  a.scap = static_cast<uint32_t>(X->scap);
+  a.committed = static_cast<uint32_t>(t->n_slots);
+  a.cap_slots = static_cast<uint32_t>(t->cap.slots);
+  a.cap_dicts = static_cast<uint32_t>(t->cap.dicts);
+  a.hash_limit = X->hcap / 2;
+  a.tk = tk;
+  a.tk_mask = tsz - 1;
+  a.ts0 = t->timestamp;
+  a.dr = dr;
+  a.pk = pk;
+  a.pd = pd;
+  a.ps = ps;
+  a.poff = poff;
+  a.pcap = pcap;
+  a.qoff = qoff;
+  a.qn = qn;
+  a.undo = undo;
+  a.ucnt = ucnt;
+  a.grave = grave;
+  uint32_t g0 = 0, levels = 0;
+  uint32_t lv_g0[ILR_MAXL + 2] = {};
+  for (uint32_t L = 1; L <= maxlen; ++L) {
+    const uint32_t cnt = lv[L];
+    lv_g0[L] = g0;
+    if (!cnt) continue;
+    LAUNCH(k_ilr_mark, dim3(1), dim3(1), 0, s, dr, marks + L);
+    LAUNCH(k_ilr_level, dim3(cnt), dim3(64), 0, s, a, o, vs, gbeg, gend, g0, st);
+    LAUNCH(k_ilr_publish, dim3(256), dim3(BLOCK), 0, s, a.T, a.H, qoff, g0, g0 + cnt, a.committed, marks + L, dr,
+           a.cap_slots);
+    g0 += cnt;
+    ++levels;
+  }
+  if ((r = sync_read(c))) return r;
+  const DevResult h = *c->hres;
+  const long long new_ts = t->timestamp + h.own_ok_adds;
+  const bool drift = replica_of(new_ts) != replica_of(t->timestamp);
+  static const bool debug = getenv("CRDTM_ILR_DEBUG") != nullptr;
+  if (debug)
+    fprintf(stderr, "ilr: n=%u groups=%u levels=%u conflict=%u why=%#x overflow=%#x drift=%d err=%d slots+%u\n", n, G,
+            levels, h.ilr_conflict, h.ilr_why, h.ilr_overflow, drift ? 1 : 0,
+            h.err_index == NONE ? -1 : static_cast<int>(h.err_index),
+            h.ilr_slots - static_cast<uint32_t>(t->n_slots));
+  if (h.ilr_conflict || h.ilr_overflow || drift || h.err_index != NONE) {
+    for (uint32_t L = maxlen; L >= 1; --L)
+      if (lv[L])
+        LAUNCH(k_ilr_rollback, dim3(grid_for(lv[L])), dim3(BLOCK), 0, s, t->d, undo, ucnt, gbeg, lv_g0[L], lv[L]);
+    t->ilr_valid = false;  // (its hash, member lists and event times hold the batch)
+    if (h.ilr_conflict || h.ilr_overflow || drift) {  // the re-merge decides
+      HIP_CHECK(hipStreamSynchronize(s));
+      ws.used = mark0;
+      return CRDTM_OK;
+    }
+    // the first failing op in batch order (every op saw only earlier ops)
+    *handled = true;
+    res->path_taken = CRDTM_PATH_DICT_REPLAY;
+    res->flags |= CRDTM_FLAG_DICT_INCR;
+    uint8_t est = 0;
+    HIP_CHECK(hipMemcpyAsync(&est, st + h.err_index, 1, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    res->code = est == ST_INVALID ? CRDTM_INVALID_PATH : CRDTM_OPERATION_FAILED;
+    res->err_index = h.err_index;
+    if (st_out) LAUNCH(k_status_out, dim3(grid_for(n)), dim3(BLOCK), 0, s, st, n, h.err_index, st_out);
+    return CRDTM_OK;
+  }
+  // ---- commit: log (applied ops in order), sources, dropped children, replicas ----
+  *handled = true;
+  uint32_t* appl = ws.alloc<uint32_t>(n + 1);
+  uint32_t* plen = ws.alloc<uint32_t>(n + 1);
+  long long* rep = ws.alloc<long long>(2 * static_cast<uint64_t>(n) + 2);
+  LAUNCH(k_post_flags, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, appl, plen);
+  if ((r = scan_excl_u32(appl, appl, n, &dr->log_n, ws, s))) return r;
+  if ((r = scan_excl_u32(plen, plen, n, &dr->log_npath, ws, s))) return r;
+  LAUNCH(k_log, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, t->d, static_cast<uint32_t>(t->log_n),
+         static_cast<uint32_t>(t->log_npath), appl, plen);
+  LAUNCH(k_log_tail, dim3(1), dim3(1), 0, s, t->d, static_cast<uint32_t>(t->log_n), &dr->log_n,
+         static_cast<uint32_t>(t->log_npath), &dr->log_npath);
+  const uint32_t lo = static_cast<uint32_t>(t->n_slots), hi = h.ilr_slots;
+  const uint32_t fx = grid_for(static_cast<uint64_t>(hi - lo) + nu, BLOCK, 4096);
+  LAUNCH(k_ilr_fix, dim3(fx), dim3(BLOCK), 0, s, t->d, lo, hi, undo, static_cast<uint32_t>(nu), appl,
+         static_cast<uint32_t>(t->log_n), X->ev);
+  LAUNCH(k_ilr_ev_reset, dim3(fx), dim3(BLOCK), 0, s, lo, hi, undo, static_cast<uint32_t>(nu), X->ev);
+  if ((r = replica_fold(c, o, st, rep, ws, s))) return r;
+  if (st_out) LAUNCH(k_status_out, dim3(grid_for(n)), dim3(BLOCK), 0, s, st, n, NONE, st_out);
+  if ((r = sync_read(c))) return r;
+  if ((r = take_replicas(t, rep))) return r;
+  X->hused = h.ilr_slots;
+  t->n_slots = h.ilr_slots;
+  t->n_dicts = h.ilr_dicts;
+  t->last_begin = t->log_n;
+  t->log_n += c->hres->log_n;
+  t->log_npath += c->hres->log_npath;
+  t->last_end = t->log_n;
+  t->timestamp = new_ts;
+  if (t->max_depth < maxlen) t->max_depth = maxlen;
+  t->doc_valid = false;
+  t->flat_clean = false;
+  t->kidx_valid = false;
+  res->path_taken = CRDTM_PATH_DICT_REPLAY;
+  res->flags |= CRDTM_FLAG_DICT_INCR;
+  res->n_applied = h.n_applied;
+  res->n_already = h.n_already;
+  res->serial_dicts = G;
+  res->serial_ops = n;
+  res->serial_max = levels;
+  res->code = CRDTM_OK;
+  return CRDTM_OK;
+}
+
+}  // namespace crdtm

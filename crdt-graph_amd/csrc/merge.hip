@@ -290,12 +290,17 @@ __global__ void __launch_bounds__(BLOCK) k_range_base(const uint2* rng, uint32_t
 
 // The replica range table lives in the context and is kept clean between
 // calls: every merge resets the entries it touched (ids 0..max_replica).
-__global__ void __launch_bounds__(BLOCK) k_range_reset(uint2* rng, const DevResult* dres) {
-  const uint32_t nr = dres->max_replica + 1;
+__global__ void __launch_bounds__(BLOCK) k_range_reset(uint2* rng, uint32_t nr, const DevResult* dres) {
+  if (nr == 0) nr = dres->max_replica + 1;
   GRID_STRIDE(r, nr) rng[r] = make_uint2(NONE, 0u);
 }
 
-static void launch_pre(crdtm_ctx* c, const OpsDev& o, hipStream_t s) {
+void range_reset(crdtm_ctx* c, uint32_t nr) {
+  LAUNCH(k_range_reset, dim3(nr ? std::min<uint32_t>(grid_for(nr), 1024) : 64), dim3(BLOCK), 0, c->stream, c->crange,
+         nr, c->dres);
+}
+
+void launch_pre(crdtm_ctx* c, const OpsDev& o, hipStream_t s) {
   const uint32_t g = static_cast<uint32_t>(std::min<uint64_t>((o.n / 4 + PRE_T - 1) / PRE_T + 1, 512));
   LAUNCH(k_pre<PRE_T>, dim3(g), dim3(PRE_T), 0, s, o, c->crange, c->dres);
 }
@@ -3320,21 +3325,6 @@ static int flat_rec(crdtm_ctx* c, uint32_t Q, FlatRec& fr) {
   return CRDTM_OK;
 }
 
-// Launches k_range_reset when a merge leaves apply_batch by any path.
-// (`armed` is cleared when the merge reset the table itself, stream-ordered
-// before its final result read, and set again if it had to rebuild it)
-struct RangeReset {
-  crdtm_ctx* c;
-  bool armed = true;
-  void now() {
-    LAUNCH(k_range_reset, dim3(64), dim3(BLOCK), 0, c->stream, c->crange, c->dres);
-    armed = false;
-  }
-  ~RangeReset() {
-    if (armed) now();
-  }
-};
-
 // Flat closed form: launches K2/K4 (the order), the commit and the replica
 // collection for K nodes; nothing synchronises. The flat order's run tree
 // may be too deep (DevResult::run_fail, read with the final result): then
@@ -3660,6 +3650,8 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   RangeReset keep_clean{c};  // resets the context's replica ranges on every exit
   int r;
   if ((r = sync_read(c))) return r;
+  // (explicit from here: the replay paths reset the DevResult)
+  keep_clean.nr = c->hres->max_replica + 1;
   if (c->hres->bad_range) return CRDTM_E_RANGE;
   const uint32_t maxlen = c->hres->max_len;
   if (t->max_depth < maxlen) t->max_depth = maxlen;
@@ -4020,6 +4012,12 @@ static bool remerge_wanted(const crdtm_tree* t, uint32_t n) {
 
 static int apply_batch_paths(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res) {
   const bool fresh = t->n_slots == 1 && t->log_n == 0;
+  if (!fresh && o.n && ilr_wanted(t, o.n)) {  // per children dict on the state itself (ilr.hip)
+    bool handled = false;
+    const int r = ilr_apply(t, o, st_out, res, &handled);
+    if (r != CRDTM_OK || handled) return r;
+  }
+  t->ilr_valid = false;  // (every other path rewrites or extends the state without its index)
   if (fresh || o.n == 0 || !remerge_wanted(t, o.n)) return apply_core(t, o, st_out, res);
   crdtm_ctx* c = t->ctx;
   hipStream_t s = c->stream;
@@ -4134,6 +4132,7 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
     bool handled = false;
     int r = finc_apply(t, o, st_out, res, &handled);
     if (r != CRDTM_OK || handled) {
+      t->ilr_valid = false;
       if (r != CRDTM_OK) {
         t->flat_clean = was_clean;
         t->kidx_valid = false;

@@ -90,6 +90,8 @@ typedef struct crdtm_result {
                                     (incremental closed form, gaps of the base order; incr.hip) */
 #define CRDTM_FLAG_INCR_WINDOWS 4 /* with INCREMENTAL: blocks of the gapped order were spread over windows */
 #define CRDTM_FLAG_INCR_DENSE 8   /* with INCREMENTAL: no window could take the batch: dense merge, rebuilt */
+#define CRDTM_FLAG_DICT_INCR 16   /* non-fresh tree: the batch replayed per children dict on the state itself,
+                                     level by level (only the dicts it reaches; ilr.hip) */
 
 typedef struct crdtm_ctx crdtm_ctx;   /* device + stream + workspace */
 typedef struct crdtm_tree crdtm_tree; /* one replica's CRDTree state, resident in HBM */

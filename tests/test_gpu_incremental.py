@@ -2,9 +2,12 @@
 already holds state (src/CRDTree.elm:265-269 on a non-fresh tree — a replica
 applying remote batches), chained against `orc_apply` on one oracle tree.
 
-Both incremental paths are pinned: the re-merge of log ++ batch on the
-parallel fresh-tree paths (merge.hip apply_batch, CRDTM_FLAG_REMERGE) and the
-one-lane sequential replay on the existing state (CRDTM_INCREMENTAL=replay).
+Every incremental path is pinned: the re-merge of log ++ batch on the
+parallel fresh-tree paths (merge.hip apply_batch, CRDTM_FLAG_REMERGE), the
+one-lane sequential replay on the existing state (CRDTM_INCREMENTAL=replay)
+and the per-dict level replay on the state (ilr.hip, CRDTM_FLAG_DICT_INCR,
+forced by CRDTM_INCREMENTAL=ilr; what it cannot decide falls back to the
+re-merge).
 Every step compares the dict structure, the visible document, timestamp,
 replicas, lastOperation and the applied count; a failing batch in the middle
 must leave everything unchanged (transactional, src/CRDTree.elm:224-232).
@@ -47,7 +50,7 @@ def failing_batch(s, a):
                 path=np.concatenate([one["path"], bad["path"]]))
 
 
-@pytest.mark.parametrize("mode", ["auto", "remerge", "replay"])
+@pytest.mark.parametrize("mode", ["auto", "remerge", "replay", "ilr"])
 @pytest.mark.parametrize("name", sorted(STREAMS))
 def test_incremental_chain(name, mode, monkeypatch):
     if mode == "auto":  # the default: the incremental flat closed form where it applies
@@ -64,7 +67,7 @@ def test_incremental_chain(name, mode, monkeypatch):
     from oracle.oracle import lib as olib
     ot = olib().orc_init(0)
     et = CRDTree.init(0)
-    remerged = incr = 0
+    remerged = incr = dict_incr = 0
     for k, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
         if k == 3:  # a failing batch in the middle: Err, nothing changes
             before = engine_summary(et)
@@ -85,7 +88,10 @@ def test_incremental_chain(name, mode, monkeypatch):
             remerged += 1
         if k and mode == "replay":
             assert res.path_taken == N.PATH_REPLAY and not res.flags & N.FLAG_REMERGE
-        if mode != "auto":
+        if k and res.flags & N.FLAG_DICT_INCR:
+            dict_incr += 1
+            assert mode in ("auto", "ilr")
+        if mode not in ("auto", "ilr"):
             assert not res.flags & N.FLAG_INCREMENTAL
         elif res.flags & N.FLAG_INCREMENTAL:
             incr += 1
@@ -99,6 +105,42 @@ def test_incremental_chain(name, mode, monkeypatch):
     if mode == "auto":
         # adds-only flat batches into a flat document: the incremental closed form
         assert (incr == len(cuts) - 2) if name == "flat_adds" else incr == 0
+    if mode == "ilr" and name != "flat_adds":
+        assert dict_incr >= (len(cuts) - 2) // 2, (dict_incr, len(cuts))
+    olib().orc_free(ot)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_dict_incremental_adversarial(seed, monkeypatch):
+    """The per-dict level replay (ilr.hip) on the reference-test-shaped
+    adversarial streams (copy quirks, nested copies, orphans, duplicates,
+    deletes under deleted branches, errors): each stream applied as a base
+    and then in chunks of varied size, every step against one oracle tree
+    (structure, visible document, timestamp, replicas, log); batches it
+    cannot decide fall back to the re-merge, failing ones leave the state
+    unchanged."""
+    monkeypatch.setenv("CRDTM_INCREMENTAL", "ilr")
+    from adversarial import adversarial
+    from crdtm.tree import pack
+    from oracle.oracle import lib as olib
+    s = pack(adversarial(seed, [600, 1500][seed % 2], replicas=2 + seed % 3, max_depth=1 + seed % 4))
+    n = len(s["path_off"]) - 1
+    rng = np.random.default_rng(seed)
+    cuts = [0, max(1, n // 3)]
+    while cuts[-1] < n:
+        cuts.append(min(n, cuts[-1] + int(rng.choice([1, 3, 17, 60, 200]))))
+    ot = olib().orc_init(0)
+    et = CRDTree.init(0)
+    used = 0
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        chunk = sub(s, a, b)
+        _, rc, oerr = oracle_apply_arrays(chunk, b - a, tree=ot)
+        res = et.apply_arrays(chunk, b - a)
+        assert (res.code, res.err_index if rc else -1) == (rc, oerr if rc else -1), (a, b)
+        used += bool(res.flags & N.FLAG_DICT_INCR)  # (quirk-heavy chunks may all fall back)
+        assert engine_summary(et) == oracle_summary(ot), (a, b)
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
     olib().orc_free(ot)
 
 
@@ -214,3 +256,25 @@ def test_versions_copy_on_write():
     assert engine_summary(v3) == oracle_summary(oracle_upto(10000))
     for t in (o20, o15):
         olib().orc_free(t)
+
+
+@pytest.mark.parametrize("mode", ["auto", "ilr"])
+def test_failed_fresh_batch_then_flat_op(mode, monkeypatch):
+    """A fresh batch that fails after the nested merge handed it to the
+    replay (which resets the device result block) must leave the context's
+    replica range table clean: the next batch, one flat Add anchored at a key
+    of that failed batch from another replica, is NotFound (adversarial seed
+    14: ops [0, 200) fail at 192, op 200 anchors at op 185's key)."""
+    monkeypatch.setenv("CRDTM_INCREMENTAL", mode)
+    from adversarial import adversarial
+    from crdtm.tree import pack
+    from oracle.oracle import lib as olib
+    s = pack(adversarial(14, 600, replicas=4, max_depth=3))
+    ot = olib().orc_init(0)
+    et = CRDTree.init(0)
+    for a, b in ((0, 200), (200, 201), (201, 260)):
+        _, rc, oerr = oracle_apply_arrays(sub(s, a, b), b - a, tree=ot)
+        res = et.apply_arrays(sub(s, a, b), b - a)
+        assert (res.code, res.err_index if rc else -1) == (rc, oerr if rc else -1), (a, b)
+        assert engine_summary(et) == oracle_summary(ot), (a, b)
+    olib().orc_free(ot)
