@@ -95,6 +95,7 @@ struct DevResult {
   uint32_t ilr_undo;        // undo entries used
   uint32_t ilr_groups;      // dict groups of the batch
   uint32_t ilr_why;         // conflict reasons (ilr.hip IW_* bits)
+  uint32_t ilr_jobs;        // deferred copies created so far
   // flat claim/check counters, 16 shards one cache line apart (shard k at
   // [32 k]): +0 slots holding an Add, +1 Adds with a timestamp slot, +2 Adds
   // of the own replica, +3 ops that need per-op statuses (empty path, ts 0)
@@ -104,7 +105,7 @@ struct DevResult {
   uint32_t run_maxd;        // flat order: deepest run
   uint32_t run_lhist[64];   // flat order: runs per depth
   long long rep_inline[2 * REP_INLINE];  // replicas table entries collected by a commit (the first REP_INLINE)
-  uint32_t ilr_levels[68];  // host staging: groups per level, private table entries (ilr.hip)
+  uint32_t ilr_levels[136];  // host staging: groups per level, private table entries (ilr.hip)
 };
 
 #define HIP_CHECK(x)                                                                         \

@@ -178,8 +178,9 @@ struct IlrIndex {
   uint64_t hused = 0;          // entries in use
   uint32_t* dhead = nullptr;   // [dcap] first member slot of each dict
   uint32_t* mnext = nullptr;   // [scap] next member of the slot's dict
-  uint32_t* ev = nullptr;      // [3 * scap] per slot: created / deleted / refilled at op (NONE)
+  uint32_t* ev = nullptr;      // [4 * scap] per slot: created / deleted / refilled at op, old children (NONE)
   uint32_t* xmap = nullptr;    // [scap] source slot -> its copy, during one deep copy
+  uint32_t* dsrc = nullptr;    // [dcap] a dict filled by a deferred copy its lane reads back: the source
   uint64_t dcap = 0, scap = 0;
   ~IlrIndex();
 };

@@ -18,12 +18,21 @@
 // Inside a group's dict only that group writes, so the dict is exactly at
 // op i when op i runs.
 //
+// Paths are resolved for all ops of a level in parallel before its lanes run
+// (the lanes then only touch their own dicts). A copy quirk whose copied
+// node has batch activity below it needs the node's children as of the
+// quirk: it becomes a deferred copy, made by the lane that owns those
+// children at the next level when it passes the quirk's op; the lanes of
+// ops landing in the copy run in a second phase of that level. A slot may
+// carry a Delete and a re-fill (either order).
+//
 // What this order cannot decide sends the batch to the re-merge (merge.hip
-// apply_batch_paths; nothing is written): a path slot with two events (a
-// Delete and a re-fill), a group whose ops resolve to different dicts, and a
-// copy quirk whose copied node has batch activity below it (its deep copy
-// must be the children as of the quirk). Any error (the first failing op in
-// batch order is exact: each op only sees earlier ops) rolls the state back
+// apply_batch_paths; nothing is written): a slot with three events, an op
+// landing under a deleted-then-refilled node before its Delete, a deferred
+// copy whose source has no lane or activity two levels down, a lane that is
+// both the source and the target of deferred copies. Any error (the first
+// failing op in batch order is exact: each op only sees earlier ops) rolls
+// the state back
 // through per-group undo logs. Each group takes its Adds' slots from a range
 // reserved for it (a prefix sum over the groups; an Add that does not apply
 // leaves a dead slot in a dict nothing reaches); materialised sentinels,
@@ -40,8 +49,10 @@
 // the slots it creates go to a table of its own (per group, in the arena),
 // published into the shared (dict, key) hash by a separate kernel after the
 // level. During a level the shared hash is read-only.
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 #include "engine.h"
 #include "scan.h"
@@ -56,40 +67,72 @@ IlrIndex::~IlrIndex() {
   if (mnext) hipFree(mnext);
   if (ev) hipFree(ev);
   if (xmap) hipFree(xmap);
+  if (dsrc) hipFree(dsrc);
 }
 
 constexpr uint32_t ILR_TAG = 0x80000000u;  // s_src of this batch: ILR_TAG | op index
 constexpr uint32_t ILR_MAXL = 64;          // deeper paths: the re-merge
-constexpr uint32_t EV_CRE = 0, EV_DEL = 1, EV_CPY = 2;
+constexpr uint32_t EVW = 4;                // event words per slot
+constexpr uint32_t EV_CRE = 0, EV_DEL = 1, EV_CPY = 2, EV_OCH = 3;
 constexpr uint32_t IMPLICIT = 0xFFFFFFFEu;  // a live node's children still the implicit {0: Tombstone}
+constexpr uint32_t ST_CONFLICT = 0xFF;     // (prep: the batch goes to the re-merge)
 constexpr uint32_t LV_PTOT = ILR_MAXL + 1, LV_QTOT = ILR_MAXL + 2, LV_N = ILR_MAXL + 4;
+constexpr uint32_t ILR_JOBS = 4;  // deferred copies one lane makes
 // conflict reasons (DevResult::ilr_why) and overflow reasons (ilr_overflow)
-enum : uint32_t { IW_TWO_EVENTS = 1, IW_TWO_DICTS = 2, IW_COPY_BELOW = 4, IW_REFILL = 8, IW_SHAPE = 16, IW_DEPTH = 32 };
-enum : uint32_t { IO_SLOTS = 1, IO_DICTS = 2, IO_UNDO = 4, IO_PRIV = 8 };
+enum : uint32_t {
+  IW_EVENTS = 1,      // a slot with a third event
+  IW_COPY_BELOW = 2,  // a deferred copy two levels down, or with no lane at its level
+  IW_REFILL = 4,      // an op lands under a deleted-then-refilled node before the Delete
+  IW_CHAIN = 8,       // a lane both source and target of deferred copies (or > ILR_JOBS)
+  IW_DEPTH = 16       // a deep copy deeper than ILR_MAXL
+};
+enum : uint32_t { IO_SLOTS = 1, IO_DICTS = 2, IO_UNDO = 4, IO_PRIV = 8, IO_JOBS = 16 };
 enum : uint32_t { IF_NEXT = 0, IF_SRC = 1, IF_CHILD = 2, IF_FLAGS = 3 };
+enum : uint32_t { GF_SRC = 1, GF_DST = 2 };
 
 // per group of m ops with `adds` Adds: private table entries (at most half
-// used: its nodes and a materialised sentinel), undo triples and their offset
+// used: its nodes and materialised sentinels), undo triples and their offset
 __host__ __device__ inline uint32_t ilr_pcap(uint32_t adds) {
   uint32_t p = 16;
-  while (p < 2 * (adds + 1)) p <<= 1;
+  while (p < 2 * (adds + 2)) p <<= 1;
   return p;
 }
 __host__ __device__ inline uint32_t ilr_ucap(uint32_t m) { return 3 * m + 8; }
 __host__ __device__ inline uint64_t ilr_uoff(uint32_t gbeg, uint32_t g) { return 3ULL * gbeg + 8ULL * g; }
+
+// a level's ops, resolved before its lanes (per sorted position)
+struct IlrPrep {
+  uint8_t* res;    // ST_APPLIED (lands), ST_ALREADY / ST_INVALID (stops on the way), ST_CONFLICT
+  uint32_t* d;     // landing dict, or IMPLICIT
+  uint32_t* own;   // its owner slot (NONE: the root dict)
+  uint32_t* ts;    // the Add's timestamp in d before this level (NONE: absent)
+  uint32_t* kk;    // the anchor / Delete target in d before this level (NONE: absent)
+};
+
+struct IlrJobs {
+  uint32_t* own;   // the copied node (its children as of `at` are copied)
+  uint32_t* dst;   // the copy's dict (children of the re-filled slot)
+  uint32_t* at;    // the quirk's op
+  uint32_t* next;  // per group list
+  uint32_t* head;  // [groups] first job of the group that owns the source
+  uint8_t* same;   // the copy's ops are in the source's group (its lane looks the copy up through xmap)
+  uint8_t* gflag;  // [groups] GF_SRC / GF_DST
+  uint32_t* freel; // jobs whose source no op of the level reaches (one lane copies them first)
+  uint32_t cap;
+};
 
 struct IlrArgs {
   TreeDev T;
   SlotHash H;
   uint32_t* dhead;
   uint32_t* mnext;
-  uint32_t* ev;  // [3 * scap]
+  uint32_t* ev;  // [EVW * scap]
   uint32_t* xmap;
   uint32_t scap;
   uint32_t committed;  // slots of the state before the batch
   uint32_t cap_slots, cap_dicts;
   uint32_t hash_limit;  // entries the shared hash may hold
-  // (depth, key) of every node some op's path crosses (deep-copy conflict check)
+  // (depth, key) of every node some op's path crosses (activity below a node)
   const unsigned long long* tk;
   uint32_t tk_mask;
   long long ts0;
@@ -107,6 +150,11 @@ struct IlrArgs {
   uint32_t* undo;
   uint32_t* ucnt;
   uint32_t grave;  // the dead dict of this batch's unused reserved slots
+  IlrPrep P;
+  IlrJobs J;
+  uint32_t* dsrc;    // [dicts] a copy made by a same-group deferred copy: its source dict (else NONE)
+  uint32_t dnew;     // dicts of the state before the batch
+  unsigned long long* stats;  // (CRDTM_ILR_STATS: per group ops, walk steps, tombstone skips, quirks, marks, ticks)
 };
 
 __device__ __forceinline__ unsigned long long ilr_tk_key(uint32_t depth, long long key) {
@@ -123,14 +171,49 @@ __device__ void ilr_set_insert(unsigned long long* t, uint32_t mask, unsigned lo
     p = (p + 1) & mask;
   }
 }
-__device__ bool ilr_set_has(const unsigned long long* t, uint32_t mask, unsigned long long k) {
+// position of key k in an insert-only set, or NONE
+__device__ uint32_t ilr_set_pos(const unsigned long long* t, uint32_t mask, unsigned long long k) {
   uint32_t p = ilr_hash64(k, mask);
   for (;;) {
     const unsigned long long v = t[p];
-    if (v == k) return true;
-    if (v == 0ULL) return false;
+    if (v == k) return p;
+    if (v == 0ULL) return NONE;
     p = (p + 1) & mask;
   }
+}
+__device__ __forceinline__ bool ilr_set_has(const unsigned long long* t, uint32_t mask, unsigned long long k) {
+  return ilr_set_pos(t, mask, k) != NONE;
+}
+
+// Slot s as of op i, from the events of the shallower levels: 0 = a live node
+// (its children dict in *child, NONE = implicit), 1 = a Tombstone, 2 = not
+// created yet, 3 = undecidable. *hi = min(*hi, the next event after i).
+__device__ __forceinline__ uint32_t ilr_slot_state(const IlrArgs& a, uint32_t s, uint32_t i, uint32_t* child,
+                                                   uint32_t* hi) {
+  const uint32_t* e = a.ev + static_cast<uint64_t>(EVW) * s;
+  const uint32_t cr = e[EV_CRE], de = e[EV_DEL], cp = e[EV_CPY];
+  if (cr != NONE && cr > i) *hi = min(*hi, cr);
+  if (de != NONE && de > i) *hi = min(*hi, de);
+  if (cp != NONE && cp > i) *hi = min(*hi, cp);
+  if (cr != NONE && cr > i) return 2;
+  bool live;
+  uint32_t c = a.T.s_child[s];
+  if (de != NONE && cp != NONE) {
+    if (de < cp) {  // deleted, then re-filled by the copy quirk: its old children before the Delete
+      live = i < de || i > cp;
+      if (i < de) c = e[EV_OCH];
+    } else {  // re-filled, then deleted
+      live = i > cp && i < de;
+    }
+  } else if (de != NONE) {
+    live = i < de;
+  } else if (cp != NONE) {
+    live = i > cp;
+  } else {
+    live = !(a.T.s_flags[s] & F_TOMB);
+  }
+  *child = c;
+  return live ? 0u : 1u;
 }
 
 // One group's lane: the Replayer's literal semantics (merge.hip) on the
@@ -139,6 +222,7 @@ __device__ bool ilr_set_has(const unsigned long long* t, uint32_t mask, unsigned
 struct IlrLane {
   IlrArgs a;
   bool bad;  // overflow or conflict: the batch goes to the re-merge
+  uint32_t depth;  // of the group's dicts (= the level)
   long long* pk;
   uint32_t* pd;
   uint32_t* ps;
@@ -147,7 +231,7 @@ struct IlrLane {
   uint32_t* un;
   uint32_t ucap, ucnt;
 
-  __device__ uint32_t& ev(uint32_t s, uint32_t k) { return a.ev[3ULL * s + k]; }
+  __device__ uint32_t& ev(uint32_t s, uint32_t k) { return a.ev[static_cast<uint64_t>(EVW) * s + k]; }
   __device__ void conflict(uint32_t why) {
     atomicOr(&a.dr->ilr_why, why);
     atomicOr(&a.dr->ilr_conflict, 1u);
@@ -157,14 +241,30 @@ struct IlrLane {
     atomicOr(&a.dr->ilr_overflow, why);
     bad = true;
   }
-  // (dict, key) -> slot: the slots this group created in this level, then
-  // the shared hash (complete for everything before this level)
-  __device__ uint32_t find(uint32_t d, long long k) const {
+  // (dict, key) -> slot among the slots this lane created in this level
+  __device__ uint32_t pfind(uint32_t d, long long k) const {
     for (uint32_t p = slothash_pos(d, k, pmask);; p = (p + 1) & pmask) {
       const uint32_t v = ps[p];
-      if (v == NONE) break;
+      if (v == NONE) return NONE;
       if (pd[p] == d && pk[p] == k) return v;
     }
+  }
+  // a dict this lane filled by a deferred copy: its entries are the source's
+  // as of the copy (through xmap) or this lane's own later slots
+  __device__ uint32_t copy_src(uint32_t d) const { return d >= a.dnew ? a.dsrc[d] : NONE; }
+  __device__ uint32_t via_copy(uint32_t d, uint32_t src, long long k) const {
+    uint32_t s = pfind(src, k);
+    if (s == NONE) s = slothash_find(a.H, src, k);
+    if (s == NONE) return NONE;
+    const uint32_t x = a.xmap[s];
+    return (x < a.scap && a.T.s_dict[x] == d && a.T.s_key[x] == k) ? x : NONE;
+  }
+  // ... then the shared hash (everything before this level, or this phase)
+  __device__ uint32_t find(uint32_t d, long long k) const {
+    uint32_t v = pfind(d, k);
+    if (v != NONE) return v;
+    const uint32_t src = copy_src(d);
+    if (src != NONE && (v = via_copy(d, src, k)) != NONE) return v;
     return slothash_find(a.H, d, k);
   }
   __device__ void log_undo(uint32_t s, uint32_t field, uint32_t old) {
@@ -178,11 +278,14 @@ struct IlrLane {
     un[3 * ucnt + 2] = old;
     ++ucnt;
   }
-  __device__ void set_next(uint32_t s, uint32_t v) { log_undo(s, IF_NEXT, a.T.s_next[s]); a.T.s_next[s] = v; }
+  __device__ void set_next(uint32_t s, uint32_t old, uint32_t v) {
+    log_undo(s, IF_NEXT, old);
+    a.T.s_next[s] = v;
+  }
   __device__ void set_src(uint32_t s, uint32_t v) { log_undo(s, IF_SRC, a.T.s_src[s]); a.T.s_src[s] = v; }
   __device__ void set_child(uint32_t s, uint32_t v) { log_undo(s, IF_CHILD, a.T.s_child[s]); a.T.s_child[s] = v; }
-  __device__ void set_flags(uint32_t s, uint32_t v) {
-    log_undo(s, IF_FLAGS, a.T.s_flags[s]);
+  __device__ void set_flags(uint32_t s, uint32_t old, uint32_t v) {
+    log_undo(s, IF_FLAGS, old);
     a.T.s_flags[s] = static_cast<uint8_t>(v);
   }
 
@@ -195,9 +298,9 @@ struct IlrLane {
     }
     return s;
   }
-  // slot s into dict d (a dict this lane owns); `priv`: this level's ops may
-  // look it up (its nodes and sentinels; deep copies are reached by later
-  // levels only, through the shared hash)
+  // slot s into dict d (a dict this lane writes); `priv`: later ops of this
+  // lane may look it up (its nodes and sentinels; copies are reached by
+  // other lanes only, through the shared hash)
   __device__ void put_slot(uint32_t s, uint32_t d, long long key, uint32_t next, uint32_t src, uint32_t child,
                            uint8_t flags, uint32_t at, bool priv) {
     a.T.s_key[s] = key;
@@ -206,9 +309,11 @@ struct IlrLane {
     a.T.s_src[s] = src;
     a.T.s_child[s] = child;
     a.T.s_flags[s] = flags;
-    ev(s, EV_CRE) = at;
-    ev(s, EV_DEL) = NONE;
-    ev(s, EV_CPY) = NONE;
+    uint32_t* e = a.ev + static_cast<uint64_t>(EVW) * s;
+    e[EV_CRE] = at;
+    e[EV_DEL] = NONE;
+    e[EV_CPY] = NONE;
+    e[EV_OCH] = NONE;
     if (priv) {
       if (2 * (pused + 1) > pmask + 1) {
         overflow(IO_PRIV);
@@ -231,28 +336,34 @@ struct IlrLane {
       return NONE;
     }
     a.dhead[d] = NONE;
+    a.dsrc[d] = NONE;
     a.T.d_owner[d] = owner;
     a.T.d_sent[d] = NONE;
     return d;
   }
-  // the children dict of live node s, created on first use: its sentinel only
-  // (emptyChildren, src/Internal/Node.elm:46-48); the sentinel has always
-  // been there for earlier ops (no creation time)
+  // a sentinel into dict dd (emptyChildren, src/Internal/Node.elm:46-48)
+  __device__ bool put_sentinel(uint32_t dd, uint32_t at, bool priv) {
+    const uint32_t ss = take_slot(false);
+    if (ss == NONE) return false;
+    put_slot(ss, dd, 0, NONE, NONE, NONE, F_TOMB | F_SENT, at, priv);
+    a.T.d_sent[dd] = ss;
+    return !bad;
+  }
+  // the children dict of live node s, created on first use: its sentinel
+  // only; it has always been there for earlier ops (no creation time)
   __device__ uint32_t materialise(uint32_t s) {
     const uint32_t dd = new_dict(s);
-    if (dd == NONE) return NONE;
-    const uint32_t ss = take_slot(false);
-    if (ss == NONE) return NONE;
-    put_slot(ss, dd, 0, NONE, NONE, NONE, F_TOMB | F_SENT, NONE, true);
-    a.T.d_sent[dd] = ss;
+    if (dd == NONE || !put_sentinel(dd, NONE, true)) return NONE;
     set_child(s, dd);
     return bad ? NONE : dd;
   }
-  // Persistent copy of dict `src` and every dict below it into `dst`
-  // (depth-first over an explicit stack; the source subtree holds no slot of
-  // this batch: the conflict check before the quirk guarantees it). xmap
-  // maps each source slot to its copy for the `next` links.
-  __device__ void deep_copy(uint32_t src, uint32_t dst, uint32_t at) {
+  // Persistent copy of dict `src` (at depth d0) and every dict below it into
+  // `dst` (depth-first over an explicit stack). Nothing below a copied
+  // member may have batch activity (its children would be needed as of
+  // `at`, from a later level). xmap maps each source slot to its copy.
+  // With `defer`, a member of `src` itself with activity below gets an empty
+  // children dict and a deferred copy for the next level instead.
+  __device__ void deep_copy(uint32_t src, uint32_t dst, uint32_t at, uint32_t d0, bool defer = false) {
     uint32_t stk_s[ILR_MAXL], stk_d[ILR_MAXL], stk_m[ILR_MAXL];
     int sp = 0;
     stk_s[0] = src;
@@ -276,6 +387,17 @@ struct IlrLane {
       a.xmap[m] = nm;
       if (fl & F_SENT) a.T.d_sent[dd] = nm;
       const uint32_t c = a.T.s_child[m];
+      const bool below = !(fl & F_TOMB) && ilr_set_has(a.tk, a.tk_mask, ilr_tk_key(d0 + sp, a.T.s_key[m]));
+      if (below) {
+        if (!defer || sp != 0) {
+          conflict(IW_COPY_BELOW);
+          return;
+        }
+        const uint32_t nc = new_dict(nm);
+        if (nc == NONE || !add_job(m, nc, at)) return;
+        a.T.s_child[nm] = nc;
+        continue;
+      }
       if (c != NONE && !(fl & F_TOMB)) {  // (a Tombstone has no children, :237-238)
         const uint32_t nc = new_dict(nm);
         if (nc == NONE) return;
@@ -291,38 +413,29 @@ struct IlrLane {
       }
     }
   }
-
-  // The prefix path[b .. b+L-2] as of op i (update, src/Internal/Node.elm:
-  // 138-163): ST_APPLIED with the landing dict d (or IMPLICIT) and its owner
-  // slot, ST_ALREADY (a Tombstone on the way), ST_INVALID (a key not there
-  // yet), or 3 (undecidable: a conflict). hi = the first later op at which a
-  // crossed slot changes state: the answer holds for the ops in (i, hi).
-  __device__ uint32_t resolve(const OpsDev& o, uint32_t b, uint32_t L, uint32_t i, uint32_t& d, uint32_t& own,
-                              uint32_t& hi) {
-    d = 0;
-    own = NONE;
-    hi = NONE;
-    for (uint32_t l = 0; l + 1 < L; ++l) {
-      const long long key = o.path[b + l];
-      if (d == IMPLICIT) return key == 0 ? ST_ALREADY : ST_INVALID;
-      const uint32_t sl = slothash_find(a.H, d, key);  // (shallower dicts: all in the shared hash)
-      if (sl == NONE) return ST_INVALID;
-      const uint32_t cr = ev(sl, EV_CRE), de = ev(sl, EV_DEL), cp = ev(sl, EV_CPY);
-      if (cr != NONE && cr > i) hi = min(hi, cr);
-      if (de != NONE && de > i) hi = min(hi, de);
-      if (cp != NONE && cp > i) hi = min(hi, cp);
-      if (cr != NONE && cr > i) return ST_INVALID;
-      if (de != NONE && cp != NONE) {
-        conflict(IW_TWO_EVENTS);
-        return 3;
-      }
-      const bool live = de != NONE ? i < de : (cp != NONE ? i > cp : !(a.T.s_flags[sl] & F_TOMB));
-      if (!live) return ST_ALREADY;
-      own = sl;
-      const uint32_t c = a.T.s_child[sl];
-      d = c == NONE ? IMPLICIT : c;
+  // a deferred copy of node's children as of op `at`, for the next level
+  __device__ bool add_job(uint32_t node, uint32_t dst, uint32_t at) {
+    const uint32_t j = atomicAdd(&a.dr->ilr_jobs, 1u);
+    if (j >= a.J.cap) {
+      overflow(IO_JOBS);
+      return false;
     }
-    return ST_APPLIED;
+    a.J.own[j] = node;
+    a.J.dst[j] = dst;
+    a.J.at[j] = at;
+    return true;
+  }
+  // run a deferred copy: node's children (a dict of this lane, now exactly as
+  // of op `at`, or one no op of this level reaches) into dict dst; `same`:
+  // this lane's later ops land in the copy (they find it through xmap)
+  __device__ void run_job(uint32_t node, uint32_t dst, uint32_t at, bool same) {
+    const uint32_t c = a.T.s_child[node];
+    if (c == NONE) {
+      put_sentinel(dst, at, same);
+      return;
+    }
+    if (same) a.dsrc[dst] = c;
+    deep_copy(c, dst, at, depth, true);
   }
 };
 
@@ -359,37 +472,150 @@ __global__ void __launch_bounds__(BLOCK) k_ilr_group(OpsDev o, unsigned long lon
 __global__ void __launch_bounds__(BLOCK) k_ilr_gflag(const uint32_t* sk, uint32_t n, uint32_t gbits, uint32_t* flag) {
   GRID_STRIDE(k, n) flag[k] = ((sk[k] >> gbits) != 0 && (k == 0 || sk[k] != sk[k - 1])) ? 1u : 0u;
 }
-// group j = [gbeg[j], gend[j]) of the sorted ops; groups per level; per
-// group its Adds (reserved slots) and private table size
+// group j = [gbeg[j], gend[j]) of the sorted ops; groups and ops per level;
+// per group its Adds (reserved slots) and private table size; group hash
+// slot -> group
 __global__ void __launch_bounds__(BLOCK) k_ilr_glist(const uint32_t* sk, const uint32_t* sv, uint32_t n,
                                                      uint32_t gbits, const uint32_t* flag, const uint32_t* gidx,
                                                      OpsDev o, uint32_t* gbeg, uint32_t* gend, uint32_t* lvcnt,
-                                                     uint32_t* qn, uint32_t* pcap) {
+                                                     uint32_t* lvops, uint32_t* qn, uint32_t* pcap,
+                                                     uint32_t* slot2grp) {
   GRID_STRIDE(k, n) {
     if (!flag[k]) continue;
     const uint32_t j = gidx[k];
     gbeg[j] = k;
-    atomicAdd(&lvcnt[sk[k] >> gbits], 1u);
+    const uint32_t L = sk[k] >> gbits;
+    atomicAdd(&lvcnt[L], 1u);
     uint32_t e = k, adds = 0;
     do {  // (groups are short; the walk stays inside the group)
       adds += o.kind[sv[e]] == CRDTM_ADD;
       ++e;
     } while (e < n && sk[e] == sk[k]);
     gend[j] = e;
+    atomicAdd(&lvops[L], e - k);
     qn[j] = adds;
     pcap[j] = ilr_pcap(adds);
+    slot2grp[sk[k] & ((1u << gbits) - 1u)] = j;
   }
 }
 
-// ---- one level: one lane per group ----
+// ---- a level's paths, in parallel: each op's prefix as of the op
+// (update, src/Internal/Node.elm:138-163) and its landing lookups ----
+__global__ void __launch_bounds__(BLOCK) k_ilr_prep(IlrArgs a, OpsDev o, const uint32_t* vs, uint32_t p0,
+                                                    uint32_t p1) {
+  for (uint32_t k = p0 + blockIdx.x * blockDim.x + threadIdx.x; k < p1; k += gridDim.x * blockDim.x) {
+    const uint32_t i = vs[k];
+    const uint32_t b = o.off[i], L = o.off[i + 1] - b;
+    uint32_t d = 0, own = NONE, res = ST_APPLIED, hi = NONE, last = 0;
+    for (uint32_t l = 0; l + 1 < L; ++l) {
+      const long long key = o.path[b + l];
+      if (d == IMPLICIT) {  // the implicit children hold only the sentinel 0 (a Tombstone)
+        res = key == 0 ? ST_ALREADY : ST_INVALID;
+        break;
+      }
+      const uint32_t sl = slothash_find(a.H, d, key);  // (shallower dicts: all in the shared hash)
+      if (sl == NONE) {
+        res = ST_INVALID;
+        break;
+      }
+      uint32_t c = NONE;
+      const uint32_t sv = ilr_slot_state(a, sl, i, &c, &hi);
+      if (sv == 2) {
+        res = ST_INVALID;
+        break;
+      }
+      if (sv == 1) {
+        res = ST_ALREADY;
+        break;
+      }
+      own = sl;
+      last = l + 1;
+      d = c == NONE ? IMPLICIT : c;
+    }
+    uint32_t pts = NONE, pkk = NONE;
+    if (res == ST_APPLIED && own != NONE && last + 1 == L) {
+      // landing under a deleted-then-refilled node before its Delete: its
+      // old children, which the lanes cannot tell from its new ones
+      const uint32_t* e = a.ev + static_cast<uint64_t>(EVW) * own;
+      if (e[EV_DEL] != NONE && e[EV_CPY] != NONE && i < e[EV_DEL]) {
+        atomicOr(&a.dr->ilr_why, IW_REFILL);
+        atomicOr(&a.dr->ilr_conflict, 1u);
+        res = ST_CONFLICT;
+      }
+    }
+    if (res == ST_APPLIED && d != IMPLICIT) {
+      const long long kk = o.path[b + L - 1];
+      if (o.kind[i] == CRDTM_ADD) pts = slothash_find(a.H, d, o.ts[i]);
+      pkk = slothash_find(a.H, d, kk);
+    }
+    a.P.res[k] = static_cast<uint8_t>(res);
+    a.P.d[k] = d;
+    a.P.own[k] = own;
+    a.P.ts[k] = pts;
+    a.P.kk[k] = pkk;
+  }
+}
+
+// ---- the deferred copies made at level L - 1, to the lanes of level L ----
+__global__ void __launch_bounds__(BLOCK) k_ilr_jobs(IlrArgs a, uint32_t L, const unsigned long long* gk,
+                                                    uint32_t gmask, const uint32_t* slot2grp, const uint32_t* jlo_p,
+                                                    const uint32_t* jhi_p, uint32_t* nfree) {
+  const uint32_t jlo = *jlo_p, jhi = min(*jhi_p, a.J.cap);
+  for (uint32_t j = jlo + blockIdx.x * blockDim.x + threadIdx.x; j < jhi; j += gridDim.x * blockDim.x) {
+    const uint32_t node = a.J.own[j], dst = a.J.dst[j];
+    const uint32_t ps = ilr_set_pos(gk, gmask, ilr_tk_key(L, a.T.s_key[node]));
+    const uint32_t gs = ps == NONE ? NONE : slot2grp[ps];
+    const uint32_t pd = ilr_set_pos(gk, gmask, ilr_tk_key(L, a.T.s_key[a.T.d_owner[dst]]));
+    const uint32_t gd = pd == NONE ? NONE : slot2grp[pd];
+    a.J.same[j] = gd != NONE && gd == gs;
+    if (gd != NONE && gd != gs) atomicOr(reinterpret_cast<uint32_t*>(a.J.gflag) + (gd >> 2), GF_DST << (8 * (gd & 3)));
+    if (gs == NONE) {  // nothing of this level lands in node's children: copied first, by one lane
+      a.J.freel[atomicAdd(nfree, 1u)] = j;
+      continue;
+    }
+    if (gd != gs) atomicOr(reinterpret_cast<uint32_t*>(a.J.gflag) + (gs >> 2), GF_SRC << (8 * (gs & 3)));
+    a.J.next[j] = atomicExch(&a.J.head[gs], j);
+  }
+}
+
+// the level's deferred copies whose source no op of the level reaches, one
+// lane in order (their sources are the state before the level)
+__global__ void __launch_bounds__(64) k_ilr_free(IlrArgs args, uint32_t L, const uint32_t* nfree, uint32_t* empty) {
+  if (threadIdx.x != 0) return;
+  IlrLane R;
+  R.a = args;
+  R.bad = false;
+  R.depth = L;
+  R.pk = nullptr;
+  R.pd = nullptr;
+  R.ps = empty;  // (a table with no entries)
+  R.pmask = 0;
+  R.pused = 0;
+  R.qnext = R.qend = 0;
+  R.un = nullptr;
+  R.ucap = R.ucnt = 0;
+  const uint32_t nf = min(*nfree, args.J.cap);
+  for (uint32_t q = 0; q < nf && !R.bad; ++q) {
+    const uint32_t j = args.J.freel[q];
+    R.run_job(args.J.own[j], args.J.dst[j], args.J.at[j], false);
+  }
+}
+
+// ---- one level, one phase: one lane per group ----
+// phase 1: every group that receives no deferred copy (it makes those it
+// owns); phase 2: the groups landing in deferred copies
 __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const uint32_t* vs, const uint32_t* gbeg,
-                                                  const uint32_t* gend, uint32_t g0, uint8_t* st) {
+                                                  const uint32_t* gend, uint32_t g0, uint32_t L, uint32_t phase,
+                                                  uint8_t* st) {
   if (threadIdx.x != 0) return;
   const uint32_t g = g0 + blockIdx.x;
+  const uint32_t gf = args.J.gflag[g];
+  if ((gf & GF_DST) ? phase != 2 : phase != 1) return;
   const uint32_t kb = gbeg[g], ke = gend[g];
   IlrLane R;
   R.a = args;
   R.bad = false;
+  R.depth = L;
   R.pk = args.pk + args.poff[g];
   R.pd = args.pd + args.poff[g];
   R.ps = args.ps + args.poff[g];
@@ -400,81 +626,119 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
   R.un = args.undo + 3 * ilr_uoff(kb, g);
   R.ucap = ilr_ucap(ke - kb);
   R.ucnt = 0;
+  const bool pre = phase == 1;  // (phase 2: the copies changed the landing dicts after the prep)
+  if ((gf & (GF_SRC | GF_DST)) == (GF_SRC | GF_DST)) R.conflict(IW_CHAIN);
+  // the deferred copies this lane makes, by op
+  uint32_t jat[ILR_JOBS], jown[ILR_JOBS], jdst[ILR_JOBS], nj = 0;
+  bool jsame[ILR_JOBS];
+  for (uint32_t j = (gf & GF_SRC) ? args.J.head[g] : NONE; j != NONE && !R.bad; j = args.J.next[j]) {
+    if (nj == ILR_JOBS) {
+      R.conflict(IW_CHAIN);
+      break;
+    }
+    jat[nj] = args.J.at[j];
+    jown[nj] = args.J.own[j];
+    jdst[nj] = args.J.dst[j];
+    jsame[nj] = args.J.same[j];
+    for (uint32_t q = 0; q < nj; ++q)  // (two copies of one source: xmap holds one)
+      if (jsame[nj] && jown[q] == jown[nj]) R.conflict(IW_CHAIN);
+    ++nj;
+  }
+  auto run_jobs_before = [&](uint32_t i) {
+    for (;;) {
+      uint32_t best = NONE, bj = 0;
+      for (uint32_t q = 0; q < nj; ++q)
+        if (jat[q] < i && jat[q] < best) {
+          best = jat[q];
+          bj = q;
+        }
+      if (best == NONE || R.bad) return;
+      R.run_job(jown[bj], jdst[bj], jat[bj], jsame[bj]);
+      jat[bj] = NONE;
+    }
+  };
   const long long id0 = replica_of(args.ts0);
-  uint32_t app = 0, alr = 0, own = 0, err = NONE;
-  // the resolved prefix, valid for ops before chi with the same path as op cpi
-  uint32_t cpi = NONE, chi = 0, cres = 0, cd = NONE, cown = NONE, gown = NONE;
-  bool owned = false;
-  // the last slots this group created or found in its dict (typing anchors at
-  // its own previous character): key -> slot
+  uint32_t app = 0, alr = 0, own_ok = 0, err = NONE;
+  // the last slots this lane created in dict rdict (typing anchors at its own
+  // previous character): key -> slot
+  uint32_t rdict = NONE;
   long long rk0 = 0, rk1 = 0, rk2 = 0, rk3 = 0;
   uint32_t rs0 = NONE, rs1 = NONE, rs2 = NONE, rs3 = NONE;
   auto recent = [&](long long k) -> uint32_t {
     return (rs0 != NONE && rk0 == k) ? rs0 : (rs1 != NONE && rk1 == k) ? rs1 : (rs2 != NONE && rk2 == k) ? rs2
            : (rs3 != NONE && rk3 == k) ? rs3 : NONE;
   };
-  auto remember = [&](long long k, uint32_t v) {
-    rk3 = rk2; rs3 = rs2;
-    rk2 = rk1; rs2 = rs1;
-    rk1 = rk0; rs1 = rs0;
-    rk0 = k; rs0 = v;
-  };
+  unsigned long long n_walk = 0, n_skip = 0, n_quirk = 0, n_mark = 0;
+  const unsigned long long t0 = wall_clock64();
   for (uint32_t k = kb; k < ke && !R.bad; ++k) {
     const uint32_t i = vs[k];
-    const uint32_t b = o.off[i], L = o.off[i + 1] - b;
+    if (nj) run_jobs_before(i);
+    if (R.bad) break;
     const uint8_t kind = o.kind[i];
+    const uint32_t res = args.P.res[k];
     uint8_t s = ST_APPLIED;
-    // ---- the prefix as of op i (path[L-2] is the group's owner key) ----
-    bool hit = cpi != NONE && i < chi;
-    if (hit) {
-      const uint32_t cb = o.off[cpi];
-      for (uint32_t l = 0; hit && l + 2 < L; ++l) hit = o.path[b + l] == o.path[cb + l];
+    if (res == ST_CONFLICT) {
+      R.bad = true;
+      break;
     }
-    if (!hit) {
-      cres = R.resolve(o, b, L, i, cd, cown, chi);
-      cpi = i;
-      if (cres == 3) break;
-    }
-    if (cres != ST_APPLIED) {
-      s = static_cast<uint8_t>(cres);
+    if (res != ST_APPLIED) {
+      s = static_cast<uint8_t>(res);
     } else {
-      if (owned && cown != gown) {  // (one owner key, two nodes: two dicts in one group)
-        R.conflict(IW_TWO_DICTS);
-        break;
-      }
-      owned = true;
-      gown = cown;
-      const long long kk = o.path[b + L - 1];
+      const uint32_t b = o.off[i], L1 = o.off[i + 1] - b;
+      const long long kk = o.path[b + L1 - 1];
       const long long ts = o.ts[i];
-      uint32_t d = cd;
+      uint32_t d = args.P.d[k], ownr = args.P.own[k];
+      bool usepre = pre && (d == IMPLICIT || R.copy_src(d) == NONE);
+      if (d == IMPLICIT) {  // (materialised by this lane since the prep?)
+        const uint32_t c = args.T.s_child[ownr];
+        if (c != NONE) {
+          d = c;
+          usepre = false;
+        }
+      }
       if (d == IMPLICIT) {
         // the empty children {0: Tombstone}: only an Add after the sentinel
         // changes it (then the dict is created); ts 0 or Delete 0: AlreadyApplied
         if (kind == CRDTM_ADD && ts != 0 && kk == 0) {
-          d = R.materialise(cown);
+          d = R.materialise(ownr);
           if (d == NONE) break;
-          cd = d;
+          usepre = false;
         } else {
           s = (kk == 0 || (kind == CRDTM_ADD && ts == 0)) ? ST_ALREADY : ST_NOTFOUND;
         }
       }
       if (s == ST_APPLIED) {
+        if (d != rdict) {
+          rdict = d;
+          rs0 = rs1 = rs2 = rs3 = NONE;
+        }
+        auto lookup = [&](long long key, uint32_t prek) -> uint32_t {
+          const uint32_t v = R.pfind(d, key);
+          if (v != NONE) return v;
+          return usepre ? prek : slothash_find(args.H, d, key);
+        };
         if (kind == CRDTM_DELETE) {  // deleteHelp (:112-122)
           uint32_t t = recent(kk);
-          if (t == NONE) t = R.find(d, kk);
+          if (t == NONE) t = lookup(kk, args.P.kk[k]);
           if (t == NONE) {
             s = ST_NOTFOUND;
-          } else if (args.T.s_flags[t] & F_TOMB) {
-            s = ST_ALREADY;
           } else {
-            R.set_flags(t, args.T.s_flags[t] | F_TOMB);
-            if (R.ev(t, EV_DEL) == NONE) R.ev(t, EV_DEL) = i;  // children drop at the commit
+            const uint8_t tf = args.T.s_flags[t];
+            if (tf & F_TOMB) {
+              s = ST_ALREADY;
+            } else if (R.ev(t, EV_DEL) != NONE) {  // (deleted, re-filled, deleted: a third event)
+              R.conflict(IW_EVENTS);
+              break;
+            } else {
+              R.set_flags(t, tf, tf | F_TOMB);
+              R.ev(t, EV_DEL) = i;  // children drop at the commit
+            }
           }
-        } else if (R.find(d, ts) != NONE) {  // addAfterHelp (:56-90)
+        } else if (lookup(ts, args.P.ts[k]) != NONE) {  // addAfterHelp (:56-90)
           s = ST_ALREADY;
         } else {
           uint32_t found = recent(kk);
-          if (found == NONE) found = R.find(d, kk);
+          if (found == NONE) found = lookup(kk, args.P.kk[k]);
           if (found == NONE) {
             s = ST_NOTFOUND;
           } else {
@@ -482,9 +746,13 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
             uint32_t node = found, ls = found, rn;
             for (;;) {
               rn = args.T.s_next[node];
+              ++n_walk;
               if (rn == NONE) break;
               uint32_t live = rn;
-              while (live != NONE && (args.T.s_flags[live] & F_TOMB)) live = args.T.s_next[live];
+              while (live != NONE && (args.T.s_flags[live] & F_TOMB)) {
+                live = args.T.s_next[live];
+                ++n_skip;
+              }
               if (live == NONE) break;
               if (ts > args.T.s_key[rn]) break;
               ls = rn;
@@ -497,43 +765,56 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
             R.put_slot(x, d, ts, rn, ILR_TAG | i, NONE, (lsf & F_ORPHAN) ? F_ORPHAN : 0, i, true);
             if (R.bad) break;
             if (ls == node) {
-              R.set_next(node, x);
+              R.set_next(node, rn, x);
             } else {
               // the copy quirk: slot ls := copy of node with
-              // next = ts; the entries after it up to node drop off the
-              // chain. Its children are node's as of op i: undecidable here
-              // when the batch reaches below node (a later level, which may
-              // also create node's children dict). A slot the batch deleted
-              // and now re-fills would have three states for later levels.
-              if (ilr_set_has(args.tk, args.tk_mask, ilr_tk_key(L, args.T.s_key[node]))) {
-                R.conflict(IW_COPY_BELOW);
+              // next = ts; the entries after it up to node drop off the chain
+              if (R.ev(ls, EV_CPY) != NONE) {  // (re-filled, deleted, re-filled: a third event)
+                R.conflict(IW_EVENTS);
                 break;
               }
-              if (R.ev(ls, EV_CPY) != NONE || R.ev(ls, EV_DEL) != NONE) {
-                R.conflict(IW_REFILL);
-                break;
-              }
+              ++n_quirk;
               if (!(lsf & F_ORPHAN)) {
                 for (uint32_t q = args.T.s_next[ls]; q != NONE; q = args.T.s_next[q]) {
-                  R.set_flags(q, args.T.s_flags[q] | F_ORPHAN);
+                  const uint8_t qf = args.T.s_flags[q];
+                  ++n_mark;
+                  R.set_flags(q, qf, qf | F_ORPHAN);
                   if (q == node) break;
                 }
               }
               const uint32_t c = args.T.s_child[node];
+              if (R.ev(ls, EV_DEL) != NONE) R.ev(ls, EV_OCH) = args.T.s_child[ls];  // (its children before the Delete)
               R.set_src(ls, args.T.s_src[node]);
-              R.set_flags(ls, (args.T.s_flags[node] & ~F_ORPHAN) | (lsf & F_ORPHAN));
-              R.set_next(ls, x);
+              R.set_flags(ls, lsf, (args.T.s_flags[node] & ~F_ORPHAN) | (lsf & F_ORPHAN));
+              R.set_next(ls, args.T.s_next[ls], x);
               R.ev(ls, EV_CPY) = i;
+              // its children are node's as of op i: now, unless the batch
+              // reaches below node — then the lane owning node's children
+              // makes the copy at the next level when it passes op i
               uint32_t nc = NONE;
-              if (c != NONE) {
+              if (ilr_set_has(args.tk, args.tk_mask, ilr_tk_key(L, args.T.s_key[node]))) {
                 nc = R.new_dict(ls);
                 if (nc == NONE) break;
-                R.deep_copy(c, nc, i);
+                const uint32_t j = atomicAdd(&args.dr->ilr_jobs, 1u);
+                if (j >= args.J.cap) {
+                  R.overflow(IO_JOBS);
+                  break;
+                }
+                args.J.own[j] = node;
+                args.J.dst[j] = nc;
+                args.J.at[j] = i;
+              } else if (c != NONE) {
+                nc = R.new_dict(ls);
+                if (nc == NONE) break;
+                R.deep_copy(c, nc, i, L + 1);
                 if (R.bad) break;
               }
               R.set_child(ls, nc);
             }
-            remember(ts, x);
+            rk3 = rk2; rs3 = rs2;
+            rk2 = rk1; rs2 = rs1;
+            rk1 = rk0; rs1 = rs0;
+            rk0 = ts; rs0 = x;
           }
         }
       }
@@ -544,7 +825,18 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
     else if (s == ST_ALREADY) ++alr;
     else err = min(err, i);
     // incrementTimestamp (src/CRDTree.elm:337-343): Ok Adds of the own replica
-    if ((s == ST_APPLIED || s == ST_ALREADY) && kind == CRDTM_ADD && replica_of(o.ts[i]) == id0) ++own;
+    if ((s == ST_APPLIED || s == ST_ALREADY) && kind == CRDTM_ADD && replica_of(o.ts[i]) == id0) ++own_ok;
+  }
+  if (nj && !R.bad) run_jobs_before(NONE);
+  if (args.stats) {
+    unsigned long long* q = args.stats + 8ULL * g;
+    q[0] = ke - kb;
+    q[1] = n_walk;
+    q[2] = n_skip;
+    q[3] = n_quirk;
+    q[4] = n_mark;
+    q[5] = wall_clock64() - t0;
+    q[6] = L;
   }
   args.ucnt[g] = R.ucnt;
   if (!R.bad) {
@@ -556,34 +848,41 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
       args.T.s_src[x] = NONE;
       args.T.s_child[x] = NONE;
       args.T.s_flags[x] = F_TOMB | F_ORPHAN;
-      R.ev(x, EV_CRE) = NONE;
-      R.ev(x, EV_DEL) = NONE;
-      R.ev(x, EV_CPY) = NONE;
+      for (uint32_t w = 0; w < EVW; ++w) R.ev(x, w) = NONE;
       args.mnext[x] = NONE;
     }
   }
   if (app) atomicAdd(&args.dr->n_applied, app);
   if (alr) atomicAdd(&args.dr->n_already, alr);
-  if (own) atomicAdd(&args.dr->own_ok_adds, own);
+  if (own_ok) atomicAdd(&args.dr->own_ok_adds, own_ok);
   if (err != NONE) atomicMin(&args.dr->err_index, err);
 }
 
-// the slot counter before a level
-__global__ void k_ilr_mark(const DevResult* d, uint32_t* mark) { *mark = d->ilr_slots; }
-// after a level: its slots into the shared hash — the groups' reserved
-// ranges and what the counter gave (skipped once the batch overflowed or
-// conflicted: it is rolled back and the index rebuilt)
-__global__ void __launch_bounds__(BLOCK) k_ilr_publish(TreeDev T, SlotHash H, const uint32_t* qoff, uint32_t g0,
-                                                       uint32_t g1, uint32_t committed, const uint32_t* mark,
+// counters before a phase: slots (publish start) and deferred copies
+__global__ void k_ilr_mark(const DevResult* d, uint32_t* slots, uint32_t* jobs) {
+  if (slots) *slots = d->ilr_slots;
+  if (jobs) *jobs = d->ilr_jobs;
+}
+// after a phase: its slots into the shared hash — the reserved ranges of
+// its groups (one block each) and what the counter gave since the mark
+// (skipped once the batch overflowed or conflicted: it is rolled back and
+// the index rebuilt)
+__global__ void __launch_bounds__(BLOCK) k_ilr_publish(TreeDev T, SlotHash H, const uint32_t* qoff, const uint32_t* qn,
+                                                       const uint8_t* gflag, uint32_t g0, uint32_t cnt,
+                                                       uint32_t phase, uint32_t committed, const uint32_t* mark,
                                                        const DevResult* d, uint32_t cap) {
   if (d->ilr_overflow || d->ilr_conflict) return;
-  const uint32_t a0 = committed + qoff[g0], a1 = committed + qoff[g1];
-  const uint32_t b0 = *mark, b1 = min(d->ilr_slots, cap);
-  const uint32_t na = a1 - a0, nb = b1 > b0 ? b1 - b0 : 0u;
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < na + nb; j += gridDim.x * blockDim.x) {
-    const uint32_t s = j < na ? a0 + j : b0 + (j - na);
-    slothash_put_par(H, T.s_dict[s], T.s_key[s], s);
+  if (blockIdx.x < cnt) {
+    const uint32_t g = g0 + blockIdx.x;
+    if ((gflag[g] & GF_DST) ? phase != 2 : phase != 1) return;
+    const uint32_t a0 = committed + qoff[g];
+    for (uint32_t j = threadIdx.x; j < qn[g]; j += blockDim.x)
+      slothash_put_par(H, T.s_dict[a0 + j], T.s_key[a0 + j], a0 + j);
+    return;
   }
+  const uint32_t b0 = *mark, b1 = min(d->ilr_slots, cap);
+  for (uint32_t s = b0 + (blockIdx.x - cnt) * blockDim.x + threadIdx.x; s < b1; s += (gridDim.x - cnt) * blockDim.x)
+    slothash_put_par(H, T.s_dict[s], T.s_key[s], s);
 }
 
 // undo of one level's groups, each newest first (launched deepest level first:
@@ -605,13 +904,13 @@ __global__ void __launch_bounds__(BLOCK) k_ilr_rollback(TreeDev T, const uint32_
 
 // commit, for the slots the batch touched — the new ones [lo, hi) and the
 // state's slots in the undo logs: sources tagged with an op index take its
-// log index; a node the batch deleted drops its children (children
+// log index; a node the batch left deleted drops its children (children
 // Tombstone = Dict.empty, src/Internal/Node.elm:237-238)
 __device__ __forceinline__ void ilr_fix_slot(TreeDev& T, uint32_t s, const uint32_t* logidx, uint32_t log_base,
                                              const uint32_t* ev) {
   const uint32_t src = T.s_src[s];
   if (src != NONE && (src & ILR_TAG)) T.s_src[s] = log_base + logidx[src & ~ILR_TAG];
-  if (ev[3ULL * s + EV_DEL] != NONE) T.s_child[s] = NONE;
+  if (ev[static_cast<uint64_t>(EVW) * s + EV_DEL] != NONE && (T.s_flags[s] & F_TOMB)) T.s_child[s] = NONE;
 }
 __global__ void __launch_bounds__(BLOCK) k_ilr_fix(TreeDev T, uint32_t lo, uint32_t hi, const uint32_t* undo,
                                                    uint32_t nu, const uint32_t* logidx, uint32_t log_base,
@@ -621,8 +920,8 @@ __global__ void __launch_bounds__(BLOCK) k_ilr_fix(TreeDev T, uint32_t lo, uint3
     if (j < nn) {
       ilr_fix_slot(T, lo + j, logidx, log_base, ev);
     } else {
-      const uint32_t s = undo[3ULL * (j - nn)];
-      if (s != NONE && (undo[3ULL * (j - nn) + 1] == IF_SRC || undo[3ULL * (j - nn) + 1] == IF_FLAGS))
+      const uint32_t s = undo[3ULL * (j - nn)], f = undo[3ULL * (j - nn) + 1];
+      if (s != NONE && (f == IF_SRC || f == IF_FLAGS))
         ilr_fix_slot(T, s, logidx, log_base, ev);  // (the entries of one slot: same result, any order)
     }
   }
@@ -634,22 +933,22 @@ __global__ void __launch_bounds__(BLOCK) k_ilr_ev_reset(uint32_t lo, uint32_t hi
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nn + nu; j += gridDim.x * blockDim.x) {
     const uint32_t s = j < nn ? lo + j : undo[3ULL * (j - nn)];
     if (s == NONE) continue;
-    ev[3ULL * s] = NONE;
-    ev[3ULL * s + 1] = NONE;
-    ev[3ULL * s + 2] = NONE;
+    for (uint32_t w = 0; w < EVW; ++w) ev[static_cast<uint64_t>(EVW) * s + w] = NONE;
   }
 }
 
-__global__ void k_ilr_counters(DevResult* d, TreeDev T, uint32_t* dhead, uint32_t committed, const uint32_t* qtot,
-                               uint32_t grave) {
+__global__ void k_ilr_counters(DevResult* d, TreeDev T, uint32_t* dhead, uint32_t* dsrc, uint32_t committed,
+                               const uint32_t* qtot, uint32_t grave) {
   d->ilr_slots = committed + *qtot;
   d->ilr_dicts = grave + 1;
   d->ilr_conflict = 0;
   d->ilr_overflow = 0;
   d->ilr_why = 0;
-  T.d_owner[grave] = NONE;  // (no owner: never alive, src/Internal/Node.elm has no such dict)
+  d->ilr_jobs = 0;
+  T.d_owner[grave] = NONE;  // (no owner: never alive)
   T.d_sent[grave] = NONE;
   dhead[grave] = NONE;
+  dsrc[grave] = NONE;
 }
 
 static uint32_t pow2_ge(uint64_t x) {
@@ -691,8 +990,11 @@ static int ilr_build(crdtm_tree* t) {
   if (X.dcap < t->cap.dicts) {
     HIP_CHECK(hipStreamSynchronize(s));
     if (X.dhead) hipFree(X.dhead);
+    if (X.dsrc) hipFree(X.dsrc);
     X.dhead = nullptr;
+    X.dsrc = nullptr;
     HIP_CHECK(hipMalloc(&X.dhead, t->cap.dicts * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&X.dsrc, t->cap.dicts * sizeof(uint32_t)));
     X.dcap = t->cap.dicts;
   }
   if (X.scap < t->cap.slots) {
@@ -704,13 +1006,13 @@ static int ilr_build(crdtm_tree* t) {
     X.ev = nullptr;
     X.xmap = nullptr;
     HIP_CHECK(hipMalloc(&X.mnext, t->cap.slots * sizeof(uint32_t)));
-    HIP_CHECK(hipMalloc(&X.ev, 3 * t->cap.slots * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&X.ev, EVW * t->cap.slots * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&X.xmap, t->cap.slots * sizeof(uint32_t)));
     X.scap = t->cap.slots;
   }
   HIP_CHECK(hipMemsetAsync(X.H.slot, 0xFF, X.hcap * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(X.dhead, 0xFF, X.dcap * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(X.ev, 0xFF, 3 * X.scap * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(X.ev, 0xFF, EVW * X.scap * sizeof(uint32_t), s));
   LAUNCH(k_replay_index, dim3(grid_for(t->n_slots)), dim3(BLOCK), 0, s, t->d, static_cast<uint32_t>(t->n_slots), X.H,
          X.dhead, X.mnext);
   X.hused = t->n_slots;
@@ -760,6 +1062,7 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   uint32_t gbits = 0;
   while ((1u << gbits) < gsz) ++gbits;
   unsigned long long* gk = ws.alloc<unsigned long long>(gsz);
+  uint32_t* slot2grp = ws.alloc<uint32_t>(gsz);
   const uint32_t tsz = pow2_ge(2ULL * o.n_path + 16);
   unsigned long long* tk = ws.alloc<unsigned long long>(tsz);
   uint32_t* sk[2] = {ws.alloc<uint32_t>(n + 1), ws.alloc<uint32_t>(n + 1)};
@@ -775,10 +1078,11 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   uint32_t* pcap = ws.alloc<uint32_t>(n + 2);
   uint32_t* poff = ws.alloc<uint32_t>(n + 2);
   uint32_t* ucnt = ws.alloc<uint32_t>(n + 1);
-  uint32_t* lvcnt = ws.alloc<uint32_t>(LV_N);
+  uint32_t* lvcnt = ws.alloc<uint32_t>(2 * LV_N);  // groups per level, totals; then ops per level
   HIP_CHECK(hipMemsetAsync(gk, 0, gsz * sizeof(unsigned long long), s));
+  HIP_CHECK(hipMemsetAsync(slot2grp, 0xFF, gsz * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(tk, 0, tsz * sizeof(unsigned long long), s));
-  HIP_CHECK(hipMemsetAsync(lvcnt, 0, LV_N * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(lvcnt, 0, 2 * LV_N * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(qn, 0, (n + 2) * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(pcap, 0, (n + 2) * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(nd), n, 1, s));
@@ -787,30 +1091,56 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   if ((r = radix_sort_pairs(sk[0], sv[0], sk[1], sv[1], nd, n, gbits + 7, ws, s, &ks, &vs))) return r;
   LAUNCH(k_ilr_gflag, dim3(grid_for(n)), dim3(BLOCK), 0, s, ks, n, gbits, flag);
   if ((r = scan_excl_u32(flag, gidx, n, &dr->ilr_groups, ws, s))) return r;
-  LAUNCH(k_ilr_glist, dim3(grid_for(n)), dim3(BLOCK), 0, s, ks, vs, n, gbits, flag, gidx, o, gbeg, gend, lvcnt, qn,
-         pcap);
+  LAUNCH(k_ilr_glist, dim3(grid_for(n)), dim3(BLOCK), 0, s, ks, vs, n, gbits, flag, gidx, o, gbeg, gend, lvcnt,
+         lvcnt + LV_N, qn, pcap, slot2grp);
   // reserved slot ranges and private tables: offsets and totals (in lvcnt)
   if ((r = scan_excl_u32(qn, qoff, n + 1, lvcnt + LV_QTOT, ws, s))) return r;
   if ((r = scan_excl_u32(pcap, poff, n + 1, lvcnt + LV_PTOT, ws, s))) return r;
   const uint32_t grave = static_cast<uint32_t>(t->n_dicts);
-  LAUNCH(k_ilr_counters, dim3(1), dim3(1), 0, s, dr, t->d, X->dhead, static_cast<uint32_t>(t->n_slots),
+  LAUNCH(k_ilr_counters, dim3(1), dim3(1), 0, s, dr, t->d, X->dhead, X->dsrc, static_cast<uint32_t>(t->n_slots),
          lvcnt + LV_QTOT, grave);
+  static_assert(sizeof(DevResult::ilr_levels) >= 2 * LV_N * sizeof(uint32_t), "staging room");
   uint32_t* hl = c->hres->ilr_levels;  // (pinned)
-  HIP_CHECK(hipMemcpyAsync(hl, lvcnt, LV_N * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(hl, lvcnt, 2 * LV_N * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   if (int rw = stream_wait(s)) return rw;
-  uint32_t lv[LV_N];
+  uint32_t lv[2 * LV_N];
   memcpy(lv, hl, sizeof(lv));
-  uint32_t G = 0;
-  for (uint32_t L = 1; L <= ILR_MAXL; ++L) G += lv[L];
+  uint32_t G = 0, nops = 0;
+  for (uint32_t L = 1; L <= ILR_MAXL; ++L) {
+    G += lv[L];
+    nops += lv[LV_N + L];
+  }
   const uint32_t ptot = lv[LV_PTOT];
   long long* pk = ws.alloc<long long>(ptot);
   uint32_t* pd = ws.alloc<uint32_t>(ptot);
   uint32_t* ps = ws.alloc<uint32_t>(ptot);
   const uint64_t nu = 3ULL * n + 8ULL * G + 8;  // undo triples (ilr_uoff layout)
   uint32_t* undo = ws.alloc<uint32_t>(3 * nu);
-  uint32_t* marks = ws.alloc<uint32_t>(ILR_MAXL + 2);
+  uint32_t* marks = ws.alloc<uint32_t>(4 * (ILR_MAXL + 2));
+  const uint32_t jcap = n / 2 + 64;
+  IlrJobs J;
+  J.own = ws.alloc<uint32_t>(jcap);
+  J.dst = ws.alloc<uint32_t>(jcap);
+  J.at = ws.alloc<uint32_t>(jcap);
+  J.next = ws.alloc<uint32_t>(jcap);
+  J.head = ws.alloc<uint32_t>(G + 1);
+  J.same = ws.alloc<uint8_t>(jcap);
+  J.gflag = ws.alloc<uint8_t>(G + 4);
+  J.freel = ws.alloc<uint32_t>(jcap);
+  J.cap = jcap;
+  uint32_t* empty = ws.alloc<uint32_t>(16);
+  IlrPrep P;
+  P.res = ws.alloc<uint8_t>(n + 1);
+  P.d = ws.alloc<uint32_t>(n + 1);
+  P.own = ws.alloc<uint32_t>(n + 1);
+  P.ts = ws.alloc<uint32_t>(n + 1);
+  P.kk = ws.alloc<uint32_t>(n + 1);
   HIP_CHECK(hipMemsetAsync(ps, 0xFF, static_cast<size_t>(ptot) * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(undo, 0xFF, 3 * nu * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(marks, 0, 4 * (ILR_MAXL + 2) * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(J.head, 0xFF, (G + 1) * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(J.gflag, 0, G + 4, s));
+  HIP_CHECK(hipMemsetAsync(empty, 0xFF, 16 * sizeof(uint32_t), s));
   // ---- the levels ----
   IlrArgs a;
   a.T = t->d;
@@ -838,18 +1168,46 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   a.undo = undo;
   a.ucnt = ucnt;
   a.grave = grave;
-  uint32_t g0 = 0, levels = 0;
+  a.P = P;
+  a.J = J;
+  a.dsrc = X->dsrc;
+  a.dnew = grave;
+  static const bool want_stats = getenv("CRDTM_ILR_STATS") != nullptr;
+  a.stats = nullptr;
+  if (want_stats) {
+    a.stats = ws.alloc<unsigned long long>(8ULL * (G + 1));
+    HIP_CHECK(hipMemsetAsync(a.stats, 0, 8ULL * (G + 1) * sizeof(unsigned long long), s));
+  }
+  uint32_t g0 = 0, levels = 0, p0 = n - nops;  // (empty paths sort first)
   uint32_t lv_g0[ILR_MAXL + 2] = {};
+  // marks: [4 L] slots before phase 1 (and the free copies), [4 L + 1] before
+  // phase 2, [4 L + 2] jobs after level L, [4 L + 3] free copies of level L
   for (uint32_t L = 1; L <= maxlen; ++L) {
-    const uint32_t cnt = lv[L];
+    const uint32_t cnt = lv[L], m = lv[LV_N + L];
     lv_g0[L] = g0;
-    if (!cnt) continue;
-    LAUNCH(k_ilr_mark, dim3(1), dim3(1), 0, s, dr, marks + L);
-    LAUNCH(k_ilr_level, dim3(cnt), dim3(64), 0, s, a, o, vs, gbeg, gend, g0, st);
-    LAUNCH(k_ilr_publish, dim3(256), dim3(BLOCK), 0, s, a.T, a.H, qoff, g0, g0 + cnt, a.committed, marks + L, dr,
-           a.cap_slots);
+    uint32_t* mk = marks + 4 * L;
+    LAUNCH(k_ilr_mark, dim3(1), dim3(1), 0, s, dr, mk, nullptr);
+    if (L > 1) {
+      LAUNCH(k_ilr_jobs, dim3(16), dim3(BLOCK), 0, s, a, L, gk, gsz - 1, slot2grp, marks + 4 * (L - 1) - 2,
+             marks + 4 * (L - 1) + 2, mk + 3);
+      LAUNCH(k_ilr_free, dim3(1), dim3(64), 0, s, a, L, mk + 3, empty);
+    }
+    if (cnt) {
+      LAUNCH(k_ilr_prep, dim3(grid_for(m, BLOCK, 1024)), dim3(BLOCK), 0, s, a, o, vs, p0, p0 + m);
+      for (uint32_t ph = 1; ph <= 2; ++ph) {
+        if (ph == 2) LAUNCH(k_ilr_mark, dim3(1), dim3(1), 0, s, dr, mk + 1, nullptr);
+        LAUNCH(k_ilr_level, dim3(cnt), dim3(64), 0, s, a, o, vs, gbeg, gend, g0, L, ph, st);
+        LAUNCH(k_ilr_publish, dim3(cnt + 64), dim3(BLOCK), 0, s, a.T, a.H, qoff, qn, J.gflag, g0, cnt, ph,
+               a.committed, mk + ph - 1, dr, a.cap_slots);
+      }
+      ++levels;
+    } else {  // (only free copies: their slots into the shared hash)
+      LAUNCH(k_ilr_publish, dim3(64), dim3(BLOCK), 0, s, a.T, a.H, qoff, qn, J.gflag, g0, 0u, 1u, a.committed, mk,
+             dr, a.cap_slots);
+    }
+    LAUNCH(k_ilr_mark, dim3(1), dim3(1), 0, s, dr, nullptr, mk + 2);
     g0 += cnt;
-    ++levels;
+    p0 += m;
   }
   if ((r = sync_read(c))) return r;
   const DevResult h = *c->hres;
@@ -857,10 +1215,30 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   const bool drift = replica_of(new_ts) != replica_of(t->timestamp);
   static const bool debug = getenv("CRDTM_ILR_DEBUG") != nullptr;
   if (debug)
-    fprintf(stderr, "ilr: n=%u groups=%u levels=%u conflict=%u why=%#x overflow=%#x drift=%d err=%d slots+%u\n", n, G,
-            levels, h.ilr_conflict, h.ilr_why, h.ilr_overflow, drift ? 1 : 0,
+    fprintf(stderr,
+            "ilr: n=%u groups=%u levels=%u jobs=%u conflict=%u why=%#x overflow=%#x drift=%d err=%d slots+%u\n", n,
+            G, levels, h.ilr_jobs, h.ilr_conflict, h.ilr_why, h.ilr_overflow, drift ? 1 : 0,
             h.err_index == NONE ? -1 : static_cast<int>(h.err_index),
             h.ilr_slots - static_cast<uint32_t>(t->n_slots));
+  if (a.stats) {  // the slowest groups: ops, walk steps, tombstone skips, quirks, orphan marks, us
+    std::vector<unsigned long long> hs(8ULL * G);
+    HIP_CHECK(hipMemcpy(hs.data(), a.stats, hs.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> ord(G);
+    for (uint32_t g = 0; g < G; ++g) ord[g] = g;
+    std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return hs[8 * x + 5] > hs[8 * y + 5]; });
+    unsigned long long tw = 0, ts = 0, to = 0;
+    for (uint32_t g = 0; g < G; ++g) {
+      tw += hs[8 * g + 1];
+      ts += hs[8 * g + 2];
+      to += hs[8 * g];
+    }
+    fprintf(stderr, "ilr stats: ops %llu walk %llu skip %llu\n", to, tw, ts);
+    for (uint32_t q = 0; q < std::min<uint32_t>(G, 6); ++q) {
+      const unsigned long long* v = &hs[8 * ord[q]];
+      fprintf(stderr, "  L%llu ops %llu walk %llu skip %llu quirk %llu mark %llu  %.1f us\n", v[6], v[0], v[1], v[2],
+              v[3], v[4], v[5] / 100.0);
+    }
+  }
   if (h.ilr_conflict || h.ilr_overflow || drift || h.err_index != NONE) {
     for (uint32_t L = maxlen; L >= 1; --L)
       if (lv[L])
