@@ -181,6 +181,7 @@ struct IlrIndex {
   uint32_t* ev = nullptr;      // [4 * scap] per slot: created / deleted / refilled at op, old children (NONE)
   uint32_t* xmap = nullptr;    // [scap] source slot -> its copy, during one deep copy
   uint32_t* dsrc = nullptr;    // [dcap] a dict filled by a deferred copy its lane reads back: the source
+  uint4* rec = nullptr;        // [scap] per slot {next, flags, key lo, key hi}: one load per findInsertion step
   uint64_t dcap = 0, scap = 0;
   ~IlrIndex();
 };

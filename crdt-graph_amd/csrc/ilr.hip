@@ -68,6 +68,7 @@ IlrIndex::~IlrIndex() {
   if (ev) hipFree(ev);
   if (xmap) hipFree(xmap);
   if (dsrc) hipFree(dsrc);
+  if (rec) hipFree(rec);
 }
 
 constexpr uint32_t ILR_TAG = 0x80000000u;  // s_src of this batch: ILR_TAG | op index
@@ -78,6 +79,7 @@ constexpr uint32_t IMPLICIT = 0xFFFFFFFEu;  // a live node's children still the 
 constexpr uint32_t ST_CONFLICT = 0xFF;     // (prep: the batch goes to the re-merge)
 constexpr uint32_t LV_PTOT = ILR_MAXL + 1, LV_QTOT = ILR_MAXL + 2, LV_N = ILR_MAXL + 4;
 constexpr uint32_t ILR_JOBS = 4;  // deferred copies one lane makes
+
 // conflict reasons (DevResult::ilr_why) and overflow reasons (ilr_overflow)
 enum : uint32_t {
   IW_EVENTS = 1,      // a slot with a third event
@@ -128,6 +130,7 @@ struct IlrArgs {
   uint32_t* mnext;
   uint32_t* ev;  // [EVW * scap]
   uint32_t* xmap;
+  uint4* rec;    // [scap] {next, flags, key}: a copy of the walked fields (IlrIndex::rec)
   uint32_t scap;
   uint32_t committed;  // slots of the state before the batch
   uint32_t cap_slots, cap_dicts;
@@ -230,6 +233,8 @@ struct IlrLane {
   uint32_t qnext, qend;
   uint32_t* un;
   uint32_t ucap, ucnt;
+  __device__ void rec_next(uint32_t s, uint32_t v) { a.rec[s].x = v; }
+  __device__ void rec_flags(uint32_t s, uint32_t v) { a.rec[s].y = v; }
 
   __device__ uint32_t& ev(uint32_t s, uint32_t k) { return a.ev[static_cast<uint64_t>(EVW) * s + k]; }
   __device__ void conflict(uint32_t why) {
@@ -281,12 +286,14 @@ struct IlrLane {
   __device__ void set_next(uint32_t s, uint32_t old, uint32_t v) {
     log_undo(s, IF_NEXT, old);
     a.T.s_next[s] = v;
+    rec_next(s, v);
   }
   __device__ void set_src(uint32_t s, uint32_t v) { log_undo(s, IF_SRC, a.T.s_src[s]); a.T.s_src[s] = v; }
   __device__ void set_child(uint32_t s, uint32_t v) { log_undo(s, IF_CHILD, a.T.s_child[s]); a.T.s_child[s] = v; }
   __device__ void set_flags(uint32_t s, uint32_t old, uint32_t v) {
     log_undo(s, IF_FLAGS, old);
     a.T.s_flags[s] = static_cast<uint8_t>(v);
+    rec_flags(s, v);
   }
 
   // a new slot: an Add's from the group's reserved range, others from the counter
@@ -309,6 +316,7 @@ struct IlrLane {
     a.T.s_src[s] = src;
     a.T.s_child[s] = child;
     a.T.s_flags[s] = flags;
+    a.rec[s] = make_uint4(next, flags, static_cast<uint32_t>(key), static_cast<uint32_t>(key >> 32));
     uint32_t* e = a.ev + static_cast<uint64_t>(EVW) * s;
     e[EV_CRE] = at;
     e[EV_DEL] = NONE;
@@ -374,7 +382,10 @@ struct IlrLane {
       if (m == NONE) {  // every member copied: the `next` links inside the copy
         for (uint32_t q = a.dhead[sd]; q != NONE; q = a.mnext[q]) {
           const uint32_t nx = a.T.s_next[q];
-          if (nx != NONE) a.T.s_next[a.xmap[q]] = a.xmap[nx];
+          if (nx != NONE) {
+            a.T.s_next[a.xmap[q]] = a.xmap[nx];
+            rec_next(a.xmap[q], a.xmap[nx]);
+          }
         }
         --sp;
         continue;
@@ -607,10 +618,10 @@ __global__ void __launch_bounds__(64) k_ilr_free(IlrArgs args, uint32_t L, const
 __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const uint32_t* vs, const uint32_t* gbeg,
                                                   const uint32_t* gend, uint32_t g0, uint32_t L, uint32_t phase,
                                                   uint8_t* st) {
-  if (threadIdx.x != 0) return;
   const uint32_t g = g0 + blockIdx.x;
   const uint32_t gf = args.J.gflag[g];
   if ((gf & GF_DST) ? phase != 2 : phase != 1) return;
+  if (threadIdx.x != 0) return;
   const uint32_t kb = gbeg[g], ke = gend[g];
   IlrLane R;
   R.a = args;
@@ -743,20 +754,26 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
             s = ST_NOTFOUND;
           } else {
             // findInsertion (:93-104): ls = the slot of the key it returns
-            uint32_t node = found, ls = found, rn;
+            // (one 16-byte record per step: rn's next, flags and key)
+            uint32_t node = found, ls = found, rn = args.rec[found].x;
             for (;;) {
-              rn = args.T.s_next[node];
               ++n_walk;
               if (rn == NONE) break;
+              const uint4 r = args.rec[rn];
               uint32_t live = rn;
-              while (live != NONE && (args.T.s_flags[live] & F_TOMB)) {
-                live = args.T.s_next[live];
+              uint4 lr = r;
+              while (lr.y & F_TOMB) {
+                live = lr.x;
                 ++n_skip;
+                if (live == NONE) break;
+                lr = args.rec[live];
               }
               if (live == NONE) break;
-              if (ts > args.T.s_key[rn]) break;
+              const long long rk = static_cast<long long>((static_cast<unsigned long long>(r.w) << 32) | r.z);
+              if (ts > rk) break;
               ls = rn;
               node = live;
+              rn = lr.x;
             }
             const uint32_t x = R.take_slot(true);
             if (x == NONE) break;
@@ -837,6 +854,7 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
     q[4] = n_mark;
     q[5] = wall_clock64() - t0;
     q[6] = L;
+    q[7] = 0;
   }
   args.ucnt[g] = R.ucnt;
   if (!R.bad) {
@@ -848,6 +866,7 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
       args.T.s_src[x] = NONE;
       args.T.s_child[x] = NONE;
       args.T.s_flags[x] = F_TOMB | F_ORPHAN;
+      args.rec[x] = make_uint4(NONE, F_TOMB | F_ORPHAN, x, 0u);
       for (uint32_t w = 0; w < EVW; ++w) R.ev(x, w) = NONE;
       args.mnext[x] = NONE;
     }
@@ -951,6 +970,13 @@ __global__ void k_ilr_counters(DevResult* d, TreeDev T, uint32_t* dhead, uint32_
   dsrc[grave] = NONE;
 }
 
+__global__ void __launch_bounds__(BLOCK) k_ilr_rec(TreeDev T, uint32_t S, uint4* rec) {
+  GRID_STRIDE(s, S) {
+    const unsigned long long k = static_cast<unsigned long long>(T.s_key[s]);
+    rec[s] = make_uint4(T.s_next[s], T.s_flags[s], static_cast<uint32_t>(k), static_cast<uint32_t>(k >> 32));
+  }
+}
+
 static uint32_t pow2_ge(uint64_t x) {
   uint32_t p = 1024;
   while (p < x && p < (1u << 31)) p <<= 1;
@@ -1002,12 +1028,15 @@ static int ilr_build(crdtm_tree* t) {
     if (X.mnext) hipFree(X.mnext);
     if (X.ev) hipFree(X.ev);
     if (X.xmap) hipFree(X.xmap);
+    if (X.rec) hipFree(X.rec);
     X.mnext = nullptr;
     X.ev = nullptr;
     X.xmap = nullptr;
+    X.rec = nullptr;
     HIP_CHECK(hipMalloc(&X.mnext, t->cap.slots * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&X.ev, EVW * t->cap.slots * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&X.xmap, t->cap.slots * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&X.rec, t->cap.slots * sizeof(uint4)));
     X.scap = t->cap.slots;
   }
   HIP_CHECK(hipMemsetAsync(X.H.slot, 0xFF, X.hcap * sizeof(uint32_t), s));
@@ -1015,6 +1044,7 @@ static int ilr_build(crdtm_tree* t) {
   HIP_CHECK(hipMemsetAsync(X.ev, 0xFF, EVW * X.scap * sizeof(uint32_t), s));
   LAUNCH(k_replay_index, dim3(grid_for(t->n_slots)), dim3(BLOCK), 0, s, t->d, static_cast<uint32_t>(t->n_slots), X.H,
          X.dhead, X.mnext);
+  LAUNCH(k_ilr_rec, dim3(grid_for(t->n_slots)), dim3(BLOCK), 0, s, t->d, static_cast<uint32_t>(t->n_slots), X.rec);
   X.hused = t->n_slots;
   t->ilr_valid = true;
   return CRDTM_OK;
@@ -1149,6 +1179,7 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   a.mnext = X->mnext;
   a.ev = X->ev;
   a.xmap = X->xmap;
+  a.rec = X->rec;
   a.scap = static_cast<uint32_t>(X->scap);
   a.committed = static_cast<uint32_t>(t->n_slots);
   a.cap_slots = static_cast<uint32_t>(t->cap.slots);
@@ -1235,8 +1266,8 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
     fprintf(stderr, "ilr stats: ops %llu walk %llu skip %llu\n", to, tw, ts);
     for (uint32_t q = 0; q < std::min<uint32_t>(G, 6); ++q) {
       const unsigned long long* v = &hs[8 * ord[q]];
-      fprintf(stderr, "  L%llu ops %llu walk %llu skip %llu quirk %llu mark %llu  %.1f us\n", v[6], v[0], v[1], v[2],
-              v[3], v[4], v[5] / 100.0);
+      fprintf(stderr, "  L%llu ops %llu walk %llu skip %llu quirk %llu mark %llu (%llu)  %.1f us\n", v[6], v[0],
+              v[1], v[2], v[3], v[4], v[7], v[5] / 100.0);
     }
   }
   if (h.ilr_conflict || h.ilr_overflow || drift || h.err_index != NONE) {
