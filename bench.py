@@ -309,7 +309,7 @@ def want_pmc(args, world):
 def dry_run(args, rank, world):
     """--dry-run: the multi-rank plumbing of a real run on the CPU (gloo): the
     ranks the launcher started, the timing barrier and max over ranks, and the
-    config-5 exchange (shard.Exchange all-gather of the simulated replicas' op
+    config-5 exchange (shard.Exchange all-to-all of the simulated replicas' op
     logs, then each rank's assembly of the documents it owns). No merge runs,
     so no throughput is claimed (`value` null)."""
     import torch
@@ -349,6 +349,7 @@ def dry_run(args, rank, world):
                 "config": {"workload": "dry run (launcher and exchange plumbing, no merge)",
                            "parallelism": f"documents sharded by id over {world} rank(s) (gloo)"},
                 "exchange": {"documents": n_docs, "records_per_rank_block": int(getattr(ex, "block", kept)),
+                             "mode": ex.mode, "recv_bytes_per_rank": ex.recv_bytes,
                              "assembled_ok": bool(t[1] == 0)}}
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -561,7 +562,7 @@ def main():
         ex = run_trees(args, rank, world, local_rank, cpu=False)
         line["exchange"] = {k: ex[k] for k in ("metric", "value", "unit", "ms_per_step", "config")}
         line["exchange"]["roofline_frac"] = ex["roofline"]["frac"]
-        line["exchange"]["all_gather_ms"] = ex["all_gather_ms"]
+        line["exchange"]["all_gather_ms"] = ex["all_gather_ms"]  # (the exchange alone: all_to_all or all_gather)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -704,8 +705,9 @@ def run_incr(args, rank, world, local_rank):
 
 
 def run_trees(args, rank, world, local_rank, cpu=True):
-    """Config 5: all-gather of the simulated replicas' op logs (RCCL), then every
-    rank merges the documents it owns (document t -> rank t mod world)."""
+    """Config 5: the simulated replicas' op logs exchanged by document owner
+    (RCCL all_to_all_single; document t -> rank t mod world), then every rank
+    merges the documents it owns."""
     import torch
     import torch.distributed as dist
     from crdtm import _native as N
@@ -728,7 +730,7 @@ def run_trees(args, rank, world, local_rank, cpu=True):
         logs.append(rec)
     local = torch.from_numpy(np.concatenate(logs)).to(dev)
     del logs
-    ex = shard.Exchange(local)  # counts gathered once; persistent padded buffers
+    ex = shard.Exchange(local)  # records by owner rank (all_to_all); counts exchanged once; persistent buffers
     ctx = C.c_void_p()
     stream = torch.cuda.current_stream()
     N.check(L.crdtm_ctx_create(local_rank, C.c_void_p(stream.cuda_stream), C.byref(ctx)), "ctx")
@@ -813,7 +815,10 @@ def run_trees(args, rank, world, local_rank, cpu=True):
         "vs_baseline": None, "dtype": "int64", "data": "synthetic (deterministic generator, SURVEY.md §8d)",
         "config": {"workload": f"trees: {n_mine} documents x {per} ops per GPU ({n} ops), {n_docs} documents total",
                    "replicas": TREES["replicas"], "documents_ok": ok_docs,
-                   "parallelism": f"documents sharded by id over {world} GPU(s); op logs all-gathered (RCCL)"},
+                   "parallelism": f"documents sharded by id over {world} GPU(s); op logs exchanged by owner "
+                                  f"({ex.mode}, RCCL)",
+                   "exchange_mode": ex.mode, "recv_bytes_per_rank": ex.recv_bytes,
+                   "used_bytes_per_rank": int(n * shard.REC_W * 8)},
         "roofline": roofline("trees", per_k, launches, B_alg, ms_step, 1,
                              live=pmc_live(args) if (cpu and rank == 0 and want_pmc(args, world)) else None),
         "all_gather_ms": ag_ms,

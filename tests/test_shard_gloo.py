@@ -1,6 +1,7 @@
 """Multi-process (world_size 2, gloo on CPU) checks of the document sharding
 and op-log exchange used by bench.py --workload trees (RCCL on the GPU node):
-the persistent padded all-gather (shard.Exchange), the assembly of each
+the op-log exchange by document owner (shard.Exchange: all_to_all_single,
+and the padded all-gather fallback), the assembly of each
 rank's documents, and the merge of the assembled documents on the oracle
 (orc_forest_apply, oracle/crdtree_oracle.cpp) against the single-process
 stream's documents."""
@@ -9,6 +10,7 @@ import socket
 import sys
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -37,7 +39,7 @@ def _oracle_forest(ops, n_docs, per_doc):
     return out
 
 
-def _worker(rank, world, port, n_docs, per_doc, q):
+def _worker(rank, world, port, n_docs, per_doc, q, mode="auto"):
     sys.path.insert(0, os.path.join(ROOT, "crdt-graph_amd"))
     sys.path.insert(0, ROOT)
     import torch
@@ -49,10 +51,15 @@ def _worker(rank, world, port, n_docs, per_doc, q):
     s = N.synth(n_ops=per_doc, n_docs=n_docs, replicas=8, window=16, p_delete=0.2, seed=0xC0FFEE05)
     doc_off = np.arange(n_docs + 1, dtype=np.uint32) * per_doc
     local = torch.from_numpy(shard.local_log(s, doc_off, rank, world, replicas=8))
-    ex = shard.Exchange(local)
+    ex = shard.Exchange(local, mode=mode)
     for _ in range(2):  # the buffers are reused step after step
         allrec = ex.gather()
-    assert allrec.shape[0] == world * ex.block and ex.counts[rank] == local.shape[0]
+    if ex.mode == "all_gather":
+        assert allrec.shape[0] == world * ex.block and ex.counts[rank] == local.shape[0]
+    else:  # exactly this rank's documents' records, from every rank
+        assert ex.mode == "all_to_all" and mode in ("auto", "all_to_all")
+        assert allrec.shape[0] == sum(ex.recv_splits) and sum(ex.send_splits) == local.shape[0]
+        assert bool(((allrec[:, 0] >> 32) % world == rank).all())
     ops, my_off, keep = shard.assemble(allrec, rank, world, n_docs, per_doc)
     n_kept = int(keep.sum())
     # expected: the owned documents' streams, sliced directly from the generator output
@@ -67,17 +74,18 @@ def _worker(rank, world, port, n_docs, per_doc, q):
     got = _oracle_forest({k: v.numpy() for k, v in ops.items()}, len(mine), per_doc)
     want = _oracle_forest({k: s[k][idx] for k in ("kind", "ts", "path", "val")}, len(mine), per_doc)
     merged = all(np.array_equal(got[k], want[k]) for k in got) and bool(np.all(got["code"] == 0))
-    q.put((rank, bool(ok and merged), int(local.shape[0]), int(n_kept)))
+    q.put((rank, bool(ok and merged), int(local.shape[0]), int(n_kept), ex.mode))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_oplog_exchange_world2():
+@pytest.mark.parametrize("mode", ["all_to_all", "all_gather"])
+def test_oplog_exchange_world2(mode):
     world, n_docs, per_doc = 2, 12, 300
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_docs, per_doc, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_docs, per_doc, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -85,7 +93,7 @@ def test_oplog_exchange_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     res.sort()
-    assert all(ok for _, ok, _, _ in res), res
+    assert all(r[1] for r in res) and all(r[4] == mode for r in res), res
     # every op travels in exactly one rank's log; every op is kept by exactly one rank
     assert sum(r[2] for r in res) == n_docs * per_doc
     assert sum(r[3] for r in res) == n_docs * per_doc

@@ -8,7 +8,7 @@
 set -euo pipefail
 export TMPDIR=/tmp
 R=$1; W=$2; shift 2
-B="python3 bench.py --workload $W --steps 3 --warmup 1 --profile-steps 1 --cpu-sample 0 $*"
+B="python3 bench.py --workload $W --steps 3 --warmup 1 --profile-steps 1 --cpu-sample 0 --pmc off $*"
 O=gpurun_out
 mkdir -p $O
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/${R}_prof_$W -o run --output-format csv -- $B > $O/${R}_prof_$W.log 2>&1
