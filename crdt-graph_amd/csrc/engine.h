@@ -332,6 +332,10 @@ int grow_tree(crdtm_tree* t, const TreeCaps& need);
 int unshare_tree(crdtm_tree* t, bool keep_contents);
 int apply_batch(crdtm_tree* t, const OpsDev& ops, uint8_t* status_dev, crdtm_result* res);
 int linearize(crdtm_tree* t);  // fills t->d.doc / t->doc_n from the tree state
+// chain positions of the state's dict entries, every dict's chain
+// consecutive (R: slot -> position, NONE for an orphan; G: position -> slot),
+// both sized n_slots
+int chain_snapshot(crdtm_tree* t, uint32_t* R, uint32_t* G, Arena& ws, hipStream_t s);
 int fi_materialize(crdtm_tree* t);  // incr.hip: `doc` from the gapped order (doc_gapped)
 int forest_apply(crdtm_ctx* c, int64_t replica_id, const OpsDev& o, const uint32_t* doc_off_host, uint64_t n_docs,
                  int32_t* code, int64_t* err, uint32_t* applied, uint64_t* vhash, uint64_t* vwords, int64_t* tstamp);

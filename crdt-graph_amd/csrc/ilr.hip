@@ -79,6 +79,9 @@ constexpr uint32_t IMPLICIT = 0xFFFFFFFEu;  // a live node's children still the 
 constexpr uint32_t ST_CONFLICT = 0xFF;     // (prep: the batch goes to the re-merge)
 constexpr uint32_t LV_PTOT = ILR_MAXL + 1, LV_QTOT = ILR_MAXL + 2, LV_N = ILR_MAXL + 4;
 constexpr uint32_t ILR_JOBS = 4;  // deferred copies one lane makes
+constexpr uint32_t COPY_POOL = 32;  // slots a lane takes from the counter at a time (copies, sentinels)
+constexpr uint32_t PT_LDS = 2048;   // private tables up to this size live in LDS (32 KB)
+constexpr uint32_t ILR_LREC = 1024;  // LDS mirror of a lane's first reserved slots' records (16 KB)
 
 // conflict reasons (DevResult::ilr_why) and overflow reasons (ilr_overflow)
 enum : uint32_t {
@@ -103,12 +106,13 @@ __host__ __device__ inline uint32_t ilr_ucap(uint32_t m) { return 3 * m + 8; }
 __host__ __device__ inline uint64_t ilr_uoff(uint32_t gbeg, uint32_t g) { return 3ULL * gbeg + 8ULL * g; }
 
 // a level's ops, resolved before its lanes (per sorted position)
+// (everything a lane needs of an op, packed so it loads the next op's while
+// it works on this one)
 struct IlrPrep {
-  uint8_t* res;    // ST_APPLIED (lands), ST_ALREADY / ST_INVALID (stops on the way), ST_CONFLICT
-  uint32_t* d;     // landing dict, or IMPLICIT
-  uint32_t* own;   // its owner slot (NONE: the root dict)
-  uint32_t* ts;    // the Add's timestamp in d before this level (NONE: absent)
-  uint32_t* kk;    // the anchor / Delete target in d before this level (NONE: absent)
+  uint4* w1;  // {op index, kind | res << 8, landing dict (or IMPLICIT), its owner slot (NONE: the root dict)}
+              //   res: ST_APPLIED (lands), ST_ALREADY / ST_INVALID (stops on the way), ST_CONFLICT
+  uint4* w2;  // {ts lo, ts hi, last path key lo, hi} (the anchor / the Delete's target)
+  uint2* w3;  // {slot of ts in d, slot of the last key in d} before this level (NONE: absent)
 };
 
 struct IlrJobs {
@@ -155,6 +159,11 @@ struct IlrArgs {
   uint32_t grave;  // the dead dict of this batch's unused reserved slots
   IlrPrep P;
   IlrJobs J;
+  // chain order of the state at the batch's start (chain_snapshot, merge.hip):
+  // slot -> position and position -> slot (nullptr: none taken)
+  const uint32_t* R;
+  const uint32_t* G;
+  uint32_t E;
   uint32_t* dsrc;    // [dicts] a copy made by a same-group deferred copy: its source dict (else NONE)
   uint32_t dnew;     // dicts of the state before the batch
   unsigned long long* stats;  // (CRDTM_ILR_STATS: per group ops, walk steps, tombstone skips, quirks, marks, ticks)
@@ -233,17 +242,54 @@ struct IlrLane {
   uint32_t qnext, qend;
   uint32_t* un;
   uint32_t ucap, ucnt;
-  __device__ void rec_next(uint32_t s, uint32_t v) { a.rec[s].x = v; }
-  __device__ void rec_flags(uint32_t s, uint32_t v) { a.rec[s].y = v; }
+  // this lane's reserved slots' records mirrored in LDS (the walks of a busy
+  // dict run mostly over the text its own earlier ops inserted)
+  uint4* lrec;
+  uint32_t lbase, lcnt;
+  // slots for deep copies, taken from the counter COPY_POOL at a time
+  uint32_t cpnext, cpend;
+  // the head of the member list of the dict this lane last wrote
+  uint32_t hd_d, hd_v;
+  // and the last record read from the state (a typist's next character
+  // walks from the entry the previous one stopped at: a global load after
+  // this op's stores waits for them)
+  uint32_t cs;
+  uint4 cr;
+  __device__ uint4 getrec(uint32_t s) {
+    if (s - lbase < lcnt) return lrec[s - lbase];
+    if (s == cs) return cr;
+    cr = a.rec[s];
+    cs = s;
+    return cr;
+  }
+  __device__ void rec_next(uint32_t s, uint32_t v) {
+    a.rec[s].x = v;
+    if (s - lbase < lcnt) lrec[s - lbase].x = v;
+    if (s == cs) cr.x = v;
+  }
+  __device__ void rec_flags(uint32_t s, uint32_t v) {
+    a.rec[s].y = v;
+    if (s - lbase < lcnt) lrec[s - lbase].y = v;
+    if (s == cs) cr.y = v;
+  }
 
   __device__ uint32_t& ev(uint32_t s, uint32_t k) { return a.ev[static_cast<uint64_t>(EVW) * s + k]; }
+  // (the lanes of a group's wave all run the replay on the same values: one
+  // lane makes each atomic and the others take its result)
+  __device__ static uint32_t wave_add(uint32_t* p, uint32_t v) {
+    uint32_t r = 0;
+    if ((threadIdx.x & 63) == 0) r = atomicAdd(p, v);
+    return __shfl(r, 0);
+  }
   __device__ void conflict(uint32_t why) {
-    atomicOr(&a.dr->ilr_why, why);
-    atomicOr(&a.dr->ilr_conflict, 1u);
+    if ((threadIdx.x & 63) == 0) {
+      atomicOr(&a.dr->ilr_why, why);
+      atomicOr(&a.dr->ilr_conflict, 1u);
+    }
     bad = true;
   }
   __device__ void overflow(uint32_t why) {
-    atomicOr(&a.dr->ilr_overflow, why);
+    if ((threadIdx.x & 63) == 0) atomicOr(&a.dr->ilr_overflow, why);
     bad = true;
   }
   // (dict, key) -> slot among the slots this lane created in this level
@@ -297,13 +343,42 @@ struct IlrLane {
   }
 
   // a new slot: an Add's from the group's reserved range, others from the counter
-  __device__ uint32_t take_slot(bool reserved) {
-    const uint32_t s = (reserved && qnext < qend) ? qnext++ : atomicAdd(&a.dr->ilr_slots, 1u);
+  __device__ uint32_t take_slot(bool reserved, bool bulk = false) {
+    uint32_t s;
+    if (reserved && qnext < qend) {
+      s = qnext++;
+    } else if (!bulk) {
+      s = wave_add(&a.dr->ilr_slots, 1u);
+    } else {
+      if (cpnext == cpend) {
+        cpnext = wave_add(&a.dr->ilr_slots, COPY_POOL);
+        cpend = cpnext + COPY_POOL;
+      }
+      s = cpnext++;
+    }
     if (s >= a.cap_slots || s >= a.scap || s + 1 > a.hash_limit) {
       overflow(IO_SLOTS);
       return NONE;
     }
     return s;
+  }
+  // a slot nothing will use: a dead entry of the batch's dead dict
+  __device__ void put_dead(uint32_t x) {
+    a.T.s_key[x] = x;
+    a.T.s_dict[x] = a.grave;
+    a.T.s_next[x] = NONE;
+    a.T.s_src[x] = NONE;
+    a.T.s_child[x] = NONE;
+    a.T.s_flags[x] = F_TOMB | F_ORPHAN;
+    a.rec[x] = make_uint4(NONE, F_TOMB | F_ORPHAN, x, 0u);
+    for (uint32_t w = 0; w < EVW; ++w) ev(x, w) = NONE;
+    a.mnext[x] = NONE;
+  }
+  // the pool's unused slots (they were counted: the commit keeps them)
+  __device__ void retire_pool() {
+    const uint32_t e = min(min(cpend, a.cap_slots), a.scap);
+    for (uint32_t x = cpnext; x < e; ++x) put_dead(x);
+    cpnext = cpend;
   }
   // slot s into dict d (a dict this lane writes); `priv`: later ops of this
   // lane may look it up (its nodes and sentinels; copies are reached by
@@ -316,7 +391,10 @@ struct IlrLane {
     a.T.s_src[s] = src;
     a.T.s_child[s] = child;
     a.T.s_flags[s] = flags;
-    a.rec[s] = make_uint4(next, flags, static_cast<uint32_t>(key), static_cast<uint32_t>(key >> 32));
+    const uint4 r4 = make_uint4(next, flags, static_cast<uint32_t>(key), static_cast<uint32_t>(key >> 32));
+    a.rec[s] = r4;
+    if (s - lbase < lcnt) lrec[s - lbase] = r4;
+    if (s == cs) cr = r4;
     uint32_t* e = a.ev + static_cast<uint64_t>(EVW) * s;
     e[EV_CRE] = at;
     e[EV_DEL] = NONE;
@@ -334,16 +412,20 @@ struct IlrLane {
       ps[p] = s;
       ++pused;
     }
-    a.mnext[s] = a.dhead[d];
+    a.mnext[s] = d == hd_d ? hd_v : a.dhead[d];
     a.dhead[d] = s;
+    hd_d = d;
+    hd_v = s;
   }
   __device__ uint32_t new_dict(uint32_t owner) {
-    const uint32_t d = atomicAdd(&a.dr->ilr_dicts, 1u);
+    const uint32_t d = wave_add(&a.dr->ilr_dicts, 1u);
     if (d >= a.cap_dicts) {
       overflow(IO_DICTS);
       return NONE;
     }
     a.dhead[d] = NONE;
+    hd_d = d;
+    hd_v = NONE;
     a.dsrc[d] = NONE;
     a.T.d_owner[d] = owner;
     a.T.d_sent[d] = NONE;
@@ -392,7 +474,7 @@ struct IlrLane {
       }
       stk_m[sp] = a.mnext[m];
       const uint8_t fl = a.T.s_flags[m];
-      const uint32_t nm = take_slot(false);
+      const uint32_t nm = take_slot(false, true);
       if (nm == NONE) return;
       put_slot(nm, dd, a.T.s_key[m], NONE, a.T.s_src[m], NONE, fl, at, false);
       a.xmap[m] = nm;
@@ -426,7 +508,7 @@ struct IlrLane {
   }
   // a deferred copy of node's children as of op `at`, for the next level
   __device__ bool add_job(uint32_t node, uint32_t dst, uint32_t at) {
-    const uint32_t j = atomicAdd(&a.dr->ilr_jobs, 1u);
+    const uint32_t j = wave_add(&a.dr->ilr_jobs, 1u);
     if (j >= a.J.cap) {
       overflow(IO_JOBS);
       return false;
@@ -504,6 +586,7 @@ __global__ void __launch_bounds__(BLOCK) k_ilr_glist(const uint32_t* sk, const u
     } while (e < n && sk[e] == sk[k]);
     gend[j] = e;
     atomicAdd(&lvops[L], e - k);
+    atomicMax(&lvcnt[ILR_MAXL + 3], e - k);  // (the largest group)
     qn[j] = adds;
     pcap[j] = ilr_pcap(adds);
     slot2grp[sk[k] & ((1u << gbits) - 1u)] = j;
@@ -559,11 +642,12 @@ __global__ void __launch_bounds__(BLOCK) k_ilr_prep(IlrArgs a, OpsDev o, const u
       if (o.kind[i] == CRDTM_ADD) pts = slothash_find(a.H, d, o.ts[i]);
       pkk = slothash_find(a.H, d, kk);
     }
-    a.P.res[k] = static_cast<uint8_t>(res);
-    a.P.d[k] = d;
-    a.P.own[k] = own;
-    a.P.ts[k] = pts;
-    a.P.kk[k] = pkk;
+    const unsigned long long tsu = static_cast<unsigned long long>(o.ts[i]);
+    const unsigned long long kku = static_cast<unsigned long long>(L ? o.path[b + L - 1] : 0);
+    a.P.w1[k] = make_uint4(i, static_cast<uint32_t>(o.kind[i]) | (res << 8), d, own);
+    a.P.w2[k] = make_uint4(static_cast<uint32_t>(tsu), static_cast<uint32_t>(tsu >> 32), static_cast<uint32_t>(kku),
+                           static_cast<uint32_t>(kku >> 32));
+    a.P.w3[k] = make_uint2(pts, pkk);
   }
 }
 
@@ -605,11 +689,19 @@ __global__ void __launch_bounds__(64) k_ilr_free(IlrArgs args, uint32_t L, const
   R.qnext = R.qend = 0;
   R.un = nullptr;
   R.ucap = R.ucnt = 0;
+  R.lrec = nullptr;
+  R.lbase = 0;
+  R.lcnt = 0;
+  R.cpnext = R.cpend = 0;
+  R.hd_d = NONE;
+  R.hd_v = NONE;
+  R.cs = NONE;
   const uint32_t nf = min(*nfree, args.J.cap);
   for (uint32_t q = 0; q < nf && !R.bad; ++q) {
     const uint32_t j = args.J.freel[q];
     R.run_job(args.J.own[j], args.J.dst[j], args.J.at[j], false);
   }
+  if (!R.bad) R.retire_pool();
 }
 
 // ---- one level, one phase: one lane per group ----
@@ -618,25 +710,43 @@ __global__ void __launch_bounds__(64) k_ilr_free(IlrArgs args, uint32_t L, const
 __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const uint32_t* vs, const uint32_t* gbeg,
                                                   const uint32_t* gend, uint32_t g0, uint32_t L, uint32_t phase,
                                                   uint8_t* st) {
+  // (one wave per group: every lane runs the replay on the same values; the
+  // lanes part ways only in the chain-order walk below)
   const uint32_t g = g0 + blockIdx.x;
   const uint32_t gf = args.J.gflag[g];
   if ((gf & GF_DST) ? phase != 2 : phase != 1) return;
-  if (threadIdx.x != 0) return;
+  const uint32_t lane = threadIdx.x & 63;
   const uint32_t kb = gbeg[g], ke = gend[g];
+  __shared__ uint4 lrec[ILR_LREC];
+  __shared__ long long tpk[PT_LDS];
+  __shared__ uint32_t tpd[PT_LDS], tps[PT_LDS];
+  const uint32_t pc = args.pcap[g];
+  const bool plds = pc <= PT_LDS;
+  if (plds) {
+    for (uint32_t q = lane; q < pc; q += 64) tps[q] = NONE;
+    __syncthreads();
+  }
   IlrLane R;
   R.a = args;
   R.bad = false;
   R.depth = L;
-  R.pk = args.pk + args.poff[g];
-  R.pd = args.pd + args.poff[g];
-  R.ps = args.ps + args.poff[g];
-  R.pmask = args.pcap[g] - 1;
+  R.pk = plds ? tpk : args.pk + args.poff[g];
+  R.pd = plds ? tpd : args.pd + args.poff[g];
+  R.ps = plds ? tps : args.ps + args.poff[g];
+  R.pmask = pc - 1;
   R.pused = 0;
   R.qnext = args.committed + args.qoff[g];
   R.qend = R.qnext + args.qn[g];
   R.un = args.undo + 3 * ilr_uoff(kb, g);
   R.ucap = ilr_ucap(ke - kb);
   R.ucnt = 0;
+  R.lrec = lrec;
+  R.lbase = R.qnext;
+  R.lcnt = min(args.qn[g], ILR_LREC);
+  R.cpnext = R.cpend = 0;
+  R.hd_d = NONE;
+  R.hd_v = NONE;
+  R.cs = NONE;
   const bool pre = phase == 1;  // (phase 2: the copies changed the landing dicts after the prep)
   if ((gf & (GF_SRC | GF_DST)) == (GF_SRC | GF_DST)) R.conflict(IW_CHAIN);
   // the deferred copies this lane makes, by op
@@ -681,12 +791,28 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
   };
   unsigned long long n_walk = 0, n_skip = 0, n_quirk = 0, n_mark = 0;
   const unsigned long long t0 = wall_clock64();
+  uint4 c1 = args.P.w1[kb], c2 = args.P.w2[kb];
+  uint2 c3 = args.P.w3[kb];
   for (uint32_t k = kb; k < ke && !R.bad; ++k) {
-    const uint32_t i = vs[k];
+    uint4 n1 = c1, n2 = c2;
+    uint2 n3 = c3;
+    if (k + 1 < ke) {  // the next op's record, in flight while this op runs
+      n1 = args.P.w1[k + 1];
+      n2 = args.P.w2[k + 1];
+      n3 = args.P.w3[k + 1];
+    }
+    const uint32_t i = c1.x;
+    const uint8_t kind = static_cast<uint8_t>(c1.y & 0xFFu);
+    const uint32_t res = c1.y >> 8;
+    const long long ts = static_cast<long long>((static_cast<unsigned long long>(c2.y) << 32) | c2.x);
+    const long long kk = static_cast<long long>((static_cast<unsigned long long>(c2.w) << 32) | c2.z);
+    const uint32_t pre_ts = c3.x, pre_kk = c3.y;
+    uint32_t d = c1.z, ownr = c1.w;
+    c1 = n1;
+    c2 = n2;
+    c3 = n3;
     if (nj) run_jobs_before(i);
     if (R.bad) break;
-    const uint8_t kind = o.kind[i];
-    const uint32_t res = args.P.res[k];
     uint8_t s = ST_APPLIED;
     if (res == ST_CONFLICT) {
       R.bad = true;
@@ -695,10 +821,6 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
     if (res != ST_APPLIED) {
       s = static_cast<uint8_t>(res);
     } else {
-      const uint32_t b = o.off[i], L1 = o.off[i + 1] - b;
-      const long long kk = o.path[b + L1 - 1];
-      const long long ts = o.ts[i];
-      uint32_t d = args.P.d[k], ownr = args.P.own[k];
       bool usepre = pre && (d == IMPLICIT || R.copy_src(d) == NONE);
       if (d == IMPLICIT) {  // (materialised by this lane since the prep?)
         const uint32_t c = args.T.s_child[ownr];
@@ -730,7 +852,7 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
         };
         if (kind == CRDTM_DELETE) {  // deleteHelp (:112-122)
           uint32_t t = recent(kk);
-          if (t == NONE) t = lookup(kk, args.P.kk[k]);
+          if (t == NONE) t = lookup(kk, pre_kk);
           if (t == NONE) {
             s = ST_NOTFOUND;
           } else {
@@ -745,28 +867,80 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
               R.ev(t, EV_DEL) = i;  // children drop at the commit
             }
           }
-        } else if (lookup(ts, args.P.ts[k]) != NONE) {  // addAfterHelp (:56-90)
+        } else if (lookup(ts, pre_ts) != NONE) {  // addAfterHelp (:56-90)
           s = ST_ALREADY;
         } else {
           uint32_t found = recent(kk);
-          if (found == NONE) found = lookup(kk, args.P.kk[k]);
+          if (found == NONE) found = lookup(kk, pre_kk);
           if (found == NONE) {
             s = ST_NOTFOUND;
           } else {
             // findInsertion (:93-104): ls = the slot of the key it returns
             // (one 16-byte record per step: rn's next, flags and key)
-            uint32_t node = found, ls = found, rn = args.rec[found].x;
+            uint32_t node = found, ls = found, rn = R.getrec(found).x;
             for (;;) {
+              // The chain from node in the batch-start snapshot's order, 64
+              // entries at a time, each link checked against the state (a
+              // link this batch changed ends the run): the walk's steps over
+              // the checked run are decided together; only where the run
+              // ends or breaks does the walk take single steps.
+              if (args.R && node < args.committed && args.R[node] != NONE) {
+                const uint32_t pos = args.R[node] + 1 + lane;
+                const uint32_t ck = pos < args.E ? args.G[pos] : NONE;  // c_{lane+1}
+                const uint4 rc = ck != NONE ? args.rec[ck] : make_uint4(NONE, F_TOMB, 0u, 0u);
+                uint32_t nprev = __shfl_up(rc.x, 1);  // next(c_lane)
+                if (lane == 0) nprev = rn;            // next(c_0 = node)
+                const unsigned long long mlink = __ballot(ck != NONE && nprev == ck);
+                const uint32_t V = ~mlink ? static_cast<uint32_t>(__builtin_ctzll(~mlink)) : 64u;
+                // positions 0..V are the chain from node; bit p below is position p
+                const bool valid = lane < V;  // position lane + 1
+                const long long kc = static_cast<long long>((static_cast<unsigned long long>(rc.w) << 32) | rc.z);
+                const unsigned long long mlive = __ballot(valid && !(rc.y & F_TOMB)) << 1;
+                const unsigned long long mkey = __ballot(valid && ts > kc);          // compare at position lane + 1
+                const unsigned long long mend = __ballot(lane <= V && nprev == NONE);  // next(position lane) is none
+                const unsigned long long vis = mlive | 1ULL;  // visited: node, then every live entry
+                unsigned long long cand = vis & (mkey | mend);
+                if (mend) {  // the chain ends in the run: no live entry after the last visited one
+                  const uint32_t e = static_cast<uint32_t>(__builtin_ctzll(mend));
+                  const unsigned long long upto = e >= 63 ? ~0ULL : ((2ULL << e) - 1ULL);
+                  cand |= 1ULL << (63 - __builtin_clzll(vis & upto));
+                }
+                auto slot_at = [&](uint32_t p) -> uint32_t { return p == 0 ? node : __shfl(ck, p - 1); };
+                auto next_at = [&](uint32_t p) -> uint32_t { return __shfl(nprev, p); };
+                if (cand) {  // the walk stops at the first candidate
+                  const uint32_t S = static_cast<uint32_t>(__builtin_ctzll(cand));
+                  if (S > 0) {
+                    const unsigned long long below = vis & ((1ULL << S) - 1ULL);
+                    ls = slot_at(static_cast<uint32_t>(63 - __builtin_clzll(below)) + 1);
+                    node = slot_at(S);
+                    n_walk += __builtin_popcountll(below);
+                  }
+                  rn = next_at(S);
+                  break;
+                }
+                // no stop in the run: the walk passes every visited entry up
+                // to the last one (which needs what follows the run)
+                const unsigned long long inrun = vis & (V >= 63 ? ~0ULL : ((2ULL << V) - 1ULL));
+                const uint32_t Lv = static_cast<uint32_t>(63 - __builtin_clzll(inrun));
+                if (Lv > 0) {
+                  const unsigned long long below = inrun & ((1ULL << Lv) - 1ULL);
+                  ls = slot_at(static_cast<uint32_t>(63 - __builtin_clzll(below)) + 1);
+                  node = slot_at(Lv);
+                  rn = next_at(Lv);
+                  n_walk += __builtin_popcountll(below);
+                  continue;
+                }
+              }
               ++n_walk;
               if (rn == NONE) break;
-              const uint4 r = args.rec[rn];
+              const uint4 r = R.getrec(rn);
               uint32_t live = rn;
               uint4 lr = r;
               while (lr.y & F_TOMB) {
                 live = lr.x;
                 ++n_skip;
                 if (live == NONE) break;
-                lr = args.rec[live];
+                lr = R.getrec(live);
               }
               if (live == NONE) break;
               const long long rk = static_cast<long long>((static_cast<unsigned long long>(r.w) << 32) | r.z);
@@ -777,7 +951,7 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
             }
             const uint32_t x = R.take_slot(true);
             if (x == NONE) break;
-            const uint8_t lsf = args.T.s_flags[ls];
+            const uint8_t lsf = static_cast<uint8_t>(R.getrec(ls).y);
             // x is reachable from the dict's sentinel iff its predecessor is
             R.put_slot(x, d, ts, rn, ILR_TAG | i, NONE, (lsf & F_ORPHAN) ? F_ORPHAN : 0, i, true);
             if (R.bad) break;
@@ -812,7 +986,7 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
               if (ilr_set_has(args.tk, args.tk_mask, ilr_tk_key(L, args.T.s_key[node]))) {
                 nc = R.new_dict(ls);
                 if (nc == NONE) break;
-                const uint32_t j = atomicAdd(&args.dr->ilr_jobs, 1u);
+                const uint32_t j = IlrLane::wave_add(&args.dr->ilr_jobs, 1u);
                 if (j >= args.J.cap) {
                   R.overflow(IO_JOBS);
                   break;
@@ -842,7 +1016,7 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
     else if (s == ST_ALREADY) ++alr;
     else err = min(err, i);
     // incrementTimestamp (src/CRDTree.elm:337-343): Ok Adds of the own replica
-    if ((s == ST_APPLIED || s == ST_ALREADY) && kind == CRDTM_ADD && replica_of(o.ts[i]) == id0) ++own_ok;
+    if ((s == ST_APPLIED || s == ST_ALREADY) && kind == CRDTM_ADD && replica_of(ts) == id0) ++own_ok;
   }
   if (nj && !R.bad) run_jobs_before(NONE);
   if (args.stats) {
@@ -858,23 +1032,17 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
   }
   args.ucnt[g] = R.ucnt;
   if (!R.bad) {
-    // reserved slots no Add took: dead entries of the batch's dead dict
-    for (uint32_t x = R.qnext; x < R.qend; ++x) {
-      args.T.s_key[x] = x;
-      args.T.s_dict[x] = args.grave;
-      args.T.s_next[x] = NONE;
-      args.T.s_src[x] = NONE;
-      args.T.s_child[x] = NONE;
-      args.T.s_flags[x] = F_TOMB | F_ORPHAN;
-      args.rec[x] = make_uint4(NONE, F_TOMB | F_ORPHAN, x, 0u);
-      for (uint32_t w = 0; w < EVW; ++w) R.ev(x, w) = NONE;
-      args.mnext[x] = NONE;
-    }
+    // reserved slots no Add took, pool slots no copy took: dead entries of
+    // the batch's dead dict
+    for (uint32_t x = R.qnext; x < R.qend; ++x) R.put_dead(x);
+    R.retire_pool();
   }
-  if (app) atomicAdd(&args.dr->n_applied, app);
-  if (alr) atomicAdd(&args.dr->n_already, alr);
-  if (own_ok) atomicAdd(&args.dr->own_ok_adds, own_ok);
-  if (err != NONE) atomicMin(&args.dr->err_index, err);
+  if (lane == 0) {
+    if (app) atomicAdd(&args.dr->n_applied, app);
+    if (alr) atomicAdd(&args.dr->n_already, alr);
+    if (own_ok) atomicAdd(&args.dr->own_ok_adds, own_ok);
+    if (err != NONE) atomicMin(&args.dr->err_index, err);
+  }
 }
 
 // counters before a phase: slots (publish start) and deferred copies
@@ -1160,11 +1328,9 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   J.cap = jcap;
   uint32_t* empty = ws.alloc<uint32_t>(16);
   IlrPrep P;
-  P.res = ws.alloc<uint8_t>(n + 1);
-  P.d = ws.alloc<uint32_t>(n + 1);
-  P.own = ws.alloc<uint32_t>(n + 1);
-  P.ts = ws.alloc<uint32_t>(n + 1);
-  P.kk = ws.alloc<uint32_t>(n + 1);
+  P.w1 = ws.alloc<uint4>(n + 1);
+  P.w2 = ws.alloc<uint4>(n + 1);
+  P.w3 = ws.alloc<uint2>(n + 1);
   HIP_CHECK(hipMemsetAsync(ps, 0xFF, static_cast<size_t>(ptot) * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(undo, 0xFF, 3 * nu * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(marks, 0, 4 * (ILR_MAXL + 2) * sizeof(uint32_t), s));
@@ -1201,6 +1367,22 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   a.grave = grave;
   a.P = P;
   a.J = J;
+  // the chain order of the state, when a lane has enough ops for long walks
+  // (env CRDTM_ILR_SNAPSHOT=0: never)
+  static const char* snap_env = getenv("CRDTM_ILR_SNAPSHOT");
+  const uint32_t snap_min = snap_env ? static_cast<uint32_t>(atoi(snap_env)) : 64u;
+  a.R = nullptr;
+  a.G = nullptr;
+  a.E = 0;
+  if (snap_min && lv[ILR_MAXL + 3] >= snap_min) {
+    const uint64_t E = t->n_slots;
+    uint32_t* R = ws.alloc<uint32_t>(E + 1);
+    uint32_t* G = ws.alloc<uint32_t>(E + 1);
+    if ((r = chain_snapshot(t, R, G, ws, s))) return r;
+    a.R = R;
+    a.G = G;
+    a.E = static_cast<uint32_t>(E);
+  }
   a.dsrc = X->dsrc;
   a.dnew = grave;
   static const bool want_stats = getenv("CRDTM_ILR_STATS") != nullptr;
@@ -1241,7 +1423,9 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
     p0 += m;
   }
   if ((r = sync_read(c))) return r;
-  const DevResult h = *c->hres;
+  DevResult h = *c->hres;
+  if (h.ilr_slots > a.cap_slots || h.ilr_slots > a.scap || h.ilr_slots > a.hash_limit)
+    h.ilr_overflow |= IO_SLOTS;  // (slots counted by a pool but never taken lie beyond the room)
   const long long new_ts = t->timestamp + h.own_ok_adds;
   const bool drift = replica_of(new_ts) != replica_of(t->timestamp);
   static const bool debug = getenv("CRDTM_ILR_DEBUG") != nullptr;

@@ -4154,6 +4154,48 @@ int apply_batch(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* r
   return r;
 }
 
+// The chain order of every dict of the state, for the level replay's
+// findInsertion walks (ilr.hip): every dict's chain (sentinel, then `next`
+// by `next`; orphans are on none) laid end to end in dict order — a chain's
+// last entry is followed by the next dict's sentinel — and list-ranked.
+// R[slot] = its position (NONE: an orphan), G[position] = the slot there.
+// Every dict's chain occupies consecutive positions, whether or not its
+// owner is visible (ops reach a dict by key, not through the document).
+__global__ void __launch_bounds__(BLOCK) k_snap_links(TreeDev T, uint32_t S, uint32_t D, uint2* ent) {
+  GRID_STRIDE(s, S) {
+    if (T.s_flags[s] & F_ORPHAN) {
+      ent[s] = make_uint2(ABSENT, 0u);
+      continue;
+    }
+    uint32_t nx = T.s_next[s];
+    if (nx == NONE) {  // the chain's end: the next dict's sentinel
+      for (uint32_t d = T.s_dict[s] + 1; d < D; ++d)
+        if ((nx = T.d_sent[d]) != NONE) break;
+    }
+    ent[s] = make_uint2(nx, 1u);
+  }
+}
+__global__ void __launch_bounds__(BLOCK) k_snap_scatter(uint32_t S, const unsigned long long* excl, uint32_t* R,
+                                                        uint32_t* G) {
+  GRID_STRIDE(s, S) {
+    const unsigned long long r = excl[s];
+    const bool on = r != ~0ULL && r < S;
+    R[s] = on ? static_cast<uint32_t>(r) : NONE;
+    if (on) G[r] = s;
+  }
+}
+int chain_snapshot(crdtm_tree* t, uint32_t* R, uint32_t* G, Arena& ws, hipStream_t s) {
+  const uint32_t S = static_cast<uint32_t>(t->n_slots), D = static_cast<uint32_t>(t->n_dicts);
+  uint2* ent = ws.alloc<uint2>(S);
+  unsigned long long* excl = ws.alloc<unsigned long long>(S);
+  LAUNCH(k_snap_links, dim3(grid_for(S)), dim3(BLOCK), 0, s, t->d, S, D, ent);
+  int r = list_rank(ent, S, 0u /* the root dict's sentinel */, excl, ws, s);
+  if (r) return r;
+  HIP_CHECK(hipMemsetAsync(G, 0xFF, static_cast<uint64_t>(S) * sizeof(uint32_t), s));
+  LAUNCH(k_snap_scatter, dim3(grid_for(S)), dim3(BLOCK), 0, s, S, excl, R, G);
+  return CRDTM_OK;
+}
+
 int linearize(crdtm_tree* t) {
   crdtm_ctx* c = t->ctx;
   hipStream_t s = c->stream;

@@ -123,9 +123,11 @@ int crdtm_tree_clone(const crdtm_tree *t, crdtm_tree **out);
 /* CRDTree.apply (src/CRDTree.elm:265-269): apply (Batch ops) when is_batch,
  * else the single op ops[0]. Sequential-apply semantics in array order; the
  * first failing op aborts and leaves the tree unchanged (transactional).
- * Any tree, fresh or not: a tree that holds state merges log ++ ops on the
- * parallel paths (res->flags & CRDTM_FLAG_REMERGE) or, when a sequential path
- * is needed, replays ops on the existing state.
+ * Any tree, fresh or not: a tree that holds state takes the ops in place
+ * (a flat document: res->flags & CRDTM_FLAG_INCREMENTAL; per children dict
+ * on the state: CRDTM_FLAG_DICT_INCR), or merges log ++ ops on the parallel
+ * paths (CRDTM_FLAG_REMERGE) or, when a sequential path is needed, replays
+ * ops on the existing state.
  * ops_on_device: 1 if every array of `ops` is device memory (inputs already
  * resident in HBM), 0 for host memory (copied in on the context stream).
  * status_out: optional device (ops_on_device) or host array [n_ops] of CRDTM_ST_*.
