@@ -612,7 +612,7 @@ def run_incr(args, rank, world, local_rank):
     tree = C.c_void_p()
     N.check(L.crdtm_tree_create(ctx, 0, C.byref(tree)), "tree")
     res = N.Result()
-    acct = {"remerge": 0, "incremental": 0, "paths": {}}
+    acct = {"remerge": 0, "incremental": 0, "dict_incr": 0, "paths": {}}
 
     def apply(o):
         N.check(L.crdtm_apply(tree, C.byref(o), 1, 1, None, C.byref(res)), "apply")
@@ -628,6 +628,7 @@ def run_incr(args, rank, world, local_rank):
             apply(o)
             acct["remerge"] += bool(res.flags & N.FLAG_REMERGE)
             acct["incremental"] += bool(res.flags & N.FLAG_INCREMENTAL)
+            acct["dict_incr"] += bool(res.flags & N.FLAG_DICT_INCR)
             acct["paths"][res.path_taken] = acct["paths"].get(res.path_taken, 0) + 1
 
     if args.pmc_child:  # the base document alone, or the base and one step (pmc_live subtracts)
@@ -683,6 +684,7 @@ def run_incr(args, rank, world, local_rank):
                                 f"(config 3 stream), per GPU"),
                    "replicas": spec["replicas"], "window": spec["window"],
                    "batches_remerged": acct["remerge"], "batches_incremental": acct["incremental"],
+                   "batches_level_replay": acct["dict_incr"],
                    "batches": nb * (args.steps + args.warmup),
                    "paths": {({1: "closed-form", 2: "replay", 3: "per-dict replay"}).get(p_, "?"): c_
                              for p_, c_ in acct["paths"].items()},
