@@ -666,6 +666,23 @@ def run_incr(args, rank, world, local_rank):
         nm = labels[j].decode()
         per_k[nm] = per_k.get(nm, 0.0) + ms[j]
         launches[nm] = launches.get(nm, 0) + 1
+    # the state the batches built, against one fresh merge of base ++ batches
+    # (the re-merge path): structure and visible document, hash and size
+    fresh = C.c_void_p()
+    N.check(L.crdtm_tree_create(ctx, 0, C.byref(fresh)), "tree")
+    N.check(L.crdtm_apply(fresh, C.byref(ops_at(0, n)), 1, 1, None, C.byref(res)), "apply")
+
+    def canon(t_):
+        out = []
+        for which in (0, 1):
+            nw, hh = C.c_uint64(), C.c_uint64()
+            N.check(L.crdtm_tree_canonical(t_, which, None, 0, C.byref(nw), C.byref(hh)), "canonical")
+            out.append((nw.value, hh.value))
+        return out
+    verified = res.code == 0 and canon(tree) == canon(fresh)
+    L.crdtm_tree_destroy(fresh)
+    if not verified:
+        raise RuntimeError("incremental state differs from the fresh merge of the same ops")
     ms_step = elapsed / args.steps * 1e3
     # SURVEY.md 8d algorithmic bytes of the step's nb batches (Add 49 + 8L, Delete 9 + 8L)
     a0 = base
@@ -689,6 +706,7 @@ def run_incr(args, rank, world, local_rank):
                    "paths": {({1: "closed-form", 2: "replay", 3: "per-dict replay"}).get(p_, "?"): c_
                              for p_, c_ in acct["paths"].items()},
                    "ms_per_batch": ms_step / nb,
+                   "verified": "final state == fresh merge of base ++ batches (structure + document hashes)",
                    "parallelism": f"one document per GPU ({world} GPU(s)), replicas only"},
         "roofline": roofline("incr", per_k, launches, B_alg, ms_step, 1,
                              live=pmc_live(args) if (rank == 0 and want_pmc(args, world)) else None),

@@ -25,7 +25,7 @@ FLAG_DICT_INCR = 16  # non-fresh tree: replayed per children dict on the state i
 REF_NONE = 2 ** 64 - 1
 REF_ROOT = 2 ** 64 - 2
 REL_PARENT, REL_NEXT, REL_PREV, REL_HEAD = 0, 1, 2, 3
-CODES = {0: "Ok", 1: "InvalidPath", 2: "NotFound", 3: "OperationFailed", -1: "E_ARG", -2: "E_HIP", -3: "E_NOMEM",
+CODES = {0: "Ok", 1: "InvalidPath", 2: "NotFound", 3: "OperationFailed", -1: "E_ARG", -2: "E_HIP", -3: "E_NOMEM", -7: "E_STATE",
          -4: "E_RANGE", -5: "E_NODEVICE", -6: "E_PARSE"}
 
 

@@ -560,12 +560,66 @@ int crdtm_tree_ops_since(const crdtm_tree* t, int64_t ts, crdtm_ops* out) {
   return copy_log_range(t, h - 1, t->log_n, out);
 }
 
+// Every index of the state in range (a read API walks them on the host):
+// the first violation goes to stderr with CRDTM_STATE_DEBUG set.
+static int check_state(const HostTree& h, uint64_t S, uint64_t D, uint64_t L) {
+  static const bool verbose = getenv("CRDTM_STATE_DEBUG") != nullptr;
+  auto bad = [&](const char* what, uint64_t s, uint64_t v) {
+    if (verbose) fprintf(stderr, "crdtm state: slot %llu %s %llu (S %llu D %llu L %llu)\n",
+                         static_cast<unsigned long long>(s), what, static_cast<unsigned long long>(v),
+                         static_cast<unsigned long long>(S), static_cast<unsigned long long>(D),
+                         static_cast<unsigned long long>(L));
+    return CRDTM_E_STATE;
+  };
+  for (uint64_t s = 0; s < S; ++s) {
+    if (h.dict[s] >= D) return bad("dict", s, h.dict[s]);
+    if (h.next[s] != NONE && (h.next[s] >= S || h.dict[h.next[s]] != h.dict[s])) return bad("next", s, h.next[s]);
+    if (h.child[s] != NONE && h.child[s] >= D) return bad("child", s, h.child[s]);
+    if (h.src[s] != NONE && h.src[s] >= L) return bad("src", s, h.src[s]);
+  }
+  for (uint64_t d = 0; d < D; ++d)
+    if (h.d_sent[d] != NONE && h.d_sent[d] >= S) return bad("sentinel of dict", d, h.d_sent[d]);
+  // the dicts the dumps reach (live members' children, from the root): each
+  // once, with a sentinel, its chain inside it and finite
+  if (!D) return CRDTM_OK;
+  std::vector<uint8_t> seen(D, 0);
+  std::vector<uint32_t> todo{0}, ncount(D, 0), moff(D + 1, 0), mem(S);
+  for (uint64_t s = 0; s < S; ++s) ++ncount[h.dict[s]];
+  for (uint64_t d = 0; d < D; ++d) moff[d + 1] = moff[d] + ncount[d];
+  {
+    std::vector<uint32_t> fill(moff.begin(), moff.end() - 1);
+    for (uint64_t s = 0; s < S; ++s) mem[fill[h.dict[s]]++] = static_cast<uint32_t>(s);
+  }
+  seen[0] = 1;
+  while (!todo.empty()) {
+    const uint32_t d = todo.back();
+    todo.pop_back();
+    if (h.d_sent[d] == NONE) return bad("reached dict without a sentinel", d, d);
+    uint64_t steps = 0;
+    for (uint32_t q = h.d_sent[d]; q != NONE; q = h.next[q])
+      if (++steps > ncount[d]) return bad("chain cycle in dict", d, q);
+    for (uint32_t j = moff[d]; j < moff[d + 1]; ++j) {  // (the structure dump walks every member)
+      const uint32_t q = mem[j];
+      if ((h.flags[q] & F_TOMB) || h.child[q] == NONE) continue;
+      if (seen[h.child[q]]) return bad("children dict reached twice", q, h.child[q]);
+      seen[h.child[q]] = 1;
+      todo.push_back(h.child[q]);
+    }
+  }
+  return CRDTM_OK;
+}
+
 int crdtm_tree_canonical(const crdtm_tree* t, int which, int64_t* out, uint64_t cap, uint64_t* n_words,
                          uint64_t* hash) {
   if (!t) return CRDTM_E_ARG;
   HostTree h;
-  int r = fetch(t, h, which == 0);
+  int r = fetch(t, h, false);
   if (r) return r;
+  if ((r = check_state(h, t->n_slots, t->n_dicts, t->log_n))) return r;
+  if (which == 0) {
+    h.members.assign(t->n_dicts, {});
+    for (uint64_t s2 = 0; s2 < t->n_slots; ++s2) h.members[h.dict[s2]].push_back(static_cast<uint32_t>(s2));
+  }
   Sink s{out, cap};
   if (which == 0) dump_dict(h, 0, 0, s);
   else dump_visible(h, 0, 0, s);

@@ -167,6 +167,10 @@ struct IlrArgs {
   uint32_t* dsrc;    // [dicts] a copy made by a same-group deferred copy: its source dict (else NONE)
   uint32_t dnew;     // dicts of the state before the batch
   unsigned long long* stats;  // (CRDTM_ILR_STATS: per group ops, walk steps, tombstone skips, quirks, marks, ticks)
+  // (CRDTM_ILR_OFF: bits switching lane shortcuts off, for bisecting — 1 the
+  // LDS private table, 2 the LDS records, 4 the record cache, 8 the recent
+  // keys, 16 the member-head cache)
+  uint32_t off;
 };
 
 __device__ __forceinline__ unsigned long long ilr_tk_key(uint32_t depth, long long key) {
@@ -257,7 +261,7 @@ struct IlrLane {
   uint4 cr;
   __device__ uint4 getrec(uint32_t s) {
     if (s - lbase < lcnt) return lrec[s - lbase];
-    if (s == cs) return cr;
+    if (s == cs && !(a.off & 4)) return cr;
     cr = a.rec[s];
     cs = s;
     return cr;
@@ -412,7 +416,7 @@ struct IlrLane {
       ps[p] = s;
       ++pused;
     }
-    a.mnext[s] = d == hd_d ? hd_v : a.dhead[d];
+    a.mnext[s] = (d == hd_d && !(a.off & 16)) ? hd_v : a.dhead[d];
     a.dhead[d] = s;
     hd_d = d;
     hd_v = s;
@@ -668,7 +672,8 @@ __global__ void __launch_bounds__(BLOCK) k_ilr_jobs(IlrArgs a, uint32_t L, const
       a.J.freel[atomicAdd(nfree, 1u)] = j;
       continue;
     }
-    if (gd != gs) atomicOr(reinterpret_cast<uint32_t*>(a.J.gflag) + (gs >> 2), GF_SRC << (8 * (gs & 3)));
+    // (a same-group copy too: the lane reads its list only with the flag set)
+    atomicOr(reinterpret_cast<uint32_t*>(a.J.gflag) + (gs >> 2), GF_SRC << (8 * (gs & 3)));
     a.J.next[j] = atomicExch(&a.J.head[gs], j);
   }
 }
@@ -696,6 +701,7 @@ __global__ void __launch_bounds__(64) k_ilr_free(IlrArgs args, uint32_t L, const
   R.hd_d = NONE;
   R.hd_v = NONE;
   R.cs = NONE;
+  R.cr = make_uint4(NONE, 0u, 0u, 0u);
   const uint32_t nf = min(*nfree, args.J.cap);
   for (uint32_t q = 0; q < nf && !R.bad; ++q) {
     const uint32_t j = args.J.freel[q];
@@ -721,7 +727,7 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
   __shared__ long long tpk[PT_LDS];
   __shared__ uint32_t tpd[PT_LDS], tps[PT_LDS];
   const uint32_t pc = args.pcap[g];
-  const bool plds = pc <= PT_LDS;
+  const bool plds = pc <= PT_LDS && !(args.off & 1);
   if (plds) {
     for (uint32_t q = lane; q < pc; q += 64) tps[q] = NONE;
     __syncthreads();
@@ -742,7 +748,7 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
   R.ucnt = 0;
   R.lrec = lrec;
   R.lbase = R.qnext;
-  R.lcnt = min(args.qn[g], ILR_LREC);
+  R.lcnt = (args.off & 2) ? 0u : min(args.qn[g], ILR_LREC);
   R.cpnext = R.cpend = 0;
   R.hd_d = NONE;
   R.hd_v = NONE;
@@ -786,6 +792,7 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
   long long rk0 = 0, rk1 = 0, rk2 = 0, rk3 = 0;
   uint32_t rs0 = NONE, rs1 = NONE, rs2 = NONE, rs3 = NONE;
   auto recent = [&](long long k) -> uint32_t {
+    if (args.off & 8) return NONE;
     return (rs0 != NONE && rk0 == k) ? rs0 : (rs1 != NONE && rk1 == k) ? rs1 : (rs2 != NONE && rk2 == k) ? rs2
            : (rs3 != NONE && rk3 == k) ? rs3 : NONE;
   };
@@ -1369,7 +1376,7 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   a.J = J;
   // the chain order of the state, when a lane has enough ops for long walks
   // (env CRDTM_ILR_SNAPSHOT=0: never)
-  static const char* snap_env = getenv("CRDTM_ILR_SNAPSHOT");
+  const char* snap_env = getenv("CRDTM_ILR_SNAPSHOT");
   const uint32_t snap_min = snap_env ? static_cast<uint32_t>(atoi(snap_env)) : 64u;
   a.R = nullptr;
   a.G = nullptr;
@@ -1385,6 +1392,8 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   }
   a.dsrc = X->dsrc;
   a.dnew = grave;
+  const char* off_env = getenv("CRDTM_ILR_OFF");
+  a.off = off_env ? static_cast<uint32_t>(atoi(off_env)) : 0u;
   static const bool want_stats = getenv("CRDTM_ILR_STATS") != nullptr;
   a.stats = nullptr;
   if (want_stats) {

@@ -41,6 +41,7 @@ extern "C" {
 #define CRDTM_E_RANGE (-4)
 #define CRDTM_E_NODEVICE (-5)
 #define CRDTM_E_PARSE (-6)
+#define CRDTM_E_STATE (-7) /* a read API found an index out of range in the tree state (never on a sound state) */
 
 /* ---- per-op status (updateTree, src/CRDTree.elm:298-325) */
 #define CRDTM_ST_APPLIED 0 /* Ok: logged, lastOperation, replicas */

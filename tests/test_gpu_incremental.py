@@ -27,6 +27,8 @@ STREAMS = {
     "flat_adds": dict(n_ops=60000, replicas=16, window=64, seed=31),
     # config-2 shape: interleaved deletes, branches -> per-dict replay / replay
     "nested_interleaved": dict(n_ops=30000, replicas=8, window=16, p_delete=0.2, p_branch=0.1, max_depth=3, seed=5),
+    # config-2 shape itself (16 replicas, window 64, depth 4): busy dicts, long walks
+    "config2_shape": dict(n_ops=60000, replicas=16, window=64, p_delete=0.2, p_branch=0.1, max_depth=4, seed=0xC0FFEE02),
     # config-4 shape: depth 12, deletes after adds -> nested closed form
     "deep_deletes_last": dict(n_ops=40000, replicas=16, p_delete=1 / 3, max_depth=12, max_children=8,
                               deletes_last=1, seed=9),
@@ -110,8 +112,9 @@ def test_incremental_chain(name, mode, monkeypatch):
     olib().orc_free(ot)
 
 
+@pytest.mark.parametrize("snapshot", ["1", "default"])
 @pytest.mark.parametrize("seed", range(24))
-def test_dict_incremental_adversarial(seed, monkeypatch):
+def test_dict_incremental_adversarial(seed, snapshot, monkeypatch):
     """The per-dict level replay (ilr.hip) on the reference-test-shaped
     adversarial streams (copy quirks, nested copies, orphans, duplicates,
     deletes under deleted branches, errors): each stream applied as a base
@@ -120,6 +123,8 @@ def test_dict_incremental_adversarial(seed, monkeypatch):
     cannot decide fall back to the re-merge, failing ones leave the state
     unchanged."""
     monkeypatch.setenv("CRDTM_INCREMENTAL", "ilr")
+    if snapshot == "1":  # every batch walks over the chain snapshot (by default only batches with a big group)
+        monkeypatch.setenv("CRDTM_ILR_SNAPSHOT", "1")
     from adversarial import adversarial
     from crdtm.tree import pack
     from oracle.oracle import lib as olib
@@ -277,4 +282,38 @@ def test_failed_fresh_batch_then_flat_op(mode, monkeypatch):
         res = et.apply_arrays(sub(s, a, b), b - a)
         assert (res.code, res.err_index if rc else -1) == (rc, oerr if rc else -1), (a, b)
         assert engine_summary(et) == oracle_summary(ot), (a, b)
+    olib().orc_free(ot)
+
+
+def test_level_replay_config2_shape(monkeypatch):
+    """The level replay at the shape of `bench.py --workload incr_cfg2` (a
+    config-2 document, nested typing with interleaved Deletes from 16
+    replicas), scaled down: a 200k-op base, then five 10k-op batches. Every
+    batch takes the level replay or, where its lanes cannot decide, the
+    re-merge (its busy dicts walk over the chain snapshot), and must match the oracle after each batch (structure, document,
+    timestamp, replicas), with the log checked at the end."""
+    monkeypatch.delenv("CRDTM_INCREMENTAL", raising=False)
+    monkeypatch.delenv("CRDTM_ILR_SNAPSHOT", raising=False)
+    from oracle.oracle import lib as olib
+    base, bsz, nb = 200_000, 10_000, 5
+    s = N.synth(n_ops=base + bsz * nb, replicas=16, window=64, p_delete=0.2, p_branch=0.1, max_depth=4,
+                seed=0xC0FFEE02)
+    ot = olib().orc_init(0)
+    et = CRDTree.init(0)
+    cuts = [0, base] + [base + bsz * (j + 1) for j in range(nb)]
+    dict_incr = 0
+    for k, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        chunk = sub(s, a, b)
+        _, rc, _ = oracle_apply_arrays(chunk, b - a, tree=ot)
+        res = et.apply_arrays(chunk, b - a)
+        assert res.code == rc == 0, (k, res.code, rc)
+        if k and res.flags & N.FLAG_DICT_INCR:
+            assert res.path_taken == N.PATH_DICT_REPLAY
+            dict_incr += 1
+        assert engine_summary(et) == oracle_summary(ot), k
+    # (a batch the lanes cannot decide — a chain of copies, a third event on a
+    # slot — goes to the re-merge; most must not)
+    assert dict_incr >= nb - 2, dict_incr
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+    assert engine_log(et, 0) == oracle_log(ot, 0)
     olib().orc_free(ot)
