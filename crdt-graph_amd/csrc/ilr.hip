@@ -852,10 +852,12 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
           rdict = d;
           rs0 = rs1 = rs2 = rs3 = NONE;
         }
+        // (a dict this lane filled by a same-group copy holds entries the
+        // shared hash does not have yet: R.find goes through xmap)
         auto lookup = [&](long long key, uint32_t prek) -> uint32_t {
+          if (!usepre) return R.find(d, key);
           const uint32_t v = R.pfind(d, key);
-          if (v != NONE) return v;
-          return usepre ? prek : slothash_find(args.H, d, key);
+          return v != NONE ? v : prek;
         };
         if (kind == CRDTM_DELETE) {  // deleteHelp (:112-122)
           uint32_t t = recent(kk);

@@ -285,6 +285,33 @@ def test_failed_fresh_batch_then_flat_op(mode, monkeypatch):
     olib().orc_free(ot)
 
 
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("n", [1000, 4000, 16000])
+def test_level_replay_small_config2(n, seed, monkeypatch):
+    """Small config-2-shaped streams (16 replicas typing into nested dicts
+    with Deletes): half as a base, then chunks of varied size through the
+    level replay, every chunk against one oracle tree. Their copy quirks make
+    deferred copies whose source and destination dicts fall in one group
+    (the lane copies, then lands its later ops in the copy)."""
+    monkeypatch.setenv("CRDTM_INCREMENTAL", "ilr")
+    from oracle.oracle import lib as olib
+    s = N.synth(**dict(STREAMS["config2_shape"], n_ops=n, seed=seed))
+    rng = np.random.default_rng(seed)
+    cuts = [0, n // 2]
+    while cuts[-1] < n:
+        cuts.append(min(n, cuts[-1] + int(rng.choice([1, 7, 300, n // 8]))))
+    ot = olib().orc_init(0)
+    et = CRDTree.init(0)
+    for k, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        chunk = sub(s, a, b)
+        _, rc, _ = oracle_apply_arrays(chunk, b - a, tree=ot)
+        res = et.apply_arrays(chunk, b - a)
+        assert res.code == rc == 0, (k, res.code, rc)
+        assert engine_summary(et) == oracle_summary(ot), (k, a, b, res.flags)
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    olib().orc_free(ot)
+
+
 def test_level_replay_config2_shape(monkeypatch):
     """The level replay at the shape of `bench.py --workload incr_cfg2` (a
     config-2 document, nested typing with interleaved Deletes from 16
