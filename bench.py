@@ -595,13 +595,13 @@ def run_incr(args, rank, world, local_rank):
     dev = torch.device("cuda", local_rank)
     tens = {k: torch.from_numpy(s[k]).to(dev) for k in ("kind", "ts", "path", "val")}
     po = s["path_off"].astype(np.int64)
-    offs = {}  # per batch start: its path offsets rebased to 0 (device)
+    offs = {}  # per (start, size): the path offsets rebased to 0 (device)
 
     def ops_at(a, m):
-        if a not in offs:
-            offs[a] = torch.from_numpy((po[a:a + m + 1] - po[a]).astype(np.uint32).view(np.int32)).to(dev)
+        if (a, m) not in offs:
+            offs[a, m] = torch.from_numpy((po[a:a + m + 1] - po[a]).astype(np.uint32).view(np.int32)).to(dev)
         return N.Ops(m, int(po[a + m] - po[a]), tens["kind"].data_ptr() + a, tens["ts"].data_ptr() + 8 * a,
-                     offs[a].data_ptr(), tens["path"].data_ptr() + 8 * int(po[a]), tens["val"].data_ptr() + 4 * a,
+                     offs[a, m].data_ptr(), tens["path"].data_ptr() + 8 * int(po[a]), tens["val"].data_ptr() + 4 * a,
                      None)
 
     base_ops = ops_at(0, base)
@@ -631,6 +631,25 @@ def run_incr(args, rank, world, local_rank):
             acct["dict_incr"] += bool(res.flags & N.FLAG_DICT_INCR)
             acct["paths"][res.path_taken] = acct["paths"].get(res.path_taken, 0) + 1
 
+    def canon(t_):
+        out = []
+        for which in (0, 1):
+            nw, hh = C.c_uint64(), C.c_uint64()
+            N.check(L.crdtm_tree_canonical(t_, which, None, 0, C.byref(nw), C.byref(hh)), "canonical")
+            out.append((nw.value, hh.value))
+        return out
+
+    want = None
+    if not args.pmc_child:  # the expected state: one fresh merge of base ++ batches
+        fresh = C.c_void_p()
+        N.check(L.crdtm_tree_create(ctx, 0, C.byref(fresh)), "tree")
+        N.check(L.crdtm_apply(fresh, C.byref(ops_at(0, n)), 1, 1, None, C.byref(res)), "apply")
+        if res.code != 0:
+            raise RuntimeError(f"fresh merge failed: code {res.code} at op {res.err_index}")
+        want = canon(fresh)
+        L.crdtm_tree_destroy(fresh)
+    check_each = os.environ.get("CRDTM_BENCH_CHECK_EACH") is not None  # (debug: every step's state)
+
     if args.pmc_child:  # the base document alone, or the base and one step (pmc_live subtracts)
         rebuild()
         if args.pmc_child == "step":
@@ -641,7 +660,11 @@ def run_incr(args, rank, world, local_rank):
         return None
     for _ in range(args.warmup):
         rebuild()
+        if check_each:
+            print("base state", canon(tree), file=sys.stderr, flush=True)
         step()
+        if check_each:
+            print("warmup state", canon(tree) == want, canon(tree), want, file=sys.stderr, flush=True)
     elapsed = 0.0
     for _ in range(args.steps):
         rebuild()
@@ -650,6 +673,8 @@ def run_incr(args, rank, world, local_rank):
         step()
         torch.cuda.synchronize()
         elapsed += time.perf_counter() - t0
+        if check_each:
+            print("step state", canon(tree) == want, canon(tree), want, file=sys.stderr, flush=True)
     # per-kernel device time of one incremental batch (the last one of a step)
     rebuild()
     for o in batches[:-1]:
@@ -668,21 +693,9 @@ def run_incr(args, rank, world, local_rank):
         launches[nm] = launches.get(nm, 0) + 1
     # the state the batches built, against one fresh merge of base ++ batches
     # (the re-merge path): structure and visible document, hash and size
-    fresh = C.c_void_p()
-    N.check(L.crdtm_tree_create(ctx, 0, C.byref(fresh)), "tree")
-    N.check(L.crdtm_apply(fresh, C.byref(ops_at(0, n)), 1, 1, None, C.byref(res)), "apply")
-
-    def canon(t_):
-        out = []
-        for which in (0, 1):
-            nw, hh = C.c_uint64(), C.c_uint64()
-            N.check(L.crdtm_tree_canonical(t_, which, None, 0, C.byref(nw), C.byref(hh)), "canonical")
-            out.append((nw.value, hh.value))
-        return out
-    verified = res.code == 0 and canon(tree) == canon(fresh)
-    L.crdtm_tree_destroy(fresh)
+    verified = canon(tree) == want
     if not verified:
-        raise RuntimeError("incremental state differs from the fresh merge of the same ops")
+        raise RuntimeError(f"incremental state differs from the fresh merge of the same ops: {canon(tree)} {want}")
     ms_step = elapsed / args.steps * 1e3
     # SURVEY.md 8d algorithmic bytes of the step's nb batches (Add 49 + 8L, Delete 9 + 8L)
     a0 = base
