@@ -47,9 +47,17 @@ namespace crdtm {
 __device__ unsigned long long g_pdr_stats[8];
 __device__ bool pdr_stat_on;  // (unused)
 #define PDR_STAT(k) do { ++g_stc[k]; } while (0)
+#define PDR_CAT(c) (q_cat = (c))
 #else
 #define PDR_STAT(k) do { } while (0)
+#define PDR_CAT(c) do { } while (0)
 #endif
+
+// A wave-uniform load of data no kernel writes while this one runs, through
+// the scalar data cache (counted by lgkmcnt: it does not wait for the wave's
+// outstanding vector stores the way a vector load does)
+typedef const __attribute__((address_space(4))) uint32_t* ConstU32;
+__device__ __forceinline__ uint32_t ld_scalar(const uint32_t* p, uint32_t i) { return ((ConstU32)p)[i]; }
 
 constexpr uint32_t PM = 0xFFFFFFu;  // slot index mask; PM = end of chain
 enum : uint32_t { SF_TOMB = 1u << 24, SF_ORPHAN = 2u << 24, SF_COPY = 4u << 24, SF_MADE = 8u << 24 };
@@ -556,6 +564,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
   uint32_t nb = 1;
 #ifdef PDR_STATS
   unsigned long long g_stc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long q_cnt[5] = {0, 0, 0, 0, 0}, q_cyc[5] = {0, 0, 0, 0, 0};
 #endif
   __syncthreads();
   const uint32_t ob = rb, oe = p.rbase[D + 1] - 1;
@@ -719,8 +728,13 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
         done = true;
         break;
       }
+#ifdef PDR_STATS
+      const long long q_t0 = clock64();
+      uint32_t q_cat = 4;
+#endif
       uint8_t s;
       if (whi >> 31) {  // deleteHelp
+        PDR_CAT(0);
         const uint32_t t = wlo & PM;
         const uint32_t w = (t == 0 || t == OW_NF) ? 0u : wfu(t);
         if (t == 0) {
@@ -755,239 +769,271 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
           s = ST_ALREADY;
         } else if (!(wa & WF_MADE)) {
           s = ST_NOTFOUND;
-        } else if ((wa & WB_NONE) != WB_NONE) {
-          // ---- findInsertion over the blocks ----
-          const uint32_t ba = wa & WB_NONE;
-          uint32_t b = ba, cnt, nxb;
-          uint32_t e = load_blk(b, cnt, nxb);
-          const uint32_t i0 = idx_of(e, an);
-          uint32_t s0 = i0 + 1;
-          bool carry = true;        // the entry before the window: live or the anchor
-          uint32_t prev_r = an;     // that entry
-          uint32_t nkc = an;        // the compare entry that led to the latest node
-          bool at_anchor = true;    // no node visited yet
-          uint32_t node, nk, nxt;   // result (nxt: the rank after node, PM = none)
-          uint32_t cur_b = b, cur_e = e, cur_cnt = cnt, cur_nxb = nxb, node_i = i0;  // node's block (when loaded)
-          bool gfail = false;  // a Tombstone above x met by the walk (guard G)
-          for (;;) {
-            const bool valid = lane >= s0 && lane < cnt;
-            const unsigned long long ml = __ballot(valid && !(e & BE_T));
-            const unsigned long long mkey = __ballot(valid && (e & 0x7FFFu) < x);
-            const unsigned long long mval = __ballot(valid);
-            unsigned long long mc = (ml << 1) & mval;
-            if (carry && s0 < cnt) mc |= 1ULL << s0;
-            const unsigned long long m1 = mc & mkey;
-            const int j1 = m1 ? __builtin_ctzll(m1) : -1;
-            int j2 = -1;
-            if (ml) {
-              const int ll = 63 - __builtin_clzll(ml);
-              if (static_cast<uint32_t>(ll) + 1 < cnt) j2 = ll + 1;
-            } else if (carry && s0 < cnt) {
-              j2 = static_cast<int>(s0);
-            }
-            int j = -1;
-            if (j1 >= 0 && (j2 < 0 || j1 <= j2)) {
-              j = j1;
-            } else if (j2 >= 0) {  // nothing live after j2 in this block: anything live further on?
-              bool any = false;
-              for (uint32_t bb = nxb; bb != WB_NONE && !any;) {
-                uint32_t c2, n2;
-                const uint32_t e2 = load_blk(bb, c2, n2);
-                any = __ballot(lane < c2 && !(e2 & BE_T)) != 0;
-                bb = n2;
+        } else {
+          // an anchor on the chain walks the blocks; an orphan anchor (off the
+          // chain, rare) first follows the slot words as pdr_serial does, and
+          // once a live step lands on a chain entry the rest of the walk is the
+          // block walk anchored there
+          uint32_t an_w = an, wa_w = wa;
+          bool ow = (wa & WB_NONE) == WB_NONE;
+          uint32_t o_node = an, o_nk = an, o_wn = 0;
+          bool o_gfail = false;
+          if (ow) {
+            o_wn = ld_uniform(S, an);
+            for (;;) {
+              const uint32_t rn = o_wn & PM;
+              if (rn == PM) break;
+              uint32_t wl = ld_uniform(S, rn);
+              if constexpr (GST)
+                if ((wl & SF_TOMB) && x < rn) o_gfail = true;
+              const uint32_t live = pdr_next_live(S, K, lane, rn, wl STC_ARG);
+              if (live == PM) break;
+              if (x > rn) break;
+              o_nk = rn;
+              o_node = live;
+              o_wn = wl;
+              if (live == rn) {
+                const uint32_t wv = wfu(live);
+                if ((wv & WB_NONE) != WB_NONE) {
+                  an_w = live;
+                  wa_w = wv;
+                  ow = false;
+                  break;
+                }
               }
-              if (!any) j = j2;  // nextNode is Nothing: stop
             }
-            if (j >= 0) {
-              const uint32_t uj = static_cast<uint32_t>(j);
-              // compare entries passed before the stop are above x; the stop
-              // entry is above x only when nothing live follows it
-              if constexpr (GST) {
-                const unsigned long long mtomb = mval & ~ml;
-                if ((mc & mtomb & ((1ULL << uj) - 1ULL)) || (((mtomb & ~mkey) >> uj) & 1ULL)) gfail = true;
+          }
+          if (!ow) {
+            // ---- findInsertion over the blocks ----
+            const uint32_t ba = wa_w & WB_NONE;
+            uint32_t b = ba, cnt, nxb;
+            uint32_t e = load_blk(b, cnt, nxb);
+            const uint32_t i0 = idx_of(e, an_w);
+            uint32_t s0 = i0 + 1;
+            bool carry = true;        // the entry before the window: live or the anchor
+            uint32_t prev_r = an_w;     // that entry
+            uint32_t nkc = an_w;        // the compare entry that led to the latest node
+            bool at_anchor = true;    // no node visited yet
+            uint32_t node, nk, nxt;   // result (nxt: the rank after node, PM = none)
+            uint32_t cur_b = b, cur_e = e, cur_cnt = cnt, cur_nxb = nxb, node_i = i0;  // node's block (when loaded)
+            bool gfail = o_gfail;  // a Tombstone above x met by the walk (guard G)
+            for (;;) {
+              const bool valid = lane >= s0 && lane < cnt;
+              const unsigned long long ml = __ballot(valid && !(e & BE_T));
+              const unsigned long long mkey = __ballot(valid && (e & 0x7FFFu) < x);
+              const unsigned long long mval = __ballot(valid);
+              unsigned long long mc = (ml << 1) & mval;
+              if (carry && s0 < cnt) mc |= 1ULL << s0;
+              const unsigned long long m1 = mc & mkey;
+              const int j1 = m1 ? __builtin_ctzll(m1) : -1;
+              int j2 = -1;
+              if (ml) {
+                const int ll = 63 - __builtin_clzll(ml);
+                if (static_cast<uint32_t>(ll) + 1 < cnt) j2 = ll + 1;
+              } else if (carry && s0 < cnt) {
+                j2 = static_cast<int>(s0);
               }
-              nxt = rk(e, uj);
-              if (uj == s0) {  // node = the entry before the window
-                node = prev_r;
-                nk = at_anchor ? an : nkc;
-                if (b != ba || !at_anchor) {  // node sits in an earlier block: reload at insert
-                  cur_b = WB_NONE;
+              int j = -1;
+              if (j1 >= 0 && (j2 < 0 || j1 <= j2)) {
+                j = j1;
+              } else if (j2 >= 0) {  // nothing live after j2 in this block: anything live further on?
+                bool any = false;
+                for (uint32_t bb = nxb; bb != WB_NONE && !any;) {
+                  uint32_t c2, n2;
+                  const uint32_t e2 = load_blk(bb, c2, n2);
+                  any = __ballot(lane < c2 && !(e2 & BE_T)) != 0;
+                  bb = n2;
+                }
+                if (!any) j = j2;  // nextNode is Nothing: stop
+              }
+              if (j >= 0) {
+                const uint32_t uj = static_cast<uint32_t>(j);
+                // compare entries passed before the stop are above x; the stop
+                // entry is above x only when nothing live follows it
+                if constexpr (GST) {
+                  const unsigned long long mtomb = mval & ~ml;
+                  if ((mc & mtomb & ((1ULL << uj) - 1ULL)) || (((mtomb & ~mkey) >> uj) & 1ULL)) gfail = true;
+                }
+                nxt = rk(e, uj);
+                if (uj == s0) {  // node = the entry before the window
+                  node = prev_r;
+                  nk = at_anchor ? an_w : nkc;
+                  if (b != ba || !at_anchor) {  // node sits in an earlier block: reload at insert
+                    cur_b = WB_NONE;
+                  } else {
+                    cur_b = b;
+                    cur_e = e;
+                    cur_cnt = cnt;
+                    cur_nxb = nxb;
+                    node_i = i0;
+                  }
                 } else {
+                  node = rk(e, uj - 1);
+                  const unsigned long long mcl = mc & ((2ULL << (uj - 1)) - 1ULL);
+                  nk = mcl ? rk(e, 63u - static_cast<uint32_t>(__builtin_clzll(mcl))) : nkc;
                   cur_b = b;
                   cur_e = e;
                   cur_cnt = cnt;
                   cur_nxb = nxb;
-                  node_i = i0;
+                  node_i = uj - 1;
                 }
-              } else {
-                node = rk(e, uj - 1);
-                const unsigned long long mcl = mc & ((2ULL << (uj - 1)) - 1ULL);
-                nk = mcl ? rk(e, 63u - static_cast<uint32_t>(__builtin_clzll(mcl))) : nkc;
-                cur_b = b;
-                cur_e = e;
-                cur_cnt = cnt;
-                cur_nxb = nxb;
-                node_i = uj - 1;
+                break;
               }
-              break;
-            }
-            if constexpr (GST)
-              if (mc & mval & ~ml) gfail = true;  // (no stop in this block: every compare entry passed)
-            if (mc) nkc = rk(e, 63u - static_cast<uint32_t>(__builtin_clzll(mc)));
-            if (cnt > s0) {
-              carry = (ml >> (cnt - 1)) & 1ULL;
-              prev_r = rk(e, cnt - 1);
-              at_anchor = false;
-            }
-            if (nxb == WB_NONE) {  // the chain ends: `next node` is Nothing
-              node = prev_r;
-              nk = at_anchor ? an : nkc;
-              nxt = PM;
-              if (cnt > s0 || (at_anchor && b == ba)) {
-                cur_b = b;
-                cur_e = e;
-                cur_cnt = cnt;
-                cur_nxb = nxb;
-                node_i = cnt > s0 ? cnt - 1 : i0;
-              } else {
-                cur_b = WB_NONE;
+              if constexpr (GST)
+                if (mc & mval & ~ml) gfail = true;  // (no stop in this block: every compare entry passed)
+              if (mc) nkc = rk(e, 63u - static_cast<uint32_t>(__builtin_clzll(mc)));
+              if (cnt > s0) {
+                carry = (ml >> (cnt - 1)) & 1ULL;
+                prev_r = rk(e, cnt - 1);
+                at_anchor = false;
               }
-              break;
+              if (nxb == WB_NONE) {  // the chain ends: `next node` is Nothing
+                node = prev_r;
+                nk = at_anchor ? an_w : nkc;
+                nxt = PM;
+                if (cnt > s0 || (at_anchor && b == ba)) {
+                  cur_b = b;
+                  cur_e = e;
+                  cur_cnt = cnt;
+                  cur_nxb = nxb;
+                  node_i = cnt > s0 ? cnt - 1 : i0;
+                } else {
+                  cur_b = WB_NONE;
+                }
+                break;
+              }
+              b = nxb;
+              s0 = 0;
+              e = load_blk(b, cnt, nxb);
             }
-            b = nxb;
-            s0 = 0;
-            e = load_blk(b, cnt, nxb);
-          }
-          if (gst) {
-            ++g_adds;
-            if (gfail) {
-              ++g_fail;
-              g_first = min(g_first, k0 + jo);
+            if (gst) {
+              ++g_adds;
+              if (gfail) {
+                ++g_fail;
+                g_first = min(g_first, k0 + jo);
+              }
             }
-          }
-          // ---- the two inserts (src/Internal/Node.elm:87-89) ----
-          const uint32_t wx = nxt | SF_MADE;
-          if (lane == 0) S[x] = wx;
-          setwf(x, WF_MADE | WB_NONE);
-          logw(i, x, 0, wx, 0);
-          const uint32_t wnode = wfu(node);
-          if (nk == node) {
-            const uint32_t wn = wf_sflags(wnode) | x;
-            if (lane == 0) S[node] = wn;
-            logw(i, node, 0, wn, 0);
-            if (cur_b != WB_NONE) blk_insert_e(node, cur_b, node_i, x, cur_e, cur_cnt, cur_nxb);
-            else blk_insert(node, x);
-          } else {
-            // copy quirk: slot nk := copy of node with next = x;
-            // the entries after nk up to node drop off the chain
-            blk_orphan_after(nk, node, i);
-            const uint32_t wk = x | SF_MADE | SF_COPY;
-            if (lane == 0) S[nk] = wk;
-            setwf(nk, (wfu(nk) & WB_NONE) | WF_MADE | WF_COPY);
-            logw(i, nk, 0, wk, 0);
-            uint32_t cs, cd, cb;
-            if (wnode & WF_COPY) {
-              cs = p.qsrc[base + node];
-              cd = p.qcd[base + node];
-              cb = p.qcb[base + node];
+            // ---- the two inserts (src/Internal/Node.elm:87-89) ----
+            const uint32_t wx = nxt | SF_MADE;
+            if (lane == 0) S[x] = wx;
+            setwf(x, WF_MADE | WB_NONE);
+            logw(i, x, 0, wx, 0);
+            const uint32_t wnode = wfu(node);
+            PDR_CAT(nk == node ? 1 : 2);
+            if (nk == node) {
+              const uint32_t wn = wf_sflags(wnode) | x;
+              if (lane == 0) S[node] = wn;
+              logw(i, node, 0, wn, 0);
+              if (cur_b != WB_NONE) blk_insert_e(node, cur_b, node_i, x, cur_e, cur_cnt, cur_nxb);
+              else blk_insert(node, x);
             } else {
-              cs = cd = p.rop[rb + node];
-              cb = bound;
-            }
-            if (lane == 0) {
-              p.qsrc[base + nk] = cs;
-              p.qcd[base + nk] = cd;
-              p.qcb[base + nk] = min(cb, i);
-            }
-            logw(i, nk, 1, cs, cd);
-            logw(i, nk, 2, min(cb, i), 0);
-            if (ORIG && lane == 0) atomicMin(&p.tcopy[p.rop[rb + nk]], i);
-            {  // nk's entry is live again (a copy of node)
-              const uint32_t bk = wfu(nk) & WB_NONE;
-              uint32_t c3, n3;
-              const uint32_t e3 = load_blk(bk, c3, n3);
-              const uint32_t jk = idx_of(e3, nk);
-              if (lane == jk) ent[bk * BLK_E + lane] = static_cast<uint16_t>(e3 & 0x7FFFu);
-              blk_insert_e(nk, bk, jk, x, e3 & (lane == jk ? 0x7FFFu : 0xFFFFFFFFu), c3, n3);
-            }
-          }
-          s = ST_APPLIED;
-        } else {
-          // ---- an orphan anchor: pdr_serial's walk over the slot words ----
-          uint32_t node = an, nk = an;
-          uint32_t wn = ld_uniform(S, node);
-          bool gfail = false;
-          for (;;) {
-            const uint32_t rn = wn & PM;
-            if (rn == PM) break;
-            uint32_t wl = ld_uniform(S, rn);
-            if constexpr (GST)
-              if ((wl & SF_TOMB) && x < rn) gfail = true;
-            const uint32_t live = pdr_next_live(S, K, lane, rn, wl STC_ARG);
-            if (live == PM) break;
-            if (x > rn) break;
-            nk = rn;
-            node = live;
-            wn = wl;
-          }
-          if (gst) {
-            ++g_adds;
-            if (gfail) {
-              ++g_fail;
-              g_first = min(g_first, k0 + jo);
-            }
-          }
-          const uint32_t wk = nk == node ? wn : ld_uniform(S, nk);
-          const bool on_chain = !(wk & SF_ORPHAN);
-          const uint32_t wx = (wn & PM) | (wk & SF_ORPHAN) | SF_MADE;
-          if (lane == 0) S[x] = wx;
-          setwf(x, WF_MADE | (on_chain ? 0u : WF_ORPH) | WB_NONE);
-          logw(i, x, 0, wx, 0);
-          if (nk == node) {
-            if (lane == 0) S[node] = (wn & ~PM) | x;
-            logw(i, node, 0, (wn & ~PM) | x, 0);
-            if (on_chain) blk_insert(node, x);
-          } else {
-            if (on_chain) {
+              // copy quirk: slot nk := copy of node with next = x;
+              // the entries after nk up to node drop off the chain
               blk_orphan_after(nk, node, i);
-              wn |= SF_ORPHAN;
+              const uint32_t wk = x | SF_MADE | SF_COPY;
+              if (lane == 0) S[nk] = wk;
+              setwf(nk, (wfu(nk) & WB_NONE) | WF_MADE | WF_COPY);
+              logw(i, nk, 0, wk, 0);
+              uint32_t cs, cd, cb;
+              if (wnode & WF_COPY) {
+                cs = p.qsrc[base + node];
+                cd = p.qcd[base + node];
+                cb = p.qcb[base + node];
+              } else {
+                cs = cd = ld_scalar(p.rop, rb + node);
+                cb = bound;
+              }
+              if (lane == 0) {
+                p.qsrc[base + nk] = cs;
+                p.qcd[base + nk] = cd;
+                p.qcb[base + nk] = min(cb, i);
+              }
+              logw(i, nk, 1, cs, cd);
+              logw(i, nk, 2, min(cb, i), 0);
+              if (ORIG && lane == 0) atomicMin(&p.tcopy[ld_scalar(p.rop, rb + nk)], i);
+              {  // nk's entry is live again (a copy of node)
+                const uint32_t bk = wfu(nk) & WB_NONE;
+                uint32_t c3, n3;
+                const uint32_t e3 = load_blk(bk, c3, n3);
+                const uint32_t jk = idx_of(e3, nk);
+                if (lane == jk) ent[bk * BLK_E + lane] = static_cast<uint16_t>(e3 & 0x7FFFu);
+                blk_insert_e(nk, bk, jk, x, e3 & (lane == jk ? 0x7FFFu : 0xFFFFFFFFu), c3, n3);
+              }
             }
-            const uint32_t wkn = x | (wn & ~PM & ~SF_ORPHAN) | (wk & SF_ORPHAN) | SF_COPY;
-            if (lane == 0) S[nk] = wkn;
-            setwf(nk, (wfu(nk) & WB_NONE) | WF_MADE | WF_COPY | ((wk & SF_ORPHAN) ? WF_ORPH : 0u));
-            logw(i, nk, 0, wkn, 0);
-            uint32_t cs, cd, cb;
-            if (wn & SF_COPY) {
-              cs = p.qsrc[base + node];
-              cd = p.qcd[base + node];
-              cb = p.qcb[base + node];
+            s = ST_APPLIED;
+          } else {
+            // ---- the orphan walk ended off the chain ----
+            PDR_CAT(3);
+            uint32_t node = o_node, nk = o_nk;
+            uint32_t wn = o_wn;
+            if (gst) {
+              ++g_adds;
+              if (o_gfail) {
+                ++g_fail;
+                g_first = min(g_first, k0 + jo);
+              }
+            }
+            const uint32_t wk = nk == node ? wn : ld_uniform(S, nk);
+            const bool on_chain = !(wk & SF_ORPHAN);
+            const uint32_t wx = (wn & PM) | (wk & SF_ORPHAN) | SF_MADE;
+            if (lane == 0) S[x] = wx;
+            setwf(x, WF_MADE | (on_chain ? 0u : WF_ORPH) | WB_NONE);
+            logw(i, x, 0, wx, 0);
+            if (nk == node) {
+              if (lane == 0) S[node] = (wn & ~PM) | x;
+              logw(i, node, 0, (wn & ~PM) | x, 0);
+              if (on_chain) blk_insert(node, x);
             } else {
-              cs = cd = p.rop[rb + node];
-              cb = bound;
+              if (on_chain) {
+                blk_orphan_after(nk, node, i);
+                wn |= SF_ORPHAN;
+              }
+              const uint32_t wkn = x | (wn & ~PM & ~SF_ORPHAN) | (wk & SF_ORPHAN) | SF_COPY;
+              if (lane == 0) S[nk] = wkn;
+              setwf(nk, (wfu(nk) & WB_NONE) | WF_MADE | WF_COPY | ((wk & SF_ORPHAN) ? WF_ORPH : 0u));
+              logw(i, nk, 0, wkn, 0);
+              uint32_t cs, cd, cb;
+              if (wn & SF_COPY) {
+                cs = p.qsrc[base + node];
+                cd = p.qcd[base + node];
+                cb = p.qcb[base + node];
+              } else {
+                cs = cd = ld_scalar(p.rop, rb + node);
+                cb = bound;
+              }
+              if (lane == 0) {
+                p.qsrc[base + nk] = cs;
+                p.qcd[base + nk] = cd;
+                p.qcb[base + nk] = min(cb, i);
+              }
+              logw(i, nk, 1, cs, cd);
+              logw(i, nk, 2, min(cb, i), 0);
+              if (ORIG && lane == 0) atomicMin(&p.tcopy[ld_scalar(p.rop, rb + nk)], i);
+              if (on_chain) {
+                const uint32_t bk = wfu(nk) & WB_NONE;
+                uint32_t c3, n3;
+                const uint32_t e3 = load_blk(bk, c3, n3);
+                const uint32_t jk = idx_of(e3, nk);
+                if (lane == jk) ent[bk * BLK_E + lane] = static_cast<uint16_t>(e3 & 0x7FFFu);
+                blk_insert_e(nk, bk, jk, x, e3 & (lane == jk ? 0x7FFFu : 0xFFFFFFFFu), c3, n3);
+              }
             }
-            if (lane == 0) {
-              p.qsrc[base + nk] = cs;
-              p.qcd[base + nk] = cd;
-              p.qcb[base + nk] = min(cb, i);
-            }
-            logw(i, nk, 1, cs, cd);
-            logw(i, nk, 2, min(cb, i), 0);
-            if (ORIG && lane == 0) atomicMin(&p.tcopy[p.rop[rb + nk]], i);
-            if (on_chain) {
-              const uint32_t bk = wfu(nk) & WB_NONE;
-              uint32_t c3, n3;
-              const uint32_t e3 = load_blk(bk, c3, n3);
-              const uint32_t jk = idx_of(e3, nk);
-              if (lane == jk) ent[bk * BLK_E + lane] = static_cast<uint16_t>(e3 & 0x7FFFu);
-              blk_insert_e(nk, bk, jk, x, e3 & (lane == jk ? 0x7FFFu : 0xFFFFFFFFu), c3, n3);
-            }
+            s = ST_APPLIED;
           }
-          s = ST_APPLIED;
         }
       }
       if (ORIG && lane == 0) st[i] = s;
+#ifdef PDR_STATS
+      ++q_cnt[q_cat];
+      q_cyc[q_cat] += clock64() - q_t0;
+#endif
     }
   }
+#ifdef PDR_STATS  // ops and cycles per kind: Delete, plain insert, copy quirk, orphan anchor, other
+  if (ORIG && lane == 0 && K > 28000)
+    printf("pdr blocked K=%u del %llu/%llu ins %llu/%llu quirk %llu/%llu orphan %llu/%llu other %llu/%llu\n", K,
+           q_cnt[0], q_cyc[0], q_cnt[1], q_cyc[1], q_cnt[2], q_cyc[2], q_cnt[3], q_cyc[3], q_cnt[4], q_cyc[4]);
+#endif
   if (ORIG && lane == 0) p.logn[D] = (logging && ln <= lcap) ? ln : NONE;
   if (gst && lane == 0) pdr_gstat_flush(p, g_adds, g_fail, (g_first == NONE ? oe : g_first) - ob, oe - ob);
   for (uint32_t r = lane; r <= K; r += 64) p.inst[base + r] = I;
