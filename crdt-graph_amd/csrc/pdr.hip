@@ -564,7 +564,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
   uint32_t nb = 1;
 #ifdef PDR_STATS
   unsigned long long g_stc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long q_cnt[5] = {0, 0, 0, 0, 0}, q_cyc[5] = {0, 0, 0, 0, 0};
+  unsigned long long q_cnt[5] = {0, 0, 0, 0, 0}, q_cyc[5] = {0, 0, 0, 0, 0}, q_walk = 0;
 #endif
   __syncthreads();
   const uint32_t ob = rb, oe = p.rbase[D + 1] - 1;
@@ -634,6 +634,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
     if (cnt == BLK_E) {
       if (nb >= nbmax) {  // no free block: repack, then find prev again
         compact();
+        PDR_STAT(3);
         b = wfu(prev) & WB_NONE;
         e = load_blk(b, cnt, nxb);
         i = idx_of(e, prev);
@@ -641,6 +642,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
     }
     if (cnt == BLK_E) {  // split: the upper half moves to a fresh block
       const uint32_t b2 = nb++;
+      PDR_STAT(2);
       if (lane >= 32) {
         ent[b2 * BLK_E + lane - 32] = static_cast<uint16_t>(e);
         const uint32_t r = e & 0x7FFFu;
@@ -842,6 +844,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
                   uint32_t c2, n2;
                   const uint32_t e2 = load_blk(bb, c2, n2);
                   any = __ballot(lane < c2 && !(e2 & BE_T)) != 0;
+                  PDR_STAT(1);
                   bb = n2;
                 }
                 if (!any) j = j2;  // nextNode is Nothing: stop
@@ -905,7 +908,12 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
               b = nxb;
               s0 = 0;
               e = load_blk(b, cnt, nxb);
+              PDR_STAT(0);
             }
+#ifdef PDR_STATS
+            q_walk += clock64() - q_t0;
+            PDR_STAT(4);
+#endif
             if (gst) {
               ++g_adds;
               if (gfail) {
@@ -1031,8 +1039,10 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
   }
 #ifdef PDR_STATS  // ops and cycles per kind: Delete, plain insert, copy quirk, orphan anchor, other
   if (ORIG && lane == 0 && K > 28000)
-    printf("pdr blocked K=%u del %llu/%llu ins %llu/%llu quirk %llu/%llu orphan %llu/%llu other %llu/%llu\n", K,
-           q_cnt[0], q_cyc[0], q_cnt[1], q_cyc[1], q_cnt[2], q_cyc[2], q_cnt[3], q_cyc[3], q_cnt[4], q_cyc[4]);
+    printf("pdr blocked K=%u del %llu/%llu ins %llu/%llu quirk %llu/%llu orphan %llu/%llu other %llu/%llu | walks "
+           "%llu cycles %llu, next blocks %llu, scans %llu, splits %llu, compactions %llu\n", K,
+           q_cnt[0], q_cyc[0], q_cnt[1], q_cyc[1], q_cnt[2], q_cyc[2], q_cnt[3], q_cyc[3], q_cnt[4], q_cyc[4], g_stc[4],
+           q_walk, g_stc[0], g_stc[1], g_stc[2], g_stc[3]);
 #endif
   if (ORIG && lane == 0) p.logn[D] = (logging && ln <= lcap) ? ln : NONE;
   if (gst && lane == 0) pdr_gstat_flush(p, g_adds, g_fail, (g_first == NONE ? oe : g_first) - ob, oe - ob);
