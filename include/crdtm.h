@@ -41,7 +41,8 @@ extern "C" {
 #define CRDTM_E_RANGE (-4)
 #define CRDTM_E_NODEVICE (-5)
 #define CRDTM_E_PARSE (-6)
-#define CRDTM_E_STATE (-7) /* a read API found an index out of range in the tree state (never on a sound state) */
+#define CRDTM_E_STATE (-7) /* crdtm_tree_canonical found the state unsound: an index out of range, a reached
+                              dict without a sentinel, a cyclic chain or a children dict reached twice */
 
 /* ---- per-op status (updateTree, src/CRDTree.elm:298-325) */
 #define CRDTM_ST_APPLIED 0 /* Ok: logged, lastOperation, replicas */
