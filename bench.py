@@ -721,7 +721,7 @@ def run_incr(args, rank, world, local_rank):
                    "ms_per_batch": ms_step / nb,
                    "verified": "final state == fresh merge of base ++ batches (structure + document hashes)",
                    "parallelism": f"one document per GPU ({world} GPU(s)), replicas only"},
-        "roofline": roofline("incr", per_k, launches, B_alg, ms_step, 1,
+        "roofline": roofline(args.workload, per_k, launches, B_alg, ms_step, 1,
                              live=pmc_live(args) if (rank == 0 and want_pmc(args, world)) else None),
     }
     line["roofline"]["note"] = ("per step (all its batches): achieved = the batches' algorithmic bytes / step "
