@@ -89,8 +89,12 @@ enum : uint32_t {
   IW_COPY_BELOW = 2,  // a deferred copy two levels down, or with no lane at its level
   IW_REFILL = 4,      // an op lands under a deleted-then-refilled node before the Delete
   IW_CHAIN = 8,       // a lane both source and target of deferred copies (or > ILR_JOBS)
-  IW_DEPTH = 16       // a deep copy deeper than ILR_MAXL
+  IW_DEPTH = 16,      // a deep copy deeper than ILR_MAXL
+  IW_PENDING = 32     // a copy of a dict a deferred copy of this batch makes
 };
+// dsrc of a dict a deferred copy fills (other lanes never read such a dict
+// in the batch: its filling lane may run in the same launch)
+constexpr uint32_t DS_PENDING = 0xFFFFFFFEu;
 enum : uint32_t { IO_SLOTS = 1, IO_DICTS = 2, IO_UNDO = 4, IO_PRIV = 8, IO_JOBS = 16 };
 enum : uint32_t { IF_NEXT = 0, IF_SRC = 1, IF_CHILD = 2, IF_FLAGS = 3 };
 enum : uint32_t { GF_SRC = 1, GF_DST = 2 };
@@ -306,7 +310,13 @@ struct IlrLane {
   }
   // a dict this lane filled by a deferred copy: its entries are the source's
   // as of the copy (through xmap) or this lane's own later slots
-  __device__ uint32_t copy_src(uint32_t d) const { return d >= a.dnew ? a.dsrc[d] : NONE; }
+  __device__ uint32_t copy_src(uint32_t d) const {
+    if (d < a.dnew) return NONE;
+    const uint32_t v = a.dsrc[d];
+    return v == DS_PENDING ? NONE : v;
+  }
+  // a dict of this batch made by a deferred copy (pending or done)
+  __device__ bool job_made(uint32_t d) const { return d >= a.dnew && a.dsrc[d] != NONE; }
   __device__ uint32_t via_copy(uint32_t d, uint32_t src, long long k) const {
     uint32_t s = pfind(src, k);
     if (s == NONE) s = slothash_find(a.H, src, k);
@@ -459,6 +469,13 @@ struct IlrLane {
   // children dict and a deferred copy for the next level instead.
   __device__ void deep_copy(uint32_t src, uint32_t dst, uint32_t at, uint32_t d0, bool defer = false) {
     uint32_t stk_s[ILR_MAXL], stk_d[ILR_MAXL], stk_m[ILR_MAXL];
+    // a dict without a sentinel is the target of a deferred copy still to
+    // run (a quirk re-filled a slot whose children are such a copy): its
+    // contents as of `at` are not there yet
+    if (a.T.d_sent[src] == NONE || job_made(src)) {
+      conflict(IW_PENDING);
+      return;
+    }
     int sp = 0;
     stk_s[0] = src;
     stk_d[0] = dst;
@@ -503,6 +520,10 @@ struct IlrLane {
           conflict(IW_DEPTH);
           return;
         }
+        if (a.T.d_sent[c] == NONE || job_made(c)) {
+          conflict(IW_PENDING);
+          return;
+        }
         ++sp;
         stk_s[sp] = c;
         stk_d[sp] = nc;
@@ -520,6 +541,7 @@ struct IlrLane {
     a.J.own[j] = node;
     a.J.dst[j] = dst;
     a.J.at[j] = at;
+    a.dsrc[dst] = DS_PENDING;
     return true;
   }
   // run a deferred copy: node's children (a dict of this lane, now exactly as
@@ -1003,6 +1025,7 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
                 args.J.own[j] = node;
                 args.J.dst[j] = nc;
                 args.J.at[j] = i;
+                args.dsrc[nc] = DS_PENDING;
               } else if (c != NONE) {
                 nc = R.new_dict(ls);
                 if (nc == NONE) break;

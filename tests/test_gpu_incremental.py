@@ -312,6 +312,38 @@ def test_level_replay_small_config2(n, seed, monkeypatch):
     olib().orc_free(ot)
 
 
+SHAPES = [  # (replicas, window, p_delete, p_branch, max_depth, seed, chunking seed); the first re-fills
+    # a slot whose children are a deferred copy still to run (its copy must not be taken in the batch)
+    (16, 256, 0.4, 0.3, 3, 903783157, 14),
+    (32, 64, 0.2, 0.3, 6, 11, 11), (8, 16, 0.4, 0.1, 8, 12, 12), (2, 4, 0.05, 0.3, 4, 13, 13),
+    (16, 64, 0.4, 0.05, 2, 14, 14), (4, 256, 0.2, 0.1, 6, 15, 15),
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_level_replay_shapes(shape, monkeypatch):
+    """Level replay chains over stream shapes beyond config 2 (depth 2-8,
+    heavy branching and deleting), every chunk against the oracle."""
+    monkeypatch.setenv("CRDTM_INCREMENTAL", "ilr")
+    from oracle.oracle import lib as olib
+    r, w, pd, pb, md, seed, cseed = shape
+    s = N.synth(n_ops=6000, replicas=r, window=w, p_delete=pd, p_branch=pb, max_depth=md, seed=seed)
+    n = len(s["kind"])
+    rng = np.random.default_rng(cseed)
+    cuts = [0, n // 2]
+    while cuts[-1] < n:
+        cuts.append(min(n, cuts[-1] + int(rng.choice([1, 7, 300, n // 8, n // 4]))))
+    ot = olib().orc_init(0)
+    et = CRDTree.init(0)
+    for k, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        chunk = sub(s, a, b)
+        _, rc, _ = oracle_apply_arrays(chunk, b - a, tree=ot)
+        res = et.apply_arrays(chunk, b - a)
+        assert res.code == rc, (k, res.code, rc)
+        assert engine_summary(et) == oracle_summary(ot), (k, a, b, res.flags)
+    olib().orc_free(ot)
+
+
 def test_level_replay_config2_shape(monkeypatch):
     """The level replay at the shape of `bench.py --workload incr_cfg2` (a
     config-2 document, nested typing with interleaved Deletes from 16
