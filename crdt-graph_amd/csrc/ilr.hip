@@ -680,7 +680,8 @@ __global__ void __launch_bounds__(BLOCK) k_ilr_prep(IlrArgs a, OpsDev o, const u
 // ---- the deferred copies made at level L - 1, to the lanes of level L ----
 __global__ void __launch_bounds__(BLOCK) k_ilr_jobs(IlrArgs a, uint32_t L, const unsigned long long* gk,
                                                     uint32_t gmask, const uint32_t* slot2grp, const uint32_t* jlo_p,
-                                                    const uint32_t* jhi_p, uint32_t* nfree) {
+                                                    const uint32_t* jhi_p, uint32_t* nfree, uint32_t* mark_slots) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *mark_slots = a.dr->ilr_slots;  // (the level's first slot)
   const uint32_t jlo = *jlo_p, jhi = min(*jhi_p, a.J.cap);
   for (uint32_t j = jlo + blockIdx.x * blockDim.x + threadIdx.x; j < jhi; j += gridDim.x * blockDim.x) {
     const uint32_t node = a.J.own[j], dst = a.J.dst[j];
@@ -1089,7 +1090,14 @@ __global__ void k_ilr_mark(const DevResult* d, uint32_t* slots, uint32_t* jobs) 
 __global__ void __launch_bounds__(BLOCK) k_ilr_publish(TreeDev T, SlotHash H, const uint32_t* qoff, const uint32_t* qn,
                                                        const uint8_t* gflag, uint32_t g0, uint32_t cnt,
                                                        uint32_t phase, uint32_t committed, const uint32_t* mark,
-                                                       const DevResult* d, uint32_t cap) {
+                                                       const DevResult* d, uint32_t cap, uint32_t* mark_slots,
+                                                       uint32_t* mark_jobs) {
+  // (the next phase's first slot, or the level's last deferred copy: the
+  // counters as this phase left them)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (mark_slots) *mark_slots = d->ilr_slots;
+    if (mark_jobs) *mark_jobs = d->ilr_jobs;
+  }
   if (d->ilr_overflow || d->ilr_conflict) return;
   if (blockIdx.x < cnt) {
     const uint32_t g = g0 + blockIdx.x;
@@ -1433,26 +1441,25 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
     const uint32_t cnt = lv[L], m = lv[LV_N + L];
     lv_g0[L] = g0;
     uint32_t* mk = marks + 4 * L;
-    LAUNCH(k_ilr_mark, dim3(1), dim3(1), 0, s, dr, mk, nullptr);
-    if (L > 1) {
+    if (L == 1) LAUNCH(k_ilr_mark, dim3(1), dim3(1), 0, s, dr, mk, nullptr);
+    if (L > 1) {  // (which also takes the level's slots mark)
       LAUNCH(k_ilr_jobs, dim3(16), dim3(BLOCK), 0, s, a, L, gk, gsz - 1, slot2grp, marks + 4 * (L - 1) - 2,
-             marks + 4 * (L - 1) + 2, mk + 3);
+             marks + 4 * (L - 1) + 2, mk + 3, mk);
       LAUNCH(k_ilr_free, dim3(1), dim3(64), 0, s, a, L, mk + 3, empty);
     }
     if (cnt) {
       LAUNCH(k_ilr_prep, dim3(grid_for(m, BLOCK, 1024)), dim3(BLOCK), 0, s, a, o, vs, p0, p0 + m);
       for (uint32_t ph = 1; ph <= 2; ++ph) {
-        if (ph == 2) LAUNCH(k_ilr_mark, dim3(1), dim3(1), 0, s, dr, mk + 1, nullptr);
         LAUNCH(k_ilr_level, dim3(cnt), dim3(64), 0, s, a, o, vs, gbeg, gend, g0, L, ph, st);
+        // (phase 1's publish takes phase 2's slots mark, phase 2's the level's jobs mark)
         LAUNCH(k_ilr_publish, dim3(cnt + 64), dim3(BLOCK), 0, s, a.T, a.H, qoff, qn, J.gflag, g0, cnt, ph,
-               a.committed, mk + ph - 1, dr, a.cap_slots);
+               a.committed, mk + ph - 1, dr, a.cap_slots, ph == 1 ? mk + 1 : nullptr, ph == 2 ? mk + 2 : nullptr);
       }
       ++levels;
     } else {  // (only free copies: their slots into the shared hash)
       LAUNCH(k_ilr_publish, dim3(64), dim3(BLOCK), 0, s, a.T, a.H, qoff, qn, J.gflag, g0, 0u, 1u, a.committed, mk,
-             dr, a.cap_slots);
+             dr, a.cap_slots, nullptr, mk + 2);
     }
-    LAUNCH(k_ilr_mark, dim3(1), dim3(1), 0, s, dr, nullptr, mk + 2);
     g0 += cnt;
     p0 += m;
   }
