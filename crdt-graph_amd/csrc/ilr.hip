@@ -587,35 +587,52 @@ __global__ void __launch_bounds__(BLOCK) k_ilr_group(OpsDev o, unsigned long lon
   }
 }
 
-// group boundaries over the sorted keys: flag[k] = 1 at a group's first op (levels >= 1)
-__global__ void __launch_bounds__(BLOCK) k_ilr_gflag(const uint32_t* sk, uint32_t n, uint32_t gbits, uint32_t* flag) {
-  GRID_STRIDE(k, n) flag[k] = ((sk[k] >> gbits) != 0 && (k == 0 || sk[k] != sk[k - 1])) ? 1u : 0u;
+// group boundaries over the sorted keys: flag[k] = 1 at a group's first op
+// (levels >= 1); addf[k] = 1 for an Add of a group (addf[n] = 0)
+__global__ void __launch_bounds__(BLOCK) k_ilr_gflag(const uint32_t* sk, const uint32_t* sv, uint32_t n, uint32_t gbits,
+                                                     OpsDev o, uint32_t* flag, uint32_t* addf) {
+  GRID_STRIDE(k, n + 1) {
+    if (k == n) {
+      addf[n] = 0;
+      continue;
+    }
+    const bool grp = (sk[k] >> gbits) != 0;
+    flag[k] = (grp && (k == 0 || sk[k] != sk[k - 1])) ? 1u : 0u;
+    addf[k] = (grp && o.kind[sv[k]] == CRDTM_ADD) ? 1u : 0u;
+  }
 }
-// group j = [gbeg[j], gend[j]) of the sorted ops; groups and ops per level;
-// per group its Adds (reserved slots) and private table size; group hash
-// slot -> group
-__global__ void __launch_bounds__(BLOCK) k_ilr_glist(const uint32_t* sk, const uint32_t* sv, uint32_t n,
-                                                     uint32_t gbits, const uint32_t* flag, const uint32_t* gidx,
-                                                     OpsDev o, uint32_t* gbeg, uint32_t* gend, uint32_t* lvcnt,
-                                                     uint32_t* lvops, uint32_t* qn, uint32_t* pcap,
+// group j = [gbeg[j], gend[j]) of the sorted ops: its start, and the end of
+// the group before it (the last group ends at n); groups per level; group
+// hash slot -> group
+__global__ void __launch_bounds__(BLOCK) k_ilr_glist(const uint32_t* sk, uint32_t n, uint32_t gbits,
+                                                     const uint32_t* flag, const uint32_t* gidx, const uint32_t* ngrp,
+                                                     uint32_t* gbeg, uint32_t* gend, uint32_t* lvcnt,
                                                      uint32_t* slot2grp) {
+  const uint32_t G = *ngrp;
   GRID_STRIDE(k, n) {
     if (!flag[k]) continue;
     const uint32_t j = gidx[k];
     gbeg[j] = k;
-    const uint32_t L = sk[k] >> gbits;
-    atomicAdd(&lvcnt[L], 1u);
-    uint32_t e = k, adds = 0;
-    do {  // (groups are short; the walk stays inside the group)
-      adds += o.kind[sv[e]] == CRDTM_ADD;
-      ++e;
-    } while (e < n && sk[e] == sk[k]);
-    gend[j] = e;
-    atomicAdd(&lvops[L], e - k);
-    atomicMax(&lvcnt[ILR_MAXL + 3], e - k);  // (the largest group)
-    qn[j] = adds;
-    pcap[j] = ilr_pcap(adds);
+    if (j > 0) gend[j - 1] = k;
+    if (j + 1 == G) gend[j] = n;
+    atomicAdd(&lvcnt[sk[k] >> gbits], 1u);
     slot2grp[sk[k] & ((1u << gbits) - 1u)] = j;
+  }
+}
+// per group: ops per level, the largest group, its Adds (reserved slots) and
+// private table size (adds: exclusive prefix of addf)
+__global__ void __launch_bounds__(BLOCK) k_ilr_gsize(const uint32_t* sk, uint32_t n, uint32_t gbits,
+                                                     const uint32_t* flag, const uint32_t* gidx, const uint32_t* gend,
+                                                     const uint32_t* adds, uint32_t* lvcnt, uint32_t* lvops,
+                                                     uint32_t* qn, uint32_t* pcap) {
+  GRID_STRIDE(k, n) {
+    if (!flag[k]) continue;
+    const uint32_t j = gidx[k], e = gend[j];
+    atomicAdd(&lvops[sk[k] >> gbits], e - k);
+    atomicMax(&lvcnt[ILR_MAXL + 3], e - k);  // (the largest group)
+    const uint32_t a = adds[e] - adds[k];
+    qn[j] = a;
+    pcap[j] = ilr_pcap(a);
   }
 }
 
@@ -1327,10 +1344,15 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   LAUNCH(k_ilr_group, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, gk, gsz - 1, gbits, tk, tsz - 1, sk[0], sv[0], st, dr);
   uint32_t *ks = nullptr, *vs = nullptr;
   if ((r = radix_sort_pairs(sk[0], sv[0], sk[1], sv[1], nd, n, gbits + 7, ws, s, &ks, &vs))) return r;
-  LAUNCH(k_ilr_gflag, dim3(grid_for(n)), dim3(BLOCK), 0, s, ks, n, gbits, flag);
+  uint32_t* addf = ws.alloc<uint32_t>(n + 1);
+  uint32_t* adds = ws.alloc<uint32_t>(n + 1);
+  LAUNCH(k_ilr_gflag, dim3(grid_for(n + 1)), dim3(BLOCK), 0, s, ks, vs, n, gbits, o, flag, addf);
   if ((r = scan_excl_u32(flag, gidx, n, &dr->ilr_groups, ws, s))) return r;
-  LAUNCH(k_ilr_glist, dim3(grid_for(n)), dim3(BLOCK), 0, s, ks, vs, n, gbits, flag, gidx, o, gbeg, gend, lvcnt,
-         lvcnt + LV_N, qn, pcap, slot2grp);
+  if ((r = scan_excl_u32(addf, adds, n + 1, nullptr, ws, s))) return r;
+  LAUNCH(k_ilr_glist, dim3(grid_for(n)), dim3(BLOCK), 0, s, ks, n, gbits, flag, gidx, &dr->ilr_groups, gbeg, gend,
+         lvcnt, slot2grp);
+  LAUNCH(k_ilr_gsize, dim3(grid_for(n)), dim3(BLOCK), 0, s, ks, n, gbits, flag, gidx, gend, adds, lvcnt,
+         lvcnt + LV_N, qn, pcap);
   // reserved slot ranges and private tables: offsets and totals (in lvcnt)
   if ((r = scan_excl_u32(qn, qoff, n + 1, lvcnt + LV_QTOT, ws, s))) return r;
   if ((r = scan_excl_u32(pcap, poff, n + 1, lvcnt + LV_PTOT, ws, s))) return r;
