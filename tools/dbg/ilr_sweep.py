@@ -52,8 +52,9 @@ def main():
     ap.add_argument("--n", type=int, default=6000)
     ap.add_argument("--cases", type=int, default=48)
     ap.add_argument("--only", type=int, default=-1, help="run just this case")
+    ap.add_argument("--rseed", type=int, default=1234, help="seed of the shape draws")
     a = ap.parse_args()
-    rng = np.random.default_rng(1234)
+    rng = np.random.default_rng(a.rseed)
     bad = 0
     for c in range(a.cases):
         cfg = dict(n_ops=a.n, replicas=int(rng.choice([2, 4, 8, 16, 32])), window=int(rng.choice([4, 16, 64, 256])),
