@@ -50,7 +50,10 @@ WORKLOADS = {
     # SURVEY.md §8d config 1 shape: 2 replicas, 10k ops, 70/30 interleaved, depth <= 3
     "cfg1": dict(n_ops=10_000, replicas=2, window=8, p_delete=0.3, p_branch=0.05, max_depth=3, seed=0xC0FFEE01),
 }
-CPU_SAMPLE = {"flat10m": 100_000, "deep10m": 500_000, "deep10m_il": 500_000, "trees": 2_000_000, "cfg2": 100_000, "cfg1": 10_000}
+# CPU baseline samples (ops): config 2 and config 1 whole; the 10M-op batches as large a prefix as a bounded
+# run allows (their per-op CPU cost grows with the document, so a prefix flatters the CPU)
+CPU_SAMPLE = {"flat10m": 1_000_000, "deep10m": 1_000_000, "deep10m_il": 1_000_000, "trees": 2_000_000,
+              "cfg2": 1_000_000, "cfg1": 10_000}
 # 100k documents x 1k ops (80/20), 8 replicas, sharded by
 # document id; 12.5k documents per GPU (100k at 8 GPUs), weak scaling.
 # Incremental merges: a 10M-node document, then successive 10k-op batches of the same stream
@@ -323,22 +326,27 @@ def dry_run(args, rank, world):
     s = N.synth(n_ops=per, n_docs=n_docs, replicas=TREES["replicas"], window=TREES["window"],
                 p_delete=TREES["p_delete"], seed=TREES["seed"])
     doc_off = np.arange(n_docs + 1, dtype=np.uint32) * per
-    ex = shard.Exchange(torch.from_numpy(shard.local_log(s, doc_off, rank, world, TREES["replicas"])))
-    kept = 0
-    for _ in range(args.warmup):
-        ex.gather()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        _, my_off, keep = shard.assemble(ex.gather(), rank, world, n_docs, per)
-        kept = int(keep.sum())
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    local = torch.from_numpy(shard.local_log(s, doc_off, rank, world, TREES["replicas"]))
+    modes = ["all_to_all", "all_gather"] if args.exchange_mode == "both" else [args.exchange_mode]
     n_mine = (n_docs - rank + world - 1) // world
-    ok = kept == n_mine * per and int(my_off[-1]) == kept
-    t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64)
+    res = {}
+    for md in modes:  # every mode must assemble exactly this rank's documents
+        ex = shard.Exchange(local, mode=md if world > 1 else "auto")
+        kept = 0
+        for _ in range(args.warmup):
+            ex.gather()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            _, my_off, keep = shard.assemble(ex.gather(), rank, world, n_docs, per)
+            kept = int(keep.sum())
+        if world > 1:
+            dist.barrier()
+        ok = kept == n_mine * per and int(my_off[-1]) == kept
+        res[md] = (time.perf_counter() - t0, ok, ex)
+    ex = res[modes[0]][2]
+    t = torch.tensor([res[modes[0]][0], 0.0 if all(v[1] for v in res.values()) else 1.0], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     if rank == 0:
@@ -350,6 +358,8 @@ def dry_run(args, rank, world):
                            "parallelism": f"documents sharded by id over {world} rank(s) (gloo)"},
                 "exchange": {"documents": n_docs, "records_per_rank_block": int(getattr(ex, "block", kept)),
                              "mode": ex.mode, "recv_bytes_per_rank": ex.recv_bytes,
+                             "modes": {md: {"mode": v[2].mode, "recv_bytes_per_rank": v[2].recv_bytes,
+                                            "assembled_ok": bool(v[1])} for md, v in res.items()},
                              "assembled_ok": bool(t[1] == 0)}}
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -372,6 +382,9 @@ def main():
     ap.add_argument("--exchange", choices=("auto", "on", "off"), default="auto",
                     help="also run config 5 (op-log all-gather + sharded merge) after a single-document "
                          "workload and attach its line as 'exchange' (auto: when N > 1)")
+    ap.add_argument("--exchange-mode", choices=("both", "all_to_all", "all_gather"), default="both",
+                    help="config 5's op-log exchange at N > 1: all_to_all by document owner, north_star's "
+                         "all_gather of every log, or both (the step timed with each; all_to_all is `value`)")
     ap.add_argument("--force-replay", action="store_true",
                     help="every merge takes the one-lane sequential replay (env CRDTM_FORCE_REPLAY=1): "
                          "measures the fallback cliff on the same batch")
@@ -563,6 +576,7 @@ def main():
         line["exchange"] = {k: ex[k] for k in ("metric", "value", "unit", "ms_per_step", "config")}
         line["exchange"]["roofline_frac"] = ex["roofline"]["frac"]
         line["exchange"]["all_gather_ms"] = ex["all_gather_ms"]  # (the exchange alone: all_to_all or all_gather)
+        line["exchange"]["modes"] = ex["exchange_modes"]  # (each mode's whole step and exchange alone)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -763,7 +777,9 @@ def run_trees(args, rank, world, local_rank, cpu=True):
         logs.append(rec)
     local = torch.from_numpy(np.concatenate(logs)).to(dev)
     del logs
-    ex = shard.Exchange(local)  # records by owner rank (all_to_all); counts exchanged once; persistent buffers
+    # records by owner rank (all_to_all; counts exchanged once; persistent buffers), or the all-gather
+    primary = "all_gather" if args.exchange_mode == "all_gather" else ("auto" if world == 1 else "all_to_all")
+    ex = shard.Exchange(local, mode=primary)
     ctx = C.c_void_p()
     stream = torch.cuda.current_stream()
     N.check(L.crdtm_ctx_create(local_rank, C.c_void_p(stream.cuda_stream), C.byref(ctx)), "ctx")
@@ -772,7 +788,7 @@ def run_trees(args, rank, world, local_rank, cpu=True):
     applied = np.zeros(n_mine, np.uint32)
     state = {}
 
-    def step():
+    def step(ex=ex):
         allrec = ex.gather()
         ops_t, doc_off, _ = shard.assemble(allrec, rank, world, n_docs, per, ctx=ctx)
         n = int(doc_off[-1])
@@ -837,6 +853,32 @@ def run_trees(args, rank, world, local_rank, cpu=True):
         t = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ag_ms = float(t.item()) / args.steps * 1e3
+    # north_star's all-gather beside it: the whole step and the exchange alone, same clocks
+    modes = {ex.mode: {"ms_per_step": elapsed / args.steps * 1e3, "exchange_ms": ag_ms,
+                       "recv_bytes_per_rank": ex.recv_bytes}}
+    if world > 1 and args.exchange_mode == "both":
+        ex2 = shard.Exchange(local, mode="all_gather" if ex.mode == "all_to_all" else "all_to_all")
+        for _ in range(args.warmup):
+            step(ex2)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step(ex2)
+        torch.cuda.synchronize()
+        dist.barrier()
+        e_step = time.perf_counter() - t1
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            ex2.gather()
+        torch.cuda.synchronize()
+        t = torch.tensor([e_step, time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if int(np.sum(code == 0)) != n_mine:
+            raise RuntimeError(f"forest merge ({ex2.mode} exchange): documents returned an error")
+        modes[ex2.mode] = {"ms_per_step": float(t[0]) / args.steps * 1e3,
+                           "exchange_ms": float(t[1]) / args.steps * 1e3, "recv_bytes_per_rank": ex2.recv_bytes}
+        del ex2
     ot = state["ops_t"]
     kinds = ot["kind"][:n].cpu().numpy()
     B_alg = int(np.sum(np.where(kinds == 0, 57, 17)))  # flat documents: L = 1
@@ -855,6 +897,7 @@ def run_trees(args, rank, world, local_rank, cpu=True):
         "roofline": roofline("trees", per_k, launches, B_alg, ms_step, 1,
                              live=pmc_live(args) if (cpu and rank == 0 and want_pmc(args, world)) else None),
         "all_gather_ms": ag_ms,
+        "exchange_modes": modes,
     }
     if args.verbose and rank == 0:
         for nm, v in sorted(per_k.items(), key=lambda kv: -kv[1])[:12]:

@@ -85,6 +85,7 @@ SIGNATURES = [
     ("crdtm_json_canonical", C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     ("crdtm_free", None, [P]),
     ("crdtm_ctx_guard_stats", C.c_int, [P, P]),
+    ("crdtm_debug_poke", C.c_int, [P, C.c_int, C.c_uint64, C.c_uint32]),
     ("crdtm_ctx_profile", C.c_int, [P, C.c_int]),
     ("crdtm_ctx_phase_times", C.c_int, [P, C.c_char_p, C.c_size_t, P, C.c_int]),
 ]

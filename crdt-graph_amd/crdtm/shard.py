@@ -2,11 +2,13 @@
 
 One process per GPU. Every rank hosts some of the R simulated replicas and
 holds, for every document, the ops those replicas authored (their op logs).
-A step is: all-gather the op logs (RCCL over xGMI with backend "nccl"; gloo
-in CPU tests), keep the documents this rank owns (document t -> rank
-t mod world), put each document's ops back in causal order, and merge every
-owned document with `crdtm_forest_apply`. There is no second exchange: the
-documents are independent CRDTrees.
+A step is: exchange the op logs by document owner (document t -> rank
+t mod world) with one all-to-all (RCCL over xGMI with backend "nccl"; gloo in
+CPU tests) — or, in `all_gather` mode (north_star's named collective), an
+all-gather of every rank's whole log, of which each rank keeps its documents —
+put each document's ops back in causal order, and merge every owned document
+with `crdtm_forest_apply`. There is no second exchange: the documents are
+independent CRDTrees.
 
 Op record (4 x int64, flat documents): [doc << 32 | seq, kind << 32 | val, ts, anchor]
 where seq is the op's position in its document's causal stream.
@@ -78,14 +80,26 @@ class Exchange:
             self.recv = local
             self.block = local.shape[0]
             return
+        if mode not in ("auto", "all_to_all", "all_gather"):
+            raise ValueError(f"exchange mode {mode!r}")
         if mode in ("auto", "all_to_all"):
+            ok = 1
             try:
                 self._setup_all_to_all(local)
-                self.mode = "all_to_all"
-                return
             except (RuntimeError, NotImplementedError):
                 if mode == "all_to_all":
                     raise
+                ok = 0
+            if mode == "auto":
+                # every rank takes the same mode: a rank whose setup raised (or
+                # saw an asynchronous error) must not leave the others in the
+                # all-to-all while it all-gathers
+                flag = torch.tensor([ok], dtype=torch.int32, device=local.device)
+                dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+                ok = int(flag.item())
+            if ok:
+                self.mode = "all_to_all"
+                return
         self._setup_all_gather(local)
         self.mode = "all_gather"
 

@@ -595,6 +595,8 @@ static int check_state(const HostTree& h, uint64_t S, uint64_t D, uint64_t L) {
     const uint32_t d = todo.back();
     todo.pop_back();
     if (h.d_sent[d] == NONE) return bad("reached dict without a sentinel", d, d);
+    if (h.dict[h.d_sent[d]] != d || !(h.flags[h.d_sent[d]] & F_SENT))  // (its own sentinel slot)
+      return bad("sentinel slot of dict", d, h.d_sent[d]);
     uint64_t steps = 0;
     for (uint32_t q = h.d_sent[d]; q != NONE; q = h.next[q])
       if (++steps > ncount[d]) return bad("chain cycle in dict", d, q);
@@ -657,6 +659,20 @@ int crdtm_tree_document(const crdtm_tree* tc, uint32_t* vals, uint64_t cap, uint
   } catch (const ArenaOverflow&) {
     return CRDTM_E_NOMEM;
   }
+  return CRDTM_OK;
+}
+
+int crdtm_debug_poke(crdtm_tree* t, int field, uint64_t index, uint32_t value) {
+  if (!t) return CRDTM_E_ARG;
+  uint32_t* a = field == 0 ? t->d.s_next : field == 1 ? t->d.s_child : field == 2 ? t->d.s_dict
+              : field == 3 ? t->d.d_sent : nullptr;
+  const uint64_t lim = field == 3 ? t->n_dicts : t->n_slots;
+  if (!a || index >= lim) return CRDTM_E_ARG;
+  if (int ru = unshare_tree(t, true)) return ru;
+  HIP_CHECK(hipSetDevice(t->ctx->device));
+  HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+  HIP_CHECK(hipMemcpy(a + index, &value, sizeof(value), hipMemcpyHostToDevice));
+  ++t->version;  // (the host caches of this version are stale)
   return CRDTM_OK;
 }
 
@@ -1094,7 +1110,14 @@ int trav_cache(const crdtm_tree* tc, TravCache*& out) {
   if (c->version != t->version) {
     c->h = HostTree();
     int r = fetch(t, c->h, false);
-    if (r) return r;
+    // the walk follows the copy's indices on the host: an unsound state is
+    // CRDTM_E_STATE here, like crdtm_tree_canonical, never a wild read
+    if (!r) r = check_state(c->h, t->n_slots, t->n_dicts, t->log_n);
+    if (r) {
+      c->h = HostTree();
+      c->version = ~0ULL;
+      return r;
+    }
     c->index.clear();
     c->index.reserve(c->h.key.size() * 2);
     for (uint32_t sl = 0; sl < c->h.key.size(); ++sl) c->index[{c->h.dict[sl], c->h.key[sl]}] = sl;

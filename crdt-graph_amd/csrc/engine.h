@@ -283,6 +283,8 @@ constexpr int R_INCR = 1 << 20;
 int sync_read(crdtm_ctx* c);
 // replicas[replicaId t] := t over the applied ops (st) into `rep`; collected by take_replicas after a sync
 int replica_fold(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, Arena& ws, hipStream_t s);
+int replica_fold_into(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, uint32_t* rlist,
+                      hipStream_t s);
 int take_replicas(crdtm_tree* t, const long long* rep_dev);
 // incr.hip: adds-only flat batch into a clean flat tree; *handled = false leaves it to apply_batch
 int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res, bool* handled);

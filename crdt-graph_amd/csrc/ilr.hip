@@ -52,6 +52,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "engine.h"
@@ -1389,6 +1390,12 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   J.freel = ws.alloc<uint32_t>(jcap);
   J.cap = jcap;
   uint32_t* empty = ws.alloc<uint32_t>(16);
+  // the commit's arrays are taken before the first level changes the state
+  // in place: past that point an arena overflow would leave it half written
+  uint32_t* appl = ws.alloc<uint32_t>(n + 1);
+  uint32_t* plen = ws.alloc<uint32_t>(n + 1);
+  long long* rep = ws.alloc<long long>(2 * static_cast<uint64_t>(n) + 2);
+  uint32_t* rlist = ws.alloc<uint32_t>(std::min<uint64_t>(n, REPLICA_SLOTS) + 1);
   IlrPrep P;
   P.w1 = ws.alloc<uint4>(n + 1);
   P.w2 = ws.alloc<uint4>(n + 1);
@@ -1517,11 +1524,15 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
               v[1], v[2], v[3], v[4], v[7], v[5] / 100.0);
     }
   }
-  if (h.ilr_conflict || h.ilr_overflow || drift || h.err_index != NONE) {
+  // every level's changes, undone deepest level first
+  auto rollback = [&]() {
     for (uint32_t L = maxlen; L >= 1; --L)
       if (lv[L])
         LAUNCH(k_ilr_rollback, dim3(grid_for(lv[L])), dim3(BLOCK), 0, s, t->d, undo, ucnt, gbeg, lv_g0[L], lv[L]);
     t->ilr_valid = false;  // (its hash, member lists and event times hold the batch)
+  };
+  if (h.ilr_conflict || h.ilr_overflow || drift || h.err_index != NONE) {
+    rollback();
     if (h.ilr_conflict || h.ilr_overflow || drift) {  // the re-merge decides
       HIP_CHECK(hipStreamSynchronize(s));
       ws.used = mark0;
@@ -1540,13 +1551,30 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
     return CRDTM_OK;
   }
   // ---- commit: log (applied ops in order), sources, dropped children, replicas ----
+  // Until k_ilr_fix runs, the level changes can still be undone: a failure
+  // there (an arena overflow in a scan's workspace, which crdtm_apply retries
+  // with a larger arena, or an error) rolls the state back first.
+  // (test hook, env CRDTM_ILR_FAIL_COMMIT=<token>: the first commit that
+  // sees a new token fails here with an arena overflow, so the tests can
+  // check the rollback and crdtm_apply's retry)
+  static std::string fail_token;
+  try {
+    const char* fe = getenv("CRDTM_ILR_FAIL_COMMIT");
+    if (fe && fe[0] && fail_token != fe) {
+      fail_token = fe;
+      throw ArenaOverflow(ws.cap + 1);
+    }
+    LAUNCH(k_post_flags, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, appl, plen);
+    if (!(r = scan_excl_u32(appl, appl, n, &dr->log_n, ws, s))) r = scan_excl_u32(plen, plen, n, &dr->log_npath, ws, s);
+  } catch (const ArenaOverflow&) {
+    rollback();
+    throw;
+  }
+  if (r) {
+    rollback();
+    return r;
+  }
   *handled = true;
-  uint32_t* appl = ws.alloc<uint32_t>(n + 1);
-  uint32_t* plen = ws.alloc<uint32_t>(n + 1);
-  long long* rep = ws.alloc<long long>(2 * static_cast<uint64_t>(n) + 2);
-  LAUNCH(k_post_flags, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, appl, plen);
-  if ((r = scan_excl_u32(appl, appl, n, &dr->log_n, ws, s))) return r;
-  if ((r = scan_excl_u32(plen, plen, n, &dr->log_npath, ws, s))) return r;
   LAUNCH(k_log, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, st, t->d, static_cast<uint32_t>(t->log_n),
          static_cast<uint32_t>(t->log_npath), appl, plen);
   LAUNCH(k_log_tail, dim3(1), dim3(1), 0, s, t->d, static_cast<uint32_t>(t->log_n), &dr->log_n,
@@ -1556,10 +1584,14 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   LAUNCH(k_ilr_fix, dim3(fx), dim3(BLOCK), 0, s, t->d, lo, hi, undo, static_cast<uint32_t>(nu), appl,
          static_cast<uint32_t>(t->log_n), X->ev);
   LAUNCH(k_ilr_ev_reset, dim3(fx), dim3(BLOCK), 0, s, lo, hi, undo, static_cast<uint32_t>(nu), X->ev);
-  if ((r = replica_fold(c, o, st, rep, ws, s))) return r;
-  if (st_out) LAUNCH(k_status_out, dim3(grid_for(n)), dim3(BLOCK), 0, s, st, n, NONE, st_out);
-  if ((r = sync_read(c))) return r;
-  if ((r = take_replicas(t, rep))) return r;
+  // (past k_ilr_fix only a device error can fail: the state is then lost
+  // with the device context, and the index is dropped)
+  if (!(r = replica_fold_into(c, o, st, rep, rlist, s)) && st_out)
+    LAUNCH(k_status_out, dim3(grid_for(n)), dim3(BLOCK), 0, s, st, n, NONE, st_out);
+  if (r || (r = sync_read(c)) || (r = take_replicas(t, rep))) {
+    t->ilr_valid = false;
+    return r;
+  }
   X->hused = h.ilr_slots;
   t->n_slots = h.ilr_slots;
   t->n_dicts = h.ilr_dicts;

@@ -3164,9 +3164,15 @@ __global__ void __launch_bounds__(BLOCK) k_post_flags(OpsDev o, const uint8_t* s
 static_assert(offsetof(DevResult, n_rep_list) == offsetof(DevResult, n_replica_out) + sizeof(uint32_t),
               "one memset clears both counters");
 int replica_fold(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, Arena& ws, hipStream_t s) {
+  uint32_t* rlist = ws.alloc<uint32_t>(std::min<uint64_t>(o.n, REPLICA_SLOTS) + 1);
+  return replica_fold_into(c, o, st, rep, rlist, s);
+}
+
+// (rlist: min(n, REPLICA_SLOTS) + 1 words, taken by the caller)
+int replica_fold_into(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, uint32_t* rlist,
+                      hipStream_t s) {
   DevResult* dr = c->dres;
   const uint32_t n = o.n;
-  uint32_t* rlist = ws.alloc<uint32_t>(std::min<uint64_t>(n, REPLICA_SLOTS) + 1);
   HIP_CHECK(hipMemsetAsync(&dr->n_replica_out, 0, 2 * sizeof(uint32_t), s));  // n_replica_out, n_rep_list
   LAUNCH(k_rep_max, dim3(rep_grid(n)), dim3(BLOCK), 0, s, o, st, c->rtab, rlist, &dr->n_rep_list, rep_per(n));
   LAUNCH(k_rep_out, dim3(64), dim3(BLOCK), 0, s, o, c->rtab, rlist, &dr->n_rep_list, rep, &dr->n_replica_out,

@@ -84,6 +84,7 @@ Node* nextNode(Node* node, Dict& c) {
 // walk met a Tombstone above their timestamp as a raw `next` key.
 struct GStats {
   uint64_t walked = 0, fail = 0;
+  uint64_t reached = 0;  // ops whose path resolution reached their dict (update called the leaf function)
 };
 thread_local GStats g_gstats;
 
@@ -164,7 +165,10 @@ template <class F>
 int update(F&& func, const int64_t* p, size_t len, Node& parent) {
   if (parent.kind == TOMB) return N_ALREADY;
   if (len == 0) return N_INVALID;
-  if (len == 1) return func(p[0], parent);
+  if (len == 1) {
+    ++g_gstats.reached;  // (statistics only)
+    return func(p[0], parent);
+  }
   Node* found = child(p[0], parent);
   if (!found) return N_INVALID;
   return update(func, p + 1, len - 1, *found);
@@ -416,10 +420,13 @@ int orc_apply(orc_tree* o, int is_batch, int local, uint64_t n_ops, const uint8_
 }
 
 // guard G statistics of the last orc_apply: out[0] Adds whose findInsertion
-// walk ran, out[1] those that met a Tombstone above their timestamp
+// walk ran, out[1] those that met a Tombstone above their timestamp, out[2]
+// the ops whose path resolution reached their dict (no Tombstone on the way,
+// no missing child)
 void orc_guard_stats(uint64_t* out) {
   out[0] = g_gstats.walked;
   out[1] = g_gstats.fail;
+  out[2] = g_gstats.reached;
 }
 
 int64_t orc_timestamp(const orc_tree* o) { return o->t.timestamp; }

@@ -32,6 +32,14 @@ def test_self_launch_dry_run(world):
     line = json.loads(lines[0])
     assert line["n_gpus"] == world and line["dry_run"] is True and line["value"] is None
     assert line["exchange"]["assembled_ok"] is True and line["exchange"]["documents"] == 8 * world
+    # both exchange modes (--exchange-mode both, the default): the all-to-all by
+    # owner and north_star's all-gather each assemble exactly the rank's documents
+    modes = line["exchange"]["modes"]
+    assert set(modes) == {"all_to_all", "all_gather"}
+    for md, v in modes.items():
+        assert v["mode"] == md and v["assembled_ok"] is True, (md, v)
+    # the all-gather receives every rank's whole (padded) log: more bytes than the all-to-all
+    assert modes["all_gather"]["recv_bytes_per_rank"] > modes["all_to_all"]["recv_bytes_per_rank"]
 
 
 def test_rank_count_mismatch_fails():

@@ -370,9 +370,122 @@ def test_level_replay_config2_shape(monkeypatch):
             assert res.path_taken == N.PATH_DICT_REPLAY
             dict_incr += 1
         assert engine_summary(et) == oracle_summary(ot), k
-    # (a batch the lanes cannot decide — a chain of copies, a third event on a
-    # slot — goes to the re-merge; most must not)
-    assert dict_incr >= nb - 2, dict_incr
+    # every batch of this shape is decided by the level replay itself (no
+    # re-merge fallback: the bench sees none either)
+    assert dict_incr == nb, dict_incr
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    olib().orc_free(ot)
+
+
+def _statuses_match_last_operation(st, chunk, m, ot):
+    """Per-op statuses against the oracle: the ops with status Applied are
+    exactly lastOperation (src/CRDTree.elm:298-325, :328-334), in order."""
+    applied = np.nonzero(st[:m] == 0)[0]
+    want, _ = oracle_log(ot, 1)
+    off = chunk["path_off"]
+    got = [(int(chunk["kind"][i]), int(chunk["ts"][i]) if chunk["kind"][i] == 0 else 0,
+            tuple(int(x) for x in chunk["path"][off[i]:off[i + 1]]), int(chunk["val"][i]) if chunk["kind"][i] == 0 else 0)
+           for i in applied]
+    return got == want
+
+
+def test_level_replay_incr_cfg2_bench_shape(monkeypatch):
+    """`bench.py --workload incr_cfg2` at its own shape (INCR_CFG2: a 900k-op
+    config-2 document, seed 0xC0FFEE02, then ten 10k-op batches), every batch
+    against orc_apply on one oracle tree (src/CRDTree.elm:265-269): the dict
+    structure, the visible document, timestamp, replicas, lastOperation and
+    every op's status; each batch must be served by the level replay itself."""
+    monkeypatch.delenv("CRDTM_INCREMENTAL", raising=False)
+    monkeypatch.delenv("CRDTM_ILR_SNAPSHOT", raising=False)
+    from oracle.oracle import lib as olib
+    base, bsz, nb = 900_000, 10_000, 10
+    s = N.synth(n_ops=base + bsz * nb, replicas=16, window=64, p_delete=0.2, p_branch=0.1, max_depth=4,
+                seed=0xC0FFEE02)
+    ot = olib().orc_init(0)
+    et = CRDTree.init(0)
+    first = sub(s, 0, base)
+    _, rc, _ = oracle_apply_arrays(first, base, tree=ot)
+    assert et.apply_arrays(first, base).code == rc == 0
+    assert engine_summary(et) == oracle_summary(ot)
+    for j in range(nb):
+        a, b = base + j * bsz, base + (j + 1) * bsz
+        chunk = sub(s, a, b)
+        _, rc, _ = oracle_apply_arrays(chunk, bsz, tree=ot)
+        st = np.full(bsz, 9, np.uint8)
+        res = et.apply_arrays(chunk, bsz, status=st)
+        assert res.code == rc == 0, (j, res.code, rc)
+        assert res.flags & N.FLAG_DICT_INCR and res.path_taken == N.PATH_DICT_REPLAY, (j, res.flags)
+        assert engine_summary(et) == oracle_summary(ot), j
+        assert engine_log(et, 1) == oracle_log(ot, 1), j
+        assert _statuses_match_last_operation(st, chunk, bsz, ot), j
+        assert res.n_applied == int(np.sum(st == 0)), j
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    olib().orc_free(ot)
+
+
+def _sweep_shapes(cases=40, rseed=1234):
+    """Stream shapes drawn once with a fixed seed: 2-32 replicas, window 4-256,
+    depth 2-8, branching and deleting up to 0.3 / 0.4."""
+    rng = np.random.default_rng(rseed)
+    out = []
+    for _ in range(cases):
+        out.append(dict(n_ops=6000, replicas=int(rng.choice([2, 4, 8, 16, 32])),
+                        window=int(rng.choice([4, 16, 64, 256])), p_delete=float(rng.choice([0.05, 0.2, 0.4])),
+                        p_branch=float(rng.choice([0.05, 0.1, 0.3])), max_depth=int(rng.choice([2, 3, 4, 6, 8])),
+                        seed=int(rng.integers(1 << 30))))
+    return out
+
+
+@pytest.mark.parametrize("case", range(40))
+def test_level_replay_sweep(case, monkeypatch):
+    """The level replay forced over 40 fixed stream shapes (the sweep that
+    found round 4's pending-copy bug), each chained against the oracle in
+    chunks of 1 .. n/4 ops."""
+    monkeypatch.setenv("CRDTM_INCREMENTAL", "ilr")
+    from oracle.oracle import lib as olib
+    cfg = _sweep_shapes()[case]
+    s = N.synth(**cfg)
+    n = len(s["kind"])
+    rng = np.random.default_rng(case)
+    cuts = [0, n // 2]
+    while cuts[-1] < n:
+        cuts.append(min(n, cuts[-1] + int(rng.choice([1, 7, 300, n // 8, n // 4]))))
+    ot = olib().orc_init(0)
+    et = CRDTree.init(0)
+    for k, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        chunk = sub(s, a, b)
+        _, rc, _ = oracle_apply_arrays(chunk, b - a, tree=ot)
+        res = et.apply_arrays(chunk, b - a)
+        assert res.code == rc, (cfg, k, res.code, rc)
+        assert engine_summary(et) == oracle_summary(ot), (cfg, k, a, b, res.flags)
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    olib().orc_free(ot)
+
+
+def test_level_replay_commit_failure_rolls_back(monkeypatch):
+    """A level replay whose commit fails after the levels changed the state in
+    place (CRDTM_ILR_FAIL_COMMIT: an arena overflow injected at the commit's
+    first scan) rolls the levels back; crdtm_apply then retries with a larger
+    arena on the restored state, and the result matches the oracle."""
+    monkeypatch.delenv("CRDTM_INCREMENTAL", raising=False)
+    from oracle.oracle import lib as olib
+    s = N.synth(n_ops=80_000, replicas=16, window=64, p_delete=0.2, p_branch=0.1, max_depth=4, seed=0xC0FFEE02)
+    ot = olib().orc_init(0)
+    et = CRDTree.init(0)
+    cuts = [0, 60_000, 65_000, 70_000, 80_000]
+    for k, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+        chunk = sub(s, a, b)
+        _, rc, _ = oracle_apply_arrays(chunk, b - a, tree=ot)
+        if k in (1, 3):
+            monkeypatch.setenv("CRDTM_ILR_FAIL_COMMIT", f"fail{k}")
+        res = et.apply_arrays(chunk, b - a)
+        monkeypatch.delenv("CRDTM_ILR_FAIL_COMMIT", raising=False)
+        assert res.code == rc == 0, (k, res.code)
+        if k:
+            assert res.flags & N.FLAG_DICT_INCR, (k, res.flags)
+        assert engine_summary(et) == oracle_summary(ot), k
+        assert engine_log(et, 1) == oracle_log(ot, 1), k
     assert engine_log(et, 0) == oracle_log(ot, 0)
     olib().orc_free(ot)

@@ -215,7 +215,7 @@ def test_guard_g_statistics_match_oracle(monkeypatch, blocked):
     for s in streams:
         n = len(s["path_off"]) - 1  # (pack() pads its per-op arrays by one)
         ot, rc, _ = oracle_apply_arrays(s, n)
-        want = np.zeros(2, np.uint64)
+        want = np.zeros(3, np.uint64)
         olib().orc_guard_stats(want.ctypes.data_as(C.c_void_p))
         et = CRDTree.init(0)
         res = et.apply_arrays(s, n)
@@ -227,6 +227,8 @@ def test_guard_g_statistics_match_oracle(monkeypatch, blocked):
             continue
         assert ok == 1
         assert (int(got[0]), int(got[1])) == (int(want[0]), int(want[1]))
-        assert int(got[2]) <= int(got[3]) <= n  # (out[3]: the ops the replayed dicts reached)
+        # out[3]: the ops the replayed dicts reached = the oracle's ops whose
+        # path resolution called the leaf function (src/Internal/Node.elm:138-163)
+        assert int(got[3]) == int(want[2]) and int(got[2]) <= int(got[3])
         checked += 1
     assert checked >= 4

@@ -337,12 +337,15 @@ def test_guard_g_statistics_hand_traced():
     def stats(ops):
         t = OTree(0)
         assert t.apply(Batch(ops))[0] == "Ok"
-        out = np.zeros(2, np.uint64)
+        out = np.zeros(3, np.uint64)
         lib().orc_guard_stats(out.ctypes.data_as(C.c_void_p))
         return tuple(int(x) for x in out)
 
     adds = [Add(10, [0], "a"), Add(20, [10], "b"), Add(30, [20], "c")]
-    assert stats(adds + [Delete([20]), Add(15, [10], "d")]) == (4, 1)
-    assert stats(adds + [Add(15, [10], "d"), Delete([20]), Delete([30])]) == (4, 0)
+    assert stats(adds + [Delete([20]), Add(15, [10], "d")]) == (4, 1, 5)
+    assert stats(adds + [Add(15, [10], "d"), Delete([20]), Delete([30])]) == (4, 0, 6)
     # a Tombstone below the Add: 40 after 10 stops at Tombstone 20 < 40
-    assert stats(adds + [Delete([20]), Add(40, [10], "d")]) == (4, 0)
+    assert stats(adds + [Delete([20]), Add(40, [10], "d")]) == (4, 0, 5)
+    # out[2], ops that reached their dict: not one whose path meets a Tombstone
+    # (src/Internal/Node.elm:140-141: AlreadyApplied) — Add under deleted 20
+    assert stats(adds + [Delete([20]), Add(50, [20, 0], "e")]) == (3, 0, 4)

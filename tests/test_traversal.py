@@ -123,3 +123,37 @@ def test_traversal_device_queries_large_tree():
         assert [_key(c) for c in et.children(et.root())] == o.node_query("children", [])
     finally:
         T.VALUES.value = orig
+
+
+@pytest.mark.parametrize("poke", ["next_out_of_range", "next_cycle", "child_out_of_range", "sentinel_elsewhere",
+                                  "dict_out_of_range"])
+def test_host_readers_refuse_unsound_state(poke):
+    """The host readers that follow the state's indices on a host copy
+    (crdtm_tree_canonical, and crdtm_tree_walk = CRDTree.walk,
+    src/CRDTree.elm:583-625) check it first: a corrupted device state
+    (crdtm_debug_poke) is CRDTM_E_STATE (-7), never a wild read, and the
+    readers recover once the state is sound again (a reset and a merge)."""
+    import ctypes as C
+    from crdtm import _native as N
+    s = N.synth(n_ops=3000, replicas=4, window=16, p_delete=0.2, p_branch=0.1, max_depth=3, seed=3)
+    n = len(s["kind"])
+    et = CRDTree.init(0)
+    assert et.apply_arrays(s, n).code == 0
+    L = N.lib()
+    cnt = C.c_uint64()
+    assert L.crdtm_tree_walk(et._h, N.REF_NONE, None, 0, C.byref(cnt)) == 0 and cnt.value > 0
+    field, index, value = {"next_out_of_range": (0, 5, 0x7FFFFFF0), "next_cycle": (0, 0, 0),
+                           "child_out_of_range": (1, 3, 0x7FFFFFF0), "sentinel_elsewhere": (3, 0, 7),
+                           "dict_out_of_range": (2, 9, 0x7FFFFFF0)}[poke]
+    assert L.crdtm_debug_poke(et._h, field, index, value) == 0
+    h = C.c_uint64()
+    assert L.crdtm_tree_canonical(et._h, 0, None, 0, C.byref(cnt), C.byref(h)) == -7
+    assert L.crdtm_tree_canonical(et._h, 1, None, 0, C.byref(cnt), C.byref(h)) == -7
+    assert L.crdtm_tree_walk(et._h, N.REF_NONE, None, 0, C.byref(cnt)) == -7
+    assert L.crdtm_debug_poke(et._h, 0, 1 << 40, 0) == -1  # (out of range: E_ARG)
+    N.check(L.crdtm_tree_reset(et._h, 0))
+    assert et.apply_arrays(s, n).code == 0
+    ot, rc, _ = oracle_apply_arrays(s, n)
+    from parity_util import engine_summary, oracle_summary
+    assert engine_summary(et) == oracle_summary(ot)
+    assert L.crdtm_tree_walk(et._h, N.REF_NONE, None, 0, C.byref(cnt)) == 0
