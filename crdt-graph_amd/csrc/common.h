@@ -100,6 +100,9 @@ struct DevResult {
   // [32 k]): +0 slots holding an Add, +1 Adds with a timestamp slot, +2 Adds
   // of the own replica, +3 ops that need per-op statuses (empty path, ts 0)
   uint32_t fl_part[16 * 32];
+  uint32_t spec_fail;       // flat speculation: some op is not an Add with a one-element path (k_fl_claim<VERIFY>)
+  uint32_t pre_done;        // k_pre_ts: workgroups finished (the last lays the ranges out)
+  uint32_t fl_nw;           // flat order: words of 64 slots, (range_total + 63) / 64
   uint32_t run_count;       // flat order: ep-runs (scan total)
   uint32_t run_fail;        // flat order: the run tree is deeper than RUN_MAXD (generic list ranking instead)
   uint32_t run_maxd;        // flat order: deepest run

@@ -14,6 +14,39 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z;
 }
 
+// Streaming stores, for what no later pass of the merge reads back (the op
+// log, the node records): vector stores with the non-temporal hint, so the
+// hundreds of MB they stream do not displace the slot records the next
+// passes re-read from the MALL. (Built with -DCRDTM_NT=0: plain stores.)
+#ifndef CRDTM_NT
+#define CRDTM_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ void st_stream(T* p, T v) {
+#if CRDTM_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ void st_stream16(void* p, uint4 v) {
+#if CRDTM_NT
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(p));
+#else
+  *reinterpret_cast<uint4*>(p) = v;
+#endif
+}
+__device__ __forceinline__ void st_stream16(void* p, longlong2 v) {
+  st_stream16(p, make_uint4(static_cast<uint32_t>(v.x), static_cast<uint32_t>(static_cast<unsigned long long>(v.x) >> 32),
+                            static_cast<uint32_t>(v.y), static_cast<uint32_t>(static_cast<unsigned long long>(v.y) >> 32)));
+}
+__device__ __forceinline__ void st_stream4(void* p, uchar4 v) {
+  st_stream(reinterpret_cast<uint32_t*>(p), static_cast<uint32_t>(v.x) | (static_cast<uint32_t>(v.y) << 8) |
+                                                (static_cast<uint32_t>(v.z) << 16) | (static_cast<uint32_t>(v.w) << 24));
+}
+
 // replicaId ts = ts // 2^32 with Elm/JS (a / b) | 0 truncation (src/CRDTree/Timestamp.elm:16-18)
 __host__ __device__ __forceinline__ int64_t replica_of(int64_t ts) { return ts / TWO32; }
 

@@ -236,6 +236,106 @@ __global__ void __launch_bounds__(BLOCK) k_path_range(OpsDev o, DevResult* dres)
   if (threadIdx.x == 0 && bad) atomicOr(&dres->bad_range, 1u);
 }
 
+// The flat speculation's pre-pass (launched when every op may be an Add with
+// a one-element path, n_path == n: the claim checks that itself): the
+// per-replica counter ranges from the timestamps alone (16-byte loads, ids
+// below REP_SPEC in an LDS table), |ts| < 2^53, negative timestamps and the
+// largest replica id. The workgroup that finishes last lays the ranges end
+// to end (base[], range_total, the slot words fl_nw), so the claim follows
+// on the device without a host round trip.
+constexpr uint32_t REP_SPEC = 256;
+template <uint32_t PB>
+__global__ void __launch_bounds__(PB) k_pre_ts(const long long* __restrict__ ts, uint32_t n, uint2* rng,
+                                               uint32_t* base, DevResult* dres) {
+  __shared__ uint32_t rlo[REP_SPEC], rhi[REP_SPEC];
+  __shared__ uint32_t s_last, sw[PB / 64];
+  for (uint32_t j = threadIdx.x; j < REP_SPEC; j += PB) {
+    rlo[j] = NONE;
+    rhi[j] = 0;
+  }
+  __syncthreads();
+  uint32_t bad = 0, neg = 0, maxr = 0;
+  auto fold = [&](long long t) {
+    if (t >= TWO53 || t <= -TWO53) {
+      bad = 1;
+    } else if (t < 0) {
+      neg = 1;
+    } else if (t != 0) {
+      const uint32_t r = static_cast<uint32_t>(static_cast<uint64_t>(t) >> 32), c = static_cast<uint32_t>(t);
+      maxr = max(maxr, r);
+      if (r < REP_SPEC) {  // (the table only narrows: a covering read makes the atomic unnecessary)
+        if (c < rlo[r]) atomicMin(&rlo[r], c);
+        if (c > rhi[r]) atomicMax(&rhi[r], c);
+      }
+    }
+  };
+  {
+    const longlong2* t2 = reinterpret_cast<const longlong2*>(ts);
+    const uint32_t np = n / 2, gs = gridDim.x * PB;
+    uint32_t p = blockIdx.x * PB + threadIdx.x;
+    for (; p + 3 * gs < np; p += 4 * gs) {  // four pairs in flight
+      longlong2 v[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) v[u] = t2[p + u * gs];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        fold(v[u].x);
+        fold(v[u].y);
+      }
+    }
+    for (; p < np; p += gs) {
+      const longlong2 v = t2[p];
+      fold(v.x);
+      fold(v.y);
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) fold(ts[n - 1]);
+  }
+  auto mxf = [](uint32_t a, uint32_t b) { return a > b ? a : b; };
+  maxr = block_reduce_t<PB>(maxr, 0u, mxf);  // (synchronises the block)
+  for (uint32_t j = threadIdx.x; j <= maxr && j < REP_SPEC; j += PB)
+    if (rlo[j] != NONE) {
+      atomicMin(&rng[j].x, rlo[j]);
+      atomicMax(&rng[j].y, rhi[j]);
+    }
+  bad = block_reduce_t<PB>(bad, 0u, mxf);
+  neg = block_reduce_t<PB>(neg, 0u, mxf);
+  if (threadIdx.x == 0) {
+    if (bad) atomicOr(&dres->bad_range, 1u);
+    if (neg) atomicOr(&dres->has_negative, 1u);
+    if (maxr) atomicMax(&dres->max_replica, maxr);
+    // (release: this workgroup's range atomics before its arrival)
+    s_last = __hip_atomic_fetch_add(&dres->pre_done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+             gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // the last workgroup: base[r] = the sizes of the ranges before r (ids above
+  // REP_SPEC - 1 make the speculation fail on the host; they are not laid out)
+  const uint32_t nr =
+      min(__hip_atomic_load(&dres->max_replica, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT), REP_SPEC - 1) + 1;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x / 64;
+  uint32_t sz = 0;
+  if (threadIdx.x < nr) {
+    const uint32_t lo = __hip_atomic_load(&rng[threadIdx.x].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t hi = __hip_atomic_load(&rng[threadIdx.x].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sz = lo == NONE ? 0u : hi - lo + 1u;  // (counters: a range never exceeds 2^32 - 1 per replica)
+  }
+  const uint32_t inc = wave_incl_scan(sz);
+  if (lane == 63) sw[wave] = inc;
+  __syncthreads();
+  unsigned long long pre = inc - sz, tot = 0;
+  for (uint32_t w = 0; w < PB / 64; ++w) {
+    if (w < wave) pre += sw[w];
+    tot += sw[w];
+  }
+  if (threadIdx.x < nr) base[threadIdx.x] = static_cast<uint32_t>(pre < NONE ? pre : NONE);
+  if (threadIdx.x == 0) {
+    const uint32_t q = static_cast<uint32_t>(tot < NONE - 64 ? tot : NONE - 64);
+    dres->range_total = q;
+    dres->fl_nw = (q + 63) / 64;
+  }
+}
+
 // Per-op state of the level-synchronous (nested / hash-indexed) path.
 __global__ void __launch_bounds__(BLOCK) k_work_init(OpsDev o, Work w) {
   GRID_STRIDE(i, o.n) {
@@ -2034,6 +2134,15 @@ struct FlatRec {
   uint32_t ep;     // epoch << FR_ABITS (narrow), 0 (wide)
   uint32_t amask;  // anchor code field
   uint32_t anone;  // code of a missing anchor
+  // the flat speculation launches the merge before the host knows the slot
+  // range: the kernels then read it here (range_total; the host passed an
+  // upper bound for grids and buffers) and the replica count (max_replica)
+  const uint32_t* qd = nullptr;
+  const uint32_t* nrd = nullptr;
+  // (the bound stays the limit: a batch whose range exceeds it reads as cut
+  // off, and the host discards the speculation)
+  __device__ __forceinline__ uint32_t q(uint32_t Q) const { return qd ? min(*qd, Q) : Q; }
+  __device__ __forceinline__ uint32_t nrep(uint32_t nr) const { return nrd ? min(nr, *nrd + 1u) : nr; }
   __device__ __forceinline__ bool present(uint32_t w) const { return w != FR_EMPTY && (w & ~amask) == ep; }
   __device__ __forceinline__ uint32_t code(uint32_t qa) const { return (qa == NONE ? anone : qa) | ep; }
   // slot, Q (the sentinel) or NONE
@@ -2064,11 +2173,16 @@ struct FlatRec {
 // longest path 1 and as many path elements as ops), so op i's anchor is
 // path[i]: the pass reads the timestamps, anchors (and values for the log) as
 // 16-byte vectors and writes the log's kinds and offsets without reading them.
-template <bool SIMPLE>
+// VERIFY (the speculation launched without the pre-pass's kinds and path
+// lengths): the pass also checks that every op is an Add whose path is
+// path[i] alone (kind, and path_off[i] == i), else DevResult::spec_fail.
+template <bool SIMPLE, bool VERIFY>
 __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_t Q, FlatRec fr,
                                                     long long ts0, uint32_t* rtab, DevResult* dres,
                                                     uint32_t track_rep, uint32_t nrep, TreeDev T,
                                                     uint32_t log_to_tree) {
+  Q = fr.q(Q);
+  nrep = fr.nrep(nrep);
   // dynamic LDS: the replica range table (nrep ids: base, min, max counter)
   // when it fits, else lookups go to the global table; rv when track_rep
   extern __shared__ __attribute__((aligned(16))) uint32_t scl[];
@@ -2095,10 +2209,21 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
     return sbase[r] + (c - lo);
   };
   const long long id0 = replica_of(ts0);
-  uint32_t keys = 0, own = 0, slow = 0, err = NONE, mr = 0, bad = 0;
+  uint32_t keys = 0, own = 0, slow = 0, err = NONE, mr = 0, bad = 0, vfail = 0;
   QUAD_LOOP_XCD(i0, o.n) {
     Quad qd;
     long long pk[4];  // the path element of each op (flat: |path| <= 1)
+    if (VERIFY) {
+      if (i0 + 4 <= o.n) {
+        const uchar4 k4 = *reinterpret_cast<const uchar4*>(o.kind + i0);
+        const uint4 f4 = *reinterpret_cast<const uint4*>(o.off + i0);
+        vfail |= (k4.x | k4.y | k4.z | k4.w) != CRDTM_ADD ||
+                 (f4.x != i0) | (f4.y != i0 + 1) | (f4.z != i0 + 2) | (f4.w != i0 + 3);
+      } else {
+        for (uint32_t i = i0; i < o.n; ++i) vfail |= o.kind[i] != CRDTM_ADD || o.off[i] != i;
+      }
+      if (i0 + 4 >= o.n) vfail |= o.off[o.n] != o.n;
+    }
     if (SIMPLE) {
       if (i0 + 4 <= o.n) {
         qd.cnt = 4;
@@ -2126,18 +2251,18 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) bad |= (pk[k] >= TWO53 || pk[k] <= -TWO53) ? 1u : 0u;  // (|x| < 2^53)
     if (log_to_tree) {
-      if (qd.cnt == 4) {
+      if (qd.cnt == 4) {  // (streaming stores: nothing in the merge reads the log back)
         if (SIMPLE) {
-          *reinterpret_cast<uchar4*>(T.l_kind + i0) = make_uchar4(CRDTM_ADD, CRDTM_ADD, CRDTM_ADD, CRDTM_ADD);
-          *reinterpret_cast<longlong2*>(T.l_path + i0) = make_longlong2(pk[0], pk[1]);
-          *reinterpret_cast<longlong2*>(T.l_path + i0 + 2) = make_longlong2(pk[2], pk[3]);
+          st_stream4(T.l_kind + i0, make_uchar4(CRDTM_ADD, CRDTM_ADD, CRDTM_ADD, CRDTM_ADD));
+          st_stream16(T.l_path + i0, make_longlong2(pk[0], pk[1]));
+          st_stream16(T.l_path + i0 + 2, make_longlong2(pk[2], pk[3]));
         } else {
-          *reinterpret_cast<uchar4*>(T.l_kind + i0) = make_uchar4(qd.kind[0], qd.kind[1], qd.kind[2], qd.kind[3]);
+          st_stream4(T.l_kind + i0, make_uchar4(qd.kind[0], qd.kind[1], qd.kind[2], qd.kind[3]));
         }
-        *reinterpret_cast<longlong2*>(T.l_ts + i0) = make_longlong2(qd.ts[0], qd.ts[1]);
-        *reinterpret_cast<longlong2*>(T.l_ts + i0 + 2) = make_longlong2(qd.ts[2], qd.ts[3]);
-        *reinterpret_cast<uint4*>(T.l_off + i0) = make_uint4(qd.off[0], qd.off[1], qd.off[2], qd.off[3]);
-        *reinterpret_cast<uint4*>(T.l_val + i0) = *reinterpret_cast<const uint4*>(o.val + i0);
+        st_stream16(T.l_ts + i0, make_longlong2(qd.ts[0], qd.ts[1]));
+        st_stream16(T.l_ts + i0 + 2, make_longlong2(qd.ts[2], qd.ts[3]));
+        st_stream16(T.l_off + i0, make_uint4(qd.off[0], qd.off[1], qd.off[2], qd.off[3]));
+        st_stream16(T.l_val + i0, *reinterpret_cast<const uint4*>(o.val + i0));
       } else {
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {  // (static indices: no scratch)
@@ -2169,13 +2294,14 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
       const long long ts = qd.ts[k];
       if (replica_of(ts) == id0) ++own;
       const uint32_t q = slot(ts);
-      if (q == NONE) {  // ts 0: the sentinel's key (AlreadyApplied)
+      if (q >= Q) {  // ts 0: the sentinel's key (AlreadyApplied); (or past a speculation's bound)
         ++slow;
         continue;
       }
       ++keys;
       const long long kk = pk[k];
-      const uint32_t qa = kk == 0 ? Q : slot(kk);
+      uint32_t qa = kk == 0 ? Q : slot(kk);
+      if (qa > Q) qa = NONE;
       fr.rec[q] = make_uint2(fr.code(qa), i);
       if (track_rep) {
         const uint32_t rr = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32);
@@ -2197,7 +2323,9 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
   slow = block_sum(slow);
   err = block_min(err);
   bad = block_max(bad);
+  if (VERIFY) vfail = block_max(vfail);
   if (threadIdx.x == 0) {  // 16 shards a line apart: ~12 ns per atomic on one word
+    if (VERIFY && vfail) atomicOr(&dres->spec_fail, 1u);
     if (bad) atomicOr(&dres->bad_range, 1u);
     uint32_t* sh = dres->fl_part + 32 * (blockIdx.x & 15);
     if (keys) atomicAdd(&sh[1], keys);
@@ -2313,10 +2441,12 @@ __global__ void k_fl_stat_reset(DevResult* d) {
 }
 
 // replicas[r] := ts of replica r's last applied Add (flat: Adds only, ids in
-// [0, max_replica]); clears the table entries it reads.
+// [0, max_replica]); clears the table entries it reads, and (rng_clear, the
+// merge's last launch before its result read) the replica range entries.
 __global__ void __launch_bounds__(BLOCK) k_fl_rep_collect(OpsDev o, uint32_t nr, uint32_t* rtab, long long* out,
-                                                          uint32_t* n_out, long long* inl) {
+                                                          uint32_t* n_out, long long* inl, uint2* rng_clear) {
   GRID_STRIDE(r, nr) {
+    if (rng_clear) rng_clear[r] = make_uint2(NONE, 0u);
     uint32_t* e = &rtab[r + (1u << (REPLICA_BITS - 1))];
     const uint32_t v = *e;
     if (!v) continue;
@@ -2389,9 +2519,12 @@ constexpr uint32_t RM_MASK_UNROLL = 2;  // k_run_mask (48 VGPRs, full occupancy;
 template <uint32_t U>
 __global__ void __launch_bounds__(BLOCK) k_run_mask(FlatRec fr, uint32_t Q, unsigned long long* hm, uint32_t* hc,
                                                    TreeDev T, const uint32_t* qc, const uint32_t* logidx, OpsDev o,
-                                                   TsIndex x, uint32_t nrep, DevResult* chk, uint32_t* rtab) {
+                                                   TsIndex x, uint32_t nrep, DevResult* chk, uint32_t* rtab,
+                                                   uint64_t slot_cap) {
   extern __shared__ uint32_t smk[];  // dynamic: 3 * nrep words when the tables fit (HOST_RANGES)
+  Q = fr.q(Q);
   const bool lds = nrep <= HOST_RANGES;
+  nrep = fr.nrep(nrep);
   uint32_t* sb = smk;
   uint32_t* sc = smk + nrep;
   uint32_t* srv = smk + 2 * nrep;  // (chk) largest op index + 1 per replica
@@ -2440,13 +2573,15 @@ __global__ void __launch_bounds__(BLOCK) k_run_mask(FlatRec fr, uint32_t Q, unsi
       }
       uint32_t rep = NONE;
       const uint32_t fi = rq[u].y;
-      if (pres) {
+      // (a speculation over slots with no node, which the host then
+      // discards, may reach past the tree's capacity: those stores are dropped)
+      if (pres && (qc || 1ULL + q < slot_cap)) {  // (streaming stores: the merge does not read them back)
         const uint32_t slot = 1 + (qc ? qc[q] : q);
-        T.s_key[slot] = lds ? fl_key(q, sb, sc, nrep, rep) : o.ts[fi];
-        T.s_dict[slot] = 0;
-        T.s_src[slot] = logidx ? logidx[fi] : fi;
-        T.s_flags[slot] = 0;
-        T.s_child[slot] = NONE;
+        st_stream(T.s_key + slot, lds ? fl_key(q, sb, sc, nrep, rep) : o.ts[fi]);
+        st_stream(T.s_dict + slot, 0u);
+        st_stream(T.s_src + slot, logidx ? logidx[fi] : fi);
+        st_stream(T.s_flags + slot, static_cast<uint8_t>(0));
+        st_stream(T.s_child + slot, NONE);
         if (chk) {
           ++present;
           if (qa != Q) {
@@ -2490,6 +2625,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_mask(FlatRec fr, uint32_t Q, unsi
 // bounds), hh[r] = {head, anchor}; k_run_ep replaces the anchor by the
 // head's effective parent.
 __global__ void __launch_bounds__(BLOCK) k_run_heads(FlatRec fr, uint32_t Q, RunMask rm, uint2* hh) {
+  Q = fr.q(Q);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t nw = (Q + 63) >> 6;
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwave = (gridDim.x * blockDim.x) >> 6;
@@ -2688,16 +2824,20 @@ __global__ void __launch_bounds__(BLOCK) k_fl_log_copy(OpsDev o, TreeDev T) {
 constexpr uint32_t RUN_MAXD = 64;
 constexpr uint32_t EX_ITERS = 128;  // k_run_expand keeps its run-mask words in LDS up to this many iterations
 
+// One 16-byte record per run, so that a walk over runs (the bottom-up climb,
+// the top-down chain) takes every field it needs from one line:
+// rr[r] = {parent run (NONE: a child of the root sentinel, or a hole run),
+//          length (after k_run_tree_up: w, the head's rank minus its parent
+//          run head's rank), sorted positions [z, w) of its child runs ({0, 0}:
+//          none)}.
 struct RunArr {
   const uint32_t* nR;        // device: number of runs
   uint2* hh;                 // {head slot, anchor of the head (ABSENT: a hole run), then its effective parent}
-  uint32_t* par;             // parent run (NONE: a child of the root sentinel, or a hole run)
-  uint32_t* len;
-  uint2* er;                 // sorted positions [er.x, er.y) of the run's child runs ({0, 0}: none)
+  uint4* rr;                 // {par, len -> w, er.x, er.y}
+  const uint32_t* qd;        // (the flat speculation: the slot range on the device, FlatRec::qd)
   unsigned long long* ca;    // children arrived << 32 | their subtree sizes
   uint32_t* tk;              // subtree sizes in sorted order (k_run_tree_up writes T(r) at kinv[r])
   const uint32_t* kinv;      // run -> its position in the sorted order
-  uint32_t* w;               // top-down increment along the chain
   uint32_t* posh;            // document rank of the head
 };
 
@@ -2725,6 +2865,7 @@ __device__ __forceinline__ uint2 hh_load(const uint2* p) {
 }
 __global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, RunMask rm, FlatRec fr, uint32_t* skey,
                                                   uint32_t* sval) {
+  Q = fr.q(Q);
   const uint32_t R = *a.nR;
   RUN_LOOP(k) {
     const uint32_t r = R - 1 - k;
@@ -2733,9 +2874,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, RunMask 
     uint32_t d = me.y;
     const uint32_t hn = r + 1 < R ? a.hh[r + 1].x : Q;
     if (d == ABSENT) {  // a hole run
-      a.par[r] = NONE;
-      a.len[r] = 0;
-      a.er[r] = make_uint2(0u, 0u);
+      a.rr[r] = make_uint4(NONE, 0u, 0u, 0u);
       a.ca[r] = 0;
       skey[R - 1 - r] = Q + 1;
       sval[R - 1 - r] = r;
@@ -2760,9 +2899,8 @@ __global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, RunMask 
       d = Q;
       __hip_atomic_store(&a.hh[r].y, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    a.par[r] = d == Q ? NONE : run_of(rm, d);
-    a.len[r] = hn - x;  // (a hole after the run is a run of its own)
-    a.er[r] = make_uint2(0u, 0u);
+    // (len: a hole after the run is a run of its own)
+    a.rr[r] = make_uint4(d == Q ? NONE : run_of(rm, d), hn - x, 0u, 0u);
     a.ca[r] = 0;
     skey[R - 1 - r] = d;
     sval[R - 1 - r] = r;
@@ -2793,16 +2931,19 @@ __global__ void __launch_bounds__(BLOCK) k_run_ep_slots(RunArr a, uint32_t Q, Ru
 // side: a wave sums its leaves per parent first (one atomic per wave and
 // parent; a parent with thousands of children would otherwise serialise
 // thousands of atomics on one word, ~12 ns each).
-__device__ __forceinline__ void run_climb(RunArr& a, uint32_t x, uint32_t t) {
+// (ex: the record of x, loaded by the step that reached x; the parent's
+// record loads beside the atomic, so a level costs one round trip)
+__device__ __forceinline__ void run_climb(RunArr& a, uint32_t x, uint4 ex, uint32_t t) {
   for (;;) {
     a.tk[a.kinv[x]] = t;
-    const uint32_t p = a.par[x];
+    const uint32_t p = ex.x;
     if (p == NONE) return;
     const unsigned long long old = atomicAdd(&a.ca[p], (1ULL << 32) | t);
-    const uint2 e = a.er[p];
-    if (static_cast<uint32_t>(old >> 32) + 1u != e.y - e.x) return;
-    t = a.len[p] + static_cast<uint32_t>(old) + t;
+    const uint4 e = a.rr[p];
+    if (static_cast<uint32_t>(old >> 32) + 1u != e.w - e.z) return;
+    t = e.y + static_cast<uint32_t>(old) + t;
     x = p;
+    ex = e;
   }
 }
 
@@ -2814,11 +2955,10 @@ __global__ void __launch_bounds__(BLOCK) k_run_tree_up(RunArr a, const uint32_t*
     uint32_t key = NONE - 1 - static_cast<uint32_t>(lane);  // (distinct per idle lane)
     unsigned long long v = 0;                                // leaves << 32 | their sizes
     if (k < R) {
-      const uint32_t r = sarr[k];
-      key = a.par[r];
-      const uint2 e = a.er[r];
-      if (e.y == e.x) {
-        const uint32_t t = a.len[r];
+      const uint4 e = a.rr[sarr[k]];
+      key = e.x;
+      if (e.w == e.z) {
+        const uint32_t t = e.y;
         a.tk[k] = t;  // (kinv[r] == k)
         v = (1ULL << 32) | t;
       }
@@ -2833,9 +2973,9 @@ __global__ void __launch_bounds__(BLOCK) k_run_tree_up(RunArr a, const uint32_t*
     const uint32_t nk = __shfl_down(key, 1, 64);
     if ((lane == 63 || nk != key) && key < NONE - 64 && (v >> 32)) {
       const unsigned long long old = atomicAdd(&a.ca[key], v);
-      const uint2 e = a.er[key];
-      if (static_cast<uint32_t>(old >> 32) + static_cast<uint32_t>(v >> 32) == e.y - e.x)
-        run_climb(a, key, a.len[key] + static_cast<uint32_t>(old) + static_cast<uint32_t>(v));
+      const uint4 e = a.rr[key];
+      if (static_cast<uint32_t>(old >> 32) + static_cast<uint32_t>(v >> 32) == e.w - e.z)
+        run_climb(a, key, e, e.y + static_cast<uint32_t>(old) + static_cast<uint32_t>(v));
     }
   }
 }
@@ -2851,20 +2991,21 @@ __device__ __forceinline__ uint32_t run_S(const uint32_t* xs, uint32_t k) { retu
 // parents come from the adjacent lanes (a wave holds consecutive positions).
 __global__ void __launch_bounds__(BLOCK) k_run_gstart(RunArr a, uint32_t Q, const uint32_t* pk, const uint32_t* sarr,
                                                       uint32_t* groot) {
+  if (a.qd) Q = min(*a.qd, Q);  // (FlatRec::q: the bound stays the limit)
   const uint32_t R = *a.nR;
   const uint32_t lane = threadIdx.x & 63;
   for (uint32_t k0 = blockIdx.x * blockDim.x; k0 < R; k0 += gridDim.x * blockDim.x) {
     const uint32_t k = k0 + threadIdx.x;
     const uint32_t p = k < R ? pk[k] : Q + 1;
-    const uint32_t P = p < Q ? a.par[sarr[k]] : NONE;
+    const uint32_t P = p < Q ? a.rr[sarr[k]].x : NONE;
     uint32_t Pp = __shfl_up(P, 1, 64), Pn = __shfl_down(P, 1, 64);
     if (k >= R) continue;
     if (p == Q && (k == 0 || pk[k - 1] != Q)) *groot = k;
     if (p >= Q) continue;
-    if (lane == 0) Pp = k ? (pk[k - 1] < Q ? a.par[sarr[k - 1]] : NONE) : NONE;
-    if (lane == 63 || k + 1 == R) Pn = k + 1 < R && pk[k + 1] < Q ? a.par[sarr[k + 1]] : NONE;
-    if (Pp != P) a.er[P].x = k;
-    if (Pn != P) a.er[P].y = k + 1;
+    if (lane == 0) Pp = k ? (pk[k - 1] < Q ? a.rr[sarr[k - 1]].x : NONE) : NONE;
+    if (lane == 63 || k + 1 == R) Pn = k + 1 < R && pk[k + 1] < Q ? a.rr[sarr[k + 1]].x : NONE;
+    if (Pp != P) a.rr[P].z = k;
+    if (Pn != P) a.rr[P].w = k + 1;
   }
 }
 
@@ -2875,14 +3016,16 @@ __global__ void __launch_bounds__(BLOCK) k_run_gstart(RunArr a, uint32_t Q, cons
 // ones sorted before it): together, the child runs of P sorted before r.
 __global__ void __launch_bounds__(BLOCK) k_run_w(RunArr a, uint32_t Q, const uint32_t* sarr, const uint32_t* pk,
                                                  const uint32_t* xs, const uint32_t* groot) {
+  if (a.qd) Q = min(*a.qd, Q);  // (FlatRec::q: the bound stays the limit)
   RUN_LOOP(k) {
     const uint32_t r = sarr[k], p = pk[k];
     if (p > Q) continue;  // (hole runs)
+    // (w replaces the length in the record: k_run_tree_up has used it)
     if (p == Q) {
-      a.w[r] = run_S(xs, k) - run_S(xs, *groot);
+      a.rr[r].y = run_S(xs, k) - run_S(xs, *groot);
     } else {
-      const uint32_t P = a.par[r];
-      a.w[r] = run_S(xs, k) - run_S(xs, a.er[P].x) + (p - a.hh[P].x) + 1u;
+      const uint32_t P = a.rr[r].x;
+      a.rr[r].y = run_S(xs, k) - run_S(xs, a.rr[P].z) + (p - a.hh[P].x) + 1u;
     }
   }
 }
@@ -2891,13 +3034,16 @@ __global__ void __launch_bounds__(BLOCK) k_run_w(RunArr a, uint32_t Q, const uin
 // RUN_MAXD flags the generic path instead (quadratic walks on deep trees)
 __global__ void __launch_bounds__(BLOCK) k_run_pos(RunArr a, DevResult* dres) {
   RUN_LOOP(r) {
-    uint32_t s = a.w[r], d = 0;
-    for (uint32_t x = a.par[r]; x != NONE; x = a.par[x]) {
+    const uint4 e = a.rr[r];
+    uint32_t s = e.y, d = 0;
+    for (uint32_t x = e.x; x != NONE;) {
       if (++d > RUN_MAXD) {
         atomicOr(&dres->run_fail, 1u);
         break;
       }
-      s += a.w[x];
+      const uint4 f = a.rr[x];  // (one record: the ancestor's w and its parent)
+      s += f.y;
+      x = f.x;
     }
     a.posh[r] = s;
   }
@@ -2914,10 +3060,11 @@ __global__ void __launch_bounds__(BLOCK) k_run_pos(RunArr a, DevResult* dres) {
 // before this slot's dependent loads).
 __global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint32_t K, RunMask rm,
                                                       const uint32_t* pk, const uint32_t* xs, const uint32_t* qc,
-                                                      uint32_t* doc, FlatRec fr) {
-  extern __shared__ uint32_t smw[];  // [iters * waves] {mask lo, mask hi, base}
+                                                      uint32_t* doc, FlatRec fr, uint32_t lds_iters) {
+  extern __shared__ uint32_t smw[];  // [lds_iters * waves] {mask lo, mask hi, base}
+  Q = fr.q(Q);  // (the host sized the LDS staging for its bound: at least these iterations)
   const uint32_t iters = (Q + gridDim.x * blockDim.x - 1) / (gridDim.x * blockDim.x);
-  const bool mlds = iters <= EX_ITERS;
+  const bool mlds = iters <= lds_iters;
   const uint32_t wpb = blockDim.x >> 6;
   if (mlds) {
     const uint32_t nw = (Q + 63) >> 6;
@@ -2951,8 +3098,8 @@ __global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint
     }
     const uint32_t r = bq + static_cast<uint32_t>(__popcll(mq & below)) - 1u;
     uint32_t p = a.posh[r] + (q - a.hh[r].x);
-    const uint2 er = a.er[r];
-    const uint32_t e0 = er.x, e1 = er.y;
+    const uint4 er = a.rr[r];
+    const uint32_t e0 = er.z, e1 = er.w;
     if (e1 > e0) {
       uint32_t lo = e0, hi = e1;  // first k with pk[k] >= q
       while (lo < hi) {
@@ -3371,6 +3518,7 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     const uint32_t NW = (Q + 63) / 64;
     RunArr ra;
     ra.nR = &dr->run_count;
+    ra.qd = fr.qd;
     // (a run per present slot at most, plus a hole run per absent slot)
     ra.hh = fb.hh = ws.alloc<uint2>(Q + 1);
     unsigned long long* hm = ws.alloc<unsigned long long>(NW + 1);
@@ -3388,7 +3536,7 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
       LAUNCH(k_log_tail, dim3(1), dim3(1), 0, s, t->d, 0u, &dr->log_n, 0u, &dr->log_npath);
     }
     uint32_t* qc = nullptr;
-    if (Q != K) {  // slots with no node: compact
+    if (!fr.qd && Q != K) {  // slots with no node: compact (the speculation confirms there are none)
       qc = fb.qc = ws.alloc<uint32_t>(Q);
       LAUNCH(k_fl_present, dim3(gq), dim3(BLOCK), 0, s, Q, fr, qc);
       if ((r = scan_excl_u32(qc, qc, Q, nullptr, ws, s))) return r;
@@ -3397,18 +3545,16 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
                                                                            (RM_MASK_UNROLL * (BLOCK / 64))));
     LAUNCH(k_run_mask<RM_MASK_UNROLL>, dim3(gw), dim3(BLOCK),
            maxr + 1 <= HOST_RANGES ? 3 * (maxr + 1) * sizeof(uint32_t) : 0, s, fr, Q, hm, hc, t->d, qc, logidx, o, ix,
-           maxr + 1, check ? dr : nullptr, c->rtab);
-    if ((r = dscan<SumOp, false>(ArrGen{hc}, hb, NW, &dr->run_count, ws, s, nullptr, nullptr, "k_dscan_runs")))
+           maxr + 1, check ? dr : nullptr, c->rtab, static_cast<uint64_t>(t->cap.slots));
+    if ((r = dscan<SumOp, false>(ArrGen{hc}, hb, NW, &dr->run_count, ws, s, nullptr, fr.qd ? &dr->fl_nw : nullptr,
+                                 "k_dscan_runs")))
       return r;
     LAUNCH(k_run_heads, dim3(grid_for(64ULL * NW, BLOCK, 4096)), dim3(BLOCK), 0, s, fr, Q, fb.rm, ra.hh);
     // ---- K2a (heads' effective parents), parent runs, sibling order (stable radix sort by attach slot) ----
-    ra.par = ws.alloc<uint32_t>(Q + 1);
-    ra.len = ws.alloc<uint32_t>(Q + 1);
-    ra.er = ws.alloc<uint2>(Q + 1);
+    ra.rr = ws.alloc<uint4>(Q + 1);
     ra.ca = ws.alloc<unsigned long long>(Q + 1);
     uint32_t* kinv = ws.alloc<uint32_t>(Q + 1);
     ra.kinv = kinv;
-    ra.w = ws.alloc<uint32_t>(Q + 1);
     ra.posh = ws.alloc<uint32_t>(Q + 1);
     uint32_t* sk[2] = {ws.alloc<uint32_t>(Q + 1), ws.alloc<uint32_t>(Q + 1)};
     uint32_t* sv[2] = {ws.alloc<uint32_t>(Q + 1), ws.alloc<uint32_t>(Q + 1)};
@@ -3432,15 +3578,16 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     const uint32_t ex_iters = (Q + gx * BLOCK - 1) / (gx * BLOCK);
     LAUNCH(k_run_expand, dim3(gx), dim3(BLOCK),
            ex_iters <= EX_ITERS ? 3 * ex_iters * (BLOCK / 64) * sizeof(uint32_t) : 0, s, ra, Q, K, fb.rm, pk, xs, qc,
-           t->d.doc, fr);
+           t->d.doc, fr, ex_iters <= EX_ITERS ? ex_iters : 0u);
     LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d, t->cap.slots);
     if (all_applied && !log_done) fl_log_copy(c, o, t->d, simple);
   } else if (all_applied && !log_done) {
     fl_log_copy(c, o, t->d, simple);
   }
   fb.rep = ws.alloc<long long>(2 * static_cast<uint64_t>(maxr) + 2);
+  // (the speculation's commit is the merge's last: the range table is reset here too)
   LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, fb.rep,
-         &dr->n_replica_out, dr->rep_inline);
+         &dr->n_replica_out, dr->rep_inline, check ? c->crange : nullptr);
   return CRDTM_OK;
 }
 
@@ -3495,8 +3642,15 @@ static int flat_order_fallback(crdtm_tree* t, uint32_t Q, uint32_t K, FlatBufs& 
 // final result, confirm it (one host round trip for the whole merge). A
 // batch where some op does not apply is then decided op by op and committed
 // again (the tree is fresh: its root sentinel is restored in between).
+// devq (the speculation launched without a host round trip, apply_flat_spec):
+// Q and maxr are upper bounds, the kernels read the true values on the device;
+// the result read then checks the batch's shape (SIMPLE, dense, replica ids
+// below REP_SPEC) and returns with *done = false when it is not one this path
+// serves (the caller runs the general path from the top).
 static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_t Q, uint32_t maxr, uint8_t* st,
-                      uint8_t* st_out, crdtm_result* res, bool simple, RangeReset& rr) {
+                      uint8_t* st_out, crdtm_result* res, bool simple, RangeReset& rr, bool devq = false,
+                      bool* done = nullptr) {
+  if (done) *done = true;
   crdtm_ctx* c = t->ctx;
   hipStream_t s = c->stream;
   Arena& ws = c->ws;
@@ -3522,18 +3676,25 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     return CRDTM_OK;
   };
   // speculation (below): every op applies, so the claim also writes the log
-  const bool spec = Q >= n && !t->remerge;
+  const bool spec = (devq || Q >= n) && !t->remerge;
   if (spec && (r = grow_for(n, n))) return r;
   if ((r = flat_rec(c, Q, fb.fr))) return r;
+  if (devq) {
+    fb.fr.qd = &dr->range_total;
+    fb.fr.nrd = &dr->max_replica;
+  }
   // replicas table: folded by the check over slot order when the range table fits in LDS
   const uint32_t nrep = maxr + 1 <= HOST_RANGES ? maxr + 1 : 0u;
   const uint32_t shm = (3 * nrep + (nrep ? 0 : REP_DIRECT)) * sizeof(uint32_t);
-  if (simple)
-    LAUNCH(k_fl_claim<true>, dim3(quad_grid(n)), dim3(BLOCK), shm, s, o, ix, Q, fb.fr, t->timestamp, c->rtab, dr,
-           nrep ? 0u : 1u, nrep, t->d, spec ? 1u : 0u);
+  if (simple && devq)
+    LAUNCH((k_fl_claim<true, true>), dim3(quad_grid(n)), dim3(BLOCK), shm, s, o, ix, Q, fb.fr, t->timestamp, c->rtab,
+           dr, nrep ? 0u : 1u, nrep, t->d, spec ? 1u : 0u);
+  else if (simple)
+    LAUNCH((k_fl_claim<true, false>), dim3(quad_grid(n)), dim3(BLOCK), shm, s, o, ix, Q, fb.fr, t->timestamp,
+           c->rtab, dr, nrep ? 0u : 1u, nrep, t->d, spec ? 1u : 0u);
   else
-    LAUNCH(k_fl_claim<false>, dim3(quad_grid(n)), dim3(BLOCK), shm, s, o, ix, Q, fb.fr, t->timestamp, c->rtab, dr,
-           nrep ? 0u : 1u, nrep, t->d, spec ? 1u : 0u);
+    LAUNCH((k_fl_claim<false, false>), dim3(quad_grid(n)), dim3(BLOCK), shm, s, o, ix, Q, fb.fr, t->timestamp,
+           c->rtab, dr, nrep ? 0u : 1u, nrep, t->d, spec ? 1u : 0u);
   auto finish = [&](uint32_t K, uint32_t applied, uint32_t already, uint64_t npath, long long new_ts) -> int {
     int rr = take_replicas(t, fb.rep);
     if (rr) return rr;
@@ -3557,7 +3718,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   if (spec) {
     if ((r = flat_order_commit(t, o, ix, Q, maxr, st, n, true, true, simple, true, fb))) return r;
     if (st_out) LAUNCH(k_status_out, dim3(g), dim3(BLOCK), 0, s, nullptr, n, NONE, st_out);
-    rr.now();  // (the order's last range read is behind: no launch after the result read)
+    rr.armed = false;  // (k_fl_rep_collect reset the range table: no launch after the result read)
     if ((r = sync_read(c))) return r;
     const DevResult& h = *c->hres;
     uint32_t present = 0, keys = 0, own = 0, slow = 0;  // (k_run_expand / k_fl_claim shards)
@@ -3568,8 +3729,25 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
       slow += h.fl_part[32 * k + 3];
     }
     if (h.bad_range) return CRDTM_E_RANGE;  // (k_fl_claim's path check; the caller restores the fresh tree)
+    if (devq) {
+      // the shape the launches assumed: every op an Add with a one-element
+      // path, non-negative timestamps, a dense range within the bound, replica
+      // ids below REP_SPEC; else nothing of this merge is kept
+      if (h.spec_fail || h.has_negative || h.max_replica >= REP_SPEC || h.range_total > Q ||
+          h.range_total > 4ULL * n + 65536) {
+        LAUNCH(k_reset_root, dim3(1), dim3(1), 0, s, t->d.s_next);
+        *done = false;
+        return CRDTM_OK;
+      }
+      Q = h.range_total;  // (known from here: the later launches take the host's values)
+      maxr = h.max_replica;
+      fb.fr.qd = nullptr;
+      fb.fr.nrd = nullptr;
+      if (t->max_depth < 1) t->max_depth = 1;
+    }
     const long long new_ts = t->timestamp + own - t->own_bias;
-    const bool every = h.err_index == NONE && slow == 0 && present == keys && keys == n;
+    // (devq: the merge assumed no slot without a node, Q == n)
+    const bool every = h.err_index == NONE && slow == 0 && present == keys && keys == n && (!devq || Q == n);
     if (every && replica_of(new_ts) == replica_of(t->timestamp)) {
       if (h.run_fail && (r = flat_order_fallback(t, Q, n, fb))) return r;
       res->guard = 0;
@@ -3584,13 +3762,13 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   }
   // ---- per-op statuses: duplicates, ts 0, errors ----
   LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr, nullptr,
-         nullptr);
+         nullptr, nullptr);
   LAUNCH(k_fl_stat_reset, dim3(1), dim3(1), 0, s, dr);
   LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, fb.fr, t->timestamp, c->rtab, dr);
   if ((r = sync_read(c))) return r;
   if (c->hres->dup_fix) {  // a smaller duplicate took its slot: the records are final now, decide again
     LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr, nullptr,
-           nullptr);
+           nullptr, nullptr);
     LAUNCH(k_fl_stat_reset, dim3(1), dim3(1), 0, s, dr);
     LAUNCH(k_fl_status, dim3(quad_grid(n)), dim3(BLOCK), 0, s, o, st, ix, Q, fb.fr, t->timestamp, c->rtab, dr);
     if ((r = sync_read(c))) return r;
@@ -3603,7 +3781,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   res->guard = guard;
   if (guard || h1.err_index != NONE)  // no commit: leave the replica table clean
     LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, nullptr, nullptr,
-           nullptr);
+           nullptr, nullptr);
   if (guard) {
     r = run_replay(t, o, st, res, guard);
     if (r == CRDTM_OK && st_out)
@@ -3647,6 +3825,45 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   w.st = ws.alloc<uint8_t>(n);
   uint32_t* rbase = ws.alloc<uint32_t>(RID_SLOTS + 1);
   DevResult* dr = c->dres;
+  // (env CRDTM_FORCE_REPLAY=1: every batch takes the one-lane sequential
+  // replay, so the cost of that fallback is measurable on any workload)
+  const char* fe = getenv("CRDTM_FORCE_REPLAY");
+  const bool force_replay = fe && fe[0] == '1';
+  // The flat speculation (config 3's shape): a fresh tree and as many path
+  // elements as ops, so every op may be an Add whose path is its anchor
+  // alone. The pre-pass reads the timestamps only, the claim checks the
+  // kinds and path offsets, and the whole merge is queued at once with the
+  // slot range read on the device (no host round trip between the pre-pass
+  // and the claim). The result read confirms the shape; a batch of another
+  // shape leaves nothing behind and takes the general path below.
+  // (env CRDTM_FLAT_SPEC=0: off)
+  static const bool spec_on = [] {
+    const char* e = getenv("CRDTM_FLAT_SPEC");
+    return !(e && e[0] == '0');
+  }();
+  if (spec_on && !force_replay && t->n_slots == 1 && t->log_n == 0 && !t->remerge && o.n_path == n) {
+    // slot range bound: the radix sort's key width for n (at least 64k
+    // slots: small batches with counter gaps), within the dense limit
+    uint32_t b = 8;
+    while (b < 32 && ((static_cast<uint64_t>(n) + 2) >> b) != 0) b += 8;
+    const uint64_t qcap = std::min<uint64_t>(std::max<uint64_t>((1ULL << b) - 2, 65536), 4ULL * n + 65536);
+    if (qcap + 2 < (1ULL << FR_ABITS) - 1) {
+      LAUNCH(k_dres_init, dim3(1), dim3(64), 0, s, dr);
+      const uint32_t gp = static_cast<uint32_t>(std::min<uint64_t>((n / 2 + PRE_T - 1) / PRE_T + 1, 512));
+      LAUNCH(k_pre_ts<PRE_T>, dim3(gp), dim3(PRE_T), 0, s, o.ts, n, c->crange, rbase, dr);
+      RangeReset spec_clean{c};  // (nr 0: up to the device's max_replica)
+      TsIndex ix;
+      ix.rng = c->crange;
+      ix.base = rbase;
+      ix.dense = 1;
+      ix.h = TsHash{nullptr, nullptr, 0};
+      ix.first = nullptr;
+      bool done = false;
+      int rs = apply_flat(t, o, ix, static_cast<uint32_t>(qcap), REP_SPEC - 1, w.st, st_out, res, true, spec_clean,
+                          true, &done);
+      if (rs || done) return rs;
+    }
+  }
   LAUNCH(k_dres_init, dim3(1), dim3(64), 0, s, dr);
   // (512 workgroups: each flushes its replica ranges and counters with
   // device-scope atomics that serialise per word, ~12 ns each)
@@ -3662,10 +3879,6 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   const uint32_t maxlen = c->hres->max_len;
   if (t->max_depth < maxlen) t->max_depth = maxlen;
   const uint32_t g = grid_for(n);
-  // (env CRDTM_FORCE_REPLAY=1: every batch takes the one-lane sequential
-  // replay, so the cost of that fallback is measurable on any workload)
-  const char* fe = getenv("CRDTM_FORCE_REPLAY");
-  const bool force_replay = fe && fe[0] == '1';
   if (force_replay || t->n_slots != 1 || t->log_n != 0) {
     // incremental merge into existing state: exact replay
     if (o.n_path) {

@@ -511,57 +511,65 @@ __global__ void __launch_bounds__(BLOCK) k_rs_scatter(const uint32_t* __restrict
                                                       uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                       uint32_t* __restrict__ inv) {
   constexpr uint32_t NW = BLOCK / 64;
-  __shared__ uint32_t run[256];
-  __shared__ uint32_t wc[NW][256];
+  static_assert(BLOCK == 256, "one digit per thread in the prefix step");
+  // per (row, wave, digit): the count of the wave's items of that digit in
+  // that row, then (in place) their first output position
+  __shared__ uint32_t wc[RS_ITEMS][NW][256];
   const uint32_t n = *n_dev;
   const uint32_t nt = rs_tiles(n);
   const uint32_t base = blockIdx.x * RS_TILE;
   if (base >= n) return;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (uint32_t d = threadIdx.x; d < 256; d += BLOCK) run[d] = off[d * nt + blockIdx.x];
-  for (uint32_t d = lane; d < 256; d += 64) wc[wv][d] = 0;  // kept all-zero between rounds
   const unsigned long long lt = (1ULL << lane) - 1ULL;
-  uint32_t ka[RS_ITEMS], va[RS_ITEMS];  // the tile's items, all loads in flight before the ranking rounds
+  uint32_t ka[RS_ITEMS], va[RS_ITEMS];  // the tile's items, all loads in flight first
 #pragma unroll
   for (uint32_t j = 0; j < RS_ITEMS; ++j) {
     const uint32_t i = base + j * BLOCK + threadIdx.x;
     ka[j] = i < n ? keys[i] : 0u;
     va[j] = i < n ? vals[i] : 0u;
   }
+  const uint32_t run0 = off[threadIdx.x * nt + blockIdx.x];  // (digit threadIdx.x: its tile's output base)
+#pragma unroll
+  for (uint32_t j = 0; j < RS_ITEMS; ++j)
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w) wc[j][w][threadIdx.x] = 0;
   __syncthreads();
+  // every row ranked at once: within a wave by digit match masks (8 ballots),
+  // the leader of each digit present stores the wave's count
+  uint32_t lr[RS_ITEMS];
 #pragma unroll
   for (uint32_t j = 0; j < RS_ITEMS; ++j) {
-    const uint32_t i = base + j * BLOCK + threadIdx.x;
-    const bool valid = i < n;
-    const uint32_t k = ka[j];
-    const uint32_t v = va[j];
-    const uint32_t d = (k >> shift) & 255u;
+    const bool valid = base + j * BLOCK + threadIdx.x < n;
+    const uint32_t d = (ka[j] >> shift) & 255u;
     unsigned long long m = __ballot(valid);
 #pragma unroll
     for (uint32_t b = 0; b < 8; ++b) {
       const unsigned long long bb = __ballot((d >> b) & 1u);
       m &= ((d >> b) & 1u) ? bb : ~bb;
     }
-    const uint32_t lr = static_cast<uint32_t>(__popcll(m & lt));
-    const bool leader = valid && lr == 0;  // one lane per digit present in the wave
-    if (leader) wc[wv][d] = static_cast<uint32_t>(__popcll(m));
-    __syncthreads();
-    uint32_t pre = 0;
-    for (uint32_t w = 0; w < wv; ++w) pre += wc[w][d];
-    const uint32_t pos = run[d] + pre + lr;
-    __syncthreads();  // every lane has read run[] and wc[]
-    for (uint32_t dd = threadIdx.x; dd < 256; dd += BLOCK) {
-      uint32_t t = 0;
-      for (uint32_t w = 0; w < NW; ++w) t += wc[w][dd];
-      run[dd] += t;
-    }
-    __syncthreads();  // run[] advanced, wc[] read
-    if (leader) wc[wv][d] = 0;
-    if (valid) {
-      kout[pos] = k;
-      vout[pos] = v;
-      if (inv) inv[v] = pos;
-    }
+    lr[j] = static_cast<uint32_t>(__popcll(m & lt));
+    if (valid && lr[j] == 0) wc[j][wv][d] = static_cast<uint32_t>(__popcll(m));
+  }
+  __syncthreads();
+  {  // thread = digit: exclusive prefix over (row, wave) in item order (stable)
+    uint32_t run = run0;
+#pragma unroll
+    for (uint32_t j = 0; j < RS_ITEMS; ++j)
+#pragma unroll
+      for (uint32_t w = 0; w < NW; ++w) {
+        const uint32_t c = wc[j][w][threadIdx.x];
+        wc[j][w][threadIdx.x] = run;
+        run += c;
+      }
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < RS_ITEMS; ++j) {
+    if (base + j * BLOCK + threadIdx.x >= n) continue;
+    const uint32_t pos = wc[j][wv][(ka[j] >> shift) & 255u] + lr[j];
+    kout[pos] = ka[j];
+    vout[pos] = va[j];
+    if (inv) inv[va[j]] = pos;
   }
 }
 

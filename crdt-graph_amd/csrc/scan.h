@@ -43,19 +43,21 @@ __global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* out, uint64_
   // vector load/store instruction touch one 16-byte piece of 64 lines)
   __shared__ __attribute__((aligned(16))) uint32_t sx[DS_TILE];
   const unsigned long long ep = static_cast<unsigned long long>(epoch) << 32;
+  // a device-side item count (<= n): the workgroups past its tiles leave
+  // before drawing a ticket (the host launches for n: a launch sized for 10M
+  // slots over 1M runs had 1,100 idle workgroups serialising ~12 ns each on
+  // the ticket word)
+  if (n_dev && *n_dev < n) {
+    n = *n_dev;
+    ntiles = n ? static_cast<uint32_t>((n - 1) / DS_TILE) + 1u : 1u;
+    if (blockIdx.x >= ntiles) return;
+  }
   if (threadIdx.x == 0) {
     s_tile = atomicAdd(ticket, 1u);
     if (s_tile == ntiles - 1) atomicExch(ticket, 0u);  // every ticket is drawn: ready for the next scan
   }
   __syncthreads();
   const uint32_t tile = s_tile;
-  // a device-side item count (<= n): tiles past it only draw their ticket
-  if (n_dev && *n_dev < n) {
-    n = *n_dev;
-    const uint32_t last = n ? static_cast<uint32_t>((n - 1) / DS_TILE) : 0u;
-    if (tile > last) return;
-    ntiles = last + 1;
-  }
   const uint64_t b = static_cast<uint64_t>(tile) * DS_TILE + static_cast<uint64_t>(threadIdx.x) * DS_ITEMS;
   uint32_t v[DS_ITEMS];
   const uint64_t tb = static_cast<uint64_t>(tile) * DS_TILE;

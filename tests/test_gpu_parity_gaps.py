@@ -232,3 +232,67 @@ def test_guard_g_statistics_match_oracle(monkeypatch, blocked):
         assert int(got[3]) == int(want[2]) and int(got[2]) <= int(got[3])
         checked += 1
     assert checked >= 4
+
+
+def _arrays(ops):
+    """[(kind, ts, path list, val)] -> packed host arrays."""
+    kind = np.array([o[0] for o in ops], np.uint8)
+    ts = np.array([o[1] for o in ops], np.int64)
+    off = np.zeros(len(ops) + 1, np.uint32)
+    off[1:] = np.cumsum([len(o[2]) for o in ops])
+    path = np.array([k for o in ops for k in o[2]] or [0], np.int64)[:int(off[-1])]
+    val = np.array([o[3] for o in ops], np.uint32)
+    return dict(kind=kind, ts=ts, path_off=off, path=path, val=val)
+
+
+def _flat_ops(n, replicas=8, seed=3):
+    s = N.synth(n_ops=n, replicas=replicas, window=16, seed=seed)
+    return [(0, int(s["ts"][i]), [int(s["path"][i])], int(s["val"][i])) for i in range(n)]
+
+
+@pytest.mark.parametrize("shape", ["flat", "with_delete", "empty_and_long_path", "replica_300", "negative_ts",
+                                   "duplicate_ts", "counter_holes", "sentinel_ts"])
+def test_flat_speculation_shapes(shape):
+    """The flat speculation (merge.hip apply_core: a fresh tree whose batch has
+    as many path elements as ops is merged at once, the slot range read on
+    the device) must keep exactly the reference's result for every batch of
+    that size, also those it does not serve: a Delete among the Adds, an
+    empty path balanced by a two-key path (InvalidPath), a replica id above
+    its LDS table, a negative timestamp, duplicate timestamps and timestamps
+    with counter holes (the status path), the sentinel's key 0."""
+    ops = _flat_ops(4000)
+    if shape == "with_delete":
+        ops.append((1, 0, [ops[100][1]], 0))
+    elif shape == "empty_and_long_path":
+        ops[2000] = (0, ops[2000][1], [], 7)
+        ops[2001] = (0, ops[2001][1], [0, ops[5][1]], 7)
+    elif shape == "replica_300":
+        ops.append((0, (300 << 32) + 1, [ops[10][1]], 9))
+    elif shape == "negative_ts":
+        ops.append((0, -((3 << 32) + 5), [ops[10][1]], 9))
+    elif shape == "duplicate_ts":
+        ops.append((0, ops[50][1], [ops[10][1]], 9))
+    elif shape == "counter_holes":  # replica 7's counters jump: slots without a node
+        ops.append((0, (7 << 32) + 100000, [ops[10][1]], 9))
+        ops.append((0, (7 << 32) + 100007, [(7 << 32) + 100000], 9))
+    elif shape == "sentinel_ts":
+        ops.append((0, 0, [ops[10][1]], 9))
+    s = _arrays(ops)
+    n = len(ops)
+    assert int(s["path_off"][-1]) == n  # (the speculation's trigger)
+    ot, rc, oerr = oracle_apply_arrays(s, n)
+    et = CRDTree.init(0)
+    st = np.full(n, 9, np.uint8)
+    res = et.apply_arrays(s, n, status=st)
+    assert (res.code, res.err_index if rc else -1) == (rc, oerr if rc else -1), (shape, res.code, rc)
+    assert engine_summary(et) == oracle_summary(ot), shape
+    if rc == 0:
+        assert engine_log(et, 0) == oracle_log(ot, 0)
+        assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+        assert res.n_applied == int(np.sum(st == 0))
+    olib_free(ot)
+
+
+def olib_free(t):
+    from oracle.oracle import lib as olib
+    olib().orc_free(t)
