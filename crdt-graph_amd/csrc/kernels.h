@@ -21,6 +21,17 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 #ifndef CRDTM_NT
 #define CRDTM_NT 1
 #endif
+#ifndef CRDTM_NT_NODES
+#define CRDTM_NT_NODES 1
+#endif
+template <class T>
+__device__ __forceinline__ void st_node(T* p, T v) {  // (the node records' stores)
+#if CRDTM_NT && CRDTM_NT_NODES
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
 template <class T>
 __device__ __forceinline__ void st_stream(T* p, T v) {
 #if CRDTM_NT

@@ -237,15 +237,21 @@ __global__ void __launch_bounds__(BLOCK) k_path_range(OpsDev o, DevResult* dres)
 }
 
 // The flat speculation's pre-pass (launched when every op may be an Add with
-// a one-element path, n_path == n: the claim checks that itself): the
-// per-replica counter ranges from the timestamps alone (16-byte loads, ids
-// below REP_SPEC in an LDS table), |ts| < 2^53, negative timestamps and the
-// largest replica id. The workgroup that finishes last lays the ranges end
-// to end (base[], range_total, the slot words fl_nw), so the claim follows
-// on the device without a host round trip.
+// a one-element path, n_path == n): the per-replica counter ranges of the
+// timestamps (16-byte loads, ids below REP_SPEC in an LDS table), |ts| < 2^53,
+// negative timestamps and the largest replica id, and the check that every
+// op is an Add whose path is path[i] alone (kind, path_off[i] == i; else
+// DevResult::spec_fail). The workgroup that finishes last lays the ranges end
+// to end (base[], range_total, the slot words fl_nw), so the claim follows on
+// the device without a host round trip.
 constexpr uint32_t REP_SPEC = 256;
-template <uint32_t PB>
-__global__ void __launch_bounds__(PB) k_pre_ts(const long long* __restrict__ ts, uint32_t n, uint2* rng,
+// BLIND: every op's min/max goes to the LDS table as a no-return atomic
+// (nothing to wait for) instead of a read first and an atomic only when the
+// read does not cover it (a typing replica's counters rise through the
+// batch, so its maximum moves on nearly every op anyway)
+template <uint32_t PB, bool BLIND>
+__global__ void __launch_bounds__(PB) k_pre_ts(const long long* __restrict__ ts, const uint8_t* __restrict__ kind,
+                                               const uint32_t* __restrict__ off, uint32_t n, uint2* rng,
                                                uint32_t* base, DevResult* dres) {
   __shared__ uint32_t rlo[REP_SPEC], rhi[REP_SPEC];
   __shared__ uint32_t s_last, sw[PB / 64];
@@ -254,7 +260,7 @@ __global__ void __launch_bounds__(PB) k_pre_ts(const long long* __restrict__ ts,
     rhi[j] = 0;
   }
   __syncthreads();
-  uint32_t bad = 0, neg = 0, maxr = 0;
+  uint32_t bad = 0, neg = 0, maxr = 0, vfail = 0;
   auto fold = [&](long long t) {
     if (t >= TWO53 || t <= -TWO53) {
       bad = 1;
@@ -264,31 +270,50 @@ __global__ void __launch_bounds__(PB) k_pre_ts(const long long* __restrict__ ts,
       const uint32_t r = static_cast<uint32_t>(static_cast<uint64_t>(t) >> 32), c = static_cast<uint32_t>(t);
       maxr = max(maxr, r);
       if (r < REP_SPEC) {  // (the table only narrows: a covering read makes the atomic unnecessary)
-        if (c < rlo[r]) atomicMin(&rlo[r], c);
-        if (c > rhi[r]) atomicMax(&rhi[r], c);
+        if (BLIND || c < rlo[r]) atomicMin(&rlo[r], c);
+        if (BLIND || c > rhi[r]) atomicMax(&rhi[r], c);
       }
     }
   };
   {
     const longlong2* t2 = reinterpret_cast<const longlong2*>(ts);
+    const uchar2* k2 = reinterpret_cast<const uchar2*>(kind);
+    const uint2* o2 = reinterpret_cast<const uint2*>(off);
+    auto verify = [&](uint32_t p, uchar2 k, uint2 f) {  // ops 2p, 2p + 1
+      vfail |= (k.x | k.y) != CRDTM_ADD || f.x != 2 * p || f.y != 2 * p + 1;
+    };
     const uint32_t np = n / 2, gs = gridDim.x * PB;
     uint32_t p = blockIdx.x * PB + threadIdx.x;
     for (; p + 3 * gs < np; p += 4 * gs) {  // four pairs in flight
       longlong2 v[4];
+      uchar2 k[4];
+      uint2 f[4];
 #pragma unroll
-      for (uint32_t u = 0; u < 4; ++u) v[u] = t2[p + u * gs];
+      for (uint32_t u = 0; u < 4; ++u) {
+        v[u] = t2[p + u * gs];
+        k[u] = k2[p + u * gs];
+        f[u] = o2[p + u * gs];
+      }
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u) {
         fold(v[u].x);
         fold(v[u].y);
+        verify(p + u * gs, k[u], f[u]);
       }
     }
     for (; p < np; p += gs) {
       const longlong2 v = t2[p];
       fold(v.x);
       fold(v.y);
+      verify(p, k2[p], o2[p]);
     }
-    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) fold(ts[n - 1]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      if (n & 1) {
+        fold(ts[n - 1]);
+        vfail |= kind[n - 1] != CRDTM_ADD || off[n - 1] != n - 1;
+      }
+      vfail |= off[n] != n;
+    }
   }
   auto mxf = [](uint32_t a, uint32_t b) { return a > b ? a : b; };
   maxr = block_reduce_t<PB>(maxr, 0u, mxf);  // (synchronises the block)
@@ -299,7 +324,9 @@ __global__ void __launch_bounds__(PB) k_pre_ts(const long long* __restrict__ ts,
     }
   bad = block_reduce_t<PB>(bad, 0u, mxf);
   neg = block_reduce_t<PB>(neg, 0u, mxf);
+  vfail = block_reduce_t<PB>(vfail, 0u, mxf);
   if (threadIdx.x == 0) {
+    if (vfail) atomicOr(&dres->spec_fail, 1u);
     if (bad) atomicOr(&dres->bad_range, 1u);
     if (neg) atomicOr(&dres->has_negative, 1u);
     if (maxr) atomicMax(&dres->max_replica, maxr);
@@ -2183,18 +2210,15 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
                                                     uint32_t log_to_tree) {
   Q = fr.q(Q);
   nrep = fr.nrep(nrep);
-  // dynamic LDS: the replica range table (nrep ids: base, min, max counter)
-  // when it fits, else lookups go to the global table; rv when track_rep
+  // dynamic LDS: the replica range table (nrep ids: {base, min, max counter}
+  // in one 16-byte entry, one LDS read per lookup) when it fits, else
+  // lookups go to the global table; rv when track_rep
   extern __shared__ __attribute__((aligned(16))) uint32_t scl[];
-  uint32_t* sbase = scl;
-  uint32_t* smin = scl + nrep;
-  uint32_t* smax = scl + 2 * nrep;
-  uint32_t* rv = scl + 3 * nrep;
+  uint4* stab = reinterpret_cast<uint4*>(scl);
+  uint32_t* rv = scl + 4 * nrep;
   for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x) {
-    sbase[j] = x.base[j];
     const uint2 g = x.rng[j];
-    smin[j] = g.x;
-    smax[j] = g.y;
+    stab[j] = make_uint4(x.base[j], g.x, g.y, 0u);
   }
   if (track_rep)
     for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) rv[j] = 0;
@@ -2204,9 +2228,10 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
     if (ts <= 0) return NONE;
     const uint64_t r = static_cast<uint64_t>(ts) >> 32;
     if (r >= nrep) return NONE;
-    const uint32_t c = static_cast<uint32_t>(ts), lo = smin[r];
-    if (lo == NONE || c < lo || c > smax[r]) return NONE;
-    return sbase[r] + (c - lo);
+    const uint4 e = stab[r];
+    const uint32_t c = static_cast<uint32_t>(ts), lo = e.y;
+    if (lo == NONE || c < lo || c > e.z) return NONE;
+    return e.x + (c - lo);
   };
   const long long id0 = replica_of(ts0);
   uint32_t keys = 0, own = 0, slow = 0, err = NONE, mr = 0, bad = 0, vfail = 0;
@@ -2516,15 +2541,20 @@ __device__ __forceinline__ long long fl_key(uint32_t q, const uint32_t* sb, cons
 // The trip count is wave-uniform, so every lane takes part in the ballots.
 constexpr uint32_t RM_UNROLL = 4;       // k_run_heads: words per wave and iteration
 constexpr uint32_t RM_MASK_UNROLL = 2;  // k_run_mask (48 VGPRs, full occupancy; 4 words: 68, 120 -> 110 us at flat10m)
-template <uint32_t U>
+// DEVQ: the speculation without the host round trip (FlatRec::qd): the slot
+// range and replica count come from the device (the tree's slot capacity
+// covers the host's bound, so a speculation the host will discard stays in
+// bounds).
+template <uint32_t U, bool DEVQ>
 __global__ void __launch_bounds__(BLOCK) k_run_mask(FlatRec fr, uint32_t Q, unsigned long long* hm, uint32_t* hc,
                                                    TreeDev T, const uint32_t* qc, const uint32_t* logidx, OpsDev o,
-                                                   TsIndex x, uint32_t nrep, DevResult* chk, uint32_t* rtab,
-                                                   uint64_t slot_cap) {
+                                                   TsIndex x, uint32_t nrep, DevResult* chk, uint32_t* rtab) {
   extern __shared__ uint32_t smk[];  // dynamic: 3 * nrep words when the tables fit (HOST_RANGES)
-  Q = fr.q(Q);
   const bool lds = nrep <= HOST_RANGES;
-  nrep = fr.nrep(nrep);
+  if (DEVQ) {
+    Q = fr.q(Q);
+    nrep = fr.nrep(nrep);
+  }
   uint32_t* sb = smk;
   uint32_t* sc = smk + nrep;
   uint32_t* srv = smk + 2 * nrep;  // (chk) largest op index + 1 per replica
@@ -2573,15 +2603,38 @@ __global__ void __launch_bounds__(BLOCK) k_run_mask(FlatRec fr, uint32_t Q, unsi
       }
       uint32_t rep = NONE;
       const uint32_t fi = rq[u].y;
-      // (a speculation over slots with no node, which the host then
-      // discards, may reach past the tree's capacity: those stores are dropped)
-      if (pres && (qc || 1ULL + q < slot_cap)) {  // (streaming stores: the merge does not read them back)
+      // the replica of the word's first slot, searched once for the wave
+      // (uniform LDS reads); a lane past that replica's range (a word that
+      // straddles two ranges) searches for itself
+      uint32_t wr = 0, wlo = NONE, whi = 0;
+      if (lds) {
+        const uint32_t q0 = (w0 + u) << 6;
+        uint32_t lo = 0, hi = nrep;
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (sb[mid] <= q0) lo = mid;
+          else hi = mid;
+        }
+        wr = lo;
+        wlo = sb[lo];
+        whi = lo + 1 < nrep ? sb[lo + 1] : NONE;
+      }
+      if (pres) {  // (streaming stores: the merge does not read them back)
         const uint32_t slot = 1 + (qc ? qc[q] : q);
-        st_stream(T.s_key + slot, lds ? fl_key(q, sb, sc, nrep, rep) : o.ts[fi]);
-        st_stream(T.s_dict + slot, 0u);
-        st_stream(T.s_src + slot, logidx ? logidx[fi] : fi);
-        st_stream(T.s_flags + slot, static_cast<uint8_t>(0));
-        st_stream(T.s_child + slot, NONE);
+        long long key;
+        if (!lds) {
+          key = o.ts[fi];
+        } else if (q >= wlo && q < whi) {
+          rep = wr;
+          key = (static_cast<long long>(wr) << 32) | static_cast<long long>(sc[wr] + (q - wlo));
+        } else {
+          key = fl_key(q, sb, sc, nrep, rep);
+        }
+        st_node(T.s_key + slot, key);
+        st_node(T.s_dict + slot, 0u);
+        st_node(T.s_src + slot, logidx ? logidx[fi] : fi);
+        st_node(T.s_flags + slot, static_cast<uint8_t>(0));
+        st_node(T.s_child + slot, NONE);
         if (chk) {
           ++present;
           if (qa != Q) {
@@ -2828,8 +2881,8 @@ constexpr uint32_t EX_ITERS = 128;  // k_run_expand keeps its run-mask words in 
 // the top-down chain) takes every field it needs from one line:
 // rr[r] = {parent run (NONE: a child of the root sentinel, or a hole run),
 //          length (after k_run_tree_up: w, the head's rank minus its parent
-//          run head's rank), sorted positions [z, w) of its child runs ({0, 0}:
-//          none)}.
+//          run head's rank), sorted positions [z, w) of its child runs
+//          ({NONE, 0}: none)}.
 struct RunArr {
   const uint32_t* nR;        // device: number of runs
   uint2* hh;                 // {head slot, anchor of the head (ABSENT: a hole run), then its effective parent}
@@ -2858,11 +2911,25 @@ struct RunArr {
 // its length, and the sibling sort's input (key = attach slot, the root
 // sentinel = Q, hole runs Q + 1) listed in descending run order, so the
 // stable sort leaves siblings at one slot in descending slot order.
+// COHERENT: the {head, anchor} words are read and the effective parents
+// written at agent scope (past the XCDs' L2s, so a walk sees what walks on
+// other XCDs resolved); else through the L2 (a walk may then read an anchor
+// another XCD already replaced by its effective parent: also exact, see
+// above, only possibly longer).
+template <bool COHERENT>
 __device__ __forceinline__ uint2 hh_load(const uint2* p) {
   const unsigned long long v =
-      __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      COHERENT ? __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT)
+               : *reinterpret_cast<const unsigned long long*>(p);
   return make_uint2(static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32));
 }
+template <bool COHERENT>
+__device__ __forceinline__ void hh_store_ep(uint2* p, uint32_t d) {
+  if (COHERENT) __hip_atomic_store(&p->y, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else p->y = d;
+}
+template <bool COHERENT>
 __global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, RunMask rm, FlatRec fr, uint32_t* skey,
                                                   uint32_t* sval) {
   Q = fr.q(Q);
@@ -2874,7 +2941,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, RunMask 
     uint32_t d = me.y;
     const uint32_t hn = r + 1 < R ? a.hh[r + 1].x : Q;
     if (d == ABSENT) {  // a hole run
-      a.rr[r] = make_uint4(NONE, 0u, 0u, 0u);
+      a.rr[r] = make_uint4(NONE, 0u, NONE, 0u);  // (child range [z, w): none)
       a.ca[r] = 0;
       skey[R - 1 - r] = Q + 1;
       sval[R - 1 - r] = r;
@@ -2886,21 +2953,26 @@ __global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, RunMask 
       // or hold a cycle: those walks end at the sentinel, which keeps every
       // walk finite and in bounds, and the speculation is discarded)
       for (uint32_t steps = 0; d < Q && d > x; ++steps) {
-        const uint2 hj = hh_load(a.hh + run_of(rm, d));
+        const uint2 hj = hh_load<COHERENT>(a.hh + run_of(rm, d));
         if (hj.x <= x || steps > R) {
           d = Q;
           break;
         }
         d = hj.y;
       }
-      if (d >= Q || !fr.present(fr.rec[d].x)) d = Q;
-      __hip_atomic_store(&a.hh[r].y, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (d != Q && (d >= x || !fr.present(fr.rec[d].x))) {  // (self-anchored / nodeless anchor: a failing batch)
+      if (d >= Q) d = Q;
+      hh_store_ep<COHERENT>(&a.hh[r], d);
+    } else if (d == x) {  // (self-anchored: a failing batch)
       d = Q;
-      __hip_atomic_store(&a.hh[r].y, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      hh_store_ep<COHERENT>(&a.hh[r], d);
     }
+    // (an anchor at a slot without a node — a failing batch, whose speculation
+    // the slot pass's check discards — is left as it is: its run is a hole
+    // run with a smaller index, so the run tree stays a forest and every
+    // later index stays in range; a batch that reaches the commit after its
+    // statuses has every anchor present)
     // (len: a hole after the run is a run of its own)
-    a.rr[r] = make_uint4(d == Q ? NONE : run_of(rm, d), hn - x, 0u, 0u);
+    a.rr[r] = make_uint4(d == Q ? NONE : run_of(rm, d), hn - x, NONE, 0u);
     a.ca[r] = 0;
     skey[R - 1 - r] = d;
     sval[R - 1 - r] = r;
@@ -2957,7 +3029,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_tree_up(RunArr a, const uint32_t*
     if (k < R) {
       const uint4 e = a.rr[sarr[k]];
       key = e.x;
-      if (e.w == e.z) {
+      if (e.w <= e.z) {  // (no child runs: [NONE, 0))
         const uint32_t t = e.y;
         a.tk[k] = t;  // (kinv[r] == k)
         v = (1ULL << 32) | t;
@@ -2989,7 +3061,9 @@ __device__ __forceinline__ uint32_t run_S(const uint32_t* xs, uint32_t k) { retu
 // (contiguous: P owns a contiguous slot range and the list is by slot); the
 // first position of the root sentinel's children to *groot. Neighbours'
 // parents come from the adjacent lanes (a wave holds consecutive positions).
-__global__ void __launch_bounds__(BLOCK) k_run_gstart(RunArr a, uint32_t Q, const uint32_t* pk, const uint32_t* sarr,
+// (a parent run comes from the run masks of its attach slot, L2-resident,
+// instead of a gather of the child's record)
+__global__ void __launch_bounds__(BLOCK) k_run_gstart(RunArr a, uint32_t Q, const uint32_t* pk, RunMask rm,
                                                       uint32_t* groot) {
   if (a.qd) Q = min(*a.qd, Q);  // (FlatRec::q: the bound stays the limit)
   const uint32_t R = *a.nR;
@@ -2997,13 +3071,13 @@ __global__ void __launch_bounds__(BLOCK) k_run_gstart(RunArr a, uint32_t Q, cons
   for (uint32_t k0 = blockIdx.x * blockDim.x; k0 < R; k0 += gridDim.x * blockDim.x) {
     const uint32_t k = k0 + threadIdx.x;
     const uint32_t p = k < R ? pk[k] : Q + 1;
-    const uint32_t P = p < Q ? a.rr[sarr[k]].x : NONE;
+    const uint32_t P = p < Q ? run_of(rm, p) : NONE;
     uint32_t Pp = __shfl_up(P, 1, 64), Pn = __shfl_down(P, 1, 64);
     if (k >= R) continue;
     if (p == Q && (k == 0 || pk[k - 1] != Q)) *groot = k;
     if (p >= Q) continue;
-    if (lane == 0) Pp = k ? (pk[k - 1] < Q ? a.rr[sarr[k - 1]].x : NONE) : NONE;
-    if (lane == 63 || k + 1 == R) Pn = k + 1 < R && pk[k + 1] < Q ? a.rr[sarr[k + 1]].x : NONE;
+    if (lane == 0) Pp = k ? (pk[k - 1] < Q ? run_of(rm, pk[k - 1]) : NONE) : NONE;
+    if (lane == 63 || k + 1 == R) Pn = k + 1 < R && pk[k + 1] < Q ? run_of(rm, pk[k + 1]) : NONE;
     if (Pp != P) a.rr[P].z = k;
     if (Pn != P) a.rr[P].w = k + 1;
   }
@@ -3015,7 +3089,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_gstart(RunArr a, uint32_t Q, cons
 // itself comes after p and after its siblings at p with a larger slot (the
 // ones sorted before it): together, the child runs of P sorted before r.
 __global__ void __launch_bounds__(BLOCK) k_run_w(RunArr a, uint32_t Q, const uint32_t* sarr, const uint32_t* pk,
-                                                 const uint32_t* xs, const uint32_t* groot) {
+                                                 const uint32_t* xs, const uint32_t* groot, RunMask rm) {
   if (a.qd) Q = min(*a.qd, Q);  // (FlatRec::q: the bound stays the limit)
   RUN_LOOP(k) {
     const uint32_t r = sarr[k], p = pk[k];
@@ -3024,7 +3098,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_w(RunArr a, uint32_t Q, const uin
     if (p == Q) {
       a.rr[r].y = run_S(xs, k) - run_S(xs, *groot);
     } else {
-      const uint32_t P = a.rr[r].x;
+      const uint32_t P = run_of(rm, p);  // (= the record's parent: the run holding the attach slot)
       a.rr[r].y = run_S(xs, k) - run_S(xs, a.rr[P].z) + (p - a.hh[P].x) + 1u;
     }
   }
@@ -3543,9 +3617,17 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     }
     const uint32_t gw = std::max<uint32_t>(1, std::min<uint32_t>(2048, (NW + RM_MASK_UNROLL * (BLOCK / 64) - 1) /
                                                                            (RM_MASK_UNROLL * (BLOCK / 64))));
-    LAUNCH(k_run_mask<RM_MASK_UNROLL>, dim3(gw), dim3(BLOCK),
-           maxr + 1 <= HOST_RANGES ? 3 * (maxr + 1) * sizeof(uint32_t) : 0, s, fr, Q, hm, hc, t->d, qc, logidx, o, ix,
-           maxr + 1, check ? dr : nullptr, c->rtab, static_cast<uint64_t>(t->cap.slots));
+    const size_t mshm = maxr + 1 <= HOST_RANGES ? 3 * (maxr + 1) * sizeof(uint32_t) : 0;
+    static const bool mask_devq = [] {  // (A/B: the device-range instance on every merge)
+      const char* e = getenv("CRDTM_MASK_DEVQ");
+      return e && e[0] == '1';
+    }();
+    if (fr.qd || mask_devq)
+      LAUNCH((k_run_mask<RM_MASK_UNROLL, true>), dim3(gw), dim3(BLOCK), mshm, s, fr, Q, hm, hc, t->d, qc, logidx, o,
+             ix, maxr + 1, check ? dr : nullptr, c->rtab);
+    else
+      LAUNCH((k_run_mask<RM_MASK_UNROLL, false>), dim3(gw), dim3(BLOCK), mshm, s, fr, Q, hm, hc, t->d, qc, logidx, o,
+             ix, maxr + 1, check ? dr : nullptr, c->rtab);
     if ((r = dscan<SumOp, false>(ArrGen{hc}, hb, NW, &dr->run_count, ws, s, nullptr, fr.qd ? &dr->fl_nw : nullptr,
                                  "k_dscan_runs")))
       return r;
@@ -3561,17 +3643,29 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     uint32_t* xs = ws.alloc<uint32_t>(Q + 1);
     uint32_t* groot = fb.cnt;  // one word: the root sentinel's first child in the sorted list
     const uint32_t gr = grid_for(Q, BLOCK, 2048);
-    LAUNCH(k_run_ep, dim3(gr), dim3(BLOCK), 0, s, ra, Q, fb.rm, fr, sk[0], sv[0]);
-    uint32_t sbits = 8;
-    while (sbits < 32 && ((static_cast<uint64_t>(Q) + 1) >> sbits) != 0) sbits += 8;
+    // (env CRDTM_EP_COHERENT=1: the walks read and write at agent scope)
+    static const bool ep_coh = [] {
+      const char* e = getenv("CRDTM_EP_COHERENT");
+      return e && e[0] == '1';
+    }();
+    if (ep_coh) LAUNCH(k_run_ep<true>, dim3(gr), dim3(BLOCK), 0, s, ra, Q, fb.rm, fr, sk[0], sv[0]);
+    else LAUNCH(k_run_ep<false>, dim3(gr), dim3(BLOCK), 0, s, ra, Q, fb.rm, fr, sk[0], sv[0]);
     uint32_t *pk = nullptr, *sarr = nullptr;  // attach slot, run: siblings grouped by slot, slots ascending
-    if ((r = radix_sort_pairs(sk[0], sv[0], sk[1], sv[1], ra.nR, Q, sbits, ws, s, &pk, &sarr, kinv))) return r;
-    ra.tk = pk == sk[0] ? sk[1] : sk[0];  // (free after the sort)
-    LAUNCH(k_run_gstart, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, sarr, groot);
+    // (measured and reverted in round 5: a bucket sort — bucket histograms,
+    // one scatter, an LDS bitonic sort per bucket — was 3.4 ms against 0.09:
+    // attach slots concentrate on the document's early slots, so 53 buckets
+    // of 16k slots held 4k-28k runs and sorted in global memory)
+    {
+      uint32_t sbits = 8;
+      while (sbits < 32 && ((static_cast<uint64_t>(Q) + 1) >> sbits) != 0) sbits += 8;
+      if ((r = radix_sort_pairs(sk[0], sv[0], sk[1], sv[1], ra.nR, Q, sbits, ws, s, &pk, &sarr, kinv))) return r;
+      ra.tk = pk == sk[0] ? sk[1] : sk[0];  // (free after the sort)
+      LAUNCH(k_run_gstart, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, fb.rm, groot);
+    }
     // ---- subtree sizes (one launch, in sorted order), head ranks, the document order ----
     LAUNCH(k_run_tree_up, dim3(gr), dim3(BLOCK), 0, s, ra, sarr);
     if ((r = dscan<SumOp, true>(ArrGen{ra.tk}, xs, Q, nullptr, ws, s, nullptr, ra.nR, "k_dscan_xs"))) return r;
-    LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, groot);
+    LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, groot, fb.rm);
     LAUNCH(k_run_pos, dim3(gr), dim3(BLOCK), 0, s, ra, dr);
     // ---- the document order, the chain ----
     const uint32_t gx = grid_for(Q, BLOCK, 2048);
@@ -3579,6 +3673,10 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     LAUNCH(k_run_expand, dim3(gx), dim3(BLOCK),
            ex_iters <= EX_ITERS ? 3 * ex_iters * (BLOCK / 64) * sizeof(uint32_t) : 0, s, ra, Q, K, fb.rm, pk, xs, qc,
            t->d.doc, fr, ex_iters <= EX_ITERS ? ex_iters : 0u);
+    // (measured and reverted in round 5: the raw `next` written in slot order
+    // by the expansion — the run's next slot, the first child run at the
+    // slot, or the successor of the run's sub-document found by a walk up in
+    // k_run_pos — cost 36 + 32 us more there than this pass's 33 us)
     LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d, t->cap.slots);
     if (all_applied && !log_done) fl_log_copy(c, o, t->d, simple);
   } else if (all_applied && !log_done) {
@@ -3676,20 +3774,20 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
     return CRDTM_OK;
   };
   // speculation (below): every op applies, so the claim also writes the log
+  // (devq: slots up to the bound Q, which the device's range may reach)
   const bool spec = (devq || Q >= n) && !t->remerge;
-  if (spec && (r = grow_for(n, n))) return r;
+  if (spec && (r = grow_for(devq ? Q : n, n))) return r;
   if ((r = flat_rec(c, Q, fb.fr))) return r;
   if (devq) {
     fb.fr.qd = &dr->range_total;
     fb.fr.nrd = &dr->max_replica;
   }
   // replicas table: folded by the check over slot order when the range table fits in LDS
-  const uint32_t nrep = maxr + 1 <= HOST_RANGES ? maxr + 1 : 0u;
-  const uint32_t shm = (3 * nrep + (nrep ? 0 : REP_DIRECT)) * sizeof(uint32_t);
-  if (simple && devq)
-    LAUNCH((k_fl_claim<true, true>), dim3(quad_grid(n)), dim3(BLOCK), shm, s, o, ix, Q, fb.fr, t->timestamp, c->rtab,
-           dr, nrep ? 0u : 1u, nrep, t->d, spec ? 1u : 0u);
-  else if (simple)
+  // (16 bytes per replica in the claim's LDS table: up to 3,840 replicas there)
+  const uint32_t nrep = maxr + 1 <= HOST_RANGES && maxr + 1 <= 3840 ? maxr + 1 : 0u;
+  const uint32_t shm = (4 * nrep + (nrep ? 0 : REP_DIRECT)) * sizeof(uint32_t);
+  // (devq: k_pre_ts has checked the kinds and offsets; k_fl_claim<true, true> checks them itself)
+  if (simple)
     LAUNCH((k_fl_claim<true, false>), dim3(quad_grid(n)), dim3(BLOCK), shm, s, o, ix, Q, fb.fr, t->timestamp,
            c->rtab, dr, nrep ? 0u : 1u, nrep, t->d, spec ? 1u : 0u);
   else
@@ -3849,8 +3947,20 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
     const uint64_t qcap = std::min<uint64_t>(std::max<uint64_t>((1ULL << b) - 2, 65536), 4ULL * n + 65536);
     if (qcap + 2 < (1ULL << FR_ABITS) - 1) {
       LAUNCH(k_dres_init, dim3(1), dim3(64), 0, s, dr);
-      const uint32_t gp = static_cast<uint32_t>(std::min<uint64_t>((n / 2 + PRE_T - 1) / PRE_T + 1, 512));
-      LAUNCH(k_pre_ts<PRE_T>, dim3(gp), dim3(PRE_T), 0, s, o.ts, n, c->crange, rbase, dr);
+      // (env CRDTM_PRE_GRID: workgroups; CRDTM_PRE_BLIND=1: no-return atomics only)
+      static const uint32_t pre_grid = [] {
+        const char* e = getenv("CRDTM_PRE_GRID");
+        return e ? static_cast<uint32_t>(atoi(e)) : 256u;  // (256 x 1024 threads: 55 -> 48 us at flat10m)
+      }();
+      static const bool pre_blind = [] {
+        const char* e = getenv("CRDTM_PRE_BLIND");
+        return e && e[0] == '1';
+      }();
+      const uint32_t gp = static_cast<uint32_t>(std::min<uint64_t>((n / 2 + PRE_T - 1) / PRE_T + 1, pre_grid));
+      if (pre_blind)
+        LAUNCH((k_pre_ts<PRE_T, true>), dim3(gp), dim3(PRE_T), 0, s, o.ts, o.kind, o.off, n, c->crange, rbase, dr);
+      else
+        LAUNCH((k_pre_ts<PRE_T, false>), dim3(gp), dim3(PRE_T), 0, s, o.ts, o.kind, o.off, n, c->crange, rbase, dr);
       RangeReset spec_clean{c};  // (nr 0: up to the device's max_replica)
       TsIndex ix;
       ix.rng = c->crange;

@@ -15,7 +15,7 @@ for rep in 1 2; do
     envs=""; name=new
     if [[ $v == lib:* ]]; then envs="CRDTM_LIB=${v#lib:}"; name=$(echo ${v#lib:} | tr '/' '_');
     elif [[ $v == ab:* ]]; then envs="CRDTM_AB=${v#ab:}"; name=ab_${v#ab:};
-    elif [[ $v == env:* ]]; then envs="${v#env:}"; name=$(echo ${v#env:} | tr '=/' '__'); fi
+    elif [[ $v == env:* ]]; then envs="${v#env:}"; name=$(echo ${v#env:} | tr '=/ ' '___'); fi
     f=gpurun_out/${T}_${W}_${name}_$rep.log
     env $envs timeout -k 10 300 python -u bench.py --workload $W --cpu-sample 0 --pmc off --verbose > $f 2>&1 || { echo FAIL $v; tail -5 $f; exit 1; }
     echo "$name $rep $(grep -o '"ms_per_step": [0-9.]*' $f | head -1)"
