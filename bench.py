@@ -52,7 +52,9 @@ WORKLOADS = {
 }
 # CPU baseline samples (ops): config 2 and config 1 whole; the 10M-op batches as large a prefix as a bounded
 # run allows (their per-op CPU cost grows with the document, so a prefix flatters the CPU)
-CPU_SAMPLE = {"flat10m": 1_000_000, "deep10m": 1_000_000, "deep10m_il": 1_000_000, "trees": 2_000_000,
+# (about 10-30 s of CPU work each on the GPU box's host: `apply op` costs
+# grow with the document -- flat10m's 1M-op sample ran over 3 minutes)
+CPU_SAMPLE = {"flat10m": 200_000, "deep10m": 500_000, "deep10m_il": 500_000, "trees": 2_000_000,
               "cfg2": 1_000_000, "cfg1": 10_000}
 # 100k documents x 1k ops (80/20), 8 replicas, sharded by
 # document id; 12.5k documents per GPU (100k at 8 GPUs), weak scaling.
@@ -231,7 +233,7 @@ def roofline(workload, per_step, launches, B_alg, ms_step, steps_profiled, live=
             "dominant_kernel": kernels[0] if kernels else None, "top_kernels": kernels}
 
 
-def cpu_baseline(s, m, doc_off=None, workers=1, batch_cut=20_000):
+def cpu_baseline(s, m, doc_off=None, workers=1, batch_cut=20_000, chunk_cut=200_000):
     """CPU baseline: the Elm-compiled-to-JS cost model —
     oracle/crdtree.js (persistent red-black Dicts, cons Lists; test
     infrastructure) run by `node` on this host, ops pre-decoded, timed around
@@ -248,13 +250,21 @@ def cpu_baseline(s, m, doc_off=None, workers=1, batch_cut=20_000):
     with tempfile.TemporaryDirectory() as td:
         f = os.path.join(td, "batch.bin")
         jsoracle.write_batch(f, sub, m, doc_off=doc_off)
+        # (progress on stderr: a silent minute reads as a hang to the GPU runner)
+        print(f"[bench] cpu baseline: apply op over {m} ops", file=sys.stderr, flush=True)
         js = jsoracle.run(f, mode="op", workers=workers, timeout=900)
         out["js"] = js
         if doc_off is None and batch_cut:
+            print(f"[bench] cpu baseline: apply (Batch ops) over {min(batch_cut, m)} ops", file=sys.stderr, flush=True)
             out["js_batch"] = jsoracle.run(f, mode="batch", limit=min(batch_cut, m), timeout=900)
         if doc_off is None:  # SURVEY.md 8d mode (ii): apply over 10k-op Batch chunks
-            out["js_chunk"] = jsoracle.run(f, mode="chunk", chunk=10_000, timeout=900)
+            # (cut off at chunk_cut ops: ~9 s per 100k ops, each chunk's
+            # lastOperation accumulator being quadratic in the chunk)
+            print(f"[bench] cpu baseline: 10k-op Batch chunks over {min(chunk_cut, m)} ops", file=sys.stderr,
+                  flush=True)
+            out["js_chunk"] = jsoracle.run(f, mode="chunk", chunk=10_000, limit=min(chunk_cut, m), timeout=900)
     if doc_off is None:
+        print(f"[bench] cpu baseline: C++ restatement over {m} ops", file=sys.stderr, flush=True)
         L = olib()
         t = L.orc_init(0)
         err = C.c_int64(-1)
