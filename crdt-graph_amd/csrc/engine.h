@@ -242,7 +242,11 @@ int segmented_sort_asc_id(const uint32_t* seg_start, uint32_t n_seg, uint32_t* c
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, const uint32_t* n_dev, uint32_t n_max,
                      uint32_t bits, Arena& ws, hipStream_t st, uint32_t** out_k, uint32_t** out_v,
                      uint32_t* inv = nullptr);
-// the same for n <= RS_SMALL_MAX pairs in one workgroup (primitives.hip), into (kout, vout)
+// forest.hip: the flat documents of a forest (slot map + wave replay; fb[d] = 1
+// leaves document d to k_forest); vt holds FL_SLOTS (value, ts) pairs per document
+constexpr uint32_t FL_SLOTS = 1024;
+// the same for n <= RS_SMALL_MAX pairs in one workgroup (primitives.hip), into (kout, vout);
+// values below 2^16 (the wide kernel carries them as u16)
 constexpr uint32_t RS_SMALL_MAX = 16384;
 int radix_sort_small(const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t bits, uint32_t* kout,
                      uint32_t* vout, hipStream_t st);
@@ -283,6 +287,11 @@ constexpr int R_INCR = 1 << 20;
 int sync_read(crdtm_ctx* c);
 // replicas[replicaId t] := t over the applied ops (st) into `rep`; collected by take_replicas after a sync
 int replica_fold(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, Arena& ws, hipStream_t s);
+// forest.hip (FL_SLOTS above)
+int forest_flat_launch(const OpsDev& o, const uint32_t* doff, uint32_t n_docs, long long ts0, uint32_t* opw,
+                       uint16_t* sent, uint8_t* fb, longlong2* vt, int32_t* code, uint32_t* err, uint32_t* applied,
+                       unsigned long long* vhash, unsigned long long* vwords, long long* tstamp,
+                       uint32_t* overflow, hipStream_t s);
 int replica_fold_into(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, uint32_t* rlist,
                       hipStream_t s);
 int take_replicas(crdtm_tree* t, const long long* rep_dev);

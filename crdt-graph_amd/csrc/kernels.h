@@ -61,6 +61,16 @@ __device__ __forceinline__ void st_stream4(void* p, uchar4 v) {
 // replicaId ts = ts // 2^32 with Elm/JS (a / b) | 0 truncation (src/CRDTree/Timestamp.elm:16-18)
 __host__ __device__ __forceinline__ int64_t replica_of(int64_t ts) { return ts / TWO32; }
 
+// word-wise FNV-1a over 64-bit words (the canonical document hashes)
+struct Fnv {
+  unsigned long long h = 1469598103934665603ULL, n = 0;
+  __device__ void put(long long w) {
+    h ^= static_cast<unsigned long long>(w);
+    h *= 1099511628211ULL;
+    ++n;
+  }
+};
+
 // ---- ts -> first Add index (open addressing, linear probing). Keys are stored
 // XOR INT64_MIN so that an all-zero memset means "empty".
 struct TsHash {

@@ -5,6 +5,8 @@
 // sort and (4) Euler-tour list ranking. Everything is integer, HBM-bound work.
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 #include "engine.h"
 #include "listrank.h"
@@ -698,13 +700,117 @@ __global__ void __launch_bounds__(RS_SMALL_T) k_rs_small(const uint32_t* __restr
   }
 }
 
+// The same sort with 1024 threads x 16 items (four waves per SIMD to cover
+// the LDS latency, half the items per thread and pass) for values below
+// 2^16 (op indices of a batch of at most RS_SMALL_MAX): the values ride in
+// LDS as u16, so keys, values and the [16][1024] counts fit the 160 KB.
+constexpr uint32_t RS_W_T = 1024, RS_W_IPT = RS_SMALL_MAX / RS_W_T;
+static_assert(RS_W_IPT == 16, "one pad word per thread's 16 items");
+__device__ __forceinline__ uint32_t rs_wpad(uint32_t i) { return i + (i >> 4); }
+constexpr uint32_t RS_W_WORDS = RS_SMALL_MAX + RS_SMALL_MAX / 16;
+constexpr uint32_t RS_W_CNT = 16 * RS_W_T + 2 * (16 * RS_W_T / 64);
+constexpr size_t RS_W_LDS = RS_W_WORDS * sizeof(uint32_t) + RS_W_WORDS * sizeof(uint16_t) + RS_W_CNT * sizeof(uint16_t);
+static_assert(RS_W_LDS <= 160 * 1024, "fits the LDS");
+
+__global__ void __launch_bounds__(RS_W_T) k_rs_small_w(const uint32_t* __restrict__ kin,
+                                                       const uint32_t* __restrict__ vin, uint32_t n, uint32_t bits,
+                                                       uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
+  extern __shared__ uint32_t rs_small_lds[];
+  uint32_t* sk = rs_small_lds;
+  uint16_t* sv = reinterpret_cast<uint16_t*>(sk + RS_W_WORDS);
+  uint16_t* cnt = sv + RS_W_WORDS + (RS_W_WORDS & 1u);  // [digit][thread]
+  __shared__ uint32_t wsum[RS_W_T / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  {
+    uint32_t k0[RS_W_IPT], v0[RS_W_IPT];
+#pragma unroll
+    for (uint32_t j = 0; j < RS_W_IPT; ++j) {
+      const uint32_t i = t + j * RS_W_T;
+      k0[j] = i < n ? kin[i] : 0xFFFFFFFFu;  // padding: digit 15 in every pass, after every item
+      v0[j] = i < n ? vin[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < RS_W_IPT; ++j) {
+      sk[rs_wpad(t + j * RS_W_T)] = k0[j];
+      sv[rs_wpad(t + j * RS_W_T)] = static_cast<uint16_t>(v0[j]);
+    }
+  }
+  __syncthreads();
+  for (uint32_t shift = 0; shift < bits; shift += 4) {
+    uint32_t k[RS_W_IPT], v[RS_W_IPT];
+    unsigned long long c0 = 0, c1 = 0;  // 8-bit counters of digits 0-7 / 8-15
+#pragma unroll
+    for (uint32_t j = 0; j < RS_W_IPT; ++j) {
+      k[j] = sk[t * (RS_W_IPT + 1) + j];
+      v[j] = sv[t * (RS_W_IPT + 1) + j];
+      const uint32_t d = (k[j] >> shift) & 15u;
+      if (d < 8) c0 += 1ULL << (8 * d);
+      else c1 += 1ULL << (8 * (d - 8));
+    }
+#pragma unroll
+    for (uint32_t d = 0; d < 16; ++d)
+      cnt[rs_cpad(d * RS_W_T + t)] = static_cast<uint16_t>(((d < 8 ? c0 : c1) >> (8 * (d & 7))) & 0xFFu);
+    __syncthreads();
+    uint32_t loc[16], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      loc[j] = sum;
+      sum += cnt[rs_cpad(t * 16 + j)];
+    }
+    const uint32_t inc = wave_incl_scan(sum);
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t pre = inc - sum;
+    for (uint32_t w = 0; w < wv; ++w) pre += wsum[w];
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) cnt[rs_cpad(t * 16 + j)] = static_cast<uint16_t>(pre + loc[j]);
+    __syncthreads();
+    uint32_t q[RS_W_IPT];
+#pragma unroll
+    for (uint32_t j = 0; j < RS_W_IPT; ++j) q[j] = cnt[rs_cpad(((k[j] >> shift) & 15u) * RS_W_T + t)];
+    unsigned long long r0 = 0, r1 = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < RS_W_IPT; ++j) {
+      const uint32_t d = (k[j] >> shift) & 15u;
+      const uint32_t sh = 8 * (d & 7);
+      const uint32_t before = static_cast<uint32_t>(((d < 8 ? r0 : r1) >> sh) & 0xFFu);
+      if (d < 8) r0 += 1ULL << sh;
+      else r1 += 1ULL << sh;
+      q[j] = rs_wpad(q[j] + before);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < RS_W_IPT; ++j) {
+      sk[q[j]] = k[j];
+      sv[q[j]] = static_cast<uint16_t>(v[j]);
+    }
+    __syncthreads();
+  }
+  for (uint32_t i = t; i < n; i += RS_W_T) {
+    kout[i] = sk[rs_wpad(i)];
+    vout[i] = sv[rs_wpad(i)];
+  }
+}
+
 int radix_sort_small(const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t bits, uint32_t* kout,
                      uint32_t* vout, hipStream_t st) {
   static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_small),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  static_cast<int>(RS_SMALL_LDS)) == hipSuccess;
-  if (!lds_ok || n > RS_SMALL_MAX) return CRDTM_E_HIP;
-  if (n) LAUNCH(k_rs_small, dim3(1), dim3(RS_SMALL_T), RS_SMALL_LDS, st, kin, vin, n, bits, kout, vout);
+  static const bool w_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_small_w),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               static_cast<int>(RS_W_LDS)) == hipSuccess;
+  static const bool wide = [] {
+    const char* e = getenv("CRDTM_RS_SMALL");
+    return !(e && !strcmp(e, "512"));
+  }();
+  if (n > RS_SMALL_MAX) return CRDTM_E_HIP;
+  if (!n) return CRDTM_OK;
+  if (wide && w_ok) {  // (the caller's values are op indices of the batch: below n <= 2^14)
+    LAUNCH(k_rs_small_w, dim3(1), dim3(RS_W_T), RS_W_LDS, st, kin, vin, n, bits, kout, vout);
+    return CRDTM_OK;
+  }
+  if (!lds_ok) return CRDTM_E_HIP;
+  LAUNCH(k_rs_small, dim3(1), dim3(RS_SMALL_T), RS_SMALL_LDS, st, kin, vin, n, bits, kout, vout);
   return CRDTM_OK;
 }
 

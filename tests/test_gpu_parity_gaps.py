@@ -167,23 +167,41 @@ def test_forest_nested_and_long_documents():
         L.orc_free(t)
 
 
-@pytest.mark.parametrize("where", ["flat_path", "flat_ts", "nested_path", "flat_negative_path"])
+@pytest.mark.parametrize("where", ["flat_path", "flat_ts", "nested_path", "flat_negative_path", "nested_path_mid",
+                                   "nested_path_last", "nested_negative_last", "nested_failing_op"])
 def test_out_of_range_keys_rejected(where):
     """Elm Int runs on JS doubles: keys at or beyond 2^53 are outside the
     reference's exact range, so crdtm_apply refuses them with
-    CRDTM_E_RANGE (the flat claim checks its own path elements; the other
-    paths a pass of their own) and the tree stays the fresh tree it was."""
+    CRDTM_E_RANGE (the flat claim checks its own path elements, the level
+    kernels every element of every op's path -- the prefix and parent key in
+    k_lv_dict, the last key in k_lv_leaf, also for an op that already failed
+    -- and the other paths a pass of their own) and the tree stays the fresh
+    tree it was."""
     big = 1 << 53
-    s, n = long_path_stream(3, seed=5, interleaved=False) if where == "nested_path" else \
+    nested = where.startswith("nested")
+    s, n = long_path_stream(3, seed=5, interleaved=False) if nested else \
         (lambda v: (v, len(v["kind"])))(N.synth(n_ops=5000, replicas=8, window=16, seed=9))
     s = {k: v.copy() for k, v in s.items() if v is not None}
     j = n // 2
+    if nested:  # an op with a path of at least three keys
+        lens = np.diff(s["path_off"].astype(np.int64))
+        j = int(np.nonzero(lens >= 3)[0][len(np.nonzero(lens >= 3)[0]) // 2])
+    b, e = int(s["path_off"][j]), int(s["path_off"][j + 1])
     if where == "flat_ts":
         s["ts"][j] = big + 5
     elif where == "flat_negative_path":
-        s["path"][s["path_off"][j]] = -big
+        s["path"][b] = -big
+    elif where == "nested_path_mid":
+        s["path"][(b + e) // 2] = big
+    elif where == "nested_path_last":
+        s["path"][e - 1] = big + 1
+    elif where == "nested_negative_last":
+        s["path"][e - 1] = -big - 7
+    elif where == "nested_failing_op":  # its first key names no node: InvalidPath, its last key out of range
+        s["path"][b] = (77 << 32) + 12345
+        s["path"][e - 1] = big
     else:
-        s["path"][s["path_off"][j]] = big
+        s["path"][b] = big
     et = CRDTree.init(0)
     with pytest.raises(N.CrdtmError):
         et.apply_arrays(s, n)
