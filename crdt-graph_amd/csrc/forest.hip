@@ -4,11 +4,12 @@
 // exact sequential replay. The general documents take k_forest (merge.hip
 // forest_apply).
 //
-// Built with -structurizecfg-skip-uniform-regions (Makefile): the replay's
-// branches are all wave-uniform (scalar conditions from readfirstlane), and
-// the default structurizer turns them into flow blocks with exec-mask
-// bookkeeping the replay does not need (measured on the 12.5k config-5
-// documents: 2.61-2.64 ms per step with the flag against 2.77 without).
+// Like every kernel file, built with -structurizecfg-skip-uniform-regions
+// (Makefile): the replay's branches are all wave-uniform (scalar conditions
+// from readfirstlane), and the default structurizer turns them into flow
+// blocks with exec-mask bookkeeping the replay does not need (measured on the
+// 12.5k config-5 documents: 2.61-2.64 ms per step with the flag against 2.77
+// without).
 #include "engine.h"
 #include "kernels.h"
 
