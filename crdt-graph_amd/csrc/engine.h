@@ -245,6 +245,23 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, con
 // forest.hip: the flat documents of a forest (slot map + wave replay; fb[d] = 1
 // leaves document d to k_forest); vt holds FL_SLOTS (value, ts) pairs per document
 constexpr uint32_t FL_SLOTS = 1024;
+// Several fills in one launch (primitives.hip k_fill_batch): each region a
+// 4-byte aligned pointer, its byte count and a 32-bit pattern (a byte fill
+// passes the byte replicated), instead of one hipMemsetAsync per region.
+struct FillList {
+  static constexpr int MAX = 8;
+  void* p[MAX];
+  uint64_t bytes[MAX];
+  uint32_t pat[MAX];
+  int n = 0;
+  void add(void* q, uint64_t b, uint32_t v) {
+    p[n] = q;
+    bytes[n] = b;
+    pat[n] = v;
+    ++n;
+  }
+  int launch(hipStream_t s);  // (runs and clears the list; more than MAX regions: E_ARG)
+};
 // the same for n <= RS_SMALL_MAX pairs in one workgroup (primitives.hip), into (kout, vout);
 // values below 2^16 (the wide kernel carries them as u16)
 constexpr uint32_t RS_SMALL_MAX = 16384;

@@ -1335,13 +1335,15 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   uint32_t* poff = ws.alloc<uint32_t>(n + 2);
   uint32_t* ucnt = ws.alloc<uint32_t>(n + 1);
   uint32_t* lvcnt = ws.alloc<uint32_t>(2 * LV_N);  // groups per level, totals; then ops per level
-  HIP_CHECK(hipMemsetAsync(gk, 0, gsz * sizeof(unsigned long long), s));
-  HIP_CHECK(hipMemsetAsync(slot2grp, 0xFF, gsz * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(tk, 0, tsz * sizeof(unsigned long long), s));
-  HIP_CHECK(hipMemsetAsync(lvcnt, 0, 2 * LV_N * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(qn, 0, (n + 2) * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(pcap, 0, (n + 2) * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(nd), n, 1, s));
+  FillList fl;  // (one launch for the batch's cleared arrays)
+  fl.add(gk, gsz * sizeof(unsigned long long), 0u);
+  fl.add(slot2grp, gsz * sizeof(uint32_t), NONE);
+  fl.add(tk, tsz * sizeof(unsigned long long), 0u);
+  fl.add(lvcnt, 2 * LV_N * sizeof(uint32_t), 0u);
+  fl.add(qn, (n + 2) * sizeof(uint32_t), 0u);
+  fl.add(pcap, (n + 2) * sizeof(uint32_t), 0u);
+  fl.add(nd, sizeof(uint32_t), n);
+  if ((r = fl.launch(s))) return r;
   LAUNCH(k_ilr_group, dim3(grid_for(n)), dim3(BLOCK), 0, s, o, gk, gsz - 1, gbits, tk, tsz - 1, sk[0], sv[0], st, dr);
   uint32_t *ks = nullptr, *vs = nullptr;
   if ((r = radix_sort_pairs(sk[0], sv[0], sk[1], sv[1], nd, n, gbits + 7, ws, s, &ks, &vs))) return r;
@@ -1400,12 +1402,13 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   P.w1 = ws.alloc<uint4>(n + 1);
   P.w2 = ws.alloc<uint4>(n + 1);
   P.w3 = ws.alloc<uint2>(n + 1);
-  HIP_CHECK(hipMemsetAsync(ps, 0xFF, static_cast<size_t>(ptot) * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(undo, 0xFF, 3 * nu * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(marks, 0, 4 * (ILR_MAXL + 2) * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(J.head, 0xFF, (G + 1) * sizeof(uint32_t), s));
-  HIP_CHECK(hipMemsetAsync(J.gflag, 0, G + 4, s));
-  HIP_CHECK(hipMemsetAsync(empty, 0xFF, 16 * sizeof(uint32_t), s));
+  fl.add(ps, static_cast<size_t>(ptot) * sizeof(uint32_t), NONE);
+  fl.add(undo, 3 * nu * sizeof(uint32_t), NONE);
+  fl.add(marks, 4 * (ILR_MAXL + 2) * sizeof(uint32_t), 0u);
+  fl.add(J.head, (G + 1) * sizeof(uint32_t), NONE);
+  fl.add(J.gflag, G + 4, 0u);
+  fl.add(empty, 16 * sizeof(uint32_t), NONE);
+  if ((r = fl.launch(s))) return r;
   // ---- the levels ----
   IlrArgs a;
   a.T = t->d;

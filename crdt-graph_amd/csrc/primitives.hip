@@ -599,6 +599,50 @@ int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, con
   return CRDTM_OK;
 }
 
+struct FillArgs {
+  void* p[FillList::MAX];
+  uint64_t bytes[FillList::MAX];
+  uint32_t pat[FillList::MAX];
+};
+// region blockIdx.y: 16-byte stores over its aligned body, 4-byte stores
+// for the unaligned head words, bytes for the tail
+__global__ void __launch_bounds__(BLOCK) k_fill_batch(FillArgs a) {
+  const uint32_t j = blockIdx.y;
+  char* p = static_cast<char*>(a.p[j]);
+  const uint64_t nb = a.bytes[j];
+  const uint32_t v = a.pat[j];
+  const uint64_t head = ((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15) < nb
+                            ? ((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15) : (nb & ~3ULL);
+  const uint64_t n16 = (nb - head) / 16;
+  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x, ts = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  uint4* b16 = reinterpret_cast<uint4*>(p + head);
+  for (uint64_t i = t0; i < n16; i += ts) b16[i] = make_uint4(v, v, v, v);
+  if (t0 < head / 4) reinterpret_cast<uint32_t*>(p)[t0] = v;
+  const uint64_t done = head + 16 * n16;
+  if (t0 < nb - done) {  // (< 16 tail bytes)
+    const uint64_t q = done + t0;
+    p[q] = static_cast<char>(v >> (8 * (q & 3)));
+  }
+}
+
+int FillList::launch(hipStream_t s) {
+  if (n == 0) return CRDTM_OK;
+  if (n > MAX) return CRDTM_E_ARG;
+  FillArgs a;
+  uint64_t mx = 0;
+  for (int k = 0; k < n; ++k) {
+    if (reinterpret_cast<uintptr_t>(p[k]) & 3) return CRDTM_E_ARG;
+    a.p[k] = p[k];
+    a.bytes[k] = bytes[k];
+    a.pat[k] = pat[k];
+    mx = std::max(mx, bytes[k]);
+  }
+  const uint32_t gx = std::max<uint32_t>(1, std::min<uint64_t>(512, (mx / 16 + BLOCK - 1) / BLOCK));
+  LAUNCH(k_fill_batch, dim3(gx, static_cast<uint32_t>(n)), dim3(BLOCK), 0, s, a);
+  n = 0;
+  return CRDTM_OK;
+}
+
 // One-workgroup radix sort for small batches (n <= RS_SMALL_MAX): the pairs
 // stay in LDS for every pass (4-bit digits, 512 threads x 32 consecutive
 // items): per pass each thread counts its items' digits, one workgroup scan
