@@ -56,8 +56,14 @@ constexpr uint32_t FI_WIN_THREADS = 1024;
 
 // flags word bits (fi[0]); FI_OVER alone: no window takes a block's batch,
 // merge densely. fi[1] own-replica Adds, fi[2] gaps, fi[3] blocks landed in,
-// fi[4] overflowing blocks, fi[5] rebalance windows
-enum : uint32_t { FI_FAIL = 1u, FI_BUDGET = 2u, FI_OVER = 4u };
+// fi[4] overflowing blocks, fi[5] rebalance windows, fi[6] the commit gate
+// (k_fi_gate: FG_NONE = the general paths decide, nothing is written;
+// FG_SPARSE = the blocks the batch lands in are rewritten; FG_DENSE = the
+// batch's nodes and log are committed, the order is merged densely by the
+// host after the result read)
+enum : uint32_t { FI_FAIL = 1u, FI_BUDGET = 2u, FI_OVER = 4u, FI_REPLICA = 8u };
+enum : uint32_t { FG_NONE = 0u, FG_SPARSE = 1u, FG_DENSE = 2u };
+constexpr uint32_t FI_COMMIT_GRID = 1024;  // (grid-stride commit kernels: sized before the counts are known)
 constexpr uint32_t FI_WORDS = 8;
 
 KeyIndex::~KeyIndex() {
@@ -76,7 +82,8 @@ __global__ void __launch_bounds__(BLOCK) k_kx_build(const long long* s_key, uint
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_kx_insert(OpsDev o, uint32_t slot0, TsHash h) {
+__global__ void __launch_bounds__(BLOCK) k_kx_insert(OpsDev o, uint32_t slot0, TsHash h, const uint32_t* gate) {
+  if (gate && gate[6] == FG_NONE) return;  // (grid-uniform: incr.hip's commit gate)
   GRID_STRIDE(i, o.n) tshash_insert(h, o.ts[i], slot0 + i);
 }
 
@@ -154,10 +161,33 @@ __device__ __forceinline__ long long wave_min64(long long k) {
   return k;
 }
 
-// the batch key table and the flags words cleared (one launch)
-__global__ void __launch_bounds__(BLOCK) k_fi_clear(unsigned long long* keys, uint32_t cap, uint32_t* fi) {
-  GRID_STRIDE(q, cap) keys[q] = 0;
+// the batch key table, the statuses (not applied: a gated commit that does
+// not run leaves nothing for the replicas fold) and the flags words cleared
+// (one launch)
+__global__ void __launch_bounds__(BLOCK) k_fi_clear(unsigned long long* keys, uint32_t cap, uint32_t* fi, uint8_t* st,
+                                                    uint32_t m) {
+  GRID_STRIDE(q, cap) {
+    keys[q] = 0;
+    if (q < m) st[q] = ST_PENDING;
+  }
   if (blockIdx.x == 0 && threadIdx.x < FI_WORDS) fi[threadIdx.x] = 0;
+}
+
+// The commit gate, decided on the device so that the commit is queued
+// without a host round trip: the batch falls to the general paths when an
+// op does not take the closed form, a gap's walk ran out of budget, or the
+// own-replica Adds would carry the timestamp into the next replica id
+// (incrementTimestamp, src/CRDTree.elm:337-343); it merges densely when a
+// block overflows with no window to take it (or no LDS for the windows).
+// The flags words go to the result block, read back once at the end.
+__global__ void k_fi_gate(uint32_t* fi, long long ts0, uint32_t win_lds, DevResult* dres) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t f = fi[0];
+  if (replica_of(ts0 + fi[1]) != replica_of(ts0)) f |= FI_REPLICA;
+  if (fi[5] && !win_lds) f |= FI_OVER;
+  fi[0] = f;
+  fi[6] = (f & (FI_FAIL | FI_BUDGET | FI_REPLICA)) ? FG_NONE : (f & FI_OVER) ? FG_DENSE : FG_SPARSE;
+  for (uint32_t k = 0; k < FI_WORDS; ++k) dres->fincr[k] = fi[k];
 }
 
 // batch keys -> op index; a key seen twice fails the batch
@@ -475,17 +505,13 @@ __global__ void __launch_bounds__(BLOCK) k_fi_win_list(const uint32_t* ovl, uint
 // + its order in its gap. Moved and new entries get their position in
 // rank_of, the new nodes their next links (and the entry before each gap
 // its new first); the block's minima are recomputed.
-__global__ void __launch_bounds__(FI_CAP) k_fi_rewrite(uint32_t nbk, const uint32_t* tl, const uint32_t* fi,
-                                                       const uint32_t* sk, const uint32_t* sv, const uint32_t* ord,
-                                                       const uint32_t* first, const uint32_t* gpred, uint32_t slot0,
-                                                       const long long* ts, uint32_t* bent, long long* bdk,
-                                                       uint32_t* bcnt, uint32_t* bfirst, uint32_t* bend,
-                                                       const uint32_t* bwin, long long* bmin, uint32_t* rank_of,
-                                                       uint32_t* s_next) {
-  __shared__ uint32_t se[FI_CAP];
-  __shared__ long long sd[FI_CAP];
-  if (blockIdx.x >= fi[3]) return;  // (workgroup-uniform)
-  const uint32_t Kp = nbk * FI_CAP, k = tl[blockIdx.x], j = threadIdx.x;
+__device__ __forceinline__ void fi_rewrite_one(uint32_t nbk, uint32_t k, const uint32_t* sk, const uint32_t* sv,
+                                               const uint32_t* ord, const uint32_t* first, const uint32_t* gpred,
+                                               uint32_t slot0, const long long* ts, uint32_t* bent, long long* bdk,
+                                               uint32_t* bcnt, uint32_t* bfirst, uint32_t* bend, const uint32_t* bwin,
+                                               long long* bmin, uint32_t* rank_of, uint32_t* s_next, uint32_t* se,
+                                               long long* sd) {
+  const uint32_t Kp = nbk * FI_CAP, j = threadIdx.x;
   const uint32_t b = fi_blk(sk[k], Kp), base = b * FI_CAP;
   if (bwin[b]) return;  // a window rebalances it
   const uint32_t e = bend[b], cnt = bcnt[b];
@@ -535,6 +561,23 @@ __global__ void __launch_bounds__(FI_CAP) k_fi_rewrite(uint32_t nbk, const uint3
   }
 }
 
+__global__ void __launch_bounds__(FI_CAP) k_fi_rewrite(uint32_t nbk, const uint32_t* tl, const uint32_t* fi,
+                                                       const uint32_t* sk, const uint32_t* sv, const uint32_t* ord,
+                                                       const uint32_t* first, const uint32_t* gpred, uint32_t slot0,
+                                                       const long long* ts, uint32_t* bent, long long* bdk,
+                                                       uint32_t* bcnt, uint32_t* bfirst, uint32_t* bend,
+                                                       const uint32_t* bwin, long long* bmin, uint32_t* rank_of,
+                                                       uint32_t* s_next) {
+  __shared__ uint32_t se[FI_CAP];
+  __shared__ long long sd[FI_CAP];
+  if (fi[6] != FG_SPARSE) return;  // (grid-uniform: the gate)
+  for (uint32_t wb = blockIdx.x; wb < fi[3]; wb += gridDim.x) {  // (workgroup-uniform)
+    fi_rewrite_one(nbk, tl[wb], sk, sv, ord, first, gpred, slot0, ts, bent, bdk, bcnt, bfirst, bend, bwin, bmin,
+                   rank_of, s_next, se, sd);
+    __syncthreads();  // (the next block reuses the LDS)
+  }
+}
+
 // One workgroup per rebalance window [w0, w0 + ne): every block's merged
 // content (as in k_fi_rewrite) staged in LDS in window order, then spread
 // evenly over the window's blocks (each keeps >= 1 entry: every block had
@@ -551,8 +594,9 @@ __global__ void __launch_bounds__(FI_WIN_THREADS) k_fi_win(uint32_t nbk, const u
   long long* sd = reinterpret_cast<long long*>(fi_win_lds);     // [FI_WIN_ENT]
   uint32_t* se = reinterpret_cast<uint32_t*>(sd + FI_WIN_ENT);  // [FI_WIN_ENT]
   __shared__ uint32_t vp[(1u << FI_WIN_MAX) + 1];  // window-order start of each block's content
-  if (blockIdx.x >= fi[5]) return;  // (workgroup-uniform)
-  const uint32_t Kp = nbk * FI_CAP, w0 = wl[blockIdx.x], L = wlev[blockIdx.x];
+  if (fi[6] != FG_SPARSE) return;  // (grid-uniform: the gate)
+  for (uint32_t wi = blockIdx.x; wi < fi[5]; wi += gridDim.x) {  // (workgroup-uniform)
+  const uint32_t Kp = nbk * FI_CAP, w0 = wl[wi], L = wlev[wi];
   const uint32_t ne = min(1u << (L - 1), nbk - w0);
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = FI_WIN_THREADS / 64;
   if (tid < 64) {
@@ -624,6 +668,8 @@ __global__ void __launch_bounds__(FI_WIN_THREADS) k_fi_win(uint32_t nbk, const u
     bend[w0 + i] = 0;
     bwin[w0 + i] = 0;
   }
+  __syncthreads();  // (the next window reuses the LDS)
+  }
 }
 
 // superblock minima over the rewritten blocks' superblocks (one wave each;
@@ -635,18 +681,21 @@ __device__ __forceinline__ void fi_sup_one(uint32_t sp, uint32_t nb, const long 
 }
 __global__ void __launch_bounds__(BLOCK) k_fi_sup_fix(uint32_t Kp, const uint32_t* tl, const uint32_t* fi,
                                                       const uint32_t* sk, const long long* bmin, long long* smin) {
-  const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64;
-  if (w >= fi[3]) return;  // (wave-uniform)
-  fi_sup_one(FI_BPB * fi_blk(sk[tl[w]], Kp) / FI_SUP, Kp / FI_BLK, bmin, smin);
+  if (fi[6] != FG_SPARSE) return;  // (grid-uniform: the gate)
+  const uint32_t nw = gridDim.x * blockDim.x / 64;
+  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64; w < fi[3]; w += nw)  // (wave-uniform)
+    fi_sup_one(FI_BPB * fi_blk(sk[tl[w]], Kp) / FI_SUP, Kp / FI_BLK, bmin, smin);
 }
 // ... and over every superblock a window's blocks touch (one wave per window)
 __global__ void __launch_bounds__(BLOCK) k_fi_sup_win(uint32_t nbk, const uint32_t* wl, const uint32_t* fi,
                                                       const uint32_t* wlev, const long long* bmin, long long* smin) {
-  const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64;
-  if (w >= fi[5]) return;  // (wave-uniform)
-  const uint32_t w0 = wl[w], ne = min(1u << (wlev[w] - 1), nbk - w0);
-  for (uint32_t sp = FI_BPB * w0 / FI_SUP; sp <= (FI_BPB * (w0 + ne) - 1) / FI_SUP; ++sp)
-    fi_sup_one(sp, FI_BPB * nbk, bmin, smin);
+  if (fi[6] != FG_SPARSE) return;  // (grid-uniform: the gate)
+  const uint32_t nw = gridDim.x * blockDim.x / 64;
+  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64; w < fi[5]; w += nw) {  // (wave-uniform)
+    const uint32_t w0 = wl[w], ne = min(1u << (wlev[w] - 1), nbk - w0);
+    for (uint32_t sp = FI_BPB * w0 / FI_SUP; sp <= (FI_BPB * (w0 + ne) - 1) / FI_SUP; ++sp)
+      fi_sup_one(sp, FI_BPB * nbk, bmin, smin);
+  }
 }
 
 // the dense order from the gapped one (off = exclusive scan of bcnt)
@@ -846,7 +895,8 @@ __global__ void __launch_bounds__(BLOCK) k_fi_next(uint32_t K, uint32_t m, const
 
 // node records of the new slots and the log append (every op applied, |path| = 1)
 __global__ void __launch_bounds__(BLOCK) k_fi_commit(OpsDev o, uint32_t slot0, uint32_t log0, uint32_t lpath0,
-                                                     TreeDev T, uint8_t* st, uint8_t* st_out) {
+                                                     TreeDev T, uint8_t* st, uint8_t* st_out, const uint32_t* fi) {
+  if (fi[6] == FG_NONE) return;  // (grid-uniform: the gate)
   GRID_STRIDE(i, o.n) {
     const uint32_t sl = slot0 + i;
     st[i] = ST_APPLIED;
@@ -1016,7 +1066,7 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   const TsHash kx{X.keys, X.vals, X.mask};
   uint32_t* rank_of = X.rank;
   // ---- phase A: anchors, validity ----
-  LAUNCH(k_fi_clear, dim3(grid_for(bcap)), dim3(BLOCK), 0, s, bh.keys, bcap, fi);
+  LAUNCH(k_fi_clear, dim3(grid_for(bcap)), dim3(BLOCK), 0, s, bh.keys, bcap, fi, st, m);
   LAUNCH(k_fi_bidx, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, bh, fi);
   LAUNCH(k_fi_resolve, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, kx, bh, rank_of, replica_of(t->timestamp), par[0],
          par0, sta[0], thr[0], fi);
@@ -1047,26 +1097,13 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   LAUNCH(k_fi_win_pick, dim3(grid_for(64ULL * m)), dim3(BLOCK), 0, s, nbk, sk, tl, X.bcnt, X.bfirst, X.bend, X.bwin,
          ovl, fi);
   LAUNCH(k_fi_win_list, dim3(grid_for(m)), dim3(BLOCK), 0, s, ovl, fi, X.bwin, wl, wlev);
-  uint32_t hf[FI_WORDS];
-  HIP_CHECK(hipMemcpyAsync(hf, fi, sizeof(hf), hipMemcpyDeviceToHost, s));
-  if (int rw = stream_wait(s)) return rw;
-  const long long new_ts = t->timestamp + hf[1];
-  // (resolved before phase C: nothing may fail once the commit is queued)
+  // (resolved before the commit is queued: nothing may fail once it is)
   static const bool win_lds = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fi_win),
                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                                   FI_WIN_ENT * 12) == hipSuccess;
-  if (hf[5] && !win_lds) hf[0] |= FI_OVER;  // (no LDS for the windows: the dense merge takes the batch)
-  if ((hf[0] & (FI_FAIL | FI_BUDGET)) || replica_of(new_ts) != replica_of(t->timestamp)) {
-    // the general paths decide: the state is untouched, the key index stays
-    // valid; the blocks' per-batch marks are not cleared, so they are rebuilt
-    // when next used
-    if (t->doc_gapped && (r = fi_compact_doc(t, ws, s))) return r;
-    X.ord_ready = false;
-    ws.used = mark0;
-    return CRDTM_OK;
-  }
-  const bool dense = hf[0] & FI_OVER;
-  // ---- phase C: commit ----
+  LAUNCH(k_fi_gate, dim3(1), dim3(64), 0, s, fi, static_cast<long long>(t->timestamp), win_lds ? 1u : 0u, c->dres);
+  // ---- phase C: the commit, queued at once and gated on the device
+  // (k_fi_gate): one host round trip per batch, at its end ----
   TreeCaps need = t->cap;
   need.slots = std::max<uint64_t>(need.slots, t->n_slots + m + 1);
   need.log = std::max<uint64_t>(need.log, t->log_n + m + 1);
@@ -1076,16 +1113,35 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
     if ((r = grow_tree(t, need))) return r;
   const uint32_t slot0 = static_cast<uint32_t>(t->n_slots);
   LAUNCH(k_fi_commit, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, slot0, static_cast<uint32_t>(t->log_n),
-         static_cast<uint32_t>(t->log_npath), t->d, st, st_out);
-  if (!dense) {  // O(batch): the blocks the batch lands in
-    LAUNCH(k_fi_rewrite, dim3(hf[3]), dim3(FI_CAP), 0, s, nbk, tl, fi, sk, sv, ord, first, gpred, slot0, o.ts, X.bent,
-           X.bdk, X.bcnt, X.bfirst, X.bend, X.bwin, X.bmin, rank_of, t->d.s_next);
-    if (hf[5])
-      LAUNCH(k_fi_win, dim3(hf[5]), dim3(FI_WIN_THREADS), FI_WIN_ENT * 12, s, nbk, wl, wlev, fi, sk, sv, ord, first,
-             gpred, slot0, o.ts, X.bent, X.bdk, X.bcnt, X.bfirst, X.bend, X.bwin, X.bmin, rank_of, t->d.s_next);
-    LAUNCH(k_fi_sup_fix, dim3(grid_for(64ULL * hf[3])), dim3(BLOCK), 0, s, Kp, tl, fi, sk, X.bmin, X.smin);
-    if (hf[5])
-      LAUNCH(k_fi_sup_win, dim3(grid_for(64ULL * hf[5])), dim3(BLOCK), 0, s, nbk, wl, fi, wlev, X.bmin, X.smin);
+         static_cast<uint32_t>(t->log_npath), t->d, st, st_out, fi);
+  // O(batch): the blocks the batch lands in (grid-stride over the device's
+  // counts; blocks and windows are at most one per op)
+  const uint32_t cg = std::min<uint32_t>(FI_COMMIT_GRID, std::min<uint32_t>(m, nbk));
+  const uint32_t wg = std::min<uint32_t>(256u, cg);
+  LAUNCH(k_fi_rewrite, dim3(cg), dim3(FI_CAP), 0, s, nbk, tl, fi, sk, sv, ord, first, gpred, slot0, o.ts, X.bent,
+         X.bdk, X.bcnt, X.bfirst, X.bend, X.bwin, X.bmin, rank_of, t->d.s_next);
+  if (win_lds)
+    LAUNCH(k_fi_win, dim3(wg), dim3(FI_WIN_THREADS), FI_WIN_ENT * 12, s, nbk, wl, wlev, fi, sk, sv, ord, first, gpred,
+           slot0, o.ts, X.bent, X.bdk, X.bcnt, X.bfirst, X.bend, X.bwin, X.bmin, rank_of, t->d.s_next);
+  LAUNCH(k_fi_sup_fix, dim3(grid_for(64ULL * cg)), dim3(BLOCK), 0, s, Kp, tl, fi, sk, X.bmin, X.smin);
+  if (win_lds) LAUNCH(k_fi_sup_win, dim3(grid_for(64ULL * wg)), dim3(BLOCK), 0, s, nbk, wl, fi, wlev, X.bmin, X.smin);
+  LAUNCH(k_kx_insert, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, slot0, kx, fi);
+  if ((r = replica_fold(c, o, st, rep, ws, s))) return r;  // (statuses not applied fold nothing)
+  if ((r = sync_read(c))) return r;
+  uint32_t hf[FI_WORDS];
+  std::memcpy(hf, c->hres->fincr, sizeof(hf));
+  if (hf[6] == FG_NONE) {
+    // the general paths decide: the state is untouched (every commit kernel
+    // read the gate), the key index stays valid; the blocks' per-batch marks
+    // are not cleared, so they are rebuilt when next used
+    if (t->doc_gapped && (r = fi_compact_doc(t, ws, s))) return r;
+    X.ord_ready = false;
+    ws.used = mark0;
+    return CRDTM_OK;
+  }
+  const long long new_ts = t->timestamp + hf[1];
+  const bool dense = hf[6] == FG_DENSE;
+  if (!dense) {
     t->doc_gapped = true;
   } else {  // a block overflows: merge densely, then rebuild the blocks
     if ((r = fi_compact_doc(t, ws, s))) return r;
@@ -1109,9 +1165,6 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
     if ((r = fi_build(t, K + m, s))) return r;
     t->doc_gapped = false;
   }
-  LAUNCH(k_kx_insert, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, slot0, kx);
-  if ((r = replica_fold(c, o, st, rep, ws, s))) return r;
-  if ((r = sync_read(c))) return r;
   if ((r = take_replicas(t, rep))) return r;
   t->n_slots += m;
   t->doc_n += m;
