@@ -173,7 +173,7 @@ def roofline(workload, per_step, launches, B_alg, ms_step, steps_profiled, live=
     pmc, src = pmc_table(workload)
 
     def kbytes(nm, key="hbm_bytes"):
-        base = nm.split("<")[0]
+        base = nm.strip("()").split("<")[0]
         # labelled scan phases (k_dscan_runs, k_dscan_xs, ...) are instances of
         # k_dscan, whose PMC entry is the dispatch-weighted mean over all of
         # them: summed over the step's dispatches it gives their exact total
@@ -188,7 +188,7 @@ def roofline(workload, per_step, launches, B_alg, ms_step, steps_profiled, live=
         # measured in this run: [raw F + W, corrected 2F + W] per step (MI355X_MICROARCH.md: FETCH_SIZE
         # counts half the bytes of coalesced reads on gfx950; exact for streams, an upper bound for gathers)
         def step_bytes(nm, corrected=True):
-            base = nm.split("<")[0]
+            base = nm.strip("()").split("<")[0]
             if base.startswith("k_dscan"):
                 return None  # (labelled scan phases share k_dscan's entry: reported in the total only)
             e = live.get(base)
@@ -198,7 +198,8 @@ def roofline(workload, per_step, launches, B_alg, ms_step, steps_profiled, live=
         src = "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over one step of this workload (bench.py --pmc-child)"
         covered = True
         # the time share of the kernels whose counters the passes saw
-        seen = sum(t for nm, t in per_step.items() if nm.split("<")[0] in live or nm.startswith("k_dscan"))
+        seen = sum(t for nm, t in per_step.items()
+                   if nm.strip("()").split("<")[0] in live or nm.startswith("k_dscan"))
     else:
         def step_bytes(nm, corrected=True):
             b = kbytes(nm, "hbm_bytes" if corrected else "hbm_bytes_raw")

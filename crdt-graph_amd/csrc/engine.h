@@ -159,6 +159,7 @@ struct KeyIndex {
   uint32_t* bwin = nullptr;  // [nbk] level + 1 of the rebalance window over the block (0 between batches)
   long long* bmin = nullptr; // [nbk FI_CAP / 64] smallest key per 64 positions
   long long* smin = nullptr; // smallest key per 4096 positions
+  long long* tmin = nullptr; // smallest key per 64 superblocks (262,144 positions)
   uint64_t bcap = 0;         // blocks the arrays hold
   uint32_t nbk = 0;          // blocks in use
   uint32_t* rank = nullptr;  // slot -> position

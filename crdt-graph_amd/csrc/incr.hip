@@ -70,7 +70,8 @@ KeyIndex::~KeyIndex() {
   for (void* q : {static_cast<void*>(keys), static_cast<void*>(vals), static_cast<void*>(bent),
                   static_cast<void*>(bdk), static_cast<void*>(bcnt), static_cast<void*>(bend),
                   static_cast<void*>(bfirst), static_cast<void*>(bwin), static_cast<void*>(bmin),
-                  static_cast<void*>(smin), static_cast<void*>(rank), static_cast<void*>(doc2)})
+                  static_cast<void*>(smin), static_cast<void*>(tmin), static_cast<void*>(rank),
+                  static_cast<void*>(doc2)})
     if (q) hipFree(q);
 }
 
@@ -137,6 +138,19 @@ __global__ void __launch_bounds__(BLOCK) k_fi_bmin(uint32_t K, const long long* 
     }
     const uint32_t b = w * 4 + lane / 16;
     if ((lane & 15) == 0 && b < nb) bmin[b] = k;
+  }
+}
+
+// the top level: the smallest key per FI_SUP superblocks (262,144 positions),
+// so a search that runs far (a small threshold) crosses the document in a
+// few steps instead of one superblock row of 64 per step
+__global__ void __launch_bounds__(BLOCK) k_fi_top(uint32_t ns, const long long* smin, long long* tmin) {
+  const uint32_t nt = (ns + FI_SUP - 1) / FI_SUP;
+  GRID_STRIDE(t, nt) {
+    long long m = FI_INF;
+    const uint32_t e = min(ns, (t + 1) * FI_SUP);
+    for (uint32_t q = t * FI_SUP; q < e; ++q) m = min(m, smin[q]);
+    tmin[t] = m;
   }
 }
 
@@ -376,10 +390,10 @@ __global__ void __launch_bounds__(FI_JUMP_THREADS) k_fi_jump_lds(uint32_t m, uin
 // g = NSR(start, thr) over the base keys, one wave per query: 64 keys, 64
 // block minima or 64 superblock minima per step (ballot), then down again
 __global__ void __launch_bounds__(BLOCK) k_fi_gap(uint32_t m, uint32_t K, const long long* dk, const long long* bmin,
-                                                  const long long* smin, const uint32_t* start, const long long* thr,
-                                                  uint32_t* gkey, uint32_t* gval) {
+                                                  const long long* smin, const long long* tmin, const uint32_t* start,
+                                                  const long long* thr, uint32_t* gkey, uint32_t* gval) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t nb = (K + FI_BLK - 1) / FI_BLK, ns = (nb + FI_SUP - 1) / FI_SUP;
+  const uint32_t nb = (K + FI_BLK - 1) / FI_BLK, ns = (nb + FI_SUP - 1) / FI_SUP, nt = (ns + FI_SUP - 1) / FI_SUP;
   const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / 64;
   if (i >= m) return;  // (wave-uniform)
   const long long t = thr[i];
@@ -397,8 +411,15 @@ __global__ void __launch_bounds__(BLOCK) k_fi_gap(uint32_t m, uint32_t K, const 
     if (q == NONE && b + 1 < nb) {
       const uint32_t s0 = (b + 1) / FI_SUP;
       uint32_t bb = first64(bmin, s0 * FI_SUP, b + 1, nb);
-      for (uint32_t ss = s0 + 1; bb == NONE && ss < ns; ss += 64) {
-        const uint32_t sq = first64(smin, ss, ss, ns);
+      if (bb == NONE && s0 + 1 < ns) {
+        // the rest of the top entry that holds superblock s0 + 1, then the
+        // top level 64 entries per step, then down one superblock row
+        const uint32_t t0 = (s0 + 1) / FI_SUP;
+        uint32_t sq = first64(smin, t0 * FI_SUP, s0 + 1, ns);
+        for (uint32_t tt = t0 + 1; sq == NONE && tt < nt; tt += 64) {
+          const uint32_t tq = first64(tmin, tt, tt, nt);
+          if (tq != NONE) sq = first64(smin, tq * FI_SUP, tq * FI_SUP, ns);
+        }
         if (sq != NONE) bb = first64(bmin, sq * FI_SUP, sq * FI_SUP, nb);
       }
       if (bb != NONE) q = first64(dk, bb * FI_BLK, bb * FI_BLK, K);
@@ -698,6 +719,30 @@ __global__ void __launch_bounds__(BLOCK) k_fi_sup_win(uint32_t nbk, const uint32
   }
 }
 
+// ... then the top entries over every superblock the blocks and windows
+// touched (one wave per block or window; after k_fi_sup_fix / k_fi_sup_win)
+__device__ __forceinline__ void fi_top_one(uint32_t tp, uint32_t ns, const long long* smin, long long* tmin) {
+  const uint32_t lane = threadIdx.x & 63, q = tp * FI_SUP + lane;
+  const long long v = wave_min64(q < ns ? smin[q] : FI_INF);
+  if (lane == 0) tmin[tp] = v;
+}
+__global__ void __launch_bounds__(BLOCK) k_fi_top_fix(uint32_t nbk, const uint32_t* tl, const uint32_t* sk,
+                                                      const uint32_t* wl, const uint32_t* wlev, const uint32_t* fi,
+                                                      const long long* smin, long long* tmin) {
+  if (fi[6] != FG_SPARSE) return;  // (grid-uniform: the gate)
+  const uint32_t Kp = nbk * FI_CAP, ns = (FI_BPB * nbk + FI_SUP - 1) / FI_SUP;
+  const uint32_t nw = gridDim.x * blockDim.x / 64, nblk = fi[3], nwin = fi[5];
+  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64; w < nblk + nwin; w += nw) {  // (wave-uniform)
+    if (w < nblk) {
+      fi_top_one(FI_BPB * fi_blk(sk[tl[w]], Kp) / FI_SUP / FI_SUP, ns, smin, tmin);
+    } else {
+      const uint32_t w0 = wl[w - nblk], ne = min(1u << (wlev[w - nblk] - 1), nbk - w0);
+      for (uint32_t tp = FI_BPB * w0 / FI_SUP / FI_SUP; tp <= (FI_BPB * (w0 + ne) - 1) / FI_SUP / FI_SUP; ++tp)
+        fi_top_one(tp, ns, smin, tmin);
+    }
+  }
+}
+
 // the dense order from the gapped one (off = exclusive scan of bcnt)
 __global__ void __launch_bounds__(BLOCK) k_fi_compact(uint32_t nbk, const uint32_t* off, const uint32_t* bent,
                                                       const uint32_t* bcnt, uint32_t* doc) {
@@ -955,7 +1000,7 @@ static int fi_build(crdtm_tree* t, uint32_t K, hipStream_t s) {
   if (X.bcap < nbk) {
     for (void* q : {static_cast<void*>(X.bent), static_cast<void*>(X.bdk), static_cast<void*>(X.bcnt),
                     static_cast<void*>(X.bend), static_cast<void*>(X.bfirst), static_cast<void*>(X.bwin),
-                    static_cast<void*>(X.bmin), static_cast<void*>(X.smin)})
+                    static_cast<void*>(X.bmin), static_cast<void*>(X.smin), static_cast<void*>(X.tmin)})
       if (q) hipFree(q);
     const uint64_t bc = 2ULL * nbk + 64;
     HIP_CHECK(hipMalloc(&X.bent, bc * FI_CAP * sizeof(uint32_t)));
@@ -966,6 +1011,7 @@ static int fi_build(crdtm_tree* t, uint32_t K, hipStream_t s) {
     HIP_CHECK(hipMalloc(&X.bwin, bc * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&X.bmin, FI_BPB * bc * sizeof(long long)));
     HIP_CHECK(hipMalloc(&X.smin, (FI_BPB * bc / FI_SUP + 1) * sizeof(long long)));
+    HIP_CHECK(hipMalloc(&X.tmin, ((FI_BPB * bc / FI_SUP + 1) / FI_SUP + 2) * sizeof(long long)));
     X.bcap = bc;
   }
   X.nbk = nbk;
@@ -975,6 +1021,8 @@ static int fi_build(crdtm_tree* t, uint32_t K, hipStream_t s) {
   LAUNCH(k_fi_bmin, dim3(grid_for(static_cast<uint64_t>(Kp / FI_BLK + 3) / 4 * 64)), dim3(BLOCK), 0, s, Kp, X.bdk,
          X.bmin);
   LAUNCH(k_fi_sup, dim3(grid_for(FI_BPB * nbk / FI_SUP + 1)), dim3(BLOCK), 0, s, FI_BPB * nbk, X.bmin, X.smin);
+  LAUNCH(k_fi_top, dim3(grid_for(FI_BPB * nbk / FI_SUP / FI_SUP + 1)), dim3(BLOCK), 0, s,
+         (FI_BPB * nbk + FI_SUP - 1) / FI_SUP, X.smin, X.tmin);
   X.ord_ready = true;
   return CRDTM_OK;
 }
@@ -1082,8 +1130,11 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
            thr[0]);
   else if (rounds)
     LAUNCH(k_fi_jump, dim3(1), dim3(FI_JUMP_THREADS), 0, s, m, rounds, par[0], sta[0], thr[0], o.ts);
-  LAUNCH(k_fi_gap, dim3(grid_for(64ULL * m)), dim3(BLOCK), 0, s, m, Kp, X.bdk, X.bmin, X.smin, sta[0], thr[0], gk[0],
-         gv[0]);
+  // (measured and reverted in round 5: four queries per wave, 16 lanes
+  // each -- 0.65 ms more per 100 batches: a query's long search held up the
+  // wave's other three)
+  LAUNCH(k_fi_gap, dim3(grid_for(64ULL * m)), dim3(BLOCK), 0, s, m, Kp, X.bdk, X.bmin, X.smin, X.tmin, sta[0],
+         thr[0], gk[0], gv[0]);
   uint32_t bits = 4;  // (gap positions run to Kp inclusive)
   while (bits < 32 && (static_cast<uint64_t>(Kp) >> bits) != 0) bits += 4;
   uint32_t *sk = gk[1], *sv = gv[1];
@@ -1125,6 +1176,7 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
            slot0, o.ts, X.bent, X.bdk, X.bcnt, X.bfirst, X.bend, X.bwin, X.bmin, rank_of, t->d.s_next);
   LAUNCH(k_fi_sup_fix, dim3(grid_for(64ULL * cg)), dim3(BLOCK), 0, s, Kp, tl, fi, sk, X.bmin, X.smin);
   if (win_lds) LAUNCH(k_fi_sup_win, dim3(grid_for(64ULL * wg)), dim3(BLOCK), 0, s, nbk, wl, fi, wlev, X.bmin, X.smin);
+  LAUNCH(k_fi_top_fix, dim3(grid_for(64ULL * cg)), dim3(BLOCK), 0, s, nbk, tl, sk, wl, wlev, fi, X.smin, X.tmin);
   LAUNCH(k_kx_insert, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, slot0, kx, fi);
   if ((r = replica_fold(c, o, st, rep, ws, s))) return r;  // (statuses not applied fold nothing)
   if ((r = sync_read(c))) return r;

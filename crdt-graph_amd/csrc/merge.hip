@@ -108,6 +108,13 @@ __device__ __forceinline__ void store_quad_u8(uint8_t* p, uint32_t i0, uint32_t 
        j_ * cq_ < nq_; j_ += xs_, qd_ = j_ * cq_ + xy_ * blockDim.x + threadIdx.x, i0 = 4 * qd_)   \
     if (qd_ < nq_)
 
+// A grid cap from the environment (A/B runs), else `def`.
+static uint32_t env_grid(const char* name, uint32_t def) {
+  const char* e = getenv(name);
+  const int g = e ? atoi(e) : 0;
+  return g >= 8 && g <= (1 << 20) ? static_cast<uint32_t>(g) : def;
+}
+
 inline uint32_t quad_grid(uint64_t n) {
   const uint64_t g = (((n + 3) / 4) + BLOCK - 1) / BLOCK;
   if (g >= 2048) return 2048;
@@ -3278,23 +3285,38 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
       LAUNCH(k_fl_present, dim3(gq), dim3(BLOCK), 0, s, Q, fr, qc);
       if ((r = scan_excl_u32(qc, qc, Q, nullptr, ws, s))) return r;
     }
-    const uint32_t gw = std::max<uint32_t>(1, std::min<uint32_t>(2048, (NW + RM_MASK_UNROLL * (BLOCK / 64) - 1) /
-                                                                           (RM_MASK_UNROLL * (BLOCK / 64))));
+    // (A/B: CRDTM_MASK_U = words per wave and iteration, 1 / 2 / 4;
+    // CRDTM_MASK_GRID = the workgroup cap)
+    static const uint32_t mask_u = [] {
+      const char* e = getenv("CRDTM_MASK_U");
+      const uint32_t u = e ? static_cast<uint32_t>(atoi(e)) : RM_MASK_UNROLL;
+      return (u == 1 || u == 4) ? u : RM_MASK_UNROLL;
+    }();
+    // (1,024 workgroups: 0.689 -> 0.659 ms per flat10m step against 2,048;
+    // 512: 0.70)
+    static const uint32_t mask_grid = env_grid("CRDTM_MASK_GRID", 1024);
+    const uint32_t gw = std::max<uint32_t>(1, std::min<uint32_t>(mask_grid, (NW + mask_u * (BLOCK / 64) - 1) /
+                                                                                 (mask_u * (BLOCK / 64))));
     const size_t mshm = maxr + 1 <= HOST_RANGES ? 3 * (maxr + 1) * sizeof(uint32_t) : 0;
     static const bool mask_devq = [] {  // (A/B: the device-range instance on every merge)
       const char* e = getenv("CRDTM_MASK_DEVQ");
       return e && e[0] == '1';
     }();
-    if (fr.qd || mask_devq)
-      LAUNCH((k_run_mask<RM_MASK_UNROLL, true>), dim3(gw), dim3(BLOCK), mshm, s, fr, Q, hm, hc, t->d, qc, logidx, o,
-             ix, maxr + 1, check ? dr : nullptr, c->rtab);
-    else
-      LAUNCH((k_run_mask<RM_MASK_UNROLL, false>), dim3(gw), dim3(BLOCK), mshm, s, fr, Q, hm, hc, t->d, qc, logidx, o,
-             ix, maxr + 1, check ? dr : nullptr, c->rtab);
+    const bool dq = fr.qd || mask_devq;
+    auto mask_launch = [&](auto kern, const char* name) {
+      prof_begin(s);
+      hipLaunchKernelGGL(kern, dim3(gw), dim3(BLOCK), mshm, s, fr, Q, hm, hc, t->d, qc, logidx, o, ix, maxr + 1,
+                         check ? dr : nullptr, c->rtab);
+      prof_mark(name, s);
+    };
+    if (mask_u == 1) mask_launch(dq ? k_run_mask<1, true> : k_run_mask<1, false>, "k_run_mask");
+    else if (mask_u == 4) mask_launch(dq ? k_run_mask<4, true> : k_run_mask<4, false>, "k_run_mask");
+    else mask_launch(dq ? k_run_mask<RM_MASK_UNROLL, true> : k_run_mask<RM_MASK_UNROLL, false>, "k_run_mask");
     if ((r = dscan<SumOp, false>(ArrGen{hc}, hb, NW, &dr->run_count, ws, s, nullptr, fr.qd ? &dr->fl_nw : nullptr,
                                  "k_dscan_runs")))
       return r;
-    LAUNCH(k_run_heads, dim3(grid_for(64ULL * NW, BLOCK, 4096)), dim3(BLOCK), 0, s, fr, Q, fb.rm, ra.hh);
+    static const uint32_t heads_grid = env_grid("CRDTM_HEADS_GRID", 4096);
+    LAUNCH(k_run_heads, dim3(grid_for(64ULL * NW, BLOCK, heads_grid)), dim3(BLOCK), 0, s, fr, Q, fb.rm, ra.hh);
     // ---- K2a (heads' effective parents), parent runs, sibling order (stable radix sort by attach slot) ----
     ra.rr = ws.alloc<uint4>(Q + 1);
     ra.ca = ws.alloc<unsigned long long>(Q + 1);
@@ -3305,7 +3327,8 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     uint32_t* sv[2] = {ws.alloc<uint32_t>(Q + 1), ws.alloc<uint32_t>(Q + 1)};
     uint32_t* xs = ws.alloc<uint32_t>(Q + 1);
     uint32_t* groot = fb.cnt;  // one word: the root sentinel's first child in the sorted list
-    const uint32_t gr = grid_for(Q, BLOCK, 2048);
+    static const uint32_t run_grid = env_grid("CRDTM_RUN_GRID", 2048);
+    const uint32_t gr = grid_for(Q, BLOCK, run_grid);
     // (env CRDTM_EP_COHERENT=1: the walks read and write at agent scope)
     static const bool ep_coh = [] {
       const char* e = getenv("CRDTM_EP_COHERENT");
@@ -3331,7 +3354,8 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, groot, fb.rm);
     LAUNCH(k_run_pos, dim3(gr), dim3(BLOCK), 0, s, ra, dr);
     // ---- the document order, the chain ----
-    const uint32_t gx = grid_for(Q, BLOCK, 2048);
+    static const uint32_t ex_grid = env_grid("CRDTM_EX_GRID", 2048);
+    const uint32_t gx = grid_for(Q, BLOCK, ex_grid);
     const uint32_t ex_iters = (Q + gx * BLOCK - 1) / (gx * BLOCK);
     LAUNCH(k_run_expand, dim3(gx), dim3(BLOCK),
            ex_iters <= EX_ITERS ? 3 * ex_iters * (BLOCK / 64) * sizeof(uint32_t) : 0, s, ra, Q, K, fb.rm, pk, xs, qc,
@@ -3450,8 +3474,10 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   const uint32_t nrep = maxr + 1 <= HOST_RANGES && maxr + 1 <= 3840 ? maxr + 1 : 0u;
   const uint32_t shm = (4 * nrep + (nrep ? 0 : REP_DIRECT)) * sizeof(uint32_t);
   // (devq: k_pre_ts has checked the kinds and offsets; k_fl_claim<true, true> checks them itself)
+  static const uint32_t claim_grid = env_grid("CRDTM_CLAIM_GRID", 2048) & ~7u;  // (XCD chunks: a multiple of 8)
   if (simple)
-    LAUNCH((k_fl_claim<true, false>), dim3(quad_grid(n)), dim3(BLOCK), shm, s, o, ix, Q, fb.fr, t->timestamp,
+    LAUNCH((k_fl_claim<true, false>), dim3(std::min(quad_grid(n), std::max(8u, claim_grid))), dim3(BLOCK), shm, s, o,
+           ix, Q, fb.fr, t->timestamp,
            c->rtab, dr, nrep ? 0u : 1u, nrep, t->d, spec ? 1u : 0u);
   else
     LAUNCH((k_fl_claim<false, false>), dim3(quad_grid(n)), dim3(BLOCK), shm, s, o, ix, Q, fb.fr, t->timestamp,
