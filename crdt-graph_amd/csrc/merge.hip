@@ -3364,7 +3364,8 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     // by the expansion — the run's next slot, the first child run at the
     // slot, or the successor of the run's sub-document found by a walk up in
     // k_run_pos — cost 36 + 32 us more there than this pass's 33 us)
-    LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d, t->cap.slots);
+    static const uint32_t next_grid = env_grid("CRDTM_NEXT_GRID", 1u << 20);
+    LAUNCH(k_fl_next, dim3(grid_for(K, BLOCK, next_grid)), dim3(BLOCK), 0, s, K, t->d.doc, t->d, t->cap.slots);
     if (all_applied && !log_done) fl_log_copy(c, o, t->d, simple);
   } else if (all_applied && !log_done) {
     fl_log_copy(c, o, t->d, simple);
@@ -3781,11 +3782,13 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
       const uint32_t c = hc[lvl];
       if (!c) continue;
       const LvEnt* lst = lists + hs.v[lvl];
-      const uint32_t gl = grid_for(c);
+      static const uint32_t lv_grid = env_grid("CRDTM_LV_GRID", 1u << 20);  // (A/B)
+      static const uint32_t lv_lds = env_grid("CRDTM_LV_LDS", 40000);
+      const uint32_t gl = grid_for(c, BLOCK, lv_grid);
       // (k_lv_dict reserves 40 KB of LDS it does not use: at most 3 workgroups
       // per CU, so the lines of the prefix keys its lanes load stay in L2
       // between the load instructions; measured 1.27 -> 1.17 ms on deep10m)
-      LAUNCH(k_lv_dict, dim3(gl), dim3(BLOCK), 40000, s, o, w, ix, lst, c, lvl, dr);
+      LAUNCH(k_lv_dict, dim3(gl), dim3(BLOCK), lv_lds, s, o, w, ix, lst, c, lvl, dr);
       LAUNCH(k_lv_leaf, dim3(gl), dim3(BLOCK), 0, s, o, w, ix, lst, c, lvl, dr);
       LAUNCH(k_lv_fin, dim3(gl), dim3(BLOCK), 0, s, o, w, ix, lst, c, lvl);
     }

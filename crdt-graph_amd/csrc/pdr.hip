@@ -370,6 +370,9 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
           for (;;) {
             const uint32_t rn = wn & PM;
             if (rn == PM) break;
+            // ts > key(rn) stops the walk whatever follows rn: decided before
+            // rn's word is read (one dependent read fewer at every stop)
+            if (x > rn) break;
             PDR_STAT(0);
             if (rn == node + 1 && x < rn) {
               PDR_STAT(1);
@@ -414,7 +417,6 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
               if ((wl & SF_TOMB) && x < rn) gfail = true;  // a Tombstone above x: crossed or stopped before
             const uint32_t live = pdr_next_live(S, K, lane, rn, wl STC_ARG);
             if (live == PM) break;
-            if (x > rn) break;  // ts > key(rn)
             nk = rn;
             node = live;
             wn = wl;
@@ -785,12 +787,12 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
             for (;;) {
               const uint32_t rn = o_wn & PM;
               if (rn == PM) break;
+              if (x > rn) break;  // (decided before rn's word is read)
               uint32_t wl = ld_uniform(S, rn);
               if constexpr (GST)
                 if ((wl & SF_TOMB) && x < rn) o_gfail = true;
               const uint32_t live = pdr_next_live(S, K, lane, rn, wl STC_ARG);
               if (live == PM) break;
-              if (x > rn) break;
               o_nk = rn;
               o_node = live;
               o_wn = wl;
@@ -1114,13 +1116,13 @@ __global__ void __launch_bounds__(BLOCK) k_pdr_lane(PdrCtx p, const uint32_t* li
           for (;;) {
             const uint32_t rn = wn & PM;
             if (rn == PM) break;
+            if (x > rn) break;  // ts > key(rn): decided before rn's word is read
             uint32_t live = rn, wl = S[rn];  // nextNode: the first live node from rn on
             while (live != PM && (wl & SF_TOMB)) {
               live = wl & PM;
               if (live != PM) wl = S[live];
             }
             if (live == PM) break;
-            if (x > rn) break;  // ts > key(rn)
             nk = rn;
             node = live;
             wn = wl;
