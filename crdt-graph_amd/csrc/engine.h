@@ -184,6 +184,13 @@ struct IlrIndex {
   uint32_t* dsrc = nullptr;    // [dcap] a dict filled by a deferred copy its lane reads back: the source
   uint4* rec = nullptr;        // [scap] per slot {next, flags, key lo, key hi}: one load per findInsertion step
   uint64_t dcap = 0, scap = 0;
+  // the chain order snapshot (chain_snapshot) of the slots [0, snapE) as of
+  // `snap_age` batches ago: the walks check every link against the state,
+  // so an older snapshot is still exact, its checked runs only shorter
+  uint32_t* snapR = nullptr;
+  uint32_t* snapG = nullptr;
+  uint64_t snap_cap = 0;
+  uint32_t snapE = 0, snap_age = 0;
   ~IlrIndex();
 };
 }  // namespace crdtm

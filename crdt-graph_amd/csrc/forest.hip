@@ -13,13 +13,6 @@
 #include "engine.h"
 #include "kernels.h"
 
-#ifndef FOREST_HOIST
-#define FOREST_HOIST 0
-#endif
-#ifndef FOREST_EARLY
-#define FOREST_EARLY 0
-#endif
-
 namespace crdtm {
 
 // ---------------------------------------------------------------------------
@@ -256,10 +249,6 @@ __global__ void __launch_bounds__(64) k_forest_wave(const uint32_t* doc_off, uin
       const uint32_t w = __builtin_amdgcn_readlane(vw, k);
       const uint32_t t = w & FL_N;
       const uint32_t st = rd(t);
-#if FOREST_HOIST
-      const uint32_t a = (w >> 11) & FL_N;  // (FL_N for a Delete: slot FL_N reads 0)
-      const uint32_t sa = rd(a);  // (issued with st: both come from the op word)
-#endif
       if (wuni(w & (FO_DEL | FO_INV))) {
         if (wuni((w & FO_INV) | ((st & FW_PRESENT) ^ FW_PRESENT))) {  // InvalidPath / deleteHelp NotFound (:112-122)
           err = c0 + k;
@@ -277,10 +266,8 @@ __global__ void __launch_bounds__(64) k_forest_wave(const uint32_t* doc_off, uin
         own += ownb;
         continue;
       }
-#if !FOREST_HOIST
       const uint32_t a = (w >> 11) & FL_N;
       const uint32_t sa = rd(a);
-#endif
       if (!wuni(sa & FW_PRESENT)) {  // anchor missing: NotFound
         err = c0 + k;
         code = CRDTM_OPERATION_FAILED;
@@ -290,21 +277,15 @@ __global__ void __launch_bounds__(64) k_forest_wave(const uint32_t* doc_off, uin
       uint32_t nk = a, node = a, sn = sa;  // findInsertion (:93-104)
       for (;;) {
         const uint32_t rn = sn & FL_N;
-        // ts > key(rn) stops the walk whatever follows rn: decided before
-        // rn's word is read (rn = FL_N: x < FL_N, the read below ends it)
-#if FOREST_EARLY
-        if (wuni(x > rn)) break;
-#endif
         uint32_t live = rn, wl = rd(rn);
         while (wuni(wl & FW_TOMB)) {  // nextNode: the first live node after next
           live = wl & FL_N;
           wl = rd(live);
         }
-#if FOREST_EARLY
-        if (wuni(live == FL_N)) break;
-#else
+        // (measured in round 5: deciding `x > rn` before rn's word is read,
+        // as the per-dict replays do, 2.61 -> 3.02 ms here; the anchor's word
+        // read beside the target's, no change)
         if (wuni(live == FL_N || x > rn)) break;
-#endif
         nk = rn;
         node = live;
         sn = wl;

@@ -69,6 +69,8 @@ IlrIndex::~IlrIndex() {
   if (ev) hipFree(ev);
   if (xmap) hipFree(xmap);
   if (dsrc) hipFree(dsrc);
+  if (snapR) hipFree(snapR);
+  if (snapG) hipFree(snapG);
   if (rec) hipFree(rec);
 }
 
@@ -934,7 +936,7 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
               // link this batch changed ends the run): the walk's steps over
               // the checked run are decided together; only where the run
               // ends or breaks does the walk take single steps.
-              if (args.R && node < args.committed && args.R[node] != NONE) {
+              if (args.R && node < args.E && args.R[node] != NONE) {
                 const uint32_t pos = args.R[node] + 1 + lane;
                 const uint32_t ck = pos < args.E ? args.G[pos] : NONE;  // c_{lane+1}
                 const uint4 rc = ck != NONE ? args.rec[ck] : make_uint4(NONE, F_TOMB, 0u, 0u);
@@ -1224,6 +1226,8 @@ static int ilr_build(crdtm_tree* t) {
   hipStream_t s = c->stream;
   if (!t->ilr) t->ilr.reset(new IlrIndex);
   IlrIndex& X = *t->ilr;
+  X.snapE = 0;  // (a rebuilt index describes another state: the next level replay takes a fresh snapshot)
+  X.snap_age = 0;
   const uint32_t H = pow2_ge(2 * t->cap.slots);
   if (X.hcap < H) {
     HIP_CHECK(hipStreamSynchronize(s));
@@ -1446,14 +1450,38 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   a.R = nullptr;
   a.G = nullptr;
   a.E = 0;
+  // (kept with the index and rebuilt every CRDTM_ILR_SNAP_EVERY batches: a
+  // snapshot some batches old covers the slots it knew, and a link a later
+  // batch changed only ends a checked run early -- but the busy lane walks
+  // where the text changed: incr_cfg2 23.7 ms per 10 batches rebuilt every
+  // batch, 23.9 every 4, 25.4 every 8, 27.0 never, so 1 by default)
+  static const uint32_t snap_every = [] {
+    const char* e = getenv("CRDTM_ILR_SNAP_EVERY");
+    const int v = e ? atoi(e) : 1;
+    return static_cast<uint32_t>(v >= 1 ? v : 1);
+  }();
   if (snap_min && lv[ILR_MAXL + 3] >= snap_min) {
     const uint64_t E = t->n_slots;
-    uint32_t* R = ws.alloc<uint32_t>(E + 1);
-    uint32_t* G = ws.alloc<uint32_t>(E + 1);
-    if ((r = chain_snapshot(t, R, G, ws, s))) return r;
-    a.R = R;
-    a.G = G;
-    a.E = static_cast<uint32_t>(E);
+    if (!X->snapR || !X->snapE || X->snap_age + 1 >= snap_every || X->snapE > E) {
+      if (X->snap_cap < E + 1) {
+        if (X->snapR) hipFree(X->snapR);
+        if (X->snapG) hipFree(X->snapG);
+        X->snapR = X->snapG = nullptr;
+        X->snap_cap = 0;
+        const uint64_t cap = 2 * (E + 1) + 4096;
+        HIP_CHECK(hipMalloc(&X->snapR, cap * sizeof(uint32_t)));
+        HIP_CHECK(hipMalloc(&X->snapG, cap * sizeof(uint32_t)));
+        X->snap_cap = cap;
+      }
+      if ((r = chain_snapshot(t, X->snapR, X->snapG, ws, s))) return r;
+      X->snapE = static_cast<uint32_t>(E);
+      X->snap_age = 0;
+    } else {
+      ++X->snap_age;
+    }
+    a.R = X->snapR;
+    a.G = X->snapG;
+    a.E = X->snapE;
   }
   a.dsrc = X->dsrc;
   a.dnew = grave;
