@@ -388,7 +388,7 @@ struct IlrLane {
     a.T.s_child[x] = NONE;
     a.T.s_flags[x] = F_TOMB | F_ORPHAN;
     a.rec[x] = make_uint4(NONE, F_TOMB | F_ORPHAN, x, 0u);
-    for (uint32_t w = 0; w < EVW; ++w) ev(x, w) = NONE;
+    *reinterpret_cast<uint4*>(a.ev + static_cast<uint64_t>(EVW) * x) = make_uint4(NONE, NONE, NONE, NONE);
     a.mnext[x] = NONE;
   }
   // the pool's unused slots (they were counted: the commit keeps them)
@@ -412,11 +412,8 @@ struct IlrLane {
     a.rec[s] = r4;
     if (s - lbase < lcnt) lrec[s - lbase] = r4;
     if (s == cs) cr = r4;
-    uint32_t* e = a.ev + static_cast<uint64_t>(EVW) * s;
-    e[EV_CRE] = at;
-    e[EV_DEL] = NONE;
-    e[EV_CPY] = NONE;
-    e[EV_OCH] = NONE;
+    static_assert(EVW == 4 && EV_CRE == 0 && EV_DEL == 1 && EV_CPY == 2 && EV_OCH == 3, "one 16-byte store");
+    *reinterpret_cast<uint4*>(a.ev + static_cast<uint64_t>(EVW) * s) = make_uint4(at, NONE, NONE, NONE);
     if (priv) {
       if (2 * (pused + 1) > pmask + 1) {
         overflow(IO_PRIV);
