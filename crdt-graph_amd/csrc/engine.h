@@ -311,14 +311,16 @@ constexpr int R_INCR = 1 << 20;
 // merge.hip
 int sync_read(crdtm_ctx* c);
 // replicas[replicaId t] := t over the applied ops (st) into `rep`; collected by take_replicas after a sync
-int replica_fold(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, Arena& ws, hipStream_t s);
+// (zeroed: the caller's own kernel has cleared DevResult::n_replica_out / n_rep_list)
+int replica_fold(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, Arena& ws, hipStream_t s,
+                 bool zeroed = false);
 // forest.hip (FL_SLOTS above)
 int forest_flat_launch(const OpsDev& o, const uint32_t* doff, uint32_t n_docs, long long ts0, uint32_t* opw,
                        uint16_t* sent, uint8_t* fb, longlong2* vt, int32_t* code, uint32_t* err, uint32_t* applied,
                        unsigned long long* vhash, unsigned long long* vwords, long long* tstamp,
                        uint32_t* overflow, hipStream_t s);
 int replica_fold_into(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, uint32_t* rlist,
-                      hipStream_t s);
+                      hipStream_t s, bool zeroed = false);
 int take_replicas(crdtm_tree* t, const long long* rep_dev);
 // incr.hip: adds-only flat batch into a clean flat tree; *handled = false leaves it to apply_batch
 int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res, bool* handled);

@@ -57,10 +57,11 @@ constexpr uint32_t FI_WIN_THREADS = 1024;
 // flags word bits (fi[0]); FI_OVER alone: no window takes a block's batch,
 // merge densely. fi[1] own-replica Adds, fi[2] gaps, fi[3] blocks landed in,
 // fi[4] overflowing blocks, fi[5] rebalance windows, fi[6] the commit gate
-// (k_fi_gate: FG_NONE = the general paths decide, nothing is written;
+// (fi_gate, run by k_fi_win_list's last workgroup: FG_NONE = the general
+// paths decide, nothing is written;
 // FG_SPARSE = the blocks the batch lands in are rewritten; FG_DENSE = the
 // batch's nodes and log are committed, the order is merged densely by the
-// host after the result read)
+// host after the result read), fi[7] k_fi_win_list's workgroups done
 enum : uint32_t { FI_FAIL = 1u, FI_BUDGET = 2u, FI_OVER = 4u, FI_REPLICA = 8u };
 enum : uint32_t { FG_NONE = 0u, FG_SPARSE = 1u, FG_DENSE = 2u };
 constexpr uint32_t FI_COMMIT_GRID = 1024;  // (grid-stride commit kernels: sized before the counts are known)
@@ -83,10 +84,6 @@ __global__ void __launch_bounds__(BLOCK) k_kx_build(const long long* s_key, uint
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_kx_insert(OpsDev o, uint32_t slot0, TsHash h, const uint32_t* gate) {
-  if (gate && gate[6] == FG_NONE) return;  // (grid-uniform: incr.hip's commit gate)
-  GRID_STRIDE(i, o.n) tshash_insert(h, o.ts[i], slot0 + i);
-}
 
 // the gapped order from a dense one: block b holds ranks [FI_FILL b, FI_FILL b + FI_FILL)
 __global__ void __launch_bounds__(BLOCK) k_fi_build(uint32_t K, uint32_t nbk, const uint32_t* doc,
@@ -179,12 +176,16 @@ __device__ __forceinline__ long long wave_min64(long long k) {
 // not run leaves nothing for the replicas fold) and the flags words cleared
 // (one launch)
 __global__ void __launch_bounds__(BLOCK) k_fi_clear(unsigned long long* keys, uint32_t cap, uint32_t* fi, uint8_t* st,
-                                                    uint32_t m) {
+                                                    uint32_t m, DevResult* dres) {
   GRID_STRIDE(q, cap) {
     keys[q] = 0;
     if (q < m) st[q] = ST_PENDING;
   }
   if (blockIdx.x == 0 && threadIdx.x < FI_WORDS) fi[threadIdx.x] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // (the replicas fold's counters, for the commit's fold)
+    dres->n_replica_out = 0;
+    dres->n_rep_list = 0;
+  }
 }
 
 // The commit gate, decided on the device so that the commit is queued
@@ -194,14 +195,21 @@ __global__ void __launch_bounds__(BLOCK) k_fi_clear(unsigned long long* keys, ui
 // (incrementTimestamp, src/CRDTree.elm:337-343); it merges densely when a
 // block overflows with no window to take it (or no LDS for the windows).
 // The flags words go to the result block, read back once at the end.
-__global__ void k_fi_gate(uint32_t* fi, long long ts0, uint32_t win_lds, DevResult* dres) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint32_t f = fi[0];
-  if (replica_of(ts0 + fi[1]) != replica_of(ts0)) f |= FI_REPLICA;
-  if (fi[5] && !win_lds) f |= FI_OVER;
-  fi[0] = f;
-  fi[6] = (f & (FI_FAIL | FI_BUDGET | FI_REPLICA)) ? FG_NONE : (f & FI_OVER) ? FG_DENSE : FG_SPARSE;
-  for (uint32_t k = 0; k < FI_WORDS; ++k) dres->fincr[k] = fi[k];
+// (run by the workgroup of k_fi_win_list that finishes last: the flags words
+// are read at agent scope, every other workgroup's atomics being done)
+__device__ void fi_gate(uint32_t* fi, long long ts0, uint32_t win_lds, DevResult* dres) {
+  uint32_t v[FI_WORDS];
+#pragma unroll
+  for (uint32_t k = 0; k < FI_WORDS; ++k) v[k] = __hip_atomic_load(&fi[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t f = v[0];
+  if (replica_of(ts0 + v[1]) != replica_of(ts0)) f |= FI_REPLICA;
+  if (v[5] && !win_lds) f |= FI_OVER;
+  v[0] = f;
+  v[6] = (f & (FI_FAIL | FI_BUDGET | FI_REPLICA)) ? FG_NONE : (f & FI_OVER) ? FG_DENSE : FG_SPARSE;
+  fi[0] = v[0];
+  fi[6] = v[6];
+#pragma unroll
+  for (uint32_t k = 0; k < FI_WORDS; ++k) dres->fincr[k] = v[k];
 }
 
 // batch keys -> op index; a key seen twice fails the batch
@@ -507,7 +515,9 @@ __global__ void __launch_bounds__(BLOCK) k_fi_win_pick(uint32_t nbk, const uint3
 // of it to flag its leader lists it) in wl / fi[5]
 constexpr uint32_t FI_WIN_LISTED = 0x80u;
 __global__ void __launch_bounds__(BLOCK) k_fi_win_list(const uint32_t* ovl, uint32_t* fi, uint32_t* bwin,
-                                                       uint32_t* wl, uint32_t* wlev) {
+                                                       uint32_t* wl, uint32_t* wlev, long long ts0, uint32_t win_lds,
+                                                       DevResult* dres) {
+  __shared__ bool last;
   GRID_STRIDE(w, fi[4]) {
     const uint32_t b = ovl[w], L = bwin[b] & ~FI_WIN_LISTED;
     const uint32_t w0 = b & ~((1u << (L - 1)) - 1u);
@@ -516,6 +526,16 @@ __global__ void __launch_bounds__(BLOCK) k_fi_win_list(const uint32_t* ovl, uint
       wl[u] = w0;
       wlev[u] = L;
     }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(&fi[7], 1u) == gridDim.x - 1;  // (fi[7]: workgroups done)
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {  // the commit gate
+    __threadfence();
+    fi_gate(fi, ts0, win_lds, dres);
   }
 }
 
@@ -700,27 +720,26 @@ __device__ __forceinline__ void fi_sup_one(uint32_t sp, uint32_t nb, const long 
   const long long v = wave_min64(q < nb ? bmin[q] : FI_INF);
   if (lane == 0) smin[sp] = v;
 }
-__global__ void __launch_bounds__(BLOCK) k_fi_sup_fix(uint32_t Kp, const uint32_t* tl, const uint32_t* fi,
-                                                      const uint32_t* sk, const long long* bmin, long long* smin) {
+// (one wave per block landed in, then one per window; a superblock both
+// touch is recomputed twice from the same final minima)
+__global__ void __launch_bounds__(BLOCK) k_fi_sup_fix(uint32_t nbk, const uint32_t* tl, const uint32_t* sk,
+                                                      const uint32_t* wl, const uint32_t* wlev, const uint32_t* fi,
+                                                      const long long* bmin, long long* smin) {
   if (fi[6] != FG_SPARSE) return;  // (grid-uniform: the gate)
-  const uint32_t nw = gridDim.x * blockDim.x / 64;
-  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64; w < fi[3]; w += nw)  // (wave-uniform)
-    fi_sup_one(FI_BPB * fi_blk(sk[tl[w]], Kp) / FI_SUP, Kp / FI_BLK, bmin, smin);
-}
-// ... and over every superblock a window's blocks touch (one wave per window)
-__global__ void __launch_bounds__(BLOCK) k_fi_sup_win(uint32_t nbk, const uint32_t* wl, const uint32_t* fi,
-                                                      const uint32_t* wlev, const long long* bmin, long long* smin) {
-  if (fi[6] != FG_SPARSE) return;  // (grid-uniform: the gate)
-  const uint32_t nw = gridDim.x * blockDim.x / 64;
-  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64; w < fi[5]; w += nw) {  // (wave-uniform)
-    const uint32_t w0 = wl[w], ne = min(1u << (wlev[w] - 1), nbk - w0);
-    for (uint32_t sp = FI_BPB * w0 / FI_SUP; sp <= (FI_BPB * (w0 + ne) - 1) / FI_SUP; ++sp)
-      fi_sup_one(sp, FI_BPB * nbk, bmin, smin);
+  const uint32_t Kp = nbk * FI_CAP, nw = gridDim.x * blockDim.x / 64, nblk = fi[3], nwin = fi[5];
+  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) / 64; w < nblk + nwin; w += nw) {  // (wave-uniform)
+    if (w < nblk) {
+      fi_sup_one(FI_BPB * fi_blk(sk[tl[w]], Kp) / FI_SUP, Kp / FI_BLK, bmin, smin);
+    } else {
+      const uint32_t w0 = wl[w - nblk], ne = min(1u << (wlev[w - nblk] - 1), nbk - w0);
+      for (uint32_t sp = FI_BPB * w0 / FI_SUP; sp <= (FI_BPB * (w0 + ne) - 1) / FI_SUP; ++sp)
+        fi_sup_one(sp, FI_BPB * nbk, bmin, smin);
+    }
   }
 }
 
 // ... then the top entries over every superblock the blocks and windows
-// touched (one wave per block or window; after k_fi_sup_fix / k_fi_sup_win)
+// touched (one wave per block or window; after k_fi_sup_fix)
 __device__ __forceinline__ void fi_top_one(uint32_t tp, uint32_t ns, const long long* smin, long long* tmin) {
   const uint32_t lane = threadIdx.x & 63, q = tp * FI_SUP + lane;
   const long long v = wave_min64(q < ns ? smin[q] : FI_INF);
@@ -940,9 +959,11 @@ __global__ void __launch_bounds__(BLOCK) k_fi_next(uint32_t K, uint32_t m, const
 
 // node records of the new slots and the log append (every op applied, |path| = 1)
 __global__ void __launch_bounds__(BLOCK) k_fi_commit(OpsDev o, uint32_t slot0, uint32_t log0, uint32_t lpath0,
-                                                     TreeDev T, uint8_t* st, uint8_t* st_out, const uint32_t* fi) {
+                                                     TreeDev T, uint8_t* st, uint8_t* st_out, const uint32_t* fi,
+                                                     TsHash kx) {
   if (fi[6] == FG_NONE) return;  // (grid-uniform: the gate)
   GRID_STRIDE(i, o.n) {
+    tshash_insert(kx, o.ts[i], slot0 + i);  // (the key index: the batch's keys)
     const uint32_t sl = slot0 + i;
     st[i] = ST_APPLIED;
     if (st_out) st_out[i] = CRDTM_ST_APPLIED;
@@ -1114,7 +1135,7 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   const TsHash kx{X.keys, X.vals, X.mask};
   uint32_t* rank_of = X.rank;
   // ---- phase A: anchors, validity ----
-  LAUNCH(k_fi_clear, dim3(grid_for(bcap)), dim3(BLOCK), 0, s, bh.keys, bcap, fi, st, m);
+  LAUNCH(k_fi_clear, dim3(grid_for(bcap)), dim3(BLOCK), 0, s, bh.keys, bcap, fi, st, m, c->dres);
   LAUNCH(k_fi_bidx, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, bh, fi);
   LAUNCH(k_fi_resolve, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, kx, bh, rank_of, replica_of(t->timestamp), par[0],
          par0, sta[0], thr[0], fi);
@@ -1147,12 +1168,13 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   LAUNCH(k_fi_tblk, dim3(gm), dim3(BLOCK), 0, s, m, nbk, sk, ord, X.bent, X.bcnt, X.bfirst, X.bend, tl, gpred, fi);
   LAUNCH(k_fi_win_pick, dim3(grid_for(64ULL * m)), dim3(BLOCK), 0, s, nbk, sk, tl, X.bcnt, X.bfirst, X.bend, X.bwin,
          ovl, fi);
-  LAUNCH(k_fi_win_list, dim3(grid_for(m)), dim3(BLOCK), 0, s, ovl, fi, X.bwin, wl, wlev);
   // (resolved before the commit is queued: nothing may fail once it is)
   static const bool win_lds = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fi_win),
                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                                   FI_WIN_ENT * 12) == hipSuccess;
-  LAUNCH(k_fi_gate, dim3(1), dim3(64), 0, s, fi, static_cast<long long>(t->timestamp), win_lds ? 1u : 0u, c->dres);
+  // (its last workgroup decides the commit gate)
+  LAUNCH(k_fi_win_list, dim3(grid_for(m)), dim3(BLOCK), 0, s, ovl, fi, X.bwin, wl, wlev,
+         static_cast<long long>(t->timestamp), win_lds ? 1u : 0u, c->dres);
   // ---- phase C: the commit, queued at once and gated on the device
   // (k_fi_gate): one host round trip per batch, at its end ----
   TreeCaps need = t->cap;
@@ -1164,7 +1186,7 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
     if ((r = grow_tree(t, need))) return r;
   const uint32_t slot0 = static_cast<uint32_t>(t->n_slots);
   LAUNCH(k_fi_commit, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, slot0, static_cast<uint32_t>(t->log_n),
-         static_cast<uint32_t>(t->log_npath), t->d, st, st_out, fi);
+         static_cast<uint32_t>(t->log_npath), t->d, st, st_out, fi, kx);
   // O(batch): the blocks the batch lands in (grid-stride over the device's
   // counts; blocks and windows are at most one per op)
   const uint32_t cg = std::min<uint32_t>(FI_COMMIT_GRID, std::min<uint32_t>(m, nbk));
@@ -1174,11 +1196,10 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   if (win_lds)
     LAUNCH(k_fi_win, dim3(wg), dim3(FI_WIN_THREADS), FI_WIN_ENT * 12, s, nbk, wl, wlev, fi, sk, sv, ord, first, gpred,
            slot0, o.ts, X.bent, X.bdk, X.bcnt, X.bfirst, X.bend, X.bwin, X.bmin, rank_of, t->d.s_next);
-  LAUNCH(k_fi_sup_fix, dim3(grid_for(64ULL * cg)), dim3(BLOCK), 0, s, Kp, tl, fi, sk, X.bmin, X.smin);
-  if (win_lds) LAUNCH(k_fi_sup_win, dim3(grid_for(64ULL * wg)), dim3(BLOCK), 0, s, nbk, wl, fi, wlev, X.bmin, X.smin);
+  LAUNCH(k_fi_sup_fix, dim3(grid_for(64ULL * cg)), dim3(BLOCK), 0, s, nbk, tl, sk, wl, wlev, fi, X.bmin, X.smin);
   LAUNCH(k_fi_top_fix, dim3(grid_for(64ULL * cg)), dim3(BLOCK), 0, s, nbk, tl, sk, wl, wlev, fi, X.smin, X.tmin);
-  LAUNCH(k_kx_insert, dim3(grid_for(m)), dim3(BLOCK), 0, s, o, slot0, kx, fi);
-  if ((r = replica_fold(c, o, st, rep, ws, s))) return r;  // (statuses not applied fold nothing)
+  // (statuses not applied fold nothing; k_fi_clear zeroed the fold's counters)
+  if ((r = replica_fold(c, o, st, rep, ws, s, true))) return r;
   if ((r = sync_read(c))) return r;
   uint32_t hf[FI_WORDS];
   std::memcpy(hf, c->hres->fincr, sizeof(hf));

@@ -3054,17 +3054,18 @@ __global__ void __launch_bounds__(BLOCK) k_post_flags(OpsDev o, const uint8_t* s
 // into c->rtab, collect the touched replicas into `rep` (+ the inline copy).
 static_assert(offsetof(DevResult, n_rep_list) == offsetof(DevResult, n_replica_out) + sizeof(uint32_t),
               "one memset clears both counters");
-int replica_fold(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, Arena& ws, hipStream_t s) {
+int replica_fold(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, Arena& ws, hipStream_t s,
+                 bool zeroed) {
   uint32_t* rlist = ws.alloc<uint32_t>(std::min<uint64_t>(o.n, REPLICA_SLOTS) + 1);
-  return replica_fold_into(c, o, st, rep, rlist, s);
+  return replica_fold_into(c, o, st, rep, rlist, s, zeroed);
 }
 
 // (rlist: min(n, REPLICA_SLOTS) + 1 words, taken by the caller)
 int replica_fold_into(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, uint32_t* rlist,
-                      hipStream_t s) {
+                      hipStream_t s, bool zeroed) {
   DevResult* dr = c->dres;
   const uint32_t n = o.n;
-  HIP_CHECK(hipMemsetAsync(&dr->n_replica_out, 0, 2 * sizeof(uint32_t), s));  // n_replica_out, n_rep_list
+  if (!zeroed) HIP_CHECK(hipMemsetAsync(&dr->n_replica_out, 0, 2 * sizeof(uint32_t), s));  // n_replica_out, n_rep_list
   LAUNCH(k_rep_max, dim3(rep_grid(n)), dim3(BLOCK), 0, s, o, st, c->rtab, rlist, &dr->n_rep_list, rep_per(n));
   LAUNCH(k_rep_out, dim3(64), dim3(BLOCK), 0, s, o, c->rtab, rlist, &dr->n_rep_list, rep, &dr->n_replica_out,
          dr->rep_inline);
