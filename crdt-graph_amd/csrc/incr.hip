@@ -440,17 +440,6 @@ __global__ void __launch_bounds__(BLOCK) k_fi_gap(uint32_t m, uint32_t K, const 
   }
 }
 
-// sorted position of every op (pos) and the gap heads: the first sorted
-// position of every gap, listed (any order); one item per thread
-// (wave-aggregated tickets: ~10k heads on one counter)
-__global__ void __launch_bounds__(BLOCK) k_fi_gstart(uint32_t m, const uint32_t* gk, const uint32_t* gv,
-                                                     uint32_t* pos, uint32_t* list, uint32_t* cnt) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < m) pos[gv[k]] = k;
-  const bool head = k < m && (k == 0 || gk[k - 1] != gk[k]);
-  const uint32_t t = wave_ticket(cnt, head);
-  if (head) list[t] = k;
-}
 
 // block of a gap position (Kp = past the end: the last block)
 __device__ __forceinline__ uint32_t fi_blk(uint32_t g, uint32_t Kp) { return (g < Kp ? g : Kp - 1) / FI_CAP; }
@@ -792,14 +781,26 @@ struct FiGapLds {
   long long lk[FI_GAP_LDS];
   uint32_t la[FI_GAP_LDS], ln[FI_GAP_LDS], lo[FI_GAP_LDS];
 };
-__device__ __forceinline__ void fi_gap_one(uint32_t w, uint32_t m, const uint32_t* list, const uint32_t* gk,
-                                           const uint32_t* gv, const uint32_t* par0, const uint32_t* pos,
-                                           const long long* ts, uint32_t* nxt, uint32_t* ord, uint32_t* first,
-                                           uint32_t* fi, FiGapLds& L) {
+// (an anchor op is in the gap iff its own gap key is the gap's; its place
+// there is its rank among the gap's ops, which are in batch order)
+__device__ __forceinline__ uint32_t fi_rank_of(const uint32_t* v, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (v[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ void fi_gap_one(uint32_t k, uint32_t m, const uint32_t* gk, const uint32_t* gv,
+                                           const uint32_t* gk0, const uint32_t* par0, const long long* ts,
+                                           uint32_t* nxt, uint32_t* ord, uint32_t* first, uint32_t* fi,
+                                           FiGapLds& L) {
   long long* lk = L.lk;
   uint32_t *la = L.la, *ln = L.ln, *lo = L.lo;
   const uint32_t lane = threadIdx.x;
-  const uint32_t k = list[w], g = gk[k];
+  const uint32_t g = gk[k];
   uint32_t e = k + 1;  // the gap's end: 64 positions per step
   for (;;) {
     const uint32_t q = e + lane;
@@ -812,8 +813,9 @@ __device__ __forceinline__ void fi_gap_one(uint32_t w, uint32_t m, const uint32_
   }
   const uint32_t n = e - k;
   if (n <= FI_GAP_LDS) {
-    // three dependent gathers (op, its key and anchor, the anchor's sorted
-    // position), each issued for all of the lane's entries at once
+    // three dependent gathers (op, its key and anchor, the anchor's gap),
+    // each issued for all of the lane's entries at once; the ops staged in
+    // LDS (lo, free until the order) for the anchors' ranks
     constexpr uint32_t PER = FI_GAP_LDS / 64;
     uint32_t op[PER], av[PER];
     long long kv[PER];
@@ -821,6 +823,7 @@ __device__ __forceinline__ void fi_gap_one(uint32_t w, uint32_t m, const uint32_
     for (uint32_t u = 0; u < PER; ++u) {
       const uint32_t j = lane + 64 * u;
       op[u] = j < n ? gv[k + j] : 0u;
+      if (j < n) lo[j] = op[u];
     }
 #pragma unroll
     for (uint32_t u = 0; u < PER; ++u) {
@@ -829,12 +832,14 @@ __device__ __forceinline__ void fi_gap_one(uint32_t w, uint32_t m, const uint32_
       av[u] = in ? par0[op[u]] : NONE;
     }
 #pragma unroll
+    for (uint32_t u = 0; u < PER; ++u) av[u] = (av[u] != NONE && gk0[av[u]] == g) ? av[u] : NONE;
+    __syncthreads();  // (lo staged)
+#pragma unroll
     for (uint32_t u = 0; u < PER; ++u) {
       const uint32_t j = lane + 64 * u;
       if (j < n) {
-        const uint32_t pa = av[u] != NONE ? pos[av[u]] : NONE;
         lk[j] = kv[u];
-        la[j] = (pa >= k && pa < e) ? pa - k : NONE;
+        la[j] = av[u] != NONE ? fi_rank_of(lo, n, av[u]) : NONE;
       }
     }
     __syncthreads();
@@ -870,10 +875,7 @@ __device__ __forceinline__ void fi_gap_one(uint32_t w, uint32_t m, const uint32_
     const long long x = ts[op];
     const uint32_t a = par0[op];
     uint32_t cur = NONE;  // NONE = the gap's head
-    if (a != NONE) {
-      const uint32_t pa = pos[a];
-      if (pa >= k && pa < e) cur = pa;
-    }
+    if (a != NONE && gk0[a] == g) cur = k + fi_rank_of(gv + k, e - k, a);
     uint32_t nx = cur == NONE ? head : nxt[cur];
     while (nx != NONE && ts[gv[nx]] > x) {
       cur = nx;
@@ -901,15 +903,23 @@ __device__ __forceinline__ void fi_gap_one(uint32_t w, uint32_t m, const uint32_
 // (a grid of at most FI_GAPS_GRID single-wave workgroups loops over the gaps:
 // one per op would schedule thousands of LDS-holding workgroups that exit)
 constexpr uint32_t FI_GAPS_GRID = 2048;
-__global__ void __launch_bounds__(64) k_fi_gaps(uint32_t m, const uint32_t* list, const uint32_t* cnt,
-                                                const uint32_t* gk, const uint32_t* gv, const uint32_t* par0,
-                                                const uint32_t* pos, const long long* ts, uint32_t* nxt,
+// (each workgroup takes the gaps that start in its chunk of sorted
+// positions: a head is a position whose key differs from the one before)
+__global__ void __launch_bounds__(64) k_fi_gaps(uint32_t m, const uint32_t* gk, const uint32_t* gv, const uint32_t* gk0,
+                                                const uint32_t* par0, const long long* ts, uint32_t* nxt,
                                                 uint32_t* ord, uint32_t* first, uint32_t* fi) {
   __shared__ FiGapLds L;
-  const uint32_t ng = *cnt;
-  for (uint32_t w = blockIdx.x; w < ng; w += gridDim.x) {
-    fi_gap_one(w, m, list, gk, gv, par0, pos, ts, nxt, ord, first, fi, L);
-    __syncthreads();  // (the next gap reuses the LDS)
+  const uint32_t lane = threadIdx.x;
+  const uint32_t C = (m + gridDim.x - 1) / gridDim.x, c0 = blockIdx.x * C, c1 = min(m, c0 + C);
+  for (uint32_t b = c0; b < c1; b += 64) {
+    const uint32_t q = b + lane;
+    unsigned long long hm = __ballot(q < c1 && (q == 0 || gk[q - 1] != gk[q]));
+    while (hm) {
+      const uint32_t k = b + static_cast<uint32_t>(__builtin_ctzll(hm));
+      hm &= hm - 1;
+      fi_gap_one(k, m, gk, gv, gk0, par0, ts, nxt, ord, first, fi, L);
+      __syncthreads();  // (the next gap reuses the LDS)
+    }
   }
 }
 
@@ -1119,9 +1129,7 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   uint32_t* par0 = ws.alloc<uint32_t>(m);
   uint32_t* gk[2] = {ws.alloc<uint32_t>(m), ws.alloc<uint32_t>(m)};
   uint32_t* gv[2] = {ws.alloc<uint32_t>(m), ws.alloc<uint32_t>(m)};
-  uint32_t* pos = ws.alloc<uint32_t>(m);
   uint32_t* nxt = ws.alloc<uint32_t>(m);
-  uint32_t* glist = ws.alloc<uint32_t>(m);
   uint32_t* tl = ws.alloc<uint32_t>(m);
   uint32_t* ovl = ws.alloc<uint32_t>(m);
   uint32_t* gpred = ws.alloc<uint32_t>(m);
@@ -1163,8 +1171,10 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   // words in one workgroup's LDS, 0.47 ms per batch against 0.29)
   if ((r = radix_sort_small(gk[0], gv[0], m, bits, sk, sv, s))) return r;
   const uint32_t gm = (m + BLOCK - 1) / BLOCK;  // one item per thread
-  LAUNCH(k_fi_gstart, dim3(gm), dim3(BLOCK), 0, s, m, sk, sv, pos, glist, fi + 2);
-  LAUNCH(k_fi_gaps, dim3(std::min(m, FI_GAPS_GRID)), dim3(64), 0, s, m, glist, fi + 2, sk, sv, par0, pos, o.ts, nxt, ord, first, fi);
+  // (the gap heads and the anchors' places are found by k_fi_gaps itself:
+  // one launch fewer than a separate pass listing them)
+  LAUNCH(k_fi_gaps, dim3(std::min(m, FI_GAPS_GRID)), dim3(64), 0, s, m, sk, sv, gk[0], par0, o.ts, nxt, ord, first,
+         fi);
   LAUNCH(k_fi_tblk, dim3(gm), dim3(BLOCK), 0, s, m, nbk, sk, ord, X.bent, X.bcnt, X.bfirst, X.bend, tl, gpred, fi);
   LAUNCH(k_fi_win_pick, dim3(grid_for(64ULL * m)), dim3(BLOCK), 0, s, nbk, sk, tl, X.bcnt, X.bfirst, X.bend, X.bwin,
          ovl, fi);
