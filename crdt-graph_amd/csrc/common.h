@@ -108,7 +108,7 @@ struct DevResult {
   uint32_t run_maxd;        // flat order: deepest run
   uint32_t run_lhist[64];   // flat order: runs per depth
   long long rep_inline[2 * REP_INLINE];  // replicas table entries collected by a commit (the first REP_INLINE)
-  uint32_t ilr_levels[136];  // host staging: groups per level, private table entries (ilr.hip)
+  uint32_t ilr_levels[204];  // host staging: groups, ops and largest private table per level (ilr.hip)
   uint32_t fincr[8];         // incremental flat merge (incr.hip): its flags words, read back with the result
 };
 

@@ -627,12 +627,13 @@ __global__ void __launch_bounds__(BLOCK) k_ilr_gsize(const uint32_t* sk, uint32_
                                                      uint32_t* qn, uint32_t* pcap) {
   GRID_STRIDE(k, n) {
     if (!flag[k]) continue;
-    const uint32_t j = gidx[k], e = gend[j];
-    atomicAdd(&lvops[sk[k] >> gbits], e - k);
+    const uint32_t j = gidx[k], e = gend[j], L = sk[k] >> gbits;
+    atomicAdd(&lvops[L], e - k);
     atomicMax(&lvcnt[ILR_MAXL + 3], e - k);  // (the largest group)
     const uint32_t a = adds[e] - adds[k];
     qn[j] = a;
     pcap[j] = ilr_pcap(a);
+    atomicMax(&lvops[LV_N + L], a);  // (per level: the most Adds of a group, for its launch's LDS)
   }
 }
 
@@ -753,9 +754,12 @@ __global__ void __launch_bounds__(64) k_ilr_free(IlrArgs args, uint32_t L, const
 // ---- one level, one phase: one lane per group ----
 // phase 1: every group that receives no deferred copy (it makes those it
 // owns); phase 2: the groups landing in deferred copies
+// (LDS sized per launch from the level's largest group: lrn record mirror
+// entries and ptn private table entries; a level of small groups keeps
+// more of them resident per CU)
 __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const uint32_t* vs, const uint32_t* gbeg,
                                                   const uint32_t* gend, uint32_t g0, uint32_t L, uint32_t phase,
-                                                  uint8_t* st) {
+                                                  uint8_t* st, uint32_t lrn, uint32_t ptn) {
   // (one wave per group: every lane runs the replay on the same values; the
   // lanes part ways only in the chain-order walk below)
   const uint32_t g = g0 + blockIdx.x;
@@ -763,11 +767,13 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
   if ((gf & GF_DST) ? phase != 2 : phase != 1) return;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t kb = gbeg[g], ke = gend[g];
-  __shared__ uint4 lrec[ILR_LREC];
-  __shared__ long long tpk[PT_LDS];
-  __shared__ uint32_t tpd[PT_LDS], tps[PT_LDS];
+  extern __shared__ uint4 ilr_dyn[];
+  uint4* lrec = ilr_dyn;                                                 // [lrn]
+  long long* tpk = reinterpret_cast<long long*>(lrec + lrn);            // [ptn]
+  uint32_t* tpd = reinterpret_cast<uint32_t*>(tpk + ptn);              // [ptn]
+  uint32_t* tps = tpd + ptn;                                           // [ptn]
   const uint32_t pc = args.pcap[g];
-  const bool plds = pc <= PT_LDS && !(args.off & 1);
+  const bool plds = pc <= ptn && !(args.off & 1);
   if (plds) {
     for (uint32_t q = lane; q < pc; q += 64) tps[q] = NONE;
     __syncthreads();
@@ -788,7 +794,7 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
   R.ucnt = 0;
   R.lrec = lrec;
   R.lbase = R.qnext;
-  R.lcnt = (args.off & 2) ? 0u : min(args.qn[g], ILR_LREC);
+  R.lcnt = (args.off & 2) ? 0u : min(args.qn[g], lrn);
   R.cpnext = R.cpend = 0;
   R.hd_d = NONE;
   R.hd_v = NONE;
@@ -1335,12 +1341,12 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   uint32_t* pcap = ws.alloc<uint32_t>(n + 2);
   uint32_t* poff = ws.alloc<uint32_t>(n + 2);
   uint32_t* ucnt = ws.alloc<uint32_t>(n + 1);
-  uint32_t* lvcnt = ws.alloc<uint32_t>(2 * LV_N);  // groups per level, totals; then ops per level
+  uint32_t* lvcnt = ws.alloc<uint32_t>(3 * LV_N);  // groups per level, totals; ops per level; most Adds per level
   FillList fl;  // (one launch for the batch's cleared arrays)
   fl.add(gk, gsz * sizeof(unsigned long long), 0u);
   fl.add(slot2grp, gsz * sizeof(uint32_t), NONE);
   fl.add(tk, tsz * sizeof(unsigned long long), 0u);
-  fl.add(lvcnt, 2 * LV_N * sizeof(uint32_t), 0u);
+  fl.add(lvcnt, 3 * LV_N * sizeof(uint32_t), 0u);
   fl.add(qn, (n + 2) * sizeof(uint32_t), 0u);
   fl.add(pcap, (n + 2) * sizeof(uint32_t), 0u);
   fl.add(nd, sizeof(uint32_t), n);
@@ -1363,11 +1369,11 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   const uint32_t grave = static_cast<uint32_t>(t->n_dicts);
   LAUNCH(k_ilr_counters, dim3(1), dim3(1), 0, s, dr, t->d, X->dhead, X->dsrc, static_cast<uint32_t>(t->n_slots),
          lvcnt + LV_QTOT, grave);
-  static_assert(sizeof(DevResult::ilr_levels) >= 2 * LV_N * sizeof(uint32_t), "staging room");
+  static_assert(sizeof(DevResult::ilr_levels) >= 3 * LV_N * sizeof(uint32_t), "staging room");
   uint32_t* hl = c->hres->ilr_levels;  // (pinned)
-  HIP_CHECK(hipMemcpyAsync(hl, lvcnt, 2 * LV_N * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(hl, lvcnt, 3 * LV_N * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   if (int rw = stream_wait(s)) return rw;
-  uint32_t lv[2 * LV_N];
+  uint32_t lv[3 * LV_N];
   memcpy(lv, hl, sizeof(lv));
   uint32_t G = 0, nops = 0;
   for (uint32_t L = 1; L <= ILR_MAXL; ++L) {
@@ -1505,9 +1511,16 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
       LAUNCH(k_ilr_free, dim3(1), dim3(64), 0, s, a, L, mk + 3, empty);
     }
     if (cnt) {
+      // the level's LDS from its largest group (mirror: its Adds; private
+      // table: ilr_pcap of them, when that fits PT_LDS)
+      const uint32_t amax = lv[2 * LV_N + L];
+      const uint32_t lrn = std::max<uint32_t>(64u, std::min<uint32_t>(ILR_LREC, (amax + 63) & ~63u));
+      const uint32_t pcm = ilr_pcap(amax);
+      const uint32_t ptn = std::max<uint32_t>(64u, pcm <= PT_LDS ? pcm : PT_LDS);
+      const size_t lv_lds = lrn * sizeof(uint4) + ptn * (sizeof(long long) + 2 * sizeof(uint32_t));
       LAUNCH(k_ilr_prep, dim3(grid_for(m, BLOCK, 1024)), dim3(BLOCK), 0, s, a, o, vs, p0, p0 + m);
       for (uint32_t ph = 1; ph <= 2; ++ph) {
-        LAUNCH(k_ilr_level, dim3(cnt), dim3(64), 0, s, a, o, vs, gbeg, gend, g0, L, ph, st);
+        LAUNCH(k_ilr_level, dim3(cnt), dim3(64), lv_lds, s, a, o, vs, gbeg, gend, g0, L, ph, st, lrn, ptn);
         // (phase 1's publish takes phase 2's slots mark, phase 2's the level's jobs mark)
         LAUNCH(k_ilr_publish, dim3(cnt + 64), dim3(BLOCK), 0, s, a.T, a.H, qoff, qn, J.gflag, g0, cnt, ph,
                a.committed, mk + ph - 1, dr, a.cap_slots, ph == 1 ? mk + 1 : nullptr, ph == 2 ? mk + 2 : nullptr);

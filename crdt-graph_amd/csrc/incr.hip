@@ -34,6 +34,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 #include "engine.h"
 #include "kernels.h"
@@ -1164,6 +1165,16 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   // wave's other three)
   LAUNCH(k_fi_gap, dim3(grid_for(64ULL * m)), dim3(BLOCK), 0, s, m, Kp, X.bdk, X.bmin, X.smin, X.tmin, sta[0],
          thr[0], gk[0], gv[0]);
+  static const char* dump = getenv("CRDTM_FI_DUMP_KEYS");  // (debug: one batch's gap keys, for tools/xbench_sort.py)
+  if (dump && *dump) {
+    std::vector<uint32_t> hk(m);
+    HIP_CHECK(hipMemcpyAsync(hk.data(), gk[0], m * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (FILE* fp = fopen(dump, "wb")) {
+      fwrite(hk.data(), sizeof(uint32_t), m, fp);
+      fclose(fp);
+    }
+  }
   uint32_t bits = 4;  // (gap positions run to Kp inclusive)
   while (bits < 32 && (static_cast<uint64_t>(Kp) >> bits) != 0) bits += 4;
   uint32_t *sk = gk[1], *sv = gv[1];

@@ -763,31 +763,61 @@ __global__ void __launch_bounds__(RS_W_T) k_rs_small_w(const uint32_t* __restric
   uint32_t* sk = rs_small_lds;
   uint16_t* sv = reinterpret_cast<uint16_t*>(sk + RS_W_WORDS);
   uint16_t* cnt = sv + RS_W_WORDS + (RS_W_WORDS & 1u);  // [digit][thread]
-  __shared__ uint32_t wsum[RS_W_T / 64];
+  __shared__ uint32_t wsum[RS_W_T / 64], wor[RS_W_T / 64], wand[RS_W_T / 64];
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  uint32_t kor = 0, kand = 0xFFFFFFFFu;
   {
     uint32_t k0[RS_W_IPT], v0[RS_W_IPT];
 #pragma unroll
     for (uint32_t j = 0; j < RS_W_IPT; ++j) {
       const uint32_t i = t + j * RS_W_T;
-      k0[j] = i < n ? kin[i] : 0xFFFFFFFFu;  // padding: digit 15 in every pass, after every item
+      k0[j] = i < n ? kin[i] : 0u;
       v0[j] = i < n ? vin[i] : 0u;
+      if (i < n) {
+        kor |= k0[j];
+        kand &= k0[j];
+      }
     }
 #pragma unroll
     for (uint32_t j = 0; j < RS_W_IPT; ++j) {
-      sk[rs_wpad(t + j * RS_W_T)] = k0[j];
-      sv[rs_wpad(t + j * RS_W_T)] = static_cast<uint16_t>(v0[j]);
+      if (t + j * RS_W_T < n) {
+        sk[rs_wpad(t + j * RS_W_T)] = k0[j];
+        sv[rs_wpad(t + j * RS_W_T)] = static_cast<uint16_t>(v0[j]);
+      }
     }
   }
+  // the bits where the keys differ (OR ^ AND): a digit every key shares
+  // needs no pass (a batch typed into one gap: none at all)
+  for (uint32_t d = 32; d > 0; d >>= 1) {
+    kor |= __shfl_xor(kor, d);
+    kand &= __shfl_xor(kand, d);
+  }
+  if (lane == 0) {
+    wor[wv] = kor;
+    wand[wv] = kand;
+  }
   __syncthreads();
+  kor = 0;
+  kand = 0xFFFFFFFFu;
+#pragma unroll
+  for (uint32_t w = 0; w < RS_W_T / 64; ++w) {
+    kor |= wor[w];
+    kand &= wand[w];
+  }
+  const uint32_t diff = kor ^ kand;
+  // (the items fill positions [0, n) before and after every pass: a thread's
+  // blocked positions past n hold nothing and count nothing)
+  const uint32_t nj = n > t * RS_W_IPT ? min(RS_W_IPT, n - t * RS_W_IPT) : 0u;
   for (uint32_t shift = 0; shift < bits; shift += 4) {
+    if (!((diff >> shift) & 15u)) continue;  // (block-uniform; the padding stays last)
     uint32_t k[RS_W_IPT], v[RS_W_IPT];
     unsigned long long c0 = 0, c1 = 0;  // 8-bit counters of digits 0-7 / 8-15
 #pragma unroll
     for (uint32_t j = 0; j < RS_W_IPT; ++j) {
-      k[j] = sk[t * (RS_W_IPT + 1) + j];
-      v[j] = sv[t * (RS_W_IPT + 1) + j];
+      k[j] = j < nj ? sk[t * (RS_W_IPT + 1) + j] : 0u;
+      v[j] = j < nj ? sv[t * (RS_W_IPT + 1) + j] : 0u;
       const uint32_t d = (k[j] >> shift) & 15u;
+      if (j >= nj) continue;
       if (d < 8) c0 += 1ULL << (8 * d);
       else c1 += 1ULL << (8 * (d - 8));
     }
@@ -824,8 +854,10 @@ __global__ void __launch_bounds__(RS_W_T) k_rs_small_w(const uint32_t* __restric
     }
 #pragma unroll
     for (uint32_t j = 0; j < RS_W_IPT; ++j) {
-      sk[q[j]] = k[j];
-      sv[q[j]] = static_cast<uint16_t>(v[j]);
+      if (j < nj) {
+        sk[q[j]] = k[j];
+        sv[q[j]] = static_cast<uint16_t>(v[j]);
+      }
     }
     __syncthreads();
   }
@@ -994,3 +1026,29 @@ int list_rank(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* e
 }
 
 }  // namespace crdtm
+
+// Kernel microbenchmark hook (not part of the drop-in ABI, include/crdtm.h):
+// the batch sort of radix_sort_small on caller device buffers, on a caller
+// stream. which: 0 or 1 = 1024 threads (the default), 2 = 512 threads.
+extern "C" __attribute__((visibility("default"))) int crdtm_xbench_sort_small(const uint32_t* kin, const uint32_t* vin,
+                                                                             uint32_t n, uint32_t bits, uint32_t* kout,
+                                                                             uint32_t* vout, void* stream, int which) {
+  static const bool set = [] {
+    bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&crdtm::k_rs_small),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(crdtm::RS_SMALL_LDS)) == hipSuccess;
+    ok &= hipFuncSetAttribute(reinterpret_cast<const void*>(&crdtm::k_rs_small_w),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(crdtm::RS_W_LDS)) == hipSuccess;
+    return ok;
+  }();
+  if (!set || n > crdtm::RS_SMALL_MAX || !n) return CRDTM_E_HIP;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (which <= 1)
+    hipLaunchKernelGGL(crdtm::k_rs_small_w, dim3(1), dim3(crdtm::RS_W_T), crdtm::RS_W_LDS, s, kin, vin, n, bits,
+                       kout, vout);
+  else
+    hipLaunchKernelGGL(crdtm::k_rs_small, dim3(1), dim3(crdtm::RS_SMALL_T), crdtm::RS_SMALL_LDS, s, kin, vin, n,
+                       bits, kout, vout);
+  return hipGetLastError() == hipSuccess ? CRDTM_OK : CRDTM_E_HIP;
+}

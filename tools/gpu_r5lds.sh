@@ -1,0 +1,10 @@
+#!/bin/bash
+# round 5: the small sort's digit skip + MSD buckets (incr flat), the level
+# replay's LDS sized per level (incr_cfg2): incremental tests + A/B on both
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests/test_gpu_incremental.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r5lds_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/r5lds_tests.log; [ $rc = 0 ] || exit $rc
+tools/gpu_ab.sh r5lds "" "" incr new lib:abtest/head/libcrdtm.so && tools/gpu_ab.sh r5lds "" "" incr_cfg2 new lib:abtest/head/libcrdtm.so && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r5lds_prof_incr -o run --output-format csv -- python3 bench.py --workload incr --steps 2 --warmup 1 --profile-steps 1 --cpu-sample 0 --pmc off > gpurun_out/r5lds_prof_incr.log 2>&1
