@@ -270,11 +270,12 @@ struct FillList {
   }
   int launch(hipStream_t s);  // (runs and clears the list; more than MAX regions: E_ARG)
 };
-// the same for n <= RS_SMALL_MAX pairs in one workgroup (primitives.hip), into (kout, vout);
-// values below 2^16 (the wide kernel carries them as u16)
+// the same for n <= RS_SMALL_MAX pairs (primitives.hip), into (kout, vout); values below
+// 2^16, ties of key in value order (stable when the values are the input positions);
+// cw: scratch of n rounded up to 1,024 words for the chunked sort (nullptr: one workgroup)
 constexpr uint32_t RS_SMALL_MAX = 16384;
 int radix_sort_small(const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t bits, uint32_t* kout,
-                     uint32_t* vout, hipStream_t st);
+                     uint32_t* vout, hipStream_t st, unsigned long long* cw = nullptr);
 // ent[e] = {succ, wbits}: see primitives.hip / listrank.h (list_rank_fused)
 int list_rank(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws, hipStream_t st);
 int list_rank_packed(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* excl, Arena& ws,

@@ -1141,6 +1141,7 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   uint32_t* newrank = ws.alloc<uint32_t>(m);
   uint8_t* st = ws.alloc<uint8_t>(m);
   long long* rep = ws.alloc<long long>(2ULL * m + 2);
+  unsigned long long* scw = ws.alloc<unsigned long long>((m + 1023) & ~1023u);  // (the gap sort's chunks)
   const TsHash kx{X.keys, X.vals, X.mask};
   uint32_t* rank_of = X.rank;
   // ---- phase A: anchors, validity ----
@@ -1180,7 +1181,7 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   uint32_t *sk = gk[1], *sv = gv[1];
   // (measured and reverted in round 5: a bitonic network over (gap, op)
   // words in one workgroup's LDS, 0.47 ms per batch against 0.29)
-  if ((r = radix_sort_small(gk[0], gv[0], m, bits, sk, sv, s))) return r;
+  if ((r = radix_sort_small(gk[0], gv[0], m, bits, sk, sv, s, scw))) return r;
   const uint32_t gm = (m + BLOCK - 1) / BLOCK;  // one item per thread
   // (the gap heads and the anchors' places are found by k_fi_gaps itself:
   // one launch fewer than a separate pass listing them)

@@ -867,20 +867,96 @@ __global__ void __launch_bounds__(RS_W_T) k_rs_small_w(const uint32_t* __restric
   }
 }
 
+// The same sort over many workgroups in two launches: each chunk of 1,024
+// pairs sorts its (key << 16 | value) words in LDS (a bitonic network: the
+// words are distinct, so the order is total), then every pair's place is its
+// place in its chunk plus, per other chunk, the words below its own (16
+// lanes per pair, one binary search each over L2-resident chunks). Ties of
+// key go by value: the stable order when the values are the input positions
+// (the caller's op indices).
+constexpr uint32_t RS_C_CHUNK = 1024, RS_C_T = RS_C_CHUNK / 2, RS_C_MAXCH = RS_SMALL_MAX / RS_C_CHUNK;
+static_assert(RS_C_MAXCH == 16, "one lane of a 16-lane group per chunk");
+
+__global__ void __launch_bounds__(RS_C_T) k_rs_chunk(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                     uint32_t n, unsigned long long* __restrict__ cw) {
+  __shared__ unsigned long long w[RS_C_CHUNK];
+  const uint32_t t = threadIdx.x, c0 = blockIdx.x * RS_C_CHUNK;
+#pragma unroll
+  for (uint32_t u = 0; u < 2; ++u) {
+    const uint32_t i = c0 + t + u * RS_C_T;
+    w[t + u * RS_C_T] = i < n ? (static_cast<unsigned long long>(kin[i]) << 16) | (vin[i] & 0xFFFFu) : ~0ULL;
+  }
+  // (a stage of distance j <= 64 keeps word e with the wave e / 128: between
+  // two such stages the wave's own in-order LDS accesses suffice; a stage of
+  // distance >= 128 crosses waves and takes the workgroup barrier around it)
+  bool cross = true;  // (the load above)
+  for (uint32_t k = 2; k <= RS_C_CHUNK; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      const bool cj = j >= 128;
+      if (cross || cj) __syncthreads();
+      else __builtin_amdgcn_wave_barrier();
+      cross = cj;
+      const uint32_t i = 2 * t - (t & (j - 1)), q = i + j;  // (bit j of i clear)
+      const unsigned long long a = w[i], b = w[q];
+      if ((a > b) == !(i & k)) {  // ascending where bit k of i is clear
+        w[i] = b;
+        w[q] = a;
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t u = 0; u < 2; ++u) cw[c0 + t + u * RS_C_T] = w[t + u * RS_C_T];
+}
+
+__global__ void __launch_bounds__(BLOCK) k_rs_merge(const unsigned long long* __restrict__ cw, uint32_t n,
+                                                     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
+  const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 4, m = threadIdx.x & 15;
+  const uint32_t nch = (n + RS_C_CHUNK - 1) / RS_C_CHUNK;
+  if (g >= nch * RS_C_CHUNK) return;  // (whole 16-lane groups)
+  const unsigned long long c = cw[g];
+  const uint32_t own = g / RS_C_CHUNK;
+  uint32_t below = 0;
+  if (m == own) {
+    below = g % RS_C_CHUNK;
+  } else if (m < nch) {
+    const unsigned long long* v = cw + m * RS_C_CHUNK;
+    uint32_t lo = 0, hi = RS_C_CHUNK;  // (the words < c: padding words are above every pair's)
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (v[mid] < c) lo = mid + 1;
+      else hi = mid;
+    }
+    below = lo;
+  }
+#pragma unroll
+  for (uint32_t o = 8; o > 0; o >>= 1) below += __shfl_xor(below, o, 16);
+  if (m == 0 && c != ~0ULL) {
+    kout[below] = static_cast<uint32_t>(c >> 16);
+    vout[below] = static_cast<uint32_t>(c & 0xFFFFu);
+  }
+}
+
 int radix_sort_small(const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t bits, uint32_t* kout,
-                     uint32_t* vout, hipStream_t st) {
+                     uint32_t* vout, hipStream_t st, unsigned long long* cw) {
   static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_small),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  static_cast<int>(RS_SMALL_LDS)) == hipSuccess;
   static const bool w_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rs_small_w),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                static_cast<int>(RS_W_LDS)) == hipSuccess;
-  static const bool wide = [] {
-    const char* e = getenv("CRDTM_RS_SMALL");
-    return !(e && !strcmp(e, "512"));
-  }();
+  // CRDTM_RS_SMALL: "w" / "512" select the one-workgroup kernels (A/B)
+  static const char* sel = getenv("CRDTM_RS_SMALL");
+  static const bool wide = !(sel && !strcmp(sel, "512"));
+  static const bool chunked = !sel || !*sel;
   if (n > RS_SMALL_MAX) return CRDTM_E_HIP;
   if (!n) return CRDTM_OK;
+  if (chunked && cw) {
+    const uint32_t nch = (n + RS_C_CHUNK - 1) / RS_C_CHUNK;
+    LAUNCH(k_rs_chunk, dim3(nch), dim3(RS_C_T), 0, st, kin, vin, n, cw);
+    LAUNCH(k_rs_merge, dim3((nch * RS_C_CHUNK * 16 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, cw, n, kout, vout);
+    return CRDTM_OK;
+  }
   if (wide && w_ok) {  // (the caller's values are op indices of the batch: below n <= 2^14)
     LAUNCH(k_rs_small_w, dim3(1), dim3(RS_W_T), RS_W_LDS, st, kin, vin, n, bits, kout, vout);
     return CRDTM_OK;
@@ -1029,10 +1105,12 @@ int list_rank(const uint2* ent, uint64_t n, uint32_t head, unsigned long long* e
 
 // Kernel microbenchmark hook (not part of the drop-in ABI, include/crdtm.h):
 // the batch sort of radix_sort_small on caller device buffers, on a caller
-// stream. which: 0 or 1 = 1024 threads (the default), 2 = 512 threads.
+// stream. which: 0 or 1 = 1024 threads, 2 = 512 threads, 3 = chunks + merge (the default; cw: n rounded up to
+// 1,024 words of scratch).
 extern "C" __attribute__((visibility("default"))) int crdtm_xbench_sort_small(const uint32_t* kin, const uint32_t* vin,
                                                                              uint32_t n, uint32_t bits, uint32_t* kout,
-                                                                             uint32_t* vout, void* stream, int which) {
+                                                                             uint32_t* vout, void* stream, int which,
+                                                                             unsigned long long* cw) {
   static const bool set = [] {
     bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&crdtm::k_rs_small),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1044,7 +1122,12 @@ extern "C" __attribute__((visibility("default"))) int crdtm_xbench_sort_small(co
   }();
   if (!set || n > crdtm::RS_SMALL_MAX || !n) return CRDTM_E_HIP;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (which <= 1)
+  if (which == 3) {
+    const uint32_t nch = (n + crdtm::RS_C_CHUNK - 1) / crdtm::RS_C_CHUNK;
+    hipLaunchKernelGGL(crdtm::k_rs_chunk, dim3(nch), dim3(crdtm::RS_C_T), 0, s, kin, vin, n, cw);
+    hipLaunchKernelGGL(crdtm::k_rs_merge, dim3((nch * crdtm::RS_C_CHUNK * 16 + crdtm::BLOCK - 1) / crdtm::BLOCK),
+                       dim3(crdtm::BLOCK), 0, s, cw, n, kout, vout);
+  } else if (which <= 1)
     hipLaunchKernelGGL(crdtm::k_rs_small_w, dim3(1), dim3(crdtm::RS_W_T), crdtm::RS_W_LDS, s, kin, vin, n, bits,
                        kout, vout);
   else

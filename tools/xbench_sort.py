@@ -15,7 +15,7 @@ from crdtm import _native as N  # noqa: E402
 
 L = N.lib()
 f = L.crdtm_xbench_sort_small
-f.argtypes = [C.c_void_p] * 2 + [C.c_uint32] * 2 + [C.c_void_p] * 3 + [C.c_int]
+f.argtypes = [C.c_void_p] * 2 + [C.c_uint32] * 2 + [C.c_void_p] * 3 + [C.c_int, C.c_void_p]
 rng = np.random.default_rng(1)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 dists = {
@@ -45,8 +45,9 @@ for name, keys in dists.items():
     vo = torch.empty_like(vin)
     want = np.argsort(keys, kind="stable")
     row = []
-    for which in (1, 2):
-        args = (kin.data_ptr(), vin.data_ptr(), n, bits, ko.data_ptr(), vo.data_ptr(), s.cuda_stream, which)
+    cw = torch.empty(((n + 1023) // 1024) * 1024, dtype=torch.int64, device=dev)
+    for which in (3, 1, 2):
+        args = (kin.data_ptr(), vin.data_ptr(), n, bits, ko.data_ptr(), vo.data_ptr(), s.cuda_stream, which, cw.data_ptr())
         assert f(*args) == 0
         torch.cuda.synchronize()
         ok = np.array_equal(vo.cpu().numpy(), want) and np.array_equal(ko.cpu().numpy().view(np.uint32), keys[want])
@@ -56,5 +57,5 @@ for name, keys in dists.items():
             f(*args)
         e1.record()
         torch.cuda.synchronize()
-        row.append("%s %.1f us%s" % (["w4", "w4", "s4"][which], e0.elapsed_time(e1) * 1e3 / 50, "" if ok else " WRONG"))
+        row.append("%s %.1f us%s" % (["w4", "w4", "s4", "chunk"][which], e0.elapsed_time(e1) * 1e3 / 50, "" if ok else " WRONG"))
     print("%-12s bits %2d  %s" % (name, bits, "  ".join(row)), flush=True)
