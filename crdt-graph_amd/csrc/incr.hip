@@ -396,6 +396,87 @@ __global__ void __launch_bounds__(FI_JUMP_THREADS) k_fi_jump_lds(uint32_t m, uin
   }
 }
 
+// The same over many workgroups in two launches (anchors are earlier ops:
+// par[i] < i). Each chunk of FI_JC ops jumps in LDS along the pointers that
+// stay inside it; an op whose chain ends at a root of its chunk is final
+// there, one whose chain leaves the chunk (at e, whose anchor is an earlier
+// chunk's op) keeps jx = par[e] and jm = the chain's minimum up to e. Then
+// each such op follows jx from chunk to chunk (at most one hop per earlier
+// chunk) to a final op: its start, and the minimum over the hops.
+constexpr uint32_t FI_JC = 1024;
+__global__ void __launch_bounds__(FI_JC) k_fi_jump_chunk(uint32_t m, const uint32_t* P, uint32_t* S, long long* T,
+                                                         uint32_t* jx, long long* jm) {
+  __shared__ long long lt[FI_JC];
+  __shared__ uint16_t lp[FI_JC];
+  const uint32_t c0 = blockIdx.x * FI_JC, j = threadIdx.x, i = c0 + j;
+  const uint32_t n = min(FI_JC, m - c0);
+  const uint32_t p = i < m ? P[i] : NONE;
+  // local pointer: the anchor inside the chunk, else a stop (root or exit)
+  uint16_t mp = (p != NONE && p >= c0) ? static_cast<uint16_t>(p - c0) : FI_J_NONE;
+  long long mv = i < m ? T[i] : 0;
+  if (j < n) {
+    lp[j] = mp;
+    lt[j] = mv;
+  }
+  const uint16_t first = mp;
+  __syncthreads();
+  for (;;) {
+    int moved = 0;
+    uint16_t np = mp;
+    long long nv = mv;
+    if (j < n && mp != FI_J_NONE) {
+      const uint16_t pp = lp[mp];
+      if (pp != FI_J_NONE) {
+        nv = min(mv, lt[mp]);
+        np = pp;
+        moved = 1;
+      }
+    }
+    __syncthreads();  // every read of this round before any write
+    mp = np;
+    mv = nv;
+    if (j < n) {
+      lp[j] = mp;
+      lt[j] = mv;
+    }
+    if (!__syncthreads_or(moved)) break;
+  }
+  if (j >= n) return;
+  if (first == FI_J_NONE) {  // a root, or an op whose anchor is an earlier chunk's
+    jx[i] = p;
+    jm[i] = mv;
+    return;
+  }
+  const uint32_t e = c0 + mp;                  // the chain's last op in the chunk
+  const long long mm = min(mv, lt[mp]);        // (e never moved: lt = its own threshold)
+  const uint32_t pe = P[e];
+  if (pe == NONE) {  // final here
+    S[i] = S[e];
+    T[i] = mm;
+    jx[i] = NONE;
+  } else {
+    jx[i] = pe;
+  }
+  jm[i] = mm;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_fi_jump_fix(uint32_t m, const uint32_t* jx, const long long* jm,
+                                                       uint32_t* S, long long* T) {
+  GRID_STRIDE(i, m) {
+    uint32_t x = jx[i];
+    if (x == NONE) continue;  // (final: a root, or resolved inside its chunk)
+    long long v = jm[i];
+    for (;;) {  // (an earlier chunk's op per hop)
+      v = min(v, jm[x]);
+      const uint32_t y = jx[x];
+      if (y == NONE) break;
+      x = y;
+    }
+    S[i] = S[x];
+    T[i] = v;
+  }
+}
+
 // g = NSR(start, thr) over the base keys, one wave per query: 64 keys, 64
 // block minima or 64 superblock minima per step (ballot), then down again
 __global__ void __launch_bounds__(BLOCK) k_fi_gap(uint32_t m, uint32_t K, const long long* dk, const long long* bmin,
@@ -1142,6 +1223,8 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   uint8_t* st = ws.alloc<uint8_t>(m);
   long long* rep = ws.alloc<long long>(2ULL * m + 2);
   unsigned long long* scw = ws.alloc<unsigned long long>((m + 1023) & ~1023u);  // (the gap sort's chunks)
+  uint32_t* jx = ws.alloc<uint32_t>(m);  // (the chunked pointer jumping's exits and minima)
+  long long* jm = ws.alloc<long long>(m);
   const TsHash kx{X.keys, X.vals, X.mask};
   uint32_t* rank_of = X.rank;
   // ---- phase A: anchors, validity ----
@@ -1156,7 +1239,15 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   static const bool jump_lds = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fi_jump_lds),
                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
                                                    FI_JUMP_LDS_MAX * 10) == hipSuccess;
-  if (rounds && jump_lds && m <= FI_JUMP_LDS_MAX)
+  static const bool jump_chunks = [] {  // (CRDTM_FI_JUMP=lds: the one-workgroup kernel, for A/B)
+    const char* e = getenv("CRDTM_FI_JUMP");
+    return !(e && !strcmp(e, "lds"));
+  }();
+  if (rounds && jump_chunks) {
+    const uint32_t nch = (m + FI_JC - 1) / FI_JC;
+    LAUNCH(k_fi_jump_chunk, dim3(nch), dim3(FI_JC), 0, s, m, par[0], sta[0], thr[0], jx, jm);
+    LAUNCH(k_fi_jump_fix, dim3(grid_for(m)), dim3(BLOCK), 0, s, m, jx, jm, sta[0], thr[0]);
+  } else if (rounds && jump_lds && m <= FI_JUMP_LDS_MAX)
     LAUNCH(k_fi_jump_lds, dim3(1), dim3(FI_JUMP_THREADS), static_cast<size_t>(m) * 10, s, m, rounds, par[0], sta[0],
            thr[0]);
   else if (rounds)
