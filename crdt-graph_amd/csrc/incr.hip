@@ -859,9 +859,15 @@ __global__ void __launch_bounds__(BLOCK) k_fi_dense_gaps(uint32_t m, uint32_t Kp
 // the LDS stage walks global memory instead); then ord[] = the list order
 // and first[] = the gap's first sorted position.
 constexpr uint32_t FI_GAP_LDS = 1024;
+// (le[j]: j's successor in the gap's list and that successor's key in one
+// word, key << 11 | index: a walk step is one LDS read; keys are positive
+// timestamps below 2^53)
+constexpr uint32_t FI_LE_NONE = 0x7FF;
+static_assert(FI_GAP_LDS < FI_LE_NONE, "11-bit list indices");
 struct FiGapLds {
   long long lk[FI_GAP_LDS];
-  uint32_t la[FI_GAP_LDS], ln[FI_GAP_LDS], lo[FI_GAP_LDS];
+  unsigned long long le[FI_GAP_LDS];
+  uint32_t la[FI_GAP_LDS], lo[FI_GAP_LDS];
 };
 // (an anchor op is in the gap iff its own gap key is the gap's; its place
 // there is its rank among the gap's ops, which are in batch order)
@@ -880,7 +886,8 @@ __device__ __forceinline__ void fi_gap_one(uint32_t k, uint32_t m, const uint32_
                                            uint32_t* nxt, uint32_t* ord, uint32_t* first, uint32_t* fi,
                                            FiGapLds& L) {
   long long* lk = L.lk;
-  uint32_t *la = L.la, *ln = L.ln, *lo = L.lo;
+  unsigned long long* le = L.le;
+  uint32_t *la = L.la, *lo = L.lo;
   const uint32_t lane = threadIdx.x;
   const uint32_t g = gk[k];
   uint32_t e = k + 1;  // the gap's end: 64 positions per step
@@ -926,21 +933,29 @@ __device__ __forceinline__ void fi_gap_one(uint32_t k, uint32_t m, const uint32_
     }
     __syncthreads();
     if (lane == 0) {
-      uint32_t head = NONE;
+      unsigned long long hd = FI_LE_NONE;  // the head's entry (its key << 11 | index)
+      long long x = lk[0];
+      uint32_t a = la[0];
       for (uint32_t j = 0; j < n; ++j) {
-        const long long x = lk[j];
-        uint32_t cur = la[j];  // NONE = the head
-        uint32_t nx = cur == NONE ? head : ln[cur];
-        while (nx != NONE && lk[nx] > x) {
-          cur = nx;
-          nx = ln[cur];
+        const long long xn = j + 1 < n ? lk[j + 1] : 0;  // (the next op's, in flight)
+        const uint32_t an = j + 1 < n ? la[j + 1] : NONE;
+        uint32_t cur = a;  // NONE = the head
+        unsigned long long e = cur == NONE ? hd : le[cur];
+        while ((e & FI_LE_NONE) != FI_LE_NONE && static_cast<long long>(e >> 11) > x) {
+          cur = static_cast<uint32_t>(e & FI_LE_NONE);
+          e = le[cur];
         }
-        ln[j] = nx;
-        if (cur == NONE) head = j;
-        else ln[cur] = j;
+        le[j] = e;
+        const unsigned long long me = (static_cast<unsigned long long>(x) << 11) | j;
+        if (cur == NONE) hd = me;
+        else le[cur] = me;
+        x = xn;
+        a = an;
       }
       uint32_t o = 0;
-      for (uint32_t j = head; j != NONE; j = ln[j]) lo[j] = o++;
+      for (uint32_t j = static_cast<uint32_t>(hd & FI_LE_NONE); j != FI_LE_NONE;
+           j = static_cast<uint32_t>(le[j] & FI_LE_NONE))
+        lo[j] = o++;
     }
     __syncthreads();
     for (uint32_t j = lane; j < n; j += 64) {
@@ -1276,7 +1291,11 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   const uint32_t gm = (m + BLOCK - 1) / BLOCK;  // one item per thread
   // (the gap heads and the anchors' places are found by k_fi_gaps itself:
   // one launch fewer than a separate pass listing them)
-  LAUNCH(k_fi_gaps, dim3(std::min(m, FI_GAPS_GRID)), dim3(64), 0, s, m, sk, sv, gk[0], par0, o.ts, nxt, ord, first,
+  static const uint32_t gaps_grid = [] {  // (env CRDTM_GAPS_GRID: A/B)
+    const char* e = getenv("CRDTM_GAPS_GRID");
+    return e ? std::max(1, atoi(e)) : static_cast<int>(FI_GAPS_GRID);
+  }();
+  LAUNCH(k_fi_gaps, dim3(std::min(m, static_cast<uint32_t>(gaps_grid))), dim3(64), 0, s, m, sk, sv, gk[0], par0, o.ts, nxt, ord, first,
          fi);
   LAUNCH(k_fi_tblk, dim3(gm), dim3(BLOCK), 0, s, m, nbk, sk, ord, X.bent, X.bcnt, X.bfirst, X.bend, tl, gpred, fi);
   LAUNCH(k_fi_win_pick, dim3(grid_for(64ULL * m)), dim3(BLOCK), 0, s, nbk, sk, tl, X.bcnt, X.bfirst, X.bend, X.bwin,
