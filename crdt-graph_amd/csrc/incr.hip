@@ -868,6 +868,7 @@ struct FiGapLds {
   long long lk[FI_GAP_LDS];
   unsigned long long le[FI_GAP_LDS];
   uint32_t la[FI_GAP_LDS], lo[FI_GAP_LDS];
+  uint16_t fc[FI_GAP_LDS + 2];  // (the tour: first child per op, the gap's head list at [n])
 };
 // (an anchor op is in the gap iff its own gap key is the gap's; its place
 // there is its rank among the gap's ops, which are in batch order)
@@ -879,6 +880,121 @@ __device__ __forceinline__ uint32_t fi_rank_of(const uint32_t* v, uint32_t n, ui
     else hi = mid;
   }
   return lo;
+}
+
+// A gap whose every anchor inside it has a smaller key than its op (keys
+// grow along the anchors, as Lamport timestamps do) is its ops' tree in DFS
+// order, children by descending key: the replay's walk from an anchor passes
+// exactly the subtrees of the anchor's children with larger keys (their
+// descendants' keys are larger still) and stops at the first smaller key,
+// which is the next child, or an uncle's, whose key is below the anchor's. So
+// the order comes without the serial replay: the children grouped by anchor
+// and sorted by key (a bitonic network over (anchor << 53 | ~key) words), an
+// Euler tour through them, and the tour ranked by pointer jumping; the rank of
+// op v is n - (the enters from v's on). One wave, in LDS (the workgroup is
+// the wave: its LDS accesses are in program order). Returns false, having
+// written nothing, when some anchor's key is not below its op's.
+constexpr uint32_t FI_TOUR_MIN = 24;  // (smaller gaps: the serial replay)
+constexpr uint16_t FI_T_NONE = 0xFFFFu;
+__device__ bool fi_gap_tour(uint32_t n, FiGapLds& L) {
+  const uint32_t lane = threadIdx.x;
+  long long* lk = L.lk;
+  uint32_t* la = L.la;
+  constexpr unsigned long long KM = (1ULL << 53) - 1ULL;
+  bool bad = false;
+  for (uint32_t j = lane; j < n; j += 64) {
+    const uint32_t a = la[j];
+    const long long x = lk[j];
+    if (x <= 0 || x > static_cast<long long>(KM) || (a != NONE && !(x > lk[a]))) bad = true;
+  }
+  if (__ballot(bad)) return false;
+  // children sorted: (anchor, descending key) words, the op alongside
+  unsigned long long* c = L.le;
+  uint16_t* sp = reinterpret_cast<uint16_t*>(L.lo);  // [FI_GAP_LDS] sorted ops
+  uint16_t* ns = sp + FI_GAP_LDS;                    // [FI_GAP_LDS] next sibling
+  uint16_t* fc = L.fc;
+  uint32_t N2 = 2;
+  while (N2 < n) N2 <<= 1;
+  for (uint32_t j = lane; j < N2; j += 64) {
+    if (j < n) {
+      const uint32_t a = la[j];
+      c[j] = (static_cast<unsigned long long>(a == NONE ? 0x7FFu : a) << 53) | (KM - static_cast<unsigned long long>(lk[j]));
+      sp[j] = static_cast<uint16_t>(j);
+    } else {
+      c[j] = ~0ULL;
+      sp[j] = FI_T_NONE;
+    }
+  }
+  for (uint32_t k = 2; k <= N2; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t t = lane; t < N2 / 2; t += 64) {
+        const uint32_t i = 2 * t - (t & (j - 1)), q = i + j;
+        const unsigned long long x = c[i], y = c[q];
+        if ((x > y) == !(i & k)) {
+          c[i] = y;
+          c[q] = x;
+          const uint16_t u = sp[i];
+          sp[i] = sp[q];
+          sp[q] = u;
+        }
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  // first child per anchor (the head list at n), next sibling per op
+  for (uint32_t v = lane; v <= n; v += 64) fc[v] = FI_T_NONE;
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t p = lane; p < n; p += 64) {
+    const uint32_t P = static_cast<uint32_t>(c[p] >> 53), u = sp[p];
+    const uint32_t Pp = p ? static_cast<uint32_t>(c[p - 1] >> 53) : 0xFFFFFFFFu;
+    const uint32_t Pn = p + 1 < n ? static_cast<uint32_t>(c[p + 1] >> 53) : 0xFFFFFFFFu;
+    if (Pp != P) fc[P == 0x7FFu ? n : P] = static_cast<uint16_t>(u);
+    ns[u] = Pn == P ? sp[p + 1] : FI_T_NONE;
+  }
+  __builtin_amdgcn_wave_barrier();
+  // the tour: enter(v) = v (weight 1), exit(v) = n + v (weight 0)
+  uint16_t* tn = reinterpret_cast<uint16_t*>(lk);  // [2 FI_GAP_LDS] successor
+  uint16_t* tv = tn + 2 * FI_GAP_LDS;              // [2 FI_GAP_LDS] enters from here to the end
+  for (uint32_t v = lane; v < n; v += 64) {
+    const uint32_t f = fc[v], s = ns[v], a = la[v];
+    tn[v] = static_cast<uint16_t>(f != FI_T_NONE ? f : n + v);
+    tv[v] = 1;
+    tn[n + v] = static_cast<uint16_t>(s != FI_T_NONE ? s : (a == NONE ? FI_T_NONE : n + a));
+    tv[n + v] = 0;
+  }
+  for (;;) {  // (pointer jumping: every pair is read before any is written)
+    bool moved = false;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t x0 = lane; x0 < 2 * n; x0 += 64 * 8) {
+      uint32_t y[8], ny[8], vy[8];
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) {
+        const uint32_t x = x0 + 64 * u;
+        y[u] = x < 2 * n ? tn[x] : FI_T_NONE;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) {
+        ny[u] = y[u] != FI_T_NONE ? tn[y[u]] : FI_T_NONE;
+        vy[u] = y[u] != FI_T_NONE ? tv[y[u]] : 0u;
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) {
+        const uint32_t x = x0 + 64 * u;
+        if (y[u] != FI_T_NONE) {
+          tv[x] = static_cast<uint16_t>(tv[x] + vy[u]);
+          tn[x] = static_cast<uint16_t>(ny[u]);
+          moved = true;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (!__ballot(moved)) break;
+  }
+  // the order: n - (the enters from v's enter on)
+  for (uint32_t v = lane; v < n; v += 64) L.la[v] = n - tv[v];
+  return true;
 }
 
 __device__ __forceinline__ void fi_gap_one(uint32_t k, uint32_t m, const uint32_t* gk, const uint32_t* gv,
@@ -932,6 +1048,14 @@ __device__ __forceinline__ void fi_gap_one(uint32_t k, uint32_t m, const uint32_
       }
     }
     __syncthreads();
+    if (n >= FI_TOUR_MIN && fi_gap_tour(n, L)) {
+      __syncthreads();
+      for (uint32_t j = lane; j < n; j += 64) {
+        ord[k + j] = la[j];
+        first[k + j] = k;
+      }
+      return;
+    }
     if (lane == 0) {
       unsigned long long hd = FI_LE_NONE;  // the head's entry (its key << 11 | index)
       long long x = lk[0];
