@@ -245,16 +245,26 @@ __global__ void __launch_bounds__(BLOCK) k_fi_resolve(OpsDev o, TsHash kx, TsHas
     const long long ts = o.ts[i];
     const uint32_t b = o.off[i];
     uint32_t p = NONE, s = 0;
-    if (o.kind[i] != CRDTM_ADD || o.off[i + 1] != b + 1 || ts <= 0 || ts >= TWO53 || tshash_find(kx, ts) != NONE) {
+    // (the three probes' first slots load together: the key's in the base,
+    // the anchor's in the base and in the batch)
+    const long long a = o.path[b];
+    const bool ka = a > 0 && a < TWO53;
+    const unsigned long long hk = static_cast<unsigned long long>(ts) ^ 0x8000000000000000ULL;
+    const unsigned long long ha = static_cast<unsigned long long>(a) ^ 0x8000000000000000ULL;
+    const uint32_t p1 = static_cast<uint32_t>(mix64(hk)) & kx.mask;
+    const uint32_t p2 = static_cast<uint32_t>(mix64(ha)) & kx.mask;
+    const uint32_t p3 = static_cast<uint32_t>(mix64(ha)) & bh.mask;
+    const unsigned long long f1 = kx.keys[p1], f2 = ka ? kx.keys[p2] : 0ULL, f3 = ka ? bh.keys[p3] : 0ULL;
+    if (o.kind[i] != CRDTM_ADD || o.off[i + 1] != b + 1 || ts <= 0 || ts >= TWO53 ||
+        tshash_find_from(kx, hk, p1, f1) != NONE) {
       fail = 1;
     } else {
-      const long long a = o.path[b];
       if (a != 0) {
-        const uint32_t sl = (a > 0 && a < TWO53) ? tshash_find(kx, a) : NONE;
+        const uint32_t sl = ka ? tshash_find_from(kx, ha, p2, f2) : NONE;
         if (sl != NONE) {
           s = rank_of[sl] + 1;
         } else {
-          const uint32_t j = (a > 0 && a < TWO53) ? tshash_find(bh, a) : NONE;
+          const uint32_t j = ka ? tshash_find_from(bh, ha, p3, f3) : NONE;
           if (j == NONE || j >= i) fail = 1;  // NotFound (or not yet applied): the general paths decide
           else p = j;
         }

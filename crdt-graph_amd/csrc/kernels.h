@@ -92,6 +92,17 @@ __device__ __forceinline__ void tshash_insert(TsHash h, int64_t ts, uint32_t idx
   }
 }
 
+// the same from a first slot p whose key kk the caller has loaded (k: the
+// stored form of the timestamp, ts ^ 2^63)
+__device__ __forceinline__ uint32_t tshash_find_from(TsHash h, unsigned long long k, uint32_t p,
+                                                     unsigned long long kk) {
+  for (;;) {
+    if (kk == k) return h.vals[p];
+    if (kk == 0ULL) return NONE;
+    p = (p + 1) & h.mask;
+    kk = h.keys[p];
+  }
+}
 __device__ __forceinline__ uint32_t tshash_find(TsHash h, int64_t ts) {
   const unsigned long long k = static_cast<unsigned long long>(ts) ^ 0x8000000000000000ULL;
   uint32_t p = static_cast<uint32_t>(mix64(k)) & h.mask;
