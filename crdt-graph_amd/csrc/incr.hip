@@ -406,13 +406,14 @@ __global__ void __launch_bounds__(FI_JUMP_THREADS) k_fi_jump_lds(uint32_t m, uin
   }
 }
 
-// The same over many workgroups in two launches (anchors are earlier ops:
+// The same over many workgroups (anchors are earlier ops:
 // par[i] < i). Each chunk of FI_JC ops jumps in LDS along the pointers that
 // stay inside it; an op whose chain ends at a root of its chunk is final
 // there, one whose chain leaves the chunk (at e, whose anchor is an earlier
 // chunk's op) keeps jx = par[e] and jm = the chain's minimum up to e. Then
 // each such op follows jx from chunk to chunk (at most one hop per earlier
-// chunk) to a final op: its start, and the minimum over the hops.
+// chunk) to a final op: its start, and the minimum over the hops — done by
+// k_fi_gap's wave for the op before its search.
 constexpr uint32_t FI_JC = 1024;
 __global__ void __launch_bounds__(FI_JC) k_fi_jump_chunk(uint32_t m, const uint32_t* P, uint32_t* S, long long* T,
                                                          uint32_t* jx, long long* jm) {
@@ -470,34 +471,36 @@ __global__ void __launch_bounds__(FI_JC) k_fi_jump_chunk(uint32_t m, const uint3
   jm[i] = mm;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_fi_jump_fix(uint32_t m, const uint32_t* jx, const long long* jm,
-                                                       uint32_t* S, long long* T) {
-  GRID_STRIDE(i, m) {
-    uint32_t x = jx[i];
-    if (x == NONE) continue;  // (final: a root, or resolved inside its chunk)
-    long long v = jm[i];
-    for (;;) {  // (an earlier chunk's op per hop)
-      v = min(v, jm[x]);
-      const uint32_t y = jx[x];
-      if (y == NONE) break;
-      x = y;
-    }
-    S[i] = S[x];
-    T[i] = v;
-  }
-}
-
-// g = NSR(start, thr) over the base keys, one wave per query: 64 keys, 64
-// block minima or 64 superblock minima per step (ballot), then down again
+// (jx: the chunked pointer jumping's hops first, k_fi_jump_fix's work for
+// this op, so it needs no launch of its own)
 __global__ void __launch_bounds__(BLOCK) k_fi_gap(uint32_t m, uint32_t K, const long long* dk, const long long* bmin,
-                                                  const long long* smin, const long long* tmin, const uint32_t* start,
-                                                  const long long* thr, uint32_t* gkey, uint32_t* gval) {
+                                                  const long long* smin, const long long* tmin, uint32_t* start,
+                                                  long long* thr, uint32_t* gkey, uint32_t* gval, const uint32_t* jx,
+                                                  const long long* jm) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t nb = (K + FI_BLK - 1) / FI_BLK, ns = (nb + FI_SUP - 1) / FI_SUP, nt = (ns + FI_SUP - 1) / FI_SUP;
   const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / 64;
   if (i >= m) return;  // (wave-uniform)
-  const long long t = thr[i];
-  const uint32_t r = start[i];
+  long long t;
+  uint32_t r;
+  uint32_t x = jx ? jx[i] : NONE;
+  if (x != NONE) {  // (hops to a final op: an earlier chunk's per hop)
+    t = jm[i];
+    for (;;) {
+      t = min(t, jm[x]);
+      const uint32_t y = jx[x];
+      if (y == NONE) break;
+      x = y;
+    }
+    r = start[x];
+    if (lane == 0) {
+      start[i] = r;
+      thr[i] = t;
+    }
+  } else {
+    t = thr[i];
+    r = start[i];
+  }
   // first index >= from in [lo, hi) (64 wide, starting at lo) whose value is < t
   auto first64 = [&](const long long* v, uint32_t lo, uint32_t from, uint32_t hi) -> uint32_t {
     const uint32_t q = lo + lane;
@@ -1395,7 +1398,6 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   if (rounds && jump_chunks) {
     const uint32_t nch = (m + FI_JC - 1) / FI_JC;
     LAUNCH(k_fi_jump_chunk, dim3(nch), dim3(FI_JC), 0, s, m, par[0], sta[0], thr[0], jx, jm);
-    LAUNCH(k_fi_jump_fix, dim3(grid_for(m)), dim3(BLOCK), 0, s, m, jx, jm, sta[0], thr[0]);
   } else if (rounds && jump_lds && m <= FI_JUMP_LDS_MAX)
     LAUNCH(k_fi_jump_lds, dim3(1), dim3(FI_JUMP_THREADS), static_cast<size_t>(m) * 10, s, m, rounds, par[0], sta[0],
            thr[0]);
@@ -1405,7 +1407,7 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   // each -- 0.65 ms more per 100 batches: a query's long search held up the
   // wave's other three)
   LAUNCH(k_fi_gap, dim3(grid_for(64ULL * m)), dim3(BLOCK), 0, s, m, Kp, X.bdk, X.bmin, X.smin, X.tmin, sta[0],
-         thr[0], gk[0], gv[0]);
+         thr[0], gk[0], gv[0], (rounds && jump_chunks) ? jx : nullptr, jm);
   static const char* dump = getenv("CRDTM_FI_DUMP_KEYS");  // (debug: one batch's gap keys, for tools/xbench_sort.py)
   if (dump && *dump) {
     std::vector<uint32_t> hk(m);
