@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 
 #include "engine.h"
@@ -1134,4 +1135,29 @@ extern "C" __attribute__((visibility("default"))) int crdtm_xbench_sort_small(co
     hipLaunchKernelGGL(crdtm::k_rs_small, dim3(1), dim3(crdtm::RS_SMALL_T), crdtm::RS_SMALL_LDS, s, kin, vin, n,
                        bits, kout, vout);
   return hipGetLastError() == hipSuccess ? CRDTM_OK : CRDTM_E_HIP;
+}
+
+// Kernel microbenchmark hook: host microseconds per launch of an empty
+// kernel on `stream` (nullptr: a stream of its own), n launches after 100
+// warm-up ones.
+namespace crdtm {
+__global__ void k_xbench_null(uint32_t x, uint32_t* out) {
+  if (x == 0xFFFFFFFFu && threadIdx.x == 0) *out = x;
+}
+}  // namespace crdtm
+extern "C" __attribute__((visibility("default"))) double crdtm_xbench_launch(void* stream, int n) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  bool own = false;
+  if (!s) {
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -1.0;
+    own = true;
+  }
+  for (int i = 0; i < 100; ++i) hipLaunchKernelGGL(crdtm::k_xbench_null, dim3(64), dim3(256), 0, s, 0u, nullptr);
+  if (hipStreamSynchronize(s) != hipSuccess) return -1.0;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < n; ++i) hipLaunchKernelGGL(crdtm::k_xbench_null, dim3(64), dim3(256), 0, s, 0u, nullptr);
+  const auto t1 = std::chrono::steady_clock::now();
+  hipStreamSynchronize(s);
+  if (own) hipStreamDestroy(s);
+  return std::chrono::duration<double, std::micro>(t1 - t0).count() / n;
 }
