@@ -59,7 +59,6 @@ struct DevResult {
   uint32_t own_ok_adds;     // Ok adds with replicaId(ts) == tree id (timestamp bumps)
   uint32_t n_replica_out;
   uint32_t n_rep_list;      // replicas touched by a commit's fold (k_rep_max)
-  uint32_t rep_done;        // k_rep_max workgroups finished (the last writes the output)
   uint32_t n_nodes_kept;    // closed form: nodes that survive (dict alive)
   uint32_t n_live_kept;     // kept nodes that own a children dict
   uint32_t n_sentinels;     // present sentinels (Euler)

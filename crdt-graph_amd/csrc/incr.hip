@@ -186,7 +186,6 @@ __global__ void __launch_bounds__(BLOCK) k_fi_clear(unsigned long long* keys, ui
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // (the replicas fold's counters, for the commit's fold)
     dres->n_replica_out = 0;
     dres->n_rep_list = 0;
-    dres->rep_done = 0;
   }
 }
 

@@ -1285,15 +1285,9 @@ __device__ __forceinline__ void rep_publish(uint32_t* rv, uint32_t* rtab, uint32
     rlist[atomicAdd(rcount, 1u)] = rl;
   }
 }
-// (the workgroup that finishes last also writes the output, k_rep_out's
-// loop: the touched replicas' winners, the table entries cleared)
-__device__ void rep_out_loop(OpsDev o, uint32_t* rtab, const uint32_t* rlist, uint32_t nr, uint32_t t0, uint32_t ts,
-                             long long* out, uint32_t* n_out, long long* inl);
 __global__ void __launch_bounds__(BLOCK) k_rep_max(OpsDev o, const uint8_t* st, uint32_t* rtab, uint32_t* rlist,
-                                                   uint32_t* rcount, uint32_t per, uint32_t* done, long long* out,
-                                                   uint32_t* n_out, long long* inl) {
+                                                   uint32_t* rcount, uint32_t per) {
   __shared__ uint32_t rv[REP_DIRECT];
-  __shared__ uint32_t s_last;
   for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) rv[j] = 0;
   __syncthreads();
   const uint32_t n = o.n;
@@ -1334,25 +1328,19 @@ __global__ void __launch_bounds__(BLOCK) k_rep_max(OpsDev o, const uint8_t* st, 
   mr = block_max(mr);  // (synchronises the block) only ids <= mr were touched
   for (uint32_t j = threadIdx.x; j <= mr; j += blockDim.x)
     if (rv[j] && atomicMax(&rtab[j + OFF], rv[j]) == 0) rlist[atomicAdd(rcount, 1u)] = j + OFF;
-  __threadfence();  // (this workgroup's table and list writes before its arrival)
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  const uint32_t nr = __hip_atomic_load(rcount, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-  rep_out_loop(o, rtab, rlist, nr, threadIdx.x, blockDim.x, out, n_out, inl);
 }
 
 inline uint32_t rep_grid(uint32_t n) { return grid_for(n, BLOCK * rep_per(n)); }
 
 // One thread per touched replica: the winner is op rtab[r] - 1; the entry is
 // cleared (the table stays clean between calls).
-__device__ void rep_out_loop(OpsDev o, uint32_t* rtab, const uint32_t* rlist, uint32_t nr, uint32_t t0, uint32_t ts,
-                             long long* out, uint32_t* n_out, long long* inl) {
-  for (uint32_t k = t0; k < nr; k += ts) {
-    const uint32_t r = __hip_atomic_load(&rlist[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t i = __hip_atomic_load(&rtab[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1;
+__global__ void __launch_bounds__(BLOCK) k_rep_out(OpsDev o, uint32_t* rtab, const uint32_t* rlist,
+                                                   const uint32_t* rcount, long long* out, uint32_t* n_out,
+                                                   long long* inl) {
+  const uint32_t nr = *rcount;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nr; k += gridDim.x * blockDim.x) {
+    const uint32_t r = rlist[k];
+    const uint32_t i = rtab[r] - 1;
     rtab[r] = 0;
     const long long t = op_t(o, i);
     out[2 * k] = replica_of(t);
@@ -3064,9 +3052,8 @@ __global__ void __launch_bounds__(BLOCK) k_post_flags(OpsDev o, const uint8_t* s
 
 // replicas[replicaId t] := t, last writer wins, over the applied ops: fold
 // into c->rtab, collect the touched replicas into `rep` (+ the inline copy).
-static_assert(offsetof(DevResult, n_rep_list) == offsetof(DevResult, n_replica_out) + sizeof(uint32_t) &&
-                  offsetof(DevResult, rep_done) == offsetof(DevResult, n_rep_list) + sizeof(uint32_t),
-              "one memset clears the three counters");
+static_assert(offsetof(DevResult, n_rep_list) == offsetof(DevResult, n_replica_out) + sizeof(uint32_t),
+              "one memset clears both counters");
 int replica_fold(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long long* rep, Arena& ws, hipStream_t s,
                  bool zeroed) {
   uint32_t* rlist = ws.alloc<uint32_t>(std::min<uint64_t>(o.n, REPLICA_SLOTS) + 1);
@@ -3078,10 +3065,10 @@ int replica_fold_into(crdtm_ctx* c, const OpsDev& o, const uint8_t* st, long lon
                       hipStream_t s, bool zeroed) {
   DevResult* dr = c->dres;
   const uint32_t n = o.n;
-  // (n_replica_out, n_rep_list, rep_done)
-  if (!zeroed) HIP_CHECK(hipMemsetAsync(&dr->n_replica_out, 0, 3 * sizeof(uint32_t), s));
-  LAUNCH(k_rep_max, dim3(rep_grid(n)), dim3(BLOCK), 0, s, o, st, c->rtab, rlist, &dr->n_rep_list, rep_per(n),
-         &dr->rep_done, rep, &dr->n_replica_out, dr->rep_inline);
+  if (!zeroed) HIP_CHECK(hipMemsetAsync(&dr->n_replica_out, 0, 2 * sizeof(uint32_t), s));  // n_replica_out, n_rep_list
+  LAUNCH(k_rep_max, dim3(rep_grid(n)), dim3(BLOCK), 0, s, o, st, c->rtab, rlist, &dr->n_rep_list, rep_per(n));
+  LAUNCH(k_rep_out, dim3(64), dim3(BLOCK), 0, s, o, c->rtab, rlist, &dr->n_rep_list, rep, &dr->n_replica_out,
+         dr->rep_inline);
   return CRDTM_OK;
 }
 
