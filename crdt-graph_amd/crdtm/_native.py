@@ -21,6 +21,7 @@ FLAG_REMERGE = 1  # non-fresh tree merged as init ++ log ++ batch on the paralle
 FLAG_INCREMENTAL = 2  # adds-only batch merged into a clean flat document in place (incr.hip)
 FLAG_INCR_WINDOWS = 4  # ... and blocks of its gapped order were spread over rebalance windows
 FLAG_INCR_DENSE = 8  # ... and no window could take it: merged densely, the blocks rebuilt
+FLAG_INCR_TOUR = 32  # ... and some gap was ordered as its tree's DFS (keys growing along its anchors)
 FLAG_DICT_INCR = 16  # non-fresh tree: replayed per children dict on the state itself, level by level (ilr.hip)
 REF_NONE = 2 ** 64 - 1
 REF_ROOT = 2 ** 64 - 2

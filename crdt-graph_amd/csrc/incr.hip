@@ -63,7 +63,8 @@ constexpr uint32_t FI_WIN_THREADS = 1024;
 // FG_SPARSE = the blocks the batch lands in are rewritten; FG_DENSE = the
 // batch's nodes and log are committed, the order is merged densely by the
 // host after the result read), fi[7] k_fi_win_list's workgroups done
-enum : uint32_t { FI_FAIL = 1u, FI_BUDGET = 2u, FI_OVER = 4u, FI_REPLICA = 8u };
+// (FI_TOUR: some gap was ordered by its Euler tour -- reported, decides nothing)
+enum : uint32_t { FI_FAIL = 1u, FI_BUDGET = 2u, FI_OVER = 4u, FI_REPLICA = 8u, FI_TOUR = 16u };
 enum : uint32_t { FG_NONE = 0u, FG_SPARSE = 1u, FG_DENSE = 2u };
 constexpr uint32_t FI_COMMIT_GRID = 1024;  // (grid-stride commit kernels: sized before the counts are known)
 constexpr uint32_t FI_WORDS = 8;
@@ -1062,6 +1063,7 @@ __device__ __forceinline__ void fi_gap_one(uint32_t k, uint32_t m, const uint32_
     }
     __syncthreads();
     if (n >= FI_TOUR_MIN && fi_gap_tour(n, L)) {
+      if (lane == 0) atomicOr(&fi[0], FI_TOUR);
       __syncthreads();
       for (uint32_t j = lane; j < n; j += 64) {
         ord[k + j] = la[j];
@@ -1517,7 +1519,7 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   t->flat_clean = true;
   res->path_taken = CRDTM_PATH_CLOSED_FORM;
   res->flags |= CRDTM_FLAG_INCREMENTAL | (dense ? CRDTM_FLAG_INCR_DENSE : 0u) |
-                (!dense && hf[5] ? CRDTM_FLAG_INCR_WINDOWS : 0u);
+                (!dense && hf[5] ? CRDTM_FLAG_INCR_WINDOWS : 0u) | ((hf[0] & FI_TOUR) ? CRDTM_FLAG_INCR_TOUR : 0u);
   res->n_applied = m;
   res->n_already = 0;
   *handled = true;

@@ -94,6 +94,8 @@ typedef struct crdtm_result {
 #define CRDTM_FLAG_INCR_DENSE 8   /* with INCREMENTAL: no window could take the batch: dense merge, rebuilt */
 #define CRDTM_FLAG_DICT_INCR 16   /* non-fresh tree: the batch replayed per children dict on the state itself,
                                      level by level (only the dicts it reaches; ilr.hip) */
+#define CRDTM_FLAG_INCR_TOUR 32   /* with INCREMENTAL: some gap's new nodes were ordered as their tree's DFS
+                                     (keys growing along its anchors) instead of replayed one by one */
 
 typedef struct crdtm_ctx crdtm_ctx;   /* device + stream + workspace */
 typedef struct crdtm_tree crdtm_tree; /* one replica's CRDTree state, resident in HBM */

@@ -184,7 +184,7 @@ def test_incremental_flat_closed_form(name, monkeypatch):
         cuts.append(min(n, cuts[-1] + int(rng.choice([1, 2, 64, 1000, 5000, 16000]))))
     ot = olib().orc_init(0)
     et = CRDTree.init(0)
-    used = windows = dense = 0
+    used = windows = dense = tour = 0
     for k, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
         chunk = sub(s, a, b)
         _, rc, _ = oracle_apply_arrays(chunk, b - a, tree=ot)
@@ -193,6 +193,7 @@ def test_incremental_flat_closed_form(name, monkeypatch):
         used += bool(res.flags & N.FLAG_INCREMENTAL)
         windows += bool(res.flags & N.FLAG_INCR_WINDOWS)
         dense += bool(res.flags & N.FLAG_INCR_DENSE)
+        tour += bool(res.flags & N.FLAG_INCR_TOUR)
         if k % 7 == 0 or b == n:
             assert engine_summary(et) == oracle_summary(ot), (k, a, b)
             assert engine_log(et, 1) == oracle_log(ot, 1), k
@@ -205,6 +206,8 @@ def test_incremental_flat_closed_form(name, monkeypatch):
     assert used == len(cuts) - 2
     if name == "r1_cursor":  # one hot gap: the windows and the dense merge both ran
         assert windows and dense, (windows, dense)
+    if name in ("r2_w1", "r3_hot"):  # (typing runs: gaps in key order, ordered by their tree's DFS)
+        assert tour, name
     assert engine_log(et, 0) == oracle_log(ot, 0)
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
     # a Delete makes the document unclean: no incremental closed form afterwards
