@@ -2138,8 +2138,8 @@ __global__ void k_fl_stat_reset(DevResult* d) {
 // replicas[r] := ts of replica r's last applied Add (flat: Adds only, ids in
 // [0, max_replica]); clears the table entries it reads, and (rng_clear, the
 // merge's last launch before its result read) the replica range entries.
-__global__ void __launch_bounds__(BLOCK) k_fl_rep_collect(OpsDev o, uint32_t nr, uint32_t* rtab, long long* out,
-                                                          uint32_t* n_out, long long* inl, uint2* rng_clear) {
+__device__ __forceinline__ void fl_rep_collect(OpsDev o, uint32_t nr, uint32_t* rtab, long long* out,
+                                               uint32_t* n_out, long long* inl, uint2* rng_clear) {
   GRID_STRIDE(r, nr) {
     if (rng_clear) rng_clear[r] = make_uint2(NONE, 0u);
     uint32_t* e = &rtab[r + (1u << (REPLICA_BITS - 1))];
@@ -2156,6 +2156,20 @@ __global__ void __launch_bounds__(BLOCK) k_fl_rep_collect(OpsDev o, uint32_t nr,
     }
   }
 }
+__global__ void __launch_bounds__(BLOCK) k_fl_rep_collect(OpsDev o, uint32_t nr, uint32_t* rtab, long long* out,
+                                                          uint32_t* n_out, long long* inl, uint2* rng_clear) {
+  fl_rep_collect(o, nr, rtab, out, n_out, inl, rng_clear);
+}
+// (the collection's arguments, when it rides on k_fl_next)
+struct RepCollect {
+  OpsDev o;
+  uint32_t nr;
+  uint32_t* rtab;
+  long long* out;
+  uint32_t* n_out;
+  long long* inl;
+  uint2* rng_clear;
+};
 
 // Runs. A run is a maximal slot interval [h, e) whose every slot but h is
 // anchored at the slot before it (a replica's typing run: consecutive
@@ -2347,7 +2361,9 @@ __global__ void __launch_bounds__(BLOCK) k_run_mask(FlatRec fr, uint32_t Q, unsi
 // missing anchor reads as the sentinel so that the speculative walks stay in
 // bounds), hh[r] = {head, anchor}; k_run_ep replaces the anchor by the
 // head's effective parent.
-__global__ void __launch_bounds__(BLOCK) k_run_heads(FlatRec fr, uint32_t Q, RunMask rm, uint2* hh) {
+// (hasch: every run's has-a-child flag cleared, for k_run_ep to set)
+__global__ void __launch_bounds__(BLOCK) k_run_heads(FlatRec fr, uint32_t Q, RunMask rm, uint2* hh,
+                                                     uint8_t* hasch) {
   Q = fr.q(Q);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t nw = (Q + 63) >> 6;
@@ -2371,7 +2387,9 @@ __global__ void __launch_bounds__(BLOCK) k_run_heads(FlatRec fr, uint32_t Q, Run
         a = fr.anchor(x[u]);
         if (a == NONE) a = Q;
       }
-      hh[b[u] + static_cast<uint32_t>(__popcll(m[u] & lt))] = make_uint2(((w0 + u) << 6) + lane, a);
+      const uint32_t r = b[u] + static_cast<uint32_t>(__popcll(m[u] & lt));
+      hh[r] = make_uint2(((w0 + u) << 6) + lane, a);
+      if (hasch) hasch[r] = 0;
     }
   }
 }
@@ -2471,7 +2489,11 @@ struct FlatDocSink {
 // (The flat speculation may run this over more ranks than slots when its
 // guess fails: entries past the document are then stale, and `cap` keeps
 // the stores inside the slot arrays; the result is discarded.)
-__global__ void __launch_bounds__(BLOCK) k_fl_next(uint32_t K, const uint32_t* doc, TreeDev T, uint64_t cap) {
+// (rc.nr > 0: the replicas collection of the merge's end, k_fl_rep_collect,
+// rides on this launch)
+__global__ void __launch_bounds__(BLOCK) k_fl_next(uint32_t K, const uint32_t* doc, TreeDev T, uint64_t cap,
+                                                   RepCollect rc) {
+  if (rc.nr) fl_rep_collect(rc.o, rc.nr, rc.rtab, rc.out, rc.n_out, rc.inl, rc.rng_clear);
   GRID_STRIDE(r, K) {
     const uint32_t d = doc[r];
     if (d < cap) T.s_next[d] = r + 1 < K ? doc[r + 1] : NONE;
@@ -2562,6 +2584,7 @@ struct RunArr {
   uint32_t* tk;              // subtree sizes in sorted order (k_run_tree_up writes T(r) at kinv[r])
   const uint32_t* kinv;      // run -> its position in the sorted order
   uint32_t* posh;            // document rank of the head
+  uint8_t* hasch = nullptr;  // run -> 1 when some run is its child (k_run_sizes: leaves)
 };
 
 #define RUN_LOOP(r) for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x, nr_ = *a.nR; r < nr_; r += gridDim.x * blockDim.x)
@@ -2642,7 +2665,9 @@ __global__ void __launch_bounds__(BLOCK) k_run_ep(RunArr a, uint32_t Q, RunMask 
     // later index stays in range; a batch that reaches the commit after its
     // statuses has every anchor present)
     // (len: a hole after the run is a run of its own)
-    a.rr[r] = make_uint4(d == Q ? NONE : run_of(rm, d), hn - x, NONE, 0u);
+    const uint32_t P = d == Q ? NONE : run_of(rm, d);
+    a.rr[r] = make_uint4(P, hn - x, NONE, 0u);
+    if (a.hasch && P != NONE) a.hasch[P] = 1;  // (the same value from every child: plain stores)
     a.ca[r] = 0;
     skey[R - 1 - r] = d;
     sval[R - 1 - r] = r;
@@ -2719,6 +2744,149 @@ __global__ void __launch_bounds__(BLOCK) k_run_tree_up(RunArr a, const uint32_t*
       if (static_cast<uint32_t>(old >> 32) + static_cast<uint32_t>(v >> 32) == e.w - e.z)
         run_climb(a, key, e, e.y + static_cast<uint32_t>(old) + static_cast<uint32_t>(v));
     }
+  }
+}
+
+// Round 6: the subtree sizes and the child-run ranges in one launch, and the
+// offsets w by a segmented scan (k_run_gstart and k_run_w gone). Per sorted
+// position k (a child run c attached at slot p of parent run P, or a root
+// sentinel child):
+//  * the ends of each parent's child range [z, w) come from the neighbours'
+//    parents (lanes of one wave hold consecutive positions), written into
+//    rr[P].z / .w for the expansion;
+//  * offk[k] = SEGF when k starts a parent's range | (p - head(P) + 1), the
+//    part of w(c) before the sibling subtrees (0 for root children);
+//  * completion without child counts: P's counter (ca, high half) receives
+//    +1 per child that arrives (leaves in this pass, inner runs when their
+//    own subtree completes), +z from the lane at z and -w from the lane at
+//    w - 1; it is back at 0 exactly when every child has arrived (a partial
+//    sum is 0 only when what is missing adds nothing). A wave that holds a
+//    parent's whole range of leaves completes it without an atomic (most
+//    parents: 263k parents of ~1M runs at flat10m, 3.4 children each). The
+//    run that completes a parent climbs on with T(P) = len(P) + the sizes.
+// Leaves come from hasch (k_run_ep). Any depth.
+constexpr uint32_t SEGF = 0x80000000u;
+constexpr uint32_t PAR_ROOT = NONE - 1, PAR_HOLE = NONE - 2;
+
+__device__ __forceinline__ void run_climb2(RunArr& a, uint32_t x, uint4 ex, uint32_t t) {
+  for (;;) {
+    a.tk[a.kinv[x]] = t;
+    const uint32_t p = ex.x;
+    if (p == NONE) return;
+    const unsigned long long add = (1ULL << 32) | t;
+    const unsigned long long old = atomicAdd(&a.ca[p], add);
+    const uint4 e = a.rr[p];
+    const unsigned long long nv = old + add;
+    if ((nv >> 32) != 0) return;
+    t = e.y + static_cast<uint32_t>(nv);
+    x = p;
+    ex = e;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_run_sizes(RunArr a, uint32_t Q, const uint32_t* sarr, const uint32_t* pk,
+                                                     RunMask rm, uint32_t* offk) {
+  if (a.qd) Q = min(*a.qd, Q);  // (FlatRec::q: the bound stays the limit)
+  const uint32_t R = *a.nR;
+  const uint32_t lane = threadIdx.x & 63;
+  auto par = [&](uint32_t x) -> uint32_t {
+    return x < Q ? run_of(rm, x) : (x == Q ? PAR_ROOT : (x == Q + 1 ? PAR_HOLE : NONE));
+  };
+  for (uint32_t k0 = blockIdx.x * blockDim.x; k0 < R; k0 += gridDim.x * blockDim.x) {
+    const uint32_t k = k0 + threadIdx.x;
+    const bool valid = k < R;
+    const uint32_t r = valid ? sarr[k] : 0u;
+    const uint32_t p = valid ? pk[k] : Q + 2;
+    const uint32_t pq = (lane == 0 && valid && k > 0) ? pk[k - 1] : Q + 2;  // (the neighbours outside the wave)
+    const uint32_t pn = (lane == 63 && k + 1 < R) ? pk[k + 1] : Q + 2;
+    const uint4 e = valid ? a.rr[r] : make_uint4(NONE, 0u, NONE, 0u);
+    const bool leaf = valid && !a.hasch[r];
+    const uint32_t P = par(p);
+    uint32_t Pp = __shfl_up(P, 1, 64), Pn = __shfl_down(P, 1, 64);
+    if (lane == 0) Pp = par(pq);
+    if (lane == 63) Pn = par(pn);
+    const bool start = valid && Pp != P, end = valid && Pn != P;
+    const bool real = valid && P < PAR_HOLE;  // (a parent run, not the root sentinel or a hole)
+    uint32_t off = 0;
+    if (real) {
+      const unsigned long long m = rm.hm[p >> 6] & ((2ULL << (p & 63)) - 1ULL);  // (the word run_of read)
+      const uint32_t hp = m ? (p & ~63u) + 63u - static_cast<uint32_t>(__clzll(m)) : a.hh[P].x;
+      off = p - hp + 1u;
+      if (start) a.rr[P].z = k;
+      if (end) a.rr[P].w = k + 1;
+    }
+    if (valid) offk[k] = (start ? SEGF : 0u) | off;
+    if (leaf) a.tk[k] = e.y;  // (kinv[r] == k)
+    uint32_t hi = 0, lo = 0;
+    if (real) {
+      hi = (leaf ? 1u : 0u) + (start ? k : 0u) - (end ? k + 1u : 0u);
+      lo = leaf ? e.y : 0u;
+    }
+    unsigned long long v = (static_cast<unsigned long long>(hi) << 32) | lo;
+    const uint32_t key = real ? P : NONE - 4 - lane;  // (distinct per lane without a parent run)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {  // segmented inclusive sum over the lanes of one parent (contiguous)
+      const unsigned long long ov = __shfl_up(v, o, 64);
+      const uint32_t ok = __shfl_up(key, o, 64);
+      if (lane >= static_cast<uint32_t>(o) && ok == key) v += ov;
+    }
+    const uint32_t kp = __shfl_up(key, 1, 64), kn = __shfl_down(key, 1, 64);
+    const unsigned long long gs = __ballot(lane == 0 || kp != key);  // the groups' first lanes
+    const uint32_t f = 63u - static_cast<uint32_t>(__clzll(gs & ((2ULL << lane) - 1ULL)));
+    const bool fstart = __shfl(start ? 1u : 0u, static_cast<int>(f), 64) != 0;
+    if (real && (lane == 63 || kn != key)) {  // the group's last lane
+      if (fstart && end && (v >> 32) == 0) {  // the whole range, every child a leaf
+        const uint4 ep = a.rr[P];
+        run_climb2(a, P, ep, ep.y + static_cast<uint32_t>(v));
+      } else if (v != 0) {
+        const unsigned long long old = atomicAdd(&a.ca[P], v);
+        const uint4 ep = a.rr[P];
+        const unsigned long long nv = old + v;
+        if ((nv >> 32) == 0) run_climb2(a, P, ep, ep.y + static_cast<uint32_t>(nv));
+      }
+    }
+  }
+}
+
+// The offsets w by a segmented inclusive scan of the sizes in sorted order
+// (a parent's child range is one segment; the root sentinel's children one
+// more): its epilogue writes w(c) = the sizes of c's siblings sorted before
+// it + offk, and the expansion reads the inclusive values (xs & ~SEGF).
+struct SegSumOp {
+  static __device__ __forceinline__ uint32_t id() { return 0u; }
+  static __device__ __forceinline__ uint32_t op(uint32_t a, uint32_t b) {
+    return (b & SEGF) ? b : ((a & SEGF) | ((a & ~SEGF) + b));
+  }
+};
+struct RunSizeGen {
+  static constexpr bool kStriped = true;
+  static constexpr bool kEpilogue = false;
+  const uint32_t* tk;
+  const uint32_t* offk;
+  __device__ __forceinline__ bool aligned(uint64_t b) const {
+    return ((reinterpret_cast<uintptr_t>(tk + b) | reinterpret_cast<uintptr_t>(offk + b)) & 15) == 0;
+  }
+  __device__ __forceinline__ uint4 load4(uint64_t b) const {
+    const uint4 t = *reinterpret_cast<const uint4*>(tk + b), f = *reinterpret_cast<const uint4*>(offk + b);
+    return make_uint4(t.x | (f.x & SEGF), t.y | (f.y & SEGF), t.z | (f.z & SEGF), t.w | (f.w & SEGF));
+  }
+  __device__ __forceinline__ void load(uint64_t b, uint64_t n, uint32_t* v) const {
+#pragma unroll
+    for (int j = 0; j < DS_ITEMS; ++j) v[j] = b + j < n ? (tk[b + j] | (offk[b + j] & SEGF)) : 0u;
+  }
+};
+
+// w(c) = the sizes of c's siblings sorted before it (the segmented scan one
+// position back, 0 at a range's start) + offk (a grid-wide pass: the scan's
+// few large tiles would serialise these random stores)
+__global__ void __launch_bounds__(BLOCK) k_run_w2(RunArr a, uint32_t Q, const uint32_t* sarr, const uint32_t* pk,
+                                                  const uint32_t* xs, const uint32_t* offk) {
+  if (a.qd) Q = min(*a.qd, Q);
+  RUN_LOOP(k) {
+    const uint32_t f = offk[k], r = sarr[k], p = pk[k];
+    if (p > Q) continue;  // (hole runs)
+    const uint32_t ex = (f & SEGF) ? 0u : (xs[k - 1] & ~SEGF);
+    a.rr[r].y = ex + (f & ~SEGF);
   }
 }
 
@@ -2804,7 +2972,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_pos(RunArr a, DevResult* dres) {
 // before this slot's dependent loads).
 __global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint32_t K, RunMask rm,
                                                       const uint32_t* pk, const uint32_t* xs, const uint32_t* qc,
-                                                      uint32_t* doc, FlatRec fr, uint32_t lds_iters) {
+                                                      uint32_t* doc, FlatRec fr, uint32_t lds_iters, uint32_t seg) {
   extern __shared__ uint32_t smw[];  // [lds_iters * waves] {mask lo, mask hi, base}
   Q = fr.q(Q);  // (the host sized the LDS staging for its bound: at least these iterations)
   const uint32_t iters = (Q + gridDim.x * blockDim.x - 1) / (gridDim.x * blockDim.x);
@@ -2823,13 +2991,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, stride = gridDim.x * blockDim.x;
   const unsigned long long below = (2ULL << lane) - 1ULL;
-  uint32_t q0 = blockIdx.x * blockDim.x;
-  uint32_t x_n = q0 + threadIdx.x < Q ? fr.rec[q0 + threadIdx.x].x : FR_EMPTY;  // (prefetch)
-  for (uint32_t it = 0; q0 < Q; q0 += stride, ++it) {
-    const uint32_t q = q0 + threadIdx.x;
-    const uint32_t xq = x_n;
-    x_n = q + stride < Q ? fr.rec[q + stride].x : FR_EMPTY;
-    if (!(q < Q && fr.present(xq))) continue;
+  auto run_at = [&](uint32_t it, uint32_t q) -> uint32_t {
     unsigned long long mq;
     uint32_t bq;
     if (mlds) {
@@ -2840,9 +3002,35 @@ __global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint
       mq = rm.hm[q >> 6];
       bq = rm.hb[q >> 6];
     }
-    const uint32_t r = bq + static_cast<uint32_t>(__popcll(mq & below)) - 1u;
-    uint32_t p = a.posh[r] + (q - a.hh[r].x);
-    const uint4 er = a.rr[r];
+    return bq + static_cast<uint32_t>(__popcll(mq & below)) - 1u;
+  };
+  // the run records of the lane's next slot load before this slot's search
+  // (software pipelined: their round trip overlaps this one's)
+  uint32_t q0 = blockIdx.x * blockDim.x;
+  uint2 hn = make_uint2(0u, ABSENT);
+  uint32_t pn = 0;
+  uint4 en = make_uint4(0u, 0u, 0u, 0u);
+  auto fetch = [&](uint32_t it, uint32_t q) {
+    if (q < Q) {
+      const uint32_t r = run_at(it, q);
+      hn = a.hh[r];
+      pn = a.posh[r];
+      en = a.rr[r];
+    }
+  };
+  fetch(0, q0 + threadIdx.x);
+  for (uint32_t it = 0; q0 < Q; q0 += stride, ++it) {
+    const uint32_t q = q0 + threadIdx.x;
+    // (a slot without a node is a hole run of its own, its anchor ABSENT:
+    // presence comes with the run's record, not from a pass over the slot
+    // records)
+    const uint2 h = hn;
+    const uint32_t ph = pn;
+    const uint4 er = en;
+    hn = make_uint2(0u, ABSENT);
+    if (q0 + stride < Q) fetch(it + 1, q + stride);
+    if (q >= Q || h.y == ABSENT) continue;
+    uint32_t p = ph + (q - h.x);
     const uint32_t e0 = er.z, e1 = er.w;
     if (e1 > e0) {
       uint32_t lo = e0, hi = e1;  // first k with pk[k] >= q
@@ -2851,7 +3039,7 @@ __global__ void __launch_bounds__(BLOCK) k_run_expand(RunArr a, uint32_t Q, uint
         if (pk[mid] < q) lo = mid + 1;
         else hi = mid;
       }
-      if (lo > e0) p += xs[lo - 1] - run_S(xs, e0);
+      if (lo > e0) p += seg ? (xs[lo - 1] & ~SEGF) : xs[lo - 1] - run_S(xs, e0);
     }
     if (p < K) doc[p] = 1 + (qc ? qc[q] : q);  // (a rank past K: a speculation that fails)
   }
@@ -3316,8 +3504,15 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     if ((r = dscan<SumOp, false>(ArrGen{hc}, hb, NW, &dr->run_count, ws, s, nullptr, fr.qd ? &dr->fl_nw : nullptr,
                                  "k_dscan_runs")))
       return r;
+    // (env CRDTM_RUN_V2=0: round 5's k_run_gstart, k_run_tree_up, scan, k_run_w)
+    static const bool run_v2 = [] {
+      const char* e = getenv("CRDTM_RUN_V2");
+      return !(e && e[0] == '0');
+    }();
+    ra.hasch = run_v2 ? ws.alloc<uint8_t>(Q + 1) : nullptr;
     static const uint32_t heads_grid = env_grid("CRDTM_HEADS_GRID", 4096);
-    LAUNCH(k_run_heads, dim3(grid_for(64ULL * NW, BLOCK, heads_grid)), dim3(BLOCK), 0, s, fr, Q, fb.rm, ra.hh);
+    LAUNCH(k_run_heads, dim3(grid_for(64ULL * NW, BLOCK, heads_grid)), dim3(BLOCK), 0, s, fr, Q, fb.rm, ra.hh,
+           ra.hasch);
     // ---- K2a (heads' effective parents), parent runs, sibling order (stable radix sort by attach slot) ----
     ra.rr = ws.alloc<uint4>(Q + 1);
     ra.ca = ws.alloc<unsigned long long>(Q + 1);
@@ -3347,12 +3542,20 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
       while (sbits < 32 && ((static_cast<uint64_t>(Q) + 1) >> sbits) != 0) sbits += 8;
       if ((r = radix_sort_pairs(sk[0], sv[0], sk[1], sv[1], ra.nR, Q, sbits, ws, s, &pk, &sarr, kinv))) return r;
       ra.tk = pk == sk[0] ? sk[1] : sk[0];  // (free after the sort)
-      LAUNCH(k_run_gstart, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, fb.rm, groot);
+      if (!run_v2) LAUNCH(k_run_gstart, dim3(gr), dim3(BLOCK), 0, s, ra, Q, pk, fb.rm, groot);
     }
     // ---- subtree sizes (one launch, in sorted order), head ranks, the document order ----
-    LAUNCH(k_run_tree_up, dim3(gr), dim3(BLOCK), 0, s, ra, sarr);
-    if ((r = dscan<SumOp, true>(ArrGen{ra.tk}, xs, Q, nullptr, ws, s, nullptr, ra.nR, "k_dscan_xs"))) return r;
-    LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, groot, fb.rm);
+    if (run_v2) {
+      uint32_t* offk = ws.alloc<uint32_t>(Q + 1);
+      LAUNCH(k_run_sizes, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, fb.rm, offk);
+      if ((r = dscan<SegSumOp, true>(RunSizeGen{ra.tk, offk}, xs, Q, nullptr, ws, s, nullptr, ra.nR, "k_dscan_seg")))
+        return r;
+      LAUNCH(k_run_w2, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, offk);
+    } else {
+      LAUNCH(k_run_tree_up, dim3(gr), dim3(BLOCK), 0, s, ra, sarr);
+      if ((r = dscan<SumOp, true>(ArrGen{ra.tk}, xs, Q, nullptr, ws, s, nullptr, ra.nR, "k_dscan_xs"))) return r;
+      LAUNCH(k_run_w, dim3(gr), dim3(BLOCK), 0, s, ra, Q, sarr, pk, xs, groot, fb.rm);
+    }
     LAUNCH(k_run_pos, dim3(gr), dim3(BLOCK), 0, s, ra, dr);
     // ---- the document order, the chain ----
     static const uint32_t ex_grid = env_grid("CRDTM_EX_GRID", 2048);
@@ -3360,18 +3563,25 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     const uint32_t ex_iters = (Q + gx * BLOCK - 1) / (gx * BLOCK);
     LAUNCH(k_run_expand, dim3(gx), dim3(BLOCK),
            ex_iters <= EX_ITERS ? 3 * ex_iters * (BLOCK / 64) * sizeof(uint32_t) : 0, s, ra, Q, K, fb.rm, pk, xs, qc,
-           t->d.doc, fr, ex_iters <= EX_ITERS ? ex_iters : 0u);
+           t->d.doc, fr, ex_iters <= EX_ITERS ? ex_iters : 0u, run_v2 ? 1u : 0u);
     // (measured and reverted in round 5: the raw `next` written in slot order
     // by the expansion — the run's next slot, the first child run at the
     // slot, or the successor of the run's sub-document found by a walk up in
     // k_run_pos — cost 36 + 32 us more there than this pass's 33 us)
     static const uint32_t next_grid = env_grid("CRDTM_NEXT_GRID", 1u << 20);
-    LAUNCH(k_fl_next, dim3(grid_for(K, BLOCK, next_grid)), dim3(BLOCK), 0, s, K, t->d.doc, t->d, t->cap.slots);
+    fb.rep = ws.alloc<long long>(2 * static_cast<uint64_t>(maxr) + 2);
+    // (the replicas collection rides on this launch: it is the merge's last
+    // when the log was written by the claim)
+    RepCollect rc{o, 0u, c->rtab, fb.rep, &dr->n_replica_out, dr->rep_inline, check ? c->crange : nullptr};
+    const bool rep_here = !(all_applied && !log_done);
+    if (rep_here) rc.nr = maxr + 1;
+    LAUNCH(k_fl_next, dim3(grid_for(K, BLOCK, next_grid)), dim3(BLOCK), 0, s, K, t->d.doc, t->d, t->cap.slots, rc);
+    if (rep_here) return CRDTM_OK;
     if (all_applied && !log_done) fl_log_copy(c, o, t->d, simple);
   } else if (all_applied && !log_done) {
     fl_log_copy(c, o, t->d, simple);
   }
-  fb.rep = ws.alloc<long long>(2 * static_cast<uint64_t>(maxr) + 2);
+  if (!fb.rep) fb.rep = ws.alloc<long long>(2 * static_cast<uint64_t>(maxr) + 2);
   // (the speculation's commit is the merge's last: the range table is reset here too)
   LAUNCH(k_fl_rep_collect, dim3(grid_for(maxr + 1)), dim3(BLOCK), 0, s, o, maxr + 1, c->rtab, fb.rep,
          &dr->n_replica_out, dr->rep_inline, check ? c->crange : nullptr);
@@ -3418,7 +3628,7 @@ static int flat_order_fallback(crdtm_tree* t, uint32_t Q, uint32_t K, FlatBufs& 
   if ((r = list_rank_fused(FlatEulerSrc{Q, anc, cnt, carr, ns}, 2ULL * U, 2 * Q, FlatDocSink{Q, t->d.doc, qc},
                            ws, s)))
     return r;
-  LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d, t->cap.slots);
+  LAUNCH(k_fl_next, dim3(grid_for(K)), dim3(BLOCK), 0, s, K, t->d.doc, t->d, t->cap.slots, RepCollect{});
   return CRDTM_OK;
 }
 
@@ -3517,7 +3727,6 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
       own += h.fl_part[32 * k + 2];
       slow += h.fl_part[32 * k + 3];
     }
-    if (h.bad_range) return CRDTM_E_RANGE;  // (k_fl_claim's path check; the caller restores the fresh tree)
     if (devq) {
       // the shape the launches assumed: every op an Add with a one-element
       // path, non-negative timestamps, a dense range within the bound, replica
@@ -3528,12 +3737,17 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
         *done = false;
         return CRDTM_OK;
       }
+      // (the shape first: k_pre_ts range-checks every op's ts, a Delete's
+      // too, which the reference ignores — a batch with a Delete is not one
+      // this path serves, and the general path checks only what it reads)
+      if (h.bad_range) return CRDTM_E_RANGE;  // (every op an Add: its ts or path element is out of range)
       Q = h.range_total;  // (known from here: the later launches take the host's values)
       maxr = h.max_replica;
       fb.fr.qd = nullptr;
       fb.fr.nrd = nullptr;
       if (t->max_depth < 1) t->max_depth = 1;
     }
+    if (h.bad_range) return CRDTM_E_RANGE;  // (k_fl_claim's path check; the caller restores the fresh tree)
     const long long new_ts = t->timestamp + own - t->own_bias;
     // (devq: the merge assumed no slot without a node, Q == n)
     const bool every = h.err_index == NONE && slow == 0 && present == keys && keys == n && (!devq || Q == n);

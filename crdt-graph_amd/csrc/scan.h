@@ -83,23 +83,26 @@ __global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* out, uint64_
   uint32_t acc = OP::id();
 #pragma unroll
   for (int j = 0; j < DS_ITEMS; ++j) acc = OP::op(acc, v[j]);
-  // workgroup exclusive scan of the per-thread totals
+  // workgroup exclusive scan of the per-thread totals (every combination in
+  // item order, earlier operand first: OP need not commute — the segmented
+  // sum of the flat order's run sizes does not)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t inc = acc;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t t = __shfl_up(inc, o, 64);
-    if (lane >= o) inc = OP::op(inc, t);
+    if (lane >= o) inc = OP::op(t, inc);
   }
   if (lane == 63) sw[wave] = inc;
   __syncthreads();
   uint32_t texcl = __shfl_up(inc, 1, 64);
   if (lane == 0) texcl = OP::id();
-  uint32_t agg = OP::id();
+  uint32_t agg = OP::id(), wpre = OP::id();
   for (int w = 0; w < BLOCK / 64; ++w) {
-    if (w < wave) texcl = OP::op(texcl, sw[w]);
+    if (w < wave) wpre = OP::op(wpre, sw[w]);
     agg = OP::op(agg, sw[w]);
   }
+  texcl = OP::op(wpre, texcl);
   if (wave == 0) {
     uint32_t prefix = OP::id();
     if (tile == 0) {
@@ -125,10 +128,16 @@ __global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* out, uint64_
           __builtin_amdgcn_s_sleep(1);
           continue;
         }
+        // lane j holds tile (tile - 1 - j): fold from the farthest lane down
+        // to lane 0 (the nearest), then in front of the nearer windows' prefix
         uint32_t c = static_cast<uint32_t>(lane) < upto ? val : OP::id();
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) c = OP::op(c, __shfl_xor(c, o, 64));
-        prefix = OP::op(prefix, c);
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t t = __shfl_down(c, o, 64);
+          if (lane + o < 64) c = OP::op(t, c);
+        }
+        c = __shfl(c, 0, 64);
+        prefix = OP::op(c, prefix);
         if (pm) break;
         j -= 64;
       }

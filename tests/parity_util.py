@@ -88,6 +88,24 @@ def engine_log(tree, which=0, since=None):
     return log_tuples(kind, ts, off, path, val, n), bool(isb.value)
 
 
+def engine_log_arrays(tree, which=0):
+    """The log (0) or lastOperation (1) as packed numpy arrays (kind, ts,
+    path_off, path, val) plus is_batch, for full-size comparisons."""
+    import crdtm._native as N
+    from crdtm.tree import _ptr
+    o = N.Ops()
+    isb = C.c_int(1)
+    N.check(N.lib().crdtm_tree_ops(tree._h, which, C.byref(o), C.byref(isb)))
+    n, npth = o.n_ops, o.n_path
+    out = dict(kind=np.zeros(n + 1, np.uint8), ts=np.zeros(n + 1, np.int64), path_off=np.zeros(n + 1, np.uint32),
+               path=np.zeros(npth + 1, np.int64), val=np.zeros(n + 1, np.uint32))
+    o2 = N.Ops(n, npth, _ptr(out["kind"]), _ptr(out["ts"]), _ptr(out["path_off"]), _ptr(out["path"]),
+               _ptr(out["val"]), None)
+    N.check(N.lib().crdtm_tree_ops(tree._h, which, C.byref(o2), C.byref(isb)))
+    return dict(kind=out["kind"][:n], ts=out["ts"][:n], path_off=out["path_off"][:n + 1], path=out["path"][:npth],
+                val=out["val"][:n]), bool(isb.value)
+
+
 def engine_summary(tree):
     out = {}
     for which in (0, 1):

@@ -14,7 +14,12 @@ document).
   (`orc_flat_replay`: findInsertion's stop node through a treap, pinned
   against the literal walk in tests/test_oracle_flat.py, which
   tests/test_oracle_kat.py pins against the general restatement); the
-  reference behaviour is src/Internal/Node.elm:93-104 over 10M siblings.
+  reference behaviour is src/Internal/Node.elm:93-104 over 10M siblings;
+* the merge's other outputs at 10M, derived in numpy for an Adds-only batch
+  on a fresh tree (src/CRDTree.elm:298-325, :337-343): the op log and
+  lastOperation are the batch itself (every op Applied, in batch order), the
+  replicas table holds each replica's last Add (last writer), and the
+  timestamp counts the observer's own-replica Adds.
 """
 import ctypes as C
 
@@ -26,6 +31,7 @@ pytestmark = pytest.mark.gpu
 from crdtm import _native as N  # noqa: E402
 from crdtm.tree import CRDTree  # noqa: E402
 from oracle.oracle import _ptr, lib as olib  # noqa: E402
+from parity_util import engine_log_arrays  # noqa: E402
 
 CFG3 = dict(replicas=64, window=256, seed=0xC0FFEE03)
 
@@ -56,6 +62,23 @@ def test_flat10m_order_properties():
     for which in (0, 1):
         _, enw, eh = t.canonical(which, full=False)
         assert (enw, eh) == (int(w[which]), int(h[which])), which
+    check_flat_outputs(t, s, n)
+
+
+def check_flat_outputs(t, s, n, replica=0):
+    """Log, lastOperation, replicas and timestamp of an Adds-only batch merged
+    into a fresh `init replica` tree, every op Applied."""
+    for which in (0, 1):  # operations (oldest first) and lastOperation (src/CRDTree.elm:311, :328-334)
+        lg, isb = engine_log_arrays(t, which)
+        assert isb
+        for f in ("kind", "ts", "path_off", "path", "val"):
+            assert np.array_equal(lg[f], s[f][:len(lg[f])]) and len(lg[f]) == len(s[f][:n + (f == "path_off")]), \
+                (which, f)
+    rid = s["ts"][:n] >> 32  # Timestamp.replicaId (src/CRDTree/Timestamp.elm:16-18): ts >= 0 here
+    ids, first_rev = np.unique(rid[::-1], return_index=True)
+    last = n - 1 - first_rev  # each replica's last Add in batch order: replicas[r] := ts (last writer)
+    assert t.replicas() == {int(r): int(s["ts"][i]) for r, i in zip(ids, last)}
+    assert t.timestamp() == replica * 2 ** 32 + int(np.count_nonzero(rid == replica))
 
 
 def test_flat1m_matches_fast_restatement():
@@ -73,3 +96,4 @@ def test_flat1m_matches_fast_restatement():
     for which in (0, 1):
         _, enw, eh = t.canonical(which, full=False)
         assert (enw, eh) == (int(w[which]), int(h[which])), which
+    check_flat_outputs(t, s, m)

@@ -269,15 +269,22 @@ def _flat_ops(n, replicas=8, seed=3):
 
 
 @pytest.mark.parametrize("shape", ["flat", "with_delete", "empty_and_long_path", "replica_300", "negative_ts",
-                                   "duplicate_ts", "counter_holes", "sentinel_ts"])
+                                   "duplicate_ts", "counter_holes", "sentinel_ts", "delete_ts_2_53",
+                                   "anchor_later", "anchor_prev_later", "anchor_missing", "anchor_self"])
 def test_flat_speculation_shapes(shape):
     """The flat speculation (merge.hip apply_core: a fresh tree whose batch has
     as many path elements as ops is merged at once, the slot range read on
     the device) must keep exactly the reference's result for every batch of
-    that size, also those it does not serve: a Delete among the Adds, an
-    empty path balanced by a two-key path (InvalidPath), a replica id above
-    its LDS table, a negative timestamp, duplicate timestamps and timestamps
-    with counter holes (the status path), the sentinel's key 0."""
+    that size, also those it does not serve: a Delete among the Adds (also
+    one whose unused ts field is 2^53: the reference ignores it), an empty
+    path balanced by a two-key path (InvalidPath), a replica id above its
+    LDS table, a negative timestamp, duplicate timestamps and timestamps
+    with counter holes (the status path), the sentinel's key 0; and the
+    speculation's own failing Adds (addAfterHelp NotFound,
+    src/Internal/Node.elm:68-70): an anchor added later in the batch
+    (checked by k_run_ep), a typing continuation whose previous character
+    comes later (k_run_mask), an anchor that no op adds (k_run_heads), an
+    Add anchored at itself."""
     ops = _flat_ops(4000)
     if shape == "with_delete":
         ops.append((1, 0, [ops[100][1]], 0))
@@ -295,6 +302,19 @@ def test_flat_speculation_shapes(shape):
         ops.append((0, (7 << 32) + 100007, [(7 << 32) + 100000], 9))
     elif shape == "sentinel_ts":
         ops.append((0, 0, [ops[10][1]], 9))
+    elif shape == "delete_ts_2_53":
+        ops.append((1, 1 << 53, [ops[100][1]], 0))
+    elif shape == "anchor_later":
+        ops[100] = (0, ops[100][1], [ops[3000][1]], ops[100][3])
+    elif shape == "anchor_prev_later":  # a continuation (anchored at ts - 1) placed before its anchor
+        j = next(i for i in range(1000, len(ops)) if ops[i][2][0] == ops[i][1] - 1 and
+                 any(ops[k][1] == ops[i][1] - 1 for k in range(i - 200, i)))
+        k = next(k for k in range(j - 200, j) if ops[k][1] == ops[j][1] - 1)
+        ops[k], ops[j] = ops[j], ops[k]
+    elif shape == "anchor_missing":
+        ops[100] = (0, ops[100][1], [(5 << 32) + 999999], ops[100][3])
+    elif shape == "anchor_self":
+        ops[100] = (0, ops[100][1], [ops[100][1]], ops[100][3])
     s = _arrays(ops)
     n = len(ops)
     assert int(s["path_off"][-1]) == n  # (the speculation's trigger)
