@@ -1905,7 +1905,23 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
   };
   const long long id0 = replica_of(ts0);
   uint32_t keys = 0, own = 0, slow = 0, err = NONE, mr = 0, bad = 0, vfail = 0;
-  QUAD_LOOP_XCD(i0, o.n) {
+  // the slot records are staged in LDS and stored grouped by replica (a
+  // replica's ops of one iteration hold consecutive counters: whole lines of
+  // its slot run), instead of one scattered 8-byte store per op beside the
+  // log's streaming stores (tools/claim_bench.hip: 146 -> 101 us for the
+  // same bytes)
+  __shared__ uint32_t s_cnt[64], s_off[64];
+  __shared__ uint2 s_rec[4 * BLOCK];
+  __shared__ uint32_t s_q[4 * BLOCK];
+  const uint32_t nq_ = (o.n + 3) / 4;  // (QUAD_LOOP_XCD, with every thread in every iteration)
+  const bool x8_ = (gridDim.x & 7) == 0;
+  const uint32_t xc_ = x8_ ? blockIdx.x & 7 : 0, xy_ = x8_ ? blockIdx.x >> 3 : blockIdx.x;
+  const uint32_t cq_ = (x8_ ? gridDim.x >> 3 : gridDim.x) * blockDim.x, xs_ = x8_ ? 8 : 1;
+  for (uint32_t j_ = xc_; j_ * cq_ < nq_; j_ += xs_) {
+    const uint32_t qd_ = j_ * cq_ + xy_ * blockDim.x + threadIdx.x, i0 = 4 * qd_;
+    uint32_t sq[4] = {NONE, NONE, NONE, NONE}, sb[4] = {0u, 0u, 0u, 0u};
+    uint2 sv[4];
+    if (qd_ < nq_) {
     Quad qd;
     long long pk[4];  // the path element of each op (flat: |path| <= 1)
     if (VERIFY) {
@@ -1997,7 +2013,9 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
       const long long kk = pk[k];
       uint32_t qa = kk == 0 ? Q : slot(kk);
       if (qa > Q) qa = NONE;
-      fr.rec[q] = make_uint2(fr.code(qa), i);
+      sq[k] = q;  // (stored below: fr.rec[q] = {anchor code, op index})
+      sv[k] = make_uint2(fr.code(qa), i);
+      sb[k] = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32) & 63u;
       if (track_rep) {
         const uint32_t rr = static_cast<uint32_t>(static_cast<uint64_t>(ts) >> 32);
         if (rr < REP_DIRECT) {
@@ -2008,6 +2026,30 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
         }
       }
     }
+    }
+    // the staged stores: counting sort of the iteration's records by bucket
+    for (uint32_t b = threadIdx.x; b < 64; b += blockDim.x) s_cnt[b] = 0;
+    __syncthreads();
+    uint32_t pos[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) pos[k] = sq[k] != NONE ? atomicAdd(&s_cnt[sb[k]], 1u) : 0u;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const uint32_t c = s_cnt[threadIdx.x];
+      s_off[threadIdx.x] = wave_incl_scan(c) - c;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+      if (sq[k] != NONE) {
+        const uint32_t e = s_off[sb[k]] + pos[k];
+        s_rec[e] = sv[k];
+        s_q[e] = sq[k];
+      }
+    __syncthreads();
+    const uint32_t tot = s_off[63] + s_cnt[63];
+    for (uint32_t e = threadIdx.x; e < tot; e += blockDim.x) fr.rec[s_q[e]] = s_rec[e];
+    __syncthreads();
   }
   mr = block_max(mr);  // (synchronises the block) only ids <= mr were touched
   if (track_rep)
@@ -2224,6 +2266,7 @@ __device__ __forceinline__ long long fl_key(uint32_t q, const uint32_t* sb, cons
 //    atomic per wave and replica).
 // The trip count is wave-uniform, so every lane takes part in the ballots.
 constexpr uint32_t RM_UNROLL = 4;       // k_run_heads: words per wave and iteration
+constexpr uint32_t RM_BUCKETS = 2048;   // k_run_mask: slot buckets of the replica lookup
 constexpr uint32_t RM_MASK_UNROLL = 2;  // k_run_mask (48 VGPRs, full occupancy; 4 words: 68, 120 -> 110 us at flat10m)
 // DEVQ: the speculation without the host round trip (FlatRec::qd): the slot
 // range and replica count come from the device (the tree's slot capacity
@@ -2234,7 +2277,13 @@ __global__ void __launch_bounds__(BLOCK) k_run_mask(FlatRec fr, uint32_t Q, unsi
                                                    TreeDev T, const uint32_t* qc, const uint32_t* logidx, OpsDev o,
                                                    TsIndex x, uint32_t nrep, DevResult* chk, uint32_t* rtab) {
   extern __shared__ uint32_t smk[];  // dynamic: 3 * nrep words when the tables fit (HOST_RANGES)
-  const bool lds = nrep <= HOST_RANGES;
+  // (DEVQ, the speculation: the tables fit, no compaction, every op applies
+  // — the branches for the other cases are compiled out)
+  const bool lds = DEVQ || nrep <= HOST_RANGES;
+  if (DEVQ) {
+    qc = nullptr;
+    logidx = nullptr;
+  }
   if (DEVQ) {
     Q = fr.q(Q);
     nrep = fr.nrep(nrep);
@@ -2242,11 +2291,29 @@ __global__ void __launch_bounds__(BLOCK) k_run_mask(FlatRec fr, uint32_t Q, unsi
   uint32_t* sb = smk;
   uint32_t* sc = smk + nrep;
   uint32_t* srv = smk + 2 * nrep;  // (chk) largest op index + 1 per replica
+  // the replica of a word's first slot: the slot's bucket of 2^sh slots
+  // names the last replica starting at or before the bucket (LDS), a few
+  // steps on from there (one dependent LDS read per word instead of a
+  // binary search's seven)
+  __shared__ uint16_t sbk[RM_BUCKETS];
+  uint32_t sh = 0;
+  while ((static_cast<uint64_t>(Q) >> sh) >= RM_BUCKETS) ++sh;
   if (lds) {
     for (uint32_t j = threadIdx.x; j < nrep; j += blockDim.x) {
       sb[j] = x.base[j];
       sc[j] = x.rng[j].x;
       srv[j] = 0;
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < RM_BUCKETS; b += blockDim.x) {
+      const uint32_t q0 = b << sh;
+      uint32_t lo = 0, hi = nrep;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sb[mid] <= q0) lo = mid;
+        else hi = mid;
+      }
+      sbk[b] = static_cast<uint16_t>(lo);
     }
   }
   __syncthreads();
@@ -2254,51 +2321,67 @@ __global__ void __launch_bounds__(BLOCK) k_run_mask(FlatRec fr, uint32_t Q, unsi
   const uint32_t nw = (Q + 63) >> 6;
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwave = (gridDim.x * blockDim.x) >> 6;
   uint32_t present = 0, err = NONE;
+  // Loads are unconditional (clamped indices) and the next iteration's are
+  // issued before this one's stores: a load behind an exec-masked branch,
+  // or behind the stores, made the compiler wait for everything in flight
+  // (gfx9 counts loads and stores in issue order) twice per iteration.
+  const uint32_t qmax = Q ? Q - 1 : 0u;
+  uint2 nq[U], np;
+  auto load = [&](uint32_t w0) {
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) nq[u] = fr.rec[min(((w0 + u) << 6) + lane, qmax)];
+    np = fr.rec[w0 ? (w0 << 6) - 1 : 0u];  // (the slot before the first word: one address for the wave)
+  };
+  if (wave * U < nw) load(wave * U);
   for (uint32_t w0 = wave * U; w0 < nw; w0 += nwave * U) {
     uint2 rq[U], rp[U];
 #pragma unroll
-    for (uint32_t u = 0; u < U; ++u) {  // every load in flight first
-      const uint32_t q = ((w0 + u) << 6) + lane;
-      rq[u] = q < Q ? fr.rec[q] : make_uint2(FR_EMPTY, 0u);
-      rp[u] = (lane == 0 && q > 0 && q - 1 < Q) ? fr.rec[q - 1] : make_uint2(FR_EMPTY, 0u);
-    }
-    // the anchors' records of run heads (the check) load before this
-    // iteration's stores: gfx9 waits on loads and stores in issue order
+    for (uint32_t u = 0; u < U; ++u) rq[u] = nq[u];
+    const uint2 rprev = w0 ? np : make_uint2(FR_EMPTY, 0u);
+    if (w0 + nwave * U < nw) load(w0 + nwave * U);
+    // the slot before each lane's: the neighbouring lane's, the previous
+    // word's last for lane 0
     uint2 ra[U];
+    unsigned long long m[U];
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
       const uint32_t q = ((w0 + u) << 6) + lane;
       const uint32_t px = __shfl_up(rq[u].x, 1, 64), py = __shfl_up(rq[u].y, 1, 64);
-      if (lane != 0) rp[u] = make_uint2(px, py);
+      const uint2 last = u ? make_uint2(__shfl(rq[u - 1].x, 63, 64), __shfl(rq[u - 1].y, 63, 64)) : rprev;
+      rp[u] = lane ? make_uint2(px, py) : last;
+      const bool pres = q < Q && fr.present(rq[u].x);
       const uint32_t qa = fr.anchor(rq[u].x);
+      const bool cont = pres && q > 0 && fr.present(rp[u].x) && qa == q - 1;
+      m[u] = __ballot(q < Q && !cont);
+      // the anchors' records of run heads anchored elsewhere (the check)
       ra[u] = make_uint2(FR_EMPTY, 0u);
-      if (chk && q < Q && fr.present(rq[u].x) && qa != Q && qa != NONE && qa + 1 != q) ra[u] = fr.rec[qa];
+      if (chk && pres && qa != Q && qa != NONE && qa + 1 != q) ra[u] = fr.rec[qa];
     }
+    {  // the words' head masks and counts: one store per iteration, lane u for word u
+      unsigned long long mv = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u)
+        if (lane == u) mv = m[u];
+      if (lane < U && w0 + lane < nw) {
+        hm[w0 + lane] = mv;
+        hc[w0 + lane] = static_cast<uint32_t>(__popcll(mv));
+      }
+    }
+    uint32_t rep[U];
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
       const uint32_t q = ((w0 + u) << 6) + lane;
       const bool pres = q < Q && fr.present(rq[u].x);
-      const uint32_t qa = fr.anchor(rq[u].x);
-      const bool cont = pres && q > 0 && fr.present(rp[u].x) && qa == q - 1;
-      const unsigned long long m = __ballot(q < Q && !cont);
-      if (lane == 0 && w0 + u < nw) {
-        hm[w0 + u] = m;
-        hc[w0 + u] = static_cast<uint32_t>(__popcll(m));
-      }
-      uint32_t rep = NONE;
+      rep[u] = NONE;
       const uint32_t fi = rq[u].y;
-      // the replica of the word's first slot, searched once for the wave
+      // the replica of the word's first slot, looked up once for the wave
       // (uniform LDS reads); a lane past that replica's range (a word that
       // straddles two ranges) searches for itself
       uint32_t wr = 0, wlo = NONE, whi = 0;
       if (lds) {
         const uint32_t q0 = (w0 + u) << 6;
-        uint32_t lo = 0, hi = nrep;
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (sb[mid] <= q0) lo = mid;
-          else hi = mid;
-        }
+        uint32_t lo = sbk[min(q0 >> sh, RM_BUCKETS - 1)];
+        while (lo + 1 < nrep && sb[lo + 1] <= q0) ++lo;
         wr = lo;
         wlo = sb[lo];
         whi = lo + 1 < nrep ? sb[lo + 1] : NONE;
@@ -2309,37 +2392,44 @@ __global__ void __launch_bounds__(BLOCK) k_run_mask(FlatRec fr, uint32_t Q, unsi
         if (!lds) {
           key = o.ts[fi];
         } else if (q >= wlo && q < whi) {
-          rep = wr;
+          rep[u] = wr;
           key = (static_cast<long long>(wr) << 32) | static_cast<long long>(sc[wr] + (q - wlo));
         } else {
-          key = fl_key(q, sb, sc, nrep, rep);
+          key = fl_key(q, sb, sc, nrep, rep[u]);
         }
         st_node(T.s_key + slot, key);
         st_node(T.s_dict + slot, 0u);
         st_node(T.s_src + slot, logidx ? logidx[fi] : fi);
         st_node(T.s_flags + slot, static_cast<uint8_t>(0));
         st_node(T.s_child + slot, NONE);
-        if (chk) {
-          ++present;
-          if (qa != Q) {
-            bool ok = false;  // an Add at the anchor, before this one
-            if (qa + 1 == q) ok = fr.present(rp[u].x) && rp[u].y < fi;
-            else if (qa != NONE) ok = fr.present(ra[u].x) && ra[u].y < fi;
-            if (!ok) err = min(err, fi);
-          }
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {  // (after the stores: the wait covers the anchor loads only)
+      const uint32_t q = ((w0 + u) << 6) + lane;
+      const bool pres = q < Q && fr.present(rq[u].x);
+      const uint32_t qa = fr.anchor(rq[u].x);
+      const uint32_t fi = rq[u].y;
+      if (chk && pres) {
+        ++present;
+        if (qa != Q) {
+          bool ok = false;  // an Add at the anchor, before this one
+          if (qa + 1 == q) ok = fr.present(rp[u].x) && rp[u].y < fi;
+          else if (qa != NONE) ok = fr.present(ra[u].x) && ra[u].y < fi;
+          if (!ok) err = min(err, fi);
         }
       }
       if (chk && lds) {  // (wave-uniform) replicas[r] := its last Add
-        const unsigned long long mr = __ballot(rep != NONE);
+        const unsigned long long mr = __ballot(rep[u] != NONE);
         if (mr) {
-          const uint32_t r0 = __shfl(rep, __ffsll(static_cast<long long>(mr)) - 1, 64);
-          if (__ballot(rep != NONE && rep != r0) == 0) {
-            uint32_t v = rep != NONE ? fi + 1 : 0u;
+          const uint32_t r0 = __shfl(rep[u], __ffsll(static_cast<long long>(mr)) - 1, 64);
+          if (__ballot(rep[u] != NONE && rep[u] != r0) == 0) {
+            uint32_t v = rep[u] != NONE ? fi + 1 : 0u;
 #pragma unroll
             for (int o2 = 32; o2 > 0; o2 >>= 1) v = max(v, __shfl_xor(v, o2, 64));
             if (lane == 0) atomicMax(&srv[r0], v);
-          } else if (rep != NONE) {
-            atomicMax(&srv[rep], fi + 1);
+          } else if (rep[u] != NONE) {
+            atomicMax(&srv[rep[u]], fi + 1);
           }
         }
       }
@@ -3487,17 +3577,18 @@ static int flat_order_commit(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, 
     const uint32_t gw = std::max<uint32_t>(1, std::min<uint32_t>(mask_grid, (NW + mask_u * (BLOCK / 64) - 1) /
                                                                                  (mask_u * (BLOCK / 64))));
     const size_t mshm = maxr + 1 <= HOST_RANGES ? 3 * (maxr + 1) * sizeof(uint32_t) : 0;
-    static const bool mask_devq = [] {  // (A/B: the device-range instance on every merge)
-      const char* e = getenv("CRDTM_MASK_DEVQ");
-      return e && e[0] == '1';
-    }();
-    const bool dq = fr.qd || mask_devq;
+    const bool dq = fr.qd != nullptr;  // (the kernel's DEVQ instance assumes the speculation's shape)
     auto mask_launch = [&](auto kern, const char* name) {
       prof_begin(s);
       hipLaunchKernelGGL(kern, dim3(gw), dim3(BLOCK), mshm, s, fr, Q, hm, hc, t->d, qc, logidx, o, ix, maxr + 1,
                          check ? dr : nullptr, c->rtab);
       prof_mark(name, s);
     };
+    static const bool diag_mask2 = [] {  // (diagnostic: the pass twice, the second on a warm memory system)
+      const char* e = getenv("CRDTM_DIAG_MASK2");
+      return e && e[0] == '1';
+    }();
+    if (diag_mask2) mask_launch(dq ? k_run_mask<RM_MASK_UNROLL, true> : k_run_mask<RM_MASK_UNROLL, false>, "k_run_mask");
     if (mask_u == 1) mask_launch(dq ? k_run_mask<1, true> : k_run_mask<1, false>, "k_run_mask");
     else if (mask_u == 4) mask_launch(dq ? k_run_mask<4, true> : k_run_mask<4, false>, "k_run_mask");
     else mask_launch(dq ? k_run_mask<RM_MASK_UNROLL, true> : k_run_mask<RM_MASK_UNROLL, false>, "k_run_mask");
