@@ -1873,13 +1873,19 @@ struct FlatRec {
 // VERIFY (the speculation launched without the pre-pass's kinds and path
 // lengths): the pass also checks that every op is an Add whose path is
 // path[i] alone (kind, and path_off[i] == i), else DevResult::spec_fail.
-template <bool SIMPLE, bool VERIFY>
+// SPEC (the flat speculation's instance): log_to_tree, no per-op replica
+// tracking, the range table in LDS — the other cases' branches compiled out.
+template <bool SIMPLE, bool VERIFY, bool SPEC = false>
 __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_t Q, FlatRec fr,
                                                     long long ts0, uint32_t* rtab, DevResult* dres,
                                                     uint32_t track_rep, uint32_t nrep, TreeDev T,
                                                     uint32_t log_to_tree) {
   Q = fr.q(Q);
   nrep = fr.nrep(nrep);
+  if (SPEC) {
+    log_to_tree = 1;
+    track_rep = 0;
+  }
   // dynamic LDS: the replica range table (nrep ids: {base, min, max counter}
   // in one 16-byte entry, one LDS read per lookup) when it fits, else
   // lookups go to the global table; rv when track_rep
@@ -1894,7 +1900,7 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
     for (uint32_t j = threadIdx.x; j < REP_DIRECT; j += blockDim.x) rv[j] = 0;
   __syncthreads();
   auto slot = [&](long long ts) -> uint32_t {
-    if (!nrep) return tsindex_slot(x, ts);
+    if (!SPEC && !nrep) return tsindex_slot(x, ts);
     if (ts <= 0) return NONE;
     const uint64_t r = static_cast<uint64_t>(ts) >> 32;
     if (r >= nrep) return NONE;
@@ -3778,7 +3784,10 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   const uint32_t shm = (4 * nrep + (nrep ? 0 : REP_DIRECT)) * sizeof(uint32_t);
   // (devq: k_pre_ts has checked the kinds and offsets; k_fl_claim<true, true> checks them itself)
   static const uint32_t claim_grid = env_grid("CRDTM_CLAIM_GRID", 2048) & ~7u;  // (XCD chunks: a multiple of 8)
-  if (simple)
+  if (simple && spec && devq && nrep)
+    LAUNCH((k_fl_claim<true, false, true>), dim3(std::min(quad_grid(n), std::max(8u, claim_grid))), dim3(BLOCK), shm,
+           s, o, ix, Q, fb.fr, t->timestamp, c->rtab, dr, 0u, nrep, t->d, 1u);
+  else if (simple)
     LAUNCH((k_fl_claim<true, false>), dim3(std::min(quad_grid(n), std::max(8u, claim_grid))), dim3(BLOCK), shm, s, o,
            ix, Q, fb.fr, t->timestamp,
            c->rtab, dr, nrep ? 0u : 1u, nrep, t->d, spec ? 1u : 0u);
