@@ -5,6 +5,7 @@
 #include <unordered_map>
 
 #include "engine.h"
+#include "../../include/crdtm_test.h"  // (test-only entry points, gated by CRDTM_TEST_HOOKS)
 
 using namespace crdtm;
 
@@ -473,7 +474,6 @@ int crdtm_apply(crdtm_tree* t, const crdtm_ops* ops, int ops_on_device, int is_b
       }
       g_prof = nullptr;
       if (r != CRDTM_OK) {
-        t->doc_valid = false;
         r = CRDTM_OK;
       }
     }
@@ -663,7 +663,7 @@ int crdtm_tree_document(const crdtm_tree* tc, uint32_t* vals, uint64_t cap, uint
 }
 
 int crdtm_debug_poke(crdtm_tree* t, int field, uint64_t index, uint32_t value) {
-  if (!t) return CRDTM_E_ARG;
+  if (!t || !test_hooks()) return CRDTM_E_ARG;
   uint32_t* a = field == 0 ? t->d.s_next : field == 1 ? t->d.s_child : field == 2 ? t->d.s_dict
               : field == 3 ? t->d.d_sent : nullptr;
   const uint64_t lim = field == 3 ? t->n_dicts : t->n_slots;
@@ -673,6 +673,10 @@ int crdtm_debug_poke(crdtm_tree* t, int field, uint64_t index, uint32_t value) {
   HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
   HIP_CHECK(hipMemcpy(a + index, &value, sizeof(value), hipMemcpyHostToDevice));
   ++t->version;  // (the host caches of this version are stale)
+  // (and no merge path may trust the device indexes of the poked state)
+  t->kidx_valid = false;
+  t->ilr_valid = false;
+  t->flat_clean = false;
   return CRDTM_OK;
 }
 

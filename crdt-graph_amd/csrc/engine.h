@@ -262,7 +262,12 @@ struct FillList {
   uint64_t bytes[MAX];
   uint32_t pat[MAX];
   int n = 0;
+  bool overflow = false;  // (an add past MAX: launch() returns E_ARG, nothing was written past the arrays)
   void add(void* q, uint64_t b, uint32_t v) {
+    if (n >= MAX) {
+      overflow = true;
+      return;
+    }
     p[n] = q;
     bytes[n] = b;
     pat[n] = v;
@@ -304,6 +309,16 @@ struct PdrIn {
   const uint32_t* dtime;   // node -> first Delete that tombstoned it
   uint32_t maxlen;
 };
+
+// Test hooks (crdtm_debug_poke, fault injection, debug dumps) act only when
+// the process sets CRDTM_TEST_HOOKS=1; a production caller never reaches them.
+inline bool test_hooks() {
+  static const bool on = [] {
+    const char* e = getenv("CRDTM_TEST_HOOKS");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 
 // internal: a path that cannot run inside an incremental re-merge asks the
 // caller to replay the batch incrementally on the untouched state instead

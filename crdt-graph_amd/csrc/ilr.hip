@@ -1598,9 +1598,9 @@ int ilr_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* res
   // (test hook, env CRDTM_ILR_FAIL_COMMIT=<token>: the first commit that
   // sees a new token fails here with an arena overflow, so the tests can
   // check the rollback and crdtm_apply's retry)
-  static std::string fail_token;
+  static thread_local std::string fail_token;
   try {
-    const char* fe = getenv("CRDTM_ILR_FAIL_COMMIT");
+    const char* fe = test_hooks() ? getenv("CRDTM_ILR_FAIL_COMMIT") : nullptr;
     if (fe && fe[0] && fail_token != fe) {
       fail_token = fe;
       throw ArenaOverflow(ws.cap + 1);

@@ -1410,7 +1410,8 @@ int finc_apply(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_result* re
   // wave's other three)
   LAUNCH(k_fi_gap, dim3(grid_for(64ULL * m)), dim3(BLOCK), 0, s, m, Kp, X.bdk, X.bmin, X.smin, X.tmin, sta[0],
          thr[0], gk[0], gv[0], (rounds && jump_chunks) ? jx : nullptr, jm);
-  static const char* dump = getenv("CRDTM_FI_DUMP_KEYS");  // (debug: one batch's gap keys, for tools/xbench_sort.py)
+  // (test hook: one batch's gap keys, for tools/xbench_sort.py)
+  static const char* dump = test_hooks() ? getenv("CRDTM_FI_DUMP_KEYS") : nullptr;
   if (dump && *dump) {
     std::vector<uint32_t> hk(m);
     HIP_CHECK(hipMemcpyAsync(hk.data(), gk[0], m * sizeof(uint32_t), hipMemcpyDeviceToHost, s));

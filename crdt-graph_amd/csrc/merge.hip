@@ -3953,10 +3953,7 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
     if (qcap + 2 < (1ULL << FR_ABITS) - 1) {
       LAUNCH(k_dres_init, dim3(1), dim3(64), 0, s, dr);
       // (env CRDTM_PRE_GRID: workgroups; CRDTM_PRE_BLIND=1: no-return atomics only)
-      static const uint32_t pre_grid = [] {
-        const char* e = getenv("CRDTM_PRE_GRID");
-        return e ? static_cast<uint32_t>(atoi(e)) : 256u;  // (256 x 1024 threads: 55 -> 48 us at flat10m)
-      }();
+      static const uint32_t pre_grid = env_grid("CRDTM_PRE_GRID", 256);  // (256 x 1024 threads: 55 -> 48 us at flat10m)
       static const bool pre_blind = [] {
         const char* e = getenv("CRDTM_PRE_BLIND");
         return e && e[0] == '1';

@@ -627,8 +627,12 @@ __global__ void __launch_bounds__(BLOCK) k_fill_batch(FillArgs a) {
 }
 
 int FillList::launch(hipStream_t s) {
+  if (overflow || n > MAX) {
+    n = 0;
+    overflow = false;
+    return CRDTM_E_ARG;
+  }
   if (n == 0) return CRDTM_OK;
-  if (n > MAX) return CRDTM_E_ARG;
   FillArgs a;
   uint64_t mx = 0;
   for (int k = 0; k < n; ++k) {

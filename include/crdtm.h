@@ -264,13 +264,6 @@ void crdtm_free(void *p);
  * this context collected them, else 0 (out zeroed). */
 int crdtm_ctx_guard_stats(crdtm_ctx *ctx, uint64_t *out);
 
-/* ---- test hook: overwrite one word of the device state (field: 0 s_next,
- * 1 s_child, 2 s_dict, 3 d_sent) so the tests can check that the host
- * readers (crdtm_tree_canonical, crdtm_tree_walk) refuse an unsound state
- * with CRDTM_E_STATE instead of following a bad index. Not part of the
- * reference surface; never needed by a caller. */
-int crdtm_debug_poke(crdtm_tree *tree, int field, uint64_t index, uint32_t value);
-
 /* ---- profiling: per-kernel device time of the last apply (HIP events) ---- */
 /* Returns the number of named phases; fills names (NUL-separated) and ms. */
 int crdtm_ctx_profile(crdtm_ctx *ctx, int enable);

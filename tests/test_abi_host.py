@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def header_functions():
-    txt = open(os.path.join(ROOT, "include", "crdtm.h")).read()
+    txt = "".join(open(os.path.join(ROOT, "include", h)).read() for h in ("crdtm.h", "crdtm_test.h"))
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(crdtm_\w+)\s*\(", txt)))
 
