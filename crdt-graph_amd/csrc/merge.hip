@@ -1098,12 +1098,15 @@ __global__ void __launch_bounds__(BLOCK) k_euler(OpsDev o, Work w, const uint32_
   }
 }
 
+// order[rank] = {node, its dict owner} (NONE for the sentinels): k_next
+// takes the dict of the node after a subtree with the node itself, one
+// gather instead of two
 __global__ void __launch_bounds__(BLOCK) k_order(OpsDev o, Work w, const uint8_t* sp,
-                                                 const unsigned long long* excl, uint32_t* order) {
+                                                 const unsigned long long* excl, uint2* order) {
   const uint32_t n = o.n, U = n + 2;
   GRID_STRIDE(v, U) {
     if (!doc_present(o, w, sp, v)) continue;
-    order[static_cast<uint32_t>(excl[2 * v] >> 32)] = v;
+    order[static_cast<uint32_t>(excl[2 * v] >> 32)] = make_uint2(v, v < n ? w.addpar[v] : NONE);
   }
 }
 
@@ -1111,18 +1114,21 @@ __global__ void __launch_bounds__(BLOCK) k_order(OpsDev o, Work w, const uint8_t
 // of x, else the pre-order successor of x's whole subtree when that node
 // lives in the same dict.
 __global__ void __launch_bounds__(BLOCK) k_next(OpsDev o, Work w, const unsigned long long* excl,
-                                                const uint32_t* order, const uint32_t* f1, uint32_t* nextn) {
+                                                const uint2* order, const uint32_t* f1, uint32_t* nextn) {
   const uint32_t n = o.n;
   // tour nodes = enter-weights before leave(super root)
   const uint32_t total = static_cast<uint32_t>(excl[2 * (n + 1) + 1] >> 32);
   GRID_STRIDE(x, n) {
     if (o.kind[x] != CRDTM_ADD || w.st[x] != ST_APPLIED) continue;
-    uint32_t y = f1[x];
+    uint32_t y = f1[x];  // (the first ep-child: in x's own dict)
     if (y == NONE) {
       const uint32_t j = static_cast<uint32_t>(excl[2 * x + 1] >> 32);
-      y = j < total ? order[j] : NONE;
+      if (j < total) {
+        const uint2 e = order[j];
+        y = e.y == w.addpar[x] ? e.x : NONE;
+      }
     }
-    nextn[x] = (y < n && w.addpar[y] == w.addpar[x]) ? y : NONE;
+    nextn[x] = y;
   }
 }
 
@@ -3783,7 +3789,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
   const uint32_t nrep = maxr + 1 <= HOST_RANGES && maxr + 1 <= 3840 ? maxr + 1 : 0u;
   const uint32_t shm = (4 * nrep + (nrep ? 0 : REP_DIRECT)) * sizeof(uint32_t);
   // (devq: k_pre_ts has checked the kinds and offsets; k_fl_claim<true, true> checks them itself)
-  static const uint32_t claim_grid = env_grid("CRDTM_CLAIM_GRID", 2048) & ~7u;  // (XCD chunks: a multiple of 8)
+  static const uint32_t claim_grid = env_grid("CRDTM_CLAIM_GRID", 1024) & ~7u;  // (XCD chunks: a multiple of 8; 1,024 after the LDS staging: 0.610 -> 0.604 ms at flat10m)
   if (simple && spec && devq && nrep)
     LAUNCH((k_fl_claim<true, false, true>), dim3(std::min(quad_grid(n), std::max(8u, claim_grid))), dim3(BLOCK), shm,
            s, o, ix, Q, fb.fr, t->timestamp, c->rtab, dr, 0u, nrep, t->d, 1u);
@@ -4247,7 +4253,7 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   unsigned long long* excl = ws.alloc<unsigned long long>(E);
   LAUNCH(k_euler, dim3(gU), dim3(BLOCK), 0, s, o, w, anc, sp, fc, ns, ent);
   if ((r = list_rank_packed(ent, E, 2 * (n + 1), excl, ws, s))) return r;
-  uint32_t* order = ws.alloc<uint32_t>(U);
+  uint2* order = ws.alloc<uint2>(U);
   uint32_t* nextn = ws.alloc<uint32_t>(n);
   LAUNCH(k_order, dim3(gU), dim3(BLOCK), 0, s, o, w, sp, excl, order);
   LAUNCH(k_next, dim3(g), dim3(BLOCK), 0, s, o, w, excl, order, f1, nextn);
