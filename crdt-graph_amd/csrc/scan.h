@@ -31,6 +31,58 @@ __device__ __forceinline__ void ds_store(unsigned long long* p, unsigned long lo
 
 constexpr uint32_t DS_EPOCH_MASK = (1u << 30) - 1;
 
+// The look-back of tile `tile` with aggregate `agg`, by one whole wave: it
+// publishes the aggregate, folds the predecessors' words (64 at a time, from
+// the farthest lane down to the nearest, in front of the nearer windows'
+// prefix) until it meets an inclusive prefix, publishes its own, and returns
+// the exclusive prefix (in every lane).
+template <class OP>
+__device__ __forceinline__ uint32_t ds_lookback(unsigned long long* status, uint32_t tile, uint32_t agg,
+                                                uint32_t epoch, uint32_t* err) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long ep = static_cast<unsigned long long>(epoch) << 32;
+  uint32_t prefix = OP::id();
+  if (tile == 0) {
+    if (lane == 0) ds_store(&status[0], (2ULL << 62) | ep | agg);
+    return prefix;
+  }
+  if (lane == 0) ds_store(&status[tile], (1ULL << 62) | ep | agg);
+  long long j = static_cast<long long>(tile) - 1;
+  uint32_t spins = 0;
+  for (;;) {
+    const long long idx = j - lane;
+    const unsigned long long s = idx >= 0 ? ds_load(&status[idx]) : ((2ULL << 62) | ep | OP::id());
+    const uint32_t flag = ((s >> 32) & DS_EPOCH_MASK) == epoch ? static_cast<uint32_t>(s >> 62) : 0u;
+    const uint32_t val = static_cast<uint32_t>(s);
+    const unsigned long long pm = __ballot(flag == 2), im = __ballot(flag == 0);
+    uint32_t upto = 64;  // lanes that contribute
+    if (pm) upto = __ffsll(static_cast<long long>(pm));  // lowest prefix lane p -> lanes 0..p
+    const unsigned long long need = upto == 64 ? ~0ULL : ((1ULL << upto) - 1);
+    if (im & need) {
+      if (++spins > (1u << 24)) {  // bounded: never hang the device
+        if (lane == 0) atomicOr(err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    // lane j holds tile (tile - 1 - j): fold from the farthest lane down
+    // to lane 0 (the nearest), then in front of the nearer windows' prefix
+    uint32_t c = static_cast<uint32_t>(lane) < upto ? val : OP::id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_down(c, o, 64);
+      if (lane + o < 64) c = OP::op(t, c);
+    }
+    c = __shfl(c, 0, 64);
+    prefix = OP::op(c, prefix);
+    if (pm) break;
+    j -= 64;
+  }
+  if (lane == 0) ds_store(&status[tile], (2ULL << 62) | ep | OP::op(prefix, agg));
+  return prefix;
+}
+
 template <class OP, bool INCL, class GEN>
 __global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* out, uint64_t n,
                                                  unsigned long long* __restrict__ status, uint32_t* __restrict__ ticket,
@@ -42,7 +94,6 @@ __global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* out, uint64_
   // accesses (a lane's DS_ITEMS consecutive items would otherwise make every
   // vector load/store instruction touch one 16-byte piece of 64 lines)
   __shared__ __attribute__((aligned(16))) uint32_t sx[DS_TILE];
-  const unsigned long long ep = static_cast<unsigned long long>(epoch) << 32;
   // a device-side item count (<= n): the workgroups past its tiles leave
   // before drawing a ticket (the host launches for n: a launch sized for 10M
   // slots over 1M runs had 1,100 idle workgroups serialising ~12 ns each on
@@ -104,45 +155,7 @@ __global__ void __launch_bounds__(BLOCK) k_dscan(GEN gen, uint32_t* out, uint64_
   }
   texcl = OP::op(wpre, texcl);
   if (wave == 0) {
-    uint32_t prefix = OP::id();
-    if (tile == 0) {
-      if (lane == 0) ds_store(&status[0], (2ULL << 62) | ep | agg);
-    } else {
-      if (lane == 0) ds_store(&status[tile], (1ULL << 62) | ep | agg);
-      long long j = static_cast<long long>(tile) - 1;
-      uint32_t spins = 0;
-      for (;;) {
-        const long long idx = j - lane;
-        const unsigned long long s = idx >= 0 ? ds_load(&status[idx]) : ((2ULL << 62) | ep | OP::id());
-        const uint32_t flag = ((s >> 32) & DS_EPOCH_MASK) == epoch ? static_cast<uint32_t>(s >> 62) : 0u;
-        const uint32_t val = static_cast<uint32_t>(s);
-        const unsigned long long pm = __ballot(flag == 2), im = __ballot(flag == 0);
-        uint32_t upto = 64;  // lanes that contribute
-        if (pm) upto = __ffsll(static_cast<long long>(pm));  // lowest prefix lane p -> lanes 0..p
-        const unsigned long long need = upto == 64 ? ~0ULL : ((1ULL << upto) - 1);
-        if (im & need) {
-          if (++spins > (1u << 24)) {  // bounded: never hang the device
-            if (lane == 0) atomicOr(err, 1u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        // lane j holds tile (tile - 1 - j): fold from the farthest lane down
-        // to lane 0 (the nearest), then in front of the nearer windows' prefix
-        uint32_t c = static_cast<uint32_t>(lane) < upto ? val : OP::id();
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t t = __shfl_down(c, o, 64);
-          if (lane + o < 64) c = OP::op(t, c);
-        }
-        c = __shfl(c, 0, 64);
-        prefix = OP::op(c, prefix);
-        if (pm) break;
-        j -= 64;
-      }
-      if (lane == 0) ds_store(&status[tile], (2ULL << 62) | ep | OP::op(prefix, agg));
-    }
+    const uint32_t prefix = ds_lookback<OP>(status, tile, agg, epoch, err);
     if (lane == 0) {
       s_prefix = prefix;
       if (total && tile == ntiles - 1) *total = OP::op(prefix, agg);
