@@ -1,18 +1,21 @@
 #!/bin/bash
-# Refreshes every workload's bench line (default steps, CPU baseline on this
-# host), rocprofv3 kernel stats and FETCH/WRITE PMC summaries on the GPU box:
-#   tools/gpu_profiles.sh <tag> [workload ...]
-# Outputs gpurun_out/<tag>_<w>_{bench.log,kernel_stats.csv,pmc.json,pmc_summary.txt}
-set -euo pipefail
+# A round's judged evidence for some workloads, on the GPU box (through gpurun):
+#   tools/gpu_profiles.sh <round tag> <workload> [workload ...]
+# per workload: the default bench line (live PMC traffic, CPU baseline) in
+# gpurun_out/<tag>_<w>_bench.log, then tools/profile_workload.sh (kernel trace
+# and stats, FETCH_SIZE / WRITE_SIZE passes, the per-kernel PMC summary) and
+# the last step's timeline (tools/timeline.py). Copy what is judged into
+# profiles/ afterwards.
+set -o pipefail
 export TMPDIR=/tmp
-T=$1; shift
-WS=${*:-flat10m deep10m cfg2 trees cfg1 incr}
+R=$1; shift
 O=gpurun_out
 mkdir -p $O
-for w in $WS; do
-  timeout -k 10 400 python3 -u bench.py --workload $w > $O/${T}_${w}_bench.log 2>&1
-  if [ "$w" != cfg1 ] && [ "$w" != incr ]; then
-    bash tools/profile_workload.sh $T $w
-    cp $O/${T}_prof_$w.log $O/${T}_${w}_prof_bench.log
-  fi
+for w in "$@"; do
+  timeout -k 10 400 python3 -u bench.py --workload $w > $O/${R}_${w}_bench.log 2>&1 || { echo "FAIL bench $w"; tail -5 $O/${R}_${w}_bench.log; exit 1; }
+  echo "$w $(grep -o '"ms_per_step": [0-9.]*' $O/${R}_${w}_bench.log | head -1)"
+  bash tools/profile_workload.sh $R $w || { echo "FAIL profile $w"; exit 1; }
+  m=k_dres_init
+  python3 tools/timeline.py $O/${R}_prof_$w/run_kernel_trace.csv $m -2 > $O/${R}_${w}_timeline.txt 2>&1 || true
+  tail -1 $O/${R}_${w}_timeline.txt
 done
