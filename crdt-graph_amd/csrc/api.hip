@@ -203,7 +203,7 @@ int crdtm_ctx_create(int device, void* stream, crdtm_ctx** out) {
   HIP_CHECK(hipMalloc(&c->crange, RID_SLOTS * sizeof(uint2)));
   HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->crange), -1, 2ULL * RID_SLOTS, c->stream));
   HIP_CHECK(hipMemset2DAsync(reinterpret_cast<char*>(c->crange) + 4, 8, 0, 4, RID_SLOTS, c->stream));
-  c->ws.scan_cap = 1u << 22;  // (32 MB: also a radix pass's tile words, 256 per tile)
+  c->ws.scan_cap = 1u << 20;
   HIP_CHECK(hipMalloc(&c->ws.scan_status, (c->ws.scan_cap + 2) * sizeof(unsigned long long)));
   HIP_CHECK(hipMemsetAsync(c->ws.scan_status, 0, (c->ws.scan_cap + 2) * sizeof(unsigned long long), c->stream));
   c->ws.scan_ticket = reinterpret_cast<uint32_t*>(c->ws.scan_status + c->ws.scan_cap);

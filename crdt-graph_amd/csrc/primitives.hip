@@ -576,206 +576,13 @@ __global__ void __launch_bounds__(BLOCK) k_rs_scatter(const uint32_t* __restrict
   }
 }
 
-// Round 6: every pass's digit histogram from one read of the keys (the counts
-// of a digit over the whole input do not depend on the order a pass receives
-// it in), pass-major then digit-major over the tiles: one scan gives pass 0
-// its (digit, tile) bases as before and every later pass the global base of
-// each digit (the scanned value at (p, d, tile 0), less p x n).
-constexpr uint32_t RS_MAXP = 4;
-__global__ void __launch_bounds__(BLOCK) k_rs_hist_all(const uint32_t* __restrict__ keys, const uint32_t* n_dev,
-                                                       uint32_t npass, uint32_t* __restrict__ hist,
-                                                       uint32_t* __restrict__ hn) {
-  __shared__ uint32_t h[RS_MAXP][256];
-  const uint32_t n = *n_dev;
-  const uint32_t nt = rs_tiles(n);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *hn = npass * 256 * nt;
-  if (blockIdx.x >= nt) return;
-  for (uint32_t j = threadIdx.x; j < RS_MAXP * 256; j += BLOCK) h[j >> 8][j & 255] = 0;
-  __syncthreads();
-  const uint32_t base = blockIdx.x * RS_TILE;
-  uint32_t k[RS_ITEMS];
-#pragma unroll
-  for (uint32_t j = 0; j < RS_ITEMS; ++j) {
-    const uint32_t i = base + j * BLOCK + threadIdx.x;
-    k[j] = i < n ? keys[i] : 0u;
-  }
-#pragma unroll
-  for (uint32_t j = 0; j < RS_ITEMS; ++j)
-    if (base + j * BLOCK + threadIdx.x < n)
-      for (uint32_t p = 0; p < npass; ++p) atomicAdd(&h[p][(k[j] >> (8 * p)) & 255u], 1u);
-  __syncthreads();
-  for (uint32_t p = 0; p < npass; ++p) hist[(p * 256 + threadIdx.x) * nt + blockIdx.x] = h[p][threadIdx.x];
-}
-
-// A later pass in one launch (onesweep): each tile ranks its items as
-// k_rs_scatter does, publishes its per-digit counts, and the thread of digit d
-// looks back over the earlier tiles' words for d (decoupled look-back, the
-// status pool and epochs of scan.h: agent-scope words {flag, epoch, count},
-// tiles by ticket so that every predecessor has started). Base of an item =
-// the digit's global base + the digit's count in earlier tiles + its rank.
-__global__ void __launch_bounds__(BLOCK) k_rs_onesweep(const uint32_t* __restrict__ keys,
-                                                       const uint32_t* __restrict__ vals, const uint32_t* n_dev,
-                                                       uint32_t pass, const uint32_t* __restrict__ hist,
-                                                       unsigned long long* __restrict__ status,
-                                                       uint32_t* __restrict__ ticket, uint32_t epoch,
-                                                       uint32_t* __restrict__ err, uint32_t* __restrict__ kout,
-                                                       uint32_t* __restrict__ vout, uint32_t* __restrict__ inv) {
-  constexpr uint32_t NW = BLOCK / 64;
-  static_assert(BLOCK == 256, "one digit per thread");
-  __shared__ uint32_t wc[RS_ITEMS][NW][256];
-  __shared__ uint32_t s_tile;
-  const uint32_t n = *n_dev;
-  const uint32_t nt = rs_tiles(n);
-  if (blockIdx.x >= nt) return;  // (before the ticket: the launch covers n_max)
-  if (threadIdx.x == 0) {
-    s_tile = atomicAdd(ticket, 1u);
-    if (s_tile == nt - 1) atomicExch(ticket, 0u);  // every ticket drawn: ready for the next user
-  }
-  const uint32_t shift = 8 * pass, d = threadIdx.x;
-  // the digit's global base (its pass's scanned histogram at tile 0)
-  const uint32_t gofs = hist[(pass * 256 + d) * nt] - pass * n;
-#pragma unroll
-  for (uint32_t j = 0; j < RS_ITEMS; ++j)
-#pragma unroll
-    for (uint32_t w = 0; w < NW; ++w) wc[j][w][threadIdx.x] = 0;
-  __syncthreads();
-  const uint32_t t = s_tile;
-  const uint32_t base = t * RS_TILE;
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const unsigned long long lt = (1ULL << lane) - 1ULL;
-  uint32_t ka[RS_ITEMS], va[RS_ITEMS];
-#pragma unroll
-  for (uint32_t j = 0; j < RS_ITEMS; ++j) {
-    const uint32_t i = base + j * BLOCK + threadIdx.x;
-    ka[j] = i < n ? keys[i] : 0u;
-    va[j] = i < n ? vals[i] : 0u;
-  }
-  uint32_t lr[RS_ITEMS];
-#pragma unroll
-  for (uint32_t j = 0; j < RS_ITEMS; ++j) {
-    const bool valid = base + j * BLOCK + threadIdx.x < n;
-    const uint32_t dg = (ka[j] >> shift) & 255u;
-    unsigned long long m = __ballot(valid);
-#pragma unroll
-    for (uint32_t b = 0; b < 8; ++b) {
-      const unsigned long long bb = __ballot((dg >> b) & 1u);
-      m &= ((dg >> b) & 1u) ? bb : ~bb;
-    }
-    lr[j] = static_cast<uint32_t>(__popcll(m & lt));
-    if (valid && lr[j] == 0) wc[j][wv][dg] = static_cast<uint32_t>(__popcll(m));
-  }
-  __syncthreads();
-  uint32_t cnt = 0;  // thread = digit: the tile-local exclusive prefix in item order, then the tile's count
-#pragma unroll
-  for (uint32_t j = 0; j < RS_ITEMS; ++j)
-#pragma unroll
-    for (uint32_t w = 0; w < NW; ++w) {
-      const uint32_t c = wc[j][w][d];
-      wc[j][w][d] = cnt;
-      cnt += c;
-    }
-  const unsigned long long ep = static_cast<unsigned long long>(epoch) << 32;
-  unsigned long long* srow = status + static_cast<uint64_t>(t) * 256;
-  uint32_t excl = 0;
-  if (t == 0) {
-    ds_store(&srow[d], (2ULL << 62) | ep | cnt);
-  } else {
-    ds_store(&srow[d], (1ULL << 62) | ep | cnt);
-    // a window of RS_LB predecessors per round trip (measured: 29-31 us per
-    // pass with or without it, the chain of aggregates is the bound)
-    constexpr int RS_LB = 8;
-    uint32_t spins = 0;
-    for (long long j = static_cast<long long>(t) - 1;;) {
-      unsigned long long sv[RS_LB];
-#pragma unroll
-      for (int k = 0; k < RS_LB; ++k) {
-        const long long idx = j - k;
-        sv[k] = idx >= 0 ? ds_load(&status[static_cast<uint64_t>(idx) * 256 + d]) : ((2ULL << 62) | ep);
-      }
-      uint32_t acc = 0;
-      int state = 0;  // 0: all aggregates, 1: met a prefix, 2: a word not yet published
-#pragma unroll
-      for (int k = 0; k < RS_LB; ++k) {
-        if (state) continue;
-        const unsigned long long s = sv[k];
-        const uint32_t flag = ((s >> 32) & DS_EPOCH_MASK) == epoch ? static_cast<uint32_t>(s >> 62) : 0u;
-        if (flag == 0) {
-          state = 2;
-        } else {
-          acc += static_cast<uint32_t>(s);
-          if (flag == 2) state = 1;
-        }
-      }
-      if (state == 2) {
-        if (++spins > (1u << 24)) {  // bounded: never hang the device
-          atomicOr(err, 1u);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      excl += acc;
-      if (state == 1) break;
-      j -= RS_LB;
-    }
-    ds_store(&srow[d], (2ULL << 62) | ep | (excl + cnt));
-  }
-  const uint32_t add = gofs + excl;
-#pragma unroll
-  for (uint32_t j = 0; j < RS_ITEMS; ++j)
-#pragma unroll
-    for (uint32_t w = 0; w < NW; ++w) wc[j][w][d] += add;
-  __syncthreads();
-#pragma unroll
-  for (uint32_t j = 0; j < RS_ITEMS; ++j) {
-    if (base + j * BLOCK + threadIdx.x >= n) continue;
-    const uint32_t pos = wc[j][wv][(ka[j] >> shift) & 255u] + lr[j];
-    kout[pos] = ka[j];
-    vout[pos] = va[j];
-    if (inv) inv[va[j]] = pos;
-  }
-}
-
 // Sorts n_dev (<= n_max) pairs by the low `bits` bits of the keys, stably.
 // The result lands in (k0, v0) when the pass count is even, else in (k1, v1):
 // *out_k / *out_v point to it. inv (optional, values < n_max): inv[v] = the
 // sorted position of value v, written by the last pass.
-// (measured in round 6 and left off, env CRDTM_RS_ONESWEEP=1: 2 + passes
-// launches — every histogram, one scan, pass 0's scatter, the later passes
-// onesweep — instead of 3 per pass. Every tile of a 1M-key sort is resident
-// at once, so all reach their look-back together and the prefixes resolve
-// down a chain of aggregates: 30 us per onesweep pass against 28 for hist +
-// scan + scatter; flat10m 0.626 against 0.620 ms, deep10m 5.58 against 5.47.)
 int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, const uint32_t* n_dev, uint32_t n_max,
                      uint32_t bits, Arena& ws, hipStream_t st, uint32_t** out_k, uint32_t** out_v, uint32_t* inv) {
   const uint32_t ntiles = std::max<uint32_t>(1, (n_max + RS_TILE - 1) / RS_TILE);
-  const uint32_t npass = (bits + 7) / 8;
-  static const bool onesweep = [] {
-    const char* e = getenv("CRDTM_RS_ONESWEEP");
-    return e && e[0] == '1';
-  }();
-  if (onesweep && npass >= 2 && npass <= RS_MAXP && ws.scan_status && 256ULL * ntiles <= ws.scan_cap) {
-    const uint64_t hlen = 256ULL * npass * ntiles;
-    uint32_t* hist = ws.alloc<uint32_t>(hlen + 2);
-    uint32_t* hn = hist + hlen + 1;  // npass x 256 x the tiles that hold items (device)
-    LAUNCH(k_rs_hist_all, dim3(ntiles), dim3(BLOCK), 0, st, k0, n_dev, npass, hist, hn);
-    int r = dscan<SumOp, false>(ArrGen{hist}, hist, hlen, nullptr, ws, st, nullptr, hn);
-    if (r) return r;
-    uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
-    LAUNCH(k_rs_scatter, dim3(ntiles), dim3(BLOCK), 0, st, ki, vi, n_dev, 0u, hist, ko, vo, nullptr);
-    std::swap(ki, ko);
-    std::swap(vi, vo);
-    for (uint32_t p = 1; p < npass; ++p) {
-      ws.scan_epoch = (ws.scan_epoch % DS_EPOCH_MASK) + 1;
-      LAUNCH(k_rs_onesweep, dim3(ntiles), dim3(BLOCK), 0, st, ki, vi, n_dev, p, hist, ws.scan_status,
-             ws.scan_ticket, ws.scan_epoch, ws.scan_err, ko, vo, p + 1 == npass ? inv : nullptr);
-      std::swap(ki, ko);
-      std::swap(vi, vo);
-    }
-    *out_k = ki;
-    *out_v = vi;
-    return CRDTM_OK;
-  }
   uint32_t* hist = ws.alloc<uint32_t>(256ULL * ntiles + 2);
   uint32_t* hn = hist + 256ULL * ntiles + 1;  // 256 x the tiles that hold items (device)
   uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
