@@ -244,78 +244,77 @@ __global__ void __launch_bounds__(64) k_forest_wave(const uint32_t* doc_off, uin
   uint32_t vw = lane < nops ? opw[ob + lane] : 0u;
   for (uint32_t c0 = 0; c0 < nops; c0 += 64) {
     const uint32_t nxt = c0 + 64 + lane < nops ? opw[ob + c0 + 64 + lane] : 0u;  // next 64 op words, in flight
-    const uint32_t kend = min(64u, nops - c0);
+    const uint32_t kend = wuni(min(64u, nops - c0));
     for (uint32_t k = 0; k < kend; ++k) {
       const uint32_t w = __builtin_amdgcn_readlane(vw, k);
       const uint32_t t = w & FL_N;
       const uint32_t st = rd(t);
+      // (if/else instead of `continue`, errors leave by goto: the loop keeps
+      // no exit-code dispatch between ops)
       if (wuni(w & (FO_DEL | FO_INV))) {
         if (wuni((w & FO_INV) | ((st & FW_PRESENT) ^ FW_PRESENT))) {  // InvalidPath / deleteHelp NotFound (:112-122)
           err = c0 + k;
           code = (w & FO_INV) ? CRDTM_INVALID_PATH : CRDTM_OPERATION_FAILED;
-          break;
+          goto replay_done;
         }
         if (!wuni(st & FW_TOMB)) {
           wr(t, st | FW_TOMB);
           ++applied;
         }
-        continue;
-      }
-      const uint32_t ownb = (w >> 24) & 1u;
-      if (wuni(st & FW_PRESENT)) {  // `child ts parent` exists: AlreadyApplied
-        own += ownb;
-        continue;
-      }
-      const uint32_t a = (w >> 11) & FL_N;
-      const uint32_t sa = rd(a);
-      if (!wuni(sa & FW_PRESENT)) {  // anchor missing: NotFound
-        err = c0 + k;
-        code = CRDTM_OPERATION_FAILED;
-        break;
-      }
-      const uint32_t x = t;
-      uint32_t nk = a, node = a, sn = sa;  // findInsertion (:93-104)
-      for (;;) {
-        const uint32_t rn = sn & FL_N;
-        uint32_t live = rn, wl = rd(rn);
-        while (wuni(wl & FW_TOMB)) {  // nextNode: the first live node after next
-          live = wl & FL_N;
-          wl = rd(live);
+      } else if (wuni(st & FW_PRESENT)) {  // `child ts parent` exists: AlreadyApplied
+        own += (w >> 24) & 1u;
+      } else {
+        const uint32_t a = (w >> 11) & FL_N;
+        const uint32_t sa = rd(a);
+        if (!wuni(sa & FW_PRESENT)) {  // anchor missing: NotFound
+          err = c0 + k;
+          code = CRDTM_OPERATION_FAILED;
+          goto replay_done;
         }
-        // (measured in round 5: deciding `x > rn` before rn's word is read,
-        // as the per-dict replays do, 2.61 -> 3.02 ms here; the anchor's word
-        // read beside the target's, no change)
-        if (wuni(live == FL_N || x > rn)) break;
-        nk = rn;
-        node = live;
-        sn = wl;
-      }
-      const bool same = wuni(nk == node);
-      const uint32_t snk = same ? sn : rd(nk);
-      wr(x, (sn & FL_N) | FW_PRESENT | (snk & FW_ORPHAN));
-      if (same) {
-        wr(node, (sn & ~FL_N) | x);
-      } else {  // copy quirk: slot nk := copy of node with next = x
-        if (!wuni(snk & FW_ORPHAN)) {
-          for (uint32_t q = snk & FL_N; wuni(q != FL_N);) {
-            const uint32_t sq = rd(q);
-            wr(q, sq | FW_ORPHAN);
-            if (wuni(q == node)) break;
-            q = sq & FL_N;
+        const uint32_t x = t;
+        uint32_t nk = a, node = a, sn = sa;  // findInsertion (:93-104)
+        for (;;) {
+          const uint32_t rn = sn & FL_N;
+          uint32_t live = rn, wl = rd(rn);
+          while (wuni(wl & FW_TOMB)) {  // nextNode: the first live node after next
+            live = wl & FL_N;
+            wl = rd(live);
+          }
+          // (measured in round 5: deciding `x > rn` before rn's word is read,
+          // as the per-dict replays do, 2.61 -> 3.02 ms here; the anchor's word
+          // read beside the target's, no change)
+          if (wuni(live == FL_N || x > rn)) break;
+          nk = rn;
+          node = live;
+          sn = wl;
+        }
+        const bool same = wuni(nk == node);
+        const uint32_t snk = same ? sn : rd(nk);
+        wr(x, (sn & FL_N) | FW_PRESENT | (snk & FW_ORPHAN));
+        if (same) {
+          wr(node, (sn & ~FL_N) | x);
+        } else {  // copy quirk: slot nk := copy of node with next = x
+          if (!wuni(snk & FW_ORPHAN)) {
+            for (uint32_t q = snk & FL_N; wuni(q != FL_N);) {
+              const uint32_t sq = rd(q);
+              wr(q, sq | FW_ORPHAN);
+              if (wuni(q == node)) break;
+              q = sq & FL_N;
+            }
+          }
+          wr(nk, x | FW_PRESENT | (snk & FW_ORPHAN));
+          if (lane == 0) {
+            longlong2* v = vt + static_cast<uint64_t>(d) * FL_SLOTS;
+            v[nk] = v[node];
           }
         }
-        wr(nk, x | FW_PRESENT | (snk & FW_ORPHAN));
-        if (lane == 0) {
-          longlong2* v = vt + static_cast<uint64_t>(d) * FL_SLOTS;
-          v[nk] = v[node];
-        }
+        ++applied;
+        own += (w >> 24) & 1u;  // incrementTimestamp (src/CRDTree.elm:337-343)
       }
-      ++applied;
-      own += ownb;  // incrementTimestamp (src/CRDTree.elm:337-343)
     }
-    if (code != CRDTM_OK) break;
     vw = nxt;
   }
+replay_done:
   if (lane == 0) {
     code_out[d] = code;
     err_out[d] = err;
