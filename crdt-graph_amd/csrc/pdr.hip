@@ -305,7 +305,6 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
   for (uint32_t r = lane; r <= K; r += 64) S[r] = r == 0 ? (PM | SF_TOMB | SF_MADE) : PM;
   __syncthreads();
   const uint32_t ob = rb, oe = p.rbase[D + 1] - 1;
-  bool done = false;
   // change log (original dicts big enough to be worth rebuilding snapshots from)
   const bool logging = ORIG && p.log != nullptr && K + 1 >= p.log_min;
   const uint32_t lcap = 4 * (oe + 1 - rb);
@@ -323,7 +322,7 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
   unsigned long long nx_w = ob + lane < oe ? p.opw[ob + lane] : 0ULL;
   constexpr bool gst = GST;
   uint32_t g_adds = 0, g_fail = 0, g_first = NONE;  // (guard-G statistics)
-  for (uint32_t k0 = ob; k0 < oe && !done; k0 += 64) {
+  for (uint32_t k0 = ob; k0 < oe; k0 += 64) {
     const uint32_t my_i = nx_i;
     const unsigned long long my_w = nx_w;
     const uint32_t kn = k0 + 64 + lane;
@@ -334,10 +333,7 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
       const uint32_t i = __builtin_amdgcn_readlane(my_i, j);
       const uint32_t wlo = __builtin_amdgcn_readlane(static_cast<uint32_t>(my_w), j);
       const uint32_t whi = __builtin_amdgcn_readlane(static_cast<uint32_t>(my_w >> 32), j);
-      if (i >= bound) {
-        done = true;
-        break;
-      }
+      if (!ORIG && i >= bound) goto replay_done;  // (a snapshot stops at its bound; an original dict has none)
       uint8_t s;
       if (whi >> 31) {  // deleteHelp
         const uint32_t t = wlo & PM;
@@ -472,6 +468,7 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
       if (ORIG) st[i] = s;  // uniform store
     }
   }
+replay_done:
 #ifdef PDR_STATS
   if (ORIG && lane == 0 && K > 28000)
     printf("pdr big dict K=%u ops=%u adds %llu steps %llu windows %llu tomb %llu quirks %llu cycles %lld\n", K,
@@ -570,7 +567,6 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
 #endif
   __syncthreads();
   const uint32_t ob = rb, oe = p.rbase[D + 1] - 1;
-  bool done = false;
   const bool logging = ORIG && p.log != nullptr && K + 1 >= p.log_min;
   const uint32_t lcap = 4 * (oe + 1 - rb);
   uint4* const lg = logging ? p.log + 4ULL * rb : nullptr;
@@ -717,7 +713,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
   unsigned long long nx_w = ob + lane < oe ? p.opw[ob + lane] : 0ULL;
   constexpr bool gst = GST;
   uint32_t g_adds = 0, g_fail = 0, g_first = NONE;  // (guard-G statistics, as in pdr_serial)
-  for (uint32_t k0 = ob; k0 < oe && !done; k0 += 64) {
+  for (uint32_t k0 = ob; k0 < oe; k0 += 64) {
     const uint32_t my_i = nx_i;
     const unsigned long long my_w = nx_w;
     const uint32_t kn = k0 + 64 + lane;
@@ -728,10 +724,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
       const uint32_t i = __builtin_amdgcn_readlane(my_i, jo);
       const uint32_t wlo = __builtin_amdgcn_readlane(static_cast<uint32_t>(my_w), jo);
       const uint32_t whi = __builtin_amdgcn_readlane(static_cast<uint32_t>(my_w >> 32), jo);
-      if (i >= bound) {
-        done = true;
-        break;
-      }
+      if (!ORIG && i >= bound) goto replay_done;  // (a snapshot stops at its bound; an original dict has none)
 #ifdef PDR_STATS
       const long long q_t0 = clock64();
       uint32_t q_cat = 4;
@@ -1039,6 +1032,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
 #endif
     }
   }
+replay_done:
 #ifdef PDR_STATS  // ops and cycles per kind: Delete, plain insert, copy quirk, orphan anchor, other
   if (ORIG && lane == 0 && K > 28000)
     printf("pdr blocked K=%u del %llu/%llu ins %llu/%llu quirk %llu/%llu orphan %llu/%llu other %llu/%llu | walks "
