@@ -222,6 +222,10 @@ constexpr uint32_t FLANE_REGION = FL_N + 1;
 // register and branches on it -- no exec-mask bookkeeping around divergent
 // code on the CU's one scalar unit.
 __device__ __forceinline__ uint32_t wuni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+// a wave-uniform comparison of vector values as a branch condition: the
+// compare's lane mask itself (every lane agrees), instead of a 0/1 select
+// moved to a scalar register and tested again
+__device__ __forceinline__ bool uany(bool c) { return __builtin_amdgcn_ballot_w64(c) != 0ULL; }
 
 __global__ void __launch_bounds__(64) k_forest_wave(const uint32_t* doc_off, uint32_t n_docs, long long ts0,
                                                     const uint32_t* opw, const uint16_t* sent, const uint8_t* fb,
@@ -283,22 +287,22 @@ __global__ void __launch_bounds__(64) k_forest_wave(const uint32_t* doc_off, uin
           // (measured in round 5: deciding `x > rn` before rn's word is read,
           // as the per-dict replays do, 2.61 -> 3.02 ms here; the anchor's word
           // read beside the target's, no change)
-          if (wuni(live == FL_N || x > rn)) break;
+          if (uany(live == FL_N || x > rn)) break;
           nk = rn;
           node = live;
           sn = wl;
         }
-        const bool same = wuni(nk == node);
+        const bool same = uany(nk == node);
         const uint32_t snk = same ? sn : rd(nk);
         wr(x, (sn & FL_N) | FW_PRESENT | (snk & FW_ORPHAN));
         if (same) {
           wr(node, (sn & ~FL_N) | x);
         } else {  // copy quirk: slot nk := copy of node with next = x
           if (!wuni(snk & FW_ORPHAN)) {
-            for (uint32_t q = snk & FL_N; wuni(q != FL_N);) {
+            for (uint32_t q = snk & FL_N; uany(q != FL_N);) {
               const uint32_t sq = rd(q);
               wr(q, sq | FW_ORPHAN);
-              if (wuni(q == node)) break;
+              if (uany(q == node)) break;
               q = sq & FL_N;
             }
           }
@@ -339,7 +343,7 @@ replay_done:
           nx = wn & FL_N;
           wn = rd(nx);
         }
-        if (wuni(nx == FL_N)) {
+        if (uany(nx == FL_N)) {
           more = false;
           break;
         }
