@@ -1093,8 +1093,16 @@ __global__ void __launch_bounds__(BLOCK) k_euler(OpsDev o, Work w, const uint32_
       const uint32_t p = w.addpar[v];
       vis = (w.dtime[v] == NONE && (p == n || !w.dead[p])) ? 1u : 0u;
     }
-    ent[2 * v] = make_uint2(fc[v] != NONE ? 2 * fc[v] : 2 * v + 1, 2u | vis);
-    ent[2 * v + 1] = make_uint2(after, 0u);
+    const uint32_t f = fc[v];
+    if (f == NONE && v != n + 1) {
+      // a leaf: enter goes straight on and its leave entry is off the tour
+      // (its rank = enter's + 1, k_next): ~45% fewer tour steps at deep10m
+      ent[2 * v] = make_uint2(after, 2u | vis);
+      ent[2 * v + 1] = make_uint2(ABSENT, 0u);
+    } else {
+      ent[2 * v] = make_uint2(f != NONE ? 2 * f : 2 * v + 1, 2u | vis);
+      ent[2 * v + 1] = make_uint2(after, 0u);
+    }
   }
 }
 
@@ -1122,7 +1130,10 @@ __global__ void __launch_bounds__(BLOCK) k_next(OpsDev o, Work w, const unsigned
     if (o.kind[x] != CRDTM_ADD || w.st[x] != ST_APPLIED) continue;
     uint32_t y = f1[x];  // (the first ep-child: in x's own dict)
     if (y == NONE) {
-      const uint32_t j = static_cast<uint32_t>(excl[2 * x + 1] >> 32);
+      // the tour node after x's subtree: leave x's rank, or for a leaf (its
+      // leave entry off the tour, ~0) enter's + 1 (one 16-byte load)
+      const ulonglong2 ex = *reinterpret_cast<const ulonglong2*>(excl + 2 * static_cast<uint64_t>(x));
+      const uint32_t j = ex.y != ~0ULL ? static_cast<uint32_t>(ex.y >> 32) : static_cast<uint32_t>(ex.x >> 32) + 1u;
       if (j < total) {
         const uint2 e = order[j];
         y = e.y == w.addpar[x] ? e.x : NONE;
