@@ -225,6 +225,7 @@ int crdtm_ctx_destroy(crdtm_ctx* c) {
   if (c->ws.base) hipFree(c->ws.base);
   hipFree(c->dres);
   hipHostFree(c->hres);
+  if (c->pin) hipHostFree(c->pin);
   hipFree(c->crange);
   if (c->fl_rec) hipFree(c->fl_rec);
   hipFree(c->ws.scan_status);

@@ -102,6 +102,10 @@ struct crdtm_ctx {
   int gstat_valid = 0;
   crdtm::DevResult* dres = nullptr;  // device
   crdtm::DevResult* hres = nullptr;  // pinned host
+  // pinned host staging for bulk per-call transfers (the forest's per-document
+  // tables and results: one DMA each way instead of a pageable copy per array)
+  char* pin = nullptr;
+  size_t pin_cap = 0;
   uint32_t* rtab = nullptr;          // replica table [REPLICA_SLOTS], 0 = empty (kept clean between calls)
   uint2* crange = nullptr;           // replica counter ranges [RID_SLOTS] {min, max}, kept clean between calls
   // flat merge: slot -> anchor code tagged with the merge's epoch (merge.hip

@@ -4596,12 +4596,40 @@ int linearize(crdtm_tree* t) {
 
 namespace crdtm {
 
+// the context's pinned staging buffer, at least `bytes` (grown, contents lost)
+static char* host_pinned(crdtm_ctx* c, size_t bytes) {
+  if (bytes > c->pin_cap) {
+    if (c->pin) hipHostFree(c->pin);
+    c->pin = nullptr;
+    c->pin_cap = 0;
+    const size_t cap = std::max<size_t>(bytes, 1u << 20);
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->pin), cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+    c->pin_cap = cap;
+  }
+  return c->pin;
+}
+
 int forest_apply(crdtm_ctx* c, int64_t replica_id, const OpsDev& o, const uint32_t* doc_off_host, uint64_t n_docs,
                  int32_t* code, int64_t* err, uint32_t* applied, uint64_t* vhash, uint64_t* vwords,
                  int64_t* tstamp) {
   hipStream_t s = c->stream;
   Arena& ws = c->ws;
-  std::vector<uint64_t> sb(n_docs + 1), db(n_docs + 1), hb(n_docs + 1);
+  // the per-document tables go up and the results come back through the
+  // pinned staging buffer, one copy each way: [doc_off u32 | pad | slot,
+  // dict, hash bases u64] up; [code, err, applied, overflow u32 | vhash,
+  // vwords, tstamp u64] down
+  const uint64_t N1 = n_docs + 1;
+  const size_t in_off = (N1 * 4 + 7) & ~size_t{7};
+  const size_t in_b = in_off + 3 * N1 * 8;
+  const size_t out_off = (4 * n_docs * 4 + 7) & ~size_t{7};
+  const size_t out_b = out_off + 3 * n_docs * 8;
+  char* pin = host_pinned(c, std::max(in_b, out_b));
+  if (!pin) return CRDTM_E_NOMEM;
+  memcpy(pin, doc_off_host, N1 * 4);
+  uint64_t* sb = reinterpret_cast<uint64_t*>(pin + in_off);
+  uint64_t* db = sb + N1;
+  uint64_t* hb = db + N1;
+  sb[0] = db[0] = hb[0] = 0;
   for (uint64_t d = 0; d < n_docs; ++d) {
     const uint32_t nops = doc_off_host[d + 1] - doc_off_host[d];
     sb[d + 1] = sb[d] + forest_slot_cap(nops);
@@ -4625,24 +4653,23 @@ int forest_apply(crdtm_ctx* c, int64_t replica_id, const OpsDev& o, const uint32
   f.hkey = ws.alloc<long long>(Hn);
   f.hslot = ws.alloc<uint32_t>(Hn);
   f.queue = ws.alloc<uint32_t>(2 * D);
-  uint32_t* doff = ws.alloc<uint32_t>(n_docs + 1);
-  uint64_t* dsb = ws.alloc<uint64_t>(n_docs + 1);
-  uint64_t* ddb = ws.alloc<uint64_t>(n_docs + 1);
-  uint64_t* dhb = ws.alloc<uint64_t>(n_docs + 1);
-  f.code = ws.alloc<int32_t>(n_docs);
-  f.err = ws.alloc<uint32_t>(n_docs);
-  f.applied = ws.alloc<uint32_t>(n_docs);
-  f.vhash = ws.alloc<unsigned long long>(n_docs);
-  f.vwords = ws.alloc<unsigned long long>(n_docs);
-  f.tstamp = ws.alloc<long long>(n_docs);
-  f.overflow = ws.alloc<uint32_t>(n_docs);
+  char* din = ws.alloc<char>(in_b);
+  uint32_t* doff = reinterpret_cast<uint32_t*>(din);
+  uint64_t* dsb = reinterpret_cast<uint64_t*>(din + in_off);
+  uint64_t* ddb = dsb + N1;
+  uint64_t* dhb = ddb + N1;
+  char* dout = ws.alloc<char>(out_b);
+  f.code = reinterpret_cast<int32_t*>(dout);
+  f.err = reinterpret_cast<uint32_t*>(dout) + n_docs;
+  f.applied = reinterpret_cast<uint32_t*>(dout) + 2 * n_docs;
+  f.overflow = reinterpret_cast<uint32_t*>(dout) + 3 * n_docs;
+  f.vhash = reinterpret_cast<unsigned long long*>(dout + out_off);
+  f.vwords = f.vhash + n_docs;
+  f.tstamp = reinterpret_cast<long long*>(f.vwords + n_docs);
   f.doc_off = doff;
   f.n_docs = static_cast<uint32_t>(n_docs);
   f.ts0 = replica_id * TWO32;
-  HIP_CHECK(hipMemcpyAsync(doff, doc_off_host, (n_docs + 1) * 4, hipMemcpyHostToDevice, s));
-  HIP_CHECK(hipMemcpyAsync(dsb, sb.data(), (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
-  HIP_CHECK(hipMemcpyAsync(ddb, db.data(), (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
-  HIP_CHECK(hipMemcpyAsync(dhb, hb.data(), (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(din, pin, in_b, hipMemcpyHostToDevice, s));
   uint8_t* fb = ws.alloc<uint8_t>(n_docs);
   HIP_CHECK(hipMemsetAsync(fb, 0, n_docs, s));
   uint32_t* opw = ws.alloc<uint32_t>(o.n + 1);
@@ -4653,19 +4680,20 @@ int forest_apply(crdtm_ctx* c, int64_t replica_id, const OpsDev& o, const uint32
                                   f.vwords, f.tstamp, f.overflow, s))
     return rf;
   LAUNCH(k_forest, dim3(static_cast<uint32_t>((n_docs + 63) / 64)), dim3(64), 0, s, o, f, dsb, ddb, dhb, fb);
-  std::vector<uint32_t> e(n_docs), ov(n_docs);
-  HIP_CHECK(hipMemcpyAsync(code, f.code, n_docs * 4, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipMemcpyAsync(e.data(), f.err, n_docs * 4, hipMemcpyDeviceToHost, s));
-  if (applied) HIP_CHECK(hipMemcpyAsync(applied, f.applied, n_docs * 4, hipMemcpyDeviceToHost, s));
-  if (vhash) HIP_CHECK(hipMemcpyAsync(vhash, f.vhash, n_docs * 8, hipMemcpyDeviceToHost, s));
-  if (vwords) HIP_CHECK(hipMemcpyAsync(vwords, f.vwords, n_docs * 8, hipMemcpyDeviceToHost, s));
-  if (tstamp) HIP_CHECK(hipMemcpyAsync(tstamp, f.tstamp, n_docs * 8, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipMemcpyAsync(ov.data(), f.overflow, n_docs * 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(pin, dout, out_b, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
+  const uint32_t* hc = reinterpret_cast<const uint32_t*>(pin);
+  const unsigned long long* h8 = reinterpret_cast<const unsigned long long*>(pin + out_off);
+  memcpy(code, hc, n_docs * 4);
+  if (applied) memcpy(applied, hc + 2 * n_docs, n_docs * 4);
+  if (vhash) memcpy(vhash, h8, n_docs * 8);
+  if (vwords) memcpy(vwords, h8 + n_docs, n_docs * 8);
+  if (tstamp) memcpy(tstamp, h8 + 2 * n_docs, n_docs * 8);
   int rc = CRDTM_OK;
   for (uint64_t d = 0; d < n_docs; ++d) {
-    if (err) err[d] = e[d] == NONE ? -1 : static_cast<int64_t>(e[d]);
-    if (ov[d]) {  // a document outgrew its arena (deep copies): reported, never silently wrong
+    const uint32_t e = hc[n_docs + d];
+    if (err) err[d] = e == NONE ? -1 : static_cast<int64_t>(e);
+    if (hc[3 * n_docs + d]) {  // a document outgrew its arena (deep copies): reported, never silently wrong
       code[d] = CRDTM_E_NOMEM;
       rc = CRDTM_E_NOMEM;
     }
