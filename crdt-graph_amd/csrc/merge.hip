@@ -901,9 +901,26 @@ __global__ void __launch_bounds__(BLOCK) k_stats(OpsDev o, Work w, long long ts0
 }
 
 // Per-dict guard, only when the batch interleaves Deletes before later Adds.
+// (one atomic per wave and dict: the lanes of a wave hold consecutive ops,
+// often of one dict — config 2's two big dicts took ~39k same-word atomics
+// each, 363 us; a dict's lanes are peeled off by ballot, the highest lane
+// holding the largest op index)
 __global__ void __launch_bounds__(BLOCK) k_guard_maxadd(OpsDev o, Work w) {
-  GRID_STRIDE(i, o.n) {
-    if (o.kind[i] == CRDTM_ADD && w.st[i] == ST_APPLIED) atomicMax(&w.maxadd[w.addpar[i]], i + 1);
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < o.n; i0 += gridDim.x * blockDim.x) {  // (wave-uniform trips)
+    const uint32_t i = i0 + threadIdx.x;
+    bool act = i < o.n && o.kind[i] == CRDTM_ADD && w.st[i] == ST_APPLIED;
+    const uint32_t d = act ? w.addpar[i] : NONE;
+    unsigned long long live = __ballot(act);
+    while (live) {
+      const uint32_t lead = static_cast<uint32_t>(__ffsll(static_cast<long long>(live))) - 1u;
+      const uint32_t dk = __shfl(d, static_cast<int>(lead), 64);
+      const unsigned long long same = __ballot(act && d == dk);
+      const uint32_t top = 63u - static_cast<uint32_t>(__clzll(same));
+      if (lane == top) atomicMax(&w.maxadd[dk], i + 1);
+      if (act && d == dk) act = false;
+      live &= ~same;
+    }
   }
 }
 
