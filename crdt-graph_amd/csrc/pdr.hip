@@ -1051,6 +1051,13 @@ __global__ void __launch_bounds__(64) k_pdr_blk(PdrCtx p, const uint32_t* list, 
   pdr_blocked<MODE>(p, st, list[blockIdx.x], blk_lds, lds_words);
 }
 
+// (A/B: a workgroup cap from the environment, at least 8)
+static uint32_t pdr_env_grid(const char* name, uint32_t def) {
+  const char* e = getenv(name);
+  const int g = e ? atoi(e) : 0;
+  return g >= 8 && g <= (1 << 20) ? static_cast<uint32_t>(g) : def;
+}
+
 // Sort instances [i0, i1) into three size tiers: static LDS, dynamic LDS,
 // global memory. count = {tier sizes, largest slot count of tier 1}.
 // ---- P2c: tiny dicts, one lane each ----
@@ -1174,7 +1181,9 @@ struct PdrTiers {
 // reserves it with one device atomic per tier, then writes its entries at
 // offsets kept in LDS. A counter bumped per dict, or per wave, serialises
 // ~12 ns per atomic on one word: 20 ms, then 1.5 ms, over deep10m_il's 1.6M
-// dicts. The grid is capped, so there are few workgroups; loops are
+// dicts. The grid is capped, so there are few workgroups (2,048 since round
+// 6: 512 left 2 waves per SIMD for these gathers, 0.29 against 0.20 ms at
+// deep10m_il; the same for k_pdr_jobs, 0.50 against 0.26); loops are
 // block-uniform.)
 __device__ __forceinline__ uint32_t pdr_tier_of(const PdrCtx& p, uint32_t I, uint32_t big_cap, const PdrTiers& tt,
                                                 uint32_t& slots, uint32_t& ops) {
@@ -1569,7 +1578,8 @@ static int pdr_run_tiers(crdtm_ctx* c, const PdrCtx& p, uint32_t i0, uint32_t i1
   hipStream_t s = c->stream;
   if (i1 <= i0) return CRDTM_OK;
   HIP_CHECK(hipMemsetAsync(tt.count, 0, 8 * sizeof(uint32_t), s));
-  LAUNCH(k_pdr_tier, dim3(grid_for(i1 - i0, BLOCK, 512)), dim3(BLOCK), 0, s, p, i0, i1, big_cap, tt);
+  static const uint32_t tier_grid = pdr_env_grid("CRDTM_PDR_TIER_GRID", 2048);
+  LAUNCH(k_pdr_tier, dim3(grid_for(i1 - i0, BLOCK, tier_grid)), dim3(BLOCK), 0, s, p, i0, i1, big_cap, tt);
   HIP_CHECK(hipMemcpyAsync(hcount, tt.count, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   if (int rw = stream_wait(s)) return rw;
   const uint32_t* h = hcount;
@@ -1817,7 +1827,8 @@ int pdr_apply(crdtm_tree* t, const OpsDev& o, const PdrIn& in, uint8_t* st, crdt
   uint32_t* joff = ws.alloc<uint32_t>(JCAP + 1);
   uint32_t* epre = ws.alloc<uint32_t>(JCAP + 1);
   for (uint32_t level = 0;; ++level) {
-    LAUNCH(k_pdr_jobs, dim3(grid_for(s1 - s0, BLOCK, 512)), dim3(BLOCK), 0, s, p, ok, s0, s1, JCAP, dr);
+    static const uint32_t jobs_grid = pdr_env_grid("CRDTM_PDR_JOBS_GRID", 2048);
+    LAUNCH(k_pdr_jobs, dim3(grid_for(s1 - s0, BLOCK, jobs_grid)), dim3(BLOCK), 0, s, p, ok, s0, s1, JCAP, dr);
     if ((r = sync_read(c))) return r;
     if (c->hres->pdr_overflow || level > in.maxlen + 1) {  // no room: sequential replay
       *handled = false;
