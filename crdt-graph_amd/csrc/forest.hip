@@ -246,10 +246,7 @@ __global__ void __launch_bounds__(64 * DPW) k_forest_wave(const uint32_t* doc_of
   for (uint32_t j = lane; j < FLANE_REGION / 8; j += 64) reinterpret_cast<uint4*>(sl)[j] = make_uint4(0, 0, 0, 0);
   const uint32_t ob = wuni(doc_off[d]), nops = wuni(doc_off[d + 1]) - ob;
   const uint32_t s0 = wuni(sent[d]);
-  // (the wave's own LDS stores precede its loads in order; the fence keeps
-  // the compiler from moving them)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
+  wave_sync();  // (the wave's own LDS stores before its loads)
   auto rd = [&](uint32_t j) { return static_cast<uint32_t>(sl[j]); };
   auto wr = [&](uint32_t j, uint32_t w) { sl[j] = static_cast<uint16_t>(w); };
   wr(s0, FL_N | FW_PRESENT | FW_TOMB);

@@ -776,7 +776,7 @@ __global__ void __launch_bounds__(64) k_ilr_level(IlrArgs args, OpsDev o, const 
   const bool plds = pc <= ptn && !(args.off & 1);
   if (plds) {
     for (uint32_t q = lane; q < pc; q += 64) tps[q] = NONE;
-    __syncthreads();
+    wave_sync();  // (one wave per workgroup)
   }
   IlrLane R;
   R.a = args;

@@ -1154,7 +1154,7 @@ __global__ void __launch_bounds__(64) k_fi_gaps(uint32_t m, const uint32_t* gk, 
       const uint32_t k = b + static_cast<uint32_t>(__builtin_ctzll(hm));
       hm &= hm - 1;
       fi_gap_one(k, m, gk, gv, gk0, par0, ts, nxt, ord, first, fi, L);
-      __syncthreads();  // (the next gap reuses the LDS)
+      wave_sync();  // (the next gap reuses the LDS; one wave per workgroup)
     }
   }
 }

@@ -259,6 +259,15 @@ __device__ __forceinline__ uint32_t block_ticket(uint32_t* ctr, uint32_t which) 
 }
 
 // wave64 inclusive scan of u32 (CDNA: 64 lanes, __shfl_up over width 64)
+// The "barrier" of a one-wave workgroup: its memory accesses before are
+// ordered before those after (a wave issues in order; the fence keeps the
+// compiler from moving them and waits for the stores) without s_barrier —
+// in the forest replay __syncthreads here cost 10% of the kernel.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const int lane = threadIdx.x & 63;
 #pragma unroll

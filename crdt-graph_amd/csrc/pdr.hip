@@ -303,7 +303,7 @@ __device__ void pdr_serial(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* S
   const long long t_start = clock64();
 #endif
   for (uint32_t r = lane; r <= K; r += 64) S[r] = r == 0 ? (PM | SF_TOMB | SF_MADE) : PM;
-  __syncthreads();
+  wave_sync();  // (one wave per workgroup)
   const uint32_t ob = rb, oe = p.rbase[D + 1] - 1;
   // change log (original dicts big enough to be worth rebuilding snapshots from)
   const bool logging = ORIG && p.log != nullptr && K + 1 >= p.log_min;
@@ -476,7 +476,7 @@ replay_done:
 #endif
   if (ORIG && lane == 0) p.logn[D] = (logging && ln <= lcap) ? ln : NONE;
   if (gst && lane == 0) pdr_gstat_flush(p, g_adds, g_fail, (g_first == NONE ? oe : g_first) - ob, oe - ob);
-  __syncthreads();
+  wave_sync();  // (one wave per workgroup)
   if (S != p.S + base) {
     for (uint32_t r = lane; r <= K; r += 64) p.S[base + r] = S[r];
   }
@@ -565,7 +565,7 @@ __device__ void pdr_blocked(const PdrCtx& p, uint8_t* st, uint32_t I, uint32_t* 
   unsigned long long g_stc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long q_cnt[5] = {0, 0, 0, 0, 0}, q_cyc[5] = {0, 0, 0, 0, 0}, q_walk = 0;
 #endif
-  __syncthreads();
+  wave_sync();  // (one wave per workgroup)
   const uint32_t ob = rb, oe = p.rbase[D + 1] - 1;
   const bool logging = ORIG && p.log != nullptr && K + 1 >= p.log_min;
   const uint32_t lcap = 4 * (oe + 1 - rb);
