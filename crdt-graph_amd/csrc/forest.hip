@@ -229,9 +229,11 @@ __device__ __forceinline__ bool uany(bool c) { return __builtin_amdgcn_ballot_w6
 
 // DPW documents per workgroup, one wave each (each wave only ever touches
 // its own slot region: no workgroup barrier, so a wave may leave early).
-// Round 6: the wave's own LDS initialisation ordered by a fence instead of
-// __syncthreads: k_forest_wave 1.94-2.06 -> 1.75 ms on 12.5k documents;
-// 2 or 4 documents per workgroup measured the same as 1)
+// Round 6: in this form (lane = thread id & 63, the document from workgroup
+// and wave) the compiler keeps the replay's arithmetic on the vector units
+// instead of the CU's one scalar unit (642 -> 317 scalar instructions):
+// k_forest_wave 1.94-2.06 -> 1.67-1.75 ms on 12.5k documents; 2 or 4
+// documents per workgroup measured the same as 1)
 template <uint32_t DPW>
 __global__ void __launch_bounds__(64 * DPW) k_forest_wave(const uint32_t* doc_off, uint32_t n_docs, long long ts0,
                                                     const uint32_t* opw, const uint16_t* sent, const uint8_t* fb,
