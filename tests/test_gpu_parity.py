@@ -446,3 +446,69 @@ def test_blocked_chain_order_forced(monkeypatch, log_min, spare):
         assert res.code == rc == 0 and res.path_taken == N.PATH_DICT_REPLAY, name
         assert engine_summary(et) == oracle_summary(ot), name
         assert np.array_equal(et.document_handles(), oracle_visible_vals(ot)), name
+
+
+def _nested_rows(shape, rng):
+    """Add rows (ts, path) of a nested batch: path = the ancestors' keys, then
+    the anchor key (0 = the dict's head)."""
+    rows = []  # (ts, path)
+    ctr = [0]
+
+    def new_ts(rep=1):
+        ctr[0] += 1
+        return (rep << 32) + ctr[0]
+
+    if shape == "single":
+        a = new_ts()
+        rows += [(a, [0]), (new_ts(), [a, 0])]
+    elif shape == "chain":  # every node the only child of the one before: one leaf at the bottom
+        anc = []
+        for _ in range(40):
+            t = new_ts()
+            rows.append((t, anc + [0]))
+            anc = anc + [t]
+    elif shape == "star":  # one node with 300 leaf children, siblings anchored at random earlier ones
+        r = new_ts()
+        rows.append((r, [0]))
+        kids = []
+        for _ in range(300):
+            t = new_ts(2 + int(rng.integers(0, 8)))
+            a = kids[int(rng.integers(0, len(kids)))] if kids and rng.random() < 0.7 else 0
+            rows.append((t, [r, a]))
+            kids.append(t)
+    else:  # "random": 3000 nodes up to depth 5, anchors among existing siblings
+        nodes = [([], [])]  # (path to the dict, children keys of that dict)
+        for _ in range(3000):
+            k = int(rng.integers(0, len(nodes)))
+            path, sib = nodes[k]
+            if len(path) >= 5:
+                continue
+            t = new_ts(1 + int(rng.integers(0, 4)))
+            a = sib[int(rng.integers(0, len(sib)))] if sib and rng.random() < 0.8 else 0
+            rows.append((t, path + [a]))
+            sib.append(t)
+            nodes.append((path + [t], []))
+    return rows
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["single", "chain", "star", "random"])
+def test_nested_tour_shapes(shape):
+    """The nested closed form's document order (Euler tour whose leaves have
+    no leave entry: a chain with one leaf, a star of leaves, a single child,
+    a random tree) against the oracle's literal replay."""
+    rng = np.random.default_rng(0x70E5)
+    rows = _nested_rows(shape, rng)
+    m = len(rows)
+    off = np.zeros(m + 1, np.uint32)
+    off[1:] = np.cumsum([len(p) for _, p in rows])
+    v = dict(kind=np.zeros(m, np.uint8), ts=np.array([t for t, _ in rows], np.int64), path_off=off,
+             path=np.array([x for _, p in rows for x in p] + [0], np.int64), val=np.arange(m, dtype=np.uint32))
+    ot, rc, _ = oracle_apply_arrays(v, m)
+    assert rc == 0
+    et = CRDTree.init(0)
+    res = et.apply_arrays(v, m)
+    assert res.code == 0
+    assert engine_summary(et) == oracle_summary(ot)
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
