@@ -297,8 +297,17 @@ int crdtm_tree_reset(crdtm_tree* t, int64_t replica_id) {
   // slot 0 / dict 0 / l_off[0] keep their init values: only the root
   // sentinel's `next` can change, and only to a slot we now drop.
   // (stream-ordered, no host wait: every later read of the state synchronises)
-  hipLaunchKernelGGL(k_reset_root, dim3(1), dim3(1), 0, t->ctx->stream, t->d.s_next);
+  // (the result block's init rides on this launch: a merge that follows
+  // skips its own, crdtm_ctx::dres_ready)
+  // (env CRDTM_DRES_FOLD=0: off, A/B)
+  static const bool fold = [] {
+    const char* e = getenv("CRDTM_DRES_FOLD");
+    return !(e && e[0] == '0');
+  }();
+  hipLaunchKernelGGL(k_reset_root, dim3(1), dim3(fold ? 64 : 1), 0, t->ctx->stream, t->d.s_next,
+                     fold ? t->ctx->dres : nullptr);
   HIP_CHECK(hipGetLastError());
+  t->ctx->dres_ready = fold;
   t->n_slots = 1;
   t->n_dicts = 1;
   t->log_n = 0;
@@ -550,6 +559,7 @@ int crdtm_tree_ops_since(const crdtm_tree* t, int64_t ts, crdtm_ops* out) {
   HIP_CHECK(hipSetDevice(c->device));
   if (ts == 0) return copy_log_range(t, 0, t->log_n, out);  // operationsSince 0: the whole log
   uint32_t* end = &c->dres->since_end;
+  c->dres_ready = false;
   HIP_CHECK(hipMemsetAsync(end, 0, sizeof(uint32_t), c->stream));
   if (t->log_n)
     hipLaunchKernelGGL(k_since, dim3(grid_for(t->log_n)), dim3(BLOCK), 0, c->stream, t->d.l_kind, t->d.l_ts,

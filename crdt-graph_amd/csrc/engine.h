@@ -102,6 +102,10 @@ struct crdtm_ctx {
   int gstat_valid = 0;
   crdtm::DevResult* dres = nullptr;  // device
   crdtm::DevResult* hres = nullptr;  // pinned host
+  // dres holds k_dres_init's values: crdtm_tree_reset's launch set them, and
+  // nothing has touched dres since (the flat speculation then skips its own
+  // init launch); cleared by every apply, every result read and ops_since
+  bool dres_ready = false;
   // pinned host staging for bulk per-call transfers (the forest's per-document
   // tables and results: one DMA each way instead of a pageable copy per array)
   char* pin = nullptr;
@@ -378,7 +382,7 @@ __global__ void k_log_tail(TreeDev T, uint32_t log_base, const uint32_t* n_app, 
                            const uint32_t* np);
 __global__ void k_status_out(const uint8_t* st, uint32_t n, uint32_t err, uint8_t* out);
 __global__ void k_replay_index(TreeDev T, uint32_t n_slots, SlotHash H, uint32_t* dhead, uint32_t* mnext);
-__global__ void k_reset_root(uint32_t* s_next);
+__global__ void k_reset_root(uint32_t* s_next, DevResult* d);
 // each group's first position in sorted keys (NONE: no group) (merge.hip)
 __global__ void k_doc_gstart(const uint32_t* sk, uint32_t m, uint32_t* gs);
 int post_pass(crdtm_tree* t, const OpsDev& o, const uint8_t* st, Arena& ws);

@@ -439,7 +439,7 @@ void launch_pre(crdtm_ctx* c, const OpsDev& o, hipStream_t s) {
   LAUNCH(k_pre<PRE_T>, dim3(g), dim3(PRE_T), 0, s, o, c->crange, c->dres);
 }
 
-__global__ void k_dres_init(DevResult* d) {
+static __device__ __forceinline__ void dres_init_block(DevResult* d) {
   const uint32_t nw = sizeof(DevResult) / sizeof(uint32_t);
   uint32_t* w = reinterpret_cast<uint32_t*>(d);
   for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) w[j] = 0;
@@ -449,6 +449,7 @@ __global__ void k_dres_init(DevResult* d) {
     d->first_del = NONE;
   }
 }
+__global__ void k_dres_init(DevResult* d) { dres_init_block(d); }
 
 __global__ void __launch_bounds__(BLOCK) k_index_insert(OpsDev o, TsIndex x) {
   GRID_STRIDE(i, o.n) {
@@ -2205,7 +2206,11 @@ __global__ void k_fl_commit_reset(DevResult* d) {
 
 // A fresh tree's root sentinel points nowhere (crdtm_tree_reset, and after an
 // unconfirmed speculative commit).
-__global__ void k_reset_root(uint32_t* s_next) { s_next[0] = NONE; }
+// (d: the result block's init rides on the tree reset, crdtm_ctx::dres_ready)
+__global__ void k_reset_root(uint32_t* s_next, DevResult* d) {
+  if (threadIdx.x == 0) s_next[0] = NONE;
+  if (d) dres_init_block(d);
+}
 
 // Before the second status pass: forget the first pass's accounting.
 __global__ void k_fl_stat_reset(DevResult* d) {
@@ -3328,6 +3333,7 @@ static uint32_t pow2_at_least(uint64_t x) {
 // copy: a blocking stream synchronisation sleeps and wakes ~15 us after the
 // copy ends, idling the device between the merge's phases and calls.
 int sync_read(crdtm_ctx* c) {
+  c->dres_ready = false;
   HIP_CHECK(hipMemcpyAsync(c->hres, c->dres, sizeof(DevResult), hipMemcpyDeviceToHost, c->stream));
   HIP_CHECK(hipEventRecord(c->ev_sync, c->stream));
   for (;;) {
@@ -3867,7 +3873,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
       // ids below REP_SPEC; else nothing of this merge is kept
       if (h.spec_fail || h.has_negative || h.max_replica >= REP_SPEC || h.range_total > Q ||
           h.range_total > 4ULL * n + 65536) {
-        LAUNCH(k_reset_root, dim3(1), dim3(1), 0, s, t->d.s_next);
+        LAUNCH(k_reset_root, dim3(1), dim3(1), 0, s, t->d.s_next, nullptr);
         *done = false;
         return CRDTM_OK;
       }
@@ -3891,7 +3897,7 @@ static int apply_flat(crdtm_tree* t, const OpsDev& o, const TsIndex& ix, uint32_
       return finish(n, n, 0, o.n_path, new_ts);
     }
     // not confirmed: the fresh tree's only reachable change is its root sentinel's `next`
-    LAUNCH(k_reset_root, dim3(1), dim3(1), 0, s, t->d.s_next);
+    LAUNCH(k_reset_root, dim3(1), dim3(1), 0, s, t->d.s_next, nullptr);
     // the replica ranges again (reset above; k_pre's other results are idempotent, no Delete here)
     launch_pre(c, o, s);
     LAUNCH(k_range_base, dim3(1), dim3(BLOCK), 0, s, c->crange, const_cast<uint32_t*>(ix.base), dr);
@@ -3962,6 +3968,8 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
   w.st = ws.alloc<uint8_t>(n);
   uint32_t* rbase = ws.alloc<uint32_t>(RID_SLOTS + 1);
   DevResult* dr = c->dres;
+  const bool dres_ready = c->dres_ready;  // (the tree reset's launch initialised it)
+  c->dres_ready = false;
   // (env CRDTM_FORCE_REPLAY=1: every batch takes the one-lane sequential
   // replay, so the cost of that fallback is measurable on any workload)
   const char* fe = getenv("CRDTM_FORCE_REPLAY");
@@ -3985,7 +3993,7 @@ static int apply_core(crdtm_tree* t, const OpsDev& o, uint8_t* st_out, crdtm_res
     while (b < 32 && ((static_cast<uint64_t>(n) + 2) >> b) != 0) b += 8;
     const uint64_t qcap = std::min<uint64_t>(std::max<uint64_t>((1ULL << b) - 2, 65536), 4ULL * n + 65536);
     if (qcap + 2 < (1ULL << FR_ABITS) - 1) {
-      LAUNCH(k_dres_init, dim3(1), dim3(64), 0, s, dr);
+      if (!dres_ready) LAUNCH(k_dres_init, dim3(1), dim3(64), 0, s, dr);
       // (env CRDTM_PRE_GRID: workgroups; CRDTM_PRE_BLIND=1: no-return atomics only)
       static const uint32_t pre_grid = env_grid("CRDTM_PRE_GRID", 256);  // (256 x 1024 threads: 55 -> 48 us at flat10m)
       static const bool pre_blind = [] {
