@@ -1,0 +1,98 @@
+"""Merges after a tree reset, through the C ABI (crdtm_tree_reset / crdtm_apply).
+
+The reset's launch also initialises the context's result block, and the flat
+speculation that follows skips its own init (crdtm_ctx::dres_ready,
+csrc/api.hip crdtm_tree_reset, csrc/merge.hip apply_core). The block belongs
+to the context, not the tree, so these sequences check that every other use
+of it in between leaves the next merge exact: a merge on another tree of the
+same context, operationsSince (its search writes the block), a failing merge,
+and a reset whose merge takes the general path. Each merge is compared with
+the oracle's literal replay of the same batch (src/CRDTree.elm:298-325).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from crdtm import _native as N  # noqa: E402
+from crdtm.tree import CRDTree  # noqa: E402
+from parity_util import (engine_summary, oracle_apply_arrays, oracle_summary,  # noqa: E402
+                         oracle_visible_vals)
+
+
+DELETE = 1  # (include/crdtm.h CRDTM_DELETE)
+
+
+def _flat(n, seed):
+    return N.synth(n_ops=n, replicas=8, window=32, seed=seed)
+
+
+def _nested(n, seed):
+    return N.synth(n_ops=n, replicas=4, window=16, p_delete=0.2, p_branch=0.1, max_depth=3, seed=seed)
+
+
+def _reset(t):
+    N.check(N.lib().crdtm_tree_reset(t._h, 0), "crdtm_tree_reset")
+
+
+def _check(t, v, m, path=None):
+    ot, rc, _ = oracle_apply_arrays(v, m)
+    assert rc == 0
+    res = t.apply_arrays(v, m)
+    assert res.code == 0
+    if path is not None:
+        assert res.path_taken == path
+    assert engine_summary(t) == oracle_summary(ot)
+    assert np.array_equal(t.document_handles(), oracle_visible_vals(ot))
+
+
+def test_reset_then_merges_sharing_the_context():
+    a, b = CRDTree.init(0), CRDTree.init(0)
+    f1, f2 = _flat(20_000, 11), _flat(30_000, 12)
+    _check(a, f1, 20_000, N.PATH_CLOSED_FORM)
+    _reset(a)  # initialises the shared block
+    _check(b, f2, 30_000, N.PATH_CLOSED_FORM)  # another tree's merge takes it
+    _reset(a)
+    _check(a, f1, 20_000, N.PATH_CLOSED_FORM)
+    _reset(b)
+    _reset(a)  # (two resets in a row, then a merge on the other tree)
+    _check(b, f1, 20_000, N.PATH_CLOSED_FORM)
+    _check(a, f2, 30_000, N.PATH_CLOSED_FORM)
+
+
+def test_reset_then_operations_since_then_merge():
+    a = CRDTree.init(0)
+    f = _flat(25_000, 21)
+    _check(a, f, 25_000, N.PATH_CLOSED_FORM)
+    _reset(a)
+    a.operations_since(int(f["ts"][100]))  # (its search writes the result block)
+    _check(a, f, 25_000, N.PATH_CLOSED_FORM)
+    _reset(a)
+    a.operations_since(12345)
+    _check(a, _flat(5_000, 22), 5_000, N.PATH_CLOSED_FORM)
+
+
+def test_reset_then_failing_and_general_merges():
+    a = CRDTree.init(0)
+    f = _flat(10_000, 31)
+    # the batch plus a Delete of an earlier Add's node: the speculation's shape
+    # check fails after the reset, and the general path merges the batch
+    n = 10_000
+    mixed = dict(kind=np.append(f["kind"], np.uint8(DELETE)), ts=np.append(f["ts"], np.int64(0)),
+                 path_off=np.append(f["path_off"], np.uint32(n + 1)), path=np.append(f["path"][:n], f["ts"][100]),
+                 val=np.append(f["val"], np.uint32(0)))
+    _reset(a)
+    _check(a, mixed, n + 1)
+    # a batch the reference rejects (an Add under a missing parent): no commit
+    bad = {k: v.copy() for k, v in f.items() if v is not None}
+    bad["path"][7000] = (99 << 32) | 12345
+    _reset(a)
+    ot, rc, _ = oracle_apply_arrays(bad, 10_000)
+    res = a.apply_arrays(bad, 10_000)
+    assert (res.code == 0) == (rc == 0)
+    _reset(a)
+    _check(a, f, 10_000, N.PATH_CLOSED_FORM)
+    _reset(a)
+    _check(a, _nested(8_000, 32), 8_000)  # the general nested path after a reset
+    _reset(a)
+    _check(a, f, 10_000, N.PATH_CLOSED_FORM)
