@@ -138,7 +138,7 @@ __device__ __forceinline__ uint32_t tsindex_slot(const TsIndex& x, int64_t ts) {
   if (r >= RID_SLOTS) return NONE;
   const uint32_t c = static_cast<uint32_t>(ts);
   const uint2 g = x.rng[r];
-  if (g.x == NONE || c < g.x || c > g.y) return NONE;
+  if (c < g.x || c > g.y) return NONE;  // (an empty range {NONE, 0} holds no c; 2^32 - 1 is a counter)
   return x.base[r] + (c - g.x);
 }
 

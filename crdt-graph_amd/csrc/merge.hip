@@ -201,7 +201,7 @@ __global__ void __launch_bounds__(PB) __attribute__((amdgpu_waves_per_eu(PB == 1
   auto mxf = [](uint32_t a, uint32_t b) { return a > b ? a : b; };
   maxr = block_reduce_t<PB>(maxr, 0u, mxf);  // (synchronises the block) only ids <= maxr were touched
   for (uint32_t j = threadIdx.x; j <= maxr && j < REP_DIRECT; j += blockDim.x) {
-    if (rlo[j] != NONE) {
+    if (rlo[j] <= rhi[j]) {  // (touched: a counter of 2^32 - 1 is a real range, not the NONE mark)
       atomicMin(&rng[j].x, rlo[j]);
       atomicMax(&rng[j].y, rhi[j]);
     }
@@ -261,7 +261,8 @@ __global__ void __launch_bounds__(PB) k_pre_ts(const long long* __restrict__ ts,
                                                const uint32_t* __restrict__ off, uint32_t n, uint2* rng,
                                                uint32_t* base, DevResult* dres) {
   __shared__ uint32_t rlo[REP_SPEC], rhi[REP_SPEC];
-  __shared__ uint32_t s_last, sw[PB / 64];
+  __shared__ uint32_t s_last;
+  __shared__ unsigned long long sw[PB / 64];
   for (uint32_t j = threadIdx.x; j < REP_SPEC; j += PB) {
     rlo[j] = NONE;
     rhi[j] = 0;
@@ -325,7 +326,7 @@ __global__ void __launch_bounds__(PB) k_pre_ts(const long long* __restrict__ ts,
   auto mxf = [](uint32_t a, uint32_t b) { return a > b ? a : b; };
   maxr = block_reduce_t<PB>(maxr, 0u, mxf);  // (synchronises the block)
   for (uint32_t j = threadIdx.x; j <= maxr && j < REP_SPEC; j += PB)
-    if (rlo[j] != NONE) {
+    if (rlo[j] <= rhi[j]) {  // (touched: a counter of 2^32 - 1 is a real range, not the NONE mark)
       atomicMin(&rng[j].x, rlo[j]);
       atomicMax(&rng[j].y, rhi[j]);
     }
@@ -348,13 +349,13 @@ __global__ void __launch_bounds__(PB) k_pre_ts(const long long* __restrict__ ts,
   const uint32_t nr =
       min(__hip_atomic_load(&dres->max_replica, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT), REP_SPEC - 1) + 1;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x / 64;
-  uint32_t sz = 0;
+  unsigned long long sz = 0;  // (a range spans up to 2^32 counters: sizes and sums in 64 bits)
   if (threadIdx.x < nr) {
     const uint32_t lo = __hip_atomic_load(&rng[threadIdx.x].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t hi = __hip_atomic_load(&rng[threadIdx.x].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sz = lo == NONE ? 0u : hi - lo + 1u;  // (counters: a range never exceeds 2^32 - 1 per replica)
+    sz = lo <= hi ? static_cast<unsigned long long>(hi - lo) + 1ULL : 0ULL;  // (empty: {NONE, 0})
   }
-  const uint32_t inc = wave_incl_scan(sz);
+  const unsigned long long inc = wave_incl_scan64(sz);
   if (lane == 63) sw[wave] = inc;
   __syncthreads();
   unsigned long long pre = inc - sz, tot = 0;
@@ -396,18 +397,18 @@ __device__ __forceinline__ bool nrec_dead(const uint4& r) { return (r.y >> 24) &
 // replicas 0..max_replica, one workgroup (max_replica is read on the device,
 // so the host needs no copy of the ranges); the total goes to range_total.
 __global__ void __launch_bounds__(BLOCK) k_range_base(const uint2* rng, uint32_t* base, DevResult* dres) {
-  __shared__ uint32_t sw[BLOCK / 64];
+  __shared__ unsigned long long sw[BLOCK / 64];
   const uint32_t nr = dres->max_replica + 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   unsigned long long carry = 0;
   for (uint32_t r0 = 0; r0 < nr; r0 += BLOCK) {
     const uint32_t r = r0 + threadIdx.x;
-    uint32_t sz = 0;
+    unsigned long long sz = 0;  // (a range spans up to 2^32 counters: sizes and sums in 64 bits)
     if (r < nr) {
       const uint2 g = rng[r];
-      sz = g.x == NONE ? 0u : g.y - g.x + 1u;
+      sz = g.x <= g.y ? static_cast<unsigned long long>(g.y - g.x) + 1ULL : 0ULL;  // (empty: {NONE, 0})
     }
-    const uint32_t inc = wave_incl_scan(sz);
+    const unsigned long long inc = wave_incl_scan64(sz);
     if (lane == 63) sw[wave] = inc;
     __syncthreads();
     unsigned long long pre = carry + (inc - sz), tot = 0;
@@ -485,7 +486,7 @@ struct RangeLds {
     const uint64_t r = static_cast<uint64_t>(ts) >> 32;
     if (r >= nrep) return NONE;
     const uint32_t c = static_cast<uint32_t>(ts), lo = smin[r];
-    if (lo == NONE || c < lo || c > smax[r]) return NONE;
+    if (c < lo || c > smax[r]) return NONE;  // (an empty range {NONE, 0} holds no c)
     return sbase[r] + (c - lo);
   }
 };
@@ -1941,7 +1942,7 @@ __global__ void __launch_bounds__(BLOCK) k_fl_claim(OpsDev o, TsIndex x, uint32_
     if (r >= nrep) return NONE;
     const uint4 e = stab[r];
     const uint32_t c = static_cast<uint32_t>(ts), lo = e.y;
-    if (lo == NONE || c < lo || c > e.z) return NONE;
+    if (c < lo || c > e.z) return NONE;  // (an empty range {NONE, 0} holds no c)
     return e.x + (c - lo);
   };
   const long long id0 = replica_of(ts0);

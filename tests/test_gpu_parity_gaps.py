@@ -270,7 +270,8 @@ def _flat_ops(n, replicas=8, seed=3):
 
 @pytest.mark.parametrize("shape", ["flat", "with_delete", "empty_and_long_path", "replica_300", "negative_ts",
                                    "duplicate_ts", "counter_holes", "sentinel_ts", "delete_ts_2_53",
-                                   "anchor_later", "anchor_prev_later", "anchor_missing", "anchor_self"])
+                                   "anchor_later", "anchor_prev_later", "anchor_missing", "anchor_self",
+                                   "replica_255", "replica_256", "counter_top", "ts_max", "own_replica"])
 def test_flat_speculation_shapes(shape):
     """The flat speculation (merge.hip apply_core: a fresh tree whose batch has
     as many path elements as ops is merged at once, the slot range read on
@@ -315,6 +316,18 @@ def test_flat_speculation_shapes(shape):
         ops[100] = (0, ops[100][1], [(5 << 32) + 999999], ops[100][3])
     elif shape == "anchor_self":
         ops[100] = (0, ops[100][1], [ops[100][1]], ops[100][3])
+    elif shape == "replica_255":  # the last id the speculation's replica table holds (REP_SPEC - 1)
+        ops.append((0, (255 << 32) + 1, [ops[10][1]], 9))
+        ops.append((0, (255 << 32) + 2, [(255 << 32) + 1], 9))
+    elif shape == "replica_256":  # the first it does not: the general path
+        ops.append((0, (256 << 32) + 1, [ops[10][1]], 9))
+    elif shape == "counter_top":  # a replica's counter at 2^32 - 1 (a range far from its others)
+        ops.append((0, (3 << 32) + 0xFFFFFFFF, [ops[10][1]], 9))
+    elif shape == "ts_max":  # the largest timestamp the reference's Int keeps exact
+        ops.append((0, (1 << 53) - 1, [ops[10][1]], 9))
+    elif shape == "own_replica":  # Adds of the observer's own replica 0 bump its timestamp
+        ops.append((0, 1, [ops[10][1]], 9))
+        ops.append((0, 2, [1], 9))
     s = _arrays(ops)
     n = len(ops)
     assert int(s["path_off"][-1]) == n  # (the speculation's trigger)
