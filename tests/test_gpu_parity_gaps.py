@@ -347,3 +347,50 @@ def test_flat_speculation_shapes(shape):
 def olib_free(t):
     from oracle.oracle import lib as olib
     olib().orc_free(t)
+
+
+TS_MAX = (1 << 53) - 1  # the largest timestamp the reference's Int keeps exact: replica 2^21 - 1, counter 2^32 - 1
+
+
+def _boundary_ops(base_ops):
+    """Adds at the timestamp boundaries, anchored in the given stream: the
+    largest timestamp, a counter of 2^32 - 1 on a replica the stream uses
+    (its range spans 2^32 counters), a counter of 0 on a fresh replica, and a
+    child dict under the largest timestamp's node."""
+    a = base_ops[10][1]
+    return [(0, TS_MAX, [a], 11), (0, (3 << 32) + 0xFFFFFFFF, [TS_MAX], 12), (0, 77 << 32, [a], 13),
+            (0, (5 << 32) + 999_999, [TS_MAX, 0], 14), (0, (5 << 32) + 1_000_000, [TS_MAX, (5 << 32) + 999_999], 15)]
+
+
+def _nested_ops(n, seed):
+    s = N.synth(n_ops=n, replicas=6, window=16, p_delete=0.2, p_branch=0.1, max_depth=3, seed=seed)
+    off = s["path_off"]
+    return [(int(s["kind"][i]), int(s["ts"][i]), [int(x) for x in s["path"][off[i]:off[i + 1]]], int(s["val"][i]))
+            for i in range(n)]
+
+
+@pytest.mark.parametrize("where", ["flat_fresh", "nested_fresh", "flat_incremental", "nested_incremental"])
+def test_timestamp_boundaries(where):
+    """Every merge path at the timestamp boundaries (src/CRDTree.elm:298-325;
+    the reference's Int is exact below 2^53): the largest timestamp, a
+    replica whose counters span 2^32 values, counter 0, and a children dict
+    under the largest key — in a fresh tree's batch (flat closed form /
+    general nested path) and in a second batch merged into existing state."""
+    base = _flat_ops(3000, seed=41) if where.startswith("flat") else _nested_ops(3000, 42)
+    extra = _boundary_ops(base)
+    et = CRDTree.init(0)
+    if where.endswith("fresh"):
+        s = _arrays(base + extra)
+        ot, rc, oerr = oracle_apply_arrays(s, len(base) + len(extra))
+        res = et.apply_arrays(s, len(base) + len(extra))
+    else:
+        s0, s1 = _arrays(base), _arrays(extra)
+        ot, rc0, _ = oracle_apply_arrays(s0, len(base))
+        assert rc0 == 0
+        assert et.apply_arrays(s0, len(base)).code == 0
+        _, rc, oerr = oracle_apply_arrays(s1, len(extra), tree=ot)
+        res = et.apply_arrays(s1, len(extra))
+    assert (res.code, res.err_index if rc else -1) == (rc, oerr if rc else -1), (where, res.code, rc)
+    assert engine_summary(et) == oracle_summary(ot), where
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
