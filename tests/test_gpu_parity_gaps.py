@@ -394,3 +394,40 @@ def test_timestamp_boundaries(where):
     assert engine_summary(et) == oracle_summary(ot), where
     assert engine_log(et, 0) == oracle_log(ot, 0)
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+
+
+def test_forest_timestamp_boundaries():
+    """The forest (config 5's path: k_forest_prep's per-document replica
+    ranges and slot map, the wave replay, the fallbacks) with documents that
+    hold the timestamp boundaries of test_timestamp_boundaries: flat documents
+    the wave replay takes (the largest timestamp alone on its replica; a
+    replica whose counters span 2^32 values, which leaves the dense slot map),
+    nested ones, and plain ones beside them; each against the oracle."""
+    from oracle.oracle import lib as olib
+    parts = []
+    for d in range(12):
+        k = d % 4
+        if k in (0, 1):  # flat, wave replay: the largest timestamp (and at k == 1 the 2^32-counter range)
+            base = _flat_ops(600, seed=200 + d)
+            extra = [(0, TS_MAX, [base[10][1]], 11)]
+            if k == 1:
+                extra.append((0, (3 << 32) + 0xFFFFFFFF, [TS_MAX], 12))
+            parts.append(_arrays(base + extra))
+        elif k == 2:  # nested, with a dict under the largest key
+            base = _nested_ops(600, 300 + d)
+            parts.append(_arrays(base + _boundary_ops(base)))
+        else:
+            parts.append(N.synth(n_ops=700, replicas=8, window=16, p_delete=0.2, seed=400 + d))
+    s, doc_off = _concat(parts)
+    out = forest_apply(s, doc_off)
+    assert out["rc"] == 0
+    L = olib()
+    for d, p in enumerate(parts):
+        t, rc, err = oracle_apply_arrays(p, len(p["kind"]))
+        assert out["code"][d] == rc, d
+        h = C.c_uint64()
+        nw = L.orc_canonical(t, 1, None, 0, C.byref(h))
+        assert (int(out["words"][d]), int(out["hash"][d])) == (nw, h.value), f"document {d}"
+        assert int(out["timestamp"][d]) == L.orc_timestamp(t), d
+        assert int(out["applied"][d]) == len(oracle_log(t, 0)[0]), d
+        L.orc_free(t)
