@@ -431,3 +431,31 @@ def test_forest_timestamp_boundaries():
         assert int(out["timestamp"][d]) == L.orc_timestamp(t), d
         assert int(out["applied"][d]) == len(oracle_log(t, 0)[0]), d
         L.orc_free(t)
+
+
+@pytest.mark.parametrize("rid", [5, (1 << 21) - 1])
+@pytest.mark.parametrize("fresh", [True, False])
+def test_own_replica_counter_top(rid, fresh):
+    """The observer's own replica at its last counters (incrementTimestamp
+    counts own Adds, src/CRDTree.elm:337-343; timestamps compare as Ints):
+    a tree whose replica is `rid` merges Adds of its own replica at counters
+    2^32 - 2 and 2^32 - 1, in a fresh tree's batch or a second batch."""
+    from oracle.oracle import lib as olib
+    base = _flat_ops(2000, seed=51)
+    a = base[10][1]
+    extra = [(0, (rid << 32) + 0xFFFFFFFE, [a], 1), (0, (rid << 32) + 0xFFFFFFFF, [(rid << 32) + 0xFFFFFFFE], 2)]
+    et = CRDTree.init(rid)
+    if fresh:
+        s = _arrays(base + extra)
+        ot, rc, oerr = oracle_apply_arrays(s, len(base) + len(extra), replica=rid)
+        res = et.apply_arrays(s, len(base) + len(extra))
+    else:
+        ot, rc0, _ = oracle_apply_arrays(_arrays(base), len(base), replica=rid)
+        assert rc0 == 0 and et.apply_arrays(_arrays(base), len(base)).code == 0
+        _, rc, oerr = oracle_apply_arrays(_arrays(extra), len(extra), replica=rid, tree=ot)
+        res = et.apply_arrays(_arrays(extra), len(extra))
+    assert (res.code, res.err_index if rc else -1) == (rc, oerr if rc else -1), (rid, res.code, rc)
+    assert et.timestamp() == olib().orc_timestamp(ot)
+    assert engine_summary(et) == oracle_summary(ot)
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
