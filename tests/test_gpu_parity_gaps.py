@@ -369,7 +369,8 @@ def _nested_ops(n, seed):
             for i in range(n)]
 
 
-@pytest.mark.parametrize("where", ["flat_fresh", "nested_fresh", "flat_incremental", "nested_incremental"])
+@pytest.mark.parametrize("where", ["flat_fresh", "nested_fresh", "flat_incremental", "nested_incremental",
+                                   "flat_incremental_flat"])
 def test_timestamp_boundaries(where):
     """Every merge path at the timestamp boundaries (src/CRDTree.elm:298-325;
     the reference's Int is exact below 2^53): the largest timestamp, a
@@ -378,6 +379,8 @@ def test_timestamp_boundaries(where):
     general nested path) and in a second batch merged into existing state."""
     base = _flat_ops(3000, seed=41) if where.startswith("flat") else _nested_ops(3000, 42)
     extra = _boundary_ops(base)
+    if where == "flat_incremental_flat":  # root-dict Adds only: the incremental flat merge's shape
+        extra = extra[:3]
     et = CRDTree.init(0)
     if where.endswith("fresh"):
         s = _arrays(base + extra)
