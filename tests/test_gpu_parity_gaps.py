@@ -462,3 +462,30 @@ def test_own_replica_counter_top(rid, fresh):
     assert engine_summary(et) == oracle_summary(ot)
     assert engine_log(et, 0) == oracle_log(ot, 0)
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+
+
+@pytest.mark.parametrize("nrep", [3839, 3840, 3841, 4096, 4097])
+def test_flat_replica_table_sizes(nrep):
+    """A fresh flat batch over `nrep` replica ids (the largest id nrep - 1):
+    around the claim's LDS replica table (3,840 ids), the host-scanned ranges
+    (HOST_RANGES = 4,096) and the slot-order pass's replica buckets; every
+    Add anchored at the previous one of its replica or at the head."""
+    rng = np.random.default_rng(nrep)
+    ids = np.concatenate([np.arange(1, nrep), rng.integers(1, nrep, 6000)])
+    rng.shuffle(ids)
+    ctr = {}
+    ops = []
+    for r in ids:
+        c = ctr.get(int(r), 0) + 1
+        ctr[int(r)] = c
+        a = ((int(r) << 32) + c - 1) if c > 1 else 0
+        ops.append((0, (int(r) << 32) + c, [a], len(ops) % 1000))
+    s = _arrays(ops)
+    n = len(ops)
+    ot, rc, oerr = oracle_apply_arrays(s, n)
+    et = CRDTree.init(0)
+    res = et.apply_arrays(s, n)
+    assert (res.code, res.err_index if rc else -1) == (rc, oerr if rc else -1)
+    assert engine_summary(et) == oracle_summary(ot)
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
