@@ -489,3 +489,31 @@ def test_flat_replica_table_sizes(nrep):
     assert engine_summary(et) == oracle_summary(ot)
     assert engine_log(et, 0) == oracle_log(ot, 0)
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+
+
+@pytest.mark.parametrize("n", [1, 2, 255, 256, 257, 65533, 65534, 65535, 65536, 65537])
+def test_flat_batch_size_edges(n):
+    """Fresh flat batches at the sizes where the speculation's slot bound and
+    sort widths step (n + 2 crossing 2^8 and 2^16) and the smallest ones."""
+    s = N.synth(n_ops=n, replicas=8, window=32, seed=7000 + n)
+    ot, rc, oerr = oracle_apply_arrays(s, n)
+    et = CRDTree.init(0)
+    res = et.apply_arrays(s, n)
+    assert (res.code, res.err_index if rc else -1) == (rc, oerr if rc else -1)
+    assert engine_summary(et) == oracle_summary(ot)
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+
+
+@pytest.mark.parametrize("n", [16383, 16384, 16385])
+def test_nested_batch_size_edges(n):
+    """Fresh nested batches (Deletes interleaved, depth <= 3) around the
+    one-workgroup sorts' limit (RS_SMALL_MAX = 16,384 items)."""
+    s = N.synth(n_ops=n, replicas=4, window=16, p_delete=0.2, p_branch=0.1, max_depth=3, seed=8000 + n)
+    ot, rc, oerr = oracle_apply_arrays(s, n)
+    et = CRDTree.init(0)
+    res = et.apply_arrays(s, n)
+    assert (res.code, res.err_index if rc else -1) == (rc, oerr if rc else -1)
+    assert engine_summary(et) == oracle_summary(ot)
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
