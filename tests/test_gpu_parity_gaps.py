@@ -517,3 +517,19 @@ def test_nested_batch_size_edges(n):
     assert engine_summary(et) == oracle_summary(ot)
     assert engine_log(et, 0) == oracle_log(ot, 0)
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+
+
+@pytest.mark.parametrize("n", [39_000, 41_000, 43_000])
+def test_big_dict_tier_edges(n):
+    """One root dict of ~31k-34k Adds with Deletes interleaved (the exact
+    per-dict replay): around the blocked tier's limit (15-bit ranks,
+    BLK_KMAX = 32,766, and its LDS fit), past which the dict takes the
+    global-memory tier."""
+    s = N.synth(n_ops=n, replicas=16, window=64, p_delete=0.2, seed=9000 + n)
+    ot, rc, oerr = oracle_apply_arrays(s, n)
+    et = CRDTree.init(0)
+    res = et.apply_arrays(s, n)
+    assert (res.code, res.err_index if rc else -1) == (rc, oerr if rc else -1)
+    assert engine_summary(et) == oracle_summary(ot)
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
