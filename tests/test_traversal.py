@@ -157,3 +157,23 @@ def test_host_readers_refuse_unsound_state(poke):
     from parity_util import engine_summary, oracle_summary
     assert engine_summary(et) == oracle_summary(ot)
     assert L.crdtm_tree_walk(et._h, N.REF_NONE, None, 0, C.byref(cnt)) == 0
+
+
+def test_traversal_timestamp_boundaries():
+    """The device queries over keys at the timestamp boundaries (the largest
+    timestamp, a counter of 2^32 - 1, counter 0, a children dict under the
+    largest key: tests/test_gpu_parity_gaps.py _boundary_ops) in a nested
+    tree, against the oracle."""
+    from oracle.oracle import lib as olib
+    from test_gpu_parity_gaps import TS_MAX, _arrays, _boundary_ops, _nested_ops
+    base = _nested_ops(2000, 61)
+    extra = _boundary_ops(base)
+    s = _arrays(base + extra)
+    ot = olib().orc_init(0)
+    _, rc, _ = oracle_apply_arrays(s, len(base) + len(extra), tree=ot)
+    et = CRDTree.init(0)
+    assert et.apply_arrays(s, len(base) + len(extra)).code == rc
+    paths = [[TS_MAX], [TS_MAX, 0], [TS_MAX, (5 << 32) + 999_999], [TS_MAX, (5 << 32) + 1_000_000],
+             [(3 << 32) + 0xFFFFFFFF], [77 << 32], [TS_MAX, TS_MAX], [0]]
+    paths += [[k for k in o[2][:-1]] + [o[1]] for o in base[:200] if o[0] == 0]
+    check_tree(et, _oracle(ot), paths)
