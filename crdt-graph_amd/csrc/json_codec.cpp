@@ -399,7 +399,9 @@ bool decodeInt(const char* s, const Span& sp, long long& out) {
   if (!parseNumber(q, v, ie, iv)) return false;
   q.ws();
   if (q.i != sp.e) return false;
-  if (ie) { out = iv; return true; }
+  // (beyond 2^53 the reference's platform holds the nearest double, which
+  // strtod gives: JSON.parse("9007199254740993") is 9007199254740992)
+  if (ie && iv <= (1LL << 53) && iv >= -(1LL << 53)) { out = iv; return true; }
   if (!std::isfinite(v) || std::floor(v) != v || std::fabs(v) >= 9.2e18) return false;
   out = static_cast<long long>(v);
   return true;
@@ -508,7 +510,12 @@ T* dup(const std::vector<T>& v) {
   return p;
 }
 
-void encodeInt(std::string& o, int64_t v) { o += std::to_string(v); }
+// (beyond 2^53 as JSON.stringify prints the double: shortest digits, zero
+// padded — a decoded value there is already a double's exact integer)
+void encodeInt(std::string& o, int64_t v) {
+  if (v <= (1LL << 53) && v >= -(1LL << 53)) o += std::to_string(v);
+  else jsNumber(o, static_cast<double>(v));
+}
 
 void encodeOp(std::string& o, const crdtm_ops* ops, uint64_t i, const char* vb, const uint64_t* voff) {
   const uint32_t b = ops->path_off[i], e = ops->path_off[i + 1];
