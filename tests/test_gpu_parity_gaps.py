@@ -533,3 +533,35 @@ def test_big_dict_tier_edges(n):
     assert engine_summary(et) == oracle_summary(ot)
     assert engine_log(et, 0) == oracle_log(ot, 0)
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+
+
+def test_incremental_flat_batches_wide_replicas():
+    """Small flat batches merged one after another into a flat tree (the
+    incremental flat merge's shape), whose Adds come from replica ids around
+    the speculation's and the claim's tables (255, 256, 3,840, 4,097) and the
+    largest id, typing at their own previous Adds or at the document's."""
+    rng = np.random.default_rng(77)
+    base = _flat_ops(4000, seed=71)
+    s0 = _arrays(base)
+    ot, rc0, _ = oracle_apply_arrays(s0, len(base))
+    et = CRDTree.init(0)
+    assert rc0 == 0 and et.apply_arrays(s0, len(base)).code == 0
+    keys = [o[1] for o in base]
+    ids = [255, 256, 3840, 4097, (1 << 21) - 1, 3]
+    ctr = {r: 10_000 for r in ids}
+    for b in range(6):
+        ops = []
+        for _ in range(300):
+            r = ids[int(rng.integers(0, len(ids)))]
+            ctr[r] += 1
+            a = keys[int(rng.integers(max(0, len(keys) - 50), len(keys)))]
+            ts = (r << 32) + ctr[r]
+            ops.append((0, ts, [a], b))
+            keys.append(ts)
+        s = _arrays(ops)
+        _, rc, oerr = oracle_apply_arrays(s, len(ops), tree=ot)
+        res = et.apply_arrays(s, len(ops))
+        assert (res.code, res.err_index if rc else -1) == (rc, oerr if rc else -1), b
+        assert engine_summary(et) == oracle_summary(ot), b
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
