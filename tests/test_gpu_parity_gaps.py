@@ -565,3 +565,19 @@ def test_incremental_flat_batches_wide_replicas():
         assert engine_summary(et) == oracle_summary(ot), b
     assert engine_log(et, 0) == oracle_log(ot, 0)
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+
+
+def test_operations_since_timestamp_boundaries():
+    """operationsSince (src/CRDTree.elm:408-418, src/Internal/Operation.elm:
+    25-53) from keys at the timestamp boundaries: the largest timestamp, a
+    counter of 2^32 - 1, counter 0, a key no Add holds, and 0 (the whole log)."""
+    from parity_util import oracle_since
+    base = _flat_ops(2000, seed=81)
+    extra = _boundary_ops(base)
+    s = _arrays(base + extra)
+    ot, rc, _ = oracle_apply_arrays(s, len(base) + len(extra))
+    et = CRDTree.init(0)
+    assert rc == 0 and et.apply_arrays(s, len(base) + len(extra)).code == 0
+    for ts in (TS_MAX, (3 << 32) + 0xFFFFFFFF, 77 << 32, (5 << 32) + 999_999, (9 << 32) + 12345, 0, base[0][1]):
+        got = engine_log(et, since=ts)[0]
+        assert got == oracle_since(ot, ts), ts
