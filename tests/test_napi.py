@@ -71,6 +71,15 @@ def test_addon_matches_oracle(tmp_path):
     adds = [o.ts for o in ops if o.kind == "add"]
     cases.append({"replica": 0, "calls": [encoder(big)], "since": [adds[10], adds[-1], 12345]})
     expect.append((0, [big]))
+    # keys at the timestamp boundaries (exact JS Numbers up to 2^53 - 1), through JSON both ways
+    ts_max = (1 << 53) - 1
+    fs = N.synth(n_ops=500, replicas=8, window=16, seed=78)
+    edge = [Add(int(fs["ts"][i]), [int(fs["path"][i])], "f%d" % i) for i in range(500)]
+    a = edge[10].ts
+    edge += [Add(ts_max, [a], "max"), Add((3 << 32) + 0xFFFFFFFF, [ts_max], "top"), Add(77 << 32, [a], "zero"),
+             Add((5 << 32) + 999_999, [ts_max, 0], "child")]
+    cases.append({"replica": 0, "calls": [encoder(Batch(edge))], "since": [ts_max, 77 << 32, (5 << 32) + 999_999]})
+    expect.append((0, [Batch(edge)]))
 
     # the same scenarios again with every apply queued before the first is
     # awaited (the addon's per-tree FIFO keeps the reference's call order)
@@ -120,3 +129,10 @@ def test_addon_matches_oracle(tmp_path):
         assert [(0 if o.kind == "add" else 1, o.ts if o.kind == "add" else 0, tuple(o.path))
                 for o in flatten(log)] == [(k, t, p) for k, t, p, _ in olog]
         assert res["timestamp"] == oracle_summary(ot)["ts"]
+        # operationsSince through the addon (src/CRDTree.elm:408-418)
+        from parity_util import oracle_since
+        for ts in case["since"]:
+            got = flatten(decoder(res["since"][str(ts)]))
+            want = oracle_since(ot, ts)
+            assert [(0 if o.kind == "add" else 1, o.ts if o.kind == "add" else 0, tuple(o.path)) for o in got] == \
+                [(k, t, p) for k, t, p, _ in want], ts
