@@ -96,3 +96,26 @@ def test_reset_then_failing_and_general_merges():
     _check(a, _nested(8_000, 32), 8_000)  # the general nested path after a reset
     _reset(a)
     _check(a, f, 10_000, N.PATH_CLOSED_FORM)
+
+
+def test_reset_of_a_tree_whose_version_is_shared():
+    """A clone shares the merged state (copy on write); resetting the original
+    then merging into it must leave the clone's version untouched, and the
+    clone merges on from its own state."""
+    a = CRDTree.init(0)
+    f1, f2 = _flat(15_000, 41), _flat(12_000, 42)
+    _check(a, f1, 15_000, N.PATH_CLOSED_FORM)
+    b = a.clone()
+    _reset(a)
+    _check(a, f2, 12_000, N.PATH_CLOSED_FORM)
+    ot1, rc, _ = oracle_apply_arrays(f1, 15_000)
+    assert rc == 0
+    assert engine_summary(b) == oracle_summary(ot1)
+    assert np.array_equal(b.document_handles(), oracle_visible_vals(ot1))
+    extra = dict(kind=np.zeros(2, np.uint8), ts=np.array([(9 << 32) + 1, (9 << 32) + 2], np.int64),
+                 path_off=np.array([0, 1, 2], np.uint32), path=np.array([int(f1["ts"][5]), (9 << 32) + 1], np.int64),
+                 val=np.array([1, 2], np.uint32))
+    _, rc2, _ = oracle_apply_arrays(extra, 2, tree=ot1)
+    assert rc2 == 0 and b.apply_arrays(extra, 2).code == 0
+    assert engine_summary(b) == oracle_summary(ot1)
+    assert np.array_equal(b.document_handles(), oracle_visible_vals(ot1))
