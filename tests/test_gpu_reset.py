@@ -8,6 +8,7 @@ of it in between leaves the next merge exact: a merge on another tree of the
 same context, operationsSince (its search writes the block), a failing merge,
 and a reset whose merge takes the general path. Each merge is compared with
 the oracle's literal replay of the same batch (src/CRDTree.elm:298-325).
+Also: device-resident ops at any alignment (the bench's and the ports' path).
 """
 import numpy as np
 import pytest
@@ -119,3 +120,34 @@ def test_reset_of_a_tree_whose_version_is_shared():
     assert rc2 == 0 and b.apply_arrays(extra, 2).code == 0
     assert engine_summary(b) == oracle_summary(ot1)
     assert np.array_equal(b.document_handles(), oracle_visible_vals(ot1))
+
+
+@pytest.mark.parametrize("pad", [0, 1, 3])
+@pytest.mark.parametrize("kind", ["flat", "nested"])
+def test_device_resident_ops_any_alignment(pad, kind):
+    """crdtm_apply on device-resident ops (ops_on_device = 1, the bench's and
+    the Elm ports' path) whose arrays start `pad` elements into their
+    allocations: misaligned columns are copied to aligned scratch
+    (csrc/api.hip align_ops) and the merge equals the oracle's."""
+    import torch
+    n = 12_000
+    s = _flat(n, 91) if kind == "flat" else _nested(n, 92)
+    dev = torch.device("cuda", 0)
+    keep = []
+
+    def on_dev(a):
+        t = torch.zeros(len(a) + pad, dtype=torch.from_numpy(a[:1]).dtype, device=dev)
+        t[pad:] = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        keep.append(t)
+        return t[pad:].data_ptr()
+
+    npath = int(s["path_off"][n])
+    ops = N.Ops(n, npath, on_dev(s["kind"]), on_dev(s["ts"]), on_dev(s["path_off"]), on_dev(s["path"][:npath]),
+                on_dev(s["val"]), None)
+    torch.cuda.synchronize()
+    ot, rc, _ = oracle_apply_arrays(s, n)
+    et = CRDTree.init(0)
+    res = et.apply_arrays(ops, n, on_device=True)
+    assert res.code == rc
+    assert engine_summary(et) == oracle_summary(ot)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
