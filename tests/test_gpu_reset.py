@@ -151,3 +151,30 @@ def test_device_resident_ops_any_alignment(pad, kind):
     assert res.code == rc
     assert engine_summary(et) == oracle_summary(ot)
     assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
+
+
+def test_two_contexts_interleaved():
+    """Two engine contexts on one device (each its own stream, result block,
+    pinned staging and scratch arena), their merges interleaved: each tree
+    equals the oracle's."""
+    import ctypes as C
+    L = N.lib()
+    ctx2 = C.c_void_p()
+    N.check(L.crdtm_ctx_create(0, None, C.byref(ctx2)), "crdtm_ctx_create")
+    h = C.c_void_p()
+    N.check(L.crdtm_tree_create(ctx2, 0, C.byref(h)), "crdtm_tree_create")
+    b = CRDTree(h)
+    a = CRDTree.init(0)
+    try:
+        f1, f2 = _flat(20_000, 51), _nested(9_000, 52)
+        _check(a, f1, 20_000, N.PATH_CLOSED_FORM)
+        _check(b, f2, 9_000)
+        _reset(a)
+        _reset(b)
+        _check(b, f1, 20_000, N.PATH_CLOSED_FORM)
+        _check(a, f2, 9_000)
+    finally:
+        del b
+        import gc
+        gc.collect()
+        L.crdtm_ctx_destroy(ctx2)
