@@ -581,3 +581,24 @@ def test_operations_since_timestamp_boundaries():
     for ts in (TS_MAX, (3 << 32) + 0xFFFFFFFF, 77 << 32, (5 << 32) + 999_999, (9 << 32) + 12345, 0, base[0][1]):
         got = engine_log(et, since=ts)[0]
         assert got == oracle_since(ot, ts), ts
+
+
+def test_forest_calls_of_growing_and_shrinking_size():
+    """Forest calls of 4, 1,500 and 7 documents in a row on one context: the
+    pinned staging of the per-document tables and results grows and is
+    reused (csrc/merge.hip forest_apply); every document against the oracle."""
+    from oracle.oracle import lib as olib
+    L = olib()
+    for nd, seed in ((4, 500), (1500, 600), (7, 700)):
+        parts = [N.synth(n_ops=100 + (d % 3) * 50, replicas=8, window=16, p_delete=0.2, seed=seed + d)
+                 for d in range(nd)]
+        s, doc_off = _concat(parts)
+        out = forest_apply(s, doc_off)
+        assert out["rc"] == 0
+        for d, p in enumerate(parts):
+            t, rc, err = oracle_apply_arrays(p, len(p["kind"]))
+            assert out["code"][d] == rc, (nd, d)
+            h = C.c_uint64()
+            nw = L.orc_canonical(t, 1, None, 0, C.byref(h))
+            assert (int(out["words"][d]), int(out["hash"][d])) == (nw, h.value), (nd, d)
+            L.orc_free(t)
