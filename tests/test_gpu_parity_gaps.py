@@ -602,3 +602,44 @@ def test_forest_calls_of_growing_and_shrinking_size():
             nw = L.orc_canonical(t, 1, None, 0, C.byref(h))
             assert (int(out["words"][d]), int(out["hash"][d])) == (nw, h.value), (nd, d)
             L.orc_free(t)
+
+
+def _remap_keys(s, rmap, cshift):
+    """The same stream with every key (ts and path element) moved to replica
+    rmap[r] and counter c + cshift: a bijection of the keys that keeps 0 (the
+    head sentinel) — engine and oracle both merge the remapped stream."""
+    def f(k):
+        k = np.asarray(k, np.int64)
+        r = (k >> 32).astype(np.int64)
+        c = (k & 0xFFFFFFFF).astype(np.int64)
+        out = (np.array([rmap[int(x)] for x in r.ravel()], np.int64).reshape(r.shape) << 32) + c + cshift
+        return np.where(k == 0, 0, out).astype(np.int64)
+    t = {k: v.copy() for k, v in s.items() if v is not None}
+    t["ts"] = np.where(s["kind"] == 0, f(s["ts"]), s["ts"])
+    npth = int(s["path_off"][-1])
+    t["path"] = f(s["path"][:npth]) if npth else s["path"][:0].copy()
+    return t
+
+
+@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("shape", ["flat", "nested"])
+def test_remapped_streams_at_key_boundaries(seed, shape):
+    """Synthetic streams (flat; nested with interleaved Deletes) whose keys
+    are moved to replica ids near 2^21 and the tables' edges and to counters
+    within 5,000 of 2^32: every tier the batch takes against the oracle."""
+    n = 4000
+    if shape == "flat":
+        s = N.synth(n_ops=n, replicas=6, window=16, seed=1000 + seed)
+    else:
+        s = N.synth(n_ops=n, replicas=6, window=16, p_delete=0.2, p_branch=0.1, max_depth=3, seed=2000 + seed)
+    ids = [(1 << 21) - 1, (1 << 21) - 2, 255, 256, 4097, 3, 3840]
+    rmap = {r: ids[(r + seed) % len(ids)] for r in range(0, 16)}
+    assert int(np.max(s["ts"] & 0xFFFFFFFF)) < 5000
+    t = _remap_keys(s, rmap, 0xFFFFFFFF - 5000)
+    ot, rc, oerr = oracle_apply_arrays(t, n)
+    et = CRDTree.init(0)
+    res = et.apply_arrays(t, n)
+    assert (res.code, res.err_index if rc else -1) == (rc, oerr if rc else -1)
+    assert engine_summary(et) == oracle_summary(ot)
+    assert engine_log(et, 0) == oracle_log(ot, 0)
+    assert np.array_equal(et.document_handles(), oracle_visible_vals(ot))
